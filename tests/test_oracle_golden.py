@@ -1,0 +1,52 @@
+"""Pin the oracle (CPU restatement) to golden vectors produced by the reference itself."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_cpu as oc
+from tests.golden_util import GOLDEN, check_packed, check_post, load
+
+TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb"]
+
+
+def test_param_counts_match_reference_kats():
+    # notebook-logged parameter counts + the counts the reference printed here
+    kat = json.load(open(os.path.join(GOLDEN, "param_counts.json")))
+    assert kat["har"] == 4298291          # GSTCAN_HAR_conv_10kfold.ipynb:921
+    assert kat["ur_nb"] == 4311324        # GSTCAN_UR_conv.ipynb:797
+    assert kat["two"] == 4250783          # GSTCAN_HAR_skeleton_10kfold.ipynb:954
+    assert kat["bilstm"] == 47387         # GSTCAN_HAR_sensor(lstm)_10kfold.ipynb:968
+    for tag in TAGS:
+        d, spec = load(tag)
+        n = sum(int(np.prod(s)) for k, s in oc.param_shapes(spec).items() if not oc.is_buffer(k))
+        assert n == kat[tag], tag
+
+
+def test_graphs_match_reference():
+    z = np.load(os.path.join(GOLDEN, "graphs.npz"))
+    for key in z.files:
+        layout, strat = key.split(":")
+        np.testing.assert_array_equal(oc.graph_adjacency(layout, strat), z[key])
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_train_step_matches_reference(tag):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    d, spec = load(tag)
+    st = oc.init_state(spec, int(d["seed"][0]))
+    skel, sensor, label = (torch.from_numpy(d[k]) for k in ("skel", "sensor", "label"))
+    out, loss, grads = oc.train_step(st, spec, skel, sensor, label)
+    np.testing.assert_allclose(out.numpy(), d["out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(loss.item(), d["loss"][0], rtol=1e-6, atol=1e-6)
+    for name, g in grads.items():
+        if "nograd:" + name in d:
+            continue
+        check_packed(d, "grad:" + name, g.numpy(), rtol=1e-4, atol=1e-6)
+    for name, g in grads.items():
+        check_post(d, name, st[name].numpy(), g.numpy())
+    for name, b in st.items():
+        if name.endswith(("running_mean", "running_var")):
+            check_packed(d, "buf:" + name, b.numpy(), rtol=1e-5, atol=1e-6)

@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REFERENCE's own modules (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+Writes: tests/golden/*.npz  (small, committed; the reference itself never travels).
+
+How the reference is imported: the packaged 3-stream model lives in
+/root/reference/Multimodal_Fall3/model/{stgcan,graph,bilstm,combination}.py, but
+combination.py:5-6 imports a non-existent `model.st_gcn` subpackage, so that name is
+aliased to the real modules. The UR notebook model is obtained by exec'ing cells 1-2
+of GSTCAN_UR_conv.ipynb on CPU. Nothing is copied into this repo: only inputs,
+outputs, gradients and post-step parameter samples are stored.
+
+Weights come from oracle/prng.py (seeded per parameter name), so a fixture stores
+only the seed; `load_state_dict(strict=True)` also proves that the oracle's
+parameter table has the reference's exact state_dict keys and shapes.
+"""
+from __future__ import annotations
+
+import contextlib
+import importlib
+import io
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+from oracle import model_cpu as oc  # noqa: E402
+from oracle.prng import synthetic_batch  # noqa: E402
+
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+FULL_LIMIT = 128    # tensors up to this many elements are stored whole
+SAMPLES = 32
+
+
+def import_reference():
+    sys.path.insert(0, REF + "/Multimodal_Fall3")
+    stg = importlib.import_module("model.stgcan")
+    gr = importlib.import_module("model.graph")
+    pkg = types.ModuleType("model.st_gcn")
+    pkg.__path__ = []
+    sys.modules.update({"model.st_gcn": pkg, "model.st_gcn.stgcan": stg, "model.st_gcn.graph": gr})
+    comb = importlib.import_module("model.combination")
+    bil = importlib.import_module("model.bilstm")
+    nb = json.load(open(REF + "/GSTCAN_UR_conv.ipynb"))
+    ns = {"__name__": "nbmod", "device": torch.device("cpu")}
+    exec(compile("\n".join("".join(nb["cells"][i]["source"]) for i in (1, 2)), "nb_ur", "exec"), ns)
+    return stg, gr, comb, bil, ns
+
+
+def sample_idx(n):
+    if n <= SAMPLES:
+        return np.arange(n)
+    return (np.arange(SAMPLES) * (n // SAMPLES) + 7) % n
+
+
+def pack(prefix, d, t):
+    a = t.detach().double().numpy().reshape(-1)
+    if a.size <= FULL_LIMIT:
+        d[prefix] = a.astype(np.float32)
+    else:
+        d[prefix + "@norm"] = np.array([np.linalg.norm(a)])
+        d[prefix + "@sum"] = np.array([a.sum()])
+        d[prefix + "@val"] = a[sample_idx(a.size)].astype(np.float32)
+
+
+def run_case(tag, module, spec, forward_fn, batch, seed, frames=30, sensor_frames=30):
+    torch.manual_seed(0)
+    state = oc.init_state(spec, seed, sensor_frames)
+    module.load_state_dict(state, strict=True)
+    module.train()
+    V = state[next(k for k in state if k.endswith("A"))].shape[-1] if spec.model != "bilstm" else 14
+    skel, sensor, label = synthetic_batch(batch, V, spec.num_class, spec.sensor_dim, seed + 1,
+                                          frames=frames, sensor_frames=sensor_frames)
+    sk, se, lb = (torch.from_numpy(x) for x in (skel, sensor, label))
+    opt = torch.optim.RMSprop(module.parameters(), lr=1e-3)
+    opt.zero_grad()
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = forward_fn(module, sk, se)
+    loss = torch.nn.CrossEntropyLoss()(out, lb)
+    loss.backward()
+    d = {"seed": np.array([seed]), "skel": skel, "sensor": sensor, "label": label,
+         "out": out.detach().numpy(), "loss": np.array([loss.item()]),
+         "spec": np.array([json.dumps(spec.__dict__)])}
+    nparams = 0
+    for name, p in module.named_parameters():
+        nparams += p.numel()
+        if p.grad is None:  # e.g. CNN1D.fc is built but never used (GSTCAN_UR_conv.ipynb cell 2)
+            d["nograd:" + name] = np.array([1])
+            continue
+        pack("grad:" + name, d, p.grad)
+    opt.step()
+    for name, p in module.named_parameters():
+        pack("post:" + name, d, p)
+    for name, b in module.named_buffers():
+        if name.endswith(("running_mean", "running_var")):
+            pack("buf:" + name, d, b)
+    d["nparams"] = np.array([nparams])
+    path = os.path.join(OUT, f"model_{tag}.npz")
+    np.savez_compressed(path, **d)
+    print(f"{tag}: params={nparams} loss={loss.item():.6f} -> {path} ({os.path.getsize(path)//1024} KB)")
+    return nparams
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    stg, gr, comb, bil, ns = import_reference()
+
+    # graph adjacency for every layout x strategy (graph.py:20-126)
+    graphs = {}
+    for layout in ("coco_cut", "coco_mmpose"):
+        for strat in ("uniform", "distance", "spatial"):
+            graphs[f"{layout}:{strat}"] = gr.Graph(layout=layout, strategy=strat).A.astype(np.float64)
+    np.savez_compressed(os.path.join(OUT, "graphs.npz"), **graphs)
+
+    kat = {}
+    fwd_pkg = lambda m, sk, se: m(sk, se)  # noqa: E731
+
+    def fwd_two(m, sk, se):  # reference TwoStreamSTGCAN.forward has a missing-arg bug (§0.7)
+        mot = sk[:, :2, 1:] - sk[:, :2, :-1]
+        return m.fc(torch.cat((m.stgcan_1(sk, None), m.stgcan_2(mot, None)), dim=-1))
+
+    cases = []
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_cut", num_class=11, sensor_dim=15)
+    cases.append(("har", comb.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_cut", "strategy": "spatial"}, 11,
+                                                      bilstm_input_size=15), spec, fwd_pkg, 4, 1234))
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_mmpose", num_class=11, sensor_dim=6)
+    cases.append(("ns", comb.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11,
+                                                     bilstm_input_size=6), spec, fwd_pkg, 4, 2345))
+    spec = oc.Spec(model="two_stgcan", layout="coco_cut", num_class=11, sensor="none")
+    cases.append(("two", comb.TwoStreamSTGCAN(3, {"layout": "coco_cut", "strategy": "spatial"}, 11),
+                  spec, fwd_two, 4, 3456))
+    spec = oc.Spec(model="stgcn", layout="coco_cut", num_class=11, sensor="none")
+    cases.append(("stgcn", stg.STGCAN(3, {"layout": "coco_cut", "strategy": "spatial"}, num_class=11),
+                  spec, lambda m, sk, se: m(sk, None), 3, 4567))
+    spec = oc.Spec(model="bilstm", num_class=11, sensor_dim=15)
+    cases.append(("bilstm", bil.BiLSTM(input_size=15, hidden_size=64, num_layers=1, dropout_prob=0.3,
+                                       num_classes=11, feature="mean"),
+                  spec, lambda m, sk, se: m(None, se), 5, 5678))
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_cut", num_class=2, sensor="cnn_bilstm",
+                   sensor_dim=4, sensor_classes=2, softmax_output=True, naming="notebook")
+    cases.append(("ur_nb", ns["TwoStreamSpatialTemporalGraph"]({"strategy": "spatial"}, 2),
+                  spec, lambda m, sk, se: m((sk, sk[:, :2, 1:] - sk[:, :2, :-1], se)), 4, 6789))
+    for tag, mod, spec, fn, b, seed in cases:
+        kat[tag] = run_case(tag, mod, spec, fn, b, seed)
+    with open(os.path.join(OUT, "param_counts.json"), "w") as f:
+        json.dump(kat, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
