@@ -1,0 +1,28 @@
+# Builds the gfx950 HIP library behind include/fall3.h and the C oracle pieces.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC := fall_multimodal_amd/csrc
+BLD := build
+FLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Iinclude -I$(SRC) -Wno-unused-result
+OBJS := $(BLD)/gemm.o $(BLD)/layers.o $(BLD)/sensor.o $(BLD)/head.o $(BLD)/net.o
+LIB := fall_multimodal_amd/libfall3.so
+HDRS := $(wildcard $(SRC)/*.h) include/fall3.h
+
+all: $(LIB)
+
+$(BLD):
+	mkdir -p $(BLD)
+
+$(BLD)/%.o: $(SRC)/%.hip $(HDRS) | $(BLD)
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(BLD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BLD)
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC -o $@ $(OBJS)
+
+clean:
+	rm -rf $(BLD) $(LIB)
+
+.PHONY: all clean

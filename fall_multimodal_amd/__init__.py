@@ -1,0 +1,20 @@
+"""fall_multimodal_amd — MI355X-native (gfx950) training path for the 3-stream
+fall-detection model of musaru/Fall_Multimodal (skeleton-position ST-GCAN, skeleton-motion
+ST-GCAN, IMU BiLSTM; late fusion; soft-target CE; RMSprop).
+
+Public surface mirrors the reference (Multimodal_Fall3/model/):
+    build_model(config)          -> model/build_model.py
+    build_optimizer(model, cfg)  -> model/optimizer.py
+    get_cfg_defaults()           -> model/config.py
+plus TrainStep, the fused graph-capturable step used by bench.py.
+"""
+from .config import CfgNode, get_cfg_defaults
+from .graph import Graph
+from .model import (BiLSTM, Fall3Net, NetSpec, STGCAN, TwoStreamSpatialTemporalGraph, TwoStreamSTGCAN,
+                    TwoStreamSTGCAN_BiLSTM, build_model)
+from .optim import RMSprop, build_optimizer
+from .train import TrainStep
+
+__all__ = ["build_model", "build_optimizer", "get_cfg_defaults", "CfgNode", "Graph", "Fall3Net", "NetSpec",
+           "STGCAN", "BiLSTM", "TwoStreamSTGCAN", "TwoStreamSTGCAN_BiLSTM", "TwoStreamSpatialTemporalGraph",
+           "RMSprop", "TrainStep"]

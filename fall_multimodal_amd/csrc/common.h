@@ -1,0 +1,85 @@
+// Shared device helpers for the fall3 MI355X (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define F3_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace f3 {
+
+constexpr float kBnEps = 1e-5f;
+
+// Batch-norm coefficient source. Train mode derives mean/var from fp64 batch sums that
+// the producing kernel accumulated in its epilogue; eval mode uses the running stats
+// (nn.BatchNorm semantics: biased variance for normalisation).
+struct BnRef {
+  const double* sum;      // [C] sum x          (train)
+  const double* sumsq;    // [C] sum x^2        (train)
+  const float* gamma;     // [C]
+  const float* beta;      // [C]
+  const float* rmean;     // [C] running mean   (eval)
+  const float* rvar;      // [C] running var    (eval)
+  float count;            // elements per channel in the batch
+  int eval;
+};
+
+// y = x*scale + shift ; also returns mean and 1/sqrt(var+eps) for backward formulas.
+F3_DEV void bn_coeff(const BnRef& b, int c, float& scale, float& shift, float& mean, float& rstd) {
+  if (b.eval) {
+    mean = b.rmean[c];
+    rstd = rsqrtf(b.rvar[c] + kBnEps);
+  } else {
+    double m = b.sum[c] / (double)b.count;
+    double v = b.sumsq[c] / (double)b.count - m * m;
+    if (v < 0) v = 0;
+    mean = (float)m;
+    rstd = (float)(1.0 / sqrt(v + (double)kBnEps));
+  }
+  scale = b.gamma[c] * rstd;
+  shift = b.beta[c] - mean * scale;
+}
+
+F3_DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+F3_DEV double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+F3_DEV void atomic_add_d(double* p, double v) { atomicAdd(p, v); }
+F3_DEV void atomic_add_f(float* p, float v) { atomicAdd(p, v); }
+
+F3_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+}  // namespace f3
+
+// Error plumbing for the C ABI: never abort, return a status.
+#define F3_OK 0
+#define F3_EINVAL 1001
+#define F3_EBATCH 1002   // train-mode batch of 1 (nn.BatchNorm: "Expected more than 1 value per channel")
+#define F3_EHIP 1003
+
+#include <stdio.h>
+#include <stdlib.h>
+// F3_DEBUG_SYNC=1 synchronises the device after every launch (debugging aid)
+inline bool f3_debug_sync() {
+  static const bool on = getenv("F3_DEBUG_SYNC") != nullptr;
+  return on;
+}
+#define F3_LAUNCH_CHECK()                                                              \
+  do {                                                                                 \
+    if (f3_debug_sync()) (void)hipDeviceSynchronize();                                 \
+    hipError_t _e = hipGetLastError();                                                 \
+    if (_e != hipSuccess) {                                                            \
+      fprintf(stderr, "fall3: %s:%d launch failed: %s\n", __FILE__, __LINE__,          \
+              hipGetErrorString(_e));                                                  \
+      return F3_EHIP;                                                                  \
+    }                                                                                  \
+  } while (0)

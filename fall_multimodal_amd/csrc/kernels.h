@@ -1,0 +1,61 @@
+// Internal kernel-launcher interface (host side). The public C ABI is include/fall3.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "common.h"
+
+namespace f3 {
+
+// Row geometry of a temporal conv over [N][T][V][C] rows (row m = (n*T + t)*V + v).
+struct ConvGeom {
+  int M;            // output rows = N*T_out*V
+  int Nc;           // output channels
+  int Kc;           // input channels per tap
+  int KT, S, P;     // taps, stride, zero padding
+  int transposed;   // 1: input-gradient row map of a strided conv
+  int T_out, T_in, V;
+  int lda, ldo;     // row strides (elements) of input / output
+};
+
+enum : int {
+  EPI_BIAS = 1,       // + bias[j]
+  EPI_BIASV = 2,      // + bias[v][j]  (graph-mixed gcn bias)
+  EPI_STATS = 4,      // fp64 sum / sum-of-squares per output channel (BN forward)
+  EPI_GAP = 8,        // per (clip, channel) sum over the clip's rows (channel attention pool)
+  EPI_RELUMASK = 16,  // zero where BN(aux)<=0, accumulate sum dv and sum dv*xhat(aux)
+  EPI_ADD = 32,       // out += value
+};
+
+struct ConvGemmArgs {
+  ConvGeom g;
+  const float* in;
+  const float* w;     // packed [Nc][KT*Kc]
+  float* out;
+  BnRef pro_bn;       // prologue: relu(bn(x)) on input channels
+  const float* bias;
+  double* st_sum;
+  double* st_sq;
+  float* gap;         // [N][Nc]
+  const float* aux;   // RELUMASK source rows
+  int ldaux;
+  BnRef epi_bn;
+};
+
+enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };
+
+struct WgradArgs {
+  ConvGeom g;         // geometry of the FORWARD conv (M = its output rows)
+  const float* dy;    // [M][ldy]
+  int ldy;
+  const float* in;    // forward input rows
+  float* dw;          // accumulated (+=)
+  float* db;          // [Nc] accumulated (+=) or null
+  int outmap;
+  int gcn_cin;
+  BnRef pro_bn;
+  int rows_per_split;
+};
+
+}  // namespace f3
+
+int f3_conv_gemm(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
+int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);

@@ -1,0 +1,162 @@
+// Argument blocks of the byte-moving layer kernels (layers.hip) and sensor/head kernels.
+#pragma once
+#include "common.h"
+
+namespace f3 {
+
+enum : int { PREP_MUL = 0, PREP_PACK_CONV, PREP_PACK_CONV_T, PREP_PACK_GCN, PREP_PACK_GCN_T, PREP_GCN_BIAS, PREP_COPY };
+
+struct PrepJob {
+  int type, n;
+  float* dst;
+  const float* s0;
+  const float* s1;
+  const float* s2;
+  int d0, d1, d2;
+};
+
+struct DataBnArgs {
+  int N, T, V, C, motion;
+  const float* skel;     // reference layout [N][3][T(+1)][V]
+  float* out;            // [N][T][V][C]
+  BnRef bn;
+  double* st_sum;
+  double* st_sq;
+  const float* dout;     // backward
+  float* dgamma;
+  float* dbeta;
+};
+
+struct MixArgs {
+  int K, V, Cin, frames;
+  const float* A;        // A_eff [K][V][V]
+  const float* x;        // [frames][V][Cin]
+  float* z;              // [frames][V][K][Cin] (fwd out / bwd in)
+  float* dx;             // bwd out
+  float* dA;             // bwd accumulate [K][V][V]
+  int accumulate;
+};
+
+struct GcnBiasBwdArgs {
+  int K, V, C;
+  const float* Aeff;
+  const float* A;
+  const float* G;        // [V][C] per-node column sums of dg
+  const float* bias;     // gcn conv bias [K*C]
+  float* db;
+  const float* dAeff;
+  float* dE;
+};
+
+enum : int { RES_NONE = 0, RES_ID = 1, RES_CONV = 2 };
+
+struct BlockArgs {
+  int N, TV, C, chunks, res_kind;
+  float inv_tv;
+  BnRef bn2, bnr;
+  const float* h;        // tcn output before BN2 [M][C]
+  const float* r;        // residual conv output before BN_r
+  const float* x;        // block input (identity residual)
+  const float* att;      // channel attention [N][C]
+  float* out;            // block output [M][C]
+  float* pool;           // [N][C] mean over (T,V) or null
+  // backward
+  const float* dout;     // [M][C] or null when dout_nc is given
+  const float* dout_nc;  // [N][C] gradient of the pooled mean (broadcast * inv_tv)
+  float* P1;
+  float* P2;
+  double* bnr_bsum;
+  double* bnr_bsq;
+  const double* bn2_bsum;
+  const double* bn2_bsq;
+  const float* e;        // [N][C] dgap / TV
+  float* dh;
+  float* dres;           // dr (conv) or dx (identity)
+  float* dgamma2;
+  float* dbeta2;
+  float* dgammar;
+  float* dbetar;
+};
+
+struct BnBwdArgs {
+  int N, TV, C, V, chunks;
+  BnRef bn;
+  const double* bsum;
+  const double* bsq;
+  float* dgamma;
+  float* dbeta;
+  const float* dv;
+  const float* g;
+  float* dg;
+  float* G;              // [V][C]
+};
+
+struct CaArgs {
+  int N, C;
+  float inv_tv;
+  BnRef bn2, bnca;
+  const float* W1;       // [C/4][C]
+  const float* b1;
+  const float* W2;       // [C][C/4]
+  const float* b2;
+  const float* gapsum;   // [N][C] sum over rows of the tcn output (pre-BN2)
+  float* q1;             // [N][C/4]
+  float* hid;            // [N][C/4]
+  float* att;            // [N][C]
+  double* ca_sum;
+  double* ca_sq;
+  // backward
+  const float* P1;
+  const float* P2;
+  float* dq2;
+  float* dbn;
+  float* dq1;
+  float* e;
+  double* bn2_bsum;
+  double* bn2_bsq;
+  float* g_bnca_gamma;
+  float* g_bnca_beta;
+  float* g_b1;
+  float* g_W1;
+  float* g_W2;
+  float* g_b2;
+};
+
+struct BnRunJob {
+  const double* sum;
+  const double* sumsq;
+  double count;
+  int C;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+};
+
+// job tables travel as kernel arguments (by value, < 4 KB), so a step needs no
+// host->device copies and stays graph-capturable
+constexpr int kMaxPrepJobs = 56;
+struct PrepTable {
+  int n;
+  PrepJob jobs[kMaxPrepJobs];
+};
+constexpr int kMaxBnJobs = 56;
+struct BnRunTable {
+  int n;
+  BnRunJob jobs[kMaxBnJobs];
+};
+
+}  // namespace f3
+
+int f3_prep(const f3::PrepTable& t, hipStream_t s);
+int f3_databn_fwd(const f3::DataBnArgs* a, hipStream_t s);
+int f3_databn_bwd(const f3::DataBnArgs* a, hipStream_t s);
+int f3_mix_fwd(const f3::MixArgs* a, hipStream_t s);
+int f3_mix_bwd(const f3::MixArgs* a, hipStream_t s);
+int f3_gcn_bias_bwd(const f3::GcnBiasBwdArgs* a, hipStream_t s);
+int f3_block_out(f3::BlockArgs a, hipStream_t s);
+int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);
+int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);
+int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
+int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);
+int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);
+int f3_bn_running(const f3::BnRunTable& t, hipStream_t s);

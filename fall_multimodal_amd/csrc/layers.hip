@@ -1,0 +1,773 @@
+// Per-layer byte-moving kernels of the st_gcan block and the skeleton stream ends:
+// data_bn, graph mix (A_eff einsum), BatchNorm apply / backward, channel attention,
+// residual + ReLU, average pool, weight packing and running-stat updates.
+//
+// Activations are channels-last rows [N][T][V][C] (row m = (n*T+t)*V + v). Elementwise
+// kernels give each workgroup a chunk of ONE clip's rows, so per-(clip, channel)
+// reductions (the channel-attention pool, its backward) finish in LDS and cost one
+// atomic per channel per workgroup.
+#include "common.h"
+#include "layers.h"
+
+namespace f3 {
+
+// ----------------------------------------------------------------------------
+// prep: A_eff = A * E, gcn bias through the graph, weight packing  (one launch)
+// ----------------------------------------------------------------------------
+__global__ void prep_kernel(PrepTable t) {
+  const PrepJob j = t.jobs[blockIdx.y];
+  const int stride = gridDim.x * blockDim.x;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) {
+    switch (j.type) {
+      case PREP_MUL:
+        j.dst[e] = j.s0[e] * j.s1[e];
+        break;
+      case PREP_COPY:
+        j.dst[e] = j.s0[e];
+        break;
+      case PREP_PACK_CONV: {  // src [J][I][KT] -> dst [J][KT*I] (k = dt*I + i)
+        const int J = j.d0, I = j.d1, KT = j.d2;
+        const int jj = e / (KT * I), r = e - jj * KT * I, dt = r / I, i = r - dt * I;
+        (void)J;
+        j.dst[e] = j.s0[((size_t)jj * I + i) * KT + dt];
+        break;
+      }
+      case PREP_PACK_CONV_T: {  // dgrad operand: dst [I][KT*J] (k = dt*J + j)
+        const int J = j.d0, I = j.d1, KT = j.d2;
+        const int i = e / (KT * J), r = e - i * KT * J, dt = r / J, jj = r - dt * J;
+        j.dst[e] = j.s0[((size_t)jj * I + i) * KT + dt];
+        break;
+      }
+      case PREP_PACK_GCN: {  // W[k*C+c][ci] -> dst [C][K*Cin] (k-major then ci)
+        const int C = j.d0, Cin = j.d1, K = j.d2;
+        const int c = e / (K * Cin), r = e - c * K * Cin, k = r / Cin, ci = r - k * Cin;
+        j.dst[e] = j.s0[((size_t)k * C + c) * Cin + ci];
+        break;
+      }
+      case PREP_PACK_GCN_T: {  // dgrad operand: dst [K*Cin][C]
+        const int C = j.d0, Cin = j.d1;
+        const int kc = e / C, c = e - kc * C, k = kc / Cin, ci = kc - k * Cin;
+        j.dst[e] = j.s0[((size_t)k * C + c) * Cin + ci];
+        break;
+      }
+      case PREP_GCN_BIAS: {  // dst[w][c] = sum_k colsum(A*E)_k[w] * b[k*C+c]
+        const int C = j.d0, V = j.d1, K = j.d2;
+        const int w = e / C, c = e - w * C;
+        float acc = 0.f;
+        for (int k = 0; k < K; ++k) {
+          float cs = 0.f;
+          for (int v = 0; v < V; ++v) cs += j.s0[(k * V + v) * V + w] * j.s1[(k * V + v) * V + w];
+          acc += cs * j.s2[k * C + c];
+        }
+        j.dst[e] = acc;
+        break;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// data_bn (stgcan.py:213-218): BatchNorm1d over V*C channels (index v*C + c), stats
+// over (N, T). The motion stream's input (combination.py:39) is formed on the fly.
+// ----------------------------------------------------------------------------
+F3_DEV float stream_in(const float* skel, int motion, int n, int c, int t, int v, int T, int V) {
+  // skel is the reference layout [N][3][T][V]; motion: [N][2][T-1][V] = skel[t+1]-skel[t]
+  const int Ts = motion ? T + 1 : T;
+  const float* p = skel + (((size_t)n * 3 + c) * Ts + t) * V + v;
+  return motion ? (p[V] - p[0]) : p[0];
+}
+
+__global__ void databn_stats_kernel(DataBnArgs a) {
+  const int ch = blockIdx.x, v = ch / a.C, c = ch - v * a.C;
+  double s = 0.0, q = 0.0;
+  for (int e = threadIdx.x; e < a.N * a.T; e += blockDim.x) {
+    const int n = e / a.T, t = e - n * a.T;
+    const float x = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V);
+    s += x;
+    q += (double)x * x;
+  }
+  __shared__ double rs[2][16];
+  s = warp_sum_d(s);
+  q = warp_sum_d(q);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { rs[0][w] = s; rs[1][w] = q; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double S = 0, Q = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { S += rs[0][i]; Q += rs[1][i]; }
+    a.st_sum[ch] = S;
+    a.st_sq[ch] = Q;
+  }
+}
+
+__global__ void databn_apply_kernel(DataBnArgs a) {
+  const int total = a.N * a.T * a.V * a.C;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c = e % a.C, m = e / a.C, v = m % a.V, nt = m / a.V, t = nt % a.T, n = nt / a.T;
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn, v * a.C + c, sc, sh, mu, rs);
+    a.out[e] = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V) * sc + sh;
+  }
+}
+
+// d gamma / d beta of data_bn from the gradient of its (channels-last) output
+__global__ void databn_bwd_kernel(DataBnArgs a) {
+  const int ch = blockIdx.x, v = ch / a.C, c = ch - v * a.C;
+  float sc, sh, mu, rs;
+  bn_coeff(a.bn, ch, sc, sh, mu, rs);
+  double s = 0.0, q = 0.0;
+  for (int e = threadIdx.x; e < a.N * a.T; e += blockDim.x) {
+    const int n = e / a.T, t = e - n * a.T;
+    const float x = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V);
+    const float dy = a.dout[(((size_t)n * a.T + t) * a.V + v) * a.C + c];
+    s += dy;
+    q += (double)dy * ((x - mu) * rs);
+  }
+  __shared__ double rsd[2][16];
+  s = warp_sum_d(s);
+  q = warp_sum_d(q);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { rsd[0][w] = s; rsd[1][w] = q; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double S = 0, Q = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { S += rsd[0][i]; Q += rsd[1][i]; }
+    a.dgamma[ch] += (float)Q;
+    a.dbeta[ch] += (float)S;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// graph mix (stgcan.py:54, reordered): Z[(f,w), k*Cin+ci] = sum_v A_eff[k,v,w] x[(f,v),ci]
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mix_fwd_kernel(MixArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* As = sm;                       // [K][V][V]
+  float* xs = sm + a.K * a.V * a.V;     // [V][Cin]
+  const int KVV = a.K * a.V * a.V;
+  for (int i = threadIdx.x; i < KVV; i += blockDim.x) As[i] = a.A[i];
+  const int per = a.V * a.Cin;
+  const int outs = a.V * a.K * a.Cin;
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = a.x[(size_t)f * per + i];
+    __syncthreads();
+    for (int o = threadIdx.x; o < outs; o += blockDim.x) {
+      const int ci = o % a.Cin, wk = o / a.Cin, k = wk % a.K, w = wk / a.K;
+      float acc = 0.f;
+      for (int v = 0; v < a.V; ++v) acc += As[(k * a.V + v) * a.V + w] * xs[v * a.Cin + ci];
+      a.z[(size_t)f * outs + o] = acc;
+    }
+  }
+}
+
+// dx[(f,v),ci] (+)= sum_{k,w} A_eff[k,v,w] dZ[(f,w),(k,ci)]
+// dA[k,v,w]   += sum_{f,ci} x[(f,v),ci] dZ[(f,w),(k,ci)]
+__global__ __launch_bounds__(256) void mix_bwd_kernel(MixArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int KVV = a.K * a.V * a.V;
+  const int per = a.V * a.Cin, outs = a.V * a.K * a.Cin;
+  float* As = sm;                 // [K][V][V]
+  float* xs = As + KVV;           // [V][Cin]
+  float* zs = xs + per;           // [V][K][Cin]
+  for (int i = threadIdx.x; i < KVV; i += blockDim.x) As[i] = a.A[i];
+  // dA accumulators: each thread owns up to 4 (k,v,w) entries
+  float dacc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = a.x[(size_t)f * per + i];
+    for (int i = threadIdx.x; i < outs; i += blockDim.x) zs[i] = a.z[(size_t)f * outs + i];
+    __syncthreads();
+    for (int o = threadIdx.x; o < per; o += blockDim.x) {
+      const int ci = o % a.Cin, v = o / a.Cin;
+      float acc = 0.f;
+      for (int k = 0; k < a.K; ++k)
+        for (int w = 0; w < a.V; ++w) acc += As[(k * a.V + v) * a.V + w] * zs[(w * a.K + k) * a.Cin + ci];
+      float* dst = a.dx + (size_t)f * per + o;
+      if (a.accumulate) *dst += acc;
+      else *dst = acc;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + q * blockDim.x;
+      if (idx >= KVV) break;
+      const int k = idx / (a.V * a.V), r = idx - k * a.V * a.V, v = r / a.V, w = r - v * a.V;
+      const float* xr = xs + v * a.Cin;
+      const float* zr = zs + (w * a.K + k) * a.Cin;
+      float acc = 0.f;
+      for (int ci = 0; ci < a.Cin; ++ci) acc += xr[ci] * zr[ci];
+      dacc[q] += acc;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = threadIdx.x + q * blockDim.x;
+    if (idx < KVV) atomic_add_f(a.dA + idx, dacc[q]);
+  }
+}
+
+// gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
+// dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
+__global__ void gcn_bias_bwd_kernel(GcnBiasBwdArgs a) {
+  const int KVV = a.K * a.V * a.V;
+  for (int e = threadIdx.x; e < a.K * a.C; e += blockDim.x) {
+    const int k = e / a.C, c = e - k * a.C;
+    float acc = 0.f;
+    for (int w = 0; w < a.V; ++w) {
+      float cs = 0.f;
+      for (int v = 0; v < a.V; ++v) cs += a.Aeff[(k * a.V + v) * a.V + w];
+      acc += cs * a.G[w * a.C + c];
+    }
+    a.db[e] += acc;
+  }
+  for (int e = threadIdx.x; e < KVV; e += blockDim.x) {
+    const int k = e / (a.V * a.V), w = e % a.V;
+    float acc = 0.f;
+    for (int c = 0; c < a.C; ++c) acc += a.bias[k * a.C + c] * a.G[w * a.C + c];
+    a.dE[e] += a.A[e] * (a.dAeff[e] + acc);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// clip-chunk elementwise kernels. Thread t handles channel quad t % C4 of rows
+// t / C4, t / C4 + RP, ... of its chunk (C4 = C/4, RP = 256/C4).
+// ----------------------------------------------------------------------------
+F3_DEV void chunk_rows(int TV, int chunks, int& r0, int& r1) {
+  const int n = blockIdx.y, ch = blockIdx.x;
+  const int per = (TV + chunks - 1) / chunks;
+  r0 = n * TV + ch * per;
+  r1 = min(n * TV + TV, r0 + per);
+}
+
+// reduce float4 partials over the RP row-lanes sharing a channel quad; returns in thread cq < C4
+F3_DEV f32x4 quad_reduce(f32x4 v, float* lds, int C4) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  reinterpret_cast<f32x4*>(lds)[tid] = v;
+  __syncthreads();
+  f32x4 r = {0.f, 0.f, 0.f, 0.f};
+  if (tid < C4) {
+    for (int i = tid; i < 256; i += C4) r += reinterpret_cast<f32x4*>(lds)[i];
+  }
+  return r;
+}
+
+// out = relu(bn2(h) * a[n,c] + res), res = bn_r(r) | x | 0 ; optional pooled mean
+__global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
+  __shared__ float sc2[256], sh2[256], scr[256], shr[256];
+  __shared__ __attribute__((aligned(16))) float lds[1024];
+  const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
+  for (int c = tid; c < C; c += 256) {
+    float mu, rs;
+    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
+    if (a.res_kind == RES_CONV) bn_coeff(a.bnr, c, scr[c], shr[c], mu, rs);
+  }
+  __syncthreads();
+  int r0, r1;
+  chunk_rows(a.TV, a.chunks, r0, r1);
+  const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
+  f32x4 pool = {0.f, 0.f, 0.f, 0.f};
+  for (int m = r0 + tid / C4; m < r1; m += RP) {
+    const size_t off = (size_t)m * C + c0;
+    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    f32x4 res = {0.f, 0.f, 0.f, 0.f};
+    if (a.res_kind == RES_CONV) res = *reinterpret_cast<const f32x4*>(a.r + off);
+    else if (a.res_kind == RES_ID) res = *reinterpret_cast<const f32x4*>(a.x + off);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float rv = res[e];
+      if (a.res_kind == RES_CONV) rv = rv * scr[c0 + e] + shr[c0 + e];
+      o[e] = fmaxf((h[e] * sc2[c0 + e] + sh2[c0 + e]) * av[e] + rv, 0.f);
+    }
+    *reinterpret_cast<f32x4*>(a.out + off) = o;
+    pool += o;
+  }
+  if (a.pool) {
+    f32x4 r = quad_reduce(pool, lds, C4);
+    if (tid < C4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomic_add_f(a.pool + (size_t)n * C + tid * 4 + e, r[e] * a.inv_tv);
+    }
+  }
+}
+
+// backward reductions over a block's output gradient:
+//   dz = dout * (out > 0);  P1[n,c] = sum_tv dz;  P2[n,c] = sum_tv dz*xhat2
+//   conv residual: R[c] += (sum dz, sum dz*xhat_r)
+__global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
+  __shared__ float mu2[256], rs2[256], mur[256], rsr[256];
+  __shared__ __attribute__((aligned(16))) float lds[1024];
+  const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
+  for (int c = tid; c < C; c += 256) {
+    float sc, sh;
+    bn_coeff(a.bn2, c, sc, sh, mu2[c], rs2[c]);
+    if (a.res_kind == RES_CONV) bn_coeff(a.bnr, c, sc, sh, mur[c], rsr[c]);
+  }
+  __syncthreads();
+  int r0, r1;
+  chunk_rows(a.TV, a.chunks, r0, r1);
+  const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  f32x4 p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, q1 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
+  f32x4 dbc = {0, 0, 0, 0};
+  if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
+  for (int m = r0 + tid / C4; m < r1; m += RP) {
+    const size_t off = (size_t)m * C + c0;
+    const f32x4 o = *reinterpret_cast<const f32x4*>(a.out + off);
+    const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
+    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    f32x4 rr = {0, 0, 0, 0};
+    if (a.res_kind == RES_CONV) rr = *reinterpret_cast<const f32x4*>(a.r + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float dz = o[e] > 0.f ? d[e] : 0.f;
+      p1[e] += dz;
+      p2[e] += dz * ((h[e] - mu2[c0 + e]) * rs2[c0 + e]);
+      if (a.res_kind == RES_CONV) {
+        q1[e] += dz;
+        q2[e] += dz * ((rr[e] - mur[c0 + e]) * rsr[c0 + e]);
+      }
+    }
+  }
+  f32x4 s1 = quad_reduce(p1, lds, C4);
+  if (tid < C4) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomic_add_f(a.P1 + (size_t)n * C + tid * 4 + e, s1[e]);
+  }
+  f32x4 s2 = quad_reduce(p2, lds, C4);
+  if (tid < C4) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomic_add_f(a.P2 + (size_t)n * C + tid * 4 + e, s2[e]);
+  }
+  if (a.res_kind == RES_CONV) {
+    f32x4 t1 = quad_reduce(q1, lds, C4);
+    if (tid < C4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomic_add_d(a.bnr_bsum + tid * 4 + e, (double)t1[e]);
+    }
+    f32x4 t2 = quad_reduce(q2, lds, C4);
+    if (tid < C4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomic_add_d(a.bnr_bsq + tid * 4 + e, (double)t2[e]);
+    }
+  }
+}
+
+// dh = g2*rs2*(dz*a + e - D1/M - xhat2*D2/M);  residual: dr (conv) or dx = dz (identity)
+__global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
+  __shared__ float mu2[256], k2[256], m1[256], m2[256], rs2[256];
+  __shared__ float mur[256], kr[256], n1[256], n2[256], rsr[256];
+  const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
+  const float invM = 1.f / (float)a.bn2.count;
+  for (int c = tid; c < C; c += 256) {
+    float sc, sh, rs;
+    bn_coeff(a.bn2, c, sc, sh, mu2[c], rs);
+    rs2[c] = rs;
+    k2[c] = a.bn2.gamma[c] * rs;
+    m1[c] = (float)a.bn2_bsum[c] * invM;
+    m2[c] = (float)a.bn2_bsq[c] * invM;
+    if (a.res_kind == RES_CONV) {
+      bn_coeff(a.bnr, c, sc, sh, mur[c], rs);
+      rsr[c] = rs;
+      kr[c] = a.bnr.gamma[c] * rs;
+      n1[c] = (float)a.bnr_bsum[c] * invM;
+      n2[c] = (float)a.bnr_bsq[c] * invM;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
+    for (int c = tid; c < C; c += 256) {
+      a.dgamma2[c] += (float)a.bn2_bsq[c];
+      a.dbeta2[c] += (float)a.bn2_bsum[c];
+      if (a.res_kind == RES_CONV) {
+        a.dgammar[c] += (float)a.bnr_bsq[c];
+        a.dbetar[c] += (float)a.bnr_bsum[c];
+      }
+    }
+  }
+  int r0, r1;
+  chunk_rows(a.TV, a.chunks, r0, r1);
+  const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
+  const f32x4 ev = *reinterpret_cast<const f32x4*>(a.e + (size_t)n * C + c0);
+  f32x4 dbc = {0, 0, 0, 0};
+  if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
+  for (int m = r0 + tid / C4; m < r1; m += RP) {
+    const size_t off = (size_t)m * C + c0;
+    const f32x4 o = *reinterpret_cast<const f32x4*>(a.out + off);
+    const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
+    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    f32x4 dh, dr;
+    f32x4 rr = {0, 0, 0, 0};
+    if (a.res_kind == RES_CONV) rr = *reinterpret_cast<const f32x4*>(a.r + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + e;
+      const float dz = o[e] > 0.f ? d[e] : 0.f;
+      const float xh = (h[e] - mu2[c]) * rs2[c];
+      dh[e] = k2[c] * (dz * av[e] + ev[e] - m1[c] - xh * m2[c]);
+      if (a.res_kind == RES_CONV) {
+        const float xr = (rr[e] - mur[c]) * rsr[c];
+        dr[e] = kr[c] * (dz - n1[c] - xr * n2[c]);
+      } else {
+        dr[e] = dz;
+      }
+    }
+    *reinterpret_cast<f32x4*>(a.dh + off) = dh;
+    if (a.res_kind != RES_NONE) *reinterpret_cast<f32x4*>(a.dres + off) = dr;
+  }
+}
+
+// BN1 backward: dg = g1*rs1*(dv - S1/M - xhat1*S2/M); G[v][c] += dg (gcn bias grad)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
+  __shared__ float mu[256], kk[256], m1[256], m2[256], rsv[256];
+  extern __shared__ __attribute__((aligned(16))) float gl[];  // [V][C]
+  const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
+  const float invM = 1.f / (float)a.bn.count;
+  for (int c = tid; c < C; c += 256) {
+    float sc, sh, rs;
+    bn_coeff(a.bn, c, sc, sh, mu[c], rs);
+    rsv[c] = rs;
+    kk[c] = a.bn.gamma[c] * rs;
+    m1[c] = (float)a.bsum[c] * invM;
+    m2[c] = (float)a.bsq[c] * invM;
+  }
+  for (int i = tid; i < a.V * C; i += 256) gl[i] = 0.f;
+  __syncthreads();
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
+    for (int c = tid; c < C; c += 256) {
+      a.dgamma[c] += (float)a.bsq[c];
+      a.dbeta[c] += (float)a.bsum[c];
+    }
+  }
+  int r0, r1;
+  chunk_rows(a.TV, a.chunks, r0, r1);
+  const int cq = tid % C4, c0 = cq * 4;
+  for (int m = r0 + tid / C4; m < r1; m += RP) {
+    const size_t off = (size_t)m * C + c0;
+    const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dv + off);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(a.g + off);
+    f32x4 o;
+    const int v = m % a.V;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + e;
+      const float xh = (g[e] - mu[c]) * rsv[c];
+      o[e] = kk[c] * (dv[e] - m1[c] - xh * m2[c]);
+      atomicAdd(&gl[v * C + c], o[e]);
+    }
+    *reinterpret_cast<f32x4*>(a.dg + off) = o;
+  }
+  __syncthreads();
+  for (int i = tid; i < a.V * C; i += 256) atomic_add_f(a.G + i, gl[i]);
+}
+
+// ----------------------------------------------------------------------------
+// channel attention (stgcan.py:59-74)
+// ----------------------------------------------------------------------------
+F3_DEV float block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+// one workgroup per hidden unit j: q = W1 gap + b1, BN over the batch, ReLU
+__global__ __launch_bounds__(256) void ca_fwd1_kernel(CaArgs a) {
+  __shared__ float w1[256], sc2[256], sh2[256], red[8];
+  const int j = blockIdx.x, C = a.C, H = C / 4;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float mu, rs;
+    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
+    w1[c] = a.W1[j * C + c];
+  }
+  __syncthreads();
+  float s = 0.f, s2 = 0.f;
+  for (int n = threadIdx.x; n < a.N; n += 256) {
+    float q = a.b1[j];
+    const float* gp = a.gapsum + (size_t)n * C;
+    for (int c = 0; c < C; ++c) q += w1[c] * (gp[c] * a.inv_tv * sc2[c] + sh2[c]);
+    a.q1[(size_t)n * H + j] = q;
+    s += q;
+    s2 += q * q;
+  }
+  s = block_sum(s, red);
+  s2 = block_sum(s2, red);
+  if (threadIdx.x == 0 && !a.bnca.eval) {
+    a.ca_sum[j] = (double)s;
+    a.ca_sq[j] = (double)s2;
+  }
+  float mean, rstd;
+  if (a.bnca.eval) {
+    mean = a.bnca.rmean[j];
+    rstd = rsqrtf(a.bnca.rvar[j] + kBnEps);
+  } else {
+    mean = s / (float)a.N;
+    float var = fmaxf(s2 / (float)a.N - mean * mean, 0.f);
+    rstd = rsqrtf(var + kBnEps);
+  }
+  const float gm = a.bnca.gamma[j] * rstd, bt = a.bnca.beta[j] - mean * gm;
+  for (int n = threadIdx.x; n < a.N; n += 256) {
+    const float q = a.q1[(size_t)n * H + j];
+    a.hid[(size_t)n * H + j] = fmaxf(q * gm + bt, 0.f);
+  }
+}
+
+// one workgroup per clip: a = sigmoid(W2 hid + b2)
+__global__ __launch_bounds__(256) void ca_fwd2_kernel(CaArgs a) {
+  __shared__ float hs[64];
+  const int n = blockIdx.x, C = a.C, H = C / 4;
+  if (threadIdx.x < H) hs[threadIdx.x] = a.hid[(size_t)n * H + threadIdx.x];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float q = a.b2[c];
+    const float* w = a.W2 + (size_t)c * H;
+    for (int k = 0; k < H; ++k) q += w[k] * hs[k];
+    a.att[(size_t)n * C + c] = sigmoidf_(q);
+  }
+}
+
+// per clip: da = g2*P2 + b2*P1 ; dq2 = da*a*(1-a) ; dhid = W2^T dq2 ; dbn = dhid*(hid>0)
+__global__ __launch_bounds__(256) void ca_bwd1_kernel(CaArgs a) {
+  __shared__ float dq[256];
+  const int n = blockIdx.x, C = a.C, H = C / 4;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float da = a.bn2.gamma[c] * a.P2[(size_t)n * C + c] + a.bn2.beta[c] * a.P1[(size_t)n * C + c];
+    const float at = a.att[(size_t)n * C + c];
+    const float d = da * at * (1.f - at);
+    dq[c] = d;
+    a.dq2[(size_t)n * C + c] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x < H) {
+    const int j = threadIdx.x;
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc += dq[c] * a.W2[(size_t)c * H + j];
+    a.dbn[(size_t)n * H + j] = a.hid[(size_t)n * H + j] > 0.f ? acc : 0.f;
+  }
+}
+
+// per hidden unit j: BN(batch) backward -> dq1; dW1, db1, dW2[:,j], db2, BN grads
+__global__ __launch_bounds__(256) void ca_bwd2_kernel(CaArgs a) {
+  __shared__ float dq1s[256], hs[256], red[8];
+  __shared__ float sc2[256], sh2[256];
+  const int j = blockIdx.x, C = a.C, H = C / 4, N = a.N;
+  const float mean = (float)(a.ca_sum[j] / N);
+  const float var = fmaxf((float)(a.ca_sq[j] / N) - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + kBnEps);
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float d = a.dbn[(size_t)n * H + j];
+    const float xh = (a.q1[(size_t)n * H + j] - mean) * rstd;
+    s1 += d;
+    s2 += d * xh;
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  const float k = a.bnca.gamma[j] * rstd;
+  float db1 = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float d = a.dbn[(size_t)n * H + j];
+    const float xh = (a.q1[(size_t)n * H + j] - mean) * rstd;
+    const float dq = k * (d - s1 / N - xh * s2 / N);
+    dq1s[n] = dq;
+    a.dq1[(size_t)n * H + j] = dq;
+    hs[n] = a.hid[(size_t)n * H + j];
+    db1 += dq;
+  }
+  db1 = block_sum(db1, red);
+  if (threadIdx.x == 0) {
+    a.g_bnca_gamma[j] += s2;
+    a.g_bnca_beta[j] += s1;
+    a.g_b1[j] += db1;
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float mu, rs;
+    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float w1g = 0.f, w2g = 0.f, b2g = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float gap = a.gapsum[(size_t)n * C + c] * a.inv_tv * sc2[c] + sh2[c];
+      w1g += dq1s[n] * gap;
+      const float d2 = a.dq2[(size_t)n * C + c];
+      w2g += d2 * hs[n];
+      b2g += d2;
+    }
+    a.g_W1[(size_t)j * C + c] += w1g;
+    a.g_W2[(size_t)c * H + j] += w2g;
+    if (j == 0) a.g_b2[c] += b2g;
+  }
+}
+
+// per clip: dgap = W1^T dq1 ; e = dgap/TV ; BN2 backward sums D1, D2
+__global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
+  __shared__ float dq[64];
+  const int n = blockIdx.x, C = a.C, H = C / 4;
+  if (threadIdx.x < H) dq[threadIdx.x] = a.dq1[(size_t)n * H + threadIdx.x];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float dg = 0.f;
+    for (int k = 0; k < H; ++k) dg += dq[k] * a.W1[(size_t)k * C + c];
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn2, c, sc, sh, mu, rs);
+    const size_t o = (size_t)n * C + c;
+    a.e[o] = dg * a.inv_tv;
+    const float at = a.att[o];
+    const float xsum = (a.gapsum[o] - mu / a.inv_tv) * rs;  // sum_tv xhat2
+    atomic_add_d(a.bn2_bsum + c, (double)(at * a.P1[o] + dg));
+    atomic_add_d(a.bn2_bsq + c, (double)(at * a.P2[o] + dg * a.inv_tv * xsum));
+  }
+}
+
+// ----------------------------------------------------------------------------
+// BatchNorm running statistics (momentum 0.1, unbiased variance), all BNs at once
+// ----------------------------------------------------------------------------
+__global__ void bn_running_kernel(BnRunTable t) {
+  const BnRunJob j = t.jobs[blockIdx.x];
+  const double cnt = j.count;
+  for (int c = threadIdx.x; c < j.C; c += blockDim.x) {
+    const double m = j.sum[c] / cnt;
+    double v = j.sumsq[c] / cnt - m * m;
+    if (v < 0) v = 0;
+    const double vu = cnt > 1 ? v * cnt / (cnt - 1) : v;
+    j.rmean[c] = (float)(0.9 * j.rmean[c] + 0.1 * m);
+    j.rvar[c] = (float)(0.9 * j.rvar[c] + 0.1 * vu);
+  }
+  if (threadIdx.x == 0 && j.nbt) j.nbt[0] += 1;
+}
+
+}  // namespace f3
+
+using namespace f3;
+
+int f3_prep(const PrepTable& t, hipStream_t s) {
+  if (t.n <= 0) return F3_OK;
+  if (t.n > kMaxPrepJobs) return F3_EINVAL;
+  hipLaunchKernelGGL(prep_kernel, dim3(64, t.n), dim3(256), 0, s, t);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_databn_fwd(const DataBnArgs* a, hipStream_t s) {
+  if (!a->bn.eval) {
+    hipLaunchKernelGGL(databn_stats_kernel, dim3(a->V * a->C), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+  }
+  const int total = a->N * a->T * a->V * a->C;
+  hipLaunchKernelGGL(databn_apply_kernel, dim3(min(2048, (total + 255) / 256)), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_databn_bwd(const DataBnArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(databn_bwd_kernel, dim3(a->V * a->C), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+static size_t mix_lds(const MixArgs& a, bool bwd) {
+  size_t f = (size_t)a.K * a.V * a.V + (size_t)a.V * a.Cin;
+  if (bwd) f += (size_t)a.V * a.K * a.Cin;
+  return f * sizeof(float);
+}
+
+// kernels with no static LDS may take up to the full 160 KiB as dynamic LDS
+static void allow_big_lds(const void* fn) {
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipGetLastError();  // a refused attribute must not surface as the next launch's error
+}
+
+int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
+  static bool once = (allow_big_lds((const void*)mix_fwd_kernel), true);
+  (void)once;
+  if (mix_lds(*a, false) > 160 * 1024) return F3_EINVAL;
+  const int grid = min(a->frames, 2048);
+  hipLaunchKernelGGL(mix_fwd_kernel, dim3(grid), dim3(256), mix_lds(*a, false), s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
+  static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
+  (void)once;
+  if (a->K * a->V * a->V > 1024 || mix_lds(*a, true) > 160 * 1024) return F3_EINVAL;
+  const int grid = min(a->frames, 1024);
+  hipLaunchKernelGGL(mix_bwd_kernel, dim3(grid), dim3(256), mix_lds(*a, true), s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(gcn_bias_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
+
+int f3_block_out(BlockArgs a, hipStream_t s) {
+  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
+  a.chunks = chunks_for(a.TV);
+  hipLaunchKernelGGL(block_out_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
+  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
+  a.chunks = chunks_for(a.TV);
+  hipLaunchKernelGGL(block_bwd_reduce_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
+  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
+  a.chunks = chunks_for(a.TV);
+  hipLaunchKernelGGL(block_bwd_apply_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
+  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4) || (size_t)a.V * a.C * 4 > 60 * 1024) return F3_EINVAL;
+  a.chunks = chunks_for(a.TV);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(a.chunks, a.N), dim3(256), (size_t)a.V * a.C * 4, s, a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
+  if (a->C > 256 || a->N > 256 * 64) return F3_EINVAL;
+  hipLaunchKernelGGL(ca_fwd1_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ca_fwd2_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
+  if (a->C > 256 || a->N > 256) return F3_EINVAL;
+  hipLaunchKernelGGL(ca_bwd1_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ca_bwd3_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_bn_running(const BnRunTable& t, hipStream_t s) {
+  if (t.n <= 0) return F3_OK;
+  if (t.n > kMaxBnJobs) return F3_EINVAL;
+  hipLaunchKernelGGL(bn_running_kernel, dim3(t.n), dim3(256), 0, s, t);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}

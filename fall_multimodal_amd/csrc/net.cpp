@@ -1,0 +1,999 @@
+// Native network plan + step schedule behind the C ABI (include/fall3.h).
+//
+// The plan mirrors the reference module tree (build_model.py:5-19 ->
+// combination.py TwoStreamSTGCAN(_BiLSTM) / stgcan.py STGCAN / bilstm.py BiLSTM and the
+// UR notebook CNN_BiLSTM) as a flat parameter table whose names, order and shapes are
+// exactly the reference state_dict, so checkpoints interchange. Parameters, buffers and
+// gradients live in flat arrays owned by the caller; activations, saved tensors, packed
+// weights and reduction scratch live in one caller-provided workspace whose layout is a
+// pure function of the batch size.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "layers.h"
+#include "sensor.h"
+#include "fall3.h"
+
+using namespace f3;
+
+namespace {
+
+struct Entry {
+  std::string name;
+  int kind;
+  std::vector<int64_t> shape;
+  int64_t offset, numel;
+};
+
+struct BnIdx {
+  int w = -1, b = -1, rm = -1, rv = -1, nbt = -1, C = 0;
+};
+
+struct LayerIdx {
+  int cin, cout, stride, res, T_in, T_out;
+  int gcn_w, gcn_b, tcn_w, tcn_b, res_w = -1, res_b = -1, ca_w1, ca_b1, ca_w2, ca_b2, edge;
+  BnIdx bn1, bn2, bnr, bnca;
+};
+
+struct StreamIdx {
+  int cin, T, motion, A;
+  BnIdx dbn;
+  LayerIdx L[7];
+  int cls_w = -1, cls_b = -1;
+};
+
+struct LstmIdx {
+  int wih[2], whh[2], bih[2], bhh[2];
+  BnIdx bn;
+  int ca_w1, ca_b1, ca_w2, ca_b2, fc_w, fc_b;
+  int S, Cs;
+};
+
+struct CnnIdx {
+  int w1, b1, w2, b2, fcw, fcb;
+  BnIdx bn1, bn2;
+};
+
+const int kChan[7][4] = {{-1, 64, 1, RES_NONE}, {64, 64, 1, RES_ID},    {64, 64, 1, RES_ID},
+                         {64, 128, 2, RES_CONV}, {128, 128, 1, RES_ID}, {128, 256, 2, RES_CONV},
+                         {256, 256, 1, RES_ID}};  // stgcan.py:182-194
+
+}  // namespace
+
+struct f3_net {
+  f3_config cfg;
+  std::vector<Entry> entries;
+  int64_t nparam = 0, nbuf = 0, ncnt = 0;
+  int nstreams = 0;
+  StreamIdx st[2];
+  bool has_sensor = false, has_cnn = false;
+  LstmIdx lstm;
+  CnnIdx cnn;
+  int fc_w = -1, fc_b = -1;
+  int K, V;
+
+  int add(const std::string& name, int kind, std::vector<int64_t> shape) {
+    Entry e;
+    e.name = name;
+    e.kind = kind;
+    e.shape = shape;
+    e.numel = 1;
+    for (auto d : shape) e.numel *= d;
+    int64_t* ctr = kind == F3_ENTRY_PARAM ? &nparam : (kind == F3_ENTRY_BUFFER ? &nbuf : &ncnt);
+    e.offset = *ctr;
+    *ctr += e.numel;
+    entries.push_back(e);
+    return (int)entries.size() - 1;
+  }
+  BnIdx add_bn(const std::string& p, int C) {
+    BnIdx b;
+    b.C = C;
+    b.w = add(p + ".weight", F3_ENTRY_PARAM, {C});
+    b.b = add(p + ".bias", F3_ENTRY_PARAM, {C});
+    b.rm = add(p + ".running_mean", F3_ENTRY_BUFFER, {C});
+    b.rv = add(p + ".running_var", F3_ENTRY_BUFFER, {C});
+    b.nbt = add(p + ".num_batches_tracked", F3_ENTRY_COUNTER, {});
+    return b;
+  }
+  void add_stream(StreamIdx& s, const std::string& pre, int cin, int motion, int num_class) {
+    const std::string layers = cfg.naming == F3_NAMING_NOTEBOOK ? "st_gcn_networks" : "st_gcan_networks";
+    s.cin = cin;
+    s.motion = motion;
+    s.T = motion ? cfg.frames - 1 : cfg.frames;
+    s.A = add(pre + "A", F3_ENTRY_BUFFER, {K, V, V});
+    s.dbn = add_bn(pre + "data_bn", cin * V);
+    int T = s.T;
+    for (int i = 0; i < 7; ++i) {
+      LayerIdx& L = s.L[i];
+      L.cin = kChan[i][0] < 0 ? cin : kChan[i][0];
+      L.cout = kChan[i][1];
+      L.stride = kChan[i][2];
+      L.res = kChan[i][3];
+      L.T_in = T;
+      L.T_out = (T - 1) / L.stride + 1;  // (T + 2*4 - 9)/s + 1
+      T = L.T_out;
+      const int ci = L.cin, co = L.cout;
+      const std::string p = pre + layers + "." + std::to_string(i) + ".";
+      L.gcn_w = add(p + "gcn.conv.weight", F3_ENTRY_PARAM, {K * co, ci, 1, 1});
+      L.gcn_b = add(p + "gcn.conv.bias", F3_ENTRY_PARAM, {K * co});
+      L.bn1 = add_bn(p + "tcn.0", co);
+      L.tcn_w = add(p + "tcn.2.weight", F3_ENTRY_PARAM, {co, co, 9, 1});
+      L.tcn_b = add(p + "tcn.2.bias", F3_ENTRY_PARAM, {co});
+      L.bn2 = add_bn(p + "tcn.3", co);
+      if (L.res == RES_CONV) {
+        L.res_w = add(p + "residual.0.weight", F3_ENTRY_PARAM, {co, ci, 1, 1});
+        L.res_b = add(p + "residual.0.bias", F3_ENTRY_PARAM, {co});
+        L.bnr = add_bn(p + "residual.1", co);
+      }
+      const std::string q = p + "channel_attention_module.atten.";
+      L.ca_w1 = add(q + "1.weight", F3_ENTRY_PARAM, {co / 4, co, 1, 1});
+      L.ca_b1 = add(q + "1.bias", F3_ENTRY_PARAM, {co / 4});
+      L.bnca = add_bn(q + "2", co / 4);
+      L.ca_w2 = add(q + "4.weight", F3_ENTRY_PARAM, {co, co / 4, 1, 1});
+      L.ca_b2 = add(q + "4.bias", F3_ENTRY_PARAM, {co});
+    }
+    for (int i = 0; i < 7; ++i) s.L[i].edge = add(pre + "edge_importance." + std::to_string(i), F3_ENTRY_PARAM, {K, V, V});
+    if (num_class > 0) {
+      s.cls_w = add(pre + "cls.weight", F3_ENTRY_PARAM, {num_class, 256, 1, 1});
+      s.cls_b = add(pre + "cls.bias", F3_ENTRY_PARAM, {num_class});
+    }
+  }
+  void add_bilstm(const std::string& p, int S, int C) {
+    const int H = 64;
+    lstm.S = S;
+    lstm.Cs = C;
+    const char* sfx[2] = {"", "_reverse"};
+    for (int d = 0; d < 2; ++d) {
+      lstm.wih[d] = add(p + "lstm1.weight_ih_l0" + sfx[d], F3_ENTRY_PARAM, {4 * H, S});
+      lstm.whh[d] = add(p + "lstm1.weight_hh_l0" + sfx[d], F3_ENTRY_PARAM, {4 * H, H});
+      lstm.bih[d] = add(p + "lstm1.bias_ih_l0" + sfx[d], F3_ENTRY_PARAM, {4 * H});
+      lstm.bhh[d] = add(p + "lstm1.bias_hh_l0" + sfx[d], F3_ENTRY_PARAM, {4 * H});
+    }
+    lstm.bn = add_bn(p + "batchnorm", 2 * H);
+    lstm.ca_w1 = add(p + "channelattention.attention.0.weight", F3_ENTRY_PARAM, {2 * H / 8, 2 * H});
+    lstm.ca_b1 = add(p + "channelattention.attention.0.bias", F3_ENTRY_PARAM, {2 * H / 8});
+    lstm.ca_w2 = add(p + "channelattention.attention.2.weight", F3_ENTRY_PARAM, {2 * H, 2 * H / 8});
+    lstm.ca_b2 = add(p + "channelattention.attention.2.bias", F3_ENTRY_PARAM, {2 * H});
+    lstm.fc_w = add(p + "fc.1.weight", F3_ENTRY_PARAM, {C, 2 * H});
+    lstm.fc_b = add(p + "fc.1.bias", F3_ENTRY_PARAM, {C});
+  }
+  void add_cnn(const std::string& p, int S, int T) {
+    cnn.w1 = add(p + "layer1.0.weight", F3_ENTRY_PARAM, {16, S, 5});
+    cnn.b1 = add(p + "layer1.0.bias", F3_ENTRY_PARAM, {16});
+    cnn.bn1 = add_bn(p + "layer1.1", 16);
+    cnn.w2 = add(p + "layer2.0.weight", F3_ENTRY_PARAM, {32, 16, 5});
+    cnn.b2 = add(p + "layer2.0.bias", F3_ENTRY_PARAM, {32});
+    cnn.bn2 = add_bn(p + "layer2.1", 32);
+    cnn.fcw = add(p + "fc.weight", F3_ENTRY_PARAM, {32, 32 * ((T / 2) / 2)});  // unused in forward
+    cnn.fcb = add(p + "fc.bias", F3_ENTRY_PARAM, {32});
+  }
+};
+
+namespace {
+
+struct Arena {
+  char* base;
+  size_t off = 0;
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+struct BnWs {
+  double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
+};
+
+struct LayerWs {
+  const float* x = nullptr;  // block input (previous block output or data_bn output)
+  float *z, *g, *h, *r = nullptr, *out, *q1, *hid, *att, *gap;
+  float *gw, *gwT, *tw, *twT, *rw = nullptr, *rwT = nullptr, *aeff, *beff;
+  BnWs bn1, bn2, bnr, bnca;
+  float *P1, *P2, *G, *dAeff, *dq2, *dbn, *dq1, *e;
+};
+
+struct StreamWs {
+  float *x0, *pool, *A;  // A: copy of the adjacency buffer (backward has no buffer pointer)
+  BnWs dbn;
+  LayerWs L[7];
+  float *dh, *dres, *dv, *dg, *dZ, *dx[2], *dpool;
+};
+
+struct Ws {
+  StreamWs st[2];
+  // sensor
+  float *y1, *p1, *y2, *p2, *dy1, *dp1, *dy2, *dp2;
+  BnWs cbn1, cbn2, sbn;
+  float *seq, *gates, *cell, *hmean, *ybn, *a1, *satt, *sout, *sdy, *sdpre2, *sdpre1, *dhmean;
+  // head
+  float *out, *dlogits, *ds;
+  float *skel, *sensor;  // copies of the step's inputs (backward re-reads them)
+  char *zf0, *zf1, *zb0, *zb1;
+  size_t bytes;
+};
+
+void bn_take(Arena& A, BnWs& b, int C) {
+  b.fsum = A.take<double>(C);
+  b.fsq = A.take<double>(C);
+}
+void bn_take_b(Arena& A, BnWs& b, int C) {
+  b.bsum = A.take<double>(C);
+  b.bsq = A.take<double>(C);
+}
+
+Ws plan(const f3_net& net, int N, char* base) {
+  Ws w;
+  std::memset(&w, 0, sizeof(w));
+  Arena A{base};
+  const int K = net.K, V = net.V;
+  const bool cnn = net.has_cnn;
+  const int Ts = net.cfg.sensor_frames;
+  const int Tl = cnn ? (Ts / 2) / 2 : Ts;
+  // ---- zero-at-forward region ----
+  w.zf0 = A.take<char>(0);
+  for (int si = 0; si < net.nstreams; ++si) {
+    const StreamIdx& S = net.st[si];
+    StreamWs& W = w.st[si];
+    bn_take(A, W.dbn, S.cin * V);
+    W.pool = A.take<float>((size_t)N * 256);
+    for (int l = 0; l < 7; ++l) {
+      const LayerIdx& L = S.L[l];
+      LayerWs& X = W.L[l];
+      bn_take(A, X.bn1, L.cout);
+      bn_take(A, X.bn2, L.cout);
+      if (L.res == RES_CONV) bn_take(A, X.bnr, L.cout);
+      bn_take(A, X.bnca, L.cout / 4);
+      X.gap = A.take<float>((size_t)N * L.cout);
+    }
+  }
+  if (net.has_sensor) {
+    if (cnn) {
+      bn_take(A, w.cbn1, 16);
+      bn_take(A, w.cbn2, 32);
+    }
+    bn_take(A, w.sbn, 128);
+  }
+  w.zf1 = A.take<char>(0);
+  // ---- zero-at-backward region ----
+  w.zb0 = A.take<char>(0);
+  for (int si = 0; si < net.nstreams; ++si) {
+    const StreamIdx& S = net.st[si];
+    StreamWs& W = w.st[si];
+    for (int l = 0; l < 7; ++l) {
+      const LayerIdx& L = S.L[l];
+      LayerWs& X = W.L[l];
+      bn_take_b(A, X.bn1, L.cout);
+      bn_take_b(A, X.bn2, L.cout);
+      if (L.res == RES_CONV) bn_take_b(A, X.bnr, L.cout);
+      X.P1 = A.take<float>((size_t)N * L.cout);
+      X.P2 = A.take<float>((size_t)N * L.cout);
+      X.G = A.take<float>((size_t)V * L.cout);
+      X.dAeff = A.take<float>((size_t)K * V * V);
+    }
+  }
+  if (net.has_sensor && cnn) {
+    bn_take_b(A, w.cbn1, 16);
+    bn_take_b(A, w.cbn2, 32);
+    w.dp2 = A.take<float>((size_t)N * Tl * 32);
+  }
+  w.zb1 = A.take<char>(0);
+  // ---- saved activations, packed weights, scratch ----
+  for (int si = 0; si < net.nstreams; ++si) {
+    const StreamIdx& S = net.st[si];
+    StreamWs& W = w.st[si];
+    W.x0 = A.take<float>((size_t)N * S.T * V * S.cin);
+    W.A = A.take<float>((size_t)K * V * V);
+    size_t maxMC = 0, maxZ = 0;
+    const float* xin = W.x0;
+    for (int l = 0; l < 7; ++l) {
+      const LayerIdx& L = S.L[l];
+      LayerWs& X = W.L[l];
+      const size_t Mi = (size_t)N * L.T_in * V, Mo = (size_t)N * L.T_out * V;
+      const int C = L.cout, Ci = L.cin;
+      X.x = xin;
+      X.z = A.take<float>(Mi * K * Ci);
+      X.g = A.take<float>(Mi * C);
+      X.h = A.take<float>(Mo * C);
+      if (L.res == RES_CONV) X.r = A.take<float>(Mo * C);
+      X.out = A.take<float>(Mo * C);
+      X.q1 = A.take<float>((size_t)N * C / 4);
+      X.hid = A.take<float>((size_t)N * C / 4);
+      X.att = A.take<float>((size_t)N * C);
+      X.gw = A.take<float>((size_t)C * K * Ci);
+      X.gwT = A.take<float>((size_t)C * K * Ci);
+      X.tw = A.take<float>((size_t)C * 9 * C);
+      X.twT = A.take<float>((size_t)C * 9 * C);
+      if (L.res == RES_CONV) {
+        X.rw = A.take<float>((size_t)C * Ci);
+        X.rwT = A.take<float>((size_t)C * Ci);
+      }
+      X.aeff = A.take<float>((size_t)K * V * V);
+      X.beff = A.take<float>((size_t)V * C);
+      X.dq2 = A.take<float>((size_t)N * C);
+      X.dbn = A.take<float>((size_t)N * C / 4);
+      X.dq1 = A.take<float>((size_t)N * C / 4);
+      X.e = A.take<float>((size_t)N * C);
+      xin = X.out;
+      maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
+      maxMC = std::max(maxMC, Mo * C);
+      maxZ = std::max(maxZ, Mi * K * Ci);
+    }
+    W.dh = A.take<float>(maxMC);
+    W.dres = A.take<float>(maxMC);
+    W.dv = A.take<float>(maxMC);
+    W.dg = A.take<float>(maxMC);
+    W.dZ = A.take<float>(maxZ);
+    W.dx[0] = A.take<float>(maxMC);
+    W.dx[1] = A.take<float>(maxMC);
+    W.dpool = A.take<float>((size_t)N * 256);
+  }
+  if (net.has_sensor) {
+    if (cnn) {
+      w.y1 = A.take<float>((size_t)N * Ts * 16);
+      w.p1 = A.take<float>((size_t)N * (Ts / 2) * 16);
+      w.y2 = A.take<float>((size_t)N * (Ts / 2) * 32);
+      w.p2 = A.take<float>((size_t)N * Tl * 32);
+      w.dy1 = A.take<float>((size_t)N * Ts * 16);
+      w.dp1 = A.take<float>((size_t)N * (Ts / 2) * 16);
+      w.dy2 = A.take<float>((size_t)N * (Ts / 2) * 32);
+    }
+    w.seq = A.take<float>((size_t)N * Tl * 128);
+    w.gates = A.take<float>((size_t)2 * N * Tl * 256);
+    w.cell = A.take<float>((size_t)2 * N * Tl * 64);
+    w.hmean = A.take<float>((size_t)N * 128);
+    w.ybn = A.take<float>((size_t)N * 128);
+    w.a1 = A.take<float>((size_t)N * 16);
+    w.satt = A.take<float>((size_t)N * 128);
+    w.sout = A.take<float>((size_t)N * net.lstm.Cs);
+    w.sdy = A.take<float>((size_t)N * 128);
+    w.sdpre2 = A.take<float>((size_t)N * 128);
+    w.sdpre1 = A.take<float>((size_t)N * 16);
+    w.dhmean = A.take<float>((size_t)N * 128);
+    w.ds = A.take<float>((size_t)N * net.lstm.Cs);
+  }
+  if (net.nstreams) w.skel = A.take<float>((size_t)N * 3 * net.cfg.frames * V);
+  if (net.has_sensor) w.sensor = A.take<float>((size_t)N * Ts * net.cfg.sensor_dim);
+  w.out = A.take<float>((size_t)N * net.cfg.num_class);
+  w.dlogits = A.take<float>((size_t)N * net.cfg.num_class);
+  w.bytes = (A.off + 255) & ~(size_t)255;
+  return w;
+}
+
+struct Ptrs {
+  const f3_net& net;
+  const float* P;
+  float* B;
+  int64_t* C;
+  float* G;
+  const float* p(int i) const { return P + net.entries[i].offset; }
+  float* g(int i) const { return G + net.entries[i].offset; }
+  float* b(int i) const { return B + net.entries[i].offset; }
+  long long* c(int i) const { return reinterpret_cast<long long*>(C + net.entries[i].offset); }
+  BnRef ref(const BnIdx& bi, const BnWs& w, float count, int eval) const {
+    BnRef r;
+    r.sum = w.fsum;
+    r.sumsq = w.fsq;
+    r.gamma = p(bi.w);
+    r.beta = p(bi.b);
+    r.rmean = B ? b(bi.rm) : nullptr;
+    r.rvar = B ? b(bi.rv) : nullptr;
+    r.count = count;
+    r.eval = eval;
+    return r;
+  }
+};
+
+#define F3_TRY(x)              \
+  do {                         \
+    int _s = (x);              \
+    if (_s != F3_OK) return _s; \
+  } while (0)
+
+ConvGeom geom(int M, int Nc, int Kc, int KT, int S, int P, int tr, int T_out, int T_in, int V, int lda, int ldo) {
+  ConvGeom g;
+  g.M = M; g.Nc = Nc; g.Kc = Kc; g.KT = KT; g.S = S; g.P = P; g.transposed = tr;
+  g.T_out = T_out; g.T_in = T_in; g.V = V; g.lda = lda; g.ldo = ldo;
+  return g;
+}
+
+void add_job(PrepTable& t, int type, int n, float* dst, const float* s0, const float* s1, const float* s2, int d0,
+             int d1, int d2) {
+  PrepJob& j = t.jobs[t.n++];
+  j.type = type; j.n = n; j.dst = dst; j.s0 = s0; j.s1 = s1; j.s2 = s2; j.d0 = d0; j.d1 = d1; j.d2 = d2;
+}
+
+void add_bnrun(BnRunTable& t, const Ptrs& q, const BnIdx& bi, const double* sum, const double* sq, double count) {
+  BnRunJob& j = t.jobs[t.n++];
+  j.sum = sum; j.sumsq = sq; j.count = count; j.C = bi.C;
+  j.rmean = q.b(bi.rm); j.rvar = q.b(bi.rv); j.nbt = q.c(bi.nbt);
+}
+
+int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, Ws& w, const float* skel,
+                   BnRunTable& run, hipStream_t s) {
+  const StreamIdx& S = net.st[si];
+  StreamWs& W = w.st[si];
+  const int K = net.K, V = net.V, eval = !train;
+  // weights: A_eff, gcn bias through the graph, packed GEMM operands
+  PrepTable pt;
+  pt.n = 0;
+  add_job(pt, PREP_COPY, K * V * V, W.A, q.b(S.A), nullptr, nullptr, 0, 0, 0);
+  for (int l = 0; l < 7; ++l) {
+    const LayerIdx& L = S.L[l];
+    LayerWs& X = W.L[l];
+    const int C = L.cout, Ci = L.cin;
+    add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
+    add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
+    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K);
+    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9);
+    if (train) {
+      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K);
+      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9);
+    }
+    if (L.res == RES_CONV) {
+      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1);
+      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1);
+    }
+  }
+  F3_TRY(f3_prep(pt, s));
+  // data_bn
+  DataBnArgs d;
+  std::memset(&d, 0, sizeof(d));
+  d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel; d.out = W.x0;
+  d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), eval);
+  d.st_sum = W.dbn.fsum; d.st_sq = W.dbn.fsq;
+  F3_TRY(f3_databn_fwd(&d, s));
+  if (train) add_bnrun(run, q, S.dbn, W.dbn.fsum, W.dbn.fsq, (double)N * S.T);
+  for (int l = 0; l < 7; ++l) {
+    const LayerIdx& L = S.L[l];
+    LayerWs& X = W.L[l];
+    const int C = L.cout, Ci = L.cin, Ti = L.T_in, To = L.T_out;
+    const int Mi = N * Ti * V, Mo = N * To * V;
+    const BnRef bn1 = q.ref(L.bn1, X.bn1, (float)Mi, eval);
+    const BnRef bn2 = q.ref(L.bn2, X.bn2, (float)Mo, eval);
+    BnRef bnr;
+    std::memset(&bnr, 0, sizeof(bnr));
+    if (L.res == RES_CONV) bnr = q.ref(L.bnr, X.bnr, (float)Mo, eval);
+    // graph mix then 1x1 conv (stgcan.py:50-56)
+    MixArgs mx;
+    std::memset(&mx, 0, sizeof(mx));
+    mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
+    F3_TRY(f3_mix_fwd(&mx, s));
+    ConvGemmArgs ga;
+    std::memset(&ga, 0, sizeof(ga));
+    ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
+    ga.in = X.z; ga.w = X.gw; ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+    F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
+    if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
+      ConvGemmArgs ra;
+      std::memset(&ra, 0, sizeof(ra));
+      ra.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
+      ra.in = X.x; ra.w = X.rw; ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
+      F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
+    }
+    // tcn: BN1 + ReLU prologue, (9,1) conv, bias, BN2 stats + channel-attention pool epilogue
+    ConvGemmArgs ta;
+    std::memset(&ta, 0, sizeof(ta));
+    ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
+    ta.in = X.g; ta.w = X.tw; ta.out = X.h; ta.pro_bn = bn1; ta.bias = q.p(L.tcn_b);
+    ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
+    F3_TRY(f3_conv_gemm(&ta, 1, EPI_BIAS | EPI_STATS | EPI_GAP, s));
+    // channel attention (stgcan.py:59-74)
+    CaArgs ca;
+    std::memset(&ca, 0, sizeof(ca));
+    ca.N = N; ca.C = C; ca.inv_tv = 1.f / (float)(To * V); ca.bn2 = bn2;
+    ca.bnca = q.ref(L.bnca, X.bnca, (float)N, eval);
+    ca.W1 = q.p(L.ca_w1); ca.b1 = q.p(L.ca_b1); ca.W2 = q.p(L.ca_w2); ca.b2 = q.p(L.ca_b2);
+    ca.gapsum = X.gap; ca.q1 = X.q1; ca.hid = X.hid; ca.att = X.att; ca.ca_sum = X.bnca.fsum; ca.ca_sq = X.bnca.fsq;
+    F3_TRY(f3_ca_fwd(&ca, s));
+    // residual add + ReLU (stgcan.py:143-144), pooled mean after the last block (stgcan.py:224)
+    BlockArgs ba;
+    std::memset(&ba, 0, sizeof(ba));
+    ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
+    ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
+    ba.pool = l == 6 ? W.pool : nullptr;
+    F3_TRY(f3_block_out(ba, s));
+    if (train) {
+      add_bnrun(run, q, L.bn1, X.bn1.fsum, X.bn1.fsq, Mi);
+      add_bnrun(run, q, L.bn2, X.bn2.fsum, X.bn2.fsq, Mo);
+      if (L.res == RES_CONV) add_bnrun(run, q, L.bnr, X.bnr.fsum, X.bnr.fsq, Mo);
+      add_bnrun(run, q, L.bnca, X.bnca.fsum, X.bnca.fsq, N);
+    }
+  }
+  return F3_OK;
+}
+
+// debugging aid: F3_DEBUG_BWD_STOP="stream,layer" ends the backward right after that
+// layer's tcn input-gradient so its scratch tensors can be inspected (tools/diag_layer.py)
+bool debug_stop(int si, int l) {
+  static const char* e = getenv("F3_DEBUG_BWD_STOP");
+  if (!e) return false;
+  int a = -1, b = -1;
+  sscanf(e, "%d,%d", &a, &b);
+  return a == si && b == l;
+}
+
+int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s) {
+  const StreamIdx& S = net.st[si];
+  StreamWs& W = w.st[si];
+  const int K = net.K, V = net.V;
+  const float* dout = nullptr;
+  int pp = 0;
+  for (int l = 6; l >= 0; --l) {
+    const LayerIdx& L = S.L[l];
+    LayerWs& X = W.L[l];
+    const int C = L.cout, Ci = L.cin, Ti = L.T_in, To = L.T_out;
+    const int Mi = N * Ti * V, Mo = N * To * V;
+    float* dx = W.dx[pp];
+    const BnRef bn1 = q.ref(L.bn1, X.bn1, (float)Mi, 0);
+    const BnRef bn2 = q.ref(L.bn2, X.bn2, (float)Mo, 0);
+    BnRef bnr;
+    std::memset(&bnr, 0, sizeof(bnr));
+    if (L.res == RES_CONV) bnr = q.ref(L.bnr, X.bnr, (float)Mo, 0);
+    BlockArgs ba;
+    std::memset(&ba, 0, sizeof(ba));
+    ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
+    ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
+    ba.dout = dout; ba.dout_nc = l == 6 ? W.dpool : nullptr;
+    ba.P1 = X.P1; ba.P2 = X.P2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
+    ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = W.dh;
+    ba.dres = L.res == RES_CONV ? W.dres : (L.res == RES_ID ? dx : nullptr);
+    ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
+    if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
+    F3_TRY(f3_block_bwd_reduce(ba, s));
+    CaArgs ca;
+    std::memset(&ca, 0, sizeof(ca));
+    ca.N = N; ca.C = C; ca.inv_tv = 1.f / (float)(To * V); ca.bn2 = bn2;
+    ca.bnca = q.ref(L.bnca, X.bnca, (float)N, 0);
+    ca.W1 = q.p(L.ca_w1); ca.b1 = q.p(L.ca_b1); ca.W2 = q.p(L.ca_w2); ca.b2 = q.p(L.ca_b2);
+    ca.gapsum = X.gap; ca.q1 = X.q1; ca.hid = X.hid; ca.att = X.att; ca.ca_sum = X.bnca.fsum; ca.ca_sq = X.bnca.fsq;
+    ca.P1 = X.P1; ca.P2 = X.P2; ca.dq2 = X.dq2; ca.dbn = X.dbn; ca.dq1 = X.dq1; ca.e = X.e;
+    ca.bn2_bsum = X.bn2.bsum; ca.bn2_bsq = X.bn2.bsq;
+    ca.g_bnca_gamma = q.g(L.bnca.w); ca.g_bnca_beta = q.g(L.bnca.b);
+    ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
+    F3_TRY(f3_ca_bwd(&ca, s));
+    F3_TRY(f3_block_bwd_apply(ba, s));
+    // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
+    ConvGemmArgs td;
+    std::memset(&td, 0, sizeof(td));
+    td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
+    td.in = W.dh; td.w = X.twT; td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
+    F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
+    if (debug_stop(si, l)) return F3_OK;
+    WgradArgs tw;
+    std::memset(&tw, 0, sizeof(tw));
+    tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
+    tw.dy = W.dh; tw.ldy = C; tw.in = X.g; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
+    tw.outmap = WG_OUT_CONV; tw.pro_bn = bn1;
+    F3_TRY(f3_conv_wgrad(&tw, 1, s));
+    BnBwdArgs bb;
+    std::memset(&bb, 0, sizeof(bb));
+    bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
+    bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = W.dg; bb.G = X.G;
+    F3_TRY(f3_bn_bwd_apply(bb, s));
+    // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
+    ConvGemmArgs gd;
+    std::memset(&gd, 0, sizeof(gd));
+    gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
+    gd.in = W.dg; gd.w = X.gwT; gd.out = W.dZ;
+    F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
+    WgradArgs gw;
+    std::memset(&gw, 0, sizeof(gw));
+    gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
+    gw.dy = W.dg; gw.ldy = C; gw.in = X.z; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
+    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci;
+    F3_TRY(f3_conv_wgrad(&gw, 0, s));
+    MixArgs mx;
+    std::memset(&mx, 0, sizeof(mx));
+    mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
+    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID;
+    F3_TRY(f3_mix_bwd(&mx, s));
+    GcnBiasBwdArgs gb;
+    gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
+    gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
+    F3_TRY(f3_gcn_bias_bwd(&gb, s));
+    if (L.res == RES_CONV) {
+      ConvGemmArgs rd;
+      std::memset(&rd, 0, sizeof(rd));
+      rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
+      rd.in = W.dres; rd.w = X.rwT; rd.out = dx;
+      F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
+      WgradArgs rw;
+      std::memset(&rw, 0, sizeof(rw));
+      rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
+      rw.dy = W.dres; rw.ldy = C; rw.in = X.x; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV;
+      F3_TRY(f3_conv_wgrad(&rw, 0, s));
+    }
+    dout = dx;
+    pp ^= 1;
+  }
+  DataBnArgs d;
+  std::memset(&d, 0, sizeof(d));
+  d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
+  d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), 0);
+  d.dout = dout; d.dgamma = q.g(S.dbn.w); d.dbeta = q.g(S.dbn.b);
+  F3_TRY(f3_databn_bwd(&d, s));
+  return F3_OK;
+}
+
+void sensor_args(const f3_net& net, int N, int train, const Ptrs& q, Ws& w, const float* sensor, LstmArgs& la,
+                 SHeadArgs& sa, Conv1dArgs& c1, Conv1dArgs& c2) {
+  const int Ts = net.cfg.sensor_frames;
+  const int eval = !train;
+  std::memset(&la, 0, sizeof(la));
+  std::memset(&sa, 0, sizeof(sa));
+  std::memset(&c1, 0, sizeof(c1));
+  std::memset(&c2, 0, sizeof(c2));
+  if (net.has_cnn) {
+    c1.N = N; c1.T = Ts; c1.Ci = net.cfg.sensor_dim; c1.Co = 16; c1.x = sensor; c1.w = q.p(net.cnn.w1);
+    c1.b = q.p(net.cnn.b1); c1.y = w.y1; c1.st_sum = w.cbn1.fsum; c1.st_sq = w.cbn1.fsq;
+    c1.bn = q.ref(net.cnn.bn1, w.cbn1, (float)(N * Ts), eval); c1.p = w.p1;
+    c1.dp = w.dp1; c1.dy = w.dy1; c1.bsum = w.cbn1.bsum; c1.bsq = w.cbn1.bsq;
+    c1.g_gamma = q.G ? q.g(net.cnn.bn1.w) : nullptr; c1.g_beta = q.G ? q.g(net.cnn.bn1.b) : nullptr;
+    c1.g_b = q.G ? q.g(net.cnn.b1) : nullptr; c1.g_w = q.G ? q.g(net.cnn.w1) : nullptr; c1.dx = nullptr;
+    c2 = c1;
+    c2.T = Ts / 2; c2.Ci = 16; c2.Co = 32; c2.x = w.p1; c2.w = q.p(net.cnn.w2); c2.b = q.p(net.cnn.b2);
+    c2.y = w.y2; c2.st_sum = w.cbn2.fsum; c2.st_sq = w.cbn2.fsq;
+    c2.bn = q.ref(net.cnn.bn2, w.cbn2, (float)(N * (Ts / 2)), eval); c2.p = w.p2;
+    c2.dp = w.dp2; c2.dy = w.dy2; c2.bsum = w.cbn2.bsum; c2.bsq = w.cbn2.bsq;
+    c2.g_gamma = q.G ? q.g(net.cnn.bn2.w) : nullptr; c2.g_beta = q.G ? q.g(net.cnn.bn2.b) : nullptr;
+    c2.g_b = q.G ? q.g(net.cnn.b2) : nullptr; c2.g_w = q.G ? q.g(net.cnn.w2) : nullptr; c2.dx = w.dp1;
+  }
+  la.N = N;
+  la.T = net.has_cnn ? (Ts / 2) / 2 : Ts;
+  la.S = net.has_cnn ? 32 : net.lstm.S;
+  la.x = net.has_cnn ? w.p2 : sensor;
+  for (int d = 0; d < 2; ++d) {
+    la.w_ih[d] = q.p(net.lstm.wih[d]); la.w_hh[d] = q.p(net.lstm.whh[d]);
+    la.b_ih[d] = q.p(net.lstm.bih[d]); la.b_hh[d] = q.p(net.lstm.bhh[d]);
+    if (q.G) {
+      la.g_w_ih[d] = q.g(net.lstm.wih[d]); la.g_w_hh[d] = q.g(net.lstm.whh[d]);
+      la.g_b_ih[d] = q.g(net.lstm.bih[d]); la.g_b_hh[d] = q.g(net.lstm.bhh[d]);
+    }
+  }
+  la.seq = w.seq; la.gates = w.gates; la.cell = w.cell; la.hmean = w.hmean;
+  la.dhmean = w.dhmean; la.dx = net.has_cnn ? w.dp2 : nullptr;
+  sa.N = N; sa.Cs = net.lstm.Cs; sa.hmean = w.hmean;
+  sa.bn = q.ref(net.lstm.bn, w.sbn, (float)N, eval); sa.bn_sum = w.sbn.fsum; sa.bn_sq = w.sbn.fsq;
+  sa.W1 = q.p(net.lstm.ca_w1); sa.b1 = q.p(net.lstm.ca_b1); sa.W2 = q.p(net.lstm.ca_w2); sa.b2 = q.p(net.lstm.ca_b2);
+  sa.W3 = q.p(net.lstm.fc_w); sa.b3 = q.p(net.lstm.fc_b);
+  sa.ybn = w.ybn; sa.a1 = w.a1; sa.att = w.satt; sa.out = w.sout; sa.out_ld = net.lstm.Cs;
+  sa.dout = w.ds; sa.dout_ld = net.lstm.Cs; sa.dy = w.sdy; sa.dpre2 = w.sdpre2; sa.dpre1 = w.sdpre1;
+  sa.dhmean = w.dhmean;
+  if (q.G) {
+    sa.g_W1 = q.g(net.lstm.ca_w1); sa.g_b1 = q.g(net.lstm.ca_b1); sa.g_W2 = q.g(net.lstm.ca_w2);
+    sa.g_b2 = q.g(net.lstm.ca_b2); sa.g_W3 = q.g(net.lstm.fc_w); sa.g_b3 = q.g(net.lstm.fc_b);
+    sa.g_gamma = q.g(net.lstm.bn.w); sa.g_beta = q.g(net.lstm.bn.b);
+  }
+}
+
+void head_args(const f3_net& net, int N, const Ptrs& q, Ws& w, HeadArgs& h) {
+  std::memset(&h, 0, sizeof(h));
+  h.N = N;
+  h.C = net.cfg.num_class;
+  h.softmax_out = net.cfg.softmax_output;
+  h.out = w.out;
+  h.dlogits = w.dlogits;
+  const int m = net.cfg.model;
+  if (m == F3_MODEL_STGCN) {
+    h.nblk = 1;
+    h.feat[0] = w.st[0].pool; h.width[0] = 256; h.ld[0] = 256; h.dfeat[0] = w.st[0].dpool;
+    h.W = q.p(net.st[0].cls_w); h.b = q.p(net.st[0].cls_b);
+    if (q.G) { h.g_W = q.g(net.st[0].cls_w); h.g_b = q.g(net.st[0].cls_b); }
+  } else if (m == F3_MODEL_BILSTM) {
+    h.nblk = 0;
+  } else {
+    h.nblk = net.has_sensor ? 3 : 2;
+    for (int i = 0; i < 2; ++i) {
+      h.feat[i] = w.st[i].pool; h.width[i] = 256; h.ld[i] = 256; h.dfeat[i] = w.st[i].dpool;
+    }
+    if (net.has_sensor) {
+      h.feat[2] = w.sout; h.width[2] = net.lstm.Cs; h.ld[2] = net.lstm.Cs; h.dfeat[2] = w.ds;
+    }
+    h.W = q.p(net.fc_w); h.b = q.p(net.fc_b);
+    if (q.G) { h.g_W = q.g(net.fc_w); h.g_b = q.g(net.fc_b); }
+  }
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int f3_net_create(const f3_config* cfg, f3_net** out) {
+  if (!cfg || !out) return F3_EINVAL;
+  if (cfg->num_node < 2 || cfg->num_partition < 1 || cfg->num_class < 1 || cfg->num_class > 64) return F3_EINVAL;
+  if (cfg->frames < 2 || cfg->model < 0 || cfg->model > 3) return F3_EINVAL;
+  if (cfg->num_partition * cfg->num_node * cfg->num_node > 1024) return F3_EINVAL;
+  f3_net* n = new f3_net();
+  n->cfg = *cfg;
+  n->K = cfg->num_partition;
+  n->V = cfg->num_node;
+  const bool nb = cfg->naming == F3_NAMING_NOTEBOOK;
+  const std::string p1 = nb ? "pts_stream." : "stgcan_1.", p2 = nb ? "mot_stream." : "stgcan_2.";
+  const std::string ps = nb ? "sensor." : "lstm.", pf = nb ? "fcn." : "fc.";
+  const int Cs = cfg->sensor_classes > 0 ? cfg->sensor_classes : cfg->num_class;
+  switch (cfg->model) {
+    case F3_MODEL_STGCN:
+      n->nstreams = 1;
+      n->add_stream(n->st[0], "", cfg->in_channels, 0, cfg->num_class);
+      break;
+    case F3_MODEL_BILSTM:
+      n->has_sensor = true;
+      if (cfg->sensor_dim > 32) { delete n; return F3_EINVAL; }
+      n->add_bilstm("", cfg->sensor_dim, cfg->num_class);
+      break;
+    default: {
+      n->nstreams = 2;
+      n->add_stream(n->st[0], p1, 3, 0, 0);
+      n->add_stream(n->st[1], p2, 2, 1, 0);
+      const bool sens = cfg->model == F3_MODEL_TWO_STGCAN_BILSTM;
+      n->has_sensor = sens;
+      n->has_cnn = sens && cfg->sensor == F3_SENSOR_CNN_BILSTM;
+      if (sens && !n->has_cnn && cfg->sensor_dim > 32) { delete n; return F3_EINVAL; }
+      auto add_sensor = [&]() {
+        if (!sens) return;
+        if (n->has_cnn) {
+          n->add_cnn(ps + "cnn.", cfg->sensor_dim, cfg->sensor_frames);
+          n->add_bilstm(ps + "bilstm.", 32, Cs);
+        } else {
+          n->add_bilstm(ps, cfg->sensor_dim, Cs);
+        }
+      };
+      auto add_fc = [&]() {
+        n->fc_w = n->add(pf + "weight", F3_ENTRY_PARAM, {cfg->num_class, 512 + (sens ? Cs : 0)});
+        n->fc_b = n->add(pf + "bias", F3_ENTRY_PARAM, {cfg->num_class});
+      };
+      if (nb) { add_fc(); add_sensor(); } else { add_sensor(); add_fc(); }
+    }
+  }
+  *out = n;
+  return F3_OK;
+}
+
+void f3_net_destroy(f3_net* net) { delete net; }
+
+int f3_net_num_entries(const f3_net* net) { return net ? (int)net->entries.size() : 0; }
+
+int f3_net_entry(const f3_net* net, int i, const char** name, int* kind, int* ndim, int64_t* shape8, int64_t* offset) {
+  if (!net || i < 0 || i >= (int)net->entries.size()) return F3_EINVAL;
+  const Entry& e = net->entries[i];
+  if (name) *name = e.name.c_str();
+  if (kind) *kind = e.kind;
+  if (ndim) *ndim = (int)e.shape.size();
+  if (shape8) for (size_t d = 0; d < e.shape.size() && d < 8; ++d) shape8[d] = e.shape[d];
+  if (offset) *offset = e.offset;
+  return F3_OK;
+}
+
+int64_t f3_net_param_count(const f3_net* net) { return net ? net->nparam : 0; }
+int64_t f3_net_buffer_count(const f3_net* net) { return net ? net->nbuf : 0; }
+int64_t f3_net_counter_count(const f3_net* net) { return net ? net->ncnt : 0; }
+
+int64_t f3_net_workspace_bytes(const f3_net* net, int batch) {
+  if (!net || batch < 1) return 0;
+  return (int64_t)plan(*net, batch, nullptr).bytes;
+}
+
+int f3_net_forward(f3_net* net, int N, int training, const float* params, float* buffers, int64_t* counters,
+                   const float* skel, const float* sensor, float* out, void* workspace, void* stream) {
+  if (!net || !params || !buffers || !out || !workspace || N < 1) return F3_EINVAL;
+  if (training && N < 2) return F3_EBATCH;
+  hipStream_t s = (hipStream_t)stream;
+  Ws w = plan(*net, N, (char*)workspace);
+  Ptrs q{*net, params, buffers, counters, nullptr};
+  if (training && !counters) return F3_EINVAL;
+  if (hipMemsetAsync(w.zf0, 0, w.zf1 - w.zf0, s) != hipSuccess) return F3_EHIP;
+  if (net->nstreams) {
+    if (!skel) return F3_EINVAL;
+    if (hipMemcpyAsync(w.skel, skel, sizeof(float) * N * 3 * net->cfg.frames * net->V, hipMemcpyDeviceToDevice, s) !=
+        hipSuccess)
+      return F3_EHIP;
+  }
+  if (net->has_sensor) {
+    if (!sensor) return F3_EINVAL;
+    if (hipMemcpyAsync(w.sensor, sensor, sizeof(float) * N * net->cfg.sensor_frames * net->cfg.sensor_dim,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return F3_EHIP;
+  }
+  BnRunTable run;
+  run.n = 0;
+  for (int si = 0; si < net->nstreams; ++si) F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, s));
+  if (net->has_sensor) {
+    LstmArgs la;
+    SHeadArgs sa;
+    Conv1dArgs c1, c2;
+    sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
+    if (net->has_cnn) {
+      F3_TRY(f3_conv1d_fwd(&c1, s));
+      F3_TRY(f3_bnrelupool_fwd(&c1, s));
+      F3_TRY(f3_conv1d_fwd(&c2, s));
+      F3_TRY(f3_bnrelupool_fwd(&c2, s));
+      if (training) {
+        add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
+        add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
+      }
+    }
+    F3_TRY(f3_lstm_fwd(&la, s));
+    F3_TRY(f3_shead_fwd(&sa, s));
+    if (training) add_bnrun(run, q, net->lstm.bn, w.sbn.fsum, w.sbn.fsq, N);
+  }
+  HeadArgs h;
+  head_args(*net, N, q, w, h);
+  if (net->cfg.model == F3_MODEL_BILSTM) {
+    if (hipMemcpyAsync(w.out, w.sout, sizeof(float) * N * net->cfg.num_class, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return F3_EHIP;
+  } else {
+    F3_TRY(f3_head_fwd(&h, s));
+  }
+  if (hipMemcpyAsync(out, w.out, sizeof(float) * N * net->cfg.num_class, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return F3_EHIP;
+  if (training) F3_TRY(f3_bn_running(run, s));
+  return F3_OK;
+}
+
+int f3_net_loss(f3_net* net, int N, const float* out, const float* label, float* loss, float* dout, void* stream) {
+  if (!net || !out || !label || !loss || !dout) return F3_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(loss, 0, sizeof(float), s) != hipSuccess) return F3_EHIP;
+  HeadArgs h;
+  std::memset(&h, 0, sizeof(h));
+  h.N = N; h.C = net->cfg.num_class; h.out = const_cast<float*>(out); h.label = label; h.loss = loss; h.dout = dout;
+  return f3_ce(&h, s);
+}
+
+int f3_net_backward(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
+                    void* stream) {
+  if (!net || !params || !dout || !grads || !workspace || N < 2) return F3_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  Ws w = plan(*net, N, (char*)workspace);
+  Ptrs q{*net, params, nullptr, nullptr, grads};
+  if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
+  if (hipMemsetAsync(w.zb0, 0, w.zb1 - w.zb0, s) != hipSuccess) return F3_EHIP;
+  HeadArgs h;
+  head_args(*net, N, q, w, h);
+  h.g_out = dout;
+  LstmArgs la;
+  SHeadArgs sa;
+  Conv1dArgs c1, c2;
+  if (net->has_sensor) sensor_args(*net, N, 1, q, w, w.sensor, la, sa, c1, c2);
+  if (net->cfg.model == F3_MODEL_BILSTM) {
+    sa.dout = dout;
+    sa.dout_ld = net->cfg.num_class;
+  } else {
+    F3_TRY(f3_head_bwd(&h, s));
+  }
+  if (net->has_sensor) {
+    F3_TRY(f3_shead_bwd(&sa, s));
+    F3_TRY(f3_lstm_bwd(&la, s));
+    if (net->has_cnn) {
+      F3_TRY(f3_conv1d_bwd(&c2, s));
+      F3_TRY(f3_conv1d_bwd(&c1, s));
+    }
+  }
+  for (int si = 0; si < net->nstreams; ++si) {
+    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, s));
+    if (getenv("F3_DEBUG_BWD_STOP") && si == atoi(getenv("F3_DEBUG_BWD_STOP"))) break;
+  }
+  return F3_OK;
+}
+
+int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_t n, float lr, float alpha,
+                    float eps, float grad_scale, void* stream) {
+  if (!params || !square_avg || !grads) return F3_EINVAL;
+  return f3_rmsprop(params, square_avg, grads, n, lr, alpha, eps, grad_scale, (hipStream_t)stream);
+}
+
+int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
+                    int V, int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  PrepTable t;
+  t.n = 0;
+  add_job(t, PREP_PACK_CONV, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT);
+  F3_TRY(f3_prep(t, s));
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
+  a.in = x; a.w = wpack; a.out = out; a.bias = bias;
+  return f3_conv_gemm(&a, 0, EPI_BIAS, s);
+}
+
+int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
+                          int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  PrepTable t;
+  t.n = 0;
+  add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT);
+  F3_TRY(f3_prep(t, s));
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_in * V, Cin, Cout, KT, stride, pad, 1, T_in, T_out, V, Cout, Cin);
+  a.in = dy; a.w = wpack; a.out = dx;
+  return f3_conv_gemm(&a, 0, 0, s);
+}
+
+int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
+                            int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
+  if (db && hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
+  WgradArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
+  a.dy = dy; a.ldy = Cout; a.in = x; a.dw = dw; a.db = db; a.outmap = WG_OUT_CONV;
+  return f3_conv_wgrad(&a, 0, s);
+}
+
+// debug accessor (tests/tools only): device pointer of a named per-layer workspace tensor
+void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, int layer, const char* what) {
+  if (!net || stream < 0 || stream >= net->nstreams || layer < 0 || layer > 6) return nullptr;
+  Ws w = plan(*net, batch, (char*)workspace);
+  StreamWs& W = w.st[stream];
+  LayerWs& X = W.L[layer];
+  const std::string k(what);
+  if (k == "x") return (void*)X.x;
+  if (k == "z") return X.z;
+  if (k == "g") return X.g;
+  if (k == "h") return X.h;
+  if (k == "r") return X.r;
+  if (k == "out") return X.out;
+  if (k == "att") return X.att;
+  if (k == "dh") return W.dh;
+  if (k == "dv") return W.dv;
+  if (k == "dg") return W.dg;
+  if (k == "dZ") return W.dZ;
+  if (k == "dres") return W.dres;
+  if (k == "dx0") return W.dx[0];
+  if (k == "dx1") return W.dx[1];
+  if (k == "bn1_fsum") return X.bn1.fsum;
+  if (k == "bn1_fsq") return X.bn1.fsq;
+  if (k == "bn1_bsum") return X.bn1.bsum;
+  if (k == "bn1_bsq") return X.bn1.bsq;
+  if (k == "twT") return X.twT;
+  if (k == "P1") return X.P1;
+  if (k == "P2") return X.P2;
+  if (k == "e") return X.e;
+  if (k == "gap") return X.gap;
+  if (k == "q1") return X.q1;
+  if (k == "hid") return X.hid;
+  if (k == "dq1") return X.dq1;
+  if (k == "dq2") return X.dq2;
+  if (k == "dbn") return X.dbn;
+  if (k == "bn2_fsum") return X.bn2.fsum;
+  if (k == "bn2_fsq") return X.bn2.fsq;
+  if (k == "bn2_bsum") return X.bn2.bsum;
+  if (k == "bn2_bsq") return X.bn2.bsq;
+  if (k == "ca_fsum") return X.bnca.fsum;
+  if (k == "ca_fsq") return X.bnca.fsq;
+  if (k == "dpool") return W.dpool;
+  if (k == "pool") return W.pool;
+  return nullptr;
+}
+
+const char* f3_status_string(int st) {
+  switch (st) {
+    case F3_OK: return "ok";
+    case F3_EINVAL: return "invalid argument or unsupported shape";
+    case F3_EBATCH: return "Expected more than 1 value per channel when training";
+    case F3_EHIP: return "HIP launch error";
+    case F3_ESTATE: return "backward without a training forward";
+    default: return "unknown status";
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,516 @@
+// IMU branch: (optional CNN1D front end) -> bidirectional LSTM -> mean over time ->
+// BatchNorm1d -> channel attention MLP -> Linear.
+//   BiLSTM            Multimodal_Fall3/model/bilstm.py:21-59 (nn.LSTM gate order i,f,g,o)
+//   ChannelAttention  Multimodal_Fall3/model/bilstm.py:5-19
+//   CNN1D             GSTCAN_UR_conv.ipynb cell 2 (:493-514)
+//
+// The recurrence is latency-bound (30 dependent steps): one persistent workgroup per
+// (direction, group of LSTM_NB clips) keeps its gate rows of W_ih / W_hh in registers
+// (thread g owns gate row g of 4H = 256) and walks all timesteps inside the kernel; the
+// backward kernel runs BPTT in the same layout with W_hh staged in LDS for dh.
+#include "common.h"
+#include "sensor.h"
+
+namespace f3 {
+
+constexpr int H = 64, G4 = 256;
+
+// ----------------------------------------------------------------------------
+// LSTM forward: x [N][T][S] -> seq [N][T][2H] (saved h), gates [2][N][T][4H]
+// (post-activation), cell [2][N][T][H], hmean [N][2H]
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int dir = blockIdx.y, n0 = blockIdx.x * LSTM_NB, S = a.S, T = a.T;
+  float* xs = sm;                        // [NB][T][S]
+  float* hs = xs + LSTM_NB * T * S;      // [NB][H]
+  float* gs = hs + LSTM_NB * H;          // [NB][4H]
+  const int tid = threadIdx.x;
+  const float* wih = a.w_ih[dir];
+  const float* whh = a.w_hh[dir];
+  float wi[32], wh[H];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) wi[s] = s < S ? wih[tid * S + s] : 0.f;
+#pragma unroll
+  for (int u = 0; u < H; ++u) wh[u] = whh[tid * H + u];
+  const float bias = a.b_ih[dir][tid] + a.b_hh[dir][tid];
+  for (int i = tid; i < LSTM_NB * T * S; i += 256) {
+    const int b = i / (T * S), r = i - b * T * S;
+    xs[i] = (n0 + b < a.N) ? a.x[(size_t)(n0 + b) * T * S + r] : 0.f;
+  }
+  for (int i = tid; i < LSTM_NB * H; i += 256) hs[i] = 0.f;
+  const int cb = tid / H, cu = tid % H;  // cell-update ownership (LSTM_NB*H == 256)
+  float c = 0.f, hsum = 0.f;
+  const bool valid = n0 + cb < a.N;
+  __syncthreads();
+  for (int step = 0; step < T; ++step) {
+    const int t = dir ? T - 1 - step : step;
+#pragma unroll
+    for (int b = 0; b < LSTM_NB; ++b) {
+      float acc = bias;
+      const float* xr = xs + (b * T + t) * S;
+#pragma unroll
+      for (int s = 0; s < 32; ++s)
+        if (s < S) acc += wi[s] * xr[s];
+      const float* hr = hs + b * H;
+#pragma unroll
+      for (int u = 0; u < H; ++u) acc += wh[u] * hr[u];
+      const int gate = tid / H;  // 0 i, 1 f, 2 g, 3 o
+      gs[b * G4 + tid] = gate == 2 ? tanhf(acc) : sigmoidf_(acc);
+    }
+    __syncthreads();
+    const float gi = gs[cb * G4 + cu], gf = gs[cb * G4 + H + cu];
+    const float gg = gs[cb * G4 + 2 * H + cu], go = gs[cb * G4 + 3 * H + cu];
+    c = gf * c + gi * gg;
+    const float h = go * tanhf(c);
+    hs[cb * H + cu] = h;
+    hsum += h;
+    if (valid) {
+      const size_t nt = (size_t)(n0 + cb) * T + t;
+      a.seq[nt * 2 * H + dir * H + cu] = h;
+      a.cell[((size_t)dir * a.N * T + nt) * H + cu] = c;
+      float* gsv = a.gates + ((size_t)dir * a.N * T + nt) * G4;
+      gsv[cu] = gi; gsv[H + cu] = gf; gsv[2 * H + cu] = gg; gsv[3 * H + cu] = go;
+    }
+    __syncthreads();
+  }
+  if (valid) a.hmean[(size_t)(n0 + cb) * 2 * H + dir * H + cu] = hsum / (float)T;
+}
+
+// ----------------------------------------------------------------------------
+// LSTM backward (BPTT). dhmean [N][2H] -> weight grads (+= via atomics), dx (+=)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int dir = blockIdx.y, n0 = blockIdx.x * LSTM_NB, S = a.S, T = a.T;
+  float* whs = sm;                        // [4H][H+1]
+  float* wis = whs + G4 * (H + 1);        // [4H][S]
+  float* xs = wis + G4 * S;               // [NB][T][S]
+  float* hp = xs + LSTM_NB * T * S;       // [NB][H] h_{prev}
+  float* dgs = hp + LSTM_NB * H;          // [NB][4H]
+  float* dhr = dgs + LSTM_NB * G4;        // [NB][H] recurrent dh
+  const int tid = threadIdx.x;
+  for (int i = tid; i < G4 * H; i += 256) whs[(i / H) * (H + 1) + (i % H)] = a.w_hh[dir][i];
+  for (int i = tid; i < G4 * S; i += 256) wis[i] = a.w_ih[dir][i];
+  for (int i = tid; i < LSTM_NB * T * S; i += 256) {
+    const int b = i / (T * S), r = i - b * T * S;
+    xs[i] = (n0 + b < a.N) ? a.x[(size_t)(n0 + b) * T * S + r] : 0.f;
+  }
+  for (int i = tid; i < LSTM_NB * H; i += 256) dhr[i] = 0.f;
+  const int cb = tid / H, cu = tid % H;
+  const bool valid = n0 + cb < a.N;
+  const float dmean = valid ? a.dhmean[(size_t)(n0 + cb) * 2 * H + dir * H + cu] / (float)T : 0.f;
+  float dc = 0.f;
+  float gwh[H], gwi[32], gb = 0.f;
+#pragma unroll
+  for (int u = 0; u < H; ++u) gwh[u] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 32; ++s) gwi[s] = 0.f;
+  __syncthreads();
+  for (int step = T - 1; step >= 0; --step) {
+    const int t = dir ? T - 1 - step : step;           // time of this processing step
+    const int tp = dir ? t + 1 : t - 1;                // time of the previous step's state
+    const bool has_prev = step > 0;
+    // (b, u): cell backward
+    {
+      float gi = 0, gf = 0, gg = 0, go = 0, ct = 0, cp = 0;
+      if (valid) {
+        const size_t nt = (size_t)(n0 + cb) * T + t;
+        const float* gsv = a.gates + ((size_t)dir * a.N * T + nt) * G4;
+        gi = gsv[cu]; gf = gsv[H + cu]; gg = gsv[2 * H + cu]; go = gsv[3 * H + cu];
+        ct = a.cell[((size_t)dir * a.N * T + nt) * H + cu];
+        if (has_prev) {
+          const size_t ntp = (size_t)(n0 + cb) * T + tp;
+          cp = a.cell[((size_t)dir * a.N * T + ntp) * H + cu];
+          hp[cb * H + cu] = a.seq[ntp * 2 * H + dir * H + cu];
+        } else {
+          hp[cb * H + cu] = 0.f;
+        }
+      } else {
+        hp[cb * H + cu] = 0.f;
+      }
+      const float dh = dmean + dhr[cb * H + cu];
+      const float tc = tanhf(ct);
+      const float dov = dh * tc;
+      dc += dh * go * (1.f - tc * tc);
+      const float div = dc * gg, dgv = dc * gi, dfv = dc * cp;
+      dc = dc * gf;
+      float* dg = dgs + cb * G4;
+      dg[cu] = valid ? div * gi * (1.f - gi) : 0.f;
+      dg[H + cu] = valid ? dfv * gf * (1.f - gf) : 0.f;
+      dg[2 * H + cu] = valid ? dgv * (1.f - gg * gg) : 0.f;
+      dg[3 * H + cu] = valid ? dov * go * (1.f - go) : 0.f;
+    }
+    __syncthreads();
+    // thread = gate row: weight-gradient accumulation
+#pragma unroll
+    for (int b = 0; b < LSTM_NB; ++b) {
+      const float d = dgs[b * G4 + tid];
+      gb += d;
+      const float* xr = xs + (b * T + t) * S;
+#pragma unroll
+      for (int s = 0; s < 32; ++s)
+        if (s < S) gwi[s] += d * xr[s];
+      const float* hr = hp + b * H;
+#pragma unroll
+      for (int u = 0; u < H; ++u) gwh[u] += d * hr[u];
+    }
+    // (b, u'): recurrent dh
+    {
+      float acc = 0.f;
+      const float* dg = dgs + cb * G4;
+      for (int g = 0; g < G4; ++g) acc += dg[g] * whs[g * (H + 1) + cu];
+      __syncthreads();  // everyone finished reading dhr of this step (dh above)
+      dhr[cb * H + cu] = acc;
+    }
+    if (a.dx) {
+      for (int i = tid; i < LSTM_NB * S; i += 256) {
+        const int b = i / S, s = i - b * S;
+        if (n0 + b >= a.N) continue;
+        float acc = 0.f;
+        for (int g = 0; g < G4; ++g) acc += dgs[b * G4 + g] * wis[g * S + s];
+        atomic_add_f(a.dx + ((size_t)(n0 + b) * T + t) * S + s, acc);
+      }
+    }
+    __syncthreads();
+  }
+  atomic_add_f(a.g_b_ih[dir] + tid, gb);
+  atomic_add_f(a.g_b_hh[dir] + tid, gb);
+  for (int s = 0; s < S && s < 32; ++s) atomic_add_f(a.g_w_ih[dir] + tid * S + s, gwi[s]);
+#pragma unroll
+  for (int u = 0; u < H; ++u) atomic_add_f(a.g_w_hh[dir] + tid * H + u, gwh[u]);
+}
+
+// ----------------------------------------------------------------------------
+// sensor head: hmean -> BN1d(2H, batch stats) -> CA (2H->2H/8->2H) -> Linear(2H->Cs)
+// single workgroup (N <= 1024): every stage is a [N x 128] pass
+// ----------------------------------------------------------------------------
+constexpr int HC = 2 * H, HR = HC / 8;
+
+__global__ __launch_bounds__(1024) void shead_fwd_kernel(SHeadArgs a) {
+  __shared__ float sc[HC], sh[HC], w1[HR * HC], w2[HC * HR], b1[HR], b2[HC];
+  const int tid = threadIdx.x, N = a.N;
+  for (int i = tid; i < HR * HC; i += 1024) { w1[i] = a.W1[i]; w2[i] = a.W2[i]; }
+  if (tid < HR) b1[tid] = a.b1[tid];
+  if (tid < HC) b2[tid] = a.b2[tid];
+  if (tid < HC) {
+    const int c = tid;
+    float mean, rstd;
+    if (a.bn.eval) {
+      mean = a.bn.rmean[c];
+      rstd = rsqrtf(a.bn.rvar[c] + kBnEps);
+    } else {
+      double s = 0, q = 0;
+      for (int n = 0; n < N; ++n) {
+        const double v = a.hmean[(size_t)n * HC + c];
+        s += v;
+        q += v * v;
+      }
+      a.bn_sum[c] = s;
+      a.bn_sq[c] = q;
+      const double m = s / N;
+      double var = q / N - m * m;
+      if (var < 0) var = 0;
+      mean = (float)m;
+      rstd = (float)(1.0 / sqrt(var + kBnEps));
+    }
+    sc[c] = a.bn.gamma[c] * rstd;
+    sh[c] = a.bn.beta[c] - mean * sc[c];
+  }
+  __syncthreads();
+  for (int i = tid; i < N * HC; i += 1024) {
+    const int c = i % HC;
+    a.ybn[i] = a.hmean[i] * sc[c] + sh[c];
+  }
+  __syncthreads();
+  for (int i = tid; i < N * HR; i += 1024) {
+    const int n = i / HR, j = i - n * HR;
+    float q = b1[j];
+    const float* y = a.ybn + (size_t)n * HC;
+    for (int c = 0; c < HC; ++c) q += w1[j * HC + c] * y[c];
+    a.a1[i] = fmaxf(q, 0.f);
+  }
+  __syncthreads();
+  for (int i = tid; i < N * HC; i += 1024) {
+    const int n = i / HC, c = i - n * HC;
+    float q = b2[c];
+    const float* h1 = a.a1 + (size_t)n * HR;
+    for (int j = 0; j < HR; ++j) q += w2[c * HR + j] * h1[j];
+    a.att[i] = sigmoidf_(q);
+  }
+  __syncthreads();
+  for (int i = tid; i < N * a.Cs; i += 1024) {
+    const int n = i / a.Cs, k = i - n * a.Cs;
+    float q = a.b3[k];
+    const float* y = a.ybn + (size_t)n * HC;
+    const float* at = a.att + (size_t)n * HC;
+    const float* w = a.W3 + (size_t)k * HC;
+    for (int c = 0; c < HC; ++c) q += w[c] * y[c] * at[c];
+    a.out[(size_t)n * a.out_ld + k] = q;
+  }
+}
+
+__global__ __launch_bounds__(1024) void shead_bwd_kernel(SHeadArgs a) {
+  __shared__ float w1[HR * HC], w2[HC * HR];
+  __shared__ float red1[HC], red2[HC], mean_s[HC], rstd_s[HC];
+  const int tid = threadIdx.x, N = a.N, Cs = a.Cs;
+  for (int i = tid; i < HR * HC; i += 1024) { w1[i] = a.W1[i]; w2[i] = a.W2[i]; }
+  __syncthreads();
+  // out = W3 (y*att) + b3
+  for (int i = tid; i < Cs * HC; i += 1024) {
+    const int k = i / HC, c = i - k * HC;
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n)
+      acc += a.dout[(size_t)n * a.dout_ld + k] * a.ybn[(size_t)n * HC + c] * a.att[(size_t)n * HC + c];
+    a.g_W3[i] += acc;
+  }
+  for (int k = tid; k < Cs; k += 1024) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += a.dout[(size_t)n * a.dout_ld + k];
+    a.g_b3[k] += acc;
+  }
+  // d(y*att): dy2 ; dyn_a = dy2*att ; dpre2 = dy2*y*att*(1-att)
+  for (int i = tid; i < N * HC; i += 1024) {
+    const int n = i / HC, c = i - n * HC;
+    float d = 0.f;
+    for (int k = 0; k < Cs; ++k) d += a.dout[(size_t)n * a.dout_ld + k] * a.W3[(size_t)k * HC + c];
+    const float at = a.att[i];
+    a.dy[i] = d * at;                                   // dyn partial
+    a.dpre2[i] = d * a.ybn[i] * at * (1.f - at);
+  }
+  __syncthreads();
+  for (int i = tid; i < HC * HR; i += 1024) {          // dW2[c][j], db2 by j==0 threads
+    const int c = i / HR, j = i - c * HR;
+    float acc = 0.f, accb = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float d = a.dpre2[(size_t)n * HC + c];
+      acc += d * a.a1[(size_t)n * HR + j];
+      accb += d;
+    }
+    a.g_W2[i] += acc;
+    if (j == 0) a.g_b2[c] += accb;
+  }
+  for (int i = tid; i < N * HR; i += 1024) {           // dpre1 = (W2^T dpre2) * (a1 > 0)
+    const int n = i / HR, j = i - n * HR;
+    float acc = 0.f;
+    for (int c = 0; c < HC; ++c) acc += a.dpre2[(size_t)n * HC + c] * w2[c * HR + j];
+    a.dpre1[i] = a.a1[i] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < HR * HC; i += 1024) {          // dW1[j][c], db1
+    const int j = i / HC, c = i - j * HC;
+    float acc = 0.f, accb = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float d = a.dpre1[(size_t)n * HR + j];
+      acc += d * a.ybn[(size_t)n * HC + c];
+      accb += d;
+    }
+    a.g_W1[i] += acc;
+    if (c == 0) a.g_b1[j] += accb;
+  }
+  for (int i = tid; i < N * HC; i += 1024) {           // dyn += W1^T dpre1
+    const int n = i / HC, c = i - n * HC;
+    float acc = 0.f;
+    for (int j = 0; j < HR; ++j) acc += a.dpre1[(size_t)n * HR + j] * w1[j * HC + c];
+    a.dy[i] += acc;
+  }
+  __syncthreads();
+  // BatchNorm1d backward over the batch
+  if (tid < HC) {
+    const int c = tid;
+    const double m = a.bn_sum[c] / N;
+    double var = a.bn_sq[c] / N - m * m;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + kBnEps));
+    float s1 = 0.f, s2 = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float d = a.dy[(size_t)n * HC + c];
+      const float xh = (a.hmean[(size_t)n * HC + c] - (float)m) * rstd;
+      s1 += d;
+      s2 += d * xh;
+    }
+    a.g_gamma[c] += s2;
+    a.g_beta[c] += s1;
+    red1[c] = s1 / N;
+    red2[c] = s2 / N;
+    mean_s[c] = (float)m;
+    rstd_s[c] = rstd;
+  }
+  __syncthreads();
+  for (int i = tid; i < N * HC; i += 1024) {
+    const int c = i % HC;
+    const float mean = mean_s[c], rstd = rstd_s[c];
+    const float xh = (a.hmean[i] - mean) * rstd;
+    a.dhmean[i] = a.bn.gamma[c] * rstd * (a.dy[i] - red1[c] - xh * red2[c]);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// CNN1D: Conv1d(k5,p2) -> BN (batch stats) -> ReLU -> MaxPool1d(2), twice
+// layout: [N][T][C] rows (time-major, channel contiguous)
+// ----------------------------------------------------------------------------
+__global__ void conv1d_fwd_kernel(Conv1dArgs a) {
+  const int n = blockIdx.x;
+  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
+    const int t = i / a.Co, o = i - t * a.Co;
+    float acc = a.b[o];
+    for (int k = 0; k < 5; ++k) {
+      const int ti = t + k - 2;
+      if (ti < 0 || ti >= a.T) continue;
+      const float* xr = a.x + ((size_t)n * a.T + ti) * a.Ci;
+      for (int s = 0; s < a.Ci; ++s) acc += a.w[(o * a.Ci + s) * 5 + k] * xr[s];
+    }
+    a.y[((size_t)n * a.T + t) * a.Co + o] = acc;
+    atomic_add_d(a.st_sum + o, (double)acc);
+    atomic_add_d(a.st_sq + o, (double)acc * acc);
+  }
+}
+
+__global__ void bnrelupool_fwd_kernel(Conv1dArgs a) {
+  const int n = blockIdx.x, Tp = a.T / 2;
+  for (int i = threadIdx.x; i < Tp * a.Co; i += blockDim.x) {
+    const int tp = i / a.Co, o = i - tp * a.Co;
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn, o, sc, sh, mu, rs);
+    const float v0 = fmaxf(a.y[((size_t)n * a.T + 2 * tp) * a.Co + o] * sc + sh, 0.f);
+    const float v1 = fmaxf(a.y[((size_t)n * a.T + 2 * tp + 1) * a.Co + o] * sc + sh, 0.f);
+    a.p[((size_t)n * Tp + tp) * a.Co + o] = fmaxf(v0, v1);
+  }
+}
+
+// gradient through MaxPool + ReLU to the BN output, with BN-backward sums
+__global__ void bnrelupool_bwd_kernel(Conv1dArgs a) {
+  const int n = blockIdx.x, Tp = a.T / 2;
+  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
+    const int t = i / a.Co, o = i - t * a.Co;
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn, o, sc, sh, mu, rs);
+    const float yv = a.y[((size_t)n * a.T + t) * a.Co + o];
+    float d = 0.f;
+    const int tp = t / 2;
+    if (tp < Tp) {
+      const float v0 = fmaxf(a.y[((size_t)n * a.T + 2 * tp) * a.Co + o] * sc + sh, 0.f);
+      const float v1 = fmaxf(a.y[((size_t)n * a.T + 2 * tp + 1) * a.Co + o] * sc + sh, 0.f);
+      const int win = (v1 > v0) ? 1 : 0;  // first max wins ties (max_pool1d)
+      const float me = fmaxf(yv * sc + sh, 0.f);
+      if ((t & 1) == win && me > 0.f) d = a.dp[((size_t)n * Tp + tp) * a.Co + o];
+    }
+    a.dy[((size_t)n * a.T + t) * a.Co + o] = d;
+    atomic_add_d(a.bsum + o, (double)d);
+    atomic_add_d(a.bsq + o, (double)d * ((yv - mu) * rs));
+  }
+}
+
+// BN apply backward then conv1d backward (dx += , dW, db via atomics)
+__global__ void conv1d_bwd_kernel(Conv1dArgs a) {
+  extern __shared__ float dcs[];  // [T][Co]
+  const int n = blockIdx.x;
+  const float M = a.bn.count;
+  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
+    const int o = i % a.Co;
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn, o, sc, sh, mu, rs);
+    const float yv = a.y[(size_t)n * a.T * a.Co + i];
+    const float xh = (yv - mu) * rs;
+    const float d = a.dy[(size_t)n * a.T * a.Co + i];
+    dcs[i] = a.bn.gamma[o] * rs * (d - (float)a.bsum[o] / M - xh * (float)a.bsq[o] / M);
+  }
+  __syncthreads();
+  if (n == 0) {
+    for (int o = threadIdx.x; o < a.Co; o += blockDim.x) {
+      a.g_gamma[o] += (float)a.bsq[o];
+      a.g_beta[o] += (float)a.bsum[o];
+    }
+  }
+  for (int i = threadIdx.x; i < a.Co; i += blockDim.x) {
+    float acc = 0.f;
+    for (int t = 0; t < a.T; ++t) acc += dcs[t * a.Co + i];
+    atomic_add_f(a.g_b + i, acc);
+  }
+  for (int i = threadIdx.x; i < a.Co * a.Ci * 5; i += blockDim.x) {
+    const int o = i / (a.Ci * 5), r = i - o * a.Ci * 5, s = r / 5, k = r - s * 5;
+    float acc = 0.f;
+    for (int t = 0; t < a.T; ++t) {
+      const int ti = t + k - 2;
+      if (ti < 0 || ti >= a.T) continue;
+      acc += dcs[t * a.Co + o] * a.x[((size_t)n * a.T + ti) * a.Ci + s];
+    }
+    atomic_add_f(a.g_w + i, acc);
+  }
+  if (a.dx) {
+    for (int i = threadIdx.x; i < a.T * a.Ci; i += blockDim.x) {
+      const int ti = i / a.Ci, s = i - ti * a.Ci;
+      float acc = 0.f;
+      for (int k = 0; k < 5; ++k) {
+        const int t = ti - k + 2;
+        if (t < 0 || t >= a.T) continue;
+        for (int o = 0; o < a.Co; ++o) acc += dcs[t * a.Co + o] * a.w[(o * a.Ci + s) * 5 + k];
+      }
+      a.dx[((size_t)n * a.T + ti) * a.Ci + s] = acc;
+    }
+  }
+}
+
+}  // namespace f3
+
+using namespace f3;
+
+static size_t lstm_fwd_lds(const LstmArgs& a) {
+  return ((size_t)LSTM_NB * a.T * a.S + LSTM_NB * H + LSTM_NB * G4) * 4;
+}
+static size_t lstm_bwd_lds(const LstmArgs& a) {
+  return ((size_t)G4 * (H + 1) + G4 * a.S + LSTM_NB * a.T * a.S + LSTM_NB * H + LSTM_NB * G4 + LSTM_NB * H) * 4;
+}
+
+int f3_lstm_fwd(const LstmArgs* a, hipStream_t s) {
+  if (a->S > 32 || a->S < 1) return F3_EINVAL;
+  dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
+  hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), lstm_fwd_lds(*a), s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
+  if (a->S > 32 || a->S < 1) return F3_EINVAL;
+  dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
+  const size_t lds = lstm_bwd_lds(*a);
+  if (lds > 160 * 1024) return F3_EINVAL;
+  static bool once = (hipFuncSetAttribute((const void*)lstm_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024), (void)hipGetLastError(), true);
+  (void)once;
+  hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), lds, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(shead_fwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_shead_bwd(const SHeadArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(shead_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_conv1d_fwd(const Conv1dArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(conv1d_fwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_bnrelupool_fwd(const Conv1dArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(bnrelupool_fwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(bnrelupool_bwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(conv1d_bwd_kernel, dim3(a->N), dim3(256), (size_t)a->T * a->Co * 4, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}

@@ -1,0 +1,112 @@
+/* fall3 — MI355X-native (gfx950) 3-stream fall-detection training step: C ABI.
+ *
+ * This is the drop-in boundary for the reference's model/step interface
+ * (/root/reference/Multimodal_Fall3/model/...). Each entry point replaces one call of
+ * the reference training loop (model/main.py:91-148):
+ *
+ *   f3_net_create      <- build_model(config)            model/build_model.py:5-19
+ *   f3_net_entry       <- model.state_dict() keys/shapes  (same names, order, shapes)
+ *   f3_net_forward     <- pred = model(data, sensor)      model/main.py:112, combination.py:37-46
+ *   f3_net_loss        <- loss_fn(pred, label_onehot)     model/main.py:113,280 (CE, soft targets)
+ *   f3_net_backward    <- loss.backward()                 model/main.py:115
+ *   f3_rmsprop_step    <- optimizer.step()                model/main.py:127, optimizer.py:21
+ *
+ * Conventions: plain pointers to device memory (HIP), sizes in elements, a HIP stream
+ * passed as void*. No call allocates, frees or synchronises: every buffer (flat
+ * parameters, flat grads, BN buffers, workspace) is owned by the caller, so a full
+ * step can be captured into a HIP graph. Every function returns 0 on success or an
+ * F3_E* status (never aborts); f3_status_string() names it.
+ */
+#ifndef FALL3_H
+#define FALL3_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define F3_OK 0
+#define F3_EINVAL 1001 /* bad argument / unsupported shape */
+#define F3_EBATCH 1002 /* train-mode batch of 1: BatchNorm needs >1 value per channel */
+#define F3_EHIP 1003   /* HIP launch error */
+#define F3_ESTATE 1004 /* backward without a training forward on this workspace */
+
+enum { F3_MODEL_TWO_STGCAN_BILSTM = 0, F3_MODEL_TWO_STGCAN = 1, F3_MODEL_STGCN = 2, F3_MODEL_BILSTM = 3 };
+enum { F3_SENSOR_NONE = 0, F3_SENSOR_BILSTM = 1, F3_SENSOR_CNN_BILSTM = 2 };
+enum { F3_NAMING_PACKAGE = 0, F3_NAMING_NOTEBOOK = 1 };
+enum { F3_ENTRY_PARAM = 0, F3_ENTRY_BUFFER = 1, F3_ENTRY_COUNTER = 2 };
+
+typedef struct f3_config {
+  int model;           /* F3_MODEL_*  (build_model.py:9-17 MODEL.NAME) */
+  int num_node;        /* V: 14 coco_cut, 18 coco_mmpose (graph.py:24-49) */
+  int num_partition;   /* K: 1 uniform, 2 distance, 3 spatial (graph.py:50-90) */
+  int num_class;       /* DATA.NUM_CLASSES */
+  int in_channels;     /* DATA.IN_CHANNELS (stgcn model) */
+  int sensor;          /* F3_SENSOR_* */
+  int sensor_dim;      /* DATA.SENSOR_DIM */
+  int sensor_classes;  /* BiLSTM head width (package: num_class; UR notebook: 2) */
+  int softmax_output;  /* notebook form returns softmax (GSTCAN_HAR_conv_10kfold.ipynb:444) */
+  int naming;          /* F3_NAMING_* state_dict prefixes */
+  int frames;          /* skeleton window T (30) */
+  int sensor_frames;   /* IMU window Ts (30) */
+} f3_config;
+
+typedef struct f3_net f3_net;
+
+int f3_net_create(const f3_config* cfg, f3_net** out);
+void f3_net_destroy(f3_net* net);
+
+/* state_dict table: entries in reference order. kind = F3_ENTRY_*; offset indexes the
+ * flat fp32 parameter array (PARAM), the flat fp32 buffer array (BUFFER: A, running
+ * stats) or the flat int64 counter array (COUNTER: num_batches_tracked). */
+int f3_net_num_entries(const f3_net* net);
+int f3_net_entry(const f3_net* net, int i, const char** name, int* kind, int* ndim, int64_t* shape8,
+                 int64_t* offset);
+int64_t f3_net_param_count(const f3_net* net);
+int64_t f3_net_buffer_count(const f3_net* net);
+int64_t f3_net_counter_count(const f3_net* net);
+int64_t f3_net_workspace_bytes(const f3_net* net, int batch);
+
+/* Forward. skel f32[N,3,T,V] (reference layout), sensor f32[N,Ts,S] (ignored without a
+ * sensor stream), out f32[N,C] (logits, or softmax for softmax_output). training=1 uses
+ * batch statistics and updates running stats / num_batches_tracked in place (momentum
+ * 0.1); training=0 uses running statistics. The workspace keeps what backward needs. */
+int f3_net_forward(f3_net* net, int batch, int training, const float* params, float* buffers, int64_t* counters,
+                   const float* skel, const float* sensor, float* out, void* workspace, void* stream);
+
+/* loss = -(1/N) sum_i sum_c y_ic log_softmax(out_i)_c ; dout = dloss/dout. */
+int f3_net_loss(f3_net* net, int batch, const float* out, const float* label, float* loss, float* dout,
+                void* stream);
+
+/* Backward of the last training forward on `workspace`: grads (flat, same layout as
+ * params) are OVERWRITTEN with d(sum dout*out)/dparams. */
+int f3_net_backward(f3_net* net, int batch, const float* params, const float* dout, float* grads,
+                    void* workspace, void* stream);
+
+/* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
+ * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):
+ * sq = alpha*sq + (1-alpha)*g^2 ; p -= lr*g/(sqrt(sq)+eps). */
+int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_t n, float lr, float alpha,
+                    float eps, float grad_scale, void* stream);
+
+/* Kernel-level entry used by the unit tests: out[N,T_out,V,Cout] = conv_(KT,1)(x) with
+ * x [N,T_in,V,Cin] channels-last, w in reference layout [Cout][Cin][KT], bias [Cout]. */
+int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
+                    int V, int Cin, int Cout, int KT, int stride, int pad, void* stream);
+
+/* Its gradients: dx = conv^T(dy) [N,T_in,V,Cin]; dw [Cout][Cin][KT] and db [Cout] (overwritten). */
+int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
+                          int Cout, int KT, int stride, int pad, void* stream);
+int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
+                            int Cout, int KT, int stride, int pad, void* stream);
+
+const char* f3_status_string(int status);
+
+/* Debug accessor for tools/tests: device pointer of a per-layer workspace tensor
+ * ("x","z","g","h","r","out","att","dh","dv","dg","dZ","dres","bn1_fsum",...) or NULL. */
+void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, int layer, const char* what);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FALL3_H */

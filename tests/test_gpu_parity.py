@@ -1,0 +1,210 @@
+"""HIP path vs the oracle / the reference's golden vectors (needs an MI355X)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_cpu as oc
+from oracle.prng import synthetic_batch
+from tests.golden_util import check_grads_conditioned, check_packed, check_post, load
+
+pytestmark = pytest.mark.gpu
+
+TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb"]
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda")
+
+
+def build_from_spec(spec, device):
+    import fall_multimodal_amd as f3
+    g = {"layout": spec.layout, "strategy": spec.strategy}
+    if spec.model == "stgcn":
+        return f3.STGCAN(spec.in_channels, g, spec.num_class, device=device)
+    if spec.model == "bilstm":
+        return f3.BiLSTM(spec.sensor_dim, num_classes=spec.num_class, device=device)
+    if spec.model == "two_stgcan":
+        return f3.TwoStreamSTGCAN(3, g, spec.num_class, device=device)
+    if spec.naming == "notebook":
+        return f3.TwoStreamSpatialTemporalGraph(g, spec.num_class, sensor=spec.sensor, sensor_dim=spec.sensor_dim,
+                                                sensor_classes=spec.sensor_classes, device=device)
+    return f3.TwoStreamSTGCAN_BiLSTM(3, g, spec.num_class, spec.sensor_dim, device=device)
+
+
+def call(model, spec, skel, sensor):
+    if spec.naming == "notebook":
+        return model((skel, skel[:, :2, 1:] - skel[:, :2, :-1], sensor))
+    if spec.model == "bilstm":
+        return model(None, sensor)
+    return model(skel, sensor)
+
+
+def test_conv_kernel_matches_torch():
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    torch.manual_seed(0)
+    for (N, T, V, Ci, Co, KT, s, p) in [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4),
+                                         (2, 15, 14, 128, 256, 1, 2, 0), (2, 30, 14, 9, 64, 1, 1, 0),
+                                         (4, 8, 18, 256, 256, 9, 1, 4)]:
+        x = torch.randn(N, Ci, T, V)
+        w = torch.randn(Co, Ci, KT, 1) / np.sqrt(Ci * KT)
+        b = torch.randn(Co)
+        ref = torch.nn.functional.conv2d(x, w, b, stride=(s, 1), padding=(p, 0))  # [N,Co,To,V]
+        xg = x.permute(0, 2, 3, 1).contiguous().to(d)
+        To = (T + 2 * p - KT) // s + 1
+        out = torch.empty(N, To, V, Co, device=d)
+        wp = torch.empty(Co * KT * Ci, device=d)
+        wg, bg = w.contiguous().to(d), b.to(d)  # keep alive until the async launches have consumed them
+        st = L.lib().f3_conv_forward(L.ptr(xg), L.ptr(wg), L.ptr(bg), L.ptr(out), L.ptr(wp),
+                                     N, T, V, Ci, Co, KT, s, p, L.stream_handle())
+        L.check(st, "conv")
+        got = out.cpu().permute(0, 3, 1, 2)
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+CONV_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
+               (4, 29, 14, 128, 128, 9, 2, 4), (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4)]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_backward_kernels_match_torch(shape):
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    N, T, V, Ci, Co, KT, s, p = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, T, V, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(Co, Ci, KT, 1, dtype=torch.float64) / np.sqrt(Ci * KT)).requires_grad_(True)
+    b = torch.zeros(Co, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, b, stride=(s, 1), padding=(p, 0))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    To = y.shape[2]
+    dyg = dy.float().permute(0, 2, 3, 1).contiguous().to(d)
+    xg = x.detach().float().permute(0, 2, 3, 1).contiguous().to(d)
+    wg = w.detach().float().contiguous().to(d)
+    dx = torch.empty(N, T, V, Ci, device=d)
+    wp = torch.empty(Co * KT * Ci, device=d)
+    dw = torch.empty(Co, Ci, KT, device=d)
+    db = torch.empty(Co, device=d)
+    L.check(L.lib().f3_conv_backward_data(L.ptr(dyg), L.ptr(wg), L.ptr(dx), L.ptr(wp), N, T, V, Ci, Co, KT, s, p,
+                                          L.stream_handle()), "dgrad")
+    L.check(L.lib().f3_conv_backward_weight(L.ptr(dyg), L.ptr(xg), L.ptr(dw), L.ptr(db), N, T, V, Ci, Co, KT, s, p,
+                                            L.stream_handle()), "wgrad")
+    ref_dx = x.grad.permute(0, 2, 3, 1).numpy()
+    np.testing.assert_allclose(dx.cpu().numpy(), ref_dx, rtol=0, atol=2e-5 * np.abs(ref_dx).max() + 1e-6)
+    ref_dw = w.grad.reshape(Co, Ci, KT).numpy()
+    np.testing.assert_allclose(dw.cpu().numpy(), ref_dw, rtol=0, atol=2e-5 * np.abs(ref_dw).max() + 1e-6)
+    np.testing.assert_allclose(db.cpu().numpy(), b.grad.numpy(), rtol=0, atol=2e-5 * np.abs(b.grad.numpy()).max())
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_train_step_matches_reference_golden(tag):
+    """fp32 path vs the reference's own outputs (golden, B=4):
+    * forward: logits within 1e-3 (north-star gate; measured ~1e-6), identical argmax, loss;
+    * BN running stats after the step;
+    * gradients: conditioning-aware (see golden_util.check_grads_conditioned — at B=4 the
+      reference's gradients move by up to ~1e-1 under 1e-6 perturbations of its BN outputs);
+    * RMSprop: post-step parameters exactly as torch.optim.RMSprop would produce from our grads."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g, spec = load(tag)
+    st = oc.init_state(spec, int(g["seed"][0]))
+    model = build_from_spec(spec, d)
+    model.load_state_dict(st, strict=True)
+    model.train()
+    skel = torch.from_numpy(g["skel"]).to(d)
+    sensor = torch.from_numpy(g["sensor"]).to(d)
+    label = torch.from_numpy(g["label"]).to(d)
+    out = call(model, spec, skel, sensor)
+    ref_out = g["out"]
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref_out, rtol=0, atol=1e-3)
+    assert (out.detach().cpu().numpy().argmax(1) == ref_out.argmax(1)).all()
+    loss = torch.nn.CrossEntropyLoss()(out, label)
+    np.testing.assert_allclose(loss.item(), g["loss"][0], rtol=1e-4, atol=1e-5)
+    opt = f3.RMSprop(model.parameters(), lr=1e-3)
+    opt.zero_grad()
+    loss.backward()
+    pre = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+    grads = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
+    env = oc.gradient_sensitivity(st, spec, *(torch.from_numpy(g[k]) for k in ("skel", "sensor", "label")),
+                                  eps=1e-6, trials=4, per_param=True)
+    check_grads_conditioned(g, grads, env, what=tag)
+    opt.step()
+    for name, p in model.named_parameters():
+        if name not in grads:
+            continue
+        gg = grads[name].astype(np.float64)
+        sq = 0.01 * gg * gg
+        expect = pre[name] - 1e-3 * gg / (np.sqrt(sq) + 1e-8)
+        np.testing.assert_allclose(p.detach().cpu().numpy(), expect, rtol=0, atol=2e-6, err_msg=name)
+    sd = model.state_dict()
+    for name, b in sd.items():
+        if name.endswith(("running_mean", "running_var")):
+            check_packed(g, "buf:" + name, b.cpu().numpy(), rtol=1e-4, atol=1e-5, what=tag + " ")
+        if name.endswith("num_batches_tracked"):
+            assert int(b) == 1, name
+
+
+@pytest.mark.parametrize("layout,S,B", [("coco_mmpose", 6, 32), ("coco_cut", 15, 24)])
+def test_fused_train_step_vs_oracle(layout, S, B):
+    """TrainStep (native fwd + CE + bwd + RMSprop) vs the CPU oracle at a larger batch."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    spec = oc.Spec(model="two_stgcan_bilstm", layout=layout, num_class=11, sensor_dim=S)
+    st = oc.init_state(spec, 77)
+    V = 18 if layout == "coco_mmpose" else 14
+    skel, sensor, label = synthetic_batch(B, V, 11, S, 5)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": layout, "strategy": "spatial"}, 11, S, device=d)
+    model.load_state_dict(st)
+    step = f3.TrainStep(model, B, lr=1e-3)
+    loss = step(torch.from_numpy(skel).to(d), torch.from_numpy(sensor).to(d), torch.from_numpy(label).to(d))
+    out_ref, loss_ref, grads_ref = oc.train_step(st, spec, *(torch.from_numpy(x) for x in (skel, sensor, label)))
+    np.testing.assert_allclose(step.out.cpu().numpy(), out_ref.numpy(), atol=1e-3, rtol=0)
+    assert (step.out.cpu().numpy().argmax(1) == out_ref.numpy().argmax(1)).all()
+    np.testing.assert_allclose(loss.item(), loss_ref.item(), rtol=1e-4)
+    env = oc.gradient_sensitivity(oc.init_state(spec, 77), spec, *(torch.from_numpy(x) for x in (skel, sensor, label)),
+                                  eps=1e-6, trials=3, per_param=True)
+    fake = {"grad:" + k: v.numpy().reshape(-1) for k, v in grads_ref.items()}
+    ours = {name: p.grad.detach().cpu().numpy() for (name, shape, off), p in zip(model.param_views(), model.parameters())}
+    check_grads_conditioned(fake, ours, env, what=f"{layout} B={B}")
+
+
+@pytest.mark.parametrize("tag", ["har", "ur_nb", "stgcn", "bilstm"])
+def test_workspace_poison_no_uninitialized_reads(tag):
+    """Every workspace byte a step reads must have been written by that step: with the
+    workspace pre-filled with NaN (0xFF) or huge (0x7F) bytes the outputs and gradients
+    must stay finite, the forward identical to a zero-filled run, the gradients the same
+    up to this model's fp32 conditioning (cosine)."""
+    d = dev()
+    g, spec = load(tag)
+    st = oc.init_state(spec, int(g["seed"][0]))
+    model = build_from_spec(spec, d)
+    skel = torch.from_numpy(g["skel"]).to(d)
+    sensor = torch.from_numpy(g["sensor"]).to(d)
+    N, C = skel.shape[0], spec.num_class
+    dout = torch.randn(N, C, generator=torch.Generator().manual_seed(3)).to(d)
+    res = []
+    for fill in (0x00, 0xFF, 0x7F):
+        model.load_state_dict(st)
+        ws = torch.full((model._native.workspace_bytes(N),), fill, dtype=torch.uint8, device=d)
+        out = torch.empty(N, C, device=d)
+        sk = None if spec.model == "bilstm" else skel
+        se = sensor if spec.model in ("bilstm", "two_stgcan_bilstm") else None
+        model.native_forward(sk, se, out, ws, True)
+        grads = torch.full((model._native.nparam,), float("nan"), device=d)
+        model.native_backward(N, dout, grads, ws)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), f"fill {fill:#x}: non-finite output"
+        assert torch.isfinite(grads).all(), f"fill {fill:#x}: non-finite gradients"
+        res.append((out.cpu().double(), grads.cpu().double()))
+    for o, gr in res[1:]:
+        torch.testing.assert_close(o, res[0][0], rtol=1e-5, atol=1e-5)
+        cos = float(gr @ res[0][1] / (gr.norm() * res[0][1].norm()))
+        assert cos > 0.999, cos
