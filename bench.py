@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Benchmark: clips/s of the 3-stream fall-detection training step (fwd + CE + bwd +
+RMSprop, + gradient all-reduce for N > 1) on MI355X, one process per GPU.
+
+Workload (BASELINE.json north star / configs[3] per GPU): synthetic clips with B=256 per
+GPU, T=30 frames, J=17 COCO joints + centre node (coco_mmpose, V=18), 3-channel skeleton
++ 6-axis IMU at the frame rate (Ts=30), 11 classes; random-init weights of the reference
+architecture (TwoStreamSTGCAN_BiLSTM, combination.py:27-46). The reference has no RGB
+branch, so none is built or timed.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-graph]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
+ranks), the roofline of the dominant kernel (implicit-GEMM temporal conv, measured live
+with HIP events on the stream it runs on) and the CPU baseline (the oracle timed on this
+host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="clips per GPU")
+    p.add_argument("--layout", default="coco_mmpose")
+    p.add_argument("--sensor-dim", type=int, default=6)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def conv_roofline(dev, batch, V):
+    """Dominant kernel: the (9,1) temporal conv implicit GEMM (conv_gemm_f32), measured on
+    the layer-6 shape of the step (C=256, T=8). Algorithmic FLOP = 2*M*N*K per launch."""
+    import fall_multimodal_amd._lib as L
+    lib = L.lib()
+    N, T, C, KT = batch, 8, 256, 9
+    x = torch.randn(N, T, V, C, device=dev)
+    w = torch.randn(C, C, KT, device=dev) / 48.0
+    b = torch.zeros(C, device=dev)
+    out = torch.empty(N, T, V, C, device=dev)
+    wp = torch.empty(C * KT * C, device=dev)
+    st = L.stream_handle()
+    args = (L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(wp), N, T, V, C, C, KT, 1, 4, st)
+    for _ in range(3):
+        L.check(lib.f3_conv_forward(*args), "conv")
+    reps = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        lib.f3_conv_forward(*args)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    M = N * T * V
+    flop = 2.0 * M * C * (KT * C)
+    achieved = flop / (ms * 1e-3) / 1e12
+    return {"kernel": "conv_gemm_f32 (tcn 9x1, C=256, T=8, incl. weight pack)", "bound": "mfma",
+            "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+            "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}
+
+
+def cpu_baseline(layout, V, S, seconds):
+    """The oracle (CPU PyTorch restatement, pinned to the reference) on this host's cores."""
+    from oracle import model_cpu as oc
+    from oracle.prng import synthetic_batch
+    threads = min(os.cpu_count() or 1, 64)
+    torch.set_num_threads(threads)
+    spec = oc.Spec(model="two_stgcan_bilstm", layout=layout, num_class=11, sensor_dim=S)
+    st = oc.init_state(spec, 7)
+    B = 64
+    sk, se, lb = (torch.from_numpy(x) for x in synthetic_batch(B, V, 11, S, 1))
+    oc.train_step(st, spec, sk, se, lb)  # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds and n < 50:
+        oc.train_step(st, spec, sk, se, lb)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 2), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps (fwd+CE+bwd+RMSprop) of B={B}, V={V}, S={S}, fp32, torch CPU"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234 + rank)
+
+    import fall_multimodal_amd as f3
+    from oracle.prng import synthetic_batch
+
+    V = 18 if a.layout == "coco_mmpose" else 14
+    B, S, C = a.batch, a.sensor_dim, 11
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev)
+    if world > 1:  # identical replicas
+        dist.broadcast(model.flat_parameters(), 0)
+    step = f3.TrainStep(model, B, lr=1e-3)
+    sk, se, lb = (torch.from_numpy(x).to(dev) for x in synthetic_batch(B, V, C, S, 100 + rank))
+    if not a.no_graph:
+        step.capture(sk, se, lb)
+    for _ in range(a.warmup):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss = float(step.loss.item())
+    roof = conv_roofline(dev, B, V) if rank == 0 else None
+    if rank == 0:
+        cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
+        rec = {
+            "metric": "clips/sec (fwd+bwd) 3-stream Fall3, B=256, 1/2/4/8 GPUs; top-1 acc parity",
+            "value": round(world * B * a.steps / dt, 2),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": f"fall3_3stream_{a.layout}_V{V}_S{S}_B{B}_per_gpu",
+                       "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
+                       "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
+                       "hip_graph": not a.no_graph, "final_loss": round(loss, 5)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

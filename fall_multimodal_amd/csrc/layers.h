@@ -50,6 +50,8 @@ struct GcnBiasBwdArgs {
 
 enum : int { RES_NONE = 0, RES_ID = 1, RES_CONV = 2 };
 
+constexpr int kCaMaxRowsPerThread = 4;  // channel attention: batch <= 1024 per GPU
+
 struct BlockArgs {
   int N, TV, C, chunks, res_kind;
   float inv_tv;

@@ -9,6 +9,8 @@
 #include "common.h"
 #include "layers.h"
 
+#include <algorithm>
+
 namespace f3 {
 
 // ----------------------------------------------------------------------------
@@ -206,25 +208,181 @@ __global__ __launch_bounds__(256) void mix_bwd_kernel(MixArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA forms of the graph mix (Cin % 16 == 0, K*V <= 64, V <= 32). Per frame f the mix
+// is a tiny fixed left matrix times a [V x Cin] slab, so each wave keeps its fragments
+// of A~[(w,k)][v] = A_eff[k][v][w] in registers and streams 16-channel column tiles.
+//   fwd:  Z_f[(w,k)][ci] = sum_v  A~[(w,k)][v]  X_f[v][ci]
+//   dx:   dX_f[v][ci]    = sum_wk A~[(w,k)][v]  dZ_f[(w,k)][ci]
+//   dA:   dA[k][v][w]   += sum_{f,ci} X_f[v][ci] dZ_f[(w,k)][ci]
+// (v_mfma_f32_16x16x4_f32; lane l: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
+//  D row 4*(l>>4)+r, col l&15)
+// ---------------------------------------------------------------------------
+F3_DEV f32x4 mfma16x4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+F3_DEV float atil(const float* A, int K, int V, int wk, int v) {
+  if (wk >= K * V || v >= V) return 0.f;
+  const int w = wk / K, k = wk - w * K;
+  return A[(k * V + v) * V + w];
+}
+
+__global__ __launch_bounds__(256) void mix_fwd_mfma_kernel(MixArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
+  const int ksteps = (V + 3) / 4;  // <= 8
+  float af[4][8];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg) : 0.f;
+  const int ctiles = Cin / 16;
+  const long long items = (long long)a.frames * ctiles;
+  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
+    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
+    const float* x = a.x + (size_t)f * V * Cin + ci0 + fr;
+    f32x4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks >= ksteps) break;
+      const int v = 4 * ks + fg;
+      const float b = v < V ? x[(size_t)v * Cin] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b, acc[mt]);
+    }
+    float* z = a.z + (size_t)f * KV * Cin + ci0 + fr;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int wk = 16 * mt + 4 * fg + r;
+        if (wk < KV) z[(size_t)wk * Cin] = acc[mt][r];
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void mix_dx_mfma_kernel(MixArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
+  const int ksteps = (KV + 3) / 4;  // <= 16
+  float af[2][16];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 4 * ks + fg, 16 * mt + fr) : 0.f;
+  const int ctiles = Cin / 16;
+  const long long items = (long long)a.frames * ctiles;
+  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
+    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
+    const float* dz = a.z + (size_t)f * KV * Cin + ci0 + fr;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (ks >= ksteps) break;
+      const int wk = 4 * ks + fg;
+      const float b = wk < KV ? dz[(size_t)wk * Cin] : 0.f;
+      acc[0] = mfma16x4(af[0][ks], b, acc[0]);
+      acc[1] = mfma16x4(af[1][ks], b, acc[1]);
+    }
+    float* dx = a.dx + (size_t)f * V * Cin + ci0 + fr;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int v = 16 * mt + 4 * fg + r;
+        if (v < V) {
+          float* d = dx + (size_t)v * Cin;
+          if (a.accumulate) *d += acc[mt][r];
+          else *d = acc[mt][r];
+        }
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
+  const int ctiles = Cin / 16;
+  const long long items = (long long)a.frames * ctiles;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
+    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
+    const float* x = a.x + (size_t)f * V * Cin + ci0 + 4 * fg;
+    const float* dz = a.z + (size_t)f * KV * Cin + ci0 + 4 * fg;
+    f32x4 xa[2], zb[4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int v = 16 * mt + fr;
+      xa[mt] = v < V ? *reinterpret_cast<const f32x4*>(x + (size_t)v * Cin) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int wk = 16 * nt + fr;
+      zb[nt] = wk < KV ? *reinterpret_cast<const f32x4*>(dz + (size_t)wk * Cin) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x4(xa[mt][s], zb[nt][s], acc[mt][nt]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = 16 * mt + 4 * fg + r;
+      if (v >= V) continue;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int wk = 16 * nt + fr;
+        if (wk >= KV) continue;
+        const int w = wk / K, k = wk - w * K;
+        atomic_add_f(a.dA + (k * V + v) * V + w, acc[mt][nt][r]);
+      }
+    }
+}
+
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
-__global__ void gcn_bias_bwd_kernel(GcnBiasBwdArgs a) {
-  const int KVV = a.K * a.V * a.V;
-  for (int e = threadIdx.x; e < a.K * a.C; e += blockDim.x) {
-    const int k = e / a.C, c = e - k * a.C;
+__global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
+  __shared__ float cs[1024];  // colsum_k[w] of A_eff
+  for (int e = threadIdx.x; e < a.K * a.V; e += blockDim.x) {
+    const int k = e / a.V, w = e - k * a.V;
     float acc = 0.f;
-    for (int w = 0; w < a.V; ++w) {
-      float cs = 0.f;
-      for (int v = 0; v < a.V; ++v) cs += a.Aeff[(k * a.V + v) * a.V + w];
-      acc += cs * a.G[w * a.C + c];
-    }
-    a.db[e] += acc;
+    for (int v = 0; v < a.V; ++v) acc += a.Aeff[(k * a.V + v) * a.V + w];
+    cs[e] = acc;
   }
-  for (int e = threadIdx.x; e < KVV; e += blockDim.x) {
-    const int k = e / (a.V * a.V), w = e % a.V;
-    float acc = 0.f;
-    for (int c = 0; c < a.C; ++c) acc += a.bias[k * a.C + c] * a.G[w * a.C + c];
-    a.dE[e] += a.A[e] * (a.dAeff[e] + acc);
+  __syncthreads();
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.K * a.C) return;
+  const int k = e / a.C, c = e - k * a.C;
+  float acc = 0.f;
+  for (int w = 0; w < a.V; ++w) acc += cs[k * a.V + w] * a.G[w * a.C + c];
+  a.db[e] += acc;
+}
+
+// one workgroup per (k, w): s = sum_c b[k*C+c] G[w][c]; dE[k][v][w] += A*(dAeff + s)
+__global__ __launch_bounds__(256) void gcn_bias_dE_kernel(GcnBiasBwdArgs a) {
+  __shared__ float red[4];
+  const int k = blockIdx.x / a.V, w = blockIdx.x - k * a.V;
+  float acc = 0.f;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) acc += a.bias[k * a.C + c] * a.G[w * a.C + c];
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float sb = red[0] + red[1] + red[2] + red[3];
+  for (int v = threadIdx.x; v < a.V; v += blockDim.x) {
+    const int e = (k * a.V + v) * a.V + w;
+    a.dE[e] += a.A[e] * (a.dAeff[e] + sb);
   }
 }
 
@@ -477,7 +635,10 @@ F3_DEV float block_sum(float v, float* red) {
   return s;
 }
 
-// one workgroup per hidden unit j: q = W1 gap + b1, BN over the batch, ReLU
+// one workgroup per hidden unit j: q = W1 gap + b1, BN over the batch, ReLU.
+// The batch here is only N values per unit and mean^2/var reaches ~1e3 in practice, so
+// the variance is two-pass (sum (q-mean)^2), not E[q^2]-E[q]^2; the stats slots receive
+// sum = N*mean and sumsq = N*(var + mean^2) in double for the running update/backward.
 __global__ __launch_bounds__(256) void ca_fwd1_kernel(CaArgs a) {
   __shared__ float w1[256], sc2[256], sh2[256], red[8];
   const int j = blockIdx.x, C = a.C, H = C / 4;
@@ -487,34 +648,48 @@ __global__ __launch_bounds__(256) void ca_fwd1_kernel(CaArgs a) {
     w1[c] = a.W1[j * C + c];
   }
   __syncthreads();
-  float s = 0.f, s2 = 0.f;
-  for (int n = threadIdx.x; n < a.N; n += 256) {
-    float q = a.b1[j];
-    const float* gp = a.gapsum + (size_t)n * C;
-    for (int c = 0; c < C; ++c) q += w1[c] * (gp[c] * a.inv_tv * sc2[c] + sh2[c]);
-    a.q1[(size_t)n * H + j] = q;
-    s += q;
-    s2 += q * q;
+  float qv[kCaMaxRowsPerThread];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < kCaMaxRowsPerThread; ++r) {
+    const int n = threadIdx.x + r * 256;
+    qv[r] = 0.f;
+    if (n < a.N) {
+      float q = a.b1[j];
+      const float* gp = a.gapsum + (size_t)n * C;
+      for (int c = 0; c < C; ++c) q += w1[c] * (gp[c] * a.inv_tv * sc2[c] + sh2[c]);
+      a.q1[(size_t)n * H + j] = q;
+      qv[r] = q;
+      s += q;
+    }
   }
   s = block_sum(s, red);
+  const float mean_b = s / (float)a.N;
+  float s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < kCaMaxRowsPerThread; ++r) {
+    const int n = threadIdx.x + r * 256;
+    if (n < a.N) s2 += (qv[r] - mean_b) * (qv[r] - mean_b);
+  }
   s2 = block_sum(s2, red);
+  const float var_b = s2 / (float)a.N;
   if (threadIdx.x == 0 && !a.bnca.eval) {
-    a.ca_sum[j] = (double)s;
-    a.ca_sq[j] = (double)s2;
+    a.ca_sum[j] = (double)mean_b * a.N;
+    a.ca_sq[j] = ((double)var_b + (double)mean_b * mean_b) * a.N;
   }
   float mean, rstd;
   if (a.bnca.eval) {
     mean = a.bnca.rmean[j];
     rstd = rsqrtf(a.bnca.rvar[j] + kBnEps);
   } else {
-    mean = s / (float)a.N;
-    float var = fmaxf(s2 / (float)a.N - mean * mean, 0.f);
-    rstd = rsqrtf(var + kBnEps);
+    mean = mean_b;
+    rstd = rsqrtf(var_b + kBnEps);
   }
   const float gm = a.bnca.gamma[j] * rstd, bt = a.bnca.beta[j] - mean * gm;
-  for (int n = threadIdx.x; n < a.N; n += 256) {
-    const float q = a.q1[(size_t)n * H + j];
-    a.hid[(size_t)n * H + j] = fmaxf(q * gm + bt, 0.f);
+#pragma unroll
+  for (int r = 0; r < kCaMaxRowsPerThread; ++r) {
+    const int n = threadIdx.x + r * 256;
+    if (n < a.N) a.hid[(size_t)n * H + j] = fmaxf(qv[r] * gm + bt, 0.f);
   }
 }
 
@@ -557,8 +732,9 @@ __global__ __launch_bounds__(256) void ca_bwd2_kernel(CaArgs a) {
   __shared__ float dq1s[256], hs[256], red[8];
   __shared__ float sc2[256], sh2[256];
   const int j = blockIdx.x, C = a.C, H = C / 4, N = a.N;
-  const float mean = (float)(a.ca_sum[j] / N);
-  const float var = fmaxf((float)(a.ca_sq[j] / N) - mean * mean, 0.f);
+  const double md = a.ca_sum[j] / N;
+  const float mean = (float)md;
+  const float var = (float)fmax(a.ca_sq[j] / N - md * md, 0.0);  // double: see ca_fwd1
   const float rstd = rsqrtf(var + kBnEps);
   float s1 = 0.f, s2 = 0.f;
   for (int n = threadIdx.x; n < N; n += 256) {
@@ -684,7 +860,16 @@ static void allow_big_lds(const void* fn) {
   (void)hipGetLastError();  // a refused attribute must not surface as the next launch's error
 }
 
+static bool mix_mfma_ok(const MixArgs& a) { return a.Cin % 16 == 0 && a.K * a.V <= 64 && a.V <= 32; }
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
+  if (mix_mfma_ok(*a)) {
+    const long long items = (long long)a->frames * (a->Cin / 16);
+    const int grid = (int)std::min<long long>((items + 3) / 4, 8192);
+    hipLaunchKernelGGL(mix_fwd_mfma_kernel, dim3(grid), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   static bool once = (allow_big_lds((const void*)mix_fwd_kernel), true);
   (void)once;
   if (mix_lds(*a, false) > 160 * 1024) return F3_EINVAL;
@@ -695,6 +880,16 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
 }
 
 int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
+  if (mix_mfma_ok(*a)) {
+    const long long items = (long long)a->frames * (a->Cin / 16);
+    const int grid = (int)std::min<long long>((items + 3) / 4, 8192);
+    hipLaunchKernelGGL(mix_dx_mfma_kernel, dim3(grid), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    const int grid2 = (int)std::min<long long>((items + 3) / 4, 512);
+    hipLaunchKernelGGL(mix_dA_mfma_kernel, dim3(grid2), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
   (void)once;
   if (a->K * a->V * a->V > 1024 || mix_lds(*a, true) > 160 * 1024) return F3_EINVAL;
@@ -705,7 +900,10 @@ int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
 }
 
 int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(gcn_bias_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  if (a->K * a->V > 1024) return F3_EINVAL;
+  hipLaunchKernelGGL(gcn_bias_db_kernel, dim3((a->K * a->C + 255) / 256), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gcn_bias_dE_kernel, dim3(a->K * a->V), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -745,7 +943,7 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
 }
 
 int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
-  if (a->C > 256 || a->N > 256 * 64) return F3_EINVAL;
+  if (a->C > 256 || a->N > 256 * kCaMaxRowsPerThread) return F3_EINVAL;
   hipLaunchKernelGGL(ca_fwd1_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_fwd2_kernel, dim3(a->N), dim3(256), 0, s, *a);

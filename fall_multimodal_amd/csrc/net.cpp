@@ -939,6 +939,25 @@ int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* d
   return f3_conv_wgrad(&a, 0, s);
 }
 
+int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frames, int K, int V, int Cin,
+                         void* stream) {
+  MixArgs m;
+  std::memset(&m, 0, sizeof(m));
+  m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = x; m.z = z;
+  return f3_mix_fwd(&m, (hipStream_t)stream);
+}
+
+int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, float* dx, float* dA, int frames, int K,
+                          int V, int Cin, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(dA, 0, sizeof(float) * K * V * V, s) != hipSuccess) return F3_EHIP;
+  MixArgs m;
+  std::memset(&m, 0, sizeof(m));
+  m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = x; m.z = const_cast<float*>(dz);
+  m.dx = dx; m.dA = dA; m.accumulate = 0;
+  return f3_mix_bwd(&m, s);
+}
+
 // debug accessor (tests/tools only): device pointer of a named per-layer workspace tensor
 void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, int layer, const char* what) {
   if (!net || stream < 0 || stream >= net->nstreams || layer < 0 || layer > 6) return nullptr;

@@ -100,6 +100,13 @@ int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpa
 int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, void* stream);
 
+/* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):
+ * z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci]; backward gives dx and dA_eff (overwritten). */
+int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frames, int K, int V, int Cin,
+                         void* stream);
+int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, float* dx, float* dA, int frames, int K,
+                          int V, int Cin, void* stream);
+
 const char* f3_status_string(int status);
 
 /* Debug accessor for tools/tests: device pointer of a per-layer workspace tensor
