@@ -29,7 +29,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+PEAK_MFMA_TFLOPS = {"fp32": 157.3,    # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+                    "bf16": 2500.0}   # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -41,15 +42,18 @@ def parse():
     p.add_argument("--batch", type=int, default=256, help="clips per GPU")
     p.add_argument("--layout", default="coco_mmpose")
     p.add_argument("--sensor-dim", type=int, default=6)
+    p.add_argument("--precision", default="bf16", choices=("bf16", "fp32"),
+                   help="GEMM operand type (bf16: fp32 accumulate; fp32: exact parity mode)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
 
 
-def conv_roofline(dev, batch, V):
-    """Dominant kernel: the (9,1) temporal conv implicit GEMM (conv_gemm_f32), measured on
-    the layer-6 shape of the step (C=256, T=8). Algorithmic FLOP = 2*M*N*K per launch."""
+def conv_roofline(dev, batch, V, precision):
+    """Dominant kernel: the (9,1) temporal conv implicit GEMM (conv_gemm_<precision>),
+    measured on the layer-6 shape of the step (C=256, T=8) with the weight operand already
+    packed (the GEMM launch alone). Algorithmic FLOP = 2*M*N*K per launch."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
     N, T, C, KT = batch, 8, 256, 9
@@ -59,7 +63,10 @@ def conv_roofline(dev, batch, V):
     out = torch.empty(N, T, V, C, device=dev)
     wp = torch.empty(C * KT * C, device=dev)
     st = L.stream_handle()
-    args = (L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(wp), N, T, V, C, C, KT, 1, 4, st)
+    prec = 1 if precision == "bf16" else 0
+    args = (L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(wp), N, T, V, C, C, KT, 1, 4, prec, st)
+    L.check(lib.f3_conv_forward(*args), "conv")  # packs w into wp
+    args = (L.ptr(x), None) + args[2:]
     for _ in range(3):
         L.check(lib.f3_conv_forward(*args), "conv")
     reps = 20
@@ -74,9 +81,10 @@ def conv_roofline(dev, batch, V):
     M = N * T * V
     flop = 2.0 * M * C * (KT * C)
     achieved = flop / (ms * 1e-3) / 1e12
-    return {"kernel": "conv_gemm_f32 (tcn 9x1, C=256, T=8, incl. weight pack)", "bound": "mfma",
-            "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+    peak = PEAK_MFMA_TFLOPS[precision]
+    return {"kernel": f"conv_gemm_{precision} (tcn 9x1, C=256, T=8, N={N}, V={V})", "bound": "mfma",
+            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None,
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}
 
 
@@ -117,7 +125,8 @@ def main():
 
     V = 18 if a.layout == "coco_mmpose" else 14
     B, S, C = a.batch, a.sensor_dim, 11
-    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev,
+                                      precision=a.precision)
     if world > 1:  # identical replicas
         dist.broadcast(model.flat_parameters(), 0)
     step = f3.TrainStep(model, B, lr=1e-3)
@@ -142,7 +151,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(step.loss.item())
-    roof = conv_roofline(dev, B, V) if rank == 0 else None
+    roof = conv_roofline(dev, B, V, a.precision) if rank == 0 else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
         rec = {
@@ -156,7 +165,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": a.precision,
             "data": "synthetic",
             "config": {"workload": f"fall3_3stream_{a.layout}_V{V}_S{S}_B{B}_per_gpu",
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",

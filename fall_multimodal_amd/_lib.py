@@ -30,7 +30,7 @@ ENTRY_PARAM, ENTRY_BUFFER, ENTRY_COUNTER = 0, 1, 2
 class F3Config(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "model", "num_node", "num_partition", "num_class", "in_channels", "sensor", "sensor_dim",
-        "sensor_classes", "softmax_output", "naming", "frames", "sensor_frames")]
+        "sensor_classes", "softmax_output", "naming", "frames", "sensor_frames", "precision")]
 
 
 _lib = None
@@ -58,11 +58,11 @@ def lib():
         "f3_net_loss": (I, [P, I, P, P, P, P, P]),
         "f3_net_backward": (I, [P, I, P, P, P, P, P]),
         "f3_rmsprop_step": (I, [P, P, P, I64, F, F, F, F, P]),
-        "f3_conv_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_status_string": (ctypes.c_char_p, [I]),
         "f3_net_debug_tensor": (P, [P, I, P, I, I, ctypes.c_char_p]),
-        "f3_conv_backward_data": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
-        "f3_conv_backward_weight": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_backward_data": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_backward_weight": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
     }

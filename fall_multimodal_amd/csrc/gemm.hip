@@ -400,6 +400,7 @@ using namespace f3;
 
 int f3_conv_gemm(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
+  if (a.wb) return f3_conv_gemm_bf16(args, pro, epi, s);
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (pro && a.g.Kc > 256) return F3_EINVAL;
   dim3 grid((a.g.M + BM - 1) / BM, (a.g.Nc + BN - 1) / BN);
@@ -422,6 +423,7 @@ int f3_conv_gemm(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
 }
 
 int f3_conv_wgrad(const WgradArgs* args, int pro, hipStream_t s) {
+  if (args->bf16) return f3_conv_wgrad_bf16(args, pro, s);
   WgradArgs a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (pro && a.g.Kc > 256) return F3_EINVAL;

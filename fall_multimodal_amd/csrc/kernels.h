@@ -29,6 +29,7 @@ struct ConvGemmArgs {
   ConvGeom g;
   const float* in;
   const float* w;     // packed [Nc][KT*Kc]
+  const unsigned short* wb;  // same, bf16; non-null selects the bf16 MFMA kernel
   float* out;
   BnRef pro_bn;       // prologue: relu(bn(x)) on input channels
   const float* bias;
@@ -53,9 +54,12 @@ struct WgradArgs {
   int gcn_cin;
   BnRef pro_bn;
   int rows_per_split;
+  int bf16;           // 1: bf16 MFMA (operands rounded to bf16, fp32 accumulate)
 };
 
 }  // namespace f3
 
 int f3_conv_gemm(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
 int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);
+int f3_conv_gemm_bf16(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
+int f3_conv_wgrad_bf16(const f3::WgradArgs* a, int pro, hipStream_t s);

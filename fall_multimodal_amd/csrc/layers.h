@@ -13,6 +13,7 @@ struct PrepJob {
   const float* s1;
   const float* s2;
   int d0, d1, d2;
+  int bf16;  // store dst as bf16 (packed GEMM operands of the bf16 mode)
 };
 
 struct DataBnArgs {

@@ -20,36 +20,36 @@ __global__ void prep_kernel(PrepTable t) {
   const PrepJob j = t.jobs[blockIdx.y];
   const int stride = gridDim.x * blockDim.x;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) {
+    float val = 0.f;
     switch (j.type) {
       case PREP_MUL:
-        j.dst[e] = j.s0[e] * j.s1[e];
+        val = j.s0[e] * j.s1[e];
         break;
       case PREP_COPY:
-        j.dst[e] = j.s0[e];
+        val = j.s0[e];
         break;
       case PREP_PACK_CONV: {  // src [J][I][KT] -> dst [J][KT*I] (k = dt*I + i)
-        const int J = j.d0, I = j.d1, KT = j.d2;
+        const int I = j.d1, KT = j.d2;
         const int jj = e / (KT * I), r = e - jj * KT * I, dt = r / I, i = r - dt * I;
-        (void)J;
-        j.dst[e] = j.s0[((size_t)jj * I + i) * KT + dt];
+        val = j.s0[((size_t)jj * I + i) * KT + dt];
         break;
       }
       case PREP_PACK_CONV_T: {  // dgrad operand: dst [I][KT*J] (k = dt*J + j)
         const int J = j.d0, I = j.d1, KT = j.d2;
         const int i = e / (KT * J), r = e - i * KT * J, dt = r / J, jj = r - dt * J;
-        j.dst[e] = j.s0[((size_t)jj * I + i) * KT + dt];
+        val = j.s0[((size_t)jj * I + i) * KT + dt];
         break;
       }
       case PREP_PACK_GCN: {  // W[k*C+c][ci] -> dst [C][K*Cin] (k-major then ci)
         const int C = j.d0, Cin = j.d1, K = j.d2;
         const int c = e / (K * Cin), r = e - c * K * Cin, k = r / Cin, ci = r - k * Cin;
-        j.dst[e] = j.s0[((size_t)k * C + c) * Cin + ci];
+        val = j.s0[((size_t)k * C + c) * Cin + ci];
         break;
       }
       case PREP_PACK_GCN_T: {  // dgrad operand: dst [K*Cin][C]
         const int C = j.d0, Cin = j.d1;
         const int kc = e / C, c = e - kc * C, k = kc / Cin, ci = kc - k * Cin;
-        j.dst[e] = j.s0[((size_t)k * C + c) * Cin + ci];
+        val = j.s0[((size_t)k * C + c) * Cin + ci];
         break;
       }
       case PREP_GCN_BIAS: {  // dst[w][c] = sum_k colsum(A*E)_k[w] * b[k*C+c]
@@ -61,10 +61,12 @@ __global__ void prep_kernel(PrepTable t) {
           for (int v = 0; v < V; ++v) cs += j.s0[(k * V + v) * V + w] * j.s1[(k * V + v) * V + w];
           acc += cs * j.s2[k * C + c];
         }
-        j.dst[e] = acc;
+        val = acc;
         break;
       }
     }
+    if (j.bf16) reinterpret_cast<__bf16*>(j.dst)[e] = (__bf16)val;  // RNE (v_cvt_pk_bf16_f32)
+    else j.dst[e] = val;
   }
 }
 

@@ -407,10 +407,14 @@ ConvGeom geom(int M, int Nc, int Kc, int KT, int S, int P, int tr, int T_out, in
 }
 
 void add_job(PrepTable& t, int type, int n, float* dst, const float* s0, const float* s1, const float* s2, int d0,
-             int d1, int d2) {
+             int d1, int d2, int bf16 = 0) {
   PrepJob& j = t.jobs[t.n++];
   j.type = type; j.n = n; j.dst = dst; j.s0 = s0; j.s1 = s1; j.s2 = s2; j.d0 = d0; j.d1 = d1; j.d2 = d2;
+  j.bf16 = bf16;
 }
+
+// bf16 view of a packed operand (the fp32-sized slot holds the bf16 copy in bf16 mode)
+inline const unsigned short* bf(const float* p, int on) { return on ? reinterpret_cast<const unsigned short*>(p) : nullptr; }
 
 void add_bnrun(BnRunTable& t, const Ptrs& q, const BnIdx& bi, const double* sum, const double* sq, double count) {
   BnRunJob& j = t.jobs[t.n++];
@@ -423,6 +427,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V, eval = !train;
+  const int hb = net.cfg.precision == F3_PRECISION_BF16;
   // weights: A_eff, gcn bias through the graph, packed GEMM operands
   PrepTable pt;
   pt.n = 0;
@@ -433,15 +438,15 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     const int C = L.cout, Ci = L.cin;
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
-    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K);
-    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9);
+    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, hb);
+    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, hb);
     if (train) {
-      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K);
-      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9);
+      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, hb);
+      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, hb);
     }
     if (L.res == RES_CONV) {
-      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1);
-      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1);
+      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, hb);
+      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, hb);
     }
   }
   F3_TRY(f3_prep(pt, s));
@@ -471,20 +476,20 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     ConvGemmArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
-    ga.in = X.z; ga.w = X.gw; ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+    ga.in = X.z; ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
     F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
       ConvGemmArgs ra;
       std::memset(&ra, 0, sizeof(ra));
       ra.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      ra.in = X.x; ra.w = X.rw; ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
+      ra.in = X.x; ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
     // tcn: BN1 + ReLU prologue, (9,1) conv, bias, BN2 stats + channel-attention pool epilogue
     ConvGemmArgs ta;
     std::memset(&ta, 0, sizeof(ta));
     ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    ta.in = X.g; ta.w = X.tw; ta.out = X.h; ta.pro_bn = bn1; ta.bias = q.p(L.tcn_b);
+    ta.in = X.g; ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.pro_bn = bn1; ta.bias = q.p(L.tcn_b);
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
     F3_TRY(f3_conv_gemm(&ta, 1, EPI_BIAS | EPI_STATS | EPI_GAP, s));
     // channel attention (stgcan.py:59-74)
@@ -526,6 +531,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V;
+  const int hb = net.cfg.precision == F3_PRECISION_BF16;
   const float* dout = nullptr;
   int pp = 0;
   for (int l = 6; l >= 0; --l) {
@@ -566,7 +572,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
-    td.in = W.dh; td.w = X.twT; td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.in = W.dh; td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
     if (debug_stop(si, l)) return F3_OK;
@@ -574,7 +580,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&tw, 0, sizeof(tw));
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
     tw.dy = W.dh; tw.ldy = C; tw.in = X.g; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
-    tw.outmap = WG_OUT_CONV; tw.pro_bn = bn1;
+    tw.outmap = WG_OUT_CONV; tw.pro_bn = bn1; tw.bf16 = hb;
     F3_TRY(f3_conv_wgrad(&tw, 1, s));
     BnBwdArgs bb;
     std::memset(&bb, 0, sizeof(bb));
@@ -585,13 +591,13 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ConvGemmArgs gd;
     std::memset(&gd, 0, sizeof(gd));
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
-    gd.in = W.dg; gd.w = X.gwT; gd.out = W.dZ;
+    gd.in = W.dg; gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
     F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
     gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
     gw.dy = W.dg; gw.ldy = C; gw.in = X.z; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
-    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci;
+    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
     F3_TRY(f3_conv_wgrad(&gw, 0, s));
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
@@ -606,12 +612,12 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       ConvGemmArgs rd;
       std::memset(&rd, 0, sizeof(rd));
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
-      rd.in = W.dres; rd.w = X.rwT; rd.out = dx;
+      rd.in = W.dres; rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
       F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
       rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      rw.dy = W.dres; rw.ldy = C; rw.in = X.x; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV;
+      rw.dy = W.dres; rw.ldy = C; rw.in = X.x; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
       F3_TRY(f3_conv_wgrad(&rw, 0, s));
     }
     dout = dx;
@@ -717,6 +723,7 @@ int f3_net_create(const f3_config* cfg, f3_net** out) {
   if (cfg->num_node < 2 || cfg->num_partition < 1 || cfg->num_class < 1 || cfg->num_class > 64) return F3_EINVAL;
   if (cfg->frames < 2 || cfg->model < 0 || cfg->model > 3) return F3_EINVAL;
   if (cfg->num_partition * cfg->num_node * cfg->num_node > 1024) return F3_EINVAL;
+  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) return F3_EINVAL;
   f3_net* n = new f3_net();
   n->cfg = *cfg;
   n->K = cfg->num_partition;
@@ -897,37 +904,41 @@ int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_
 }
 
 int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
-                    int V, int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+                    int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  PrepTable t;
-  t.n = 0;
-  add_job(t, PREP_PACK_CONV, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT);
-  F3_TRY(f3_prep(t, s));
+  const int hb = precision == F3_PRECISION_BF16;
+  if (w) {  // w == NULL: wpack already holds the packed operand (timing the GEMM alone)
+    PrepTable t;
+    t.n = 0;
+    add_job(t, PREP_PACK_CONV, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, hb);
+    F3_TRY(f3_prep(t, s));
+  }
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
-  a.in = x; a.w = wpack; a.out = out; a.bias = bias;
+  a.in = x; a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias;
   return f3_conv_gemm(&a, 0, EPI_BIAS, s);
 }
 
 int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
-                          int Cout, int KT, int stride, int pad, void* stream) {
+                          int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const int hb = precision == F3_PRECISION_BF16;
   PrepTable t;
   t.n = 0;
-  add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT);
+  add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, hb);
   F3_TRY(f3_prep(t, s));
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_in * V, Cin, Cout, KT, stride, pad, 1, T_in, T_out, V, Cout, Cin);
-  a.in = dy; a.w = wpack; a.out = dx;
+  a.in = dy; a.w = wpack; a.wb = bf(wpack, hb); a.out = dx;
   return f3_conv_gemm(&a, 0, 0, s);
 }
 
 int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
-                            int Cout, int KT, int stride, int pad, void* stream) {
+                            int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
@@ -936,6 +947,7 @@ int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* d
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
   a.dy = dy; a.ldy = Cout; a.in = x; a.dw = dw; a.db = db; a.outmap = WG_OUT_CONV;
+  a.bf16 = precision == F3_PRECISION_BF16;
   return f3_conv_wgrad(&a, 0, s);
 }
 

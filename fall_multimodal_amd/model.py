@@ -33,6 +33,7 @@ from .graph import STRATEGY_PARTITIONS, Graph
 
 MODEL_IDS = {"two_stgcan_bilstm": 0, "two_stgcan": 1, "stgcn": 2, "bilstm": 3}
 SENSOR_IDS = {"none": 0, "bilstm": 1, "cnn_bilstm": 2}
+PRECISION_IDS = {"fp32": 0, "bf16": 1}
 
 
 @dataclass
@@ -49,6 +50,7 @@ class NetSpec:
     naming: str = "package"
     frames: int = 30
     sensor_frames: int = 30
+    precision: str = "fp32"   # "fp32": exact fp32 MFMA (parity mode); "bf16": bf16 operands, fp32 accumulate
     extra: dict = field(default_factory=dict)
 
 
@@ -67,6 +69,9 @@ class NativeNet:
         c.softmax_output = int(spec.softmax_output)
         c.naming = 1 if spec.naming == "notebook" else 0
         c.frames, c.sensor_frames = spec.frames, spec.sensor_frames
+        if spec.precision not in PRECISION_IDS:
+            raise ValueError(f"precision must be one of {sorted(PRECISION_IDS)}, got {spec.precision!r}")
+        c.precision = PRECISION_IDS[spec.precision]
         h = ctypes.c_void_p()
         check(L.f3_net_create(ctypes.byref(c), ctypes.byref(h)), "f3_net_create")
         self.h = h
@@ -308,10 +313,11 @@ def _graph_args(graph_args):
 class STGCAN(Fall3Net):
     """stgcan.py:147-228 with a classifier (build_model 'stgcn')."""
 
-    def __init__(self, in_channels, graph_args, num_class, device=None, frames=30):
+    def __init__(self, in_channels, graph_args, num_class, device=None, frames=30, precision="fp32"):
         layout, strategy = _graph_args(graph_args)
         super().__init__(NetSpec(model="stgcn", layout=layout, strategy=strategy, num_class=num_class,
-                                 in_channels=in_channels, sensor="none", frames=frames), device)
+                                 in_channels=in_channels, sensor="none", frames=frames, precision=precision),
+                         device)
 
 
 class BiLSTM(Fall3Net):
@@ -328,21 +334,21 @@ class BiLSTM(Fall3Net):
 class TwoStreamSTGCAN(Fall3Net):
     """combination.py:9-25 (forward fixed to pass the sensor argument)."""
 
-    def __init__(self, in_channels, graph_args, num_class, device=None, frames=30):
+    def __init__(self, in_channels, graph_args, num_class, device=None, frames=30, precision="fp32"):
         layout, strategy = _graph_args(graph_args)
         super().__init__(NetSpec(model="two_stgcan", layout=layout, strategy=strategy, num_class=num_class,
-                                 sensor="none", frames=frames), device)
+                                 sensor="none", frames=frames, precision=precision), device)
 
 
 class TwoStreamSTGCAN_BiLSTM(Fall3Net):
     """combination.py:27-46."""
 
     def __init__(self, in_channels, graph_args, num_class, bilstm_input_size=15, device=None, frames=30,
-                 sensor_frames=30):
+                 sensor_frames=30, precision="fp32"):
         layout, strategy = _graph_args(graph_args)
         super().__init__(NetSpec(model="two_stgcan_bilstm", layout=layout, strategy=strategy,
                                  num_class=num_class, sensor="bilstm", sensor_dim=bilstm_input_size,
-                                 frames=frames, sensor_frames=sensor_frames), device)
+                                 frames=frames, sensor_frames=sensor_frames, precision=precision), device)
 
 
 class TwoStreamSpatialTemporalGraph(Fall3Net):
@@ -355,7 +361,7 @@ class TwoStreamSpatialTemporalGraph(Fall3Net):
     """
 
     def __init__(self, graph_args, num_class, sensor="bilstm", sensor_dim=None, sensor_classes=None,
-                 device=None, frames=30, sensor_frames=30):
+                 device=None, frames=30, sensor_frames=30, precision="fp32"):
         layout, strategy = _graph_args(graph_args)
         if sensor_dim is None:
             sensor_dim = 4 if sensor == "cnn_bilstm" else 15
@@ -364,24 +370,26 @@ class TwoStreamSpatialTemporalGraph(Fall3Net):
         super().__init__(NetSpec(model="two_stgcan_bilstm", layout=layout, strategy=strategy,
                                  num_class=num_class, sensor=sensor, sensor_dim=sensor_dim,
                                  sensor_classes=sensor_classes, softmax_output=True, naming="notebook",
-                                 frames=frames, sensor_frames=sensor_frames), device)
+                                 frames=frames, sensor_frames=sensor_frames, precision=precision), device)
 
 
-def build_model(config, device=None):
-    """build_model.py:5-19: MODEL.NAME in {stgcn, bilstm, two_stgcan, two_stgcan_bilstm}."""
+def build_model(config, device=None, precision="fp32"):
+    """build_model.py:5-19: MODEL.NAME in {stgcn, bilstm, two_stgcan, two_stgcan_bilstm}.
+    `precision` ("fp32" | "bf16") selects the GEMM operand type of the skeleton streams."""
     name = config.MODEL.NAME
     graph_args = {"layout": config.GRAPH.LAYOUT, "strategy": config.GRAPH.STRATEGY}
     if name == "stgcn":
-        return STGCAN(config.DATA.IN_CHANNELS, graph_args, num_class=config.DATA.NUM_CLASSES, device=device)
+        return STGCAN(config.DATA.IN_CHANNELS, graph_args, num_class=config.DATA.NUM_CLASSES, device=device,
+                      precision=precision)
     if name == "bilstm":
         return BiLSTM(input_size=config.DATA.SENSOR_DIM, hidden_size=64, num_layers=1, dropout_prob=0.3,
                       num_classes=config.DATA.NUM_CLASSES, feature="mean", device=device)
     if name == "two_stgcan":
         return TwoStreamSTGCAN(config.DATA.IN_CHANNELS, graph_args, num_class=config.DATA.NUM_CLASSES,
-                               device=device)
+                               device=device, precision=precision)
     if name == "two_stgcan_bilstm":
         return TwoStreamSTGCAN_BiLSTM(config.DATA.IN_CHANNELS, graph_args, num_class=config.DATA.NUM_CLASSES,
-                                      bilstm_input_size=config.DATA.SENSOR_DIM, device=device)
+                                      bilstm_input_size=config.DATA.SENSOR_DIM, device=device, precision=precision)
     raise RuntimeError(f"Model name [{name}] is not implemented.")
 
 

@@ -34,6 +34,8 @@ extern "C" {
 enum { F3_MODEL_TWO_STGCAN_BILSTM = 0, F3_MODEL_TWO_STGCAN = 1, F3_MODEL_STGCN = 2, F3_MODEL_BILSTM = 3 };
 enum { F3_SENSOR_NONE = 0, F3_SENSOR_BILSTM = 1, F3_SENSOR_CNN_BILSTM = 2 };
 enum { F3_NAMING_PACKAGE = 0, F3_NAMING_NOTEBOOK = 1 };
+enum { F3_PRECISION_FP32 = 0, /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
+       F3_PRECISION_BF16 = 1  /* bf16 operands, fp32 accumulate (v_mfma_f32_16x16x32_bf16) */ };
 enum { F3_ENTRY_PARAM = 0, F3_ENTRY_BUFFER = 1, F3_ENTRY_COUNTER = 2 };
 
 typedef struct f3_config {
@@ -49,6 +51,7 @@ typedef struct f3_config {
   int naming;          /* F3_NAMING_* state_dict prefixes */
   int frames;          /* skeleton window T (30) */
   int sensor_frames;   /* IMU window Ts (30) */
+  int precision;       /* F3_PRECISION_*: GEMM operand type of the skeleton streams' convs */
 } f3_config;
 
 typedef struct f3_net f3_net;
@@ -89,16 +92,18 @@ int f3_net_backward(f3_net* net, int batch, const float* params, const float* do
 int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_t n, float lr, float alpha,
                     float eps, float grad_scale, void* stream);
 
-/* Kernel-level entry used by the unit tests: out[N,T_out,V,Cout] = conv_(KT,1)(x) with
- * x [N,T_in,V,Cin] channels-last, w in reference layout [Cout][Cin][KT], bias [Cout]. */
+/* Kernel-level entries used by the unit tests and bench.py: out[N,T_out,V,Cout] = conv_(KT,1)(x)
+ * with x [N,T_in,V,Cin] channels-last, w in reference layout [Cout][Cin][KT], bias [Cout]
+ * (stgcan.py:24-31 tcn Conv2d). wpack is scratch of Cout*KT*Cin floats for the packed
+ * operand; w == NULL reuses what a previous call packed there. precision = F3_PRECISION_*. */
 int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
-                    int V, int Cin, int Cout, int KT, int stride, int pad, void* stream);
+                    int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream);
 
 /* Its gradients: dx = conv^T(dy) [N,T_in,V,Cin]; dw [Cout][Cin][KT] and db [Cout] (overwritten). */
 int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
-                          int Cout, int KT, int stride, int pad, void* stream);
+                          int Cout, int KT, int stride, int pad, int precision, void* stream);
 int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
-                            int Cout, int KT, int stride, int pad, void* stream);
+                            int Cout, int KT, int stride, int pad, int precision, void* stream);
 
 /* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):
  * z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci]; backward gives dx and dA_eff (overwritten). */

@@ -1,0 +1,82 @@
+"""C-ABI checks that need no GPU: libfall3.so loads, exports every function include/fall3.h
+declares, and its host-side state_dict table (f3_net_create / f3_net_entry, no device
+work) matches the reference's parameter names, shapes and order (oracle.param_shapes,
+itself pinned to the reference's param-count golden vectors)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch  # noqa: F401  (shared HIP runtime before the CDLL)
+
+from oracle import model_cpu as oc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fall3.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(f3_\w+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    fns = header_functions()
+    for name in ("f3_net_create", "f3_net_forward", "f3_net_loss", "f3_net_backward", "f3_rmsprop_step"):
+        assert name in fns
+
+
+def test_library_exports_every_declared_symbol():
+    import fall_multimodal_amd._lib as L
+    so = ctypes.CDLL(L.LIB_PATH)
+    missing = [f for f in header_functions() if not hasattr(so, f)]
+    assert not missing, f"declared in fall3.h but not exported: {missing}"
+    assert sorted(L.EXPORTS) == header_functions(), "_lib.EXPORTS out of sync with fall3.h"
+    L.lib()  # every signature binds
+
+
+def test_status_strings():
+    import fall_multimodal_amd._lib as L
+    for st in (L.F3_OK, L.F3_EINVAL, L.F3_EBATCH, L.F3_EHIP, L.F3_ESTATE):
+        assert L.lib().f3_status_string(st)
+    with pytest.raises(ValueError):
+        L.check(L.F3_EBATCH, "x")
+    with pytest.raises(RuntimeError):
+        L.check(L.F3_EINVAL, "x")
+
+
+SPECS = [
+    oc.Spec(model="two_stgcan_bilstm", layout="coco_cut", num_class=11, sensor_dim=15),
+    oc.Spec(model="two_stgcan_bilstm", layout="coco_mmpose", num_class=11, sensor_dim=6),
+    oc.Spec(model="two_stgcan", layout="coco_cut", num_class=11),
+    oc.Spec(model="stgcn", layout="coco_cut", strategy="spatial", num_class=11, in_channels=3),
+    oc.Spec(model="bilstm", num_class=11, sensor_dim=15),
+    oc.Spec(model="two_stgcan_bilstm", layout="coco_cut", num_class=2, sensor="cnn_bilstm", sensor_dim=4,
+            sensor_classes=2, softmax_output=True, naming="notebook"),
+]
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: f"{s.model}-{s.layout}-{s.naming}-{s.sensor}")
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_entry_table_matches_reference_state_dict(spec, precision):
+    from fall_multimodal_amd.graph import STRATEGY_PARTITIONS
+    from fall_multimodal_amd.model import NativeNet, NetSpec
+    ns = NetSpec(model=spec.model, layout=spec.layout, strategy=spec.strategy, num_class=spec.num_class,
+                 in_channels=spec.in_channels, sensor=spec.sensor, sensor_dim=spec.sensor_dim,
+                 sensor_classes=spec.sensor_classes, softmax_output=spec.softmax_output, naming=spec.naming,
+                 precision=precision)
+    V = 18 if spec.layout == "coco_mmpose" else 14
+    net = NativeNet(ns, STRATEGY_PARTITIONS[spec.strategy], V)
+    ref = oc.param_shapes(spec)
+    got = [(n, tuple(sh)) for n, kind, sh, off in net.entries]
+    assert [n for n, _ in got] == list(ref.keys())
+    for n, sh in got:
+        assert sh == tuple(ref[n]), n
+    assert net.workspace_bytes(8) > 0
+
+
+def test_bad_precision_rejected():
+    from fall_multimodal_amd.model import NativeNet, NetSpec
+    with pytest.raises(ValueError):
+        NativeNet(NetSpec(precision="fp8"), 3, 14)

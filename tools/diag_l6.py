@@ -82,7 +82,7 @@ else:
     ref = torch.from_numpy(np.load('gpurun_out/l6_ref.npy')).to(d)
 for rep in range(4 if STOPPED else 0):
     dw = torch.empty(Cl, Cl, 9, device=d); db = torch.empty(Cl, device=d)
-    L.check(lib.f3_conv_backward_weight(L.ptr(dh), L.ptr(u), L.ptr(dw), L.ptr(db), N, Ti, V, Cl, Cl, 9, stride, 4,
+    L.check(lib.f3_conv_backward_weight(L.ptr(dh), L.ptr(u), L.ptr(dw), L.ptr(db), N, Ti, V, Cl, Cl, 9, stride, 4, 0,
                                         L.stream_handle()), "wg")
     torch.cuda.synchronize()
     print("isolated wgrad vs torch", ((dw.double() - ref).abs().max() / ref.abs().max()).item())
