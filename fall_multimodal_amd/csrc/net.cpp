@@ -68,6 +68,15 @@ const int kChan[7][4] = {{-1, 64, 1, RES_NONE}, {64, 64, 1, RES_ID},    {64, 64,
 }  // namespace
 
 struct f3_net {
+  // branch concurrency: the position stream runs on the caller's stream, the motion stream
+  // and the sensor branch on two private streams forked/joined with events (capturable)
+  hipStream_t aux[2] = {nullptr, nullptr};
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  bool par_init = false, par_ok = false;
+  ~f3_net() {
+    for (auto& a : aux) if (a) (void)hipStreamDestroy(a);
+    for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+  }
   f3_config cfg;
   std::vector<Entry> entries;
   int64_t nparam = 0, nbuf = 0, ncnt = 0;
@@ -711,6 +720,47 @@ void head_args(const f3_net& net, int N, const Ptrs& q, Ws& w, HeadArgs& h) {
   }
 }
 
+// Private branch streams, created on the first eager call (never during a capture: there the
+// branches stay on the caller's stream). F3_SERIAL=1 keeps everything on one stream.
+bool ensure_parallel(f3_net& n, hipStream_t s) {
+  if (n.par_init) return n.par_ok;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return false;
+  }
+  n.par_init = true;
+  if (getenv("F3_SERIAL")) return n.par_ok = false;
+  bool ok = true;
+  for (auto& a : n.aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  (void)hipGetLastError();
+  return n.par_ok = ok;
+}
+
+// Fork `k` branch streams off s (they see all work queued on s so far) / join them back.
+struct Branches {
+  f3_net& n;
+  hipStream_t s;
+  bool par;
+  hipStream_t at(int i) const { return par && i > 0 ? n.aux[i - 1] : s; }
+  int fork() {
+    if (!par) return F3_OK;
+    if (hipEventRecord(n.ev[0], s) != hipSuccess) return F3_EHIP;
+    for (auto a : n.aux)
+      if (hipStreamWaitEvent(a, n.ev[0], 0) != hipSuccess) return F3_EHIP;
+    return F3_OK;
+  }
+  int join() {
+    if (!par) return F3_OK;
+    for (int i = 0; i < 2; ++i) {
+      if (hipEventRecord(n.ev[1 + i], n.aux[i]) != hipSuccess) return F3_EHIP;
+      if (hipStreamWaitEvent(s, n.ev[1 + i], 0) != hipSuccess) return F3_EHIP;
+    }
+    return F3_OK;
+  }
+};
+
 }  // namespace
 
 // ============================================================================
@@ -817,26 +867,31 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
   }
   BnRunTable run;
   run.n = 0;
-  for (int si = 0; si < net->nstreams; ++si) F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, s));
+  Branches br{*net, s, ensure_parallel(*net, s)};
+  F3_TRY(br.fork());
+  for (int si = 0; si < net->nstreams; ++si)
+    F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, br.at(si)));
   if (net->has_sensor) {
+    const hipStream_t ss = br.at(2);
     LstmArgs la;
     SHeadArgs sa;
     Conv1dArgs c1, c2;
     sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
     if (net->has_cnn) {
-      F3_TRY(f3_conv1d_fwd(&c1, s));
-      F3_TRY(f3_bnrelupool_fwd(&c1, s));
-      F3_TRY(f3_conv1d_fwd(&c2, s));
-      F3_TRY(f3_bnrelupool_fwd(&c2, s));
+      F3_TRY(f3_conv1d_fwd(&c1, ss));
+      F3_TRY(f3_bnrelupool_fwd(&c1, ss));
+      F3_TRY(f3_conv1d_fwd(&c2, ss));
+      F3_TRY(f3_bnrelupool_fwd(&c2, ss));
       if (training) {
         add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
         add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
       }
     }
-    F3_TRY(f3_lstm_fwd(&la, s));
-    F3_TRY(f3_shead_fwd(&sa, s));
+    F3_TRY(f3_lstm_fwd(&la, ss));
+    F3_TRY(f3_shead_fwd(&sa, ss));
     if (training) add_bnrun(run, q, net->lstm.bn, w.sbn.fsum, w.sbn.fsq, N);
   }
+  F3_TRY(br.join());
   HeadArgs h;
   head_args(*net, N, q, w, h);
   if (net->cfg.model == F3_MODEL_BILSTM) {
@@ -882,18 +937,22 @@ int f3_net_backward(f3_net* net, int N, const float* params, const float* dout, 
   } else {
     F3_TRY(f3_head_bwd(&h, s));
   }
+  Branches br{*net, s, ensure_parallel(*net, s)};
+  F3_TRY(br.fork());
   if (net->has_sensor) {
-    F3_TRY(f3_shead_bwd(&sa, s));
-    F3_TRY(f3_lstm_bwd(&la, s));
+    const hipStream_t ss = br.at(2);
+    F3_TRY(f3_shead_bwd(&sa, ss));
+    F3_TRY(f3_lstm_bwd(&la, ss));
     if (net->has_cnn) {
-      F3_TRY(f3_conv1d_bwd(&c2, s));
-      F3_TRY(f3_conv1d_bwd(&c1, s));
+      F3_TRY(f3_conv1d_bwd(&c2, ss));
+      F3_TRY(f3_conv1d_bwd(&c1, ss));
     }
   }
   for (int si = 0; si < net->nstreams; ++si) {
-    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, s));
+    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si)));
     if (getenv("F3_DEBUG_BWD_STOP") && si == atoi(getenv("F3_DEBUG_BWD_STOP"))) break;
   }
+  F3_TRY(br.join());
   return F3_OK;
 }
 
