@@ -20,7 +20,7 @@ EXPORTS = (
     "f3_net_buffer_count", "f3_net_counter_count", "f3_net_workspace_bytes", "f3_net_forward",
     "f3_net_loss", "f3_net_backward", "f3_rmsprop_step", "f3_conv_forward", "f3_status_string",
     "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_graph_mix_forward",
-    "f3_graph_mix_backward",
+    "f3_graph_mix_backward", "f3_net_backward_phase", "f3_net_grad_split",
 )
 
 F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE = 0, 1001, 1002, 1003, 1004
@@ -57,6 +57,8 @@ def lib():
         "f3_net_forward": (I, [P, I, I, P, P, P, P, P, P, P, P]),
         "f3_net_loss": (I, [P, I, P, P, P, P, P]),
         "f3_net_backward": (I, [P, I, P, P, P, P, P]),
+        "f3_net_backward_phase": (I, [P, I, P, P, P, P, I, P]),
+        "f3_net_grad_split": (I64, [P]),
         "f3_rmsprop_step": (I, [P, P, P, I64, F, F, F, F, P]),
         "f3_conv_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_status_string": (ctypes.c_char_p, [I]),

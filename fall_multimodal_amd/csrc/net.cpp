@@ -30,7 +30,15 @@ struct Entry {
   int kind;
   std::vector<int64_t> shape;
   int64_t offset, numel;
+  int phase;  // params: backward phase that finalises the gradient (1 = head side, 2 = input side)
 };
+
+// Backward runs in two phases so DP can all-reduce the first phase's gradients while the
+// second computes: phase 1 = head, sensor branch and skeleton layers >= kSplitLayer;
+// phase 2 = skeleton layers < kSplitLayer and data_bn. Parameter OFFSETS in the flat buffer
+// are assigned phase-1-first (state_dict ORDER is unchanged), so each phase's gradients
+// form one contiguous range.
+constexpr int kSplitLayer = 4;
 
 struct BnIdx {
   int w = -1, b = -1, rm = -1, rv = -1, nbt = -1, C = 0;
@@ -88,10 +96,13 @@ struct f3_net {
   int fc_w = -1, fc_b = -1;
   int K, V;
 
+  int cur_phase = 1;
+  int64_t nparam_phase1 = 0;
   int add(const std::string& name, int kind, std::vector<int64_t> shape) {
     Entry e;
     e.name = name;
     e.kind = kind;
+    e.phase = cur_phase;
     e.shape = shape;
     e.numel = 1;
     for (auto d : shape) e.numel *= d;
@@ -100,6 +111,17 @@ struct f3_net {
     *ctr += e.numel;
     entries.push_back(e);
     return (int)entries.size() - 1;
+  }
+  void finalize_offsets() {
+    int64_t off = 0;
+    for (int ph = 1; ph <= 2; ++ph) {
+      for (auto& e : entries)
+        if (e.kind == F3_ENTRY_PARAM && e.phase == ph) {
+          e.offset = off;
+          off += e.numel;
+        }
+      if (ph == 1) nparam_phase1 = off;
+    }
   }
   BnIdx add_bn(const std::string& p, int C) {
     BnIdx b;
@@ -117,6 +139,7 @@ struct f3_net {
     s.motion = motion;
     s.T = motion ? cfg.frames - 1 : cfg.frames;
     s.A = add(pre + "A", F3_ENTRY_BUFFER, {K, V, V});
+    cur_phase = 2;
     s.dbn = add_bn(pre + "data_bn", cin * V);
     int T = s.T;
     for (int i = 0; i < 7; ++i) {
@@ -130,6 +153,7 @@ struct f3_net {
       T = L.T_out;
       const int ci = L.cin, co = L.cout;
       const std::string p = pre + layers + "." + std::to_string(i) + ".";
+      cur_phase = i >= kSplitLayer ? 1 : 2;
       L.gcn_w = add(p + "gcn.conv.weight", F3_ENTRY_PARAM, {K * co, ci, 1, 1});
       L.gcn_b = add(p + "gcn.conv.bias", F3_ENTRY_PARAM, {K * co});
       L.bn1 = add_bn(p + "tcn.0", co);
@@ -148,7 +172,11 @@ struct f3_net {
       L.ca_w2 = add(q + "4.weight", F3_ENTRY_PARAM, {co, co / 4, 1, 1});
       L.ca_b2 = add(q + "4.bias", F3_ENTRY_PARAM, {co});
     }
-    for (int i = 0; i < 7; ++i) s.L[i].edge = add(pre + "edge_importance." + std::to_string(i), F3_ENTRY_PARAM, {K, V, V});
+    for (int i = 0; i < 7; ++i) {
+      cur_phase = i >= kSplitLayer ? 1 : 2;
+      s.L[i].edge = add(pre + "edge_importance." + std::to_string(i), F3_ENTRY_PARAM, {K, V, V});
+    }
+    cur_phase = 1;
     if (num_class > 0) {
       s.cls_w = add(pre + "cls.weight", F3_ENTRY_PARAM, {num_class, 256, 1, 1});
       s.cls_b = add(pre + "cls.bias", F3_ENTRY_PARAM, {num_class});
@@ -536,14 +564,17 @@ bool debug_stop(int si, int l) {
   return a == si && b == l;
 }
 
-int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s) {
+// Backward of layers l_hi..l_lo (descending); data_bn after layer 0. Layer l writes its
+// input gradient to W.dx[(6-l)&1] and reads layer l+1's from W.dx[(5-l)&1].
+int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
+                    int l_hi, int l_lo) {
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V;
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
-  const float* dout = nullptr;
-  int pp = 0;
-  for (int l = 6; l >= 0; --l) {
+  const float* dout = l_hi == 6 ? nullptr : W.dx[(5 - l_hi) & 1];
+  int pp = (6 - l_hi) & 1;
+  for (int l = l_hi; l >= l_lo; --l) {
     const LayerIdx& L = S.L[l];
     LayerWs& X = W.L[l];
     const int C = L.cout, Ci = L.cin, Ti = L.T_in, To = L.T_out;
@@ -632,6 +663,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     dout = dx;
     pp ^= 1;
   }
+  if (l_lo > 0) return F3_OK;
   DataBnArgs d;
   std::memset(&d, 0, sizeof(d));
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
@@ -816,6 +848,7 @@ int f3_net_create(const f3_config* cfg, f3_net** out) {
       if (nb) { add_fc(); add_sensor(); } else { add_sensor(); add_fc(); }
     }
   }
+  n->finalize_offsets();
   *out = n;
   return F3_OK;
 }
@@ -918,10 +951,26 @@ int f3_net_loss(f3_net* net, int N, const float* out, const float* label, float*
 
 int f3_net_backward(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
                     void* stream) {
-  if (!net || !params || !dout || !grads || !workspace || N < 2) return F3_EINVAL;
+  return f3_net_backward_phase(net, N, params, dout, grads, workspace, 0, stream);
+}
+
+int64_t f3_net_grad_split(const f3_net* net) { return net ? net->nparam_phase1 : 0; }
+
+int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
+                          int phase, void* stream) {
+  if (!net || !params || !grads || !workspace || N < 2 || phase < 0 || phase > 2) return F3_EINVAL;
+  if (phase != 2 && !dout) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   Ws w = plan(*net, N, (char*)workspace);
   Ptrs q{*net, params, nullptr, nullptr, grads};
+  if (phase == 2) {
+    Branches br{*net, s, ensure_parallel(*net, s)};
+    F3_TRY(br.fork());
+    for (int si = 0; si < net->nstreams; ++si)
+      F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), kSplitLayer - 1, 0));
+    F3_TRY(br.join());
+    return F3_OK;
+  }
   if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
   if (hipMemsetAsync(w.zb0, 0, w.zb1 - w.zb0, s) != hipSuccess) return F3_EHIP;
   HeadArgs h;
@@ -949,7 +998,7 @@ int f3_net_backward(f3_net* net, int N, const float* params, const float* dout, 
     }
   }
   for (int si = 0; si < net->nstreams; ++si) {
-    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si)));
+    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), 6, phase == 1 ? kSplitLayer : 0));
     if (getenv("F3_DEBUG_BWD_STOP") && si == atoi(getenv("F3_DEBUG_BWD_STOP"))) break;
   }
   F3_TRY(br.join());

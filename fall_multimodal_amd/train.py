@@ -1,12 +1,15 @@
 """Fused training step: forward -> soft-target CE -> backward -> (all-reduce) -> RMSprop.
 
 This is the reference's inner loop body (Multimodal_Fall3/model/main.py:97-132; notebook
-GSTCAN_HAR_conv_10kfold.ipynb:1103-1116) as four native calls on one HIP stream with every
-buffer preallocated, so it can be captured once into a HIP graph and replayed per batch.
+GSTCAN_HAR_conv_10kfold.ipynb:1103-1116) as native calls on one HIP stream with every
+buffer preallocated, so it can be captured into HIP graphs and replayed per batch.
 
-Data parallel: one process per GPU; gradients live in ONE flat fp32 buffer, all-reduced
-(sum) over RCCL and scaled by 1/world inside the RMSprop kernel. BatchNorm statistics stay
-per-rank (the reference's per-device batch semantics).
+Data parallel: one process per GPU. Gradients live in ONE flat fp32 buffer whose layout
+puts the parameters the first backward phase finalises (head, sensor branch, skeleton
+layers 4-6; f3_net_grad_split) first. Their all-reduce (RCCL, sum) is issued as soon as
+phase 1 ends and runs on the process group's communication stream WHILE phase 2 (layers
+0-3, data_bn) computes; the remainder follows. 1/world is applied inside the RMSprop
+kernel. BatchNorm statistics stay per-rank (the reference's per-device batch semantics).
 """
 from __future__ import annotations
 
@@ -17,8 +20,41 @@ import torch.distributed as dist
 from ._lib import check, lib, ptr, stream_handle
 
 
+class GradSync:
+    """Two-bucket gradient all-reduce over a flat buffer: `head` = grads[:split] (final after
+    backward phase 1), `tail` = grads[split:]. Both are issued async on the group's
+    communication stream; `finish()` orders the caller's stream after them."""
+
+    def __init__(self, grads: torch.Tensor, split: int, group=None):
+        self.grads, self.split, self.group = grads, int(split), group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self._work = []
+
+    def _reduce(self, t):
+        if t.numel():
+            self._work.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def start_head(self):
+        if self.world > 1:
+            self._reduce(self.grads[:self.split])
+
+    def start_tail(self):
+        if self.world > 1:
+            self._reduce(self.grads[self.split:])
+
+    def finish(self):
+        for w in self._work:
+            w.wait()
+        self._work = []
+
+    def all(self):
+        self.start_head()
+        self.start_tail()
+        self.finish()
+
+
 class TrainStep:
-    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None, bucket_mb=None):
+    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None):
         self.model = model
         self.N = batch
         self.lr, self.alpha, self.eps = lr, alpha, eps
@@ -31,22 +67,32 @@ class TrainStep:
         self.dout = torch.empty_like(self.out)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.sync = GradSync(self.grads, lib().f3_net_grad_split(nat.h), process_group)
+        self.world = self.sync.world
         # expose the flat gradient through the usual .grad attributes
         for (name, shape, off), p in zip(model.param_views(), model.parameters()):
             p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
         self.graph = None
         self._static = None
 
-    # one step, eager
-    def forward_backward(self, skel, sensor, label):
+    # -- the pieces ------------------------------------------------------------
+    def forward_loss(self, skel, sensor, label):
         L = lib()
         st = stream_handle()
         m = self.model
         m.native_forward(skel, sensor, self.out, self.ws, True, st)
         check(L.f3_net_loss(m._native.h, self.N, ptr(self.out), ptr(label), ptr(self.loss), ptr(self.dout), st),
               "fall3 loss")
-        m.native_backward(self.N, self.dout, self.grads, self.ws, st)
+
+    def backward_phase(self, phase):
+        m = self.model
+        check(lib().f3_net_backward_phase(m._native.h, self.N, ptr(m.flat_parameters()), ptr(self.dout),
+                                          ptr(self.grads), ptr(self.ws), phase, stream_handle()),
+              f"fall3 backward phase {phase}")
+
+    def forward_backward(self, skel, sensor, label):
+        self.forward_loss(skel, sensor, label)
+        self.backward_phase(0)
 
     def optimizer_step(self):
         scale = 1.0 / self.world
@@ -55,33 +101,47 @@ class TrainStep:
               "rmsprop")
 
     def allreduce(self):
+        self.sync.all()
+
+    # -- one step ----------------------------------------------------------------
+    def _eager(self, skel, sensor, label):
+        self.forward_loss(skel, sensor, label)
         if self.world > 1:
-            dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.pg)
+            self.backward_phase(1)
+            self.sync.start_head()       # overlaps phase 2
+            self.backward_phase(2)
+            self.sync.start_tail()
+            self.sync.finish()
+        else:
+            self.backward_phase(0)
+        self.optimizer_step()
 
     def __call__(self, skel, sensor, label):
-        if self.graph is not None:
-            s = self._static
-            if skel is not None and skel.data_ptr() != s[0].data_ptr():
-                s[0].copy_(skel)
-            if sensor is not None and sensor.data_ptr() != s[1].data_ptr():
-                s[1].copy_(sensor)
-            if label.data_ptr() != s[2].data_ptr():
-                s[2].copy_(label)
-            self.graph[0].replay()
-            self.allreduce()
-            if self.graph[1] is not None:
-                self.graph[1].replay()
-            else:
-                self.optimizer_step()
+        if self.graph is None:
+            self._eager(skel, sensor, label)
             return self.loss
-        self.forward_backward(skel, sensor, label)
-        self.allreduce()
-        self.optimizer_step()
+        s = self._static
+        if skel is not None and skel.data_ptr() != s[0].data_ptr():
+            s[0].copy_(skel)
+        if sensor is not None and sensor.data_ptr() != s[1].data_ptr():
+            s[1].copy_(sensor)
+        if label.data_ptr() != s[2].data_ptr():
+            s[2].copy_(label)
+        g_head, g_tail, g_opt = self.graph
+        g_head.replay()
+        if g_tail is not None:
+            self.sync.start_head()       # RCCL on the comm stream, concurrent with phase 2
+            g_tail.replay()
+            self.sync.start_tail()
+            self.sync.finish()
+        g_opt.replay()
         return self.loss
 
     def capture(self, skel, sensor, label, warmup=2):
-        """Capture forward+loss+backward (and the optimizer) into HIP graphs; the given
-        tensors become the static inputs (later calls copy new batches into them)."""
+        """Capture the step into HIP graphs; the given tensors become the static inputs
+        (later calls copy new batches into them). world == 1: [fwd+loss+bwd], [RMSprop].
+        world > 1: [fwd+loss+bwd phase 1], [bwd phase 2], [RMSprop], with the two all-reduce
+        buckets issued between replays."""
         self._static = (skel, sensor, label)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -90,10 +150,19 @@ class TrainStep:
                 self.forward_backward(skel, sensor, label)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            self.forward_backward(skel, sensor, label)
-        g2 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g2):
+        g_head = torch.cuda.CUDAGraph()
+        g_tail = None
+        if self.world > 1:
+            with torch.cuda.graph(g_head):
+                self.forward_loss(skel, sensor, label)
+                self.backward_phase(1)
+            g_tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_tail):
+                self.backward_phase(2)
+        else:
+            with torch.cuda.graph(g_head):
+                self.forward_backward(skel, sensor, label)
+        g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_opt):
             self.optimizer_step()
-        self.graph = (g1, g2)
+        self.graph = (g_head, g_tail, g_opt)

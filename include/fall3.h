@@ -86,6 +86,15 @@ int f3_net_loss(f3_net* net, int batch, const float* out, const float* label, fl
 int f3_net_backward(f3_net* net, int batch, const float* params, const float* dout, float* grads,
                     void* workspace, void* stream);
 
+/* The same backward in two phases, for overlapping the data-parallel gradient all-reduce
+ * with compute: phase 1 = zero grads, head, sensor branch and skeleton layers 4-6 (their
+ * gradients, params[0 .. f3_net_grad_split) in the flat buffer, are final when it ends);
+ * phase 2 = skeleton layers 0-3 and data_bn (the rest). phase 0 = both (f3_net_backward).
+ * Parameter offsets are laid out phase-1-first; state_dict order is unchanged. */
+int f3_net_backward_phase(f3_net* net, int batch, const float* params, const float* dout, float* grads,
+                          void* workspace, int phase, void* stream);
+int64_t f3_net_grad_split(const f3_net* net);
+
 /* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
  * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):
  * sq = alpha*sq + (1-alpha)*g^2 ; p -= lr*g/(sqrt(sq)+eps). */

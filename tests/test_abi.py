@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 import torch  # noqa: F401  (shared HIP runtime before the CDLL)
 
@@ -80,3 +81,29 @@ def test_bad_precision_rejected():
     from fall_multimodal_amd.model import NativeNet, NetSpec
     with pytest.raises(ValueError):
         NativeNet(NetSpec(precision="fp8"), 3, 14)
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: f"{s.model}-{s.layout}-{s.naming}-{s.sensor}")
+def test_param_offsets_tile_flat_buffer_phase1_first(spec):
+    """Parameter offsets tile [0, nparam) exactly; the gradients final after backward phase 1
+    (head, sensor, skeleton layers >= 4 and their edge_importance) occupy [0, grad_split)."""
+    import fall_multimodal_amd._lib as L
+    from fall_multimodal_amd.graph import STRATEGY_PARTITIONS
+    from fall_multimodal_amd.model import NativeNet, NetSpec
+    ns = NetSpec(model=spec.model, layout=spec.layout, strategy=spec.strategy, num_class=spec.num_class,
+                 in_channels=spec.in_channels, sensor=spec.sensor, sensor_dim=spec.sensor_dim,
+                 sensor_classes=spec.sensor_classes, softmax_output=spec.softmax_output, naming=spec.naming)
+    V = 18 if spec.layout == "coco_mmpose" else 14
+    net = NativeNet(ns, STRATEGY_PARTITIONS[spec.strategy], V)
+    split = L.lib().f3_net_grad_split(net.h)
+    spans = sorted((off, off + int(np.prod(sh)), n) for n, kind, sh, off in net.entries if kind == L.ENTRY_PARAM)
+    pos = 0
+    for a, b, n in spans:
+        assert a == pos, n
+        pos = b
+    assert pos == net.nparam
+    assert 0 < split <= net.nparam
+    for a, b, n in spans:
+        m = re.search(r"(?:st_gc[a]?n_networks|edge_importance)\.(\d+)", n)
+        phase1 = (m is None and "data_bn" not in n) or (m is not None and int(m.group(1)) >= 4)
+        assert (b <= split) == phase1, n
