@@ -429,7 +429,7 @@ int f3_conv_wgrad(const WgradArgs* args, int pro, hipStream_t s) {
   if (pro && a.g.Kc > 256) return F3_EINVAL;
   const int gx = (a.g.Nc + BN - 1) / BN;
   const int gy = a.g.KT * ((a.g.Kc + BN - 1) / BN);
-  int splits = (2048 + gx * gy - 1) / (gx * gy);
+  int splits = (f3_wgrad_target_wgs() + gx * gy - 1) / (gx * gy);
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + BK - 1) / BK) * BK;
   if (rps < 4 * BK) rps = 4 * BK;

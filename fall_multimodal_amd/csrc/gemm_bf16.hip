@@ -506,7 +506,7 @@ int f3_conv_wgrad_bf16(const WgradArgs* args, int pro, hipStream_t s) {
   const int BJ = big ? 128 : 64, BI = big ? 128 : 64;
   const int gx = (a.g.Nc + BJ - 1) / BJ;
   const int gy = a.g.KT * ((a.g.Kc + BI - 1) / BI);
-  int splits = (2048 + gx * gy - 1) / (gx * gy);
+  int splits = (f3_wgrad_target_wgs() + gx * gy - 1) / (gx * gy);
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + HBK - 1) / HBK) * HBK;
   if (rps < 4 * HBK) rps = 4 * HBK;

@@ -59,6 +59,18 @@ struct WgradArgs {
 
 }  // namespace f3
 
+// Weight-gradient split-K sizing: target number of workgroups per launch. Each workgroup
+// adds its whole output tile with float atomics (executed at the memory side, ~1.3 TB/s
+// chip-wide), so more splits = more atomic traffic; F3_WGRAD_WGS overrides (tuning).
+inline int f3_wgrad_target_wgs() {
+  static const int v = [] {
+    const char* e = getenv("F3_WGRAD_WGS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 512;
+  }();
+  return v;
+}
+
 int f3_conv_gemm(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
 int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);
 int f3_conv_gemm_bf16(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);

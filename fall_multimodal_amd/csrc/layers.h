@@ -36,7 +36,9 @@ struct MixArgs {
   float* dx;             // bwd out
   float* dA;             // bwd accumulate [K][V][V]
   int accumulate;
+  float* part;           // bwd scratch [kMixParts][K*V*V] (MFMA path)
 };
+constexpr int kMixParts = 1024;
 
 struct GcnBiasBwdArgs {
   int K, V, C;

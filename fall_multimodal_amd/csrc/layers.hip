@@ -304,10 +304,15 @@ __global__ __launch_bounds__(256) void mix_dx_mfma_kernel(MixArgs a) {
   }
 }
 
+// dA partials: each workgroup reduces its 4 waves in LDS and writes ONE row of
+// part[gridDim.x][K*V*V]; mix_dA_reduce adds the rows into dA. (Global float atomics run at
+// the memory side and crawl when every workgroup hits the same few rows.)
 __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
+  __shared__ float red[1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, KVV = KV * V;
+  for (int i = threadIdx.x; i < KVV; i += 256) red[i] = 0.f;
   const int ctiles = Cin / 16;
   const long long items = (long long)a.frames * ctiles;
   f32x4 acc[2][4];
@@ -337,6 +342,7 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x4(xa[mt][s], zb[nt][s], acc[mt][nt]);
   }
+  __syncthreads();
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -348,9 +354,28 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
         const int wk = 16 * nt + fr;
         if (wk >= KV) continue;
         const int w = wk / K, k = wk - w * K;
-        atomic_add_f(a.dA + (k * V + v) * V + w, acc[mt][nt][r]);
+        atomicAdd(&red[(k * V + v) * V + w], acc[mt][nt][r]);  // LDS
       }
     }
+  __syncthreads();
+  float* row = a.part + (size_t)blockIdx.x * KVV;
+  for (int i = threadIdx.x; i < KVV; i += 256) row[i] = red[i];
+}
+
+__global__ __launch_bounds__(256) void mix_dA_reduce_kernel(MixArgs a, int nparts) {
+  const int KVV = a.K * a.V * a.V;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= KVV) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int p = 0;
+  for (; p + 3 < nparts; p += 4) {
+    s0 += a.part[(size_t)p * KVV + i];
+    s1 += a.part[(size_t)(p + 1) * KVV + i];
+    s2 += a.part[(size_t)(p + 2) * KVV + i];
+    s3 += a.part[(size_t)(p + 3) * KVV + i];
+  }
+  for (; p < nparts; ++p) s0 += a.part[(size_t)p * KVV + i];
+  a.dA[i] += (s0 + s1) + (s2 + s3);
 }
 
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
@@ -887,8 +912,12 @@ int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
     const int grid = (int)std::min<long long>((items + 3) / 4, 8192);
     hipLaunchKernelGGL(mix_dx_mfma_kernel, dim3(grid), dim3(256), 0, s, *a);
     F3_LAUNCH_CHECK();
-    const int grid2 = (int)std::min<long long>((items + 3) / 4, 512);
+    if (!a->part) return F3_EINVAL;
+    const int grid2 = (int)std::min<long long>((items + 3) / 4, kMixParts);
     hipLaunchKernelGGL(mix_dA_mfma_kernel, dim3(grid2), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    const int KVV = a->K * a->V * a->V;
+    hipLaunchKernelGGL(mix_dA_reduce_kernel, dim3((KVV + 255) / 256), dim3(256), 0, s, *a, grid2);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }

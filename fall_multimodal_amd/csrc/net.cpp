@@ -244,6 +244,7 @@ struct StreamWs {
   BnWs dbn;
   LayerWs L[7];
   float *dh, *dres, *dv, *dg, *dZ, *dx[2], *dpool;
+  float* mixpart;  // graph-mix dA partials [kMixParts][K*V*V]
 };
 
 struct Ws {
@@ -373,6 +374,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     W.dx[0] = A.take<float>(maxMC);
     W.dx[1] = A.take<float>(maxMC);
     W.dpool = A.take<float>((size_t)N * 256);
+    W.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
   }
   if (net.has_sensor) {
     if (cnn) {
@@ -642,7 +644,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
-    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID;
+    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart;
     F3_TRY(f3_mix_bwd(&mx, s));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
@@ -1075,6 +1077,9 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
   std::memset(&m, 0, sizeof(m));
   m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = x; m.z = const_cast<float*>(dz);
   m.dx = dx; m.dA = dA; m.accumulate = 0;
+  static float* part = nullptr;  // test entry only: scratch kept for the process lifetime
+  if (!part && hipMalloc(&part, sizeof(float) * kMixParts * 1024) != hipSuccess) return F3_EHIP;
+  m.part = part;
   return f3_mix_bwd(&m, s);
 }
 
