@@ -58,6 +58,8 @@ def conv_roofline(dev, batch, V, precision):
     lib = L.lib()
     N, T, C, KT = batch, 8, 256, 9
     x = torch.randn(N, T, V, C, device=dev)
+    if precision == "bf16":  # the network's bf16 GEMM operand tensors are bf16 in HBM
+        x = x.to(torch.bfloat16)
     w = torch.randn(C, C, KT, device=dev) / 48.0
     b = torch.zeros(C, device=dev)
     out = torch.empty(N, T, V, C, device=dev)
@@ -82,7 +84,7 @@ def conv_roofline(dev, batch, V, precision):
     flop = 2.0 * M * C * (KT * C)
     achieved = flop / (ms * 1e-3) / 1e12
     peak = PEAK_MFMA_TFLOPS[precision]
-    return {"kernel": f"conv_gemm_{precision} (tcn 9x1, C=256, T=8, N={N}, V={V})", "bound": "mfma",
+    return {"kernel": f"{'igemm_bf16' if precision == 'bf16' else 'conv_gemm_f32'} (tcn 9x1, C=256, T=8, N={N}, V={V})", "bound": "mfma",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None,
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}

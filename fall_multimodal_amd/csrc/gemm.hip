@@ -423,7 +423,10 @@ int f3_conv_gemm(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
 }
 
 int f3_conv_wgrad(const WgradArgs* args, int pro, hipStream_t s) {
-  if (args->bf16) return f3_conv_wgrad_bf16(args, pro, s);
+  if (args->bf16) {
+    if (!pro && f3_wgrad_glds_ok(*args)) return f3_wgrad_glds_bf16(args, s);
+    return f3_conv_wgrad_bf16(args, pro, s);
+  }
   WgradArgs a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (pro && a.g.Kc > 256) return F3_EINVAL;

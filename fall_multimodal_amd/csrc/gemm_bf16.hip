@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void conv_gemm_bf16(ConvGemmArgs a) {
   const int m0 = blockIdx.x * BM, j0 = blockIdx.y * BN;
   const int Ktot = g.KT * g.Kc;
   const int nchunk = (Ktot + HBK - 1) / HBK;
-  const bool fastA = (g.Kc % HBK) == 0 && (g.lda % 4) == 0;
+  const bool fastA = (g.Kc % HBK) == 0 && (g.lda % (a.inb ? 8 : 4)) == 0;
   const bool fastB = (Ktot % 8) == 0;
   const unsigned short* wb = reinterpret_cast<const unsigned short*>(a.wb);
 
@@ -100,7 +100,19 @@ __global__ __launch_bounds__(256) void conv_gemm_bf16(ConvGemmArgs a) {
     if (fastA) {
       const int dt = k0 / g.Kc, i = k0 - dt * g.Kc;
       const int r = arow ? src_row_b(an, at, av, dt, g) : -1;
-      if (r >= 0) {
+      if (r >= 0 && a.inb) {  // bf16 activations (alignment: lda % 8 == 0, checked by the launcher)
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(a.inb + (size_t)r * g.lda + i);
+#pragma unroll
+        for (int q = 0; q < KPT / 8; ++q) {
+          const bf16x8 v = p[q];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x = (float)v[e];
+            if (PRO) x = fmaxf(x * pro_sc[i + 8 * q + e] + pro_sh[i + 8 * q + e], 0.f);
+            ra[8 * q + e] = x;
+          }
+        }
+      } else if (r >= 0) {
         const f32x4* p = reinterpret_cast<const f32x4*>(a.in + (size_t)r * g.lda + i);
 #pragma unroll
         for (int q = 0; q < KPT / 4; ++q) {
@@ -125,7 +137,8 @@ __global__ __launch_bounds__(256) void conv_gemm_bf16(ConvGemmArgs a) {
           const int dt = k / g.Kc, i = k - dt * g.Kc;
           const int r = src_row_b(an, at, av, dt, g);
           if (r >= 0) {
-            x = a.in[(size_t)r * g.lda + i];
+            x = a.inb ? (float)reinterpret_cast<const __bf16*>(a.inb)[(size_t)r * g.lda + i]
+                      : a.in[(size_t)r * g.lda + i];
             if (PRO) x = fmaxf(x * pro_sc[i] + pro_sh[i], 0.f);
           }
         }
@@ -310,6 +323,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16(WgradArgs a) {
   const int cy = (tid & 7) * VPY, cx = (tid & 7) * VPX;
   const bool fastY = (a.ldy % 4) == 0 && (g.Nc % 4) == 0;
   const bool fastX = (g.lda % 4) == 0 && (g.Kc % 4) == 0;
+  const bool fastYb = (a.ldy % 8) == 0 && (g.Nc % 8) == 0;
+  const bool fastXb = (g.lda % 8) == 0 && (g.Kc % 8) == 0;
   float ry[VPY], rx[VPX], dbp[VPY];
 #pragma unroll
   for (int e = 0; e < VPY; ++e) dbp[e] = 0.f;
@@ -318,7 +333,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16(WgradArgs a) {
     const int m = r0 + lrow;
     const bool ok = m < r_end;
     const int j = j0 + cy;
-    if (ok && fastY && j + VPY <= g.Nc) {
+    if (a.dyb) {  // bf16 dy
+      const __bf16* yb = reinterpret_cast<const __bf16*>(a.dyb);
+      if (ok && fastYb && j + VPY <= g.Nc) {
+#pragma unroll
+        for (int q = 0; q < VPY / 8; ++q) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(yb + (size_t)m * a.ldy + j + 8 * q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ry[8 * q + e] = (float)v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VPY; ++e) ry[e] = (ok && j + e < g.Nc) ? (float)yb[(size_t)m * a.ldy + j + e] : 0.f;
+      }
+    } else if (ok && fastY && j + VPY <= g.Nc) {
 #pragma unroll
       for (int q = 0; q < VPY / 4; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(a.dy + (size_t)m * a.ldy + j + 4 * q);
@@ -339,7 +367,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16(WgradArgs a) {
       r = src_row_b(n, t, v, dt, g);
     }
     const int i = i0 + cx;
-    if (r >= 0 && fastX && i + VPX <= g.Kc) {
+    if (a.inb) {  // bf16 input rows
+      const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+      if (r >= 0 && fastXb && i + VPX <= g.Kc) {
+#pragma unroll
+        for (int q = 0; q < VPX / 8; ++q) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(xb + (size_t)r * g.lda + i + 8 * q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x = (float)v[e];
+            if (PRO) x = fmaxf(x * pro_sc[i + 8 * q + e] + pro_sh[i + 8 * q + e], 0.f);
+            rx[8 * q + e] = x;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VPX; ++e) {
+          float x = 0.f;
+          if (r >= 0 && i + e < g.Kc) {
+            x = (float)xb[(size_t)r * g.lda + i + e];
+            if (PRO) x = fmaxf(x * pro_sc[i + e] + pro_sh[i + e], 0.f);
+          }
+          rx[e] = x;
+        }
+      }
+    } else if (r >= 0 && fastX && i + VPX <= g.Kc) {
 #pragma unroll
       for (int q = 0; q < VPX / 4; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(a.in + (size_t)r * g.lda + i + 4 * q);
@@ -491,6 +543,7 @@ static int launch_gemm_bf16(const ConvGemmArgs& a, int pro, int epi, hipStream_t
 int f3_conv_gemm_bf16(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
+  if (a.inb && !pro && f3_igemm_ok(a)) return f3_igemm_bf16(args, epi, s);
   if (pro && a.g.Kc > 256) return F3_EINVAL;
   if (!a.wb) return F3_EINVAL;
   // wide output channels: 128x128 tiles; narrow (64 / small gcn dgrad): 128x64

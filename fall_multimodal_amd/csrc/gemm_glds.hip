@@ -1,0 +1,490 @@
+// bf16 implicit-GEMM temporal convolution with bf16 activations in HBM, staged by LDS-DMA
+// (global_load_lds_dwordx4) — the throughput form of conv_gemm for the bf16 mode.
+//
+//   Out[m][j] = sum_{dt,i} In[src(m,dt)][i] * W[j][dt*Kc+i]      (fwd, or dgrad via the
+//                                                                  transposed row map)
+// In (bf16, row stride lda) is the GEMM operand tensor its producer wrote in bf16 (the
+// tcn input is the materialised relu(bn1(g)), so there is no prologue here). W is the
+// prep-packed bf16 operand [Nc][KT*Kc]. Requirements: Kc % 64 == 0 (a 64-deep k step never
+// straddles two taps), lda % 8 == 0.
+//
+// Tile 128 x BN (BN = 128 or 64) x 64, 4 waves in 2x2 (each 64 x BN/2 = 4 x BN/32 MFMA
+// 16x16x32 tiles), two LDS stages. Each stage is filled by 1-KiB LDS-DMA wave-instructions
+// (8 rows x 128 B); a row's 16-B chunks are stored XOR-swizzled (chunk c of row r at
+// c ^ ((r>>1)&7)) through the per-lane SOURCE address, which makes the 16-lane ds_read_b128
+// fragment reads conflict-free. The implicit-GEMM row gather is also in the source address:
+// a row outside the clip (temporal zero padding) or past M reads a zero line.
+// Epilogues as conv_gemm_f32 (bias, graph-mixed bias, BN statistics, channel-attention
+// pooling, ReLU mask + BN-backward sums, accumulate).
+#include "common.h"
+#include "kernels.h"
+
+namespace f3 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int G_BM = 128, G_BK = 64;
+
+F3_DEV f32x4 mfma_bf16x(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
+F3_DEV int g_src_row(int n, int t, int v, int dt, const ConvGeom& g) {
+  int ti;
+  if (!g.transposed) {
+    ti = t * g.S + dt - g.P;
+    if (ti < 0 || ti >= g.T_in) return -1;
+  } else {
+    const int num = t + g.P - dt;
+    if (num < 0 || (num % g.S) != 0) return -1;
+    ti = num / g.S;
+    if (ti >= g.T_in) return -1;
+  }
+  return (n * g.T_in + ti) * g.V + v;
+}
+
+F3_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// bijective XCD-aware remap: consecutive logical tiles land on one XCD (shared A panels)
+F3_DEV int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <int EPI, int WN>
+__global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
+  constexpr int BM = G_BM, BN = 32 * WN;
+  constexpr int A_BYTES = BM * G_BK * 2, B_BYTES = BN * G_BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / 4, B_INSTR = B_BYTES / 1024 / 4;  // per wave
+  // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code): two
+  // stages, then the epilogue coefficient tables; the reductions reuse stage 0.
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 4 * BN * 4];
+  float* epi_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
+  float* epi_sh = epi_sc + BN;
+  float* epi_mu = epi_sh + BN;
+  float* epi_rs = epi_mu + BN;
+
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (g.Nc + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / ntn) * BM, j0 = (tile % ntn) * BN;
+  const int Ktot = g.KT * g.Kc;
+  const int nchunk = Ktot / G_BK;
+  const unsigned short* in = a.inb;
+  const unsigned short* wb = a.wb;
+
+  if (EPI & EPI_RELUMASK) {
+    for (int t = tid; t < BN; t += 256) {
+      if (j0 + t < g.Nc) {
+        float sc, sh, mu, rs;
+        bn_coeff(a.epi_bn, j0 + t, sc, sh, mu, rs);
+        epi_sc[t] = sc; epi_sh[t] = sh; epi_mu[t] = mu; epi_rs[t] = rs;
+      }
+    }
+  }
+
+  // per-lane staging rows (fixed for the whole k loop)
+  const int sub = lane >> 3, pch = lane & 7;
+  int a_n[A_INSTR], a_t[A_INSTR], a_v[A_INSTR], a_c[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int rr = (wave * A_INSTR + i) * 8 + sub;
+    const int m = m0 + rr;
+    a_c[i] = swz(rr, pch);
+    if (m < g.M) {
+      const int nt = m / g.V;
+      a_v[i] = m - nt * g.V;
+      a_n[i] = nt / g.T_out;
+      a_t[i] = nt - a_n[i] * g.T_out;
+    } else {
+      a_n[i] = -1; a_t[i] = 0; a_v[i] = 0;
+    }
+  }
+  const unsigned short* b_row[B_INSTR];
+  int b_c[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int rb = (wave * B_INSTR + i) * 8 + sub;
+    const int j = j0 + rb;
+    b_c[i] = swz(rb, pch);
+    b_row[i] = j < g.Nc ? wb + (size_t)j * Ktot : nullptr;
+  }
+
+  auto stage = [&](int t, int buf) {
+    const int k0 = t * G_BK;
+    const int dt = k0 / g.Kc, i0 = k0 - dt * g.Kc;
+    char* sa = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int r = a_n[i] >= 0 ? g_src_row(a_n[i], a_t[i], a_v[i], dt, g) : -1;
+      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + i0 + a_c[i] * 8 : a.zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sa + (wave * A_INSTR + i) * 1024), 16, 0, 0);
+    }
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) {
+      const unsigned short* src = b_row[i] ? b_row[i] + k0 + b_c[i] * 8 : a.zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sb + (wave * B_INSTR + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave >> 1, wj = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 acc[4][WN];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < WN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nchunk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nchunk) stage(t + 1, buf ^ 1);
+    const char* sa = smem + buf * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4], fb[WN];
+      const int c = ks * 4 + fg;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int r = wm * 64 + x * 16 + fr;
+        fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int y = 0; y < WN; ++y) {
+        const int r = wj * 16 * WN + y * 16 + fr;
+        fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  float* red = reinterpret_cast<float*>(smem);   // [2][2][BN]  (stage 0 is free now)
+  float* gred = red + 4 * BN;                    // [2][2][BN]
+  float ssum[WN], ssq[WN], gap0[WN], gap1[WN];
+#pragma unroll
+  for (int y = 0; y < WN; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
+  const int TV = g.T_out * g.V;
+  const int nlo = m0 / TV;
+#pragma unroll
+  for (int y = 0; y < WN; ++y) {
+    const int jl = wj * 16 * WN + y * 16 + fr;
+    const int j = j0 + jl;
+    const bool jok = j < g.Nc;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + x * 16 + fg * 4 + r;
+        if (!jok || m >= g.M) continue;
+        float v = acc[x][y][r];
+        if (EPI & EPI_BIAS) v += a.bias[j];
+        if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
+        if (EPI & EPI_RELUMASK) {
+          const float gv = a.aux[(size_t)m * a.ldaux + j];
+          if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
+          const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
+          ssum[y] += v;
+          ssq[y] += v * xh;
+        } else if (EPI & EPI_STATS) {
+          ssum[y] += v;
+          ssq[y] += v * v;
+        }
+        if (EPI & EPI_GAP) {
+          const int n = m / TV;
+          if (n == nlo) gap0[y] += v;
+          else if (n == nlo + 1) gap1[y] += v;
+          else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
+        }
+        float* o = a.out + (size_t)m * g.ldo + j;
+        if (EPI & EPI_ADD) *o += v;
+        else *o = v;
+      }
+    }
+  }
+  if (EPI & (EPI_STATS | EPI_RELUMASK | EPI_GAP)) {
+#pragma unroll
+    for (int y = 0; y < WN; ++y) {
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        ssum[y] += __shfl_xor(ssum[y], o, 64);
+        ssq[y] += __shfl_xor(ssq[y], o, 64);
+        gap0[y] += __shfl_xor(gap0[y], o, 64);
+        gap1[y] += __shfl_xor(gap1[y], o, 64);
+      }
+    }
+    if (fg == 0) {
+#pragma unroll
+      for (int y = 0; y < WN; ++y) {
+        const int jl = wj * 16 * WN + y * 16 + fr;
+        red[(wm * 2 + 0) * BN + jl] = ssum[y];
+        red[(wm * 2 + 1) * BN + jl] = ssq[y];
+        gred[(wm * 2 + 0) * BN + jl] = gap0[y];
+        gred[(wm * 2 + 1) * BN + jl] = gap1[y];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < BN; t += 256) {
+      const int j = j0 + t;
+      if (j >= g.Nc) continue;
+      if (EPI & (EPI_STATS | EPI_RELUMASK)) {
+        atomic_add_d(a.st_sum + j, (double)(red[0 * BN + t] + red[2 * BN + t]));
+        atomic_add_d(a.st_sq + j, (double)(red[1 * BN + t] + red[3 * BN + t]));
+      }
+      if (EPI & EPI_GAP) {
+        const float s0 = gred[0 * BN + t] + gred[2 * BN + t];
+        const float s1 = gred[1 * BN + t] + gred[3 * BN + t];
+        atomic_add_f(a.gap + (size_t)nlo * g.Nc + j, s0);
+        if ((nlo + 1) * TV < g.M && s1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + j, s1);
+      }
+    }
+  }
+}
+
+}  // namespace f3
+
+using namespace f3;
+
+bool f3_igemm_ok(const ConvGemmArgs& a) {
+  return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0;
+}
+
+template <int WN>
+static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
+  const int tiles = ((a.g.M + G_BM - 1) / G_BM) * ((a.g.Nc + 32 * WN - 1) / (32 * WN));
+#define F3_ICASE(E)                                                              \
+  if (epi == (E)) {                                                             \
+    hipLaunchKernelGGL((igemm_bf16<(E), WN>), dim3(tiles), dim3(256), 0, s, a); \
+    F3_LAUNCH_CHECK();                                                           \
+    return F3_OK;                                                                \
+  }
+  F3_ICASE(EPI_BIASV | EPI_STATS)            // gcn forward
+  F3_ICASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
+  F3_ICASE(EPI_BIAS | EPI_STATS)             // residual forward
+  F3_ICASE(EPI_RELUMASK)                     // tcn dgrad
+  F3_ICASE(0)                                // gcn dgrad
+  F3_ICASE(EPI_ADD)                          // residual dgrad
+  F3_ICASE(EPI_BIAS)                         // plain conv (tests)
+#undef F3_ICASE
+  return F3_EINVAL;
+}
+
+int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
+  const ConvGemmArgs& a = *args;
+  if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
+  if (!f3_igemm_ok(a)) return F3_EINVAL;
+  if (a.g.Nc > 64) return launch_igemm<4>(a, epi, s);
+  return launch_igemm<2>(a, epi, s);
+}
+
+// ============================================================================
+// Weight gradient, bf16 operands by LDS-DMA:
+//   dW[j][dt*Kc+i] += sum_m dY[m][j] * In[src(m,dt)][i]
+// GEMM over k = rows m (64 per stage): both tiles are staged row-major [64 m][128 cols]
+// (1-KiB DMA pieces = 4 rows of 256 B, or 8 rows of 128 B for 64-wide tiles) and read as
+// MFMA operands with the gfx950 transposed LDS read ds_read_b64_tr_b16. 32-B units of a row
+// are XOR-swizzled (unit u of row r at u ^ f(r)) through the source address so each
+// half-wave tr read (8 rows x 32 B) covers all 64 banks once.
+// Output: WG_OUT_GCN -> the reference gcn layout directly; WG_OUT_CONV -> a packed
+// [Nc][KT*Kc] accumulator (contiguous i for the atomics) that f3_unpack_conv_grad moves
+// into the reference [Nc][Kc][KT] layout.
+// ============================================================================
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+template <int U>
+F3_DEV int wswz(int r) {  // unit permutation of row r (U 32-B units per row)
+  if (U == 8) return (r & 3) | (((r >> 3) & 1) << 2);
+  return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+}
+
+template <int TJ, int TI>  // tile widths: 128 or 64
+__global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
+  constexpr int UJ = TJ / 16, UI = TI / 16;         // 32-B units per row
+  constexpr int Y_BYTES = 64 * TJ * 2, X_BYTES = 64 * TI * 2, STAGE = Y_BYTES + X_BYTES;
+  constexpr int Y_INSTR = Y_BYTES / 1024 / 4, X_INSTR = X_BYTES / 1024 / 4;
+  constexpr int YRPI = 1024 / (TJ * 2), XRPI = 1024 / (TI * 2);  // rows per DMA piece
+  constexpr int WJ = TJ / 32, WI = TI / 32;          // MFMA tiles per wave (2x2 waves)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + TJ * 4];
+  float* dbs = reinterpret_cast<float*>(smem + 2 * STAGE);   // [TJ]
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = blockIdx.x * TJ;
+  const int itiles = (g.Kc + TI - 1) / TI;
+  const int dt = blockIdx.y / itiles;
+  const int i0 = (blockIdx.y - dt * itiles) * TI;
+  const int r_begin = blockIdx.z * a.rows_per_split;
+  const int r_end = min(g.M, r_begin + a.rows_per_split);
+  const bool do_db = a.db && blockIdx.y == 0;
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const __bf16* zero = reinterpret_cast<const __bf16*>(a.zero);
+
+  // staging lanes: piece rows and the logical column each lane fetches
+  const int ysub = lane / (TJ / 8), yph = lane % (TJ / 8);   // 16-B chunk index within the row
+  const int xsub = lane / (TI / 8), xph = lane % (TI / 8);
+  auto stage = [&](int r0, int buf) {
+    char* sy = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < Y_INSTR; ++i) {
+      const int rr = (wave * Y_INSTR + i) * YRPI + ysub;
+      const int m = r0 + rr;
+      const int lu = (yph >> 1) ^ wswz<UJ>(rr);
+      const int col = (lu * 2 + (yph & 1)) * 8;
+      const __bf16* src = (m < r_end && j0 + col < g.Nc) ? dyb + (size_t)m * a.ldy + j0 + col : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sy + (wave * Y_INSTR + i) * 1024), 16, 0, 0);
+    }
+    char* sx = sy + Y_BYTES;
+#pragma unroll
+    for (int i = 0; i < X_INSTR; ++i) {
+      const int rr = (wave * X_INSTR + i) * XRPI + xsub;
+      const int m = r0 + rr;
+      const int lu = (xph >> 1) ^ wswz<UI>(rr);
+      const int col = (lu * 2 + (xph & 1)) * 8;
+      int r = -1;
+      if (m < r_end && i0 + col < g.Kc) {
+        const int nt = m / g.V, v = m - nt * g.V, n = nt / g.T_out, t = nt - n * g.T_out;
+        r = g_src_row(n, t, v, dt, g);
+      }
+      const __bf16* src = r >= 0 ? xb + (size_t)r * g.lda + i0 + col : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sx + (wave * X_INSTR + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
+  // transposed fragment of a [64][cols] tile: lane (fg, fr) gets column c0+fr of rows
+  // kb+8fg .. kb+8fg+7 (kb = 0 or 32)
+  auto tr_frag = [&](const char* tile, int U, int c0, int kb) {
+    typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+    const int r_lo = kb + 8 * fg + tq, r_hi = r_lo + 4;
+    const int u = c0 >> 4;
+    const int R = U * 32;
+    const int f_lo = U == 8 ? wswz<8>(r_lo) : wswz<4>(r_lo);
+    const int f_hi = U == 8 ? wswz<8>(r_hi) : wswz<4>(r_hi);
+    const char* p0 = tile + r_lo * R + ((u ^ f_lo) * 32) + tp * 8;
+    const char* p1 = tile + r_hi * R + ((u ^ f_hi) * 32) + tp * 8;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+    s16x8_t v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x4 acc[WJ][WI];
+#pragma unroll
+  for (int x = 0; x < WJ; ++x)
+#pragma unroll
+    for (int y = 0; y < WI; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbp[WJ];
+#pragma unroll
+  for (int x = 0; x < WJ; ++x) dbp[x] = 0.f;
+
+  const int nst = r_end > r_begin ? (r_end - r_begin + 63) / 64 : 0;
+  if (nst > 0) {
+    stage(r_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < nst; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nst) stage(r_begin + (t + 1) * 64, buf ^ 1);
+    const char* sy = smem + buf * STAGE;
+    const char* sx = sy + Y_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[WJ], fb[WI];
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) fa[x] = tr_frag(sy, UJ, wm * 16 * WJ + x * 16, ks * 32);
+#pragma unroll
+      for (int y = 0; y < WI; ++y) fb[y] = tr_frag(sx, UI, wn * 16 * WI + y * 16, ks * 32);
+      if (do_db && wn == 0) {
+#pragma unroll
+        for (int x = 0; x < WJ; ++x)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dbp[x] += (float)fa[x][e];
+      }
+#pragma unroll
+      for (int x = 0; x < WJ; ++x)
+#pragma unroll
+        for (int y = 0; y < WI; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (do_db) {
+    // lane (fg, fr) holds column wm*16*WJ + x*16 + fr summed over its rows; add the 4 fg groups
+#pragma unroll
+    for (int x = 0; x < WJ; ++x) {
+      dbp[x] += __shfl_xor(dbp[x], 16, 64);
+      dbp[x] += __shfl_xor(dbp[x], 32, 64);
+    }
+    if (wn == 0 && fg == 0) {
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) dbs[wm * 16 * WJ + x * 16 + fr] = dbp[x];
+    }
+    __syncthreads();
+    for (int t = tid; t < TJ; t += 256)
+      if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
+  }
+  if (nst == 0) return;
+#pragma unroll
+  for (int x = 0; x < WJ; ++x) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = j0 + wm * 16 * WJ + x * 16 + fg * 4 + r;
+      if (j >= g.Nc) continue;
+#pragma unroll
+      for (int y = 0; y < WI; ++y) {
+        const int i = i0 + wn * 16 * WI + y * 16 + fr;
+        if (i >= g.Kc) continue;
+        size_t idx;
+        if (a.outmap == WG_OUT_GCN) {
+          const int k = i / a.gcn_cin, ci = i - k * a.gcn_cin;
+          idx = ((size_t)k * g.Nc + j) * a.gcn_cin + ci;
+        } else {  // packed [Nc][KT*Kc]
+          idx = (size_t)j * g.KT * g.Kc + (size_t)dt * g.Kc + i;
+        }
+        atomic_add_f(a.dw + idx, acc[x][y][r]);
+      }
+    }
+  }
+}
+
+bool f3_wgrad_glds_ok(const WgradArgs& a) {
+  return a.dyb && a.inb && a.zero && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && a.ldy % 8 == 0 && a.g.lda % 8 == 0;
+}
+
+// dW accumulation target: WG_OUT_GCN writes the reference layout; WG_OUT_CONV writes the
+// PACKED layout [Nc][KT*Kc] (caller unpacks with PREP_UNPACK_CONV).
+int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
+  WgradArgs a = *args;
+  if (a.g.M <= 0) return F3_OK;
+  if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;
+  const int gx = (a.g.Nc + TJ - 1) / TJ;
+  const int gy = a.g.KT * ((a.g.Kc + TI - 1) / TI);
+  int splits = (f3_wgrad_target_wgs() + gx * gy - 1) / (gx * gy);
+  int rps = (a.g.M + splits - 1) / splits;
+  rps = ((rps + 63) / 64) * 64;
+  if (rps < 256) rps = 256;
+  splits = (a.g.M + rps - 1) / rps;
+  a.rows_per_split = rps;
+  dim3 grid(gx, gy, splits);
+  if (TJ == 128 && TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 128>), grid, dim3(256), 0, s, a);
+  else if (TJ == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 64>), grid, dim3(256), 0, s, a);
+  else if (TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<64, 128>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_glds_bf16<64, 64>), grid, dim3(256), 0, s, a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}

@@ -29,7 +29,9 @@ struct ConvGemmArgs {
   ConvGeom g;
   const float* in;
   const float* w;     // packed [Nc][KT*Kc]
-  const unsigned short* wb;  // same, bf16; non-null selects the bf16 MFMA kernel
+  const unsigned short* wb;  // same, bf16; non-null selects the bf16 MFMA kernels
+  const unsigned short* inb; // bf16 activations (instead of `in`); with wb: LDS-DMA kernel when shapes allow
+  const unsigned short* zero;  // >= 16 zero bytes (rows outside the clip / tile for the LDS-DMA kernel)
   float* out;
   BnRef pro_bn;       // prologue: relu(bn(x)) on input channels
   const float* bias;
@@ -55,6 +57,9 @@ struct WgradArgs {
   BnRef pro_bn;
   int rows_per_split;
   int bf16;           // 1: bf16 MFMA (operands rounded to bf16, fp32 accumulate)
+  const unsigned short* dyb;  // bf16 dy (instead of dy)
+  const unsigned short* inb;  // bf16 input rows (instead of in)
+  const unsigned short* zero; // >= 16 zero bytes (LDS-DMA kernel)
 };
 
 }  // namespace f3
@@ -74,4 +79,8 @@ inline int f3_wgrad_target_wgs() {
 int f3_conv_gemm(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
 int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);
 int f3_conv_gemm_bf16(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
+bool f3_igemm_ok(const f3::ConvGemmArgs& a);
+int f3_igemm_bf16(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
+bool f3_wgrad_glds_ok(const f3::WgradArgs& a);
+int f3_wgrad_glds_bf16(const f3::WgradArgs* a, hipStream_t s);
 int f3_conv_wgrad_bf16(const f3::WgradArgs* a, int pro, hipStream_t s);

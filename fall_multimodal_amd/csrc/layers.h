@@ -4,7 +4,8 @@
 
 namespace f3 {
 
-enum : int { PREP_MUL = 0, PREP_PACK_CONV, PREP_PACK_CONV_T, PREP_PACK_GCN, PREP_PACK_GCN_T, PREP_GCN_BIAS, PREP_COPY };
+enum : int { PREP_MUL = 0, PREP_PACK_CONV, PREP_PACK_CONV_T, PREP_PACK_GCN, PREP_PACK_GCN_T, PREP_GCN_BIAS, PREP_COPY,
+              PREP_UNPACK_CONV };
 
 struct PrepJob {
   int type, n;
@@ -37,6 +38,7 @@ struct MixArgs {
   float* dA;             // bwd accumulate [K][V][V]
   int accumulate;
   float* part;           // bwd scratch [kMixParts][K*V*V] (MFMA path)
+  unsigned short* zb;    // fwd: write z as bf16 (bf16 mode GEMM operand) instead of fp32
 };
 constexpr int kMixParts = 1024;
 
@@ -65,6 +67,7 @@ struct BlockArgs {
   const float* att;      // channel attention [N][C]
   float* out;            // block output [M][C]
   float* pool;           // [N][C] mean over (T,V) or null
+  unsigned short* outb;  // optional bf16 copy of out (next block's residual-conv operand)
   // backward
   const float* dout;     // [M][C] or null when dout_nc is given
   const float* dout_nc;  // [N][C] gradient of the pooled mean (broadcast * inv_tv)
@@ -77,6 +80,8 @@ struct BlockArgs {
   const float* e;        // [N][C] dgap / TV
   float* dh;
   float* dres;           // dr (conv) or dx (identity)
+  unsigned short* dhb;   // bf16 mode: dh written as bf16 (GEMM operand) instead of fp32
+  unsigned short* dresb; // bf16 mode, conv residual: dr as bf16 instead of fp32
   float* dgamma2;
   float* dbeta2;
   float* dgammar;
@@ -93,7 +98,16 @@ struct BnBwdArgs {
   const float* dv;
   const float* g;
   float* dg;
-  float* G;              // [V][C]
+  float* G;              // [V][C] (accumulated from Gpart by a column reduction)
+  float* Gpart;          // [gridDim][V*C] per-workgroup partial rows
+  unsigned short* dgb;   // bf16 mode: dg as bf16 (GEMM operand) instead of fp32
+};
+
+struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the bf16 mode
+  int M, C;
+  BnRef bn;
+  const float* g;
+  unsigned short* u;
 };
 
 struct CaArgs {
@@ -162,6 +176,9 @@ int f3_block_out(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);
 int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
+int f3_bn_bwd_parts(int N, int TV);  // Gpart rows f3_bn_bwd_apply writes
+int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
+int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);  // out[c] += sum_r part[r][c]
 int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);
 int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);
 int f3_bn_running(const f3::BnRunTable& t, hipStream_t s);

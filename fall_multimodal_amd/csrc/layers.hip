@@ -13,6 +13,9 @@
 
 namespace f3 {
 
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
 // ----------------------------------------------------------------------------
 // prep: A_eff = A * E, gcn bias through the graph, weight packing  (one launch)
 // ----------------------------------------------------------------------------
@@ -32,6 +35,12 @@ __global__ void prep_kernel(PrepTable t) {
         const int I = j.d1, KT = j.d2;
         const int jj = e / (KT * I), r = e - jj * KT * I, dt = r / I, i = r - dt * I;
         val = j.s0[((size_t)jj * I + i) * KT + dt];
+        break;
+      }
+      case PREP_UNPACK_CONV: {  // packed weight gradient [J][KT*I] -> reference layout [J][I][KT]
+        const int I = j.d1, KT = j.d2;
+        const int jj = e / (I * KT), r = e - jj * I * KT, i = r / KT, dt = r - i * KT;
+        val = j.s0[(size_t)jj * KT * I + (size_t)dt * I + i];
         break;
       }
       case PREP_PACK_CONV_T: {  // dgrad operand: dst [I][KT*J] (k = dt*J + j)
@@ -160,7 +169,8 @@ __global__ __launch_bounds__(256) void mix_fwd_kernel(MixArgs a) {
       const int ci = o % a.Cin, wk = o / a.Cin, k = wk % a.K, w = wk / a.K;
       float acc = 0.f;
       for (int v = 0; v < a.V; ++v) acc += As[(k * a.V + v) * a.V + w] * xs[v * a.Cin + ci];
-      a.z[(size_t)f * outs + o] = acc;
+      if (a.zb) reinterpret_cast<__bf16*>(a.zb)[(size_t)f * outs + o] = (__bf16)acc;
+      else a.z[(size_t)f * outs + o] = acc;
     }
   }
 }
@@ -254,13 +264,15 @@ __global__ __launch_bounds__(256) void mix_fwd_mfma_kernel(MixArgs a) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b, acc[mt]);
     }
-    float* z = a.z + (size_t)f * KV * Cin + ci0 + fr;
+    const size_t zoff = (size_t)f * KV * Cin + ci0 + fr;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int wk = 16 * mt + 4 * fg + r;
-        if (wk < KV) z[(size_t)wk * Cin] = acc[mt][r];
+        if (wk >= KV) continue;
+        if (a.zb) reinterpret_cast<__bf16*>(a.zb)[zoff + (size_t)wk * Cin] = (__bf16)acc[mt][r];
+        else a.z[zoff + (size_t)wk * Cin] = acc[mt][r];
       }
   }
 }
@@ -362,22 +374,6 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
   for (int i = threadIdx.x; i < KVV; i += 256) row[i] = red[i];
 }
 
-__global__ __launch_bounds__(256) void mix_dA_reduce_kernel(MixArgs a, int nparts) {
-  const int KVV = a.K * a.V * a.V;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= KVV) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int p = 0;
-  for (; p + 3 < nparts; p += 4) {
-    s0 += a.part[(size_t)p * KVV + i];
-    s1 += a.part[(size_t)(p + 1) * KVV + i];
-    s2 += a.part[(size_t)(p + 2) * KVV + i];
-    s3 += a.part[(size_t)(p + 3) * KVV + i];
-  }
-  for (; p < nparts; ++p) s0 += a.part[(size_t)p * KVV + i];
-  a.dA[i] += (s0 + s1) + (s2 + s3);
-}
-
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
 __global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
@@ -467,6 +463,12 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
       o[e] = fmaxf((h[e] * sc2[c0 + e] + sh2[c0 + e]) * av[e] + rv, 0.f);
     }
     *reinterpret_cast<f32x4*>(a.out + off) = o;
+    if (a.outb) {
+      bf16x4 ob;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off) = ob;
+    }
     pool += o;
   }
   if (a.pool) {
@@ -599,8 +601,22 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
         dr[e] = dz;
       }
     }
-    *reinterpret_cast<f32x4*>(a.dh + off) = dh;
-    if (a.res_kind != RES_NONE) *reinterpret_cast<f32x4*>(a.dres + off) = dr;
+    if (a.dhb) {
+      bf16x4 hb;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hb[e] = (__bf16)dh[e];
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off) = hb;
+    } else {
+      *reinterpret_cast<f32x4*>(a.dh + off) = dh;
+    }
+    if (a.res_kind == RES_CONV && a.dresb) {
+      bf16x4 rb;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rb[e] = (__bf16)dr[e];
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off) = rb;
+    } else if (a.res_kind != RES_NONE) {
+      *reinterpret_cast<f32x4*>(a.dres + off) = dr;
+    }
   }
 }
 
@@ -642,10 +658,63 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
       o[e] = kk[c] * (dv[e] - m1[c] - xh * m2[c]);
       atomicAdd(&gl[v * C + c], o[e]);
     }
-    *reinterpret_cast<f32x4*>(a.dg + off) = o;
+    if (a.dgb) {
+      bf16x4 ob;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
+    } else {
+      *reinterpret_cast<f32x4*>(a.dg + off) = o;
+    }
   }
   __syncthreads();
-  for (int i = tid; i < a.V * C; i += 256) atomic_add_f(a.G + i, gl[i]);
+  // one partial row per workgroup (plain stores); f3_colsum adds the rows into G
+  float* row = a.Gpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * a.V * C;
+  for (int i = tid; i < a.V * C; i += 256) row[i] = gl[i];
+}
+
+// u = relu(g * scale + shift) in bf16 (BN1 + ReLU of the tcn input, bf16 mode)
+__global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
+  __shared__ float sc[256], sh[256];
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    float mu, rs;
+    bn_coeff(a.bn, c, sc[c], sh[c], mu, rs);
+  }
+  __syncthreads();
+  const size_t total8 = (size_t)a.M * a.C / 8;
+  for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < total8; q += (size_t)gridDim.x * 256) {
+    const size_t e0 = q * 8;
+    const int c0 = (int)(e0 % a.C);
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(a.g + e0);
+    const f32x4 x1 = *reinterpret_cast<const f32x4*>(a.g + e0 + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = (__bf16)fmaxf(x0[e] * sc[c0 + e] + sh[c0 + e], 0.f);
+      o[4 + e] = (__bf16)fmaxf(x1[e] * sc[c0 + 4 + e] + sh[c0 + 4 + e], 0.f);
+    }
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + e0) = o;
+  }
+}
+
+// out[c] += sum_r part[r][c]: 64 columns x 64 rows per workgroup, one atomic per column
+__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int rows, int cols, float* out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 64 + rg * 16, r1 = min(rows, r0 + 16);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < cols) {
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+      s0 += part[(size_t)r * cols + c];
+      s1 += part[(size_t)(r + 1) * cols + c];
+    }
+    if (r < r1) s0 += part[(size_t)r * cols + c];
+  }
+  red[rg][lane] = s0 + s1;
+  __syncthreads();
+  if (rg == 0 && c < cols) atomic_add_f(out + c, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
 }
 
 // ----------------------------------------------------------------------------
@@ -916,10 +985,7 @@ int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
     const int grid2 = (int)std::min<long long>((items + 3) / 4, kMixParts);
     hipLaunchKernelGGL(mix_dA_mfma_kernel, dim3(grid2), dim3(256), 0, s, *a);
     F3_LAUNCH_CHECK();
-    const int KVV = a->K * a->V * a->V;
-    hipLaunchKernelGGL(mix_dA_reduce_kernel, dim3((KVV + 255) / 256), dim3(256), 0, s, *a, grid2);
-    F3_LAUNCH_CHECK();
-    return F3_OK;
+    return f3_colsum(a->part, grid2, a->K * a->V * a->V, a->dA, s);
   }
   static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
   (void)once;
@@ -965,10 +1031,28 @@ int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
   return F3_OK;
 }
 
+int f3_bn_bwd_parts(int N, int TV) { return chunks_for(TV) * N; }
+
 int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
-  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4) || (size_t)a.V * a.C * 4 > 60 * 1024) return F3_EINVAL;
+  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4) || (size_t)a.V * a.C * 4 > 60 * 1024 || !a.Gpart) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(a.chunks, a.N), dim3(256), (size_t)a.V * a.C * 4, s, a);
+  F3_LAUNCH_CHECK();
+  return f3_colsum(a.Gpart, a.chunks * a.N, a.V * a.C, a.G, s);
+}
+
+int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return F3_OK;
+  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, s, part, rows, cols, out);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
+  if (a->C % 8 || a->C > 256) return F3_EINVAL;
+  const size_t total8 = (size_t)a->M * a->C / 8;
+  const int grid = (int)std::min<size_t>((total8 + 255) / 256, 4096);
+  hipLaunchKernelGGL(bnrelu_bf16_kernel, dim3(grid), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -237,6 +237,11 @@ struct LayerWs {
   float *gw, *gwT, *tw, *twT, *rw = nullptr, *rwT = nullptr, *aeff, *beff;
   BnWs bn1, bn2, bnr, bnca;
   float *P1, *P2, *G, *dAeff, *dq2, *dbn, *dq1, *e;
+  // bf16 mode: u = relu(bn1(g)) (tcn GEMM operand, saved for its wgrad), a bf16 copy of the
+  // block output when the next block has a residual conv, the packed tcn weight gradient
+  unsigned short *u = nullptr, *outb = nullptr;
+  const unsigned short* xb = nullptr;  // bf16 copy of the block input (RES_CONV blocks)
+  float* dWp = nullptr;
 };
 
 struct StreamWs {
@@ -245,6 +250,7 @@ struct StreamWs {
   LayerWs L[7];
   float *dh, *dres, *dv, *dg, *dZ, *dx[2], *dpool;
   float* mixpart;  // graph-mix dA partials [kMixParts][K*V*V]
+  float* gpart;    // BN1-backward per-node column-sum partials
 };
 
 struct Ws {
@@ -257,6 +263,7 @@ struct Ws {
   float *out, *dlogits, *ds;
   float *skel, *sensor;  // copies of the step's inputs (backward re-reads them)
   char *zf0, *zf1, *zb0, *zb1;
+  const unsigned short* zero;  // 256 zero bytes (LDS-DMA GEMM padding rows)
   size_t bytes;
 };
 
@@ -277,8 +284,10 @@ Ws plan(const f3_net& net, int N, char* base) {
   const bool cnn = net.has_cnn;
   const int Ts = net.cfg.sensor_frames;
   const int Tl = cnn ? (Ts / 2) / 2 : Ts;
+  const bool hb = net.cfg.precision == F3_PRECISION_BF16;
   // ---- zero-at-forward region ----
   w.zf0 = A.take<char>(0);
+  w.zero = reinterpret_cast<const unsigned short*>(A.take<char>(256));
   for (int si = 0; si < net.nstreams; ++si) {
     const StreamIdx& S = net.st[si];
     StreamWs& W = w.st[si];
@@ -317,6 +326,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.P2 = A.take<float>((size_t)N * L.cout);
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
+      if (hb) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);
     }
   }
   if (net.has_sensor && cnn) {
@@ -331,16 +341,19 @@ Ws plan(const f3_net& net, int N, char* base) {
     StreamWs& W = w.st[si];
     W.x0 = A.take<float>((size_t)N * S.T * V * S.cin);
     W.A = A.take<float>((size_t)K * V * V);
-    size_t maxMC = 0, maxZ = 0;
+    size_t maxMC = 0, maxZ = 0, maxG = 0;
     const float* xin = W.x0;
+    const unsigned short* xinb = nullptr;
     for (int l = 0; l < 7; ++l) {
       const LayerIdx& L = S.L[l];
       LayerWs& X = W.L[l];
       const size_t Mi = (size_t)N * L.T_in * V, Mo = (size_t)N * L.T_out * V;
       const int C = L.cout, Ci = L.cin;
       X.x = xin;
+      X.xb = xinb;
       X.z = A.take<float>(Mi * K * Ci);
       X.g = A.take<float>(Mi * C);
+      if (hb) X.u = A.take<unsigned short>(Mi * C);
       X.h = A.take<float>(Mo * C);
       if (L.res == RES_CONV) X.r = A.take<float>(Mo * C);
       X.out = A.take<float>(Mo * C);
@@ -362,6 +375,9 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
       xin = X.out;
+      xinb = nullptr;
+      if (hb && l + 1 < 7 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(Mo * C);
+      maxG = std::max(maxG, (size_t)f3_bn_bwd_parts(N, L.T_in * V) * V * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
@@ -375,6 +391,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     W.dx[1] = A.take<float>(maxMC);
     W.dpool = A.take<float>((size_t)N * 256);
     W.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
+    W.gpart = A.take<float>(maxG);
   }
   if (net.has_sensor) {
     if (cnn) {
@@ -454,6 +471,8 @@ void add_job(PrepTable& t, int type, int n, float* dst, const float* s0, const f
 
 // bf16 view of a packed operand (the fp32-sized slot holds the bf16 copy in bf16 mode)
 inline const unsigned short* bf(const float* p, int on) { return on ? reinterpret_cast<const unsigned short*>(p) : nullptr; }
+// bf16 view of an activation slot (bf16 mode stores GEMM operand tensors as bf16)
+inline unsigned short* bfa(float* p, int on) { return on ? reinterpret_cast<unsigned short*>(p) : nullptr; }
 
 void add_bnrun(BnRunTable& t, const Ptrs& q, const BnIdx& bi, const double* sum, const double* sq, double count) {
   BnRunJob& j = t.jobs[t.n++];
@@ -511,26 +530,39 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
+    mx.zb = bfa(X.z, hb);
     F3_TRY(f3_mix_fwd(&mx, s));
     ConvGemmArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
-    ga.in = X.z; ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+    ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
+    ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
     F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
       ConvGemmArgs ra;
       std::memset(&ra, 0, sizeof(ra));
       ra.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      ra.in = X.x; ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
+      ra.in = hb ? nullptr : X.x; ra.inb = hb ? X.xb : nullptr; ra.zero = w.zero;
+      if (hb && !X.xb) return F3_ESTATE;
+      ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
     // tcn: BN1 + ReLU prologue, (9,1) conv, bias, BN2 stats + channel-attention pool epilogue
     ConvGemmArgs ta;
     std::memset(&ta, 0, sizeof(ta));
     ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    ta.in = X.g; ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.pro_bn = bn1; ta.bias = q.p(L.tcn_b);
+    ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.bias = q.p(L.tcn_b);
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
-    F3_TRY(f3_conv_gemm(&ta, 1, EPI_BIAS | EPI_STATS | EPI_GAP, s));
+    if (hb) {  // materialise u = relu(bn1(g)) in bf16 (also the tcn wgrad operand)
+      BnReluArgs br;
+      br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u;
+      F3_TRY(f3_bnrelu_bf16(&br, s));
+      ta.inb = X.u; ta.zero = w.zero;
+      F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
+    } else {
+      ta.in = X.g; ta.pro_bn = bn1;
+      F3_TRY(f3_conv_gemm(&ta, 1, EPI_BIAS | EPI_STATS | EPI_GAP, s));
+    }
     // channel attention (stgcan.py:59-74)
     CaArgs ca;
     std::memset(&ca, 0, sizeof(ca));
@@ -545,6 +577,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.pool = l == 6 ? W.pool : nullptr;
+    ba.outb = X.outb;
     F3_TRY(f3_block_out(ba, s));
     if (train) {
       add_bnrun(run, q, L.bn1, X.bn1.fsum, X.bn1.fsq, Mi);
@@ -576,6 +609,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
   const float* dout = l_hi == 6 ? nullptr : W.dx[(5 - l_hi) & 1];
   int pp = (6 - l_hi) & 1;
+  PrepTable unpack;  // bf16 mode: packed tcn weight gradients -> reference layout
+  unpack.n = 0;
   for (int l = l_hi; l >= l_lo; --l) {
     const LayerIdx& L = S.L[l];
     LayerWs& X = W.L[l];
@@ -595,6 +630,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.P1 = X.P1; ba.P2 = X.P2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
     ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = W.dh;
     ba.dres = L.res == RES_CONV ? W.dres : (L.res == RES_ID ? dx : nullptr);
+    ba.dhb = bfa(W.dh, hb);
+    ba.dresb = L.res == RES_CONV ? bfa(W.dres, hb) : nullptr;
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     F3_TRY(f3_block_bwd_reduce(ba, s));
@@ -614,31 +651,47 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
-    td.in = W.dh; td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.in = hb ? nullptr : W.dh; td.inb = bfa(W.dh, hb); td.zero = w.zero;
+    td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
     if (debug_stop(si, l)) return F3_OK;
     WgradArgs tw;
     std::memset(&tw, 0, sizeof(tw));
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    tw.dy = W.dh; tw.ldy = C; tw.in = X.g; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
-    tw.outmap = WG_OUT_CONV; tw.pro_bn = bn1; tw.bf16 = hb;
-    F3_TRY(f3_conv_wgrad(&tw, 1, s));
+    tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
+    tw.outmap = WG_OUT_CONV; tw.bf16 = hb;
+    if (hb) {  // bf16 operands dh, u; packed accumulator (unpacked into the grads below)
+      tw.dyb = bfa(W.dh, 1); tw.inb = X.u; tw.zero = w.zero; tw.dw = X.dWp;
+      if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
+      F3_TRY(f3_conv_wgrad(&tw, 0, s));
+      add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
+    } else {
+      tw.dy = W.dh; tw.in = X.g; tw.pro_bn = bn1;
+      F3_TRY(f3_conv_wgrad(&tw, 1, s));
+    }
     BnBwdArgs bb;
     std::memset(&bb, 0, sizeof(bb));
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = W.dg; bb.G = X.G;
+    bb.Gpart = W.gpart; bb.dgb = bfa(W.dg, hb);
     F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     ConvGemmArgs gd;
     std::memset(&gd, 0, sizeof(gd));
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
-    gd.in = W.dg; gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
+    gd.in = hb ? nullptr : W.dg; gd.inb = bfa(W.dg, hb); gd.zero = w.zero;
+    gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
     F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
     gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
-    gw.dy = W.dg; gw.ldy = C; gw.in = X.z; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
+    gw.ldy = C; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
+    if (hb) {
+      gw.dyb = bfa(W.dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero;
+    } else {
+      gw.dy = W.dg; gw.in = X.z;
+    }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
     F3_TRY(f3_conv_wgrad(&gw, 0, s));
     MixArgs mx;
@@ -654,17 +707,24 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       ConvGemmArgs rd;
       std::memset(&rd, 0, sizeof(rd));
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
-      rd.in = W.dres; rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
+      rd.in = hb ? nullptr : W.dres; rd.inb = bfa(W.dres, hb); rd.zero = w.zero;
+      rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
       F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
       rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      rw.dy = W.dres; rw.ldy = C; rw.in = X.x; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
+      rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
+      if (hb) {
+        rw.dyb = bfa(W.dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+      } else {
+        rw.dy = W.dres; rw.in = X.x;
+      }
       F3_TRY(f3_conv_wgrad(&rw, 0, s));
     }
     dout = dx;
     pp ^= 1;
   }
+  F3_TRY(f3_prep(unpack, s));
   if (l_lo > 0) return F3_OK;
   DataBnArgs d;
   std::memset(&d, 0, sizeof(d));
@@ -807,7 +867,7 @@ int f3_net_create(const f3_config* cfg, f3_net** out) {
   if (cfg->num_node < 2 || cfg->num_partition < 1 || cfg->num_class < 1 || cfg->num_class > 64) return F3_EINVAL;
   if (cfg->frames < 2 || cfg->model < 0 || cfg->model > 3) return F3_EINVAL;
   if (cfg->num_partition * cfg->num_node * cfg->num_node > 1024) return F3_EINVAL;
-  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) return F3_EINVAL;
+  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) return F3_EINVAL;  // not 2
   f3_net* n = new f3_net();
   n->cfg = *cfg;
   n->K = cfg->num_partition;
@@ -1013,10 +1073,29 @@ int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_
   return f3_rmsprop(params, square_avg, grads, n, lr, alpha, eps, grad_scale, (hipStream_t)stream);
 }
 
-int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
+// test-entry scratch (kept for the process lifetime; the network uses its workspace)
+static const unsigned short* test_zero_page() {
+  static void* z = nullptr;
+  if (!z && hipMalloc(&z, 4096) == hipSuccess) (void)hipMemset(z, 0, 4096);
+  return (const unsigned short*)z;
+}
+static float* test_scratch(size_t n) {
+  static float* p = nullptr;
+  static size_t cap = 0;
+  if (n > cap) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return nullptr;
+    cap = n;
+  }
+  return p;
+}
+
+int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
                     int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int hb = precision == F3_PRECISION_BF16;
+  if (precision < 0 || precision > 2) return F3_EINVAL;
+  const int hb = precision != F3_PRECISION_FP32;
   if (w) {  // w == NULL: wpack already holds the packed operand (timing the GEMM alone)
     PrepTable t;
     t.n = 0;
@@ -1027,14 +1106,21 @@ int f3_conv_forward(const float* x, const float* w, const float* bias, float* ou
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
-  a.in = x; a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias;
+  if (precision == F3_PRECISION_BF16) {
+    a.inb = (const unsigned short*)x;
+    a.zero = test_zero_page();
+  } else {
+    a.in = (const float*)x;
+  }
+  a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias;
   return f3_conv_gemm(&a, 0, EPI_BIAS, s);
 }
 
-int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
+int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
                           int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int hb = precision == F3_PRECISION_BF16;
+  if (precision < 0 || precision > 2) return F3_EINVAL;
+  const int hb = precision != F3_PRECISION_FP32;
   PrepTable t;
   t.n = 0;
   add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, hb);
@@ -1043,21 +1129,47 @@ int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpa
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_in * V, Cin, Cout, KT, stride, pad, 1, T_in, T_out, V, Cout, Cin);
-  a.in = dy; a.w = wpack; a.wb = bf(wpack, hb); a.out = dx;
+  if (precision == F3_PRECISION_BF16) {
+    a.inb = (const unsigned short*)dy;
+    a.zero = test_zero_page();
+  } else {
+    a.in = (const float*)dy;
+  }
+  a.w = wpack; a.wb = bf(wpack, hb); a.out = dx;
   return f3_conv_gemm(&a, 0, 0, s);
 }
 
-int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
+int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (precision < 0 || precision > 2) return F3_EINVAL;
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
   if (db && hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
   WgradArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
-  a.dy = dy; a.ldy = Cout; a.in = x; a.dw = dw; a.db = db; a.outmap = WG_OUT_CONV;
-  a.bf16 = precision == F3_PRECISION_BF16;
+  a.ldy = Cout; a.dw = dw; a.db = db; a.outmap = WG_OUT_CONV;
+  a.bf16 = precision != F3_PRECISION_FP32;
+  if (precision == F3_PRECISION_BF16) {
+    a.dyb = (const unsigned short*)dy;
+    a.inb = (const unsigned short*)x;
+    a.zero = test_zero_page();
+    if (f3_wgrad_glds_ok(a) && KT > 1) {  // packed accumulator, then unpack
+      float* packed = test_scratch((size_t)Cout * Cin * KT);
+      if (!packed) return F3_EHIP;
+      if (hipMemsetAsync(packed, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
+      a.dw = packed;
+      F3_TRY(f3_conv_wgrad(&a, 0, s));
+      PrepTable t;
+      t.n = 0;
+      add_job(t, PREP_UNPACK_CONV, Cout * Cin * KT, dw, packed, nullptr, nullptr, Cout, Cin, KT);
+      return f3_prep(t, s);
+    }
+  } else {
+    a.dy = (const float*)dy;
+    a.in = (const float*)x;
+  }
   return f3_conv_wgrad(&a, 0, s);
 }
 

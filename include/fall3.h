@@ -35,7 +35,8 @@ enum { F3_MODEL_TWO_STGCAN_BILSTM = 0, F3_MODEL_TWO_STGCAN = 1, F3_MODEL_STGCN =
 enum { F3_SENSOR_NONE = 0, F3_SENSOR_BILSTM = 1, F3_SENSOR_CNN_BILSTM = 2 };
 enum { F3_NAMING_PACKAGE = 0, F3_NAMING_NOTEBOOK = 1 };
 enum { F3_PRECISION_FP32 = 0, /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
-       F3_PRECISION_BF16 = 1  /* bf16 operands, fp32 accumulate (v_mfma_f32_16x16x32_bf16) */ };
+       F3_PRECISION_BF16 = 1, /* bf16 GEMM operands in HBM, fp32 accumulate (v_mfma_f32_16x16x32_bf16) */
+       F3_PRECISION_BF16_FP32IN = 2 /* kernel-level entries only: bf16 arithmetic on fp32 activations */ };
 enum { F3_ENTRY_PARAM = 0, F3_ENTRY_BUFFER = 1, F3_ENTRY_COUNTER = 2 };
 
 typedef struct f3_config {
@@ -104,14 +105,16 @@ int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_
 /* Kernel-level entries used by the unit tests and bench.py: out[N,T_out,V,Cout] = conv_(KT,1)(x)
  * with x [N,T_in,V,Cin] channels-last, w in reference layout [Cout][Cin][KT], bias [Cout]
  * (stgcan.py:24-31 tcn Conv2d). wpack is scratch of Cout*KT*Cin floats for the packed
- * operand; w == NULL reuses what a previous call packed there. precision = F3_PRECISION_*. */
-int f3_conv_forward(const float* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
+ * operand; w == NULL reuses what a previous call packed there. precision = F3_PRECISION_*:
+ * FP32 -> x/dy are fp32; BF16 -> x/dy are bf16 (the network's bf16 operand tensors);
+ * BF16_FP32IN -> fp32 x/dy rounded to bf16 while staging. */
+int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
                     int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream);
 
 /* Its gradients: dx = conv^T(dy) [N,T_in,V,Cin]; dw [Cout][Cin][KT] and db [Cout] (overwritten). */
-int f3_conv_backward_data(const float* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
+int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
                           int Cout, int KT, int stride, int pad, int precision, void* stream);
-int f3_conv_backward_weight(const float* dy, const float* x, float* dw, float* db, int N, int T_in, int V, int Cin,
+int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, int precision, void* stream);
 
 /* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):

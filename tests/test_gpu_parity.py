@@ -44,14 +44,24 @@ def call(model, spec, skel, sensor):
     return model(skel, sensor)
 
 
+PRECISIONS = [0, 1, 2]
+PREC_IDS = ["fp32", "bf16", "bf16_fp32in"]
+
+
 def _q(t, precision):
-    """Operand rounding of a precision mode: bf16 mode rounds GEMM operands to bf16 (RNE)
-    and accumulates in fp32, so the fp64 reference on bf16-rounded operands is exact up to
+    """Operand rounding of a precision mode: the bf16 modes round GEMM operands to bf16 (RNE)
+    and accumulate in fp32, so the fp64 reference on bf16-rounded operands is exact up to
     fp32 accumulation error."""
-    return t.to(torch.bfloat16).to(t.dtype) if precision == 1 else t
+    return t.to(torch.bfloat16).to(t.dtype) if precision else t
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "bf16"])
+def _act(t_cl, precision, d):
+    """Activation tensor as the kernel entry takes it: bf16 for precision 1, else fp32."""
+    t = t_cl.to(d)
+    return t.to(torch.bfloat16).contiguous() if precision == 1 else t.float().contiguous()
+
+
+@pytest.mark.parametrize("precision", PRECISIONS, ids=PREC_IDS)
 def test_conv_kernel_matches_torch(precision):
     d = dev()
     import fall_multimodal_amd._lib as L
@@ -64,7 +74,7 @@ def test_conv_kernel_matches_torch(precision):
         b = torch.randn(Co)
         ref = torch.nn.functional.conv2d(_q(x.double(), precision), _q(w.double(), precision), b.double(),
                                          stride=(s, 1), padding=(p, 0)).float()  # [N,Co,To,V]
-        xg = x.permute(0, 2, 3, 1).contiguous().to(d)
+        xg = _act(x.permute(0, 2, 3, 1).contiguous(), precision, d)
         To = (T + 2 * p - KT) // s + 1
         out = torch.empty(N, To, V, Co, device=d)
         wp = torch.empty(Co * KT * Ci, device=d)
@@ -77,10 +87,11 @@ def test_conv_kernel_matches_torch(precision):
 
 
 CONV_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
-               (4, 29, 14, 128, 128, 9, 2, 4), (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4)]
+               (4, 29, 14, 128, 128, 9, 2, 4), (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4),
+               (2, 30, 14, 9, 64, 1, 1, 0), (2, 30, 18, 64, 192, 1, 1, 0), (3, 30, 18, 192, 64, 1, 1, 0)]
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "bf16"])
+@pytest.mark.parametrize("precision", PRECISIONS, ids=PREC_IDS)
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 def test_conv_backward_kernels_match_torch(shape, precision):
     d = dev()
@@ -94,8 +105,8 @@ def test_conv_backward_kernels_match_torch(shape, precision):
     dy = _q(torch.randn_like(y), precision)
     y.backward(dy)
     To = y.shape[2]
-    dyg = dy.float().permute(0, 2, 3, 1).contiguous().to(d)
-    xg = x.detach().float().permute(0, 2, 3, 1).contiguous().to(d)
+    dyg = _act(dy.permute(0, 2, 3, 1).contiguous(), precision, d)
+    xg = _act(x.detach().permute(0, 2, 3, 1).contiguous(), precision, d)
     wg = w.detach().float().contiguous().to(d)
     dx = torch.empty(N, T, V, Ci, device=d)
     wp = torch.empty(Co * KT * Ci, device=d)
