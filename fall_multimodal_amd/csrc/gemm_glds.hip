@@ -50,15 +50,46 @@ F3_DEV int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <int EPI, int WN>
+// Per staging row: branch-free source row for tap dt. Forward: ti = t*S + dt - P, valid in
+// [0, T_in). Transposed (dgrad): x = t + P - dt, valid if x >= 0, x % S == 0, x / S < T_in
+// (S is 1 or 2). base = first source row of the clip + v; q = t*S - P (fwd) or t + P (dgrad).
+struct RowMap {
+  int base, q;  // base < 0: row outside M
+};
+
+F3_DEV RowMap rowmap(int m, const ConvGeom& g) {
+  RowMap r;
+  if (m >= g.M) { r.base = -1; r.q = 0; return r; }
+  const int nt = m / g.V, v = m - nt * g.V, n = nt / g.T_out, t = nt - n * g.T_out;
+  r.base = n * g.T_in * g.V + v;
+  r.q = g.transposed ? t + g.P : t * g.S - g.P;
+  return r;
+}
+
+F3_DEV int rowmap_src(const RowMap& r, int dt, const ConvGeom& g) {
+  int ti;
+  bool ok;
+  if (!g.transposed) {
+    ti = r.q + dt;
+    ok = ti >= 0 && ti < g.T_in;
+  } else {
+    const int x = r.q - dt;
+    ti = g.S == 2 ? (x >> 1) : x;
+    ok = x >= 0 && (g.S == 1 || (x & 1) == 0) && ti < g.T_in;
+  }
+  return (ok && r.base >= 0) ? r.base + ti * g.V : -1;
+}
+
+template <int EPI, int WN, int NST>
 __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   constexpr int BM = G_BM, BN = 32 * WN;
   constexpr int A_BYTES = BM * G_BK * 2, B_BYTES = BN * G_BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = A_BYTES / 1024 / 4, B_INSTR = B_BYTES / 1024 / 4;  // per wave
-  // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code): two
+  constexpr int NPS = A_INSTR + B_INSTR;  // LDS-DMA instructions per wave per stage
+  // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code): NST
   // stages, then the epilogue coefficient tables; the reductions reuse stage 0.
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 4 * BN * 4];
-  float* epi_sc = reinterpret_cast<float*>(smem + 2 * STAGE);
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + 4 * BN * 4];
+  float* epi_sc = reinterpret_cast<float*>(smem + NST * STAGE);
   float* epi_sh = epi_sc + BN;
   float* epi_mu = epi_sh + BN;
   float* epi_rs = epi_mu + BN;
@@ -85,30 +116,23 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 
   // per-lane staging rows (fixed for the whole k loop)
   const int sub = lane >> 3, pch = lane & 7;
-  int a_n[A_INSTR], a_t[A_INSTR], a_v[A_INSTR], a_c[A_INSTR];
+  RowMap a_map[A_INSTR];
+  int a_c[A_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int rr = (wave * A_INSTR + i) * 8 + sub;
-    const int m = m0 + rr;
-    a_c[i] = swz(rr, pch);
-    if (m < g.M) {
-      const int nt = m / g.V;
-      a_v[i] = m - nt * g.V;
-      a_n[i] = nt / g.T_out;
-      a_t[i] = nt - a_n[i] * g.T_out;
-    } else {
-      a_n[i] = -1; a_t[i] = 0; a_v[i] = 0;
-    }
+    a_c[i] = swz(rr, pch) * 8;
+    a_map[i] = rowmap(m0 + rr, g);
   }
   const unsigned short* b_row[B_INSTR];
-  int b_c[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
     const int rb = (wave * B_INSTR + i) * 8 + sub;
     const int j = j0 + rb;
-    b_c[i] = swz(rb, pch);
-    b_row[i] = j < g.Nc ? wb + (size_t)j * Ktot : nullptr;
+    b_row[i] = j < g.Nc ? wb + (size_t)j * Ktot + swz(rb, pch) * 8 : a.zero;
   }
+  const int b_step = 1;  // (kept for clarity: zero rows never advance)
+  (void)b_step;
 
   auto stage = [&](int t, int buf) {
     const int k0 = t * G_BK;
@@ -116,14 +140,14 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     char* sa = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
-      const int r = a_n[i] >= 0 ? g_src_row(a_n[i], a_t[i], a_v[i], dt, g) : -1;
-      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + i0 + a_c[i] * 8 : a.zero;
+      const int r = rowmap_src(a_map[i], dt, g);
+      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + i0 + a_c[i] : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sa + (wave * A_INSTR + i) * 1024), 16, 0, 0);
     }
     char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
-      const unsigned short* src = b_row[i] ? b_row[i] + k0 + b_c[i] * 8 : a.zero;
+      const unsigned short* src = b_row[i] == a.zero ? a.zero : b_row[i] + k0;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sb + (wave * B_INSTR + i) * 1024), 16, 0, 0);
     }
   };
@@ -136,12 +160,27 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 #pragma unroll
     for (int y = 0; y < WN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (NST == 2) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {  // NST == 3: two stages in flight; raw barriers keep the newest one in flight
+    stage(0, 0);
+    if (nchunk > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
   for (int t = 0; t < nchunk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nchunk) stage(t + 1, buf ^ 1);
+    const int buf = NST == 2 ? (t & 1) : (t % 3);
+    if (NST == 2) {
+      if (t + 1 < nchunk) stage(t + 1, buf ^ 1);
+    } else {
+      if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
+    }
     const char* sa = smem + buf * STAGE;
     const char* sb = sa + A_BYTES;
 #pragma unroll
@@ -163,9 +202,17 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 #pragma unroll
         for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NST == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
+  if (NST != 2) __syncthreads();
 
   // ---------------- epilogue ----------------
   float* red = reinterpret_cast<float*>(smem);   // [2][2][BN]  (stage 0 is free now)
@@ -205,9 +252,13 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
           else if (n == nlo + 1) gap1[y] += v;
           else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
         }
-        float* o = a.out + (size_t)m * g.ldo + j;
-        if (EPI & EPI_ADD) *o += v;
-        else *o = v;
+        if (!(EPI & EPI_ADD) && a.outb) {
+          reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+        } else {
+          float* o = a.out + (size_t)m * g.ldo + j;
+          if (EPI & EPI_ADD) *o += v;
+          else *o = v;
+        }
       }
     }
   }
@@ -258,14 +309,22 @@ bool f3_igemm_ok(const ConvGemmArgs& a) {
   return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0;
 }
 
-template <int WN>
+static int igemm_stages() {
+  static const int v = [] {
+    const char* e = getenv("F3_IGEMM_STAGES");
+    return e && atoi(e) == 3 ? 3 : 2;
+  }();
+  return v;
+}
+
+template <int WN, int NST>
 static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
   const int tiles = ((a.g.M + G_BM - 1) / G_BM) * ((a.g.Nc + 32 * WN - 1) / (32 * WN));
-#define F3_ICASE(E)                                                              \
-  if (epi == (E)) {                                                             \
-    hipLaunchKernelGGL((igemm_bf16<(E), WN>), dim3(tiles), dim3(256), 0, s, a); \
-    F3_LAUNCH_CHECK();                                                           \
-    return F3_OK;                                                                \
+#define F3_ICASE(E)                                                                   \
+  if (epi == (E)) {                                                                  \
+    hipLaunchKernelGGL((igemm_bf16<(E), WN, NST>), dim3(tiles), dim3(256), 0, s, a); \
+    F3_LAUNCH_CHECK();                                                                \
+    return F3_OK;                                                                     \
   }
   F3_ICASE(EPI_BIASV | EPI_STATS)            // gcn forward
   F3_ICASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
@@ -282,8 +341,12 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
-  if (a.g.Nc > 64) return launch_igemm<4>(a, epi, s);
-  return launch_igemm<2>(a, epi, s);
+  if (igemm_stages() == 3) {
+    if (a.g.Nc > 64) return launch_igemm<4, 3>(a, epi, s);
+    return launch_igemm<2, 3>(a, epi, s);
+  }
+  if (a.g.Nc > 64) return launch_igemm<4, 2>(a, epi, s);
+  return launch_igemm<2, 2>(a, epi, s);
 }
 
 // ============================================================================

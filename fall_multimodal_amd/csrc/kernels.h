@@ -32,6 +32,7 @@ struct ConvGemmArgs {
   const unsigned short* wb;  // same, bf16; non-null selects the bf16 MFMA kernels
   const unsigned short* inb; // bf16 activations (instead of `in`); with wb: LDS-DMA kernel when shapes allow
   const unsigned short* zero;  // >= 16 zero bytes (rows outside the clip / tile for the LDS-DMA kernel)
+  unsigned short* outb;        // LDS-DMA kernel: write the output as bf16 here instead of `out`
   float* out;
   BnRef pro_bn;       // prologue: relu(bn(x)) on input channels
   const float* bias;

@@ -39,6 +39,7 @@ struct MixArgs {
   int accumulate;
   float* part;           // bwd scratch [kMixParts][K*V*V] (MFMA path)
   unsigned short* zb;    // fwd: write z as bf16 (bf16 mode GEMM operand) instead of fp32
+  const unsigned short* dzb;  // bwd: dZ in bf16 (instead of z) — LDS mix path only
 };
 constexpr int kMixParts = 1024;
 

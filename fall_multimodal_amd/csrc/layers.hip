@@ -374,6 +374,177 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
   for (int i = threadIdx.x; i < KVV; i += 256) row[i] = red[i];
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged graph mix (Cin % 16 == 0, K*V <= 64, V <= 32): one frame at a time per
+// workgroup, the frame's [V][Cin] input (and [K*V][Cin] gradient) loaded with coalesced
+// 16-B reads into LDS (row stride Cin+20 floats: conflict-light scalar and b128 fragment
+// reads), fp32 MFMA 16x16x4 with the fixed A~ fragments in registers, outputs written
+// back through LDS as whole rows. The backward computes dX and dA from ONE read of dZ.
+// ---------------------------------------------------------------------------
+F3_DEV int mix_stride(int Cin) { return Cin + 20; }
+
+__global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, S = mix_stride(Cin), SZ = Cin + 4;
+  float* xs = sm;                 // [V][S]
+  float* zs = sm + V * S;         // [KV][SZ]
+  const int ksteps = (V + 3) / 4;  // <= 8
+  float af[4][8];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg) : 0.f;
+  const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+    for (int i = tid; i < n4; i += 256) {
+      const int v = i / C4, c = (i - v * C4) * 4;
+      *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+    }
+    __syncthreads();
+    for (int t = wave; t < tiles; t += 4) {
+      const int ci0 = t * 16;
+      f32x4 acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        if (ks >= ksteps) break;
+        const int v = 4 * ks + fg;
+        const float b = v < V ? xs[v * S + ci0 + fr] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b, acc[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int wk = 16 * mt + 4 * fg + r;
+          if (wk < KV) zs[wk * SZ + ci0 + fr] = acc[mt][r];
+        }
+    }
+    __syncthreads();
+    const size_t zoff = (size_t)f * KV * Cin;
+    for (int i = tid; i < n8; i += 256) {
+      const int wk = i / C8, c = (i - wk * C8) * 8;
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(zs + wk * SZ + c);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(zs + wk * SZ + c + 4);
+      if (a.zb) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = (__bf16)u0[e]; o[4 + e] = (__bf16)u1[e]; }
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.zb) + zoff + (size_t)i * 8) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8) = u0;
+        *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8 + 4) = u1;
+      }
+    }
+    // the next frame's first __syncthreads orders these zs reads before its zs writes
+  }
+}
+
+__global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, KVV = KV * V, S = mix_stride(Cin);
+  float* xs = sm;            // [V][S]
+  float* zs = sm + V * S;    // [KV][S]
+  const int ksteps = (KV + 3) / 4;  // <= 16
+  float adx[2][16];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) adx[mt][ks] = ks < ksteps ? atil(a.A, K, V, 4 * ks + fg, 16 * mt + fr) : 0.f;
+  // dA tiles of this wave: (mt, nt) = (wave >> 1, 2*(wave & 1) + {0,1}) over [32 v][64 wk]
+  const int dmt = wave >> 1, dnt0 = 2 * (wave & 1);
+  f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int tiles = Cin / 16, n4x = V * Cin / 4, n4z = KV * Cin / 4, C4 = Cin / 4;
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+    for (int i = tid; i < n4x; i += 256) {
+      const int v = i / C4, c = (i - v * C4) * 4;
+      *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+    }
+    if (a.dzb) {
+      const bf16x4* zg = reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.dzb) + (size_t)f * KV * Cin);
+      for (int i = tid; i < n4z; i += 256) {
+        const int wk = i / C4, c = (i - wk * C4) * 4;
+        const bf16x4 u = zg[i];
+        *reinterpret_cast<f32x4*>(zs + wk * S + c) = f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
+      }
+    } else {
+      const f32x4* zg = reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * Cin);
+      for (int i = tid; i < n4z; i += 256) {
+        const int wk = i / C4, c = (i - wk * C4) * 4;
+        *reinterpret_cast<f32x4*>(zs + wk * S + c) = zg[i];
+      }
+    }
+    __syncthreads();
+    // dX_f[v][ci] = sum_wk A~[v][wk] dZ_f[wk][ci]
+    for (int t = wave; t < tiles; t += 4) {
+      const int ci0 = t * 16;
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        if (ks >= ksteps) break;
+        const int wk = 4 * ks + fg;
+        const float b = wk < KV ? zs[wk * S + ci0 + fr] : 0.f;
+        acc[0] = mfma16x4(adx[0][ks], b, acc[0]);
+        acc[1] = mfma16x4(adx[1][ks], b, acc[1]);
+      }
+      float* dx = a.dx + (size_t)f * V * Cin + ci0 + fr;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = 16 * mt + 4 * fg + r;
+          if (v < V) {
+            float* d = dx + (size_t)v * Cin;
+            if (a.accumulate) *d += acc[mt][r];
+            else *d = acc[mt][r];
+          }
+        }
+    }
+    // dA[v][wk] += sum_ci X_f[v][ci] dZ_f[wk][ci]   (k index of the MFMA = lane group,
+    // the 4 components of each b128 read are 4 k-steps)
+    {
+      const int v = 16 * dmt + fr;
+      for (int c16 = 0; c16 < Cin; c16 += 16) {
+        const f32x4 xa = v < V ? *reinterpret_cast<const f32x4*>(xs + v * S + c16 + 4 * fg) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int wk = 16 * (dnt0 + q) + fr;
+          const f32x4 zb = wk < KV ? *reinterpret_cast<const f32x4*>(zs + wk * S + c16 + 4 * fg)
+                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 4; ++s) dacc[q] = mfma16x4(xa[s], zb[s], dacc[q]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // workgroup partial row of dA (each (v, wk) has exactly one owner lane), then f3_colsum
+  float* red = sm;
+  for (int i = tid; i < KVV; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = 16 * dmt + 4 * fg + r, wk = 16 * (dnt0 + q) + fr;
+      if (v < V && wk < KV) {
+        const int w = wk / K, k = wk - w * K;
+        red[(k * V + v) * V + w] = dacc[q][r];
+      }
+    }
+  __syncthreads();
+  float* row = a.part + (size_t)blockIdx.x * KVV;
+  for (int i = tid; i < KVV; i += 256) row[i] = red[i];
+}
+
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
 __global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
@@ -958,11 +1129,21 @@ static void allow_big_lds(const void* fn) {
 
 static bool mix_mfma_ok(const MixArgs& a) { return a.Cin % 16 == 0 && a.K * a.V <= 64 && a.V <= 32; }
 
+static size_t mix_lds_fwd2(const MixArgs& a) {
+  return sizeof(float) * ((size_t)a.V * (a.Cin + 20) + (size_t)a.K * a.V * (a.Cin + 4));
+}
+static size_t mix_lds_bwd2(const MixArgs& a) {
+  return sizeof(float) * std::max((size_t)(a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
+}
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
   if (mix_mfma_ok(*a)) {
-    const long long items = (long long)a->frames * (a->Cin / 16);
-    const int grid = (int)std::min<long long>((items + 3) / 4, 8192);
-    hipLaunchKernelGGL(mix_fwd_mfma_kernel, dim3(grid), dim3(256), 0, s, *a);
+    static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel), true);
+    (void)once;
+    const size_t lds = mix_lds_fwd2(*a);
+    if (lds > 160 * 1024) return F3_EINVAL;
+    const int grid = std::min(a->frames, 4096);
+    hipLaunchKernelGGL(mix_fwd_lds_kernel, dim3(grid), dim3(256), lds, s, *a);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }
@@ -977,15 +1158,15 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
 
 int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
   if (mix_mfma_ok(*a)) {
-    const long long items = (long long)a->frames * (a->Cin / 16);
-    const int grid = (int)std::min<long long>((items + 3) / 4, 8192);
-    hipLaunchKernelGGL(mix_dx_mfma_kernel, dim3(grid), dim3(256), 0, s, *a);
-    F3_LAUNCH_CHECK();
     if (!a->part) return F3_EINVAL;
-    const int grid2 = (int)std::min<long long>((items + 3) / 4, kMixParts);
-    hipLaunchKernelGGL(mix_dA_mfma_kernel, dim3(grid2), dim3(256), 0, s, *a);
+    static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel), true);
+    (void)once;
+    const size_t lds = mix_lds_bwd2(*a);
+    if (lds > 160 * 1024) return F3_EINVAL;
+    const int grid = std::min(a->frames, kMixParts);
+    hipLaunchKernelGGL(mix_bwd_lds_kernel, dim3(grid), dim3(256), lds, s, *a);
     F3_LAUNCH_CHECK();
-    return f3_colsum(a->part, grid2, a->K * a->V * a->V, a->dA, s);
+    return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
   }
   static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
   (void)once;

@@ -682,6 +682,11 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : W.dg; gd.inb = bfa(W.dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
+    const bool dzb = hb && Ci % 16 == 0 && K * V <= 64 && V <= 32;  // bf16 dZ feeds the LDS graph-mix backward
+    if (dzb) {
+      if (!f3_igemm_ok(gd)) return F3_EINVAL;
+      gd.outb = bfa(W.dZ, 1);
+    }
     F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
@@ -698,6 +703,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
     mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart;
+    mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
     F3_TRY(f3_mix_bwd(&mx, s));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
