@@ -177,7 +177,7 @@ int f3_block_out(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);
 int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
-int f3_bn_bwd_parts(int N, int TV);  // Gpart rows f3_bn_bwd_apply writes
+int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);  // out[c] += sum_r part[r][c]
 int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);

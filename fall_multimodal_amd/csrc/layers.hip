@@ -383,6 +383,11 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
 // ---------------------------------------------------------------------------
 F3_DEV int mix_stride(int Cin) { return Cin + 20; }
 
+// Frame inputs are prefetched into registers one frame ahead (kMixPX / kMixPZ 16-B pieces
+// per thread; larger frames load the remainder synchronously), so a workgroup's HBM
+// latency overlaps its MFMA work on the previous frame.
+constexpr int kMixPX = 2, kMixPZ = 4;
+
 __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -397,13 +402,35 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg) : 0.f;
   const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
-  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+  f32x4 rx[kMixPX];
+  auto prefetch = [&](int f) {
     const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
-    for (int i = tid; i < n4; i += 256) {
-      const int v = i / C4, c = (i - v * C4) * 4;
-      *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+#pragma unroll
+    for (int q = 0; q < kMixPX; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4) rx[q] = xg[i];
+    }
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame is done with xs / zs
+#pragma unroll
+    for (int q = 0; q < kMixPX; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4) {
+        const int v = i / C4, c = (i - v * C4) * 4;
+        *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
+      }
+    }
+    {
+      const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+      for (int i = tid + kMixPX * 256; i < n4; i += 256) {
+        const int v = i / C4, c = (i - v * C4) * 4;
+        *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+      }
     }
     __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
     for (int t = wave; t < tiles; t += 4) {
       const int ci0 = t * 16;
       f32x4 acc[4];
@@ -441,7 +468,6 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
         *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8 + 4) = u1;
       }
     }
-    // the next frame's first __syncthreads orders these zs reads before its zs writes
   }
 }
 
@@ -462,27 +488,61 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
   const int dmt = wave >> 1, dnt0 = 2 * (wave & 1);
   f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const int tiles = Cin / 16, n4x = V * Cin / 4, n4z = KV * Cin / 4, C4 = Cin / 4;
-  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
-    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
-    for (int i = tid; i < n4x; i += 256) {
-      const int v = i / C4, c = (i - v * C4) * 4;
-      *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+  const bool zb16 = a.dzb != nullptr;
+  f32x4 rx[kMixPX];
+  f32x4 rz[kMixPZ];  // bf16 pieces travel as 8 bytes in .xy
+  auto zpiece = [&](int f, int i) -> f32x4 {
+    if (zb16) {
+      const bf16x4 u = reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.dzb) + (size_t)f * KV * Cin)[i];
+      return f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
     }
-    if (a.dzb) {
-      const bf16x4* zg = reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.dzb) + (size_t)f * KV * Cin);
-      for (int i = tid; i < n4z; i += 256) {
-        const int wk = i / C4, c = (i - wk * C4) * 4;
-        const bf16x4 u = zg[i];
-        *reinterpret_cast<f32x4*>(zs + wk * S + c) = f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
+    return reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * Cin)[i];
+  };
+  auto prefetch = [&](int f) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+#pragma unroll
+    for (int q = 0; q < kMixPX; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4x) rx[q] = xg[i];
+    }
+#pragma unroll
+    for (int q = 0; q < kMixPZ; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4z) rz[q] = zpiece(f, i);
+    }
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame is done with xs / zs
+#pragma unroll
+    for (int q = 0; q < kMixPX; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4x) {
+        const int v = i / C4, c = (i - v * C4) * 4;
+        *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
       }
-    } else {
-      const f32x4* zg = reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * Cin);
-      for (int i = tid; i < n4z; i += 256) {
+    }
+#pragma unroll
+    for (int q = 0; q < kMixPZ; ++q) {
+      const int i = tid + q * 256;
+      if (i < n4z) {
         const int wk = i / C4, c = (i - wk * C4) * 4;
-        *reinterpret_cast<f32x4*>(zs + wk * S + c) = zg[i];
+        *reinterpret_cast<f32x4*>(zs + wk * S + c) = rz[q];
+      }
+    }
+    {
+      const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+      for (int i = tid + kMixPX * 256; i < n4x; i += 256) {
+        const int v = i / C4, c = (i - v * C4) * 4;
+        *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
+      }
+      for (int i = tid + kMixPZ * 256; i < n4z; i += 256) {
+        const int wk = i / C4, c = (i - wk * C4) * 4;
+        *reinterpret_cast<f32x4*>(zs + wk * S + c) = zpiece(f, i);
       }
     }
     __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
     // dX_f[v][ci] = sum_wk A~[v][wk] dZ_f[wk][ci]
     for (int t = wave; t < tiles; t += 4) {
       const int ci0 = t * 16;
@@ -520,13 +580,13 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
           const f32x4 zb = wk < KV ? *reinterpret_cast<const f32x4*>(zs + wk * S + c16 + 4 * fg)
                                    : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < 4; ++s) dacc[q] = mfma16x4(xa[s], zb[s], dacc[q]);
+          for (int s2 = 0; s2 < 4; ++s2) dacc[q] = mfma16x4(xa[s2], zb[s2], dacc[q]);
         }
       }
     }
-    __syncthreads();
   }
   // workgroup partial row of dA (each (v, wk) has exactly one owner lane), then f3_colsum
+  __syncthreads();
   float* red = sm;
   for (int i = tid; i < KVV; i += 256) red[i] = 0.f;
   __syncthreads();
@@ -791,13 +851,18 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   }
 }
 
-// BN1 backward: dg = g1*rs1*(dv - S1/M - xhat1*S2/M); G[v][c] += dg (gcn bias grad)
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
+// BN1 backward: dg = g1*rs1*(dv - S1/M - xhat1*S2/M), and the per-node column sums
+// G[v][c] = sum_{n,t} dg (gcn bias / edge-importance gradients). One workgroup per
+// (clip, kBnBwdFrames frames); thread (v, 8-channel group) walks the frames, so each
+// thread owns its G entries (no atomics) and a frame [V][C] is read contiguously. Each
+// workgroup writes one partial row [V][C]; f3_colsum adds the rows into G.
+constexpr int kBnBwdFrames = 4;
+
+__global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __shared__ float mu[256], kk[256], m1[256], m2[256], rsv[256];
-  extern __shared__ __attribute__((aligned(16))) float gl[];  // [V][C]
-  const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
+  const int C = a.C, CG = C / 8, V = a.V, T = a.TV / V, tid = threadIdx.x;
   const float invM = 1.f / (float)a.bn.count;
-  for (int c = tid; c < C; c += 256) {
+  for (int c = tid; c < C; c += blockDim.x) {
     float sc, sh, rs;
     bn_coeff(a.bn, c, sc, sh, mu[c], rs);
     rsv[c] = rs;
@@ -805,43 +870,47 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
     m1[c] = (float)a.bsum[c] * invM;
     m2[c] = (float)a.bsq[c] * invM;
   }
-  for (int i = tid; i < a.V * C; i += 256) gl[i] = 0.f;
   __syncthreads();
   if (blockIdx.x == 0 && blockIdx.y == 0) {
-    for (int c = tid; c < C; c += 256) {
+    for (int c = tid; c < C; c += blockDim.x) {
       a.dgamma[c] += (float)a.bsq[c];
       a.dbeta[c] += (float)a.bsum[c];
     }
   }
-  int r0, r1;
-  chunk_rows(a.TV, a.chunks, r0, r1);
-  const int cq = tid % C4, c0 = cq * 4;
-  for (int m = r0 + tid / C4; m < r1; m += RP) {
-    const size_t off = (size_t)m * C + c0;
-    const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dv + off);
-    const f32x4 g = *reinterpret_cast<const f32x4*>(a.g + off);
-    f32x4 o;
-    const int v = m % a.V;
+  const int v = tid / CG, c0 = (tid - v * CG) * 8;
+  if (v >= V) return;
+  const int n = blockIdx.y, t0 = blockIdx.x * kBnBwdFrames, t1 = min(T, t0 + kBnBwdFrames);
+  float acc[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int t = t0; t < t1; ++t) {
+    const size_t off = ((size_t)(n * T + t) * V + v) * C + c0;
+    const f32x4 d0 = *reinterpret_cast<const f32x4*>(a.dv + off);
+    const f32x4 d1 = *reinterpret_cast<const f32x4*>(a.dv + off + 4);
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.g + off);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(a.g + off + 4);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
       const int c = c0 + e;
-      const float xh = (g[e] - mu[c]) * rsv[c];
-      o[e] = kk[c] * (dv[e] - m1[c] - xh * m2[c]);
-      atomicAdd(&gl[v * C + c], o[e]);
+      const float dv = e < 4 ? d0[e] : d1[e - 4];
+      const float gv = e < 4 ? g0[e] : g1[e - 4];
+      o[e] = kk[c] * (dv - m1[c] - (gv - mu[c]) * rsv[c] * m2[c]);
+      acc[e] += o[e];
     }
     if (a.dgb) {
-      bf16x4 ob;
+      bf16x8 ob;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
+      for (int e = 0; e < 8; ++e) ob[e] = (__bf16)o[e];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
     } else {
-      *reinterpret_cast<f32x4*>(a.dg + off) = o;
+      *reinterpret_cast<f32x4*>(a.dg + off) = f32x4{o[0], o[1], o[2], o[3]};
+      *reinterpret_cast<f32x4*>(a.dg + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
     }
   }
-  __syncthreads();
-  // one partial row per workgroup (plain stores); f3_colsum adds the rows into G
-  float* row = a.Gpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * a.V * C;
-  for (int i = tid; i < a.V * C; i += 256) row[i] = gl[i];
+  float* row = a.Gpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * V * C + v * C + c0;
+  *reinterpret_cast<f32x4*>(row) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<f32x4*>(row + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
 // u = relu(g * scale + shift) in bf16 (BN1 + ReLU of the tcn input, bf16 mode)
@@ -1029,24 +1098,62 @@ __global__ __launch_bounds__(256) void ca_bwd2_kernel(CaArgs a) {
     a.g_bnca_beta[j] += s1;
     a.g_b1[j] += db1;
   }
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float mu, rs;
-    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
+  (void)dq1s; (void)hs; (void)sc2; (void)sh2;
+}
+
+// channel-attention weight gradients as small GEMMs over the batch, one workgroup per
+// (64 channels, kCaWClips clips): gW1[j][c] += sum_n dq1[n][j] gapn[n][c];
+// gW2[c][j] += sum_n dq2[n][c] hid[n][j];  gb2[c] += sum_n dq2[n][c]
+constexpr int kCaWClips = 8;
+__global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
+  __shared__ float dq1s[64][64];  // rows 0..31: dq1 tile, rows 32..63: hid tile; then the gW2 transpose
+  float (*hs)[64] = dq1s + 32;
+  const int C = a.C, H = C / 4, N = a.N;
+  const int cl = threadIdx.x & 63, jg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, n0 = blockIdx.y * kCaWClips, n1 = min(N, n0 + kCaWClips);
+  for (int i = threadIdx.x; i < kCaWClips * H; i += 256) {
+    const int nn = i / H, j = i - nn * H, n = n0 + nn;
+    dq1s[nn][j] = n < n1 ? a.dq1[(size_t)n * H + j] : 0.f;
+    hs[nn][j] = n < n1 ? a.hid[(size_t)n * H + j] : 0.f;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float w1g = 0.f, w2g = 0.f, b2g = 0.f;
-    for (int n = 0; n < N; ++n) {
-      const float gap = a.gapsum[(size_t)n * C + c] * a.inv_tv * sc2[c] + sh2[c];
-      w1g += dq1s[n] * gap;
-      const float d2 = a.dq2[(size_t)n * C + c];
-      w2g += d2 * hs[n];
-      b2g += d2;
+  const bool cok = c < C;
+  float sc = 0.f, sh = 0.f, mu, rs;
+  if (cok) bn_coeff(a.bn2, c, sc, sh, mu, rs);
+  float w1[16], w2[16], b2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) w1[q] = w2[q] = 0.f;
+  for (int n = n0; n < n1 && cok; ++n) {
+    const float gap = a.gapsum[(size_t)n * C + c] * a.inv_tv * sc + sh;
+    const float d2 = a.dq2[(size_t)n * C + c];
+    b2 += d2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = jg + 4 * q;
+      if (j < H) {
+        w1[q] += dq1s[n - n0][j] * gap;
+        w2[q] += d2 * hs[n - n0][j];
+      }
     }
-    a.g_W1[(size_t)j * C + c] += w1g;
-    a.g_W2[(size_t)c * H + j] += w2g;
-    if (j == 0) a.g_b2[c] += b2g;
   }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = jg + 4 * q;
+    if (j < H && cok) atomic_add_f(a.g_W1 + (size_t)j * C + c, w1[q]);  // lanes: consecutive c
+  }
+  if (jg == 0 && cok) atomic_add_f(a.g_b2 + c, b2);
+  // gW2 rows c0..c0+63 are one contiguous [64][H] block: transpose through LDS so the
+  // atomics go out lane-contiguous
+  float* t2 = &dq1s[0][0];  // 32*64 floats >= 64*H/2; use both arrays (64*H <= 4096)
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = jg + 4 * q;
+    if (j < H) t2[cl * H + j] = w2[q];
+  }
+  __syncthreads();
+  const int c0 = blockIdx.x * 64, nc = min(64, C - c0);
+  for (int e = threadIdx.x; e < nc * H; e += 256) atomic_add_f(a.g_W2 + (size_t)c0 * H + e, t2[e]);
 }
 
 // per clip: dgap = W1^T dq1 ; e = dgap/TV ; BN2 backward sums D1, D2
@@ -1212,14 +1319,15 @@ int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_bn_bwd_parts(int N, int TV) { return chunks_for(TV) * N; }
+int f3_bn_bwd_parts(int N, int TV, int V) { return ((TV / V + kBnBwdFrames - 1) / kBnBwdFrames) * N; }
 
 int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
-  if (a.C % 4 || a.C > 256 || 256 % (a.C / 4) || (size_t)a.V * a.C * 4 > 60 * 1024 || !a.Gpart) return F3_EINVAL;
-  a.chunks = chunks_for(a.TV);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(a.chunks, a.N), dim3(256), (size_t)a.V * a.C * 4, s, a);
+  if (a.C % 8 || a.C > 256 || a.TV % a.V || a.V * (a.C / 8) > 1024 || !a.Gpart) return F3_EINVAL;
+  const int T = a.TV / a.V, fch = (T + kBnBwdFrames - 1) / kBnBwdFrames;
+  const int threads = ((a.V * (a.C / 8) + 63) / 64) * 64;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(fch, a.N), dim3(threads), 0, s, a);
   F3_LAUNCH_CHECK();
-  return f3_colsum(a.Gpart, a.chunks * a.N, a.V * a.C, a.G, s);
+  return f3_colsum(a.Gpart, fch * a.N, a.V * a.C, a.G, s);
 }
 
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) {
@@ -1252,6 +1360,8 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(ca_bwd1_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, (a->N + kCaWClips - 1) / kCaWClips), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd3_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();

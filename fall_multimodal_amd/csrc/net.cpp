@@ -377,7 +377,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       xin = X.out;
       xinb = nullptr;
       if (hb && l + 1 < 7 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(Mo * C);
-      maxG = std::max(maxG, (size_t)f3_bn_bwd_parts(N, L.T_in * V) * V * C);
+      maxG = std::max(maxG, (size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
