@@ -172,6 +172,7 @@ int f3_databn_fwd(const f3::DataBnArgs* a, hipStream_t s);
 int f3_databn_bwd(const f3::DataBnArgs* a, hipStream_t s);
 int f3_mix_fwd(const f3::MixArgs* a, hipStream_t s);
 int f3_mix_bwd(const f3::MixArgs* a, hipStream_t s);
+bool f3_mix_lds_ok(int K, int V, int Cin);  // the LDS/MFMA mix path (takes bf16 dZ)
 int f3_gcn_bias_bwd(const f3::GcnBiasBwdArgs* a, hipStream_t s);
 int f3_block_out(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);

@@ -238,142 +238,6 @@ F3_DEV float atil(const float* A, int K, int V, int wk, int v) {
   return A[(k * V + v) * V + w];
 }
 
-__global__ __launch_bounds__(256) void mix_fwd_mfma_kernel(MixArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
-  const int ksteps = (V + 3) / 4;  // <= 8
-  float af[4][8];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg) : 0.f;
-  const int ctiles = Cin / 16;
-  const long long items = (long long)a.frames * ctiles;
-  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
-    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
-    const float* x = a.x + (size_t)f * V * Cin + ci0 + fr;
-    f32x4 acc[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (ks >= ksteps) break;
-      const int v = 4 * ks + fg;
-      const float b = v < V ? x[(size_t)v * Cin] : 0.f;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b, acc[mt]);
-    }
-    const size_t zoff = (size_t)f * KV * Cin + ci0 + fr;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int wk = 16 * mt + 4 * fg + r;
-        if (wk >= KV) continue;
-        if (a.zb) reinterpret_cast<__bf16*>(a.zb)[zoff + (size_t)wk * Cin] = (__bf16)acc[mt][r];
-        else a.z[zoff + (size_t)wk * Cin] = acc[mt][r];
-      }
-  }
-}
-
-__global__ __launch_bounds__(256) void mix_dx_mfma_kernel(MixArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V;
-  const int ksteps = (KV + 3) / 4;  // <= 16
-  float af[2][16];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 4 * ks + fg, 16 * mt + fr) : 0.f;
-  const int ctiles = Cin / 16;
-  const long long items = (long long)a.frames * ctiles;
-  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
-    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
-    const float* dz = a.z + (size_t)f * KV * Cin + ci0 + fr;
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      if (ks >= ksteps) break;
-      const int wk = 4 * ks + fg;
-      const float b = wk < KV ? dz[(size_t)wk * Cin] : 0.f;
-      acc[0] = mfma16x4(af[0][ks], b, acc[0]);
-      acc[1] = mfma16x4(af[1][ks], b, acc[1]);
-    }
-    float* dx = a.dx + (size_t)f * V * Cin + ci0 + fr;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = 16 * mt + 4 * fg + r;
-        if (v < V) {
-          float* d = dx + (size_t)v * Cin;
-          if (a.accumulate) *d += acc[mt][r];
-          else *d = acc[mt][r];
-        }
-      }
-  }
-}
-
-// dA partials: each workgroup reduces its 4 waves in LDS and writes ONE row of
-// part[gridDim.x][K*V*V]; mix_dA_reduce adds the rows into dA. (Global float atomics run at
-// the memory side and crawl when every workgroup hits the same few rows.)
-__global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
-  __shared__ float red[1024];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, KVV = KV * V;
-  for (int i = threadIdx.x; i < KVV; i += 256) red[i] = 0.f;
-  const int ctiles = Cin / 16;
-  const long long items = (long long)a.frames * ctiles;
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (long long it = (long long)blockIdx.x * 4 + wave; it < items; it += (long long)gridDim.x * 4) {
-    const int f = (int)(it / ctiles), ci0 = (int)(it - (long long)f * ctiles) * 16;
-    const float* x = a.x + (size_t)f * V * Cin + ci0 + 4 * fg;
-    const float* dz = a.z + (size_t)f * KV * Cin + ci0 + 4 * fg;
-    f32x4 xa[2], zb[4];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int v = 16 * mt + fr;
-      xa[mt] = v < V ? *reinterpret_cast<const f32x4*>(x + (size_t)v * Cin) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int wk = 16 * nt + fr;
-      zb[nt] = wk < KV ? *reinterpret_cast<const f32x4*>(dz + (size_t)wk * Cin) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x4(xa[mt][s], zb[nt][s], acc[mt][nt]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int v = 16 * mt + 4 * fg + r;
-      if (v >= V) continue;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int wk = 16 * nt + fr;
-        if (wk >= KV) continue;
-        const int w = wk / K, k = wk - w * K;
-        atomicAdd(&red[(k * V + v) * V + w], acc[mt][nt][r]);  // LDS
-      }
-    }
-  __syncthreads();
-  float* row = a.part + (size_t)blockIdx.x * KVV;
-  for (int i = threadIdx.x; i < KVV; i += 256) row[i] = red[i];
-}
-
 // ---------------------------------------------------------------------------
 // LDS-staged graph mix (Cin % 16 == 0, K*V <= 64, V <= 32): one frame at a time per
 // workgroup, the frame's [V][Cin] input (and [K*V][Cin] gradient) loaded with coalesced
@@ -381,26 +245,39 @@ __global__ __launch_bounds__(256) void mix_dA_mfma_kernel(MixArgs a) {
 // reads), fp32 MFMA 16x16x4 with the fixed A~ fragments in registers, outputs written
 // back through LDS as whole rows. The backward computes dX and dA from ONE read of dZ.
 // ---------------------------------------------------------------------------
-F3_DEV int mix_stride(int Cin) { return Cin + 20; }
 
-// Frame inputs are prefetched into registers one frame ahead (kMixPX / kMixPZ 16-B pieces
-// per thread; larger frames load the remainder synchronously), so a workgroup's HBM
-// latency overlaps its MFMA work on the previous frame.
-constexpr int kMixPX = 2, kMixPZ = 4;
+// Frame inputs are prefetched into registers one frame ahead as RAW 16-B / 8-B pieces
+// (converted only when written to LDS, so the loads stay in flight during the previous
+// frame's MFMAs); MFMA operand reads from LDS are unconditional (clamped row + 0/1 mask)
+// so the compiler batches them.
+// per-thread prefetch capacity (16-B x pieces / 8-B bf16 gradient pieces) for V <= 18, K <= 3
+template <int CIN> struct MixCap {
+  static constexpr int PX = (18 * CIN + 1023) / 1024;
+  static constexpr int PZ = (54 * CIN + 1023) / 1024;
+};
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+F3_DEV f32x4 bf4_to_f4(u32x2 r) {
+  return f32x4{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+               __uint_as_float(r.y & 0xffff0000u)};
+}
+
+template <int KS, int CIN>  // k steps over v: ceil(V/4); compile-time so the A~ fragments stay in registers
 __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
+  constexpr int kMixPX = MixCap<CIN>::PX;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, S = mix_stride(Cin), SZ = Cin + 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  constexpr int Cin = CIN, S = CIN + 20, SZ = CIN + 4;
   float* xs = sm;                 // [V][S]
   float* zs = sm + V * S;         // [KV][SZ]
-  const int ksteps = (V + 3) / 4;  // <= 8
-  float af[4][8];
+  float af[4][KS];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) af[mt][ks] = ks < ksteps ? atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg) : 0.f;
+    for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg);
   const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
   f32x4 rx[kMixPX];
   auto prefetch = [&](int f) {
@@ -422,13 +299,6 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
         *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
       }
     }
-    {
-      const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
-      for (int i = tid + kMixPX * 256; i < n4; i += 256) {
-        const int v = i / C4, c = (i - v * C4) * 4;
-        *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
-      }
-    }
     __syncthreads();
     if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
     for (int t = wave; t < tiles; t += 4) {
@@ -436,14 +306,16 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
       f32x4 acc[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float b[KS];
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        if (ks >= ksteps) break;
+      for (int ks = 0; ks < KS; ++ks) {
         const int v = 4 * ks + fg;
-        const float b = v < V ? xs[v * S + ci0 + fr] : 0.f;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b, acc[mt]);
+        b[ks] = xs[min(v, V - 1) * S + ci0 + fr] * (v < V ? 1.f : 0.f);
       }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b[ks], acc[mt]);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -471,74 +343,87 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
   }
 }
 
+template <int KS, int CIN, bool ZB16>  // k steps over (w,k): ceil(K*V/4); ZB16: dZ is bf16
 __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
+  constexpr int kMixPX = MixCap<CIN>::PX, kMixPZ = MixCap<CIN>::PZ;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, Cin = a.Cin, KV = K * V, KVV = KV * V, S = mix_stride(Cin);
+  const int K = a.K, V = a.V, KV = K * V, KVV = KV * V;
+  constexpr int Cin = CIN, S = CIN + 20;
   float* xs = sm;            // [V][S]
   float* zs = sm + V * S;    // [KV][S]
-  const int ksteps = (KV + 3) / 4;  // <= 16
-  float adx[2][16];
+  float* ds = zs + KV * S;   // [V][S] current dx (accumulate: identity-residual gradient)
+  float adx[2][KS];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) adx[mt][ks] = ks < ksteps ? atil(a.A, K, V, 4 * ks + fg, 16 * mt + fr) : 0.f;
+    for (int ks = 0; ks < KS; ++ks) adx[mt][ks] = atil(a.A, K, V, 4 * ks + fg, 16 * mt + fr);
   // dA tiles of this wave: (mt, nt) = (wave >> 1, 2*(wave & 1) + {0,1}) over [32 v][64 wk]
   const int dmt = wave >> 1, dnt0 = 2 * (wave & 1);
   f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const int tiles = Cin / 16, n4x = V * Cin / 4, n4z = KV * Cin / 4, C4 = Cin / 4;
-  const bool zb16 = a.dzb != nullptr;
-  f32x4 rx[kMixPX];
-  f32x4 rz[kMixPZ];  // bf16 pieces travel as 8 bytes in .xy
-  auto zpiece = [&](int f, int i) -> f32x4 {
-    if (zb16) {
-      const bf16x4 u = reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.dzb) + (size_t)f * KV * Cin)[i];
-      return f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
-    }
-    return reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * Cin)[i];
-  };
+  constexpr bool zb16 = ZB16;
+  f32x4 rx[kMixPX], rd[kMixPX];
+  u32x2 rz[ZB16 ? kMixPZ : 1];  // bf16 gradient pieces, raw
   auto prefetch = [&](int f) {
     const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
+    const f32x4* dg = reinterpret_cast<const f32x4*>(a.dx + (size_t)f * V * Cin);
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
       const int i = tid + q * 256;
-      if (i < n4x) rx[q] = xg[i];
+      if (i < n4x) {
+        rx[q] = xg[i];
+        if (a.accumulate) rd[q] = dg[i];
+      }
     }
+    if constexpr (zb16) {
+      const u32x2* zg = reinterpret_cast<const u32x2*>(a.dzb + (size_t)f * KV * Cin);
 #pragma unroll
-    for (int q = 0; q < kMixPZ; ++q) {
-      const int i = tid + q * 256;
-      if (i < n4z) rz[q] = zpiece(f, i);
+      for (int q = 0; q < kMixPZ; ++q) {
+        const int i = tid + q * 256;
+        if (i < n4z) rz[q] = zg[i];
+      }
     }
   };
   if (blockIdx.x < a.frames) prefetch(blockIdx.x);
   for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
-    __syncthreads();  // the previous frame is done with xs / zs
+    __syncthreads();  // the previous frame is done with xs / zs / ds
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
       const int i = tid + q * 256;
       if (i < n4x) {
         const int v = i / C4, c = (i - v * C4) * 4;
         *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
+        if (a.accumulate) *reinterpret_cast<f32x4*>(ds + v * S + c) = rd[q];
       }
     }
+    if constexpr (zb16) {
 #pragma unroll
-    for (int q = 0; q < kMixPZ; ++q) {
-      const int i = tid + q * 256;
-      if (i < n4z) {
-        const int wk = i / C4, c = (i - wk * C4) * 4;
-        *reinterpret_cast<f32x4*>(zs + wk * S + c) = rz[q];
+      for (int q = 0; q < kMixPZ; ++q) {
+        const int i = tid + q * 256;
+        if (i < n4z) {
+          const int wk = i / C4, c = (i - wk * C4) * 4;
+          *reinterpret_cast<f32x4*>(zs + wk * S + c) = bf4_to_f4(rz[q]);
+        }
       }
-    }
-    {
-      const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
-      for (int i = tid + kMixPX * 256; i < n4x; i += 256) {
-        const int v = i / C4, c = (i - v * C4) * 4;
-        *reinterpret_cast<f32x4*>(xs + v * S + c) = xg[i];
-      }
-      for (int i = tid + kMixPZ * 256; i < n4z; i += 256) {
-        const int wk = i / C4, c = (i - wk * C4) * 4;
-        *reinterpret_cast<f32x4*>(zs + wk * S + c) = zpiece(f, i);
+    } else {  // fp32 mode: load the gradient frame now (batched: all loads, then the writes)
+      const f32x4* zg = reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * Cin);
+      for (int i0 = 0; i0 < n4z; i0 += 8 * 256) {
+        f32x4 tmp[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = i0 + tid + q * 256;
+          if (i < n4z) tmp[q] = zg[i];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = i0 + tid + q * 256;
+          if (i < n4z) {
+            const int wk = i / C4, c = (i - wk * C4) * 4;
+            *reinterpret_cast<f32x4*>(zs + wk * S + c) = tmp[q];
+          }
+        }
       }
     }
     __syncthreads();
@@ -547,13 +432,16 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
     for (int t = wave; t < tiles; t += 4) {
       const int ci0 = t * 16;
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      float b[KS];
 #pragma unroll
-      for (int ks = 0; ks < 16; ++ks) {
-        if (ks >= ksteps) break;
+      for (int ks = 0; ks < KS; ++ks) {
         const int wk = 4 * ks + fg;
-        const float b = wk < KV ? zs[wk * S + ci0 + fr] : 0.f;
-        acc[0] = mfma16x4(adx[0][ks], b, acc[0]);
-        acc[1] = mfma16x4(adx[1][ks], b, acc[1]);
+        b[ks] = zs[min(wk, KV - 1) * S + ci0 + fr] * (wk < KV ? 1.f : 0.f);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        acc[0] = mfma16x4(adx[0][ks], b[ks], acc[0]);
+        acc[1] = mfma16x4(adx[1][ks], b[ks], acc[1]);
       }
       float* dx = a.dx + (size_t)f * V * Cin + ci0 + fr;
 #pragma unroll
@@ -561,26 +449,27 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int v = 16 * mt + 4 * fg + r;
-          if (v < V) {
-            float* d = dx + (size_t)v * Cin;
-            if (a.accumulate) *d += acc[mt][r];
-            else *d = acc[mt][r];
-          }
+          if (v < V) dx[(size_t)v * Cin] = acc[mt][r] + (a.accumulate ? ds[v * S + ci0 + fr] : 0.f);
         }
     }
     // dA[v][wk] += sum_ci X_f[v][ci] dZ_f[wk][ci]   (k index of the MFMA = lane group,
     // the 4 components of each b128 read are 4 k-steps)
     {
       const int v = 16 * dmt + fr;
+      const float mv = v < V ? 1.f : 0.f;
+      const float* xrow = xs + min(v, V - 1) * S + 4 * fg;
+      const int wk0 = 16 * dnt0 + fr, wk1 = wk0 + 16;
+      const float m0 = wk0 < KV ? 1.f : 0.f, m1 = wk1 < KV ? 1.f : 0.f;
+      const float* z0 = zs + min(wk0, KV - 1) * S + 4 * fg;
+      const float* z1 = zs + min(wk1, KV - 1) * S + 4 * fg;
       for (int c16 = 0; c16 < Cin; c16 += 16) {
-        const f32x4 xa = v < V ? *reinterpret_cast<const f32x4*>(xs + v * S + c16 + 4 * fg) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 xa = *reinterpret_cast<const f32x4*>(xrow + c16) * mv;
+        const f32x4 za = *reinterpret_cast<const f32x4*>(z0 + c16) * m0;
+        const f32x4 zb = *reinterpret_cast<const f32x4*>(z1 + c16) * m1;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int wk = 16 * (dnt0 + q) + fr;
-          const f32x4 zb = wk < KV ? *reinterpret_cast<const f32x4*>(zs + wk * S + c16 + 4 * fg)
-                                   : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) dacc[q] = mfma16x4(xa[s2], zb[s2], dacc[q]);
+        for (int s2 = 0; s2 < 4; ++s2) {
+          dacc[0] = mfma16x4(xa[s2], za[s2], dacc[0]);
+          dacc[1] = mfma16x4(xa[s2], zb[s2], dacc[1]);
         }
       }
     }
@@ -1234,25 +1123,42 @@ static void allow_big_lds(const void* fn) {
   (void)hipGetLastError();  // a refused attribute must not surface as the next launch's error
 }
 
-static bool mix_mfma_ok(const MixArgs& a) { return a.Cin % 16 == 0 && a.K * a.V <= 64 && a.V <= 32; }
-
 static size_t mix_lds_fwd2(const MixArgs& a) {
   return sizeof(float) * ((size_t)a.V * (a.Cin + 20) + (size_t)a.K * a.V * (a.Cin + 4));
 }
 static size_t mix_lds_bwd2(const MixArgs& a) {
-  return sizeof(float) * std::max((size_t)(a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
+  return sizeof(float) * std::max((size_t)(2 * a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
 }
 
+template <int KS, int CIN>
+static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
+  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN>), true);
+  (void)once;
+  const int grid = std::min(a->frames, 1024);  // resident workgroups loop over frames
+  hipLaunchKernelGGL((mix_fwd_lds_kernel<KS, CIN>), dim3(grid), dim3(256), mix_lds_fwd2(*a), s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+template <int CIN>
+static int mix_fwd_ks(const MixArgs* a, hipStream_t s) {
+  switch ((a->V + 3) / 4) {
+    case 4: return launch_mix_fwd<4, CIN>(a, s);
+    case 5: return launch_mix_fwd<5, CIN>(a, s);
+    default: return -1;
+  }
+}
+
+// LDS path: V in {13..18}, K <= 3, Cin in {64, 128, 256}; else the generic kernel
+bool f3_mix_lds_ok(int K, int V, int Cin) {
+  return (Cin == 64 || Cin == 128 || Cin == 256) && K <= 3 && V >= 13 && V <= 18;
+}
+static bool mix_lds_ok(const MixArgs& a) { return f3_mix_lds_ok(a.K, a.V, a.Cin); }
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
-  if (mix_mfma_ok(*a)) {
-    static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel), true);
-    (void)once;
-    const size_t lds = mix_lds_fwd2(*a);
-    if (lds > 160 * 1024) return F3_EINVAL;
-    const int grid = std::min(a->frames, 4096);
-    hipLaunchKernelGGL(mix_fwd_lds_kernel, dim3(grid), dim3(256), lds, s, *a);
-    F3_LAUNCH_CHECK();
-    return F3_OK;
+  if (mix_lds_ok(*a)) {
+    const int r = a->Cin == 64 ? mix_fwd_ks<64>(a, s) : a->Cin == 128 ? mix_fwd_ks<128>(a, s) : mix_fwd_ks<256>(a, s);
+    if (r >= 0) return r;
   }
   static bool once = (allow_big_lds((const void*)mix_fwd_kernel), true);
   (void)once;
@@ -1263,18 +1169,41 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
-  if (mix_mfma_ok(*a)) {
-    if (!a->part) return F3_EINVAL;
-    static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel), true);
-    (void)once;
-    const size_t lds = mix_lds_bwd2(*a);
-    if (lds > 160 * 1024) return F3_EINVAL;
-    const int grid = std::min(a->frames, kMixParts);
-    hipLaunchKernelGGL(mix_bwd_lds_kernel, dim3(grid), dim3(256), lds, s, *a);
-    F3_LAUNCH_CHECK();
-    return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
+template <int KS, int CIN, bool ZB16>
+static int launch_mix_bwd(const MixArgs* a, hipStream_t s) {
+  static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16>), true);
+  (void)once;
+  const int grid = std::min(a->frames, 768);  // resident workgroups loop over frames
+  hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
+  F3_LAUNCH_CHECK();
+  return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
+}
+
+template <int CIN, bool ZB16>
+static int mix_bwd_ks(const MixArgs* a, hipStream_t s) {
+  switch ((a->K * a->V + 3) / 4) {
+    case 4: return launch_mix_bwd<4, CIN, ZB16>(a, s);
+    case 5: return launch_mix_bwd<5, CIN, ZB16>(a, s);
+    case 7: return launch_mix_bwd<7, CIN, ZB16>(a, s);
+    case 9: return launch_mix_bwd<9, CIN, ZB16>(a, s);
+    case 11: return launch_mix_bwd<11, CIN, ZB16>(a, s);
+    case 14: return launch_mix_bwd<14, CIN, ZB16>(a, s);
+    default: return -1;
   }
+}
+
+template <int CIN>
+static int mix_bwd_cin(const MixArgs* a, hipStream_t s) {
+  return a->dzb ? mix_bwd_ks<CIN, true>(a, s) : mix_bwd_ks<CIN, false>(a, s);
+}
+
+int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
+  if (mix_lds_ok(*a)) {
+    if (!a->part) return F3_EINVAL;
+    const int r = a->Cin == 64 ? mix_bwd_cin<64>(a, s) : a->Cin == 128 ? mix_bwd_cin<128>(a, s) : mix_bwd_cin<256>(a, s);
+    if (r >= 0) return r;
+  }
+  if (a->dzb) return F3_EINVAL;  // the generic kernel reads fp32 dZ
   static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
   (void)once;
   if (a->K * a->V * a->V > 1024 || mix_lds(*a, true) > 160 * 1024) return F3_EINVAL;

@@ -682,7 +682,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : W.dg; gd.inb = bfa(W.dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
-    const bool dzb = hb && Ci % 16 == 0 && K * V <= 64 && V <= 32;  // bf16 dZ feeds the LDS graph-mix backward
+    const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
       if (!f3_igemm_ok(gd)) return F3_EINVAL;
       gd.outb = bfa(W.dZ, 1);

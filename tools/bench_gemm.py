@@ -12,6 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import fall_multimodal_amd._lib as L  # noqa: E402
 
 SHAPES = [  # (name, N, T_in, V, Cin, Cout, KT, stride, pad)
+    ("plain4k", 1, 4096, 1, 4096, 4096, 1, 1, 0),   # a plain 4096^3 GEMM (structure ceiling)
     ("tcn l1", 256, 30, 18, 64, 64, 9, 1, 4),
     ("tcn l3", 256, 30, 18, 128, 128, 9, 2, 4),
     ("tcn l4", 256, 15, 18, 128, 128, 9, 1, 4),
@@ -42,7 +43,10 @@ def main():
     d = torch.device("cuda")
     st = L.stream_handle()
     print(f"{'shape':8s} {'prec':12s} {'fwd us':>8s} {'TF':>6s} {'dgrad us':>9s} {'TF':>6s} {'wgrad us':>9s} {'TF':>6s}")
+    only = os.environ.get("BENCH_GEMM_ONLY")
     for name, N, T, V, Ci, Co, KT, s, p in SHAPES:
+        if only and name not in only.split(","):
+            continue
         To = (T + 2 * p - KT) // s + 1
         flop = 2.0 * N * To * V * Co * KT * Ci
         x32 = torch.randn(N, T, V, Ci, device=d)
@@ -54,7 +58,8 @@ def main():
         dw = torch.empty(Co, Ci, KT, device=d)
         db = torch.empty(Co, device=d)
         wp = torch.empty(Co * KT * Ci, device=d)
-        for prec, pname in ((0, "fp32"), (2, "bf16_fp32in"), (1, "bf16")):
+        precs = ((1, "bf16"),) if os.environ.get("BENCH_GEMM_BF16_ONLY") else ((0, "fp32"), (2, "bf16_fp32in"), (1, "bf16"))
+        for prec, pname in precs:
             x = x32.to(torch.bfloat16) if prec == 1 else x32
             dy = dy32.to(torch.bfloat16) if prec == 1 else dy32
             L.check(lib.f3_conv_forward(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(wp), N, T, V, Ci, Co, KT, s,
