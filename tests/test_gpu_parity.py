@@ -304,20 +304,23 @@ def test_bf16_step_tracks_oracle():
 @pytest.mark.slow
 def test_top1_accuracy_parity():
     """BASELINE metric's 'top-1 acc parity': the oracle (reference algorithm, CPU fp32), the
-    fp32 HIP path and the bf16 HIP path trained identically (same init, same 4 synthetic
-    batches cycled for 24 RMSprop steps, B=32) reach the same held-out top-1 accuracy
-    (eval-mode forward on 256 fresh clips) within 5 points."""
+    fp32 HIP path and the bf16 HIP path trained identically (same init, same 8 synthetic
+    batches cycled for 36 RMSprop steps, B=32) reach the same held-out top-1 accuracy
+    (eval-mode forward on 256 fresh clips, through the BN running statistics) within 6
+    points. Eval-mode accuracy needs the running statistics (momentum 0.1) to move off
+    their init: the oracle measured 0.09 / 0.11 / 0.30 / 0.41 held-out accuracy after
+    12 / 24 / 36 / 48 steps (chance 0.09)."""
     d = dev()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    layout, S, B, steps = "coco_mmpose", 6, 32, 24
+    layout, S, B, steps, nb = "coco_mmpose", 6, 32, 36, 8
     spec = oc.Spec(model="two_stgcan_bilstm", layout=layout, num_class=11, sensor_dim=S)
-    batches = [synthetic_batch(B, 18, 11, S, 500 + i) for i in range(4)]
+    batches = [synthetic_batch(B, 18, 11, S, 500 + i) for i in range(nb)]
     test_sk, test_se, test_lb = synthetic_batch(256, 18, 11, S, 999)
     truth = test_lb.argmax(1)
     st = oc.init_state(spec, 123)
     sq = {k: torch.zeros_like(v) for k, v in st.items() if not oc.is_buffer(k)}
     for i in range(steps):
-        oc.train_step(st, spec, *(torch.from_numpy(x) for x in batches[i % 4]), sq=sq)
+        oc.train_step(st, spec, *(torch.from_numpy(x) for x in batches[i % nb]), sq=sq)
     with torch.no_grad():
         acc_ref = float((oc.forward(st, spec, torch.from_numpy(test_sk), torch.from_numpy(test_se),
                                     training=False).argmax(1).numpy() == truth).mean())
@@ -329,6 +332,6 @@ def test_top1_accuracy_parity():
             out = model(torch.from_numpy(test_sk).to(d), torch.from_numpy(test_se).to(d))
         accs[prec] = float((out.argmax(1).cpu().numpy() == truth).mean())
     print(f"held-out top-1: oracle {acc_ref:.3f}, fp32 {accs['fp32']:.3f}, bf16 {accs['bf16']:.3f}")
-    assert acc_ref > 1.5 / 11  # the task is learnable in this budget
+    assert acc_ref > 2.0 / 11  # the task is learnable in this budget
     for prec, acc in accs.items():
-        assert abs(acc - acc_ref) <= 0.05, (prec, acc, acc_ref)
+        assert abs(acc - acc_ref) <= 0.06, (prec, acc, acc_ref)
