@@ -44,6 +44,15 @@ F3_DEV int g_src_row(int n, int t, int v, int dt, const ConvGeom& g) {
 
 F3_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
+// Parity-split rows for a stride-2 input gradient (see igemm_bf16). Measured on MI355X (B=256,
+// V=18): tcn layer 5 (Kc=256) 162 -> 144 us, but layer 3 (Kc=128, 2 k-chunks per tap) 85 ->
+// 94 us — with short per-tap k loops the halved MFMA work does not pay for the wider row
+// footprint of a parity tile — so it is used from Kc >= 256, and for 1x1 convs (where the
+// odd rows need no work at all).
+__host__ __device__ inline bool igemm_parity(const ConvGeom& g) {
+  return g.transposed && g.S == 2 && (g.KT == 1 || g.Kc >= 256);
+}
+
 // bijective XCD-aware remap: consecutive logical tiles land on one XCD (shared A panels)
 F3_DEV int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -59,7 +68,7 @@ struct RowMap {
 
 F3_DEV RowMap rowmap(int m, const ConvGeom& g) {
   RowMap r;
-  if (m >= g.M) { r.base = -1; r.q = 0; return r; }
+  if (m < 0 || m >= g.M) { r.base = -1; r.q = 0; return r; }
   const int nt = m / g.V, v = m - nt * g.V, n = nt / g.T_out, t = nt - n * g.T_out;
   r.base = n * g.T_in * g.V + v;
   r.q = g.transposed ? t + g.P : t * g.S - g.P;
@@ -97,10 +106,30 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (g.Nc + BN - 1) / BN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // Stride-2 input gradient: an output row t only receives taps dt = t + P (mod 2), so the
+  // rows are split by the parity p of t (tiles of parity 0 first) and a tile walks only its
+  // parity's taps (5 or 4 of 9) instead of multiplying zero rows.
+  const bool par = igemm_parity(g);
+  int p = 0, Tp = g.T_out, Mp = g.M;
+  if (par) {
+    const int nclip = g.M / (g.T_out * g.V), T0 = (g.T_out + 1) >> 1;
+    const int tiles0 = ((nclip * T0 * g.V + BM - 1) / BM) * ntn;
+    Tp = T0;
+    if (tile >= tiles0) { p = 1; tile -= tiles0; Tp = g.T_out >> 1; }
+    Mp = nclip * Tp * g.V;
+  }
+  auto phys = [&](int r) -> int {  // logical row of this tile's parity class -> output row (-1: none)
+    if (r >= Mp) return -1;
+    if (!par) return r;
+    const int nt = r / g.V, v = r - nt * g.V, n = nt / Tp, tt = nt - n * Tp;
+    return (n * g.T_out + 2 * tt + p) * g.V + v;
+  };
   const int m0 = (tile / ntn) * BM, j0 = (tile % ntn) * BN;
   const int Ktot = g.KT * g.Kc;
-  const int nchunk = Ktot / G_BK;
+  const int kpt = g.Kc / G_BK;                    // k chunks per tap
+  const int dt0 = par ? ((p + g.P) & 1) : 0;      // first tap of this parity
+  const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
 
@@ -122,7 +151,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   for (int i = 0; i < A_INSTR; ++i) {
     const int rr = (wave * A_INSTR + i) * 8 + sub;
     a_c[i] = swz(rr, pch) * 8;
-    a_map[i] = rowmap(m0 + rr, g);
+    a_map[i] = rowmap(phys(m0 + rr), g);
   }
   const unsigned short* b_row[B_INSTR];
 #pragma unroll
@@ -135,8 +164,9 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   (void)b_step;
 
   auto stage = [&](int t, int buf) {
-    const int k0 = t * G_BK;
-    const int dt = k0 / g.Kc, i0 = k0 - dt * g.Kc;
+    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    const int dt = par ? dt0 + 2 * tap : tap;
+    const int k0 = dt * g.Kc + i0;
     char* sa = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
@@ -160,7 +190,12 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 #pragma unroll
     for (int y = 0; y < WN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (NST == 2) {
+  if (nchunk == 0) {
+    // a parity class with no taps (odd rows of a 1x1 stride-2 input gradient): zero rows,
+    // nothing to do at all when accumulating (uniform across the workgroup)
+    if (EPI & EPI_ADD) return;
+    __syncthreads();  // epilogue coefficient tables
+  } else if (NST == 2) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -231,8 +266,8 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     for (int x = 0; x < 4; ++x) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + x * 16 + fg * 4 + r;
-        if (!jok || m >= g.M) continue;
+        const int m = phys(m0 + wm * 64 + x * 16 + fg * 4 + r);
+        if (!jok || m < 0) continue;
         float v = acc[x][y][r];
         if (EPI & EPI_BIAS) v += a.bias[j];
         if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
@@ -319,7 +354,14 @@ static int igemm_stages() {
 
 template <int WN, int NST>
 static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
-  const int tiles = ((a.g.M + G_BM - 1) / G_BM) * ((a.g.Nc + 32 * WN - 1) / (32 * WN));
+  const int ntn = (a.g.Nc + 32 * WN - 1) / (32 * WN);
+  int tiles = ((a.g.M + G_BM - 1) / G_BM) * ntn;
+  if (igemm_parity(a.g)) {  // parity-split rows (see igemm_bf16)
+    if (a.g.M % (a.g.T_out * a.g.V) != 0 || (epi & (EPI_GAP | EPI_BIASV))) return F3_EINVAL;
+    const int nclip = a.g.M / (a.g.T_out * a.g.V);
+    const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
+    tiles = ((M0 + G_BM - 1) / G_BM + (M1 + G_BM - 1) / G_BM) * ntn;
+  }
 #define F3_ICASE(E)                                                                   \
   if (epi == (E)) {                                                                  \
     hipLaunchKernelGGL((igemm_bf16<(E), WN, NST>), dim3(tiles), dim3(256), 0, s, a); \
@@ -381,13 +423,25 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
   float* dbs = reinterpret_cast<float*>(smem + 2 * STAGE);   // [TJ]
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j0 = blockIdx.x * TJ;
+  // xcd: 1-D grid, XCD-aware: the gx*gy workgroups of one row split (they all read that
+  // split's dY and input rows) get consecutive logical ids, which xcd_remap keeps on one XCD,
+  // so the split's rows come from HBM once and are re-read from that XCD's L2.
   const int itiles = (g.Kc + TI - 1) / TI;
-  const int dt = blockIdx.y / itiles;
-  const int i0 = (blockIdx.y - dt * itiles) * TI;
-  const int r_begin = blockIdx.z * a.rows_per_split;
+  int bz = blockIdx.z, by = blockIdx.y, bx = blockIdx.x;
+  if (a.xcd) {
+    const int gx = (g.Nc + TJ - 1) / TJ, gy = g.KT * itiles;
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    bz = lin / (gx * gy);
+    const int rem = lin - bz * gx * gy;
+    by = rem / gx;
+    bx = rem - by * gx;
+  }
+  const int j0 = bx * TJ;
+  const int dt = by / itiles;
+  const int i0 = (by - dt * itiles) * TI;
+  const int r_begin = bz * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
-  const bool do_db = a.db && blockIdx.y == 0;
+  const bool do_db = a.db && by == 0;
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
   const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
   const __bf16* zero = reinterpret_cast<const __bf16*>(a.zero);
@@ -543,7 +597,12 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   if (rps < 256) rps = 256;
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
-  dim3 grid(gx, gy, splits);
+  // XCD-aware grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
+  // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the
+  // round-robin 3-D grid
+  static const int xcd = getenv("F3_WGRAD_XCD") ? atoi(getenv("F3_WGRAD_XCD")) : 1;
+  a.xcd = xcd;
+  dim3 grid = xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
   if (TJ == 128 && TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 128>), grid, dim3(256), 0, s, a);
   else if (TJ == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 64>), grid, dim3(256), 0, s, a);
   else if (TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<64, 128>), grid, dim3(256), 0, s, a);

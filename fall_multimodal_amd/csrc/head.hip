@@ -76,23 +76,36 @@ __global__ void head_dlogits_kernel(HeadArgs a) {
   }
 }
 
-// grid (C): dW[c][k] = sum_n dlog[n][c] feat[n][k], db[c]
+// grid (ceil(K/64), C): dW[c][k] = sum_n dlog[n][c] feat[n][k], db[c]. A workgroup owns 64
+// feature columns of one class; its 4 waves split the clips (coalesced 64-wide row reads,
+// independent partial sums) and combine through LDS.
 __global__ __launch_bounds__(256) void head_wgrad_kernel(HeadArgs a) {
-  const int c = blockIdx.x;
-  int off = 0;
-  for (int b = 0; b < a.nblk; ++b) {
-    for (int k = threadIdx.x; k < a.width[b]; k += blockDim.x) {
-      float acc = 0.f;
-      for (int n = 0; n < a.N; ++n) acc += a.dlogits[(size_t)n * a.C + c] * a.feat[b][(size_t)n * a.ld[b] + k];
-      const int K = a.width[0] + (a.nblk > 1 ? a.width[1] : 0) + (a.nblk > 2 ? a.width[2] : 0);
-      a.g_W[(size_t)c * K + off + k] += acc;
+  __shared__ float part[4][65];
+  const int c = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = a.width[0] + (a.nblk > 1 ? a.width[1] : 0) + (a.nblk > 2 ? a.width[2] : 0);
+  const int k = blockIdx.x * 64 + lane;
+  const float* f = nullptr;
+  int ld = 0;
+  if (k < K) {  // which concatenated block holds column k
+    int off = 0;
+    for (int b = 0; b < a.nblk; ++b) {
+      if (k < off + a.width[b]) { f = a.feat[b] + (k - off); ld = a.ld[b]; break; }
+      off += a.width[b];
     }
-    off += a.width[b];
   }
-  if (threadIdx.x == 0) {
-    float acc = 0.f;
-    for (int n = 0; n < a.N; ++n) acc += a.dlogits[(size_t)n * a.C + c];
-    a.g_b[c] += acc;
+  float acc = 0.f, accb = 0.f;
+  for (int n = wave; n < a.N; n += 4) {
+    const float d = a.dlogits[(size_t)n * a.C + c];
+    if (f) acc += d * f[(size_t)n * ld];
+    accb += d;
+  }
+  part[wave][lane] = acc;
+  if (lane == 0) part[wave][64] = accb;
+  __syncthreads();
+  if (wave == 0) {
+    const float s = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    if (k < K) a.g_W[(size_t)c * K + k] += s;
+    if (lane == 0 && blockIdx.x == 0) a.g_b[c] += part[0][64] + part[1][64] + part[2][64] + part[3][64];
   }
 }
 
@@ -159,7 +172,8 @@ int f3_head_bwd(const HeadArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(head_dlogits_kernel, dim3((a->N + 255) / 256), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   if (a->nblk > 0) {
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3(a->C), dim3(256), 0, s, *a);
+    const int K = a->width[0] + (a->nblk > 1 ? a->width[1] : 0) + (a->nblk > 2 ? a->width[2] : 0);
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3((K + 63) / 64, a->C), dim3(256), 0, s, *a);
     F3_LAUNCH_CHECK();
     hipLaunchKernelGGL(head_dfeat_kernel, dim3(a->N), dim3(256), 0, s, *a);
     F3_LAUNCH_CHECK();

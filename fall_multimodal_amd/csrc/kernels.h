@@ -61,6 +61,7 @@ struct WgradArgs {
   const unsigned short* dyb;  // bf16 dy (instead of dy)
   const unsigned short* inb;  // bf16 input rows (instead of in)
   const unsigned short* zero; // >= 16 zero bytes (LDS-DMA kernel)
+  int xcd;                    // LDS-DMA kernel: XCD-aware 1-D grid (set by the launcher)
 };
 
 }  // namespace f3

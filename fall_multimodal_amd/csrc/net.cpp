@@ -480,8 +480,15 @@ void add_bnrun(BnRunTable& t, const Ptrs& q, const BnIdx& bi, const double* sum,
   j.rmean = q.b(bi.rm); j.rvar = q.b(bi.rv); j.nbt = q.c(bi.nbt);
 }
 
+// Forward of one skeleton stream in stages: stage -1 = weight prep + data_bn, stage l = block l.
+// The caller interleaves the two streams' stages so both branch queues are fed from the start
+// (host submission, eager or graph replay, walks the launches in issue order).
+int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs& q, Ws& w, BnRunTable& run,
+                         hipStream_t s, int l);
+
 int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, Ws& w, const float* skel,
-                   BnRunTable& run, hipStream_t s) {
+                   BnRunTable& run, hipStream_t s, int stage) {
+  if (stage >= 0) return stream_forward_layer(net, si, N, train, q, w, run, s, stage);
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V, eval = !train;
@@ -516,7 +523,16 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
   d.st_sum = W.dbn.fsum; d.st_sq = W.dbn.fsq;
   F3_TRY(f3_databn_fwd(&d, s));
   if (train) add_bnrun(run, q, S.dbn, W.dbn.fsum, W.dbn.fsq, (double)N * S.T);
-  for (int l = 0; l < 7; ++l) {
+  return F3_OK;
+}
+
+int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs& q, Ws& w, BnRunTable& run,
+                         hipStream_t s, int l) {
+  const StreamIdx& S = net.st[si];
+  StreamWs& W = w.st[si];
+  const int K = net.K, V = net.V, eval = !train;
+  const int hb = net.cfg.precision == F3_PRECISION_BF16;
+  {
     const LayerIdx& L = S.L[l];
     LayerWs& X = W.L[l];
     const int C = L.cout, Ci = L.cin, Ti = L.T_in, To = L.T_out;
@@ -601,16 +617,16 @@ bool debug_stop(int si, int l) {
 
 // Backward of layers l_hi..l_lo (descending); data_bn after layer 0. Layer l writes its
 // input gradient to W.dx[(6-l)&1] and reads layer l+1's from W.dx[(5-l)&1].
+// `unpack` collects the bf16 mode's packed tcn weight-gradient -> reference-layout jobs; the
+// caller flushes it (one prep launch per stream) after the stream's last layer call.
 int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
-                    int l_hi, int l_lo) {
+                    int l_hi, int l_lo, PrepTable& unpack) {
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V;
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
   const float* dout = l_hi == 6 ? nullptr : W.dx[(5 - l_hi) & 1];
   int pp = (6 - l_hi) & 1;
-  PrepTable unpack;  // bf16 mode: packed tcn weight gradients -> reference layout
-  unpack.n = 0;
   for (int l = l_hi; l >= l_lo; --l) {
     const LayerIdx& L = S.L[l];
     LayerWs& X = W.L[l];
@@ -730,7 +746,6 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     dout = dx;
     pp ^= 1;
   }
-  F3_TRY(f3_prep(unpack, s));
   if (l_lo > 0) return F3_OK;
   DataBnArgs d;
   std::memset(&d, 0, sizeof(d));
@@ -970,8 +985,8 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
   run.n = 0;
   Branches br{*net, s, ensure_parallel(*net, s)};
   F3_TRY(br.fork());
-  for (int si = 0; si < net->nstreams; ++si)
-    F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, br.at(si)));
+  // sensor branch first (small, latency-bound), then the two skeleton streams stage by stage,
+  // interleaved, so every branch queue is fed from the start
   if (net->has_sensor) {
     const hipStream_t ss = br.at(2);
     LstmArgs la;
@@ -992,6 +1007,9 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     F3_TRY(f3_shead_fwd(&sa, ss));
     if (training) add_bnrun(run, q, net->lstm.bn, w.sbn.fsum, w.sbn.fsq, N);
   }
+  for (int stage = -1; stage < 7; ++stage)
+    for (int si = 0; si < net->nstreams; ++si)
+      F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, br.at(si), stage));
   F3_TRY(br.join());
   HeadArgs h;
   head_args(*net, N, q, w, h);
@@ -1031,11 +1049,24 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
   hipStream_t s = (hipStream_t)stream;
   Ws w = plan(*net, N, (char*)workspace);
   Ptrs q{*net, params, nullptr, nullptr, grads};
+  // skeleton streams layer by layer, interleaved (see stream_forward), then each stream's
+  // packed weight-gradient unpack
+  auto skeleton = [&](Branches& br, int l_hi, int l_lo) -> int {
+    PrepTable unpack[2];
+    unpack[0].n = unpack[1].n = 0;
+    for (int l = l_hi; l >= l_lo; --l)
+      for (int si = 0; si < net->nstreams; ++si) {
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si]));
+        if (debug_stop(si, l)) return F3_OK;  // tools/diag_layer.py: leave the scratch as is
+      }
+    for (int si = 0; si < net->nstreams; ++si)
+      F3_TRY(f3_prep(unpack[si], br.at(si)));
+    return F3_OK;
+  };
   if (phase == 2) {
     Branches br{*net, s, ensure_parallel(*net, s)};
     F3_TRY(br.fork());
-    for (int si = 0; si < net->nstreams; ++si)
-      F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), kSplitLayer - 1, 0));
+    F3_TRY(skeleton(br, kSplitLayer - 1, 0));
     F3_TRY(br.join());
     return F3_OK;
   }
@@ -1065,10 +1096,7 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
       F3_TRY(f3_conv1d_bwd(&c1, ss));
     }
   }
-  for (int si = 0; si < net->nstreams; ++si) {
-    F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), 6, phase == 1 ? kSplitLayer : 0));
-    if (getenv("F3_DEBUG_BWD_STOP") && si == atoi(getenv("F3_DEBUG_BWD_STOP"))) break;
-  }
+  F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0));
   F3_TRY(br.join());
   return F3_OK;
 }
