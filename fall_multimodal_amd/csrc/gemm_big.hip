@@ -1,0 +1,314 @@
+// Large-tile bf16 implicit-GEMM temporal/graph convolution for the 128- and 256-channel
+// layers: one 144-row (256 channels) or 288-row (128 channels) output tile per CU.
+//
+//   Out[m][j] = sum_{dt,i} In[src(m,dt)][i] * W[j][dt*Kc+i]     (fwd, or dgrad via the
+//                                                                 transposed row map)
+// Why a second kernel: at B=256, V=18 the 256-channel layers have M = 36864 output rows, so
+// 128x128 tiles give 576 tiles = 2.25 per CU — two rounds with a 1/8-full tail, at 2
+// workgroups per CU whose 2-stage vmcnt(0) loops leave the HBM/L2 latency exposed (measured
+// 430-455 TF on the layer-6 tcn). Here a workgroup owns BM x Nc with BM = 144 (256 ch) or
+// 288 (128 ch): M = 36864 is exactly 256 tiles, M = 69120 is 240 (one round either way).
+// Each of the 8 waves (2 per SIMD, so one wave's LDS reads overlap the other's MFMAs) owns
+// a 144 x 32 sub-tile (9 x 2 MFMA 16x16x32 tiles, 72 fp32 accumulators per lane): per 64-deep
+// k step a wave issues 36 MFMAs against 22 KiB of LDS fragment reads. Staging is LDS-DMA
+// (global_load_lds_dwordx4) into three stages with two in flight across raw barriers (counted
+// vmcnt) — the ~1 workgroup/CU structure of cdna_hip_programming.md §5 "Pipelining across
+// barriers". A stage is 1-KiB pieces (8 rows x 128 B, XOR-swizzled through the source address
+// as in gemm_glds.hip), dealt round-robin to the 8 waves; where the pieces do not divide
+// evenly a wave re-issues an earlier piece (identical bytes to the identical LDS address), so
+// every wave's vmcnt count is the same constant.
+// Row maps, the stride-2 parity split and the epilogues are those of igemm_bf16.
+#include "igemm.h"
+
+namespace f3 {
+
+constexpr int BG_MT = 9, BG_NT = 2, BG_NST = 3;  // per-wave MFMA tiles (rows x cols), LDS stages
+constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
+
+template <int WM, int WN>
+struct BigCfg {
+  static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
+  static constexpr int AP = BM / 8, BP = BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
+  static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;     // pieces per wave
+  static constexpr int STAGE = NP * 1024;
+  static constexpr int SMEM = BG_NST * STAGE + 4 * BN * 4;
+};
+
+template <int EPI, int WM, int WN>
+__global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
+  using Cfg = BigCfg<WM, WN>;
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
+  static_assert(WM * WN == BG_WAVES, "wave grid");
+  static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
+  // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code)
+  __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+  float* epi_sc = reinterpret_cast<float*>(smem + BG_NST * STAGE);
+  float* epi_sh = epi_sc + BN;
+  float* epi_mu = epi_sh + BN;
+  float* epi_rs = epi_mu + BN;
+
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const bool par = igemm_parity(g);
+  int p = 0, Tp = g.T_out, Mp = g.M;
+  if (par) {
+    const int nclip = g.M / (g.T_out * g.V), T0 = (g.T_out + 1) >> 1;
+    const int tiles0 = (nclip * T0 * g.V + BM - 1) / BM;
+    Tp = T0;
+    if (tile >= tiles0) { p = 1; tile -= tiles0; Tp = g.T_out >> 1; }
+    Mp = nclip * Tp * g.V;
+  }
+  auto phys = [&](int r) -> int {
+    if (r >= Mp) return -1;
+    if (!par) return r;
+    const int nt = r / g.V, v = r - nt * g.V, n = nt / Tp, tt = nt - n * Tp;
+    return (n * g.T_out + 2 * tt + p) * g.V + v;
+  };
+  const int m0 = tile * BM;
+  const int Ktot = g.KT * g.Kc;
+  const int kpt = g.Kc / G_BK;
+  const int dt0 = par ? ((p + g.P) & 1) : 0;
+  const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
+  const unsigned short* in = a.inb;
+  const unsigned short* wb = a.wb;
+
+  if (EPI & EPI_RELUMASK) {
+    for (int t = tid; t < BN; t += BG_THREADS) {
+      float sc, sh, mu, rs;
+      bn_coeff(a.epi_bn, t, sc, sh, mu, rs);
+      epi_sc[t] = sc; epi_sh[t] = sh; epi_mu[t] = mu; epi_rs[t] = rs;
+    }
+  }
+
+  // staging slots of this wave: piece q = (wave + 8 i) mod NP (A pieces, then B pieces); a
+  // wrapped slot re-issues an earlier piece's identical copy (same bytes to the same LDS
+  // address), so every wave issues PPW DMAs per stage and one vmcnt count serves all
+  const int sub = lane >> 3, pch = lane & 7;
+  RowMap amap[PPW];
+  int boff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = (wave + BG_WAVES * i) % NP;
+    amap[i].base = -1;
+    amap[i].q = 0;
+    boff[i] = 0;
+    if (q < AP) {
+      amap[i] = rowmap(phys(m0 + q * 8 + sub), g);
+    } else {
+      const int j = (q - AP) * 8 + sub;
+      boff[i] = j * Ktot + swz(j, pch) * 8;
+    }
+  }
+  auto stage = [&](int t, int buf) {
+    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    const int dt = par ? dt0 + 2 * tap : tap;
+    const int k0 = dt * g.Kc + i0;
+    char* sbase = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = (wave + BG_WAVES * i) % NP;
+      const void* src;
+      char* dst;
+      if (q < AP) {
+        const int r = rowmap_src(amap[i], dt, g);
+        src = r >= 0 ? (const void*)(in + (size_t)r * g.lda + i0 + swz(q * 8 + sub, pch) * 8) : (const void*)a.zero;
+        dst = sbase + q * 1024;
+      } else {
+        src = wb + boff[i] + k0;
+        dst = sbase + q * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 acc[BG_MT][BG_NT];
+#pragma unroll
+  for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
+    if (EPI & EPI_ADD) return;
+    __syncthreads();
+  } else {
+    stage(0, 0);
+    if (nchunk > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int t = 0; t < nchunk; ++t) {
+    const int buf = t % 3;
+    if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
+    const char* sa = smem + buf * STAGE;
+    const char* sb = sa + AP * 1024;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[BG_MT], fb[BG_NT];
+      const int c = ks * 4 + fg;
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        const int r = wn * 32 + y * 16 + fr;
+        fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int x = 0; x < BG_MT; ++x) {
+        const int r = wm * 144 + x * 16 + fr;
+        fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+    }
+    if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  __syncthreads();
+
+  // ---------------- epilogue (as igemm_bf16) ----------------
+  float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]  (stage 0 is free now)
+  float* gred = red + 2 * WM * BN;               // [WM][2][BN]
+  float ssum[BG_NT], ssq[BG_NT], gap0[BG_NT], gap1[BG_NT];
+#pragma unroll
+  for (int y = 0; y < BG_NT; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
+  const int TV = g.T_out * g.V;
+  const int nlo = m0 / TV;  // GAP is forward-only (no parity split): m0 is the first output row
+#pragma unroll
+  for (int y = 0; y < BG_NT; ++y) {
+    const int j = wn * 32 + y * 16 + fr;
+    const bool jok = j < g.Nc;
+#pragma unroll
+    for (int x = 0; x < BG_MT; ++x) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = phys(m0 + wm * 144 + x * 16 + fg * 4 + r);
+        if (!jok || m < 0) continue;
+        float v = acc[x][y][r];
+        if (EPI & EPI_BIAS) v += a.bias[j];
+        if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
+        if (EPI & EPI_RELUMASK) {
+          const float gv = a.aux[(size_t)m * a.ldaux + j];
+          if (gv * epi_sc[j] + epi_sh[j] <= 0.f) v = 0.f;
+          const float xh = (gv - epi_mu[j]) * epi_rs[j];
+          ssum[y] += v;
+          ssq[y] += v * xh;
+        } else if (EPI & EPI_STATS) {
+          ssum[y] += v;
+          ssq[y] += v * v;
+        }
+        if (EPI & EPI_GAP) {
+          const int n = m / TV;
+          if (n == nlo) gap0[y] += v;
+          else if (n == nlo + 1) gap1[y] += v;
+          else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
+        }
+        if (!(EPI & EPI_ADD) && a.outb) {
+          reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+        } else {
+          float* o = a.out + (size_t)m * g.ldo + j;
+          if (EPI & EPI_ADD) *o += v;
+          else *o = v;
+        }
+      }
+    }
+  }
+  if (EPI & (EPI_STATS | EPI_RELUMASK | EPI_GAP)) {
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) {
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        ssum[y] += __shfl_xor(ssum[y], o, 64);
+        ssq[y] += __shfl_xor(ssq[y], o, 64);
+        gap0[y] += __shfl_xor(gap0[y], o, 64);
+        gap1[y] += __shfl_xor(gap1[y], o, 64);
+      }
+    }
+    if (fg == 0) {
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        const int jl = wn * 32 + y * 16 + fr;
+        red[(wm * 2 + 0) * BN + jl] = ssum[y];
+        red[(wm * 2 + 1) * BN + jl] = ssq[y];
+        gred[(wm * 2 + 0) * BN + jl] = gap0[y];
+        gred[(wm * 2 + 1) * BN + jl] = gap1[y];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < BN; t += BG_THREADS) {
+      if (t >= g.Nc) continue;
+      float s0 = 0.f, s1 = 0.f, g0 = 0.f, g1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * 2 + 0) * BN + t];
+        s1 += red[(w * 2 + 1) * BN + t];
+        g0 += gred[(w * 2 + 0) * BN + t];
+        g1 += gred[(w * 2 + 1) * BN + t];
+      }
+      if (EPI & (EPI_STATS | EPI_RELUMASK)) {
+        atomic_add_d(a.st_sum + t, (double)s0);
+        atomic_add_d(a.st_sq + t, (double)s1);
+      }
+      if (EPI & EPI_GAP) {
+        atomic_add_f(a.gap + (size_t)nlo * g.Nc + t, g0);
+        if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + t, g1);
+      }
+    }
+  }
+}
+
+}  // namespace f3
+
+using namespace f3;
+
+// Large tiles pay when the k loop is long enough to amortise the 3-stage prologue.
+// F3_IGEMM_BIG=0 turns the kernel off (A/B against igemm_bf16).
+bool f3_igemm_big_ok(const ConvGemmArgs& a) {
+  static const int on = getenv("F3_IGEMM_BIG") ? atoi(getenv("F3_IGEMM_BIG")) : 1;
+  if (!on || !f3_igemm_ok(a)) return false;
+  if (a.g.Nc != 128 && a.g.Nc != 256) return false;
+  return a.g.KT * a.g.Kc / G_BK >= 6;
+}
+
+template <int WM, int WN>
+static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
+  constexpr int BM = BigCfg<WM, WN>::BM;
+  int tiles = (a.g.M + BM - 1) / BM;
+  if (igemm_parity(a.g)) {
+    if (a.g.M % (a.g.T_out * a.g.V) != 0 || (epi & (EPI_GAP | EPI_BIASV))) return F3_EINVAL;
+    const int nclip = a.g.M / (a.g.T_out * a.g.V);
+    const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
+    tiles = (M0 + BM - 1) / BM + (M1 + BM - 1) / BM;
+  }
+#define F3_BCASE(E)                                                                 \
+  if (epi == (E)) {                                                                \
+    hipLaunchKernelGGL((igemm_big<(E), WM, WN>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    F3_LAUNCH_CHECK();                                                              \
+    return F3_OK;                                                                   \
+  }
+  F3_BCASE(EPI_BIASV | EPI_STATS)            // gcn forward
+  F3_BCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
+  F3_BCASE(EPI_BIAS | EPI_STATS)             // residual forward
+  F3_BCASE(EPI_RELUMASK)                     // tcn dgrad
+  F3_BCASE(0)                                // gcn dgrad
+  F3_BCASE(EPI_ADD)                          // residual dgrad
+  F3_BCASE(EPI_BIAS)                         // plain conv (tests)
+#undef F3_BCASE
+  return F3_EINVAL;
+}
+
+int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
+  const ConvGemmArgs& a = *args;
+  if (a.g.M <= 0) return F3_OK;
+  if (!f3_igemm_big_ok(a)) return F3_EINVAL;
+  if (a.g.Nc == 256) return launch_big<1, 8>(a, epi, s);
+  return launch_big<2, 4>(a, epi, s);
+}
