@@ -58,6 +58,36 @@ F3_DEV void atomic_add_f(float* p, float v) { atomicAdd(p, v); }
 
 F3_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// Activation storage. The bf16 mode keeps the layer activations (gcn / tcn / residual conv
+// outputs, block outputs, the tcn input gradient) in bf16 in HBM; arithmetic stays fp32
+// (BN statistics are taken in the producers' epilogues from the fp32 values). B16 selects
+// the storage type; offsets are in elements.
+typedef __bf16 act_bf16x4 __attribute__((ext_vector_type(4)));
+F3_DEV float bf2f(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
+template <bool B16>
+F3_DEV f32x4 ld_act4(const void* p, size_t off) {
+  if constexpr (B16) {
+    const act_bf16x4 v = *reinterpret_cast<const act_bf16x4*>(reinterpret_cast<const __bf16*>(p) + off);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  } else {
+    return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off);
+  }
+}
+template <bool B16>
+F3_DEV void st_act4(void* p, size_t off, f32x4 v) {
+  if constexpr (B16) {
+    act_bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+    *reinterpret_cast<act_bf16x4*>(reinterpret_cast<__bf16*>(p) + off) = o;
+  } else {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p) + off) = v;
+  }
+}
+F3_DEV float ld_act(const void* p, size_t off, bool b16) {
+  return b16 ? bf2f(reinterpret_cast<const unsigned short*>(p)[off]) : reinterpret_cast<const float*>(p)[off];
+}
+
 }  // namespace f3
 
 // Error plumbing for the C ABI: never abort, return a status.

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void conv_gemm_bf16(ConvGemmArgs a) {
         if (EPI & EPI_BIAS) v += a.bias[j];
         if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
         if (EPI & EPI_RELUMASK) {
-          const float gv = a.aux[(size_t)m * a.ldaux + j];
+          const float gv = a.auxb ? bf2f(a.auxb[(size_t)m * a.ldaux + j]) : a.aux[(size_t)m * a.ldaux + j];
           if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
           const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
           ssum[y] += v;
@@ -248,9 +248,13 @@ __global__ __launch_bounds__(256) void conv_gemm_bf16(ConvGemmArgs a) {
           else if (n == nlo + 1) gap1[y] += v;
           else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
         }
-        float* o = a.out + (size_t)m * g.ldo + j;
-        if (EPI & EPI_ADD) *o += v;
-        else *o = v;
+        if (!(EPI & EPI_ADD) && a.outb) {
+          reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+        } else {
+          float* o = a.out + (size_t)m * g.ldo + j;
+          if (EPI & EPI_ADD) *o += v;
+          else *o = v;
+        }
       }
     }
   }

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         if (EPI & EPI_BIAS) v += a.bias[j];
         if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
         if (EPI & EPI_RELUMASK) {
-          const float gv = a.aux[(size_t)m * a.ldaux + j];
+          const float gv = a.auxb ? bf2f(a.auxb[(size_t)m * a.ldaux + j]) : a.aux[(size_t)m * a.ldaux + j];
           if (gv * epi_sc[j] + epi_sh[j] <= 0.f) v = 0.f;
           const float xh = (gv - epi_mu[j]) * epi_rs[j];
           ssum[y] += v;

@@ -41,6 +41,7 @@ struct ConvGemmArgs {
   float* gap;         // [N][Nc]
   const float* aux;   // RELUMASK source rows
   int ldaux;
+  const unsigned short* auxb;  // RELUMASK source rows stored bf16 (instead of aux)
   BnRef epi_bn;
 };
 

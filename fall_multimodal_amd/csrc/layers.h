@@ -20,7 +20,8 @@ struct PrepJob {
 struct DataBnArgs {
   int N, T, V, C, motion;
   const float* skel;     // reference layout [N][3][T(+1)][V]
-  float* out;            // [N][T][V][C]
+  float* out;            // [N][T][V][C] (bf16 when act16)
+  int act16;
   BnRef bn;
   double* st_sum;
   double* st_sq;
@@ -32,7 +33,8 @@ struct DataBnArgs {
 struct MixArgs {
   int K, V, Cin, frames;
   const float* A;        // A_eff [K][V][V]
-  const float* x;        // [frames][V][Cin]
+  const float* x;        // [frames][V][Cin] (bf16 when x16)
+  int x16;
   float* z;              // [frames][V][K][Cin] (fwd out / bwd in)
   float* dx;             // bwd out
   float* dA;             // bwd accumulate [K][V][V]
@@ -60,6 +62,7 @@ constexpr int kCaMaxRowsPerThread = 4;  // channel attention: batch <= 1024 per 
 
 struct BlockArgs {
   int N, TV, C, chunks, res_kind;
+  int act16;             // h, r, x, out stored bf16
   float inv_tv;
   BnRef bn2, bnr;
   const float* h;        // tcn output before BN2 [M][C]
@@ -91,6 +94,7 @@ struct BlockArgs {
 
 struct BnBwdArgs {
   int N, TV, C, V, chunks;
+  int act16;             // dv, g stored bf16
   BnRef bn;
   const double* bsum;
   const double* bsq;
@@ -106,6 +110,7 @@ struct BnBwdArgs {
 
 struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the bf16 mode
   int M, C;
+  int g16;               // g stored bf16
   BnRef bn;
   const float* g;
   unsigned short* u;

@@ -119,7 +119,9 @@ __global__ void databn_apply_kernel(DataBnArgs a) {
     const int c = e % a.C, m = e / a.C, v = m % a.V, nt = m / a.V, t = nt % a.T, n = nt / a.T;
     float sc, sh, mu, rs;
     bn_coeff(a.bn, v * a.C + c, sc, sh, mu, rs);
-    a.out[e] = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V) * sc + sh;
+    const float val = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V) * sc + sh;
+    if (a.act16) reinterpret_cast<__bf16*>(a.out)[e] = (__bf16)val;
+    else a.out[e] = val;
   }
 }
 
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void mix_fwd_kernel(MixArgs a) {
   const int outs = a.V * a.K * a.Cin;
   for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
     __syncthreads();
-    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = a.x[(size_t)f * per + i];
+    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = ld_act(a.x, (size_t)f * per + i, a.x16);
     __syncthreads();
     for (int o = threadIdx.x; o < outs; o += blockDim.x) {
       const int ci = o % a.Cin, wk = o / a.Cin, k = wk % a.K, w = wk / a.K;
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(256) void mix_bwd_kernel(MixArgs a) {
   float dacc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
     __syncthreads();
-    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = a.x[(size_t)f * per + i];
+    for (int i = threadIdx.x; i < per; i += blockDim.x) xs[i] = ld_act(a.x, (size_t)f * per + i, a.x16);
     for (int i = threadIdx.x; i < outs; i += blockDim.x) zs[i] = a.z[(size_t)f * outs + i];
     __syncthreads();
     for (int o = threadIdx.x; o < per; o += blockDim.x) {
@@ -263,8 +265,8 @@ F3_DEV f32x4 bf4_to_f4(u32x2 r) {
                __uint_as_float(r.y & 0xffff0000u)};
 }
 
-template <int KS, int CIN>  // k steps over v: ceil(V/4); compile-time so the A~ fragments stay in registers
-__global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
+template <int KS, int CIN, bool XB>  // k steps over v: ceil(V/4), compile-time so the A~ fragments stay in
+__global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {  // registers; XB: x stored bf16
   constexpr int kMixPX = MixCap<CIN>::PX;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -279,13 +281,16 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg);
   const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
-  f32x4 rx[kMixPX];
+  f32x4 rx[XB ? 1 : kMixPX];
+  u32x2 rxb[XB ? kMixPX : 1];  // raw bf16 pieces (converted when written to LDS)
   auto prefetch = [&](int f) {
-    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
       const int i = tid + q * 256;
-      if (i < n4) rx[q] = xg[i];
+      if (i < n4) {
+        if constexpr (XB) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
+        else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
+      }
     }
   };
   if (blockIdx.x < a.frames) prefetch(blockIdx.x);
@@ -296,7 +301,8 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {
       const int i = tid + q * 256;
       if (i < n4) {
         const int v = i / C4, c = (i - v * C4) * 4;
-        *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
+        if constexpr (XB) *reinterpret_cast<f32x4*>(xs + v * S + c) = bf4_to_f4(rxb[q]);
+        else *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
       }
     }
     __syncthreads();
@@ -364,16 +370,18 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
   f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const int tiles = Cin / 16, n4x = V * Cin / 4, n4z = KV * Cin / 4, C4 = Cin / 4;
   constexpr bool zb16 = ZB16;
-  f32x4 rx[kMixPX], rd[kMixPX];
+  // the bf16 mode stores x in bf16 as well (ZB16 <=> bf16 mode; the launcher checks x16)
+  f32x4 rx[ZB16 ? 1 : kMixPX], rd[kMixPX];
+  u32x2 rxb[ZB16 ? kMixPX : 1];
   u32x2 rz[ZB16 ? kMixPZ : 1];  // bf16 gradient pieces, raw
   auto prefetch = [&](int f) {
-    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin);
     const f32x4* dg = reinterpret_cast<const f32x4*>(a.dx + (size_t)f * V * Cin);
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
       const int i = tid + q * 256;
       if (i < n4x) {
-        rx[q] = xg[i];
+        if constexpr (ZB16) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
+        else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
         if (a.accumulate) rd[q] = dg[i];
       }
     }
@@ -394,7 +402,8 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
       const int i = tid + q * 256;
       if (i < n4x) {
         const int v = i / C4, c = (i - v * C4) * 4;
-        *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
+        if constexpr (ZB16) *reinterpret_cast<f32x4*>(xs + v * S + c) = bf4_to_f4(rxb[q]);
+        else *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
         if (a.accumulate) *reinterpret_cast<f32x4*>(ds + v * S + c) = rd[q];
       }
     }
@@ -554,6 +563,7 @@ F3_DEV f32x4 quad_reduce(f32x4 v, float* lds, int C4) {
 }
 
 // out = relu(bn2(h) * a[n,c] + res), res = bn_r(r) | x | 0 ; optional pooled mean
+template <bool A16>
 __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
   __shared__ float sc2[256], sh2[256], scr[256], shr[256];
   __shared__ __attribute__((aligned(16))) float lds[1024];
@@ -571,10 +581,10 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
   f32x4 pool = {0.f, 0.f, 0.f, 0.f};
   for (int m = r0 + tid / C4; m < r1; m += RP) {
     const size_t off = (size_t)m * C + c0;
-    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    const f32x4 h = ld_act4<A16>(a.h, off);
     f32x4 res = {0.f, 0.f, 0.f, 0.f};
-    if (a.res_kind == RES_CONV) res = *reinterpret_cast<const f32x4*>(a.r + off);
-    else if (a.res_kind == RES_ID) res = *reinterpret_cast<const f32x4*>(a.x + off);
+    if (a.res_kind == RES_CONV) res = ld_act4<A16>(a.r, off);
+    else if (a.res_kind == RES_ID) res = ld_act4<A16>(a.x, off);
     f32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -582,7 +592,7 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
       if (a.res_kind == RES_CONV) rv = rv * scr[c0 + e] + shr[c0 + e];
       o[e] = fmaxf((h[e] * sc2[c0 + e] + sh2[c0 + e]) * av[e] + rv, 0.f);
     }
-    *reinterpret_cast<f32x4*>(a.out + off) = o;
+    st_act4<A16>(a.out, off, o);
     if (a.outb) {
       bf16x4 ob;
 #pragma unroll
@@ -603,6 +613,7 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
 // backward reductions over a block's output gradient:
 //   dz = dout * (out > 0);  P1[n,c] = sum_tv dz;  P2[n,c] = sum_tv dz*xhat2
 //   conv residual: R[c] += (sum dz, sum dz*xhat_r)
+template <bool A16>
 __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   __shared__ float mu2[256], rs2[256], mur[256], rsr[256];
   __shared__ __attribute__((aligned(16))) float lds[1024];
@@ -621,11 +632,11 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
   for (int m = r0 + tid / C4; m < r1; m += RP) {
     const size_t off = (size_t)m * C + c0;
-    const f32x4 o = *reinterpret_cast<const f32x4*>(a.out + off);
+    const f32x4 o = ld_act4<A16>(a.out, off);
     const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
-    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    const f32x4 h = ld_act4<A16>(a.h, off);
     f32x4 rr = {0, 0, 0, 0};
-    if (a.res_kind == RES_CONV) rr = *reinterpret_cast<const f32x4*>(a.r + off);
+    if (a.res_kind == RES_CONV) rr = ld_act4<A16>(a.r, off);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float dz = o[e] > 0.f ? d[e] : 0.f;
@@ -662,6 +673,7 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
 }
 
 // dh = g2*rs2*(dz*a + e - D1/M - xhat2*D2/M);  residual: dr (conv) or dx = dz (identity)
+template <bool A16>
 __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   __shared__ float mu2[256], k2[256], m1[256], m2[256], rs2[256];
   __shared__ float mur[256], kr[256], n1[256], n2[256], rsr[256];
@@ -702,12 +714,12 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
   for (int m = r0 + tid / C4; m < r1; m += RP) {
     const size_t off = (size_t)m * C + c0;
-    const f32x4 o = *reinterpret_cast<const f32x4*>(a.out + off);
+    const f32x4 o = ld_act4<A16>(a.out, off);
     const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
-    const f32x4 h = *reinterpret_cast<const f32x4*>(a.h + off);
+    const f32x4 h = ld_act4<A16>(a.h, off);
     f32x4 dh, dr;
     f32x4 rr = {0, 0, 0, 0};
-    if (a.res_kind == RES_CONV) rr = *reinterpret_cast<const f32x4*>(a.r + off);
+    if (a.res_kind == RES_CONV) rr = ld_act4<A16>(a.r, off);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = c0 + e;
@@ -747,6 +759,7 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
 // workgroup writes one partial row [V][C]; f3_colsum adds the rows into G.
 constexpr int kBnBwdFrames = 4;
 
+template <bool A16>
 __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __shared__ float mu[256], kk[256], m1[256], m2[256], rsv[256];
   const int C = a.C, CG = C / 8, V = a.V, T = a.TV / V, tid = threadIdx.x;
@@ -774,10 +787,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
   for (int t = t0; t < t1; ++t) {
     const size_t off = ((size_t)(n * T + t) * V + v) * C + c0;
-    const f32x4 d0 = *reinterpret_cast<const f32x4*>(a.dv + off);
-    const f32x4 d1 = *reinterpret_cast<const f32x4*>(a.dv + off + 4);
-    const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.g + off);
-    const f32x4 g1 = *reinterpret_cast<const f32x4*>(a.g + off + 4);
+    const f32x4 d0 = ld_act4<A16>(a.dv, off), d1 = ld_act4<A16>(a.dv, off + 4);
+    const f32x4 g0 = ld_act4<A16>(a.g, off), g1 = ld_act4<A16>(a.g, off + 4);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -803,6 +814,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
 }
 
 // u = relu(g * scale + shift) in bf16 (BN1 + ReLU of the tcn input, bf16 mode)
+template <bool G16>
 __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
   __shared__ float sc[256], sh[256];
   for (int c = threadIdx.x; c < a.C; c += 256) {
@@ -814,8 +826,7 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
   for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < total8; q += (size_t)gridDim.x * 256) {
     const size_t e0 = q * 8;
     const int c0 = (int)(e0 % a.C);
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(a.g + e0);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(a.g + e0 + 4);
+    const f32x4 x0 = ld_act4<G16>(a.g, e0), x1 = ld_act4<G16>(a.g, e0 + 4);
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1130,12 +1141,12 @@ static size_t mix_lds_bwd2(const MixArgs& a) {
   return sizeof(float) * std::max((size_t)(2 * a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
 }
 
-template <int KS, int CIN>
+template <int KS, int CIN, bool XB>
 static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN>), true);
+  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN, XB>), true);
   (void)once;
   const int grid = std::min(a->frames, 1024);  // resident workgroups loop over frames
-  hipLaunchKernelGGL((mix_fwd_lds_kernel<KS, CIN>), dim3(grid), dim3(256), mix_lds_fwd2(*a), s, *a);
+  hipLaunchKernelGGL((mix_fwd_lds_kernel<KS, CIN, XB>), dim3(grid), dim3(256), mix_lds_fwd2(*a), s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1143,8 +1154,8 @@ static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
 template <int CIN>
 static int mix_fwd_ks(const MixArgs* a, hipStream_t s) {
   switch ((a->V + 3) / 4) {
-    case 4: return launch_mix_fwd<4, CIN>(a, s);
-    case 5: return launch_mix_fwd<5, CIN>(a, s);
+    case 4: return a->x16 ? launch_mix_fwd<4, CIN, true>(a, s) : launch_mix_fwd<4, CIN, false>(a, s);
+    case 5: return a->x16 ? launch_mix_fwd<5, CIN, true>(a, s) : launch_mix_fwd<5, CIN, false>(a, s);
     default: return -1;
   }
 }
@@ -1194,6 +1205,7 @@ static int mix_bwd_ks(const MixArgs* a, hipStream_t s) {
 
 template <int CIN>
 static int mix_bwd_cin(const MixArgs* a, hipStream_t s) {
+  if ((a->dzb != nullptr) != (a->x16 != 0)) return F3_EINVAL;  // bf16 dZ <=> bf16 x (the bf16 mode)
   return a->dzb ? mix_bwd_ks<CIN, true>(a, s) : mix_bwd_ks<CIN, false>(a, s);
 }
 
@@ -1227,7 +1239,8 @@ static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
 int f3_block_out(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  hipLaunchKernelGGL(block_out_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  if (a.act16) hipLaunchKernelGGL(block_out_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(block_out_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1235,7 +1248,8 @@ int f3_block_out(BlockArgs a, hipStream_t s) {
 int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  hipLaunchKernelGGL(block_bwd_reduce_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  if (a.act16) hipLaunchKernelGGL(block_bwd_reduce_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(block_bwd_reduce_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1243,7 +1257,8 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
 int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  hipLaunchKernelGGL(block_bwd_apply_kernel, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  if (a.act16) hipLaunchKernelGGL(block_bwd_apply_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(block_bwd_apply_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1254,7 +1269,8 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
   if (a.C % 8 || a.C > 256 || a.TV % a.V || a.V * (a.C / 8) > 1024 || !a.Gpart) return F3_EINVAL;
   const int T = a.TV / a.V, fch = (T + kBnBwdFrames - 1) / kBnBwdFrames;
   const int threads = ((a.V * (a.C / 8) + 63) / 64) * 64;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(fch, a.N), dim3(threads), 0, s, a);
+  if (a.act16) hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(fch, a.N), dim3(threads), 0, s, a);
+  else hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(fch, a.N), dim3(threads), 0, s, a);
   F3_LAUNCH_CHECK();
   return f3_colsum(a.Gpart, fch * a.N, a.V * a.C, a.G, s);
 }
@@ -1270,7 +1286,8 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   if (a->C % 8 || a->C > 256) return F3_EINVAL;
   const size_t total8 = (size_t)a->M * a->C / 8;
   const int grid = (int)std::min<size_t>((total8 + 255) / 256, 4096);
-  hipLaunchKernelGGL(bnrelu_bf16_kernel, dim3(grid), dim3(256), 0, s, *a);
+  if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

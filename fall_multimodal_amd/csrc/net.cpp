@@ -375,8 +375,8 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
       xin = X.out;
-      xinb = nullptr;
-      if (hb && l + 1 < 7 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(Mo * C);
+      // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand)
+      xinb = hb ? reinterpret_cast<const unsigned short*>(X.out) : nullptr;
       maxG = std::max(maxG, (size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
@@ -521,6 +521,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel; d.out = W.x0;
   d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), eval);
   d.st_sum = W.dbn.fsum; d.st_sq = W.dbn.fsq;
+  d.act16 = hb;  // bf16 mode: activations stored bf16
   F3_TRY(f3_databn_fwd(&d, s));
   if (train) add_bnrun(run, q, S.dbn, W.dbn.fsum, W.dbn.fsq, (double)N * S.T);
   return F3_OK;
@@ -546,13 +547,14 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
-    mx.zb = bfa(X.z, hb);
+    mx.zb = bfa(X.z, hb); mx.x16 = hb;
     F3_TRY(f3_mix_fwd(&mx, s));
     ConvGemmArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
     ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
-    ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+    ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.outb = bfa(X.g, hb);
+    ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
     F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
       ConvGemmArgs ra;
@@ -560,18 +562,19 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ra.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
       ra.in = hb ? nullptr : X.x; ra.inb = hb ? X.xb : nullptr; ra.zero = w.zero;
       if (hb && !X.xb) return F3_ESTATE;
-      ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
+      ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.outb = bfa(X.r, hb);
+      ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
     // tcn: BN1 + ReLU prologue, (9,1) conv, bias, BN2 stats + channel-attention pool epilogue
     ConvGemmArgs ta;
     std::memset(&ta, 0, sizeof(ta));
     ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.bias = q.p(L.tcn_b);
+    ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.outb = bfa(X.h, hb); ta.bias = q.p(L.tcn_b);
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
     if (hb) {  // materialise u = relu(bn1(g)) in bf16 (also the tcn wgrad operand)
       BnReluArgs br;
-      br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u;
+      br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = 1;
       F3_TRY(f3_bnrelu_bf16(&br, s));
       ta.inb = X.u; ta.zero = w.zero;
       F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
@@ -593,7 +596,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.pool = l == 6 ? W.pool : nullptr;
-    ba.outb = X.outb;
+    ba.act16 = hb;
     F3_TRY(f3_block_out(ba, s));
     if (train) {
       add_bnrun(run, q, L.bn1, X.bn1.fsum, X.bn1.fsq, Mi);
@@ -642,7 +645,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&ba, 0, sizeof(ba));
     ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
-    ba.dout = dout; ba.dout_nc = l == 6 ? W.dpool : nullptr;
+    ba.dout = dout; ba.dout_nc = l == 6 ? W.dpool : nullptr; ba.act16 = hb;
     ba.P1 = X.P1; ba.P2 = X.P2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
     ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = W.dh;
     ba.dres = L.res == RES_CONV ? W.dres : (L.res == RES_ID ? dx : nullptr);
@@ -669,6 +672,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
     td.in = hb ? nullptr : W.dh; td.inb = bfa(W.dh, hb); td.zero = w.zero;
     td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
     if (debug_stop(si, l)) return F3_OK;
@@ -690,7 +694,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&bb, 0, sizeof(bb));
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = W.dg; bb.G = X.G;
-    bb.Gpart = W.gpart; bb.dgb = bfa(W.dg, hb);
+    bb.Gpart = W.gpart; bb.dgb = bfa(W.dg, hb); bb.act16 = hb;
     F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     ConvGemmArgs gd;
@@ -718,7 +722,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
-    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart;
+    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart; mx.x16 = hb;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
     F3_TRY(f3_mix_bwd(&mx, s));
     GcnBiasBwdArgs gb;
