@@ -8,7 +8,7 @@ GPU, T=30 frames, J=17 COCO joints + centre node (coco_mmpose, V=18), 3-channel 
 architecture (TwoStreamSTGCAN_BiLSTM, combination.py:27-46). The reference has no RGB
 branch, so none is built or timed.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-graph]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
@@ -44,7 +44,10 @@ def parse():
     p.add_argument("--sensor-dim", type=int, default=6)
     p.add_argument("--precision", default="bf16", choices=("bf16", "fp32"),
                    help="GEMM operand type (bf16: fp32 accumulate; fp32: exact parity mode)")
-    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step as HIP graphs (measured slower on ROCm 7.2 for this multi-stream "
+                        "step: 10.1 vs 8.15 ms at B=256; see DESIGN.md)")
+    p.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old commands
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -133,7 +136,7 @@ def main():
         dist.broadcast(model.flat_parameters(), 0)
     step = f3.TrainStep(model, B, lr=1e-3)
     sk, se, lb = (torch.from_numpy(x).to(dev) for x in synthetic_batch(B, V, C, S, 100 + rank))
-    if not a.no_graph:
+    if a.graph and not a.no_graph:
         step.capture(sk, se, lb)
     for _ in range(a.warmup):
         step(sk, se, lb)
@@ -172,7 +175,7 @@ def main():
             "config": {"workload": f"fall3_3stream_{a.layout}_V{V}_S{S}_B{B}_per_gpu",
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
-                       "hip_graph": not a.no_graph, "final_loss": round(loss, 5)},
+                       "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

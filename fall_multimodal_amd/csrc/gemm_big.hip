@@ -180,6 +180,12 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   float ssum[BG_NT], ssq[BG_NT], gap0[BG_NT], gap1[BG_NT];
 #pragma unroll
   for (int y = 0; y < BG_NT; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
+  // bf16 outputs leave through an LDS image of the tile: the MFMA C layout gives a lane 4 rows of
+  // ONE column (2-B scattered stores); the image is copied out as 16-B row chunks instead
+  constexpr int OTS = BN + 8, OT_OFF = 16 * 1024;  // row stride (elements), byte offset past red/gred
+  static_assert(OT_OFF + BM * OTS * 2 <= (int)sizeof(smem), "output staging tile");
+  const bool stage_out = !(EPI & EPI_ADD) && a.outb && g.ldo % 8 == 0 && g.Nc % 8 == 0;
+  __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
   const int TV = g.T_out * g.V;
   const int nlo = m0 / TV;  // GAP is forward-only (no parity split): m0 is the first output row
 #pragma unroll
@@ -212,7 +218,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
           else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
         }
         if (!(EPI & EPI_ADD) && a.outb) {
-          reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+          if (stage_out) ot[(wm * 144 + x * 16 + fg * 4 + r) * OTS + j] = (__bf16)v;
+          else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
           if (EPI & EPI_ADD) *o += v;
@@ -261,6 +268,17 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         atomic_add_f(a.gap + (size_t)nlo * g.Nc + t, g0);
         if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + t, g1);
       }
+    }
+  }
+  if (stage_out) {
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+    for (int q = tid; q < BM * CPR; q += blockDim.x) {
+      const int rl = q / CPR, c = q - rl * CPR;
+      const int m = phys(m0 + rl), j = 0 + c * 8;
+      if (m < 0 || j >= g.Nc) continue;
+      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
+          *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
     }
   }
 }

@@ -18,6 +18,8 @@
 // pooling, ReLU mask + BN-backward sums, accumulate).
 #include "igemm.h"
 
+#include <algorithm>
+
 namespace f3 {
 
 constexpr int G_BM = 128;
@@ -188,6 +190,12 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   float ssum[WN], ssq[WN], gap0[WN], gap1[WN];
 #pragma unroll
   for (int y = 0; y < WN; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
+  // bf16 outputs leave through an LDS image of the tile: the MFMA C layout gives a lane 4 rows of
+  // ONE column (2-B scattered stores); the image is copied out as 16-B row chunks instead
+  constexpr int OTS = BN + 8, OT_OFF = 16 * 1024;  // row stride (elements), byte offset past red/gred
+  static_assert(OT_OFF + BM * OTS * 2 <= (int)sizeof(smem), "output staging tile");
+  const bool stage_out = !(EPI & EPI_ADD) && a.outb && g.ldo % 8 == 0 && g.Nc % 8 == 0;
+  __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
   const int TV = g.T_out * g.V;
   const int nlo = m0 / TV;
 #pragma unroll
@@ -221,7 +229,8 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
           else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
         }
         if (!(EPI & EPI_ADD) && a.outb) {
-          reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+          if (stage_out) ot[(wm * 64 + x * 16 + fg * 4 + r) * OTS + jl] = (__bf16)v;
+          else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
           if (EPI & EPI_ADD) *o += v;
@@ -265,6 +274,17 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
         atomic_add_f(a.gap + (size_t)nlo * g.Nc + j, s0);
         if ((nlo + 1) * TV < g.M && s1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + j, s1);
       }
+    }
+  }
+  if (stage_out) {
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+    for (int q = tid; q < BM * CPR; q += blockDim.x) {
+      const int rl = q / CPR, c = q - rl * CPR;
+      const int m = phys(m0 + rl), j = j0 + c * 8;
+      if (m < 0 || j >= g.Nc) continue;
+      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
+          *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
     }
   }
 }
@@ -518,14 +538,25 @@ bool f3_wgrad_glds_ok(const WgradArgs& a) {
 
 // dW accumulation target: WG_OUT_GCN writes the reference layout; WG_OUT_CONV writes the
 // PACKED layout [Nc][KT*Kc] (caller unpacks with PREP_UNPACK_CONV).
-int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
-  WgradArgs a = *args;
-  if (a.g.M <= 0) return F3_OK;
-  if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
-  const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;
+// Resident workgroups of a kernel on the whole chip (occupancy x CUs), queried once.
+static int resident_wgs(const void* fn, int threads) {
+  int per_cu = 0, dev = 0, cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetLastError();
+  return per_cu * cus;
+}
+
+template <int TJ, int TI>
+static int launch_wgrad_glds(WgradArgs a, hipStream_t s) {
   const int gx = (a.g.Nc + TJ - 1) / TJ;
   const int gy = a.g.KT * ((a.g.Kc + TI - 1) / TI);
-  int splits = (f3_wgrad_target_wgs() + gx * gy - 1) / (gx * gy);
+  // Split-K over rows sized to ONE round of resident workgroups: rounding the split count up
+  // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
+  // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
+  static const int slots = resident_wgs((const void*)wgrad_glds_bf16<TJ, TI>, 256);
+  const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
+  int splits = std::max(1, target / (gx * gy));
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + 63) / 64) * 64;
   if (rps < 256) rps = 256;
@@ -537,10 +568,18 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   static const int xcd = getenv("F3_WGRAD_XCD") ? atoi(getenv("F3_WGRAD_XCD")) : 1;
   a.xcd = xcd;
   dim3 grid = xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
-  if (TJ == 128 && TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 128>), grid, dim3(256), 0, s, a);
-  else if (TJ == 128) hipLaunchKernelGGL((wgrad_glds_bf16<128, 64>), grid, dim3(256), 0, s, a);
-  else if (TI == 128) hipLaunchKernelGGL((wgrad_glds_bf16<64, 128>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((wgrad_glds_bf16<64, 64>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((wgrad_glds_bf16<TJ, TI>), grid, dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();
   return F3_OK;
+}
+
+int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
+  const WgradArgs& a = *args;
+  if (a.g.M <= 0) return F3_OK;
+  if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;
+  if (TJ == 128 && TI == 128) return launch_wgrad_glds<128, 128>(a, s);
+  if (TJ == 128) return launch_wgrad_glds<128, 64>(a, s);
+  if (TI == 128) return launch_wgrad_glds<64, 128>(a, s);
+  return launch_wgrad_glds<64, 64>(a, s);
 }

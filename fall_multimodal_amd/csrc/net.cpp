@@ -78,12 +78,19 @@ const int kChan[7][4] = {{-1, 64, 1, RES_NONE}, {64, 64, 1, RES_ID},    {64, 64,
 struct f3_net {
   // branch concurrency: the position stream runs on the caller's stream, the motion stream
   // and the sensor branch on two private streams forked/joined with events (capturable)
-  hipStream_t aux[2] = {nullptr, nullptr};
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // aux[0]: motion stream, aux[1]: sensor branch, aux[2]: weight-gradient side stream (both
+  // skeleton streams' wgrad / gcn-bias work, off the backward critical path)
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_main[2][7] = {};  // per (skeleton stream, layer) main -> side hand-offs
   bool par_init = false, par_ok = false;
   ~f3_net() {
     for (auto& a : aux) if (a) (void)hipStreamDestroy(a);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i)
+      for (int l = 0; l < 7; ++l) {
+        if (ev_main[i][l]) (void)hipEventDestroy(ev_main[i][l]);
+      }
   }
   f3_config cfg;
   std::vector<Entry> entries;
@@ -242,13 +249,17 @@ struct LayerWs {
   unsigned short *u = nullptr, *outb = nullptr;
   const unsigned short* xb = nullptr;  // bf16 copy of the block input (RES_CONV blocks)
   float* dWp = nullptr;
+  // per-layer backward tensors the side stream's weight gradients read (dh: tcn output
+  // gradient, dg: gcn output gradient, dres: residual-conv output gradient): never re-used
+  // by another layer, so the main stream needs no wait on the side stream before the join
+  float *dh = nullptr, *dg = nullptr, *dres = nullptr;
 };
 
 struct StreamWs {
   float *x0, *pool, *A;  // A: copy of the adjacency buffer (backward has no buffer pointer)
   BnWs dbn;
   LayerWs L[7];
-  float *dh, *dres, *dv, *dg, *dZ, *dx[2], *dpool;
+  float *dv, *dZ, *dx[2], *dpool;
   float* mixpart;  // graph-mix dA partials [kMixParts][K*V*V]
   float* gpart;    // BN1-backward per-node column-sum partials
 };
@@ -374,6 +385,9 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dbn = A.take<float>((size_t)N * C / 4);
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
+      X.dh = A.take<float>(Mo * C);
+      X.dg = A.take<float>(Mi * C);
+      if (L.res == RES_CONV) X.dres = A.take<float>(Mo * C);
       xin = X.out;
       // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand)
       xinb = hb ? reinterpret_cast<const unsigned short*>(X.out) : nullptr;
@@ -382,10 +396,9 @@ Ws plan(const f3_net& net, int N, char* base) {
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
     }
-    W.dh = A.take<float>(maxMC);
-    W.dres = A.take<float>(maxMC);
+
     W.dv = A.take<float>(maxMC);
-    W.dg = A.take<float>(maxMC);
+
     W.dZ = A.take<float>(maxZ);
     W.dx[0] = A.take<float>(maxMC);
     W.dx[1] = A.take<float>(maxMC);
@@ -622,8 +635,17 @@ bool debug_stop(int si, int l) {
 // input gradient to W.dx[(6-l)&1] and reads layer l+1's from W.dx[(5-l)&1].
 // `unpack` collects the bf16 mode's packed tcn weight-gradient -> reference-layout jobs; the
 // caller flushes it (one prep launch per stream) after the stream's last layer call.
+// Main stream s: the chain that carries the input gradient down the layers. Side stream ss
+// (== s when not parallel): the layer's weight gradients (tcn / gcn / residual wgrad, gcn
+// bias + edge importance), which nothing downstream waits for. Layer l's side work starts
+// after ev_main[si][l]; it reads only per-layer tensors, so the only side -> main edge is the
+// final join. (Main also waiting on the side stream per layer — double-buffered scratch —
+// made HIP's stream-capture end fault on ROCm 7.2.)
 int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
-                    int l_hi, int l_lo, PrepTable& unpack) {
+                    int l_hi, int l_lo, PrepTable& unpack, hipStream_t ss = nullptr, int call_hi = 6) {
+  if (!ss) ss = s;
+  (void)call_hi;
+  const bool split = ss != s;
   const StreamIdx& S = net.st[si];
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V;
@@ -636,6 +658,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     const int C = L.cout, Ci = L.cin, Ti = L.T_in, To = L.T_out;
     const int Mi = N * Ti * V, Mo = N * To * V;
     float* dx = W.dx[pp];
+    float* const dh = X.dh;
+    float* const dg = X.dg;
+    float* const dres = X.dres;
     const BnRef bn1 = q.ref(L.bn1, X.bn1, (float)Mi, 0);
     const BnRef bn2 = q.ref(L.bn2, X.bn2, (float)Mo, 0);
     BnRef bnr;
@@ -647,10 +672,10 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.dout = dout; ba.dout_nc = l == 6 ? W.dpool : nullptr; ba.act16 = hb;
     ba.P1 = X.P1; ba.P2 = X.P2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
-    ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = W.dh;
-    ba.dres = L.res == RES_CONV ? W.dres : (L.res == RES_ID ? dx : nullptr);
-    ba.dhb = bfa(W.dh, hb);
-    ba.dresb = L.res == RES_CONV ? bfa(W.dres, hb) : nullptr;
+    ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = dh;
+    ba.dres = L.res == RES_CONV ? dres : (L.res == RES_ID ? dx : nullptr);
+    ba.dhb = bfa(dh, hb);
+    ba.dresb = L.res == RES_CONV ? bfa(dres, hb) : nullptr;
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     F3_TRY(f3_block_bwd_reduce(ba, s));
@@ -670,37 +695,23 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
-    td.in = hb ? nullptr : W.dh; td.inb = bfa(W.dh, hb); td.zero = w.zero;
+    td.in = hb ? nullptr : dh; td.inb = bfa(dh, hb); td.zero = w.zero;
     td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
     if (debug_stop(si, l)) return F3_OK;
-    WgradArgs tw;
-    std::memset(&tw, 0, sizeof(tw));
-    tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
-    tw.outmap = WG_OUT_CONV; tw.bf16 = hb;
-    if (hb) {  // bf16 operands dh, u; packed accumulator (unpacked into the grads below)
-      tw.dyb = bfa(W.dh, 1); tw.inb = X.u; tw.zero = w.zero; tw.dw = X.dWp;
-      if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
-      F3_TRY(f3_conv_wgrad(&tw, 0, s));
-      add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
-    } else {
-      tw.dy = W.dh; tw.in = X.g; tw.pro_bn = bn1;
-      F3_TRY(f3_conv_wgrad(&tw, 1, s));
-    }
     BnBwdArgs bb;
     std::memset(&bb, 0, sizeof(bb));
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
-    bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = W.dg; bb.G = X.G;
-    bb.Gpart = W.gpart; bb.dgb = bfa(W.dg, hb); bb.act16 = hb;
+    bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = dg; bb.G = X.G;
+    bb.Gpart = W.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb;
     F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     ConvGemmArgs gd;
     std::memset(&gd, 0, sizeof(gd));
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
-    gd.in = hb ? nullptr : W.dg; gd.inb = bfa(W.dg, hb); gd.zero = w.zero;
+    gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
     const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
@@ -708,44 +719,65 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gd.outb = bfa(W.dZ, 1);
     }
     F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
-    WgradArgs gw;
-    std::memset(&gw, 0, sizeof(gw));
-    gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
-    gw.ldy = C; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
-    if (hb) {
-      gw.dyb = bfa(W.dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero;
-    } else {
-      gw.dy = W.dg; gw.in = X.z;
-    }
-    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
-    F3_TRY(f3_conv_wgrad(&gw, 0, s));
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
     mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart; mx.x16 = hb;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
     F3_TRY(f3_mix_bwd(&mx, s));
-    GcnBiasBwdArgs gb;
-    gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
-    gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
-    F3_TRY(f3_gcn_bias_bwd(&gb, s));
     if (L.res == RES_CONV) {
       ConvGemmArgs rd;
       std::memset(&rd, 0, sizeof(rd));
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
-      rd.in = hb ? nullptr : W.dres; rd.inb = bfa(W.dres, hb); rd.zero = w.zero;
+      rd.in = hb ? nullptr : dres; rd.inb = bfa(dres, hb); rd.zero = w.zero;
       rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
       F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
+    }
+    // ---- side stream: this layer's weight gradients ----
+    if (split) {
+      if (hipEventRecord(net.ev_main[si][l], s) != hipSuccess) return F3_EHIP;
+      if (hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
+    }
+    WgradArgs tw;
+    std::memset(&tw, 0, sizeof(tw));
+    tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
+    tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
+    tw.outmap = WG_OUT_CONV; tw.bf16 = hb;
+    if (hb) {  // bf16 operands dh, u; packed accumulator (unpacked into the grads below)
+      tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero; tw.dw = X.dWp;
+      if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
+      F3_TRY(f3_conv_wgrad(&tw, 0, ss));
+      add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
+    } else {
+      tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
+      F3_TRY(f3_conv_wgrad(&tw, 1, ss));
+    }
+    WgradArgs gw;
+    std::memset(&gw, 0, sizeof(gw));
+    gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
+    gw.ldy = C; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
+    if (hb) {
+      gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero;
+    } else {
+      gw.dy = dg; gw.in = X.z;
+    }
+    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
+    F3_TRY(f3_conv_wgrad(&gw, 0, ss));
+    GcnBiasBwdArgs gb;
+    gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
+    gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
+    F3_TRY(f3_gcn_bias_bwd(&gb, ss));
+    if (L.res == RES_CONV) {
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
       rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
       rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
       if (hb) {
-        rw.dyb = bfa(W.dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+        rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
       } else {
-        rw.dy = W.dres; rw.in = X.x;
+        rw.dy = dres; rw.in = X.x;
       }
-      F3_TRY(f3_conv_wgrad(&rw, 0, s));
+      F3_TRY(f3_conv_wgrad(&rw, 0, ss));
     }
     dout = dx;
     pp ^= 1;
@@ -853,26 +885,36 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   bool ok = true;
   for (auto& a : n.aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
   for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; i < 2; ++i)
+    for (int l = 0; l < 7; ++l) {
+      ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], hipEventDisableTiming) == hipSuccess;
+    }
   (void)hipGetLastError();
   return n.par_ok = ok;
 }
 
 // Fork `k` branch streams off s (they see all work queued on s so far) / join them back.
+// Only the branch streams that will receive work are forked (mask bit i = aux[i]): a
+// forked-but-empty branch in a stream capture breaks HIP graph instantiation.
+enum : int { BR_MOTION = 1, BR_SENSOR = 2, BR_SIDE = 4 };
 struct Branches {
   f3_net& n;
   hipStream_t s;
   bool par;
-  hipStream_t at(int i) const { return par && i > 0 ? n.aux[i - 1] : s; }
+  int mask = BR_MOTION | BR_SENSOR | BR_SIDE;
+  hipStream_t at(int i) const { return par && i > 0 && (mask >> (i - 1) & 1) ? n.aux[i - 1] : s; }
+  hipStream_t side() const { return par && (mask & BR_SIDE) ? n.aux[2] : s; }
   int fork() {
-    if (!par) return F3_OK;
+    if (!par || !mask) return F3_OK;
     if (hipEventRecord(n.ev[0], s) != hipSuccess) return F3_EHIP;
-    for (auto a : n.aux)
-      if (hipStreamWaitEvent(a, n.ev[0], 0) != hipSuccess) return F3_EHIP;
+    for (int i = 0; i < 3; ++i)
+      if ((mask >> i & 1) && hipStreamWaitEvent(n.aux[i], n.ev[0], 0) != hipSuccess) return F3_EHIP;
     return F3_OK;
   }
   int join() {
     if (!par) return F3_OK;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
+      if (!(mask >> i & 1)) continue;
       if (hipEventRecord(n.ev[1 + i], n.aux[i]) != hipSuccess) return F3_EHIP;
       if (hipStreamWaitEvent(s, n.ev[1 + i], 0) != hipSuccess) return F3_EHIP;
     }
@@ -988,6 +1030,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
   BnRunTable run;
   run.n = 0;
   Branches br{*net, s, ensure_parallel(*net, s)};
+  br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0);
   F3_TRY(br.fork());
   // sensor branch first (small, latency-bound), then the two skeleton streams stage by stage,
   // interleaved, so every branch queue is fed from the start
@@ -1060,15 +1103,16 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     unpack[0].n = unpack[1].n = 0;
     for (int l = l_hi; l >= l_lo; --l)
       for (int si = 0; si < net->nstreams; ++si) {
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si]));
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], br.side(), l_hi));
         if (debug_stop(si, l)) return F3_OK;  // tools/diag_layer.py: leave the scratch as is
       }
     for (int si = 0; si < net->nstreams; ++si)
-      F3_TRY(f3_prep(unpack[si], br.at(si)));
+      F3_TRY(f3_prep(unpack[si], br.side()));  // the packed tcn weight gradients come from the side stream
     return F3_OK;
   };
   if (phase == 2) {
     Branches br{*net, s, ensure_parallel(*net, s)};
+    br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->nstreams > 0 ? BR_SIDE : 0);
     F3_TRY(br.fork());
     F3_TRY(skeleton(br, kSplitLayer - 1, 0));
     F3_TRY(br.join());
@@ -1090,6 +1134,8 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     F3_TRY(f3_head_bwd(&h, s));
   }
   Branches br{*net, s, ensure_parallel(*net, s)};
+  static const bool no_side = getenv("F3_NO_SIDE") != nullptr;
+  br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) | (net->nstreams > 0 && !no_side ? BR_SIDE : 0);
   F3_TRY(br.fork());
   if (net->has_sensor) {
     const hipStream_t ss = br.at(2);
@@ -1247,11 +1293,11 @@ void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, i
   if (k == "r") return X.r;
   if (k == "out") return X.out;
   if (k == "att") return X.att;
-  if (k == "dh") return W.dh;
+  if (k == "dh") return X.dh;
   if (k == "dv") return W.dv;
-  if (k == "dg") return W.dg;
+  if (k == "dg") return X.dg;
   if (k == "dZ") return W.dZ;
-  if (k == "dres") return W.dres;
+  if (k == "dres") return X.dres;
   if (k == "dx0") return W.dx[0];
   if (k == "dx1") return W.dx[1];
   if (k == "bn1_fsum") return X.bn1.fsum;
