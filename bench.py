@@ -12,8 +12,8 @@ branch, so none is built or timed.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
-ranks), the roofline of the dominant kernel (implicit-GEMM temporal conv, measured live
-with HIP events on the stream it runs on) and the CPU baseline (the oracle timed on this
+ranks), the roofline of the dominant kernel (the temporal-conv weight-gradient GEMM, measured
+live with HIP events on the stream it runs on; HBM traffic from profiles/r01_roofline_pmc.json) and the CPU baseline (the oracle timed on this
 host's cores on a bounded sample).
 """
 import argparse
@@ -53,44 +53,72 @@ def parse():
     return p.parse_args()
 
 
-def conv_roofline(dev, batch, V, precision):
-    """Dominant kernel: the (9,1) temporal conv implicit GEMM (conv_gemm_<precision>),
-    measured on the layer-6 shape of the step (C=256, T=8) with the weight operand already
-    packed (the GEMM launch alone). Algorithmic FLOP = 2*M*N*K per launch."""
-    import fall_multimodal_amd._lib as L
-    lib = L.lib()
-    N, T, C, KT = batch, 8, 256, 9
-    x = torch.randn(N, T, V, C, device=dev)
-    if precision == "bf16":  # the network's bf16 GEMM operand tensors are bf16 in HBM
-        x = x.to(torch.bfloat16)
-    w = torch.randn(C, C, KT, device=dev) / 48.0
-    b = torch.zeros(C, device=dev)
-    out = torch.empty(N, T, V, C, device=dev)
-    wp = torch.empty(C * KT * C, device=dev)
-    st = L.stream_handle()
-    prec = 1 if precision == "bf16" else 0
-    args = (L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(wp), N, T, V, C, C, KT, 1, 4, prec, st)
-    L.check(lib.f3_conv_forward(*args), "conv")  # packs w into wp
-    args = (L.ptr(x), None) + args[2:]
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r01_roofline_pmc.json")
+
+
+def _time_launch(fn, reps=20):
+    """Average duration of one launch, HIP events on torch's current stream — the stream the
+    library launches on (_lib.stream_handle)."""
     for _ in range(3):
-        L.check(lib.f3_conv_forward(*args), "conv")
-    reps = 20
+        fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(reps):
-        lib.f3_conv_forward(*args)
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    M = N * T * V
-    flop = 2.0 * M * C * (KT * C)
-    achieved = flop / (ms * 1e-3) / 1e12
+    return e0.elapsed_time(e1) / reps
+
+
+def roofline_kernels(dev, batch, V, precision):
+    """The step's GEMM kernels on the layer-6 tcn shape (C=256, T=8, 9 taps, B clips):
+    * "wgrad": the tcn weight gradient, wgrad_glds_bf16<128,128> — the kernel with the largest
+      share of the step's GPU time (profiles/r01_bf16_kernel_summary.txt), launched alone
+      through f3_conv_wgrad_packed exactly as the step launches it;
+    * "tcn_fwd": the forward implicit GEMM (igemm_big<1,1,8>: the step's launch is igemm_big<13,1,8>, the same GEMM with the BN-statistics and pooling epilogue), weight operand pre-packed.
+    Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for both."""
+    import fall_multimodal_amd._lib as L
+    lib = L.lib()
+    N, T, C, KT = batch, 8, 256, 9
+    flop = 2.0 * (N * T * V) * C * (KT * C)
     peak = PEAK_MFMA_TFLOPS[precision]
-    return {"kernel": f"{'igemm_bf16' if precision == 'bf16' else 'conv_gemm_f32'} (tcn 9x1, C=256, T=8, N={N}, V={V})", "bound": "mfma",
-            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
-            "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}
+    st = L.stream_handle()
+    out = {}
+    x = torch.randn(N, T, V, C, device=dev)
+    dy = torch.randn(N, T, V, C, device=dev)
+    if precision == "bf16":  # the network's bf16 GEMM operand tensors are bf16 in HBM
+        x, dy = x.to(torch.bfloat16), dy.to(torch.bfloat16)
+    w = torch.randn(C, C, KT, device=dev) / 48.0
+    b = torch.zeros(C, device=dev)
+    y = torch.empty(N, T, V, C, device=dev)
+    wp = torch.empty(C * KT * C, device=dev)
+    prec = 1 if precision == "bf16" else 0
+    L.check(lib.f3_conv_forward(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1, 4, prec, st),
+            "conv")  # packs w into wp; the timed launches reuse it (the GEMM alone)
+    ms = _time_launch(lambda: lib.f3_conv_forward(L.ptr(x), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1,
+                                                  4, prec, st))
+    out["tcn_fwd"] = {"kernel": f"{'igemm_big<1,1,8>' if prec else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, N={N}, V={V})",
+                      "ms": ms}
+    if prec:
+        dwp = torch.zeros(C * KT * C, device=dev)
+        L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(dwp), N, T, V, C, C, KT, 1, 4, st), "wgrad")
+        ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(dwp), N, T, V, C, C, KT, 1, 4, st))
+        out["wgrad"] = {"kernel": f"wgrad_glds_bf16<128,128> (tcn 9x1 weight gradient, C=256, T=8, N={N}, V={V})",
+                        "ms": ms}
+    pmc = {}
+    if os.path.exists(ROOFLINE_PMC):
+        with open(ROOFLINE_PMC) as f:
+            pmc = json.load(f)
+    res = {}
+    for key, r in out.items():
+        achieved = flop / (r["ms"] * 1e-3) / 1e12
+        t = pmc.get(key, {})
+        traffic = t.get("bytes_per_launch") if t.get("kernel") == r["kernel"] else None
+        res[key] = {"kernel": r["kernel"], "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "flop_per_launch": flop, "ms_per_launch": round(r["ms"], 4)}
+    return res
 
 
 def cpu_baseline(layout, V, S, seconds):
@@ -156,7 +184,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(step.loss.item())
-    roof = conv_roofline(dev, B, V, a.precision) if rank == 0 else None
+    roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
         rec = {
@@ -176,7 +204,8 @@ def main():
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5)},
-            "roofline": roof,
+            "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
+            "roofline_tcn_fwd": roofs["tcn_fwd"],
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

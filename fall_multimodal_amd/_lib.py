@@ -19,7 +19,7 @@ EXPORTS = (
     "f3_net_create", "f3_net_destroy", "f3_net_num_entries", "f3_net_entry", "f3_net_param_count",
     "f3_net_buffer_count", "f3_net_counter_count", "f3_net_workspace_bytes", "f3_net_forward",
     "f3_net_loss", "f3_net_backward", "f3_rmsprop_step", "f3_conv_forward", "f3_status_string",
-    "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_graph_mix_forward",
+    "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_graph_mix_forward",
     "f3_graph_mix_backward", "f3_net_backward_phase", "f3_net_grad_split",
 )
 
@@ -65,6 +65,7 @@ def lib():
         "f3_net_debug_tensor": (P, [P, I, P, I, I, ctypes.c_char_p]),
         "f3_conv_backward_data": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_conv_backward_weight": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_wgrad_packed": (I, [P, P, P, I, I, I, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
     }

@@ -1257,6 +1257,19 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
   return f3_conv_wgrad(&a, 0, s);
 }
 
+int f3_conv_wgrad_packed(const void* dy, const void* x, float* dw_packed, int N, int T_in, int V, int Cin, int Cout,
+                         int KT, int stride, int pad, void* stream) {
+  if (!dy || !x || !dw_packed || N < 1) return F3_EINVAL;
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  WgradArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
+  a.ldy = Cout; a.dw = dw_packed; a.db = nullptr; a.outmap = WG_OUT_CONV; a.bf16 = 1;
+  a.dyb = (const unsigned short*)dy; a.inb = (const unsigned short*)x; a.zero = test_zero_page();
+  if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  return f3_conv_wgrad(&a, 0, (hipStream_t)stream);
+}
+
 int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frames, int K, int V, int Cin,
                          void* stream) {
   MixArgs m;
