@@ -341,7 +341,9 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
     if (a.g.Nc > 64) return launch_igemm<4, 3>(a, epi, s);
     return launch_igemm<2, 3>(a, epi, s);
   }
-  if (a.g.Nc > 64) return launch_igemm<4, 2>(a, epi, s);
+  // 128-wide column tiles unless they would leave a partial tile (Nc = 192: the gcn input
+  // gradient of the 64-channel layers, where a second 128-wide tile is half empty)
+  if (a.g.Nc > 64 && a.g.Nc % 128 == 0) return launch_igemm<4, 2>(a, epi, s);
   return launch_igemm<2, 2>(a, epi, s);
 }
 

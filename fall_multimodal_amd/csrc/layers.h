@@ -42,6 +42,7 @@ struct MixArgs {
   float* part;           // bwd scratch [kMixParts][K*V*V] (MFMA path)
   unsigned short* zb;    // fwd: write z as bf16 (bf16 mode GEMM operand) instead of fp32
   const unsigned short* dzb;  // bwd: dZ in bf16 (instead of z) — LDS mix path only
+  int no_colsum;         // bwd: leave the dA partial rows in `part` (caller reduces: f3_mix_bwd_parts)
 };
 constexpr int kMixParts = 1024;
 
@@ -106,6 +107,7 @@ struct BnBwdArgs {
   float* G;              // [V][C] (accumulated from Gpart by a column reduction)
   float* Gpart;          // [gridDim][V*C] per-workgroup partial rows
   unsigned short* dgb;   // bf16 mode: dg as bf16 (GEMM operand) instead of fp32
+  int no_colsum;         // leave the G partial rows in Gpart (caller reduces with f3_colsum)
 };
 
 struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the bf16 mode
@@ -177,6 +179,7 @@ int f3_databn_fwd(const f3::DataBnArgs* a, hipStream_t s);
 int f3_databn_bwd(const f3::DataBnArgs* a, hipStream_t s);
 int f3_mix_fwd(const f3::MixArgs* a, hipStream_t s);
 int f3_mix_bwd(const f3::MixArgs* a, hipStream_t s);
+int f3_mix_bwd_parts(const f3::MixArgs* a);  // dA partial rows the LDS mix backward leaves (0: none)
 bool f3_mix_lds_ok(int K, int V, int Cin);  // the LDS/MFMA mix path (takes bf16 dZ)
 int f3_gcn_bias_bwd(const f3::GcnBiasBwdArgs* a, hipStream_t s);
 int f3_block_out(f3::BlockArgs a, hipStream_t s);
@@ -187,5 +190,6 @@ int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);  // out[c] += sum_r part[r][c]
 int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);
-int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);
+int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);          // input-gradient chain (ca_bwd1/2/3)
+int f3_ca_bwd_weights(const f3::CaArgs* a, hipStream_t s);  // W1/W2/b2 gradients (ca_bwd_w)
 int f3_bn_running(const f3::BnRunTable& t, hipStream_t s);

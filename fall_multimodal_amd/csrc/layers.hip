@@ -1187,6 +1187,7 @@ static int launch_mix_bwd(const MixArgs* a, hipStream_t s) {
   const int grid = std::min(a->frames, 768);  // resident workgroups loop over frames
   hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
   F3_LAUNCH_CHECK();
+  if (a->no_colsum) return F3_OK;
   return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
 }
 
@@ -1208,6 +1209,8 @@ static int mix_bwd_cin(const MixArgs* a, hipStream_t s) {
   if ((a->dzb != nullptr) != (a->x16 != 0)) return F3_EINVAL;  // bf16 dZ <=> bf16 x (the bf16 mode)
   return a->dzb ? mix_bwd_ks<CIN, true>(a, s) : mix_bwd_ks<CIN, false>(a, s);
 }
+
+int f3_mix_bwd_parts(const MixArgs* a) { return mix_lds_ok(*a) ? std::min(a->frames, 768) : 0; }
 
 int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
   if (mix_lds_ok(*a)) {
@@ -1272,6 +1275,7 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
   if (a.act16) hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(fch, a.N), dim3(threads), 0, s, a);
   else hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(fch, a.N), dim3(threads), 0, s, a);
   F3_LAUNCH_CHECK();
+  if (a.no_colsum) return F3_OK;
   return f3_colsum(a.Gpart, fch * a.N, a.V * a.C, a.G, s);
 }
 
@@ -1307,9 +1311,14 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, (a->N + kCaWClips - 1) / kCaWClips), dim3(256), 0, s, *a);
-  F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd3_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s) {
+  if (a->C > 256 || a->N > 256) return F3_EINVAL;
+  hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, (a->N + kCaWClips - 1) / kCaWClips), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

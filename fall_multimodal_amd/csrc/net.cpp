@@ -253,6 +253,9 @@ struct LayerWs {
   // gradient, dg: gcn output gradient, dres: residual-conv output gradient): never re-used
   // by another layer, so the main stream needs no wait on the side stream before the join
   float *dh = nullptr, *dg = nullptr, *dres = nullptr;
+  // per-layer partial rows of the BN1-backward node sums (G) and the graph-mix dA, reduced on
+  // the side stream
+  float *gpart = nullptr, *mixpart = nullptr;
 };
 
 struct StreamWs {
@@ -260,8 +263,6 @@ struct StreamWs {
   BnWs dbn;
   LayerWs L[7];
   float *dv, *dZ, *dx[2], *dpool;
-  float* mixpart;  // graph-mix dA partials [kMixParts][K*V*V]
-  float* gpart;    // BN1-backward per-node column-sum partials
 };
 
 struct Ws {
@@ -352,7 +353,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     StreamWs& W = w.st[si];
     W.x0 = A.take<float>((size_t)N * S.T * V * S.cin);
     W.A = A.take<float>((size_t)K * V * V);
-    size_t maxMC = 0, maxZ = 0, maxG = 0;
+    size_t maxMC = 0, maxZ = 0;
     const float* xin = W.x0;
     const unsigned short* xinb = nullptr;
     for (int l = 0; l < 7; ++l) {
@@ -387,11 +388,12 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.e = A.take<float>((size_t)N * C);
       X.dh = A.take<float>(Mo * C);
       X.dg = A.take<float>(Mi * C);
+      X.gpart = A.take<float>((size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
+      X.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
       if (L.res == RES_CONV) X.dres = A.take<float>(Mo * C);
       xin = X.out;
       // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand)
       xinb = hb ? reinterpret_cast<const unsigned short*>(X.out) : nullptr;
-      maxG = std::max(maxG, (size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
@@ -403,8 +405,6 @@ Ws plan(const f3_net& net, int N, char* base) {
     W.dx[0] = A.take<float>(maxMC);
     W.dx[1] = A.take<float>(maxMC);
     W.dpool = A.take<float>((size_t)N * 256);
-    W.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
-    W.gpart = A.take<float>(maxG);
   }
   if (net.has_sensor) {
     if (cnn) {
@@ -689,7 +689,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.bn2_bsum = X.bn2.bsum; ca.bn2_bsq = X.bn2.bsq;
     ca.g_bnca_gamma = q.g(L.bnca.w); ca.g_bnca_beta = q.g(L.bnca.b);
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
-    F3_TRY(f3_ca_bwd(&ca, s));
+    F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
     F3_TRY(f3_block_bwd_apply(ba, s));
     // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
     ConvGemmArgs td;
@@ -705,7 +705,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&bb, 0, sizeof(bb));
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = dg; bb.G = X.G;
-    bb.Gpart = W.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb;
+    bb.Gpart = X.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb; bb.no_colsum = split;
     F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     ConvGemmArgs gd;
@@ -722,7 +722,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
-    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = W.mixpart; mx.x16 = hb;
+    mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = X.mixpart; mx.x16 = hb;
+    mx.no_colsum = split;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
     F3_TRY(f3_mix_bwd(&mx, s));
     if (L.res == RES_CONV) {
@@ -751,6 +752,13 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
       F3_TRY(f3_conv_wgrad(&tw, 1, ss));
+    }
+    F3_TRY(f3_ca_bwd_weights(&ca, ss));
+    if (split) {  // reductions whose results only feed weight gradients
+      const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
+      F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
+      const int mparts = f3_mix_bwd_parts(&mx);
+      if (mparts) F3_TRY(f3_colsum(X.mixpart, mparts, K * V * V, X.dAeff, ss));
     }
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
