@@ -101,9 +101,11 @@ def roofline_kernels(dev, batch, V, precision):
     out["tcn_fwd"] = {"kernel": f"{'igemm_big<1,1,8>' if prec else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, N={N}, V={V})",
                       "ms": ms}
     if prec:
-        dwp = torch.zeros(C * KT * C, device=dev)
-        L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(dwp), N, T, V, C, C, KT, 1, 4, st), "wgrad")
-        ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(dwp), N, T, V, C, C, KT, 1, 4, st))
+        cap = 512 * 128 * 128  # the step's slab capacity (net.cpp kWgradSlabFloats)
+        slab = torch.empty(cap, device=dev)
+        L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4, st), "wgrad")
+        ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4,
+                                                           st))
         out["wgrad"] = {"kernel": f"wgrad_glds_bf16<128,128> (tcn 9x1 weight gradient, C=256, T=8, N={N}, V={V})",
                         "ms": ms}
     pmc = {}

@@ -65,7 +65,7 @@ def lib():
         "f3_net_debug_tensor": (P, [P, I, P, I, I, ctypes.c_char_p]),
         "f3_conv_backward_data": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_conv_backward_weight": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
-        "f3_conv_wgrad_packed": (I, [P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_wgrad_packed": (I, [P, P, P, ctypes.c_longlong, I, I, I, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
     }

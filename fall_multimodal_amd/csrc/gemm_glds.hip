@@ -510,7 +510,9 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
     for (int t = tid; t < TJ; t += 256)
       if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
   }
-  if (nst == 0) return;
+  const bool to_slab = a.slab != nullptr && a.outmap == WG_OUT_CONV;
+  if (nst == 0 && !to_slab) return;  // (a slab tile is written even when empty: it is summed)
+  float* slab = to_slab ? a.slab + (size_t)bz * g.Nc * g.KT * g.Kc : nullptr;
 #pragma unroll
   for (int x = 0; x < WJ; ++x) {
 #pragma unroll
@@ -528,9 +530,35 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
         } else {  // packed [Nc][KT*Kc]
           idx = (size_t)j * g.KT * g.Kc + (size_t)dt * g.Kc + i;
         }
-        atomic_add_f(a.dw + idx, acc[x][y][r]);
+        if (to_slab) slab[idx] = acc[x][y][r];
+        else atomic_add_f(a.dw + idx, acc[x][y][r]);
       }
     }
+  }
+}
+
+// dw_ref[j][i][dt] += sum_s slab[s][j][dt*Kc + i]. A workgroup owns 64 consecutive slab
+// elements (one (j, dt) row piece, Kc % 64 == 0); its 4 waves sum interleaved split subsets
+// (coalesced 256-B reads, independent loads) and combine through LDS.
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
+                                                                int Kc, int KT, float* __restrict__ dw_ref) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t e = (size_t)blockIdx.x * 64 + lane;  // slab element (j, dt, i)
+  const size_t stride = (size_t)Nc * KT * Kc;
+  float acc0 = 0.f, acc1 = 0.f;
+  int sp = wave;
+  for (; sp + 4 < splits; sp += 8) {
+    acc0 += slab[(size_t)sp * stride + e];
+    acc1 += slab[(size_t)(sp + 4) * stride + e];
+  }
+  if (sp < splits) acc0 += slab[(size_t)sp * stride + e];
+  part[wave][lane] = acc0 + acc1;
+  __syncthreads();
+  if (wave == 0) {
+    const float v = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    const int j = (int)(e / ((size_t)KT * Kc)), r = (int)(e - (size_t)j * KT * Kc), dt = r / Kc, i = r - dt * Kc;
+    dw_ref[((size_t)j * Kc + i) * KT + dt] += v;
   }
 }
 
@@ -559,6 +587,12 @@ static int launch_wgrad_glds(WgradArgs a, hipStream_t s) {
   static const int slots = resident_wgs((const void*)wgrad_glds_bf16<TJ, TI>, 256);
   const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
   int splits = std::max(1, target / (gx * gy));
+  const bool to_slab = a.slab && a.outmap == WG_OUT_CONV;
+  const long long per_split = (long long)a.g.Nc * a.g.KT * a.g.Kc;
+  if (to_slab) {
+    if (a.slab_cap < per_split) return F3_EINVAL;
+    splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
+  }
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + 63) / 64) * 64;
   if (rps < 256) rps = 256;
@@ -572,6 +606,11 @@ static int launch_wgrad_glds(WgradArgs a, hipStream_t s) {
   dim3 grid = xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
   hipLaunchKernelGGL((wgrad_glds_bf16<TJ, TI>), grid, dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();
+  if (to_slab && a.dw_ref) {
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
+                       a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref);
+    F3_LAUNCH_CHECK();
+  }
   return F3_OK;
 }
 

@@ -63,6 +63,13 @@ struct WgradArgs {
   const unsigned short* inb;  // bf16 input rows (instead of in)
   const unsigned short* zero; // >= 16 zero bytes (LDS-DMA kernel)
   int xcd;                    // LDS-DMA kernel: XCD-aware 1-D grid (set by the launcher)
+  // LDS-DMA kernel, WG_OUT_CONV: per-split partial tiles go to slab[split][Nc][KT*Kc] with plain
+  // stores instead of fp32 atomics into dw (33 MB of memory-side atomics per layer-6 launch at
+  // ~1.3 TB/s); the launcher then sums the splits into dw_ref (reference layout [Nc][Kc][KT], +=).
+  // dw_ref == null: leave the partials in the slab (roofline timing of the kernel alone).
+  float* slab;
+  long long slab_cap;         // floats
+  float* dw_ref;
 };
 
 }  // namespace f3

@@ -234,6 +234,15 @@ struct Arena {
   }
 };
 
+// slab capacity: one round of resident 128x128 weight-gradient tiles (2 per CU x 256 CUs); the
+// launcher caps the split count to it
+constexpr long long kWgradSlabFloats = 512LL * 128 * 128;
+// F3_WGRAD_SLAB=0: fp32 atomics into a packed accumulator instead of slab partials (A/B)
+inline bool wgrad_slab() {
+  static const bool on = !getenv("F3_WGRAD_SLAB") || atoi(getenv("F3_WGRAD_SLAB")) != 0;
+  return on;
+}
+
 struct BnWs {
   double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
 };
@@ -263,6 +272,7 @@ struct StreamWs {
   BnWs dbn;
   LayerWs L[7];
   float *dv, *dZ, *dx[2], *dpool;
+  float* slab;  // bf16 weight-gradient split partials (see WgradArgs::slab); one per skeleton stream
 };
 
 struct Ws {
@@ -338,7 +348,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.P2 = A.take<float>((size_t)N * L.cout);
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
-      if (hb) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);
+      if (hb && !wgrad_slab()) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);  // atomic accumulator
     }
   }
   if (net.has_sensor && cnn) {
@@ -400,6 +410,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     }
 
     W.dv = A.take<float>(maxMC);
+    W.slab = A.take<float>(kWgradSlabFloats);
 
     W.dZ = A.take<float>(maxZ);
     W.dx[0] = A.take<float>(maxMC);
@@ -744,11 +755,16 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
     tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
     tw.outmap = WG_OUT_CONV; tw.bf16 = hb;
-    if (hb) {  // bf16 operands dh, u; packed accumulator (unpacked into the grads below)
-      tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero; tw.dw = X.dWp;
+    if (hb) {  // bf16 operands dh, u; split partials in the stream's slab, summed into the grads
+      tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
+      if (wgrad_slab()) {
+        tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats; tw.dw_ref = q.g(L.tcn_w);
+      } else {  // fp32 atomics into a packed accumulator, unpacked below
+        tw.dw = X.dWp;
+        add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
+      }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       F3_TRY(f3_conv_wgrad(&tw, 0, ss));
-      add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
       F3_TRY(f3_conv_wgrad(&tw, 1, ss));
@@ -782,6 +798,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
       if (hb) {
         rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+        if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
       } else {
         rw.dy = dres; rw.in = X.x;
       }
@@ -1247,16 +1264,12 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
     a.dyb = (const unsigned short*)dy;
     a.inb = (const unsigned short*)x;
     a.zero = test_zero_page();
-    if (f3_wgrad_glds_ok(a) && KT > 1) {  // packed accumulator, then unpack
-      float* packed = test_scratch((size_t)Cout * Cin * KT);
-      if (!packed) return F3_EHIP;
-      if (hipMemsetAsync(packed, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
-      a.dw = packed;
-      F3_TRY(f3_conv_wgrad(&a, 0, s));
-      PrepTable t;
-      t.n = 0;
-      add_job(t, PREP_UNPACK_CONV, Cout * Cin * KT, dw, packed, nullptr, nullptr, Cout, Cin, KT);
-      return f3_prep(t, s);
+    if (f3_wgrad_glds_ok(a)) {  // split partials in a scratch slab, summed into dw (the step's path)
+      const long long cap = kWgradSlabFloats;
+      float* slab = test_scratch((size_t)cap);
+      if (!slab) return F3_EHIP;
+      a.slab = slab; a.slab_cap = cap; a.dw_ref = dw;
+      return f3_conv_wgrad(&a, 0, s);
     }
   } else {
     a.dy = (const float*)dy;
@@ -1265,14 +1278,15 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
   return f3_conv_wgrad(&a, 0, s);
 }
 
-int f3_conv_wgrad_packed(const void* dy, const void* x, float* dw_packed, int N, int T_in, int V, int Cin, int Cout,
-                         int KT, int stride, int pad, void* stream) {
-  if (!dy || !x || !dw_packed || N < 1) return F3_EINVAL;
+int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long slab_floats, int N, int T_in, int V,
+                         int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+  if (!dy || !x || !slab || N < 1) return F3_EINVAL;
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   WgradArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
-  a.ldy = Cout; a.dw = dw_packed; a.db = nullptr; a.outmap = WG_OUT_CONV; a.bf16 = 1;
+  a.ldy = Cout; a.dw = nullptr; a.db = nullptr; a.outmap = WG_OUT_CONV; a.bf16 = 1;
+  a.slab = slab; a.slab_cap = slab_floats; a.dw_ref = nullptr;  // the kernel alone: partials stay in the slab
   a.dyb = (const unsigned short*)dy; a.inb = (const unsigned short*)x; a.zero = test_zero_page();
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
   return f3_conv_wgrad(&a, 0, (hipStream_t)stream);

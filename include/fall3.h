@@ -116,11 +116,12 @@ int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpac
                           int Cout, int KT, int stride, int pad, int precision, void* stream);
 int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, int precision, void* stream);
-/* The bf16 weight-gradient kernel alone (what the training step launches per layer): ADDS
- * dw_packed[Cout][KT*Cin] += sum_m dy[m][j] x[src(m,dt)][i] (caller zeroes; no bias, no
- * unpack). bf16 dy / x; requires Cout % 64 == 0, Cin % 64 == 0. Used to time the kernel. */
-int f3_conv_wgrad_packed(const void* dy, const void* x, float* dw_packed, int N, int T_in, int V, int Cin, int Cout,
-                         int KT, int stride, int pad, void* stream);
+/* The bf16 weight-gradient kernel alone, as the training step launches it per layer: each
+ * split of the rows writes its partial dW tile to slab[split][Cout][KT*Cin] (plain stores; the
+ * step then sums the splits with a separate reduce launch, not done here). bf16 dy / x;
+ * requires Cout % 64 == 0, Cin % 64 == 0, slab_floats >= Cout*KT*Cin. Used to time the kernel. */
+int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long slab_floats, int N, int T_in, int V,
+                         int Cin, int Cout, int KT, int stride, int pad, void* stream);
 
 /* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):
  * z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci]; backward gives dx and dA_eff (overwritten). */
