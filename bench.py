@@ -123,6 +123,23 @@ def roofline_kernels(dev, batch, V, precision):
     return res
 
 
+def eval_throughput(model, sk, se, reps=20):
+    """Eval step: the eval-mode forward (BN running statistics) of the same
+    B clips, as model/main.py's valid/test loops run it; clips/s over `reps` forwards."""
+    B = sk.shape[0]
+    out = torch.empty(B, model.spec.num_class, device=sk.device)
+    ws = torch.empty(model._native.workspace_bytes(B), dtype=torch.uint8, device=sk.device)
+    for _ in range(3):
+        model.native_forward(sk, se, out, ws, False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        model.native_forward(sk, se, out, ws, False)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {"clips_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3), "batch": B}
+
+
 def cpu_baseline(layout, V, S, seconds):
     """The oracle (CPU PyTorch restatement, pinned to the reference) on this host's cores."""
     from oracle import model_cpu as oc
@@ -186,6 +203,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(step.loss.item())
+    ev = eval_throughput(model, sk, se) if rank == 0 else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
@@ -208,6 +226,7 @@ def main():
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5)},
             "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
+            "eval_forward": ev,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

@@ -6,7 +6,9 @@ Public surface mirrors the reference (Multimodal_Fall3/model/):
     build_model(config)          -> model/build_model.py
     build_optimizer(model, cfg)  -> model/optimizer.py
     get_cfg_defaults()           -> model/config.py
-plus TrainStep, the fused graph-capturable step used by bench.py.
+plus TrainStep, the fused multi-stream step used by bench.py, and the steps either side of it
+(SURVEY §8f): data (window files, video-wise splits, pinned double-buffered loader) and
+evaluate (valid / test loops, top-k, macro P/R/F1, best-model checkpoints).
 """
 from .config import CfgNode, get_cfg_defaults
 from .graph import Graph
@@ -14,7 +16,8 @@ from .model import (BiLSTM, Fall3Net, NetSpec, STGCAN, TwoStreamSpatialTemporalG
                     TwoStreamSTGCAN_BiLSTM, build_model)
 from .optim import RMSprop, build_optimizer
 from .train import TrainStep
+from . import data, evaluate
 
 __all__ = ["build_model", "build_optimizer", "get_cfg_defaults", "CfgNode", "Graph", "Fall3Net", "NetSpec",
            "STGCAN", "BiLSTM", "TwoStreamSTGCAN", "TwoStreamSTGCAN_BiLSTM", "TwoStreamSpatialTemporalGraph",
-           "RMSprop", "TrainStep"]
+           "RMSprop", "TrainStep", "data", "evaluate"]

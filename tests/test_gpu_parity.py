@@ -369,3 +369,37 @@ def test_top1_accuracy_parity():
     for prec, r in got.items():
         for k, b in bound.items():
             assert abs(float(np.mean(r[k])) - float(np.mean(ref[k]))) <= b, (prec, k, r[k], ref[k])
+
+
+def test_eval_step_and_loader_match_oracle():
+    """SURVEY §8f rows 1-2 on the device: the pinned, double-buffered WindowLoader feeds the
+    eval step (fall_multimodal_amd.evaluate.test: eval-mode forward through the BN running
+    statistics, top-k, macro P/R/F1) and the result equals the oracle's eval-mode forward on
+    the same windows: logits within 1e-3 (fp32 mode), identical argmax and top-k."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    from fall_multimodal_amd import data as fd
+    from fall_multimodal_amd import evaluate as fe
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_mmpose", num_class=11, sensor_dim=6)
+    st = oc.init_state(spec, 31)
+    # non-trivial running statistics (as after training): one oracle train-mode forward
+    with torch.no_grad():
+        oc.forward(st, spec, *(torch.from_numpy(x) for x in synthetic_batch(64, 18, 11, 6, 20)[:2]), training=True)
+    skel, sensor, label = synthetic_batch(80, 18, 11, 6, 21)
+    w = fd.Windows([f"v{i // 4}" for i in range(80)], np.ascontiguousarray(skel.transpose(0, 2, 3, 1)), sensor, label)
+    loader = fd.WindowLoader(w, 32, shuffle=False, drop_last=False, device=d)
+    got = [b for b in loader]
+    assert [b[0].shape[0] for b in got] == [32, 32, 16]
+    np.testing.assert_array_equal(torch.cat([b[0] for b in got]).cpu().numpy(), skel)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d)
+    model.load_state_dict(st)
+    out, _ = fe.predict(model, loader)
+    with torch.no_grad():
+        ref = oc.forward(st, spec, torch.from_numpy(skel), torch.from_numpy(sensor), training=False).numpy()
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-3, rtol=0)
+    assert (out.cpu().numpy().argmax(1) == ref.argmax(1)).all()
+    res = fe.test(model, loader, torch.nn.CrossEntropyLoss(), top_k=(1, 5), num_classes=11)
+    assert res["top_k"] == fe.cal_top_k_accuracy(torch.from_numpy(ref), torch.from_numpy(label), (1, 5))
+    ref_m = fe.class_metrics(ref.argmax(1), label.argmax(1), 11)
+    assert (res["precision"], res["recall"], res["f1"]) == (ref_m["precision"], ref_m["recall"], ref_m["f1"])
