@@ -101,12 +101,13 @@ def roofline_kernels(dev, batch, V, precision):
     out["tcn_fwd"] = {"kernel": f"{'igemm_big<1,1,8>' if prec else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, N={N}, V={V})",
                       "ms": ms}
     if prec:
-        cap = 512 * 128 * 128  # the step's slab capacity (net.cpp kWgradSlabFloats)
+        cap = 512 * 128 * 128 * max(1, int(os.environ.get("F3_SLAB_X", "1")))  # the step's slab (net.cpp wgrad_slab_floats)
         slab = torch.empty(cap, device=dev)
         L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4, st), "wgrad")
         ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4,
                                                            st))
-        out["wgrad"] = {"kernel": f"wgrad_glds_bf16<128,128> (tcn 9x1 weight gradient, C=256, T=8, N={N}, V={V})",
+        kname = "wgrad_big<4,2,4,4,64>" if os.environ.get("F3_WGRAD_BIG", "1") != "0" else "wgrad_glds_bf16<128,128>"
+        out["wgrad"] = {"kernel": f"{kname} (tcn 9x1 weight gradient, C=256, T=8, N={N}, V={V})",
                         "ms": ms}
     pmc = {}
     if os.path.exists(ROOFLINE_PMC):

@@ -364,8 +364,35 @@ typedef short s16x8_t __attribute__((ext_vector_type(8)));
 
 template <int U>
 F3_DEV int wswz(int r) {  // unit permutation of row r (U 32-B units per row)
-  if (U == 8) return (r & 3) | (((r >> 3) & 1) << 2);
+  if (U >= 8) return (r & 3) | (((r >> 3) & 1) << 2);  // 8 or 16 units
   return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+}
+
+// Transposed LDS read issued from inline asm. The builtin (__builtin_amdgcn_ds_read_tr16_b64)
+// carries no memory operand, so hipcc (ROCm 7.2) cannot tell it from a read of the LDS-DMA
+// destination and waits vmcnt(0) before the first one of every stage: the stage just issued
+// must land before the current one is consumed, which de-pipelines the ring (measured: the
+// layer-6 wgrad spent 46 of 89 us in that wait). The asm read is invisible to the compiler's
+// counters, so the caller waits lgkmcnt(0) itself (tr_wait) before using the results; the
+// results pass through that asm so nothing can read them earlier.
+typedef __attribute__((address_space(3))) const char lds_cchar_t;
+F3_DEV s16x4_t tr_issue(const char* p) {
+  s16x4_t r;
+  const unsigned addr = (unsigned)(size_t)(lds_cchar_t*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int NF>
+F3_DEV void tr_wait(s16x4_t (&lo)[NF], s16x4_t (&hi)[NF]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(lo[i]), "+v"(hi[i]));
+}
+F3_DEV bf16x8 tr_join(s16x4_t lo, s16x4_t hi) {
+  s16x8_t v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 template <int TJ, int TI>  // tile widths: 128 or 64
@@ -437,21 +464,14 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
   const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
   // transposed fragment of a [64][cols] tile: lane (fg, fr) gets column c0+fr of rows
   // kb+8fg .. kb+8fg+7 (kb = 0 or 32)
-  auto tr_frag = [&](const char* tile, int U, int c0, int kb) {
-    typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+  auto tr_frag = [&](const char* tile, int U, int c0, int kb, s16x4_t& lo, s16x4_t& hi) {
     const int r_lo = kb + 8 * fg + tq, r_hi = r_lo + 4;
     const int u = c0 >> 4;
     const int R = U * 32;
     const int f_lo = U == 8 ? wswz<8>(r_lo) : wswz<4>(r_lo);
     const int f_hi = U == 8 ? wswz<8>(r_hi) : wswz<4>(r_hi);
-    const char* p0 = tile + r_lo * R + ((u ^ f_lo) * 32) + tp * 8;
-    const char* p1 = tile + r_hi * R + ((u ^ f_hi) * 32) + tp * 8;
-    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
-    s16x8_t v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
-    return __builtin_bit_cast(bf16x8, v);
+    lo = tr_issue(tile + r_lo * R + ((u ^ f_lo) * 32) + tp * 8);
+    hi = tr_issue(tile + r_hi * R + ((u ^ f_hi) * 32) + tp * 8);
   };
 
   f32x4 acc[WJ][WI];
@@ -477,10 +497,16 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 fa[WJ], fb[WI];
+      s16x4_t lo[WJ + WI], hi[WJ + WI];
 #pragma unroll
-      for (int x = 0; x < WJ; ++x) fa[x] = tr_frag(sy, UJ, wm * 16 * WJ + x * 16, ks * 32);
+      for (int x = 0; x < WJ; ++x) tr_frag(sy, UJ, wm * 16 * WJ + x * 16, ks * 32, lo[x], hi[x]);
 #pragma unroll
-      for (int y = 0; y < WI; ++y) fb[y] = tr_frag(sx, UI, wn * 16 * WI + y * 16, ks * 32);
+      for (int y = 0; y < WI; ++y) tr_frag(sx, UI, wn * 16 * WI + y * 16, ks * 32, lo[WJ + y], hi[WJ + y]);
+      tr_wait(lo, hi);
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) fa[x] = tr_join(lo[x], hi[x]);
+#pragma unroll
+      for (int y = 0; y < WI; ++y) fb[y] = tr_join(lo[WJ + y], hi[WJ + y]);
       if (do_db && wn == 0) {
 #pragma unroll
         for (int x = 0; x < WJ; ++x)
@@ -562,6 +588,232 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
   }
 }
 
+// ----------------------------------------------------------------------------
+// wgrad_big: the same weight-gradient GEMM for the 128/256-channel layers with 8 waves
+// (512 threads, one workgroup per CU), a 3-stage LDS-DMA ring behind a counted vmcnt and raw
+// s_barrier (the igemm_big structure: two 64-row stages stay in flight while the third is
+// consumed), and tiles of TJ x TI = (WJW*16*MJ) x (WIW*16*MI). Staging pieces: 1-KiB DMA
+// instructions, piece q = i*8 + wave (dY pieces first), so every wave issues the same count
+// per stage and one vmcnt constant serves all. 32-B units are swizzled as in wgrad_glds_bf16
+// (rows of 16 units use the 8-unit permutation: the half-wave tr read still covers 64 banks).
+//
+// The loop is kept lean in VALU work — at 2 waves per SIMD the per-stage address arithmetic,
+// not the MFMA or the memory, bounded the first version (a loop with the loads and MFMAs
+// removed still took half the time): every lane's LDS fragment offsets are fixed for the
+// whole loop (the tr reads of a fragment differ only by immediates: +4 rows, +32 rows), and
+// each staging lane walks its (clip, frame, joint) row coordinates incrementally instead of
+// dividing by V and T per stage. Forward-geometry rows only (g.transposed == 0).
+// ----------------------------------------------------------------------------
+template <int WJW, int WIW, int MJ, int MI, int BK = 64>
+__global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a) {
+  constexpr int NW = WJW * WIW;  // waves: 8 (one workgroup per CU) or 4 (the 64-wide tiles)
+  constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;
+  constexpr int UJ = TJ / 16, UI = TI / 16;
+  constexpr int RJ = TJ * 2, RI = TI * 2;  // row bytes of the dY / input tiles
+  constexpr int NKS = BK / 32;             // 32-deep MFMA k steps per stage
+  constexpr int Y_BYTES = BK * RJ, X_BYTES = BK * RI, STAGE = Y_BYTES + X_BYTES;
+  constexpr int YPW = Y_BYTES / 1024 / NW, XPW = X_BYTES / 1024 / NW, PPW = YPW + XPW;  // pieces per wave
+  constexpr int YRPI = 1024 / RJ, XRPI = 1024 / RI;  // rows per piece
+  constexpr int NST = 3;
+  static_assert(BK == 32 || BK == 64, "stage depth");
+  static_assert((NW == 8 || NW == 4) && YPW * NW * 1024 == Y_BYTES && XPW * NW * 1024 == X_BYTES, "whole pieces");
+  static_assert(UJ >= 4 && UI >= 4, "64-column tiles at least");
+  static_assert(NST * STAGE + TJ * 4 <= 160 * 1024, "LDS");
+  static_assert(32 * RJ + 4 * RJ < 65536 && 32 * RI + 4 * RI < 65536, "ds offset immediates");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + TJ * 4];
+  float* dbs = reinterpret_cast<float*>(smem + NST * STAGE);  // [TJ]
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int itiles = (g.Kc + TI - 1) / TI;
+  const int gx = (g.Nc + TJ - 1) / TJ, gy = g.KT * itiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a row split's tiles stay on one XCD
+  const int bz = lin / (gx * gy);
+  const int rem = lin - bz * gx * gy;
+  const int by = rem / gx, bx = rem - by * gx;
+  const int j0 = bx * TJ;
+  const int dt = by / itiles;
+  const int i0 = (by - dt * itiles) * TI;
+  const int r_begin = bz * a.rows_per_split;
+  const int r_end = min(g.M, r_begin + a.rows_per_split);
+  const bool do_db = a.db && by == 0;
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const __bf16* zero = reinterpret_cast<const __bf16*>(a.zero);
+  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+
+  // ---- staging lanes: fixed column, rows walked 64 at a time ----
+  const int ysub = lane / (TJ / 8), yph = lane % (TJ / 8);
+  const int xsub = lane / (TI / 8), xph = lane % (TI / 8);
+  int ycol[YPW], yrow[YPW];
+#pragma unroll
+  for (int i = 0; i < YPW; ++i) {
+    const int rr = (i * NW + wave) * YRPI + ysub;
+    yrow[i] = r_begin + rr;
+    ycol[i] = j0 + ((yph >> 1) ^ wswz<UJ>(rr)) * 16 + (yph & 1) * 8;
+  }
+  // input rows: m = (n*T_out + t)*V + v -> source (n*T_in + t*S + dt - P)*V + v
+  const int dv = BK % g.V, dnt = BK / g.V;
+  int xm[XPW], xv[XPW], xt[XPW], xn[XPW], xcol[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int rr = (i * NW + wave) * XRPI + xsub;
+    const int m = r_begin + rr;
+    xm[i] = m;
+    const int nt = m / g.V;
+    xv[i] = m - nt * g.V;
+    xn[i] = nt / g.T_out;
+    xt[i] = nt - xn[i] * g.T_out;
+    xcol[i] = i0 + ((xph >> 1) ^ wswz<UI>(rr)) * 16 + (xph & 1) * 8;
+  }
+  const int tshift = dt - g.P;
+  auto stage = [&](int buf) {  // issue the next BK rows of every staging lane, then advance them
+    const unsigned sy = lds0 + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < YPW; ++i) {
+      const __bf16* src = (yrow[i] < r_end && ycol[i] < g.Nc) ? dyb + (size_t)yrow[i] * a.ldy + ycol[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (lds_void_t*)(size_t)(sy + (i * NW + wave) * 1024), 16, 0, 0);
+      yrow[i] += BK;
+    }
+    const unsigned sx = sy + Y_BYTES;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+      const int ti = xt[i] * g.S + tshift;
+      const bool ok = xm[i] < r_end && xcol[i] < g.Kc && ti >= 0 && ti < g.T_in;
+      const __bf16* src = ok ? xb + (size_t)((xn[i] * g.T_in + ti) * g.V + xv[i]) * g.lda + xcol[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (lds_void_t*)(size_t)(sx + (i * NW + wave) * 1024), 16, 0, 0);
+      xm[i] += BK;
+      xv[i] += dv;
+      xt[i] += dnt;
+      if (xv[i] >= g.V) { xv[i] -= g.V; xt[i] += 1; }
+      while (xt[i] >= g.T_out) { xt[i] -= g.T_out; xn[i] += 1; }
+    }
+  };
+
+  // ---- fragment lanes: fixed LDS offsets ----
+  const int wj = wave / WIW, wi = wave % WIW;
+  const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
+  const int r0 = 8 * fg + tq;                 // rows r0, r0+4 (lo/hi), +32 for the second k half
+  const int fj = wswz<UJ>(r0), fi = wswz<UI>(r0);  // unchanged at r0 + 4, r0 + 32, r0 + 36
+  unsigned offa[MJ], offb[MI];
+#pragma unroll
+  for (int x = 0; x < MJ; ++x) offa[x] = r0 * RJ + (((wj * MJ + x) ^ fj) * 32) + tp * 8;
+#pragma unroll
+  for (int y = 0; y < MI; ++y) offb[y] = Y_BYTES + r0 * RI + (((wi * MI + y) ^ fi) * 32) + tp * 8;
+
+  f32x4 acc[MJ][MI];
+#pragma unroll
+  for (int x = 0; x < MJ; ++x)
+#pragma unroll
+    for (int y = 0; y < MI; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbp[MJ];
+#pragma unroll
+  for (int x = 0; x < MJ; ++x) dbp[x] = 0.f;
+
+  const int nst = r_end > r_begin ? (r_end - r_begin + BK - 1) / BK : 0;
+  if (nst > 0) {
+    stage(0);
+    if (nst > 1) {
+      stage(1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int t = 0; t < nst; ++t) {
+    const int buf = t % NST;
+    if (t + 2 < nst) stage((t + 2) % NST);
+    const unsigned base = lds0 + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      s16x4_t lo[MJ + MI], hi[MJ + MI];
+#pragma unroll
+      for (int x = 0; x < MJ; ++x) {
+        const unsigned p = base + offa[x];
+        if (ks == 0) {
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[x]) : "v"(p));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[x]) : "v"(p), "n"(4 * RJ));
+        } else {
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[x]) : "v"(p), "n"(32 * RJ));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[x]) : "v"(p), "n"(36 * RJ));
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < MI; ++y) {
+        const unsigned p = base + offb[y];
+        if (ks == 0) {
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[MJ + y]) : "v"(p));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[MJ + y]) : "v"(p), "n"(4 * RI));
+        } else {
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[MJ + y]) : "v"(p), "n"(32 * RI));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[MJ + y]) : "v"(p), "n"(36 * RI));
+        }
+      }
+      tr_wait(lo, hi);
+      bf16x8 fa[MJ], fb[MI];
+#pragma unroll
+      for (int x = 0; x < MJ; ++x) fa[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[x], hi[x], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int y = 0; y < MI; ++y)
+        fb[y] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[MJ + y], hi[MJ + y], 0, 1, 2, 3, 4, 5, 6, 7));
+      if (do_db && wi == 0) {
+#pragma unroll
+        for (int x = 0; x < MJ; ++x)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dbp[x] += (float)fa[x][e];
+      }
+#pragma unroll
+      for (int x = 0; x < MJ; ++x)
+#pragma unroll
+        for (int y = 0; y < MI; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+    }
+    if (t + 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if (do_db) {
+#pragma unroll
+    for (int x = 0; x < MJ; ++x) {
+      dbp[x] += __shfl_xor(dbp[x], 16, 64);
+      dbp[x] += __shfl_xor(dbp[x], 32, 64);
+    }
+    if (wi == 0 && fg == 0) {
+#pragma unroll
+      for (int x = 0; x < MJ; ++x) dbs[wj * 16 * MJ + x * 16 + fr] = dbp[x];
+    }
+    __syncthreads();
+    for (int t = tid; t < TJ; t += NW * 64)
+      if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
+  }
+  const bool to_slab = a.slab != nullptr && a.outmap == WG_OUT_CONV;
+  if (nst == 0 && !to_slab) return;
+  float* slab = to_slab ? a.slab + (size_t)bz * g.Nc * g.KT * g.Kc : nullptr;
+#pragma unroll
+  for (int x = 0; x < MJ; ++x) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = j0 + wj * 16 * MJ + x * 16 + fg * 4 + r;
+      if (j >= g.Nc) continue;
+#pragma unroll
+      for (int y = 0; y < MI; ++y) {
+        const int i = i0 + wi * 16 * MI + y * 16 + fr;
+        if (i >= g.Kc) continue;
+        size_t idx;
+        if (a.outmap == WG_OUT_GCN) {
+          const int k = i / a.gcn_cin, ci = i - k * a.gcn_cin;
+          idx = ((size_t)k * g.Nc + j) * a.gcn_cin + ci;
+        } else {
+          idx = (size_t)j * g.KT * g.Kc + (size_t)dt * g.Kc + i;
+        }
+        if (to_slab) slab[idx] = acc[x][y][r];
+        else atomic_add_f(a.dw + idx, acc[x][y][r]);
+      }
+    }
+  }
+}
+
 bool f3_wgrad_glds_ok(const WgradArgs& a) {
   return a.dyb && a.inb && a.zero && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && a.ldy % 8 == 0 && a.g.lda % 8 == 0;
 }
@@ -577,14 +829,14 @@ static int resident_wgs(const void* fn, int threads) {
   return per_cu * cus;
 }
 
-template <int TJ, int TI>
-static int launch_wgrad_glds(WgradArgs a, hipStream_t s) {
+template <int TJ, int TI, int THREADS, void (*KERNEL)(WgradArgs)>
+static int launch_wgrad(WgradArgs a, hipStream_t s) {
   const int gx = (a.g.Nc + TJ - 1) / TJ;
   const int gy = a.g.KT * ((a.g.Kc + TI - 1) / TI);
   // Split-K over rows sized to ONE round of resident workgroups: rounding the split count up
   // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
   // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
-  static const int slots = resident_wgs((const void*)wgrad_glds_bf16<TJ, TI>, 256);
+  static const int slots = resident_wgs((const void*)KERNEL, THREADS);
   const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
   int splits = std::max(1, target / (gx * gy));
   const bool to_slab = a.slab && a.outmap == WG_OUT_CONV;
@@ -602,9 +854,9 @@ static int launch_wgrad_glds(WgradArgs a, hipStream_t s) {
   // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the
   // round-robin 3-D grid
   static const int xcd = getenv("F3_WGRAD_XCD") ? atoi(getenv("F3_WGRAD_XCD")) : 1;
-  a.xcd = xcd;
-  dim3 grid = xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
-  hipLaunchKernelGGL((wgrad_glds_bf16<TJ, TI>), grid, dim3(256), 0, s, a);
+  a.xcd = xcd || THREADS == 512;  // wgrad_big always maps its 1-D grid by XCD
+  dim3 grid = a.xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
+  hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), 0, s, a);
   F3_LAUNCH_CHECK();
   if (to_slab && a.dw_ref) {
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
@@ -618,9 +870,27 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const WgradArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
+  static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
+  const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
+  // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
+  // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
+  // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once
+  // per 256 output channels) wins. F3_WGRAD_BIG=0 restores the first 4-wave kernel (wgrad_glds_bf16).
+  if (big && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0)
+    return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
+  if (big && a.g.Nc % 128 == 0 && a.g.Kc % 256 == 0)
+    return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4>>(a, s);
+  if (big && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0)
+    return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
+  if (big) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
+    if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);
+    if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4>>(a, s);
+    return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2>>(a, s);
+  }
   const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;
-  if (TJ == 128 && TI == 128) return launch_wgrad_glds<128, 128>(a, s);
-  if (TJ == 128) return launch_wgrad_glds<128, 64>(a, s);
-  if (TI == 128) return launch_wgrad_glds<64, 128>(a, s);
-  return launch_wgrad_glds<64, 64>(a, s);
+  if (TJ == 128 && TI == 128) return launch_wgrad<128, 128, 256, wgrad_glds_bf16<128, 128>>(a, s);
+  if (TJ == 128) return launch_wgrad<128, 64, 256, wgrad_glds_bf16<128, 64>>(a, s);
+  if (TI == 128) return launch_wgrad<64, 128, 256, wgrad_glds_bf16<64, 128>>(a, s);
+  return launch_wgrad<64, 64, 256, wgrad_glds_bf16<64, 64>>(a, s);
 }

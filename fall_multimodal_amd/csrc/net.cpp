@@ -236,7 +236,11 @@ struct Arena {
 
 // slab capacity: one round of resident 128x128 weight-gradient tiles (2 per CU x 256 CUs); the
 // launcher caps the split count to it
-constexpr long long kWgradSlabFloats = 512LL * 128 * 128;
+long long wgrad_slab_floats() {  // F3_SLAB_X: capacity multiplier (A/B of split count vs slab traffic)
+  static const long long v = 512LL * 128 * 128 * (getenv("F3_SLAB_X") ? std::max(1, atoi(getenv("F3_SLAB_X"))) : 1);
+  return v;
+}
+#define kWgradSlabFloats wgrad_slab_floats()
 // F3_WGRAD_SLAB=0: fp32 atomics into a packed accumulator instead of slab partials (A/B)
 inline bool wgrad_slab() {
   static const bool on = !getenv("F3_WGRAD_SLAB") || atoi(getenv("F3_WGRAD_SLAB")) != 0;

@@ -19,14 +19,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KERNELS = {"wgrad": "wgrad_glds_bf16<128, 128>", "tcn_fwd": "igemm_big<1, 1, 8>"}
+_WG = "wgrad_big<4, 2, 4, 4, 64>" if os.environ.get("F3_WGRAD_BIG", "1") != "0" else "wgrad_glds_bf16<128, 128>"
+KERNELS = {"wgrad": _WG, "tcn_fwd": "igemm_big<1, 1, 8>"}
 
 
 def run():
     import torch
     import bench
     r = bench.roofline_kernels(torch.device("cuda"), 256, 18, "bf16")
-    print(json.dumps({k: v["kernel"] for k, v in r.items()}))
+    print(json.dumps({k: [v["kernel"], v["ms_per_launch"], v["frac"]] for k, v in r.items()}))
 
 
 def per_launch(db, counter, pattern):
@@ -39,7 +40,7 @@ def per_launch(db, counter, pattern):
 def summarize(d):
     import torch  # noqa: F401  (bench imports torch)
     import bench
-    names = {"wgrad": "wgrad_glds_bf16<128,128> (tcn 9x1 weight gradient, C=256, T=8, N=256, V=18)",
+    names = {"wgrad": KERNELS["wgrad"].replace(", ", ",") + " (tcn 9x1 weight gradient, C=256, T=8, N=256, V=18)",
              "tcn_fwd": "igemm_big<1,1,8> (tcn 9x1 fwd, C=256, T=8, N=256, V=18)"}
     out = {}
     for key, pat in KERNELS.items():
