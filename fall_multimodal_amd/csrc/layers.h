@@ -78,6 +78,7 @@ struct BlockArgs {
   const float* dout_nc;  // [N][C] gradient of the pooled mean (broadcast * inv_tv)
   float* P1;
   float* P2;
+  float* Q2;             // conv residual: [N][C] per-clip sum dz*xhat_r (ca_bwd3 folds P1, Q2 into bnr_bsum/bsq)
   double* bnr_bsum;
   double* bnr_bsq;
   const double* bn2_bsum;
@@ -135,6 +136,9 @@ struct CaArgs {
   // backward
   const float* P1;
   const float* P2;
+  const float* Q2;       // conv residual (else null): per-clip sums for the residual BN backward
+  double* bnr_bsum;
+  double* bnr_bsq;
   float* dq2;
   float* dbn;
   float* dq1;

@@ -562,44 +562,60 @@ F3_DEV f32x4 quad_reduce(f32x4 v, float* lds, int C4) {
   return r;
 }
 
+// The row loops below take U = 4 rows per trip and issue all their loads before any use: at
+// 2-4 workgroups per CU a one-row loop kept ~16 KB in flight per CU and ran the reduction at
+// 2.2 TB/s. Rows past the chunk are clamped to its last row (loads stay in bounds, no branch
+// around a load: hipcc waits vmcnt(0) per element for a conditional load) and masked out of
+// the sums; their stores rewrite the last row with the same values. The residual kind and the
+// pooled-gradient form are template parameters for the same reason.
+constexpr int kRowU = 4;
+
 // out = relu(bn2(h) * a[n,c] + res), res = bn_r(r) | x | 0 ; optional pooled mean
-template <bool A16>
+template <bool A16, int RES>
 __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
-  __shared__ float sc2[256], sh2[256], scr[256], shr[256];
   __shared__ __attribute__((aligned(16))) float lds[1024];
   const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
-  for (int c = tid; c < C; c += 256) {
-    float mu, rs;
-    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
-    if (a.res_kind == RES_CONV) bn_coeff(a.bnr, c, scr[c], shr[c], mu, rs);
-  }
-  __syncthreads();
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  float sc2[4], sh2[4], scr[4], shr[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float mu, rs;
+    bn_coeff(a.bn2, c0 + e, sc2[e], sh2[e], mu, rs);
+    if (RES == RES_CONV) bn_coeff(a.bnr, c0 + e, scr[e], shr[e], mu, rs);
+  }
   const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
   f32x4 pool = {0.f, 0.f, 0.f, 0.f};
-  for (int m = r0 + tid / C4; m < r1; m += RP) {
-    const size_t off = (size_t)m * C + c0;
-    const f32x4 h = ld_act4<A16>(a.h, off);
-    f32x4 res = {0.f, 0.f, 0.f, 0.f};
-    if (a.res_kind == RES_CONV) res = ld_act4<A16>(a.r, off);
-    else if (a.res_kind == RES_ID) res = ld_act4<A16>(a.x, off);
-    f32x4 o;
+  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
+    f32x4 h[kRowU], res[kRowU];
+    size_t off[kRowU];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float rv = res[e];
-      if (a.res_kind == RES_CONV) rv = rv * scr[c0 + e] + shr[c0 + e];
-      o[e] = fmaxf((h[e] * sc2[c0 + e] + sh2[c0 + e]) * av[e] + rv, 0.f);
+    for (int u = 0; u < kRowU; ++u) {
+      off[u] = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
+      h[u] = ld_act4<A16>(a.h, off[u]);
+      if (RES == RES_CONV) res[u] = ld_act4<A16>(a.r, off[u]);
+      else if (RES == RES_ID) res[u] = ld_act4<A16>(a.x, off[u]);
+      else res[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    st_act4<A16>(a.out, off, o);
-    if (a.outb) {
-      bf16x4 ob;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off) = ob;
+    for (int u = 0; u < kRowU; ++u) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float rv = res[u][e];
+        if (RES == RES_CONV) rv = rv * scr[e] + shr[e];
+        o[e] = fmaxf((h[u][e] * sc2[e] + sh2[e]) * av[e] + rv, 0.f);
+      }
+      st_act4<A16>(a.out, off[u], o);
+      if (a.outb) {
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off[u]) = ob;
+      }
+      if (mb + u * RP < r1) pool += o;
     }
-    pool += o;
   }
   if (a.pool) {
     f32x4 r = quad_reduce(pool, lds, C4);
@@ -613,41 +629,50 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
 // backward reductions over a block's output gradient:
 //   dz = dout * (out > 0);  P1[n,c] = sum_tv dz;  P2[n,c] = sum_tv dz*xhat2
 //   conv residual: R[c] += (sum dz, sum dz*xhat_r)
-template <bool A16>
+// DNC: the output gradient is the pooled-mean gradient dout_nc[n][c] broadcast * inv_tv
+template <bool A16, int RES, bool DNC>
 __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
-  __shared__ float mu2[256], rs2[256], mur[256], rsr[256];
   __shared__ __attribute__((aligned(16))) float lds[1024];
   const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
-  for (int c = tid; c < C; c += 256) {
-    float sc, sh;
-    bn_coeff(a.bn2, c, sc, sh, mu2[c], rs2[c]);
-    if (a.res_kind == RES_CONV) bn_coeff(a.bnr, c, sc, sh, mur[c], rsr[c]);
-  }
-  __syncthreads();
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
-  f32x4 p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, q1 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
-  f32x4 dbc = {0, 0, 0, 0};
-  if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
-  for (int m = r0 + tid / C4; m < r1; m += RP) {
-    const size_t off = (size_t)m * C + c0;
-    const f32x4 o = ld_act4<A16>(a.out, off);
-    const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
-    const f32x4 h = ld_act4<A16>(a.h, off);
-    f32x4 rr = {0, 0, 0, 0};
-    if (a.res_kind == RES_CONV) rr = ld_act4<A16>(a.r, off);
+  float mu2[4], rs2[4], mur[4], rsr[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float dz = o[e] > 0.f ? d[e] : 0.f;
-      p1[e] += dz;
-      p2[e] += dz * ((h[e] - mu2[c0 + e]) * rs2[c0 + e]);
-      if (a.res_kind == RES_CONV) {
-        q1[e] += dz;
-        q2[e] += dz * ((rr[e] - mur[c0 + e]) * rsr[c0 + e]);
+  for (int e = 0; e < 4; ++e) {
+    float sc, sh;
+    bn_coeff(a.bn2, c0 + e, sc, sh, mu2[e], rs2[e]);
+    if (RES == RES_CONV) bn_coeff(a.bnr, c0 + e, sc, sh, mur[e], rsr[e]);
+  }
+  f32x4 p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
+  f32x4 dbc = {0, 0, 0, 0};
+  if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
+  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
+    f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const size_t off = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
+      o[u] = ld_act4<A16>(a.out, off);
+      d[u] = DNC ? dbc : *reinterpret_cast<const f32x4*>(a.dout + off);
+      h[u] = ld_act4<A16>(a.h, off);
+      if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off);
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const float w = mb + u * RP < r1 ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dz = o[u][e] > 0.f ? d[u][e] * w : 0.f;
+        p1[e] += dz;
+        p2[e] += dz * ((h[u][e] - mu2[e]) * rs2[e]);
+        if (RES == RES_CONV) q2[e] += dz * ((rr[u][e] - mur[e]) * rsr[e]);
       }
     }
   }
+  // per-clip partial sums (a clip's chunks add into one row: <= chunks-way float atomics). The
+  // residual BN's channel sums over all clips (sum dz = sum_n P1, sum dz*xhat_r = sum_n Q2) are
+  // folded in by ca_bwd3, which walks the clips anyway: double atomics from every chunk of every
+  // clip onto the same C addresses made the conv-residual form of this kernel 100 us.
   f32x4 s1 = quad_reduce(p1, lds, C4);
   if (tid < C4) {
 #pragma unroll
@@ -658,48 +683,25 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) atomic_add_f(a.P2 + (size_t)n * C + tid * 4 + e, s2[e]);
   }
-  if (a.res_kind == RES_CONV) {
-    f32x4 t1 = quad_reduce(q1, lds, C4);
-    if (tid < C4) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomic_add_d(a.bnr_bsum + tid * 4 + e, (double)t1[e]);
-    }
+  if (RES == RES_CONV) {
     f32x4 t2 = quad_reduce(q2, lds, C4);
     if (tid < C4) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomic_add_d(a.bnr_bsq + tid * 4 + e, (double)t2[e]);
+      for (int e = 0; e < 4; ++e) atomic_add_f(a.Q2 + (size_t)n * C + tid * 4 + e, t2[e]);
     }
   }
 }
 
 // dh = g2*rs2*(dz*a + e - D1/M - xhat2*D2/M);  residual: dr (conv) or dx = dz (identity)
-template <bool A16>
+template <bool A16, int RES, bool DNC>
 __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
-  __shared__ float mu2[256], k2[256], m1[256], m2[256], rs2[256];
-  __shared__ float mur[256], kr[256], n1[256], n2[256], rsr[256];
   const int C = a.C, C4 = C / 4, RP = 256 / C4, tid = threadIdx.x;
   const float invM = 1.f / (float)a.bn2.count;
-  for (int c = tid; c < C; c += 256) {
-    float sc, sh, rs;
-    bn_coeff(a.bn2, c, sc, sh, mu2[c], rs);
-    rs2[c] = rs;
-    k2[c] = a.bn2.gamma[c] * rs;
-    m1[c] = (float)a.bn2_bsum[c] * invM;
-    m2[c] = (float)a.bn2_bsq[c] * invM;
-    if (a.res_kind == RES_CONV) {
-      bn_coeff(a.bnr, c, sc, sh, mur[c], rs);
-      rsr[c] = rs;
-      kr[c] = a.bnr.gamma[c] * rs;
-      n1[c] = (float)a.bnr_bsum[c] * invM;
-      n2[c] = (float)a.bnr_bsq[c] * invM;
-    }
-  }
-  __syncthreads();
   if (blockIdx.x == 0 && blockIdx.y == 0) {
     for (int c = tid; c < C; c += 256) {
       a.dgamma2[c] += (float)a.bn2_bsq[c];
       a.dbeta2[c] += (float)a.bn2_bsum[c];
-      if (a.res_kind == RES_CONV) {
+      if (RES == RES_CONV) {
         a.dgammar[c] += (float)a.bnr_bsq[c];
         a.dbetar[c] += (float)a.bnr_bsum[c];
       }
@@ -708,46 +710,68 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  float mu2[4], k2[4], m1[4], m2[4], rs2[4], mur[4], kr[4], n1[4], n2[4], rsr[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + e;
+    float sc, sh;
+    bn_coeff(a.bn2, c, sc, sh, mu2[e], rs2[e]);
+    k2[e] = a.bn2.gamma[c] * rs2[e];
+    m1[e] = (float)a.bn2_bsum[c] * invM;
+    m2[e] = (float)a.bn2_bsq[c] * invM;
+    if (RES == RES_CONV) {
+      bn_coeff(a.bnr, c, sc, sh, mur[e], rsr[e]);
+      kr[e] = a.bnr.gamma[c] * rsr[e];
+      n1[e] = (float)a.bnr_bsum[c] * invM;
+      n2[e] = (float)a.bnr_bsq[c] * invM;
+    }
+  }
   const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
   const f32x4 ev = *reinterpret_cast<const f32x4*>(a.e + (size_t)n * C + c0);
   f32x4 dbc = {0, 0, 0, 0};
-  if (a.dout_nc) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0);
-  for (int m = r0 + tid / C4; m < r1; m += RP) {
-    const size_t off = (size_t)m * C + c0;
-    const f32x4 o = ld_act4<A16>(a.out, off);
-    const f32x4 d = a.dout_nc ? dbc * a.inv_tv : *reinterpret_cast<const f32x4*>(a.dout + off);
-    const f32x4 h = ld_act4<A16>(a.h, off);
-    f32x4 dh, dr;
-    f32x4 rr = {0, 0, 0, 0};
-    if (a.res_kind == RES_CONV) rr = ld_act4<A16>(a.r, off);
+  if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
+  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
+    f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
+    size_t off[kRowU];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = c0 + e;
-      const float dz = o[e] > 0.f ? d[e] : 0.f;
-      const float xh = (h[e] - mu2[c]) * rs2[c];
-      dh[e] = k2[c] * (dz * av[e] + ev[e] - m1[c] - xh * m2[c]);
-      if (a.res_kind == RES_CONV) {
-        const float xr = (rr[e] - mur[c]) * rsr[c];
-        dr[e] = kr[c] * (dz - n1[c] - xr * n2[c]);
-      } else {
-        dr[e] = dz;
+    for (int u = 0; u < kRowU; ++u) {
+      off[u] = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
+      o[u] = ld_act4<A16>(a.out, off[u]);
+      d[u] = DNC ? dbc : *reinterpret_cast<const f32x4*>(a.dout + off[u]);
+      h[u] = ld_act4<A16>(a.h, off[u]);
+      if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      f32x4 dh, dr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dz = o[u][e] > 0.f ? d[u][e] : 0.f;
+        const float xh = (h[u][e] - mu2[e]) * rs2[e];
+        dh[e] = k2[e] * (dz * av[e] + ev[e] - m1[e] - xh * m2[e]);
+        if (RES == RES_CONV) {
+          const float xr = (rr[u][e] - mur[e]) * rsr[e];
+          dr[e] = kr[e] * (dz - n1[e] - xr * n2[e]);
+        } else {
+          dr[e] = dz;
+        }
       }
-    }
-    if (a.dhb) {
-      bf16x4 hb;
+      if (a.dhb) {
+        bf16x4 hb;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hb[e] = (__bf16)dh[e];
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off) = hb;
-    } else {
-      *reinterpret_cast<f32x4*>(a.dh + off) = dh;
-    }
-    if (a.res_kind == RES_CONV && a.dresb) {
-      bf16x4 rb;
+        for (int e = 0; e < 4; ++e) hb[e] = (__bf16)dh[e];
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off[u]) = hb;
+      } else {
+        *reinterpret_cast<f32x4*>(a.dh + off[u]) = dh;
+      }
+      if (RES == RES_CONV && a.dresb) {
+        bf16x4 rb;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) rb[e] = (__bf16)dr[e];
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off) = rb;
-    } else if (a.res_kind != RES_NONE) {
-      *reinterpret_cast<f32x4*>(a.dres + off) = dr;
+        for (int e = 0; e < 4; ++e) rb[e] = (__bf16)dr[e];
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off[u]) = rb;
+      } else if (RES != RES_NONE) {
+        *reinterpret_cast<f32x4*>(a.dres + off[u]) = dr;
+      }
     }
   }
 }
@@ -785,18 +809,33 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-  for (int t = t0; t < t1; ++t) {
+  // all frames' loads first (clamped to the last frame, masked out of the sums; see kRowU)
+  f32x4 d0[kBnBwdFrames], d1[kBnBwdFrames], g0[kBnBwdFrames], g1[kBnBwdFrames];
+#pragma unroll
+  for (int u = 0; u < kBnBwdFrames; ++u) {
+    const size_t off = ((size_t)(n * T + min(t0 + u, t1 - 1)) * V + v) * C + c0;
+    d0[u] = ld_act4<A16>(a.dv, off);
+    d1[u] = ld_act4<A16>(a.dv, off + 4);
+    g0[u] = ld_act4<A16>(a.g, off);
+    g1[u] = ld_act4<A16>(a.g, off + 4);
+  }
+  float ck[8], cm1[8], cm2[8], cmu[8], crs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ck[e] = kk[c0 + e]; cm1[e] = m1[c0 + e]; cm2[e] = m2[c0 + e]; cmu[e] = mu[c0 + e]; crs[e] = rsv[c0 + e];
+  }
+#pragma unroll
+  for (int u = 0; u < kBnBwdFrames; ++u) {
+    const int t = min(t0 + u, t1 - 1);
     const size_t off = ((size_t)(n * T + t) * V + v) * C + c0;
-    const f32x4 d0 = ld_act4<A16>(a.dv, off), d1 = ld_act4<A16>(a.dv, off + 4);
-    const f32x4 g0 = ld_act4<A16>(a.g, off), g1 = ld_act4<A16>(a.g, off + 4);
+    const bool live = t0 + u < t1;
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      const float dv = e < 4 ? d0[e] : d1[e - 4];
-      const float gv = e < 4 ? g0[e] : g1[e - 4];
-      o[e] = kk[c] * (dv - m1[c] - (gv - mu[c]) * rsv[c] * m2[c]);
-      acc[e] += o[e];
+      const float dv = e < 4 ? d0[u][e] : d1[u][e - 4];
+      const float gv = e < 4 ? g0[u][e] : g1[u][e - 4];
+      o[e] = ck[e] * (dv - cm1[e] - (gv - cmu[e]) * crs[e] * cm2[e]);
+      if (live) acc[e] += o[e];
     }
     if (a.dgb) {
       bf16x8 ob;
@@ -1073,6 +1112,10 @@ __global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
     const float xsum = (a.gapsum[o] - mu / a.inv_tv) * rs;  // sum_tv xhat2
     atomic_add_d(a.bn2_bsum + c, (double)(at * a.P1[o] + dg));
     atomic_add_d(a.bn2_bsq + c, (double)(at * a.P2[o] + dg * a.inv_tv * xsum));
+    if (a.bnr_bsum) {  // conv residual BN: channel sums of dz and dz*xhat_r over the clips
+      atomic_add_d(a.bnr_bsum + c, (double)a.P1[o]);
+      atomic_add_d(a.bnr_bsq + c, (double)a.Q2[o]);
+    }
   }
 }
 
@@ -1239,11 +1282,47 @@ int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
 
 static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
 
+// backward block kernels: instantiate on (activation type, residual kind, pooled gradient)
+template <bool A16, int RES, bool DNC>
+static void launch_block_bwd1(const BlockArgs& a, bool reduce, hipStream_t s) {
+  const dim3 grid(a.chunks, a.N);
+  if (reduce) hipLaunchKernelGGL((block_bwd_reduce_kernel<A16, RES, DNC>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((block_bwd_apply_kernel<A16, RES, DNC>), grid, dim3(256), 0, s, a);
+}
+template <bool A16, int RES>
+static void launch_block_bwd2(const BlockArgs& a, bool reduce, hipStream_t s) {
+  if (a.dout_nc) launch_block_bwd1<A16, RES, true>(a, reduce, s);
+  else launch_block_bwd1<A16, RES, false>(a, reduce, s);
+}
+template <bool REDUCE>
+static void launch_block_bwd(const BlockArgs& a, hipStream_t s) {
+  if (a.act16) {
+    if (a.res_kind == RES_CONV) launch_block_bwd2<true, RES_CONV>(a, REDUCE, s);
+    else if (a.res_kind == RES_ID) launch_block_bwd2<true, RES_ID>(a, REDUCE, s);
+    else launch_block_bwd2<true, RES_NONE>(a, REDUCE, s);
+  } else {
+    if (a.res_kind == RES_CONV) launch_block_bwd2<false, RES_CONV>(a, REDUCE, s);
+    else if (a.res_kind == RES_ID) launch_block_bwd2<false, RES_ID>(a, REDUCE, s);
+    else launch_block_bwd2<false, RES_NONE>(a, REDUCE, s);
+  }
+}
+
 int f3_block_out(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  if (a.act16) hipLaunchKernelGGL(block_out_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(block_out_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  const dim3 grid(a.chunks, a.N);
+#define F3_BO(A, R) hipLaunchKernelGGL((block_out_kernel<A, R>), grid, dim3(256), 0, s, a)
+  if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
+  if (a.act16) {
+    if (a.res_kind == RES_CONV) F3_BO(true, RES_CONV);
+    else if (a.res_kind == RES_ID) F3_BO(true, RES_ID);
+    else F3_BO(true, RES_NONE);
+  } else {
+    if (a.res_kind == RES_CONV) F3_BO(false, RES_CONV);
+    else if (a.res_kind == RES_ID) F3_BO(false, RES_ID);
+    else F3_BO(false, RES_NONE);
+  }
+#undef F3_BO
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1251,8 +1330,8 @@ int f3_block_out(BlockArgs a, hipStream_t s) {
 int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  if (a.act16) hipLaunchKernelGGL(block_bwd_reduce_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(block_bwd_reduce_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
+  launch_block_bwd<true>(a, s);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1260,8 +1339,8 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
 int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
-  if (a.act16) hipLaunchKernelGGL(block_bwd_apply_kernel<true>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(block_bwd_apply_kernel<false>, dim3(a.chunks, a.N), dim3(256), 0, s, a);
+  if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
+  launch_block_bwd<false>(a, s);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

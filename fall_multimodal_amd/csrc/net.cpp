@@ -256,7 +256,7 @@ struct LayerWs {
   float *z, *g, *h, *r = nullptr, *out, *q1, *hid, *att, *gap;
   float *gw, *gwT, *tw, *twT, *rw = nullptr, *rwT = nullptr, *aeff, *beff;
   BnWs bn1, bn2, bnr, bnca;
-  float *P1, *P2, *G, *dAeff, *dq2, *dbn, *dq1, *e;
+  float *P1, *P2, *Q2, *G, *dAeff, *dq2, *dbn, *dq1, *e;
   // bf16 mode: u = relu(bn1(g)) (tcn GEMM operand, saved for its wgrad), a bf16 copy of the
   // block output when the next block has a residual conv, the packed tcn weight gradient
   unsigned short *u = nullptr, *outb = nullptr;
@@ -350,6 +350,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       if (L.res == RES_CONV) bn_take_b(A, X.bnr, L.cout);
       X.P1 = A.take<float>((size_t)N * L.cout);
       X.P2 = A.take<float>((size_t)N * L.cout);
+      X.Q2 = L.res == RES_CONV ? A.take<float>((size_t)N * L.cout) : nullptr;
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
       if (hb && !wgrad_slab()) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);  // atomic accumulator
@@ -686,7 +687,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.dout = dout; ba.dout_nc = l == 6 ? W.dpool : nullptr; ba.act16 = hb;
-    ba.P1 = X.P1; ba.P2 = X.P2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
+    ba.P1 = X.P1; ba.P2 = X.P2; ba.Q2 = X.Q2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
     ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = dh;
     ba.dres = L.res == RES_CONV ? dres : (L.res == RES_ID ? dx : nullptr);
     ba.dhb = bfa(dh, hb);
@@ -701,6 +702,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.W1 = q.p(L.ca_w1); ca.b1 = q.p(L.ca_b1); ca.W2 = q.p(L.ca_w2); ca.b2 = q.p(L.ca_b2);
     ca.gapsum = X.gap; ca.q1 = X.q1; ca.hid = X.hid; ca.att = X.att; ca.ca_sum = X.bnca.fsum; ca.ca_sq = X.bnca.fsq;
     ca.P1 = X.P1; ca.P2 = X.P2; ca.dq2 = X.dq2; ca.dbn = X.dbn; ca.dq1 = X.dq1; ca.e = X.e;
+    ca.Q2 = X.Q2; ca.bnr_bsum = L.res == RES_CONV ? X.bnr.bsum : nullptr; ca.bnr_bsq = L.res == RES_CONV ? X.bnr.bsq : nullptr;
     ca.bn2_bsum = X.bn2.bsum; ca.bn2_bsq = X.bn2.bsq;
     ca.g_bnca_gamma = q.g(L.bnca.w); ca.g_bnca_beta = q.g(L.bnca.b);
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
