@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   float* epi_mu = epi_sh + BN;
   float* epi_rs = epi_mu + BN;
 
+  static_assert(!((EPI & EPI_ADD) && (EPI & (EPI_RELUMASK | EPI_BIASV))), "one preloaded epilogue operand");
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (g.Nc + BN - 1) / BN;
@@ -198,22 +199,47 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
   const int TV = g.T_out * g.V;
   const int nlo = m0 / TV;
+  // Per 16-row group x, every operand the epilogue reads (RELUMASK source, graph-mixed bias, the
+  // accumulated output) is loaded for the group's 4 rows x WN columns before any use, from
+  // clamped in-bounds addresses (see igemm_big: a conditional per-element load costs a
+  // vmcnt(0) round trip each).
+  const bool aux16 = a.auxb != nullptr;
 #pragma unroll
-  for (int y = 0; y < WN; ++y) {
-    const int jl = wj * 16 * WN + y * 16 + fr;
-    const int j = j0 + jl;
-    const bool jok = j < g.Nc;
+  for (int x = 0; x < 4; ++x) {
+    int mrow[4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int r = 0; r < 4; ++r) mrow[r] = phys(m0 + wm * 64 + x * 16 + fg * 4 + r);
+    float pre[4][WN];
+    auto preload = [&](auto load) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = phys(m0 + wm * 64 + x * 16 + fg * 4 + r);
+        const int mc = max(mrow[r], 0);
+#pragma unroll
+        for (int y = 0; y < WN; ++y) pre[r][y] = load(mc, min(j0 + wj * 16 * WN + y * 16 + fr, g.Nc - 1));
+      }
+    };
+    if (EPI & EPI_RELUMASK) {
+      if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
+      else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
+    } else if (EPI & EPI_BIASV) {
+      preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
+    } else if (EPI & EPI_ADD) {
+      preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
+    }
+#pragma unroll
+    for (int y = 0; y < WN; ++y) {
+      const int jl = wj * 16 * WN + y * 16 + fr;
+      const int j = j0 + jl;
+      const bool jok = j < g.Nc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mrow[r];
         if (!jok || m < 0) continue;
         float v = acc[x][y][r];
         if (EPI & EPI_BIAS) v += a.bias[j];
-        if (EPI & EPI_BIASV) v += a.bias[(m % g.V) * g.Nc + j];
+        if (EPI & EPI_BIASV) v += pre[r][y];
         if (EPI & EPI_RELUMASK) {
-          const float gv = a.auxb ? bf2f(a.auxb[(size_t)m * a.ldaux + j]) : a.aux[(size_t)m * a.ldaux + j];
+          const float gv = pre[r][y];
           if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
           const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
           ssum[y] += v;
@@ -233,7 +259,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
           else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
-          if (EPI & EPI_ADD) *o += v;
+          if (EPI & EPI_ADD) *o = pre[r][y] + v;
           else *o = v;
         }
       }
