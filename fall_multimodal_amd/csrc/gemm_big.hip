@@ -195,28 +195,35 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   // parity class, column past Nc, or the fp32/bf16 select) made hipcc wait vmcnt(0) on every
   // element: 72 dependent round trips per lane in the RELUMASK epilogue.
   const bool aux16 = a.auxb != nullptr;
+  float biasj[BG_NT];  // EPI_BIAS: one value per column, loaded once
+#pragma unroll
+  for (int y = 0; y < BG_NT; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(wn * 32 + y * 16 + fr, g.Nc - 1)] : 0.f;
+  // all groups' operands first: a load issued after the group's stores would make its first
+  // use wait (vmcnt counts stores too) for every store before it
+  float pre[BG_MT][4][BG_NT];
+  auto preload = [&](auto load) {
+#pragma unroll
+    for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mc = max(phys(m0 + wm * 144 + x * 16 + fg * 4 + r), 0);
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(wn * 32 + y * 16 + fr, g.Nc - 1));
+      }
+  };
+  if (EPI & EPI_RELUMASK) {
+    if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
+    else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
+  } else if (EPI & EPI_BIASV) {
+    preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
+  } else if (EPI & EPI_ADD) {
+    preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
+  }
 #pragma unroll
   for (int x = 0; x < BG_MT; ++x) {
     int mrow[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) mrow[r] = phys(m0 + wm * 144 + x * 16 + fg * 4 + r);
-    float pre[4][BG_NT];
-    auto preload = [&](auto load) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mc = max(mrow[r], 0);
-#pragma unroll
-        for (int y = 0; y < BG_NT; ++y) pre[r][y] = load(mc, min(wn * 32 + y * 16 + fr, g.Nc - 1));
-      }
-    };
-    if (EPI & EPI_RELUMASK) {
-      if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
-      else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
-    } else if (EPI & EPI_BIASV) {
-      preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
-    } else if (EPI & EPI_ADD) {
-      preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
-    }
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) {
       const int j = wn * 32 + y * 16 + fr;
@@ -226,10 +233,10 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         const int m = mrow[r];
         if (!jok || m < 0) continue;
         float v = acc[x][y][r];
-        if (EPI & EPI_BIAS) v += a.bias[j];
-        if (EPI & EPI_BIASV) v += pre[r][y];
+        if (EPI & EPI_BIAS) v += biasj[y];
+        if (EPI & EPI_BIASV) v += pre[x][r][y];
         if (EPI & EPI_RELUMASK) {
-          const float gv = pre[r][y];
+          const float gv = pre[x][r][y];
           if (gv * epi_sc[j] + epi_sh[j] <= 0.f) v = 0.f;
           const float xh = (gv - epi_mu[j]) * epi_rs[j];
           ssum[y] += v;
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
           else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
-          if (EPI & EPI_ADD) *o = pre[r][y] + v;
+          if (EPI & EPI_ADD) *o = pre[x][r][y] + v;
           else *o = v;
         }
       }

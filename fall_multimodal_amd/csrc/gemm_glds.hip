@@ -204,28 +204,35 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   // clamped in-bounds addresses (see igemm_big: a conditional per-element load costs a
   // vmcnt(0) round trip each).
   const bool aux16 = a.auxb != nullptr;
+  float biasj[WN];  // EPI_BIAS: one value per column, loaded once
+#pragma unroll
+  for (int y = 0; y < WN; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(j0 + wj * 16 * WN + y * 16 + fr, g.Nc - 1)] : 0.f;
+  // all groups' operands first: a load issued after the group's stores would make its first
+  // use wait (vmcnt counts stores too) for every store before it
+  float pre[4][4][WN];
+  auto preload = [&](auto load) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mc = max(phys(m0 + wm * 64 + x * 16 + fg * 4 + r), 0);
+#pragma unroll
+        for (int y = 0; y < WN; ++y) pre[x][r][y] = load(mc, min(j0 + wj * 16 * WN + y * 16 + fr, g.Nc - 1));
+      }
+  };
+  if (EPI & EPI_RELUMASK) {
+    if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
+    else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
+  } else if (EPI & EPI_BIASV) {
+    preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
+  } else if (EPI & EPI_ADD) {
+    preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
+  }
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     int mrow[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) mrow[r] = phys(m0 + wm * 64 + x * 16 + fg * 4 + r);
-    float pre[4][WN];
-    auto preload = [&](auto load) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mc = max(mrow[r], 0);
-#pragma unroll
-        for (int y = 0; y < WN; ++y) pre[r][y] = load(mc, min(j0 + wj * 16 * WN + y * 16 + fr, g.Nc - 1));
-      }
-    };
-    if (EPI & EPI_RELUMASK) {
-      if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
-      else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
-    } else if (EPI & EPI_BIASV) {
-      preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
-    } else if (EPI & EPI_ADD) {
-      preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
-    }
 #pragma unroll
     for (int y = 0; y < WN; ++y) {
       const int jl = wj * 16 * WN + y * 16 + fr;
@@ -236,10 +243,10 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
         const int m = mrow[r];
         if (!jok || m < 0) continue;
         float v = acc[x][y][r];
-        if (EPI & EPI_BIAS) v += a.bias[j];
-        if (EPI & EPI_BIASV) v += pre[r][y];
+        if (EPI & EPI_BIAS) v += biasj[y];
+        if (EPI & EPI_BIASV) v += pre[x][r][y];
         if (EPI & EPI_RELUMASK) {
-          const float gv = pre[r][y];
+          const float gv = pre[x][r][y];
           if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
           const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
           ssum[y] += v;
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
           else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
-          if (EPI & EPI_ADD) *o = pre[r][y] + v;
+          if (EPI & EPI_ADD) *o = pre[x][r][y] + v;
           else *o = v;
         }
       }
