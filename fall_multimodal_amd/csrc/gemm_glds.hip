@@ -24,16 +24,29 @@ namespace f3 {
 
 constexpr int G_BM = 128;
 
-template <int EPI, int WN, int NST>
+// WIN (stride-1 temporal convs, forward or input gradient): the 9 taps of a row tile read the
+// same input rows shifted by whole frames, so instead of staging a 128-row A tile per (tap,
+// 64-channel chunk) the tile's input WINDOW — its rows plus P frames either side — is staged
+// once per chunk and each tap reads its fragments at a row offset of dt*V. Rows whose shifted
+// frame leaves the clip (temporal zero padding) are zeroed in the fragment, per lane and tap.
+// A staging traffic drops from 9 x 128 to (128 + 2PV) rows per chunk (the 64-channel layers
+// staged 2x more A than B bytes).
+constexpr int G_WIN_ROWS = 128 + 2 * 4 * 18;  // window capacity: P <= 4, V <= 18 (3 workgroups per CU)
+
+template <int EPI, int WN, int NST, bool WIN = false>
 __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   constexpr int BM = G_BM, BN = 32 * WN;
-  constexpr int A_BYTES = BM * G_BK * 2, B_BYTES = BN * G_BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = WIN ? 0 : BM * G_BK * 2, B_BYTES = BN * G_BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = A_BYTES / 1024 / 4, B_INSTR = B_BYTES / 1024 / 4;  // per wave
   constexpr int NPS = A_INSTR + B_INSTR;  // LDS-DMA instructions per wave per stage
+  constexpr int WIN_OFF = NST * STAGE, WIN_BYTES = WIN ? G_WIN_ROWS * 128 : 0;
+  constexpr int SMEM_MAIN = WIN_OFF + WIN_BYTES > 16 * 1024 + BM * (BN + 8) * 2 ? WIN_OFF + WIN_BYTES
+                                                                                 : 16 * 1024 + BM * (BN + 8) * 2;
+  static_assert(!WIN || NST == 2, "window mode uses the 2-stage loop");
   // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code): NST
-  // stages, then the epilogue coefficient tables; the reductions reuse stage 0.
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + 4 * BN * 4];
-  float* epi_sc = reinterpret_cast<float*>(smem + NST * STAGE);
+  // stages (and the window), then the epilogue coefficient tables; the reductions reuse stage 0.
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN + 4 * BN * 4];
+  float* epi_sc = reinterpret_cast<float*>(smem + SMEM_MAIN);
   float* epi_sh = epi_sc + BN;
   float* epi_mu = epi_sh + BN;
   float* epi_rs = epi_mu + BN;
@@ -66,6 +79,10 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   const int kpt = g.Kc / G_BK;                    // k chunks per tap
   const int dt0 = par ? ((p + g.P) & 1) : 0;      // first tap of this parity
   const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
+  // window mode: stage t = (chunk t / KT, tap t % KT); window row of tile row r for tap dt:
+  // r + wofs(dt) with wofs = dt*V (forward) or (2P - dt)*V (input gradient)
+  const int PV = g.P * g.V, WR = BM + 2 * PV;
+  auto wofs = [&](int dt) { return (g.transposed ? 2 * g.P - dt : dt) * g.V; };
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
 
@@ -81,8 +98,8 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 
   // per-lane staging rows (fixed for the whole k loop)
   const int sub = lane >> 3, pch = lane & 7;
-  RowMap a_map[A_INSTR];
-  int a_c[A_INSTR];
+  RowMap a_map[A_INSTR > 0 ? A_INSTR : 1];
+  int a_c[A_INSTR > 0 ? A_INSTR : 1];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int rr = (wave * A_INSTR + i) * 8 + sub;
@@ -100,7 +117,8 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   (void)b_step;
 
   auto stage = [&](int t, int buf) {
-    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    if (WIN) { tap = t % g.KT; i0 = (t / g.KT) * G_BK; }
     const int dt = par ? dt0 + 2 * tap : tap;
     const int k0 = dt * g.Kc + i0;
     char* sa = smem + buf * STAGE;
@@ -118,8 +136,22 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     }
   };
 
+  // window staging: 1-KiB pieces of 8 rows, dealt round-robin to the 4 waves (waited with vmcnt(0))
+  auto load_win = [&](int chunk) {
+    const int i0 = chunk * G_BK, nwp = (WR + 7) >> 3;
+    for (int q = wave; q < nwp; q += 4) {
+      const int rr = q * 8 + sub, gm = m0 - PV + rr;
+      const bool ok = rr < WR && gm >= 0 && gm < g.M;
+      const unsigned short* src = ok ? in + (size_t)gm * g.lda + i0 + swz(rr, pch) * 8 : a.zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(smem + WIN_OFF + q * 1024), 16, 0, 0);
+    }
+  };
+
   const int wm = wave >> 1, wj = wave & 1;
   const int fr = lane & 15, fg = lane >> 4;
+  int tfr[4];  // window mode: frame of each of the lane's 4 A rows (the row's clip-relative t)
+#pragma unroll
+  for (int x = 0; x < 4; ++x) tfr[x] = WIN ? ((m0 + wm * 64 + x * 16 + fr) / g.V) % g.T_out : 0;
   f32x4 acc[4][WN];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -132,6 +164,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     if (EPI & EPI_ADD) return;
     __syncthreads();  // epilogue coefficient tables
   } else if (NST == 2) {
+    if (WIN) load_win(0);
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -147,6 +180,14 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   }
   for (int t = 0; t < nchunk; ++t) {
     const int buf = NST == 2 ? (t & 1) : (t % 3);
+    if (WIN && t > 0 && t % g.KT == 0) {  // next 64-channel chunk: restage the window
+      load_win(t / g.KT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    const int wdt = WIN ? t % g.KT : 0;
+    const int wo = WIN ? wofs(wdt) : 0;
+    const int wsh = WIN ? (g.transposed ? g.P - wdt : wdt - g.P) : 0;
     if (NST == 2) {
       if (t + 1 < nchunk) stage(t + 1, buf ^ 1);
     } else {
@@ -160,8 +201,15 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
       const int c = ks * 4 + fg;
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        const int r = wm * 64 + x * 16 + fr;
-        fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+        if (WIN) {
+          const int r = wm * 64 + x * 16 + fr + wo;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + WIN_OFF + r * 128 + swz(r, c) * 16);
+          const bool ok = (unsigned)(tfr[x] + wsh) < (unsigned)g.T_out;
+          fa[x] = ok ? v : bf16x8{};
+        } else {
+          const int r = wm * 64 + x * 16 + fr;
+          fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+        }
       }
 #pragma unroll
       for (int y = 0; y < WN; ++y) {
@@ -330,6 +378,20 @@ bool f3_igemm_ok(const ConvGemmArgs& a) {
   return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0;
 }
 
+// Window mode (see igemm_bf16): stride-1 temporal convs with "same" padding whose output
+// channels fit one column tile (64 or 128) and whose window fits the LDS reserve.
+// F3_IGEMM_WIN=0 turns it off.
+static bool igemm_win_ok(const ConvGemmArgs& a, int epi) {
+  static const int on = getenv("F3_IGEMM_WIN") ? atoi(getenv("F3_IGEMM_WIN")) : 1;
+  const ConvGeom& g = a.g;
+  if (!on || g.S != 1 || g.KT < 2 || 2 * g.P != g.KT - 1 || g.T_in != g.T_out) return false;
+  // 128 channels: only the input gradient (77 vs 87-111 us for igemm_big at layer 4; the
+  // forward measured 77 vs 58 us)
+  if (g.Nc != 64 && !(g.Nc == 128 && epi == EPI_RELUMASK)) return false;
+  if (G_BM + 2 * g.P * g.V > G_WIN_ROWS || g.M % (g.T_out * g.V) != 0) return false;
+  return epi == (EPI_BIAS | EPI_STATS | EPI_GAP) || epi == EPI_RELUMASK || epi == EPI_BIAS;
+}
+
 static int igemm_stages() {
   static const int v = [] {
     const char* e = getenv("F3_IGEMM_STAGES");
@@ -338,7 +400,7 @@ static int igemm_stages() {
   return v;
 }
 
-template <int WN, int NST>
+template <int WN, int NST, bool WIN = false>
 static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
   const int ntn = (a.g.Nc + 32 * WN - 1) / (32 * WN);
   int tiles = ((a.g.M + G_BM - 1) / G_BM) * ntn;
@@ -350,7 +412,7 @@ static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
   }
 #define F3_ICASE(E)                                                                   \
   if (epi == (E)) {                                                                  \
-    hipLaunchKernelGGL((igemm_bf16<(E), WN, NST>), dim3(tiles), dim3(256), 0, s, a); \
+    hipLaunchKernelGGL((igemm_bf16<(E), WN, NST, WIN>), dim3(tiles), dim3(256), 0, s, a); \
     F3_LAUNCH_CHECK();                                                                \
     return F3_OK;                                                                     \
   }
@@ -369,6 +431,10 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
+  if (igemm_win_ok(a, epi)) {
+    if (a.g.Nc == 128) return launch_igemm<4, 2, true>(a, epi, s);
+    return launch_igemm<2, 2, true>(a, epi, s);
+  }
   if (f3_igemm_big_ok(a)) return f3_igemm_big(args, epi, s);
   if (igemm_stages() == 3) {
     if (a.g.Nc > 64) return launch_igemm<4, 3>(a, epi, s);

@@ -68,7 +68,8 @@ def test_conv_kernel_matches_torch(precision):
     torch.manual_seed(0)
     for (N, T, V, Ci, Co, KT, s, p) in [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4),
                                          (2, 15, 14, 128, 256, 1, 2, 0), (2, 30, 14, 9, 64, 1, 1, 0),
-                                         (4, 8, 18, 256, 256, 9, 1, 4)]:
+                                         (4, 8, 18, 256, 256, 9, 1, 4), (2, 15, 18, 256, 128, 9, 1, 4),
+                                         (3, 8, 25, 64, 64, 9, 1, 4)]:
         x = torch.randn(N, Ci, T, V)
         w = torch.randn(Co, Ci, KT, 1) / np.sqrt(Ci * KT)
         b = torch.randn(Co)
@@ -89,7 +90,7 @@ def test_conv_kernel_matches_torch(precision):
 CONV_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
                (4, 29, 14, 128, 128, 9, 2, 4), (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4),
                (2, 30, 14, 9, 64, 1, 1, 0), (2, 30, 18, 64, 192, 1, 1, 0), (3, 30, 18, 192, 64, 1, 1, 0),
-               (2, 15, 14, 256, 128, 9, 1, 4)]
+               (2, 15, 14, 256, 128, 9, 1, 4), (2, 15, 18, 128, 128, 9, 1, 4)]
 
 
 @pytest.mark.parametrize("precision", PRECISIONS, ids=PREC_IDS)
