@@ -283,14 +283,14 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {  // regis
   const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
   f32x4 rx[XB ? 1 : kMixPX];
   u32x2 rxb[XB ? kMixPX : 1];  // raw bf16 pieces (converted when written to LDS)
+  // prefetch: unconditional loads from clamped indices (a conditional load is waited for on
+  // the spot — vmcnt(0) per element — which serialised the prefetch meant to overlap the frame)
   auto prefetch = [&](int f) {
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
-      const int i = tid + q * 256;
-      if (i < n4) {
-        if constexpr (XB) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
-        else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
-      }
+      const int i = min(tid + q * 256, n4 - 1);
+      if constexpr (XB) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
+      else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
     }
   };
   if (blockIdx.x < a.frames) prefetch(blockIdx.x);
@@ -349,8 +349,8 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {  // regis
   }
 }
 
-template <int KS, int CIN, bool ZB16>  // k steps over (w,k): ceil(K*V/4); ZB16: dZ is bf16
-__global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
+template <int KS, int CIN, bool ZB16, bool ACC>  // k steps over (w,k): ceil(K*V/4); ZB16: dZ is bf16;
+__global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {  // ACC: dx += (identity residual)
   constexpr int kMixPX = MixCap<CIN>::PX, kMixPZ = MixCap<CIN>::PZ;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -374,24 +374,19 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
   f32x4 rx[ZB16 ? 1 : kMixPX], rd[kMixPX];
   u32x2 rxb[ZB16 ? kMixPX : 1];
   u32x2 rz[ZB16 ? kMixPZ : 1];  // bf16 gradient pieces, raw
-  auto prefetch = [&](int f) {
+  auto prefetch = [&](int f) {  // unconditional loads from clamped indices (see mix_fwd_lds)
     const f32x4* dg = reinterpret_cast<const f32x4*>(a.dx + (size_t)f * V * Cin);
 #pragma unroll
     for (int q = 0; q < kMixPX; ++q) {
-      const int i = tid + q * 256;
-      if (i < n4x) {
-        if constexpr (ZB16) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
-        else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
-        if (a.accumulate) rd[q] = dg[i];
-      }
+      const int i = min(tid + q * 256, n4x - 1);
+      if constexpr (ZB16) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
+      else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
+      if constexpr (ACC) rd[q] = dg[i];
     }
     if constexpr (zb16) {
       const u32x2* zg = reinterpret_cast<const u32x2*>(a.dzb + (size_t)f * KV * Cin);
 #pragma unroll
-      for (int q = 0; q < kMixPZ; ++q) {
-        const int i = tid + q * 256;
-        if (i < n4z) rz[q] = zg[i];
-      }
+      for (int q = 0; q < kMixPZ; ++q) rz[q] = zg[min(tid + q * 256, n4z - 1)];
     }
   };
   if (blockIdx.x < a.frames) prefetch(blockIdx.x);
@@ -404,7 +399,7 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
         const int v = i / C4, c = (i - v * C4) * 4;
         if constexpr (ZB16) *reinterpret_cast<f32x4*>(xs + v * S + c) = bf4_to_f4(rxb[q]);
         else *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
-        if (a.accumulate) *reinterpret_cast<f32x4*>(ds + v * S + c) = rd[q];
+        if (ACC) *reinterpret_cast<f32x4*>(ds + v * S + c) = rd[q];
       }
     }
     if constexpr (zb16) {
@@ -458,7 +453,7 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int v = 16 * mt + 4 * fg + r;
-          if (v < V) dx[(size_t)v * Cin] = acc[mt][r] + (a.accumulate ? ds[v * S + ci0 + fr] : 0.f);
+          if (v < V) dx[(size_t)v * Cin] = acc[mt][r] + (ACC ? ds[v * S + ci0 + fr] : 0.f);
         }
     }
     // dA[v][wk] += sum_ci X_f[v][ci] dZ_f[wk][ci]   (k index of the MFMA = lane group,
@@ -1225,10 +1220,14 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
 
 template <int KS, int CIN, bool ZB16>
 static int launch_mix_bwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16>), true);
+  static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16, false>),
+                      allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16, true>), true);
   (void)once;
   const int grid = std::min(a->frames, 768);  // resident workgroups loop over frames
-  hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
+  if (a->accumulate)
+    hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16, true>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
+  else
+    hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16, false>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
   F3_LAUNCH_CHECK();
   if (a->no_colsum) return F3_OK;
   return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
