@@ -658,7 +658,7 @@ bool debug_stop(int si, int l) {
 // final join. (Main also waiting on the side stream per layer — double-buffered scratch —
 // made HIP's stream-capture end fault on ROCm 7.2.)
 int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
-                    int l_hi, int l_lo, PrepTable& unpack, hipStream_t ss = nullptr, int call_hi = 6) {
+                    int l_hi, int l_lo, PrepTable& unpack, hipStream_t ss = nullptr, int call_hi = 6, int part = 3) {
   if (!ss) ss = s;
   (void)call_hi;
   const bool split = ss != s;
@@ -694,7 +694,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.dresb = L.res == RES_CONV ? bfa(dres, hb) : nullptr;
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
-    F3_TRY(f3_block_bwd_reduce(ba, s));
+    if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
     CaArgs ca;
     std::memset(&ca, 0, sizeof(ca));
     ca.N = N; ca.C = C; ca.inv_tv = 1.f / (float)(To * V); ca.bn2 = bn2;
@@ -706,8 +706,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.bn2_bsum = X.bn2.bsum; ca.bn2_bsq = X.bn2.bsq;
     ca.g_bnca_gamma = q.g(L.bnca.w); ca.g_bnca_beta = q.g(L.bnca.b);
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
-    F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
-    F3_TRY(f3_block_bwd_apply(ba, s));
+    if (part & 1) F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
+    if (part & 1) F3_TRY(f3_block_bwd_apply(ba, s));
     // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
@@ -716,14 +716,14 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
-    F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
+    if (part & 1) F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
     if (debug_stop(si, l)) return F3_OK;
     BnBwdArgs bb;
     std::memset(&bb, 0, sizeof(bb));
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = dg; bb.G = X.G;
     bb.Gpart = X.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb; bb.no_colsum = split;
-    F3_TRY(f3_bn_bwd_apply(bb, s));
+    if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     ConvGemmArgs gd;
     std::memset(&gd, 0, sizeof(gd));
@@ -735,27 +735,25 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (!f3_igemm_ok(gd)) return F3_EINVAL;
       gd.outb = bfa(W.dZ, 1);
     }
-    F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
+    if (part & 1) F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
     mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = X.mixpart; mx.x16 = hb;
     mx.no_colsum = split;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
-    F3_TRY(f3_mix_bwd(&mx, s));
+    if (part & 1) F3_TRY(f3_mix_bwd(&mx, s));
     if (L.res == RES_CONV) {
       ConvGemmArgs rd;
       std::memset(&rd, 0, sizeof(rd));
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
       rd.in = hb ? nullptr : dres; rd.inb = bfa(dres, hb); rd.zero = w.zero;
       rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
-      F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
+      if (part & 1) F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
     }
     // ---- side stream: this layer's weight gradients ----
-    if (split) {
-      if (hipEventRecord(net.ev_main[si][l], s) != hipSuccess) return F3_EHIP;
-      if (hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
-    }
+    if (split && (part & 1) && hipEventRecord(net.ev_main[si][l], s) != hipSuccess) return F3_EHIP;
+    if (split && (part & 2) && hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
     WgradArgs tw;
     std::memset(&tw, 0, sizeof(tw));
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
@@ -767,20 +765,20 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
         tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats; tw.dw_ref = q.g(L.tcn_w);
       } else {  // fp32 atomics into a packed accumulator, unpacked below
         tw.dw = X.dWp;
-        add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
+        if (part & 2) add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
-      F3_TRY(f3_conv_wgrad(&tw, 0, ss));
+      if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
-      F3_TRY(f3_conv_wgrad(&tw, 1, ss));
+      if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 1, ss));
     }
-    F3_TRY(f3_ca_bwd_weights(&ca, ss));
+    if (part & 2) F3_TRY(f3_ca_bwd_weights(&ca, ss));
     if (split) {  // reductions whose results only feed weight gradients
       const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
-      F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
+      if (part & 2) F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
       const int mparts = f3_mix_bwd_parts(&mx);
-      if (mparts) F3_TRY(f3_colsum(X.mixpart, mparts, K * V * V, X.dAeff, ss));
+      if (mparts && (part & 2)) F3_TRY(f3_colsum(X.mixpart, mparts, K * V * V, X.dAeff, ss));
     }
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
@@ -792,11 +790,11 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
-    F3_TRY(f3_conv_wgrad(&gw, 0, ss));
+    if (part & 2) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
     gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
-    F3_TRY(f3_gcn_bias_bwd(&gb, ss));
+    if (part & 2) F3_TRY(f3_gcn_bias_bwd(&gb, ss));
     if (L.res == RES_CONV) {
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
@@ -808,7 +806,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       } else {
         rw.dy = dres; rw.in = X.x;
       }
-      F3_TRY(f3_conv_wgrad(&rw, 0, ss));
+      if (part & 2) F3_TRY(f3_conv_wgrad(&rw, 0, ss));
     }
     dout = dx;
     pp ^= 1;
@@ -819,7 +817,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
   d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), 0);
   d.dout = dout; d.dgamma = q.g(S.dbn.w); d.dbeta = q.g(S.dbn.b);
-  F3_TRY(f3_databn_bwd(&d, s));
+  if (part & 1) F3_TRY(f3_databn_bwd(&d, s));
   return F3_OK;
 }
 
@@ -935,6 +933,16 @@ struct Branches {
   int mask = BR_MOTION | BR_SENSOR | BR_SIDE;
   hipStream_t at(int i) const { return par && i > 0 && (mask >> (i - 1) & 1) ? n.aux[i - 1] : s; }
   hipStream_t side() const { return par && (mask & BR_SIDE) ? n.aux[2] : s; }
+  // weight-gradient queue of skeleton stream si: the motion stream's goes to the sensor queue,
+  // idle once the (short) sensor backward is done, so the two streams' weight gradients drain
+  // in parallel at the end of the backward instead of one after the other on aux[2]
+  hipStream_t side(int si) const {
+    return si == 1 && par && (mask & BR_SIDE) && (mask & BR_SENSOR) && side_split() ? n.aux[1] : side();
+  }
+  static bool side_split() {
+    static const bool v = getenv("F3_SIDE_SPLIT") ? atoi(getenv("F3_SIDE_SPLIT")) != 0 : true;
+    return v;
+  }
   int fork() {
     if (!par || !mask) return F3_OK;
     if (hipEventRecord(n.ev[0], s) != hipSuccess) return F3_EHIP;
@@ -1132,13 +1140,26 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
   auto skeleton = [&](Branches& br, int l_hi, int l_lo) -> int {
     PrepTable unpack[2];
     unpack[0].n = unpack[1].n = 0;
-    for (int l = l_hi; l >= l_lo; --l)
+    // Each layer's main chains are submitted before the previous layer's side-stream work (the
+    // weight gradients): the host can be held up submitting to the long side queue, and the
+    // main queues should already hold their next layer by then. F3_SIDE_LAG=0: same layer.
+    static const int lag = getenv("F3_SIDE_LAG") ? atoi(getenv("F3_SIDE_LAG")) : 1;
+    const bool defer = lag && br.side() != br.s;
+    for (int l = l_hi; l >= l_lo; --l) {
       for (int si = 0; si < net->nstreams; ++si) {
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], br.side(), l_hi));
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], br.side(si), l_hi,
+                               defer ? 1 : 3));
         if (debug_stop(si, l)) return F3_OK;  // tools/diag_layer.py: leave the scratch as is
       }
+      if (defer && l < l_hi)
+        for (int si = 0; si < net->nstreams; ++si)
+          F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, unpack[si], br.side(si), l_hi, 2));
+    }
+    if (defer)
+      for (int si = 0; si < net->nstreams; ++si)
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l_lo, l_lo, unpack[si], br.side(si), l_hi, 2));
     for (int si = 0; si < net->nstreams; ++si)
-      F3_TRY(f3_prep(unpack[si], br.side()));  // the packed tcn weight gradients come from the side stream
+      F3_TRY(f3_prep(unpack[si], br.side(si)));  // the packed tcn weight gradients come from the side stream
     return F3_OK;
   };
   if (phase == 2) {
