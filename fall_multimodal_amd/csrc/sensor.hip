@@ -345,6 +345,105 @@ __global__ __launch_bounds__(1024) void shead_bwd_kernel(SHeadArgs a) {
   }
 }
 
+// The same backward as four launches whose outputs are spread over the whole chip (one
+// thread per output, the batch reduction in a loop): the single-workgroup form took 640 us on
+// one CU and delayed the motion stream's weight gradients queued behind it.
+//
+// Batch sums use 4 independent partial sums (n = u mod 4), so the loads of 4 clips are in
+// flight together instead of one dependent add chain of N loads.
+template <class F>
+F3_DEV float batch_sum(int N, F f) {
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+  int n = 0;
+  for (; n + 4 <= N; n += 4) {
+    p0 += f(n);
+    p1 += f(n + 1);
+    p2 += f(n + 2);
+    p3 += f(n + 3);
+  }
+  for (; n < N; ++n) p0 += f(n);
+  return (p0 + p1) + (p2 + p3);
+}
+
+__global__ __launch_bounds__(256) void shead_bwd_p1(SHeadArgs a) {  // W3 / b3 grads, dy, dpre2
+  const int N = a.N, Cs = a.Cs;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < Cs * HC) {
+    const int k = i / HC, c = i - k * HC;
+    a.g_W3[i] += batch_sum(N, [&](int n) {
+      return a.dout[(size_t)n * a.dout_ld + k] * a.ybn[(size_t)n * HC + c] * a.att[(size_t)n * HC + c];
+    });
+  } else if (i < Cs * HC + Cs) {
+    const int k = i - Cs * HC;
+    a.g_b3[k] += batch_sum(N, [&](int n) { return a.dout[(size_t)n * a.dout_ld + k]; });
+  } else if (i < Cs * HC + Cs + N * HC) {
+    const int e = i - Cs * HC - Cs, n = e / HC, c = e - n * HC;
+    float d = 0.f;
+    for (int k = 0; k < Cs; ++k) d += a.dout[(size_t)n * a.dout_ld + k] * a.W3[(size_t)k * HC + c];
+    const float at = a.att[e];
+    a.dy[e] = d * at;
+    a.dpre2[e] = d * a.ybn[e] * at * (1.f - at);
+  }
+}
+
+__global__ __launch_bounds__(256) void shead_bwd_p2(SHeadArgs a) {  // W2 / b2 grads, dpre1
+  const int N = a.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < HC * HR) {
+    const int c = i / HR, j = i - c * HR;
+    a.g_W2[i] += batch_sum(N, [&](int n) { return a.dpre2[(size_t)n * HC + c] * a.a1[(size_t)n * HR + j]; });
+    if (j == 0) a.g_b2[c] += batch_sum(N, [&](int n) { return a.dpre2[(size_t)n * HC + c]; });
+  } else if (i < HC * HR + N * HR) {
+    const int e = i - HC * HR, n = e / HR, j = e - n * HR;
+    float acc = 0.f;
+    for (int c = 0; c < HC; ++c) acc += a.dpre2[(size_t)n * HC + c] * a.W2[c * HR + j];
+    a.dpre1[e] = a.a1[e] > 0.f ? acc : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void shead_bwd_p3(SHeadArgs a) {  // W1 / b1 grads, dy += W1^T dpre1
+  const int N = a.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < HR * HC) {
+    const int j = i / HC, c = i - j * HC;
+    a.g_W1[i] += batch_sum(N, [&](int n) { return a.dpre1[(size_t)n * HR + j] * a.ybn[(size_t)n * HC + c]; });
+    if (c == 0) a.g_b1[j] += batch_sum(N, [&](int n) { return a.dpre1[(size_t)n * HR + j]; });
+  } else if (i < HR * HC + N * HC) {
+    const int e = i - HR * HC, n = e / HC, c = e - n * HC;
+    float acc = 0.f;
+    for (int j = 0; j < HR; ++j) acc += a.dpre1[(size_t)n * HR + j] * a.W1[j * HC + c];
+    a.dy[e] += acc;
+  }
+}
+
+__global__ __launch_bounds__(1024) void shead_bwd_p4(SHeadArgs a) {  // BatchNorm1d backward
+  __shared__ float red1[HC], red2[HC], mean_s[HC], rstd_s[HC];
+  const int tid = threadIdx.x, N = a.N;
+  if (tid < HC) {
+    const int c = tid;
+    const double m = a.bn_sum[c] / N;
+    double var = a.bn_sq[c] / N - m * m;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + kBnEps));
+    const float mf = (float)m;
+    const float s1 = batch_sum(N, [&](int n) { return a.dy[(size_t)n * HC + c]; });
+    const float s2 = batch_sum(N, [&](int n) { return a.dy[(size_t)n * HC + c] * ((a.hmean[(size_t)n * HC + c] - mf) * rstd); });
+    a.g_gamma[c] += s2;
+    a.g_beta[c] += s1;
+    red1[c] = s1 / N;
+    red2[c] = s2 / N;
+    mean_s[c] = mf;
+    rstd_s[c] = rstd;
+  }
+  __syncthreads();
+  for (int i = tid; i < N * HC; i += 1024) {
+    const int c = i % HC;
+    const float mean = mean_s[c], rstd = rstd_s[c];
+    const float xh = (a.hmean[i] - mean) * rstd;
+    a.dhmean[i] = a.bn.gamma[c] * rstd * (a.dy[i] - red1[c] - xh * red2[c]);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // CNN1D: Conv1d(k5,p2) -> BN (batch stats) -> ReLU -> MaxPool1d(2), twice
 // layout: [N][T][C] rows (time-major, channel contiguous)
@@ -490,7 +589,21 @@ int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
 }
 
 int f3_shead_bwd(const SHeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(shead_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  static const bool one_wg = getenv("F3_SHEAD_1WG") != nullptr;  // the single-workgroup form (A/B)
+  if (one_wg) {
+    hipLaunchKernelGGL(shead_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
+  const int N = a->N, Cs = a->Cs;
+  auto blocks = [](int n) { return dim3((n + 255) / 256); };
+  hipLaunchKernelGGL(shead_bwd_p1, blocks(Cs * HC + Cs + N * HC), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shead_bwd_p2, blocks(HC * HR + N * HR), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shead_bwd_p3, blocks(HR * HC + N * HC), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shead_bwd_p4, dim3(1), dim3(1024), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
