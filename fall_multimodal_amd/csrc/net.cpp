@@ -1145,19 +1145,26 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     // main queues should already hold their next layer by then. F3_SIDE_LAG=0: same layer.
     static const int lag = getenv("F3_SIDE_LAG") ? atoi(getenv("F3_SIDE_LAG")) : 1;
     const bool defer = lag && br.side() != br.s;
+    // F3_TAIL_SIDE=0 runs the first layer's weight gradients on the stream's own queue (idle
+    // after its input gradient) instead of the side queues: measured neutral to 1 % slower
+    // (6.50-6.57 vs 6.49-6.56 ms), so the side queues stay the default.
+    static const bool tail_side = !getenv("F3_TAIL_SIDE") || atoi(getenv("F3_TAIL_SIDE")) != 0;
+    // (only with the slab wgrad: the atomic form's unpack launch runs on the side queue)
+    auto side_of = [&](int si, int l) { return l == 0 && !tail_side && wgrad_slab() ? br.at(si) : br.side(si); };
     for (int l = l_hi; l >= l_lo; --l) {
       for (int si = 0; si < net->nstreams; ++si) {
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], br.side(si), l_hi,
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], side_of(si, l), l_hi,
                                defer ? 1 : 3));
         if (debug_stop(si, l)) return F3_OK;  // tools/diag_layer.py: leave the scratch as is
       }
       if (defer && l < l_hi)
         for (int si = 0; si < net->nstreams; ++si)
-          F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, unpack[si], br.side(si), l_hi, 2));
+          F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, unpack[si], side_of(si, l + 1),
+                                 l_hi, 2));
     }
     if (defer)
       for (int si = 0; si < net->nstreams; ++si)
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l_lo, l_lo, unpack[si], br.side(si), l_hi, 2));
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l_lo, l_lo, unpack[si], side_of(si, l_lo), l_hi, 2));
     for (int si = 0; si < net->nstreams; ++si)
       F3_TRY(f3_prep(unpack[si], br.side(si)));  // the packed tcn weight gradients come from the side stream
     return F3_OK;
