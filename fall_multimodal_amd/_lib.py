@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfall3.so")
+LIB_PATH = os.environ.get("F3_LIB") or os.path.join(HERE, "libfall3.so")  # F3_LIB: A/B of two builds (tools only)
 
 # every symbol declared in include/fall3.h
 EXPORTS = (

@@ -989,10 +989,22 @@ __global__ __launch_bounds__(256) void ca_bwd1_kernel(CaArgs a) {
     a.dq2[(size_t)n * C + c] = d;
   }
   __syncthreads();
+  // dhid: the four waves each take every fourth channel, partials summed through LDS
+  __shared__ float part[4][64];
+  const int j = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (j < H) {
+    float acc0 = 0.f, acc1 = 0.f;
+    int c = wv;
+    for (; c + 4 < C; c += 8) {
+      acc0 += dq[c] * a.W2[(size_t)c * H + j];
+      acc1 += dq[c + 4] * a.W2[(size_t)(c + 4) * H + j];
+    }
+    if (c < C) acc0 += dq[c] * a.W2[(size_t)c * H + j];
+    part[wv][j] = acc0 + acc1;
+  }
+  __syncthreads();
   if (threadIdx.x < H) {
-    const int j = threadIdx.x;
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += dq[c] * a.W2[(size_t)c * H + j];
+    const float acc = (part[0][j] + part[1][j]) + (part[2][j] + part[3][j]);
     a.dbn[(size_t)n * H + j] = a.hid[(size_t)n * H + j] > 0.f ? acc : 0.f;
   }
 }
@@ -1090,26 +1102,41 @@ __global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
   for (int e = threadIdx.x; e < nc * H; e += 256) atomic_add_f(a.g_W2 + (size_t)c0 * H + e, t2[e]);
 }
 
-// per clip: dgap = W1^T dq1 ; e = dgap/TV ; BN2 backward sums D1, D2
+// per clip: dgap = W1^T dq1 ; e = dgap/TV ; BN2 backward sums D1, D2. kCaB3Clips clips per
+// workgroup, their channel sums combined in registers before the (double) atomics, so each
+// channel slot takes N/kCaB3Clips atomics instead of N.
+constexpr int kCaB3Clips = 4;
 __global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
-  __shared__ float dq[64];
-  const int n = blockIdx.x, C = a.C, H = C / 4;
-  if (threadIdx.x < H) dq[threadIdx.x] = a.dq1[(size_t)n * H + threadIdx.x];
+  __shared__ float dq[kCaB3Clips][64];
+  const int n0 = blockIdx.x * kCaB3Clips, C = a.C, H = C / 4, N = a.N;
+  for (int i = threadIdx.x; i < kCaB3Clips * H; i += 256) {
+    const int nn = i / H, k = i - nn * H;
+    dq[nn][k] = n0 + nn < N ? a.dq1[(size_t)(n0 + nn) * H + k] : 0.f;
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
-    float dg = 0.f;
-    for (int k = 0; k < H; ++k) dg += dq[k] * a.W1[(size_t)k * C + c];
     float sc, sh, mu, rs;
     bn_coeff(a.bn2, c, sc, sh, mu, rs);
-    const size_t o = (size_t)n * C + c;
-    a.e[o] = dg * a.inv_tv;
-    const float at = a.att[o];
-    const float xsum = (a.gapsum[o] - mu / a.inv_tv) * rs;  // sum_tv xhat2
-    atomic_add_d(a.bn2_bsum + c, (double)(at * a.P1[o] + dg));
-    atomic_add_d(a.bn2_bsq + c, (double)(at * a.P2[o] + dg * a.inv_tv * xsum));
-    if (a.bnr_bsum) {  // conv residual BN: channel sums of dz and dz*xhat_r over the clips
-      atomic_add_d(a.bnr_bsum + c, (double)a.P1[o]);
-      atomic_add_d(a.bnr_bsq + c, (double)a.Q2[o]);
+    double s1 = 0.0, s2 = 0.0, r1 = 0.0, r2 = 0.0;
+    for (int nn = 0; nn < kCaB3Clips && n0 + nn < N; ++nn) {
+      float dg = 0.f;
+      for (int k = 0; k < H; ++k) dg += dq[nn][k] * a.W1[(size_t)k * C + c];
+      const size_t o = (size_t)(n0 + nn) * C + c;
+      a.e[o] = dg * a.inv_tv;
+      const float at = a.att[o];
+      const float xsum = (a.gapsum[o] - mu / a.inv_tv) * rs;  // sum_tv xhat2
+      s1 += (double)(at * a.P1[o] + dg);
+      s2 += (double)(at * a.P2[o] + dg * a.inv_tv * xsum);
+      if (a.bnr_bsum) {  // conv residual BN: channel sums of dz and dz*xhat_r over the clips
+        r1 += (double)a.P1[o];
+        r2 += (double)a.Q2[o];
+      }
+    }
+    atomic_add_d(a.bn2_bsum + c, s1);
+    atomic_add_d(a.bn2_bsq + c, s2);
+    if (a.bnr_bsum) {
+      atomic_add_d(a.bnr_bsum + c, r1);
+      atomic_add_d(a.bnr_bsq + c, r2);
     }
   }
 }
@@ -1389,7 +1416,7 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ca_bwd3_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(ca_bwd3_kernel, dim3((a->N + kCaB3Clips - 1) / kCaB3Clips), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
