@@ -198,7 +198,7 @@ def test_train_step_matches_reference_golden(tag):
             assert int(b) == 1, name
 
 
-@pytest.mark.parametrize("layout,S,B", [("coco_mmpose", 6, 32), ("coco_cut", 15, 24)])
+@pytest.mark.parametrize("layout,S,B", [("coco_mmpose", 6, 32), ("coco_cut", 15, 24), ("coco_mmpose", 6, 13)])
 def test_fused_train_step_vs_oracle(layout, S, B):
     """TrainStep (native fwd + CE + bwd + RMSprop) vs the CPU oracle at a larger batch."""
     d = dev()
