@@ -1210,7 +1210,11 @@ template <int KS, int CIN, bool XB>
 static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
   static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN, XB>), true);
   (void)once;
-  const int grid = std::min(a->frames, 1024);  // resident workgroups loop over frames
+  // resident workgroups loop over frames; measured (serial step, 256-1024-4096 swept with
+  // F3_MIX_GRID): 1024 best for 64/128 channels, 512 for 256 (30.4 vs 32.7 us)
+  static const int env = getenv("F3_MIX_GRID") ? atoi(getenv("F3_MIX_GRID")) : 0;
+  const int cap = env > 0 ? env : (CIN >= 256 ? 512 : 1024);
+  const int grid = std::min(a->frames, cap);
   hipLaunchKernelGGL((mix_fwd_lds_kernel<KS, CIN, XB>), dim3(grid), dim3(256), mix_lds_fwd2(*a), s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
