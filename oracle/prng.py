@@ -15,6 +15,8 @@ The value range is chosen from the name and rank alone:
 * ``edge_importance.*``                      U(0.5, 1.5)    (reference init is ones,
                                               stgcan.py:198-201; randomised so its
                                               gradient path is exercised)
+* ``node_embeddings`` (TARGCN)               U(±sqrt 3): unit variance, as the reference's
+                                              torch.randn init (TRAGCN.py:194)
 """
 from __future__ import annotations
 
@@ -29,6 +31,8 @@ def param_value(name: str, shape, seed: int) -> np.ndarray:
     leaf = name.rsplit(".", 1)[-1]
     if "edge_importance" in name:
         lo, hi = 0.5, 1.5
+    elif name.endswith("node_embeddings"):
+        lo, hi = -np.sqrt(3.0), np.sqrt(3.0)
     elif leaf.startswith(("weight_ih", "weight_hh", "bias_ih", "bias_hh")):
         h = shape[0] // 4
         b = 1.0 / np.sqrt(h)

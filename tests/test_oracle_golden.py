@@ -50,3 +50,42 @@ def test_oracle_train_step_matches_reference(tag):
     for name, b in st.items():
         if name.endswith(("running_mean", "running_var")):
             check_packed(d, "buf:" + name, b.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_package_graph_matches_reference():
+    """fall_multimodal_amd/graph.py (the product's copy, buffer `A`) vs the reference's Graph.A."""
+    from fall_multimodal_amd.graph import Graph
+    z = np.load(os.path.join(GOLDEN, "graphs.npz"))
+    for key in z.files:
+        layout, strat = key.split(":")
+        np.testing.assert_array_equal(Graph(layout, strat).A, z[key])
+
+
+TARGCN_TAGS = ["v14", "v17"]
+
+
+def test_targcn_param_counts_match_reference_kats():
+    from oracle import targcn_cpu as tg
+    kat = json.load(open(os.path.join(GOLDEN, "param_counts.json")))
+    assert kat["targcn_v14"] == 3235763   # TARGCN_HAR_conv_10kfold.ipynb:282
+    assert kat["targcn_v17"] == 3235955   # SURVEY §8 cfg 2 (measured on the reference)
+    for tag, V in (("v14", 14), ("v17", 17)):
+        n = sum(int(np.prod(s)) for k, s in tg.param_shapes(V).items() if not tg.is_buffer(k))
+        assert n == kat["targcn_" + tag]
+
+
+@pytest.mark.parametrize("tag", TARGCN_TAGS)
+def test_targcn_oracle_train_step_matches_reference(tag):
+    from oracle import targcn_cpu as tg
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    z = np.load(os.path.join(GOLDEN, f"targcn_{tag}.npz"))
+    d = {k: z[k] for k in z.files}
+    st = tg.init_state(int(d["V"][0]), int(d["seed"][0]))
+    out, loss, grads = tg.train_step(st, torch.from_numpy(d["source"]), torch.from_numpy(d["label"]),
+                                     lr=float(d["lr"][0]))
+    np.testing.assert_allclose(out.numpy(), d["out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(loss.item(), d["loss"][0], rtol=1e-6, atol=1e-6)
+    for name, g in grads.items():
+        check_packed(d, "grad:" + name, g.numpy(), rtol=1e-4, atol=1e-7)
+    for name, g in grads.items():
+        check_packed(d, "post:" + name, st[name].numpy(), rtol=1e-5, atol=1e-7)

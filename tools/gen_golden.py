@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate golden vectors by running the REFERENCE's own modules (build container only).
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--targcn-only]
 Writes: tests/golden/*.npz  (small, committed; the reference itself never travels).
 
 How the reference is imported: the packaged 3-stream model lives in
@@ -32,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 from oracle import model_cpu as oc  # noqa: E402
+from oracle import targcn_cpu as tg  # noqa: E402
 from oracle.prng import synthetic_batch  # noqa: E402
 
 REF = "/root/reference"
@@ -109,8 +110,59 @@ def run_case(tag, module, spec, forward_fn, batch, seed, frames=30, sensor_frame
     return nparams
 
 
+def import_targcn():
+    """TRAGCN.py imports `TRAGCN.GRU` / `TRAGCN.TA` (the notebook's package name,
+    TARGCN_HAR_conv_10kfold.ipynb cell 3): alias a package of that name to the reference root."""
+    tp = types.ModuleType("TRAGCN")
+    tp.__path__ = [REF]
+    sys.modules["TRAGCN"] = tp
+    with contextlib.redirect_stdout(io.StringIO()):
+        return importlib.import_module("TRAGCN.TRAGCN")
+
+
+def run_targcn_case(tag, T, V, batch, seed, lr=1e-5):
+    """TARGCN(adj=None, num_nodes=V) train step as the notebook runs it: out = model(pts.permute(0,2,3,1)),
+    CrossEntropyLoss(out, soft labels), RMSprop(lr=1e-5). weights_pool / bias_pool are
+    uninitialised memory in the reference (EmbGCN.py:67-68): every parameter is loaded from the
+    portable PRNG instead."""
+    torch.manual_seed(0)
+    model = T.TARGCN(adj=None, num_nodes=V)
+    state = tg.init_state(V, seed)
+    model.load_state_dict(state, strict=True)
+    model.train()
+    src, label = tg.synthetic_source(batch, V, 11, seed + 1)
+    x, lb = torch.from_numpy(src), torch.from_numpy(label)
+    opt = torch.optim.RMSprop(model.parameters(), lr=lr)
+    opt.zero_grad()
+    out = model(x)
+    loss = torch.nn.CrossEntropyLoss()(out, lb)
+    loss.backward()
+    d = {"seed": np.array([seed]), "V": np.array([V]), "source": src, "label": label, "lr": np.array([lr]),
+         "out": out.detach().numpy(), "loss": np.array([loss.item()])}
+    nparams = 0
+    for name, p in model.named_parameters():
+        nparams += p.numel()
+        pack("grad:" + name, d, p.grad)
+    opt.step()
+    for name, p in model.named_parameters():
+        pack("post:" + name, d, p)
+    d["nparams"] = np.array([nparams])
+    path = os.path.join(OUT, f"targcn_{tag}.npz")
+    np.savez_compressed(path, **d)
+    print(f"targcn {tag}: params={nparams} loss={loss.item():.6f} -> {path} ({os.path.getsize(path)//1024} KB)")
+    return nparams
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--targcn-only" in sys.argv:
+        T = import_targcn()
+        kat = json.load(open(os.path.join(OUT, "param_counts.json")))
+        kat["targcn_v14"] = run_targcn_case("v14", T, 14, 4, 7001)
+        kat["targcn_v17"] = run_targcn_case("v17", T, 17, 3, 7002)
+        with open(os.path.join(OUT, "param_counts.json"), "w") as f:
+            json.dump(kat, f, indent=1, sort_keys=True)
+        return
     stg, gr, comb, bil, ns = import_reference()
 
     # graph adjacency for every layout x strategy (graph.py:20-126)
@@ -150,6 +202,9 @@ def main():
                   spec, lambda m, sk, se: m((sk, sk[:, :2, 1:] - sk[:, :2, :-1], se)), 4, 6789))
     for tag, mod, spec, fn, b, seed in cases:
         kat[tag] = run_case(tag, mod, spec, fn, b, seed)
+    T = import_targcn()
+    kat["targcn_v14"] = run_targcn_case("v14", T, 14, 4, 7001)
+    kat["targcn_v17"] = run_targcn_case("v17", T, 17, 3, 7002)
     with open(os.path.join(OUT, "param_counts.json"), "w") as f:
         json.dump(kat, f, indent=1, sort_keys=True)
 
