@@ -21,10 +21,16 @@ EXPORTS = (
     "f3_net_loss", "f3_net_backward", "f3_rmsprop_step", "f3_conv_forward", "f3_status_string",
     "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_graph_mix_forward",
     "f3_graph_mix_backward", "f3_net_backward_phase", "f3_net_grad_split",
+    "f3_targcn_create", "f3_targcn_destroy", "f3_targcn_num_entries", "f3_targcn_entry", "f3_targcn_param_count",
+    "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_soft_ce",
 )
 
 F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE = 0, 1001, 1002, 1003, 1004
 ENTRY_PARAM, ENTRY_BUFFER, ENTRY_COUNTER = 0, 1, 2
+
+
+class F3TargcnConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("num_node", "num_class", "precision")]
 
 
 class F3Config(ctypes.Structure):
@@ -68,6 +74,17 @@ def lib():
         "f3_conv_wgrad_packed": (I, [P, P, P, ctypes.c_longlong, I, I, I, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
+        "f3_targcn_create": (I, [ctypes.POINTER(F3TargcnConfig), ctypes.POINTER(P)]),
+        "f3_targcn_destroy": (None, [P]),
+        "f3_targcn_num_entries": (I, [P]),
+        "f3_targcn_entry": (I, [P, I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(I), ctypes.POINTER(I),
+                                ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "f3_targcn_param_count": (I64, [P]),
+        "f3_targcn_buffer_count": (I64, [P]),
+        "f3_targcn_workspace_bytes": (I64, [P, I]),
+        "f3_targcn_forward": (I, [P, I, P, P, P, P, P, P]),
+        "f3_targcn_backward": (I, [P, I, P, P, P, P, P, P]),
+        "f3_soft_ce": (I, [P, P, I, I, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

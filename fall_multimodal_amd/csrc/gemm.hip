@@ -256,7 +256,11 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmArgs a) {
 
 // dW[j][i'] = sum_m dY[m][j] * pro(In[src(m,dt)][i])   (split-K over rows, f32 atomics)
 template <int PRO>
-__global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
+__global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a_) {
+  WgradArgs a = a_;
+  const int nsplit = (a.g.M + a.rows_per_split - 1) / a.rows_per_split;
+  const int zsplit = blockIdx.z % nsplit;
+  wgrad_group(a, blockIdx.z / nsplit);
   __shared__ __attribute__((aligned(16))) float Ys[2][BN][LDK];
   __shared__ __attribute__((aligned(16))) float Xs[2][BN][LDK];
   __shared__ float pro_sc[256], pro_sh[256];
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
   const int itiles = (g.Kc + BN - 1) / BN;
   const int dt = blockIdx.y / itiles;
   const int i0 = (blockIdx.y - dt * itiles) * BN;
-  const int r_begin = blockIdx.z * a.rows_per_split;
+  const int r_begin = zsplit * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
   if (PRO) {
     for (int i = tid; i < g.Kc; i += 256) {
@@ -438,7 +442,7 @@ int f3_conv_wgrad(const WgradArgs* args, int pro, hipStream_t s) {
   if (rps < 4 * BK) rps = 4 * BK;
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
-  dim3 grid(gx, gy, splits);
+  dim3 grid(gx, gy, splits * std::max(1, a.groups));
   if (pro) hipLaunchKernelGGL(conv_wgrad_f32<1>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(conv_wgrad_f32<0>, grid, dim3(256), 0, s, a);
   F3_LAUNCH_CHECK();

@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
 // dividing by V and T per stage. Forward-geometry rows only (g.transposed == 0).
 // ----------------------------------------------------------------------------
 template <int WJW, int WIW, int MJ, int MI, int BK = 64>
-__global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a) {
+__global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   constexpr int NW = WJW * WIW;  // waves: 8 (one workgroup per CU) or 4 (the 64-wide tiles)
   constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;
   constexpr int UJ = TJ / 16, UI = TI / 16;
@@ -721,11 +721,17 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a) {
   static_assert(32 * RJ + 4 * RJ < 65536 && 32 * RI + 4 * RI < 65536, "ds offset immediates");
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + TJ * 4];
   float* dbs = reinterpret_cast<float*>(smem + NST * STAGE);  // [TJ]
-  const ConvGeom& g = a.g;
+  const ConvGeom& g = a_.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int itiles = (g.Kc + TI - 1) / TI;
   const int gx = (g.Nc + TJ - 1) / TJ, gy = g.KT * itiles;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a row split's tiles stay on one XCD
+  int lin = xcd_remap(blockIdx.x, gridDim.x);  // a row split's tiles stay on one XCD
+  WgradArgs a = a_;
+  if (a_.groups > 1) {  // grouped launch: problem-major over the 1-D grid
+    const int per = gridDim.x / a_.groups;
+    wgrad_group(a, lin / per);
+    lin %= per;
+  }
   const int bz = lin / (gx * gy);
   const int rem = lin - bz * gx * gy;
   const int by = rem / gx, bx = rem - by * gx;
@@ -937,7 +943,8 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
   static const int slots = resident_wgs((const void*)KERNEL, THREADS);
   const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
-  int splits = std::max(1, target / (gx * gy));
+  const int groups = std::max(1, a.groups);  // grouped launches: wgrad_big, atomics (checked by the caller)
+  int splits = std::max(1, target / (gx * gy * groups));
   const bool to_slab = a.slab && a.outmap == WG_OUT_CONV;
   const long long per_split = (long long)a.g.Nc * a.g.KT * a.g.Kc;
   if (to_slab) {
@@ -953,8 +960,8 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the
   // round-robin 3-D grid
   static const int xcd = getenv("F3_WGRAD_XCD") ? atoi(getenv("F3_WGRAD_XCD")) : 1;
-  a.xcd = xcd || THREADS == 512;  // wgrad_big always maps its 1-D grid by XCD
-  dim3 grid = a.xcd ? dim3(gx * gy * splits) : dim3(gx, gy, splits);
+  a.xcd = xcd || THREADS == 512 || groups > 1;  // wgrad_big always maps its 1-D grid by XCD
+  dim3 grid = a.xcd ? dim3(gx * gy * splits * groups) : dim3(gx, gy, splits);
   hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), 0, s, a);
   F3_LAUNCH_CHECK();
   if (to_slab && a.dw_ref) {
@@ -972,17 +979,19 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
   static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
   const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
+  if (a.groups > 1 && (a.g.transposed || a.slab)) return F3_EINVAL;  // grouped: wgrad_big + atomics only
+  const int bigv = a.groups > 1 ? 1 : big;
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once
   // per 256 output channels) wins. F3_WGRAD_BIG=0 restores the first 4-wave kernel (wgrad_glds_bf16).
-  if (big && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0)
+  if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0)
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
-  if (big && a.g.Nc % 128 == 0 && a.g.Kc % 256 == 0)
+  if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 256 == 0)
     return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4>>(a, s);
-  if (big && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0)
+  if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0)
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
-  if (big) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
+  if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);
     if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4>>(a, s);
     return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2>>(a, s);

@@ -70,7 +70,23 @@ struct WgradArgs {
   float* slab;
   long long slab_cap;         // floats
   float* dw_ref;
+  // Grouped launch (TARGCN per-node weight gradients): `groups` independent problems of the same
+  // geometry, problem q reading dy + q*gs_dy, in + q*gs_in (elements) and accumulating into
+  // dw + q*gs_dw, db + q*gs_db. groups <= 1: one problem. Atomics path only (slab == null).
+  int groups;
+  long long gs_dy, gs_in, gs_dw, gs_db;
 };
+
+// Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).
+F3_DEV void wgrad_group(WgradArgs& a, int grp) {
+  if (a.groups <= 1) return;
+  if (a.dy) a.dy += grp * a.gs_dy;
+  if (a.in) a.in += grp * a.gs_in;
+  if (a.dyb) a.dyb += grp * a.gs_dy;
+  if (a.inb) a.inb += grp * a.gs_in;
+  a.dw += grp * a.gs_dw;
+  if (a.db) a.db += grp * a.gs_db;
+}
 
 }  // namespace f3
 

@@ -132,6 +132,44 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
 
 const char* f3_status_string(int status);
 
+/* ---- TARGCN skeleton model (BASELINE config 2; TRAGCN.py, EmbGCN.py, GRU.py, TA.py) ----
+ * f3_targcn_create      <- TARGCN(adj=None, num_nodes=V)          TRAGCN.py:177-205
+ *                          (the notebook's call, TARGCN_HAR_conv_10kfold.ipynb cell 3)
+ * f3_targcn_entry       <- model.state_dict() keys/shapes (same names, order, shapes;
+ *                          PARAM offsets 16-B aligned in the flat parameter array)
+ * f3_targcn_forward     <- out = model(pts.permute(0,2,3,1))      TRAGCN.py:207-224
+ * f3_targcn_backward    <- loss.backward()
+ * f3_soft_ce            <- torch.nn.CrossEntropyLoss()(out, soft labels)
+ * Optimizer: f3_rmsprop_step (the notebook's RMSprop). precision: F3_PRECISION_FP32 (exact fp32
+ * MFMA, parity mode) or F3_PRECISION_BF16 (bf16 GEMM operands, fp32 accumulate and state). */
+typedef struct f3_targcn_config {
+  int num_node;   /* V (2..18) */
+  int num_class;  /* fc output width */
+  int precision;  /* F3_PRECISION_FP32 | F3_PRECISION_BF16 */
+} f3_targcn_config;
+
+typedef struct f3_targcn f3_targcn;
+
+int f3_targcn_create(const f3_targcn_config* cfg, f3_targcn** out);
+void f3_targcn_destroy(f3_targcn* net);
+int f3_targcn_num_entries(const f3_targcn* net);
+int f3_targcn_entry(const f3_targcn* net, int i, const char** name, int* kind, int* ndim, int64_t* shape8,
+                    int64_t* offset);
+int64_t f3_targcn_param_count(const f3_targcn* net);
+int64_t f3_targcn_buffer_count(const f3_targcn* net);
+int64_t f3_targcn_workspace_bytes(const f3_targcn* net, int batch);
+/* source f32[B,T=30,V,3] (the notebook's pts.permute(0,2,3,1)), out f32[B,num_class] logits.
+ * TARGCN has no batch statistics or dropout: train and eval forwards are the same computation;
+ * the workspace keeps what backward needs. */
+int f3_targcn_forward(f3_targcn* net, int batch, const float* params, const float* buffers, const float* source,
+                      float* out, void* workspace, void* stream);
+/* grads (flat, params layout) are OVERWRITTEN with d(sum dout*out)/dparams of the last forward. */
+int f3_targcn_backward(f3_targcn* net, int batch, const float* params, const float* buffers, const float* dout,
+                       float* grads, void* workspace, void* stream);
+/* loss = -(1/N) sum_i sum_c y_ic log_softmax(out_i)_c (soft targets, not renormalised);
+ * dout = dloss/dout. loss is overwritten. */
+int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream);
+
 /* Debug accessor for tools/tests: device pointer of a per-layer workspace tensor
  * ("x","z","g","h","r","out","att","dh","dv","dg","dZ","dres","bn1_fsum",...) or NULL. */
 void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, int layer, const char* what);
