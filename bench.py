@@ -49,6 +49,9 @@ def parse():
                         "step: 10.1 vs 8.15 ms at B=256; see DESIGN.md)")
     p.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old commands
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--model", default="fall3", choices=("fall3", "targcn"),
+                   help="fall3: the headline 3-stream step (default). targcn: BASELINE config 2 alone")
+    p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN line in the default run")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
 
@@ -141,6 +144,47 @@ def eval_throughput(model, sk, se, reps=20):
     return {"clips_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3), "batch": B}
 
 
+def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_seconds=0.0):
+    """BASELINE config 2: skeleton-only TARGCN (TRAGCN.py:177-224, V=17 joints, T=30, bf16 GEMM
+    operands) training step (fwd + CE + bwd + RMSprop) at B=256 on one GPU, synthetic clips,
+    random-init weights. ms_per_step is the whole step; the recurrence is 2 layers x 30 dependent
+    GRU steps forward and backward (per-kernel times: profiles/r02_targcn_kernel_summary.txt)."""
+    import fall_multimodal_amd as f3
+    from oracle import targcn_cpu as tg
+    src, lab = tg.synthetic_source(B, V, 11, 3)
+    model = f3.TARGCN(num_nodes=V, device=dev, precision=precision)
+    step = f3.TargcnStep(model, B, lr=1e-5)
+    x, y = torch.from_numpy(src).to(dev), torch.from_numpy(lab).to(dev)
+    for _ in range(warmup):
+        step(x, y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(x, y)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    rec = {"metric": "clips/sec (fwd+bwd) TARGCN skeleton-only, B=256, 1 GPU", "value": round(B / dt, 1),
+           "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": precision, "steps": steps,
+           "config": {"workload": f"targcn_V{V}_T30_B{B}", "global_batch": B, "joints": V, "frames": 30,
+                      "gru_layers": 2, "hidden": 64, "ta_layers": 2},
+           "final_loss": round(float(step.loss.item()), 5)}
+    if cpu_seconds > 0:  # the oracle (pinned bit-exactly to the reference) on this host's cores
+        threads = min(os.cpu_count() or 1, 64)
+        torch.set_num_threads(threads)
+        st = tg.init_state(V, 7)
+        Bc = 64
+        s_c, l_c = (torch.from_numpy(a) for a in tg.synthetic_source(Bc, V, 11, 1))
+        tg.train_step(st, s_c, l_c)
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < cpu_seconds and n < 20:
+            tg.train_step(st, s_c, l_c)
+            n += 1
+        rec["cpu_baseline"] = {"value": round(Bc * n / (time.perf_counter() - t0), 2), "unit": "clips/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{n} oracle train steps of B={Bc}, V={V}, fp32, torch CPU"}
+    return rec
+
+
 def cpu_baseline(layout, V, S, seconds):
     """The oracle (CPU PyTorch restatement, pinned to the reference) on this host's cores."""
     from oracle import model_cpu as oc
@@ -176,6 +220,12 @@ def main():
     import fall_multimodal_amd as f3
     from oracle.prng import synthetic_batch
 
+    if a.model == "targcn":
+        rec = targcn_bench(dev, steps=a.steps, warmup=a.warmup, precision=a.precision,
+                           cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        return
     V = 18 if a.layout == "coco_mmpose" else 14
     B, S, C = a.batch, a.sensor_dim, 11
     model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev,
@@ -206,6 +256,7 @@ def main():
     loss = float(step.loss.item())
     ev = eval_throughput(model, sk, se) if rank == 0 else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
+    tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
         rec = {
@@ -228,6 +279,7 @@ def main():
             "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
             "eval_forward": ev,
+            "cfg2_targcn": tgrec,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

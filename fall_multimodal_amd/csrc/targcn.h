@@ -47,6 +47,7 @@ struct GruFwdArgs {
   void* XI;           // [R][IP] gate input [x,h]
   void* UG;           // [R][IP] mixed update input S.[x,r*h]
   void* UI;           // [R][IP] update input [x,r*h]
+  long long* prof;    // optional phase stamps (F3_TG_PROF), [T][8]
 };
 
 struct GruBwdArgs {

@@ -19,6 +19,7 @@
 #include "targcn.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace f3 {
 namespace tg {
@@ -32,8 +33,11 @@ struct Op<true> {
   typedef __bf16 T;
   static constexpr int KS = 32;       // k per MFMA (v_mfma_f32_16x16x32_bf16)
   static constexpr int XS = IP + 8;   // LDS row stride: 272-B rows, conflict-free b128 A reads
-  static constexpr int BTF = 16;      // clips per workgroup, forward
-  static constexpr int BTB = 8;       // backward (four [node][clip][k] buffers in LDS)
+  static constexpr int BTF = 4;       // clips per workgroup, forward. MFMA rows 4-15 idle: the step
+                                      // time of a workgroup is set by its weight stream, not its row
+                                      // count, and fewer clips per workgroup spread the per-step
+                                      // stores over more CUs (64 workgroups at B = 256)
+  static constexpr int BTB = 4;       // backward (four [node][clip][k] buffers in LDS)
 };
 template <>
 struct Op<false> {
@@ -55,45 +59,80 @@ F3_DEV f32x4 mma(const typename Op<B16>::T* a, const typename Op<B16>::T* b, f32
   }
 }
 
+F3_DEV bf16x8_t ld8(const __bf16* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+F3_DEV f32x4 mfma8(bf16x8_t a, bf16x8_t b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
 F3_DEV float silu_grad(float s) {  // d/ds s*sigmoid(s)
   const float g = sigmoidf_(s);
   return g * (1.f + s * (1.f - g));
 }
 
-// out[n][b][k] (+)= sum_m S'[n][m] in[m][b][k] for k < I (pairs of columns per thread);
-// S' = S (forward mix, EmbGCN.py:84) or S^T (its input gradient).
+// out[n][b][k] (+)= sum_m S'[n][m] in[m][b][k] for k < I; S' = S (forward mix, EmbGCN.py:84)
+// or S^T (its input gradient). Each thread owns one output node n (its S' row in registers) and
+// walks 8-element chunks (b, k..k+7) with 16-B LDS reads: V reads + 8V FMAs per chunk.
 template <typename TY, int BT, int XS, bool TRANS, bool ACC, int NT>
 F3_DEV void node_mix(const TY* in, TY* out, const float* Sl, int V, int I, int tid) {
-  const int kp = (I + 1) >> 1;
-  for (int ci = tid; ci < BT * kp; ci += NT) {
-    const int b = ci / kp, k = (ci - b * kp) * 2;
-    float a0[VMAX], a1[VMAX];
+  const int tpn = NT / V;            // threads per output node
+  int tl = tid;
+  asm volatile("" : "+v"(tl));       // per call: keep the S row out of loop-invariant registers
+  const int n = tl / tpn, sub = tl - n * tpn;
+  if (n >= V) return;
+  const int k8 = (I + 7) >> 3;
+  const float* srow = Sl + (TRANS ? n : n * V);
+  const int sstr = TRANS ? V : 1;
+  for (int cidx = sub; cidx < BT * k8; cidx += tpn) {
+    const int b = cidx / k8, k = (cidx - b * k8) * 8;
+    float acc[8];
 #pragma unroll
-    for (int n = 0; n < VMAX; ++n) a0[n] = a1[n] = 0.f;
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll 2
     for (int m = 0; m < V; ++m) {
       const TY* src = in + (m * BT + b) * XS + k;
-      const float x0 = (float)src[0], x1 = (float)src[1];
+      const float sm = srow[m * sstr];
+      float x[8];
+      if constexpr (sizeof(TY) == 2) {
+        const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(src);
 #pragma unroll
-      for (int n = 0; n < VMAX; ++n) {
-        if (n < V) {
-          const float s = TRANS ? Sl[m * V + n] : Sl[n * V + m];
-          a0[n] += s * x0;
-          a1[n] += s * x1;
+        for (int e = 0; e < 8; ++e) x[e] = (float)v[e];
+      } else {
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = v0[e];
+          x[e + 4] = v1[e];
         }
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += sm * x[e];
     }
+    TY* dst = out + (n * BT + b) * XS + k;
+    if constexpr (sizeof(TY) == 2) {
+      bf16x8_t o;
+      if (ACC) {
+        const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>(dst);
 #pragma unroll
-    for (int n = 0; n < VMAX; ++n) {
-      if (n < V) {
-        TY* dst = out + (n * BT + b) * XS + k;
-        if (ACC) {
-          dst[0] = (TY)((float)dst[0] + a0[n]);
-          dst[1] = (TY)((float)dst[1] + a1[n]);
-        } else {
-          dst[0] = (TY)a0[n];
-          dst[1] = (TY)a1[n];
-        }
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)prev[e] + acc[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (__bf16)acc[e];
       }
+      *reinterpret_cast<bf16x8_t*>(dst) = o;
+    } else {
+      f32x4 o0, o1;
+      if (ACC) {
+        o0 = *reinterpret_cast<const f32x4*>(dst);
+        o1 = *reinterpret_cast<const f32x4*>(dst + 4);
+      } else {
+        o0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        o1 = o0;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o0[e] += acc[e];
+        o1[e] += acc[e + 4];
+      }
+      *reinterpret_cast<f32x4*>(dst) = o0;
+      *reinterpret_cast<f32x4*>(dst + 4) = o1;
     }
   }
 }
@@ -112,6 +151,10 @@ F3_DEV void store_rows(const TY* L, void* dst, int V, int B, int b0, int t, int 
   }
 }
 
+// F3_TG_PROF: workgroup 0 records wall-clock stamps at the recurrence's phase boundaries
+#define F3_TG_STAMP(k) \
+  do { if (a.prof && blockIdx.x == 0 && threadIdx.x == 0) a.prof[t * 8 + (k)] = wall_clock64(); } while (0)
+
 constexpr int GRU_THREADS = 512;
 constexpr int GRU_WAVES = GRU_THREADS / 64;
 constexpr int NJ = (4 * VMAX + GRU_WAVES - 1) / GRU_WAVES;  // owned (node, 16-column tile) jobs per wave
@@ -119,19 +162,45 @@ constexpr int NJ = (4 * VMAX + GRU_WAVES - 1) / GRU_WAVES;  // owned (node, 16-c
 // ---------------------------------------------------------------------------------------------
 // Forward recurrence of one GRU layer (GRU.py:17-27 over TRAGCN.py:162-164's time loop).
 // ---------------------------------------------------------------------------------------------
+// Gate / update GEMM jobs of the forward recurrence. A job = (node n, 16-column tile j): the gate
+// job computes the z and r column tiles of both EmbGCN products (4 MFMA tiles), the update job the
+// candidate tile (2 MFMA tiles). Jobs are dealt round-robin over the 8 waves, so a wave's jobs all
+// share j = wave % 4: the Linear (static-branch) weight tiles are the same for every job of a wave
+// and stay in registers for the whole kernel; only the node weights W_n stream from L2. bf16: the
+// K = IP reduction is 4 MFMA steps; all of a job's W_n fragments are loaded before its first MFMA,
+// and job jj+1's fragments are issued before job jj computes and stores (vmcnt counts loads and
+// stores in issue order, so a job never waits on the previous job's epilogue stores). fp32
+// (parity mode): a plain k loop.
+template <bool B16>
+struct GateJob {  // node weights of the z and r column tiles (the shared Linear tiles stay resident)
+  static constexpr int NW = B16 ? 2 * (IP / 32) : 1;
+  typename std::conditional<B16, bf16x8_t, float>::type w[NW];
+  float bv[2];
+};
+template <bool B16>
+struct UpdJob {
+  static constexpr int NW = B16 ? IP / 32 : 1;
+  typename std::conditional<B16, bf16x8_t, float>::type w[NW];
+  float bv;
+};
+
 template <bool B16>
 __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
   using TT = typename Op<B16>::T;
   constexpr int BT = Op<B16>::BTF, XS = Op<B16>::XS, KS = Op<B16>::KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int V = a.V, Din = a.Din, I = a.I;
-  TT* X = reinterpret_cast<TT*>(smem);
-  TT* Y = X + V * BT * XS;
-  float* Sl = reinterpret_cast<float*>(Y + V * BT * XS);
+  TT* X = reinterpret_cast<TT*>(smem);           // [V][BT][XS] EmbGCN input [x, h] / [x, r*h]
+  TT* Y = X + V * BT * XS;                       // [V][BT][XS] S . input
+  float* Hs = reinterpret_cast<float*>(Y + V * BT * XS);  // [V][BT][H] hidden state h (fp32)
+  float* Zs = Hs + V * BT * H;                   // [V][BT][H] update gate z of this step
+  float* Rs = Zs + V * BT * H;                   // [V][BT][H] reset gate r of this step
+  float* Sl = Rs + V * BT * H;
   float* csl = Sl + V * V;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b0 = blockIdx.x * BT;
   for (int i = tid; i < 2 * V * BT * XS; i += GRU_THREADS) X[i] = (TT)0.f;
+  for (int i = tid; i < 3 * V * BT * H; i += GRU_THREADS) Hs[i] = 0.f;  // h0 = 0 (TRAGCN.py:171-175)
   for (int i = tid; i < V * V; i += GRU_THREADS) Sl[i] = a.S[i];
   for (int i = tid; i < V; i += GRU_THREADS) csl[i] = a.cs[i];
   const int col = lane & 15, rq = lane >> 4;
@@ -143,137 +212,225 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
   const TT* gLf = reinterpret_cast<const TT*>(a.g.Lf);
   const TT* uWf = reinterpret_cast<const TT*>(a.u.Wf);
   const TT* uLf = reinterpret_cast<const TT*>(a.u.Lf);
-  float hreg[NJ][4], zreg[NJ][4], rreg[NJ][4];
+
+  static_assert(GRU_WAVES % 4 == 0, "a wave's jobs share one column tile");
+  const int jw = wave & 3, cw = 16 * jw + col;  // this wave's column tile / this lane's column
+  // resident Linear tiles (gate z / r, update) and the Linear biases of this lane's column
+  typename std::conditional<B16, bf16x8_t, float>::type lgz[B16 ? IP / 32 : 1], lgr[B16 ? IP / 32 : 1],
+      lup[B16 ? IP / 32 : 1];
+  if constexpr (B16) {
 #pragma unroll
-  for (int jj = 0; jj < NJ; ++jj)
+    for (int ks = 0; ks < IP / 32; ++ks) {
+      lgz[ks] = ld8(gLf + (size_t)cw * IP + kofs + 32 * ks);
+      lgr[ks] = ld8(gLf + (size_t)(H + cw) * IP + kofs + 32 * ks);
+      lup[ks] = ld8(uLf + (size_t)cw * IP + kofs + 32 * ks);
+    }
+  }
+  const float blz = a.g.bl[cw], blr = a.g.bl[H + cw], blu = a.u.bl[cw];
+
+  auto gate_load = [&](int jj, GateJob<B16>& J) {
+    int q = wave + GRU_WAVES * jj;
+    asm volatile("" : "+s"(q));
+    if (q < njobs) {
+      const int n = q >> 2;
+      if constexpr (B16) {
+        const TT* wz = gWf + ((size_t)n * 2 * H + cw) * IP + kofs;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) hreg[jj][r] = zreg[jj][r] = rreg[jj][r] = 0.f;
+        for (int ks = 0; ks < IP / 32; ++ks) {
+          J.w[ks] = ld8(wz + 32 * ks);
+          J.w[IP / 32 + ks] = ld8(wz + (size_t)H * IP + 32 * ks);
+        }
+      }
+      J.bv[0] = a.g.bn[n * 2 * H + cw];
+      J.bv[1] = a.g.bn[n * 2 * H + H + cw];
+    }
+  };
+  // zr = sigmoid(S.x W_n + b_n + silu(cs*x Lin^T + b))   (EmbGCN.py:78-89, GRU.py:22)
+  auto gate_compute = [&](int jj, const GateJob<B16>& J, int t) {
+    int q = wave + GRU_WAVES * jj;
+    asm volatile("" : "+s"(q));
+    if (q >= njobs) return;
+    const int n = q >> 2;
+    f32x4 gz = {0.f, 0.f, 0.f, 0.f}, gr = gz, sz = gz, sr = gz;
+    const TT* ay = Y + (n * BT + arow) * XS + kofs;
+    const TT* ax = X + (n * BT + arow) * XS + kofs;
+    if constexpr (B16) {
+#pragma unroll
+      for (int ks = 0; ks < IP / 32; ++ks) {
+        const bf16x8_t ya = ld8(ay + 32 * ks), xa = ld8(ax + 32 * ks);
+        gz = mfma8(ya, J.w[ks], gz);
+        gr = mfma8(ya, J.w[IP / 32 + ks], gr);
+        sz = mfma8(xa, lgz[ks], sz);
+        sr = mfma8(xa, lgr[ks], sr);
+      }
+    } else {
+      const TT* wz = gWf + ((size_t)n * 2 * H + cw) * IP + kofs;
+      const TT* lz = gLf + (size_t)cw * IP + kofs;
+#pragma unroll 1
+      for (int ks = 0; ks < nks; ++ks) {
+        const int o = ks * KS;
+        gz = mma<B16>(ay + o, wz + o, gz);
+        gr = mma<B16>(ay + o, wz + (size_t)H * IP + o, gr);
+        sz = mma<B16>(ax + o, lz + o, sz);
+        sr = mma<B16>(ax + o, lz + (size_t)H * IP + o, sr);
+      }
+    }
+    const float csn = csl[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = rq * 4 + r;
+      if (b >= BT) continue;
+      const float s_z = sz[r] * csn + blz, s_r = sr[r] * csn + blr;
+      const float z = sigmoidf_(gz[r] + J.bv[0] + s_z * sigmoidf_(s_z));
+      const float rr = sigmoidf_(gr[r] + J.bv[1] + s_r * sigmoidf_(s_r));
+      Zs[(n * BT + b) * H + cw] = z;
+      Rs[(n * BT + b) * H + cw] = rr;
+      if (b0 + b < a.B) {
+        const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+        a.ZR[R * 2 * H + cw] = z;
+        a.ZR[R * 2 * H + H + cw] = rr;
+        a.SG[R * 2 * H + cw] = s_z;
+        a.SG[R * 2 * H + H + cw] = s_r;
+      }
+    }
+  };
+  auto upd_load = [&](int jj, UpdJob<B16>& J) {
+    int q = wave + GRU_WAVES * jj;
+    asm volatile("" : "+s"(q));
+    if (q < njobs) {
+      const int n = q >> 2;
+      if constexpr (B16) {
+        const TT* wu = uWf + ((size_t)n * H + cw) * IP + kofs;
+#pragma unroll
+        for (int ks = 0; ks < IP / 32; ++ks) J.w[ks] = ld8(wu + 32 * ks);
+      }
+      J.bv = a.u.bn[n * H + cw];
+    }
+  };
+  // hc = tanh(EmbGCN_u([x, r*h])); h = z*h + (1-z)*hc   (GRU.py:25-26)
+  auto upd_compute = [&](int jj, const UpdJob<B16>& J, int t) {
+    int q = wave + GRU_WAVES * jj;
+    asm volatile("" : "+s"(q));
+    if (q >= njobs) return;
+    const int n = q >> 2;
+    f32x4 gu = {0.f, 0.f, 0.f, 0.f}, su = gu;
+    const TT* ay = Y + (n * BT + arow) * XS + kofs;
+    const TT* ax = X + (n * BT + arow) * XS + kofs;
+    if constexpr (B16) {
+#pragma unroll
+      for (int ks = 0; ks < IP / 32; ++ks) {
+        gu = mfma8(ld8(ay + 32 * ks), J.w[ks], gu);
+        su = mfma8(ld8(ax + 32 * ks), lup[ks], su);
+      }
+    } else {
+      const TT* wu = uWf + ((size_t)n * H + cw) * IP + kofs;
+      const TT* lu = uLf + (size_t)cw * IP + kofs;
+#pragma unroll 1
+      for (int ks = 0; ks < nks; ++ks) {
+        const int o = ks * KS;
+        gu = mma<B16>(ay + o, wu + o, gu);
+        su = mma<B16>(ax + o, lu + o, su);
+      }
+    }
+    const float csn = csl[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = rq * 4 + r;
+      if (b >= BT) continue;
+      const float s = su[r] * csn + blu;
+      const float hc = tanhf(gu[r] + J.bv + s * sigmoidf_(s));
+      const float z = Zs[(n * BT + b) * H + cw];
+      float& hs = Hs[(n * BT + b) * H + cw];
+      const float h = z * hs + (1.f - z) * hc;
+      hs = h;
+      if (b0 + b < a.B) {
+        const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+        a.HC[R * H + cw] = hc;
+        a.SU[R * H + cw] = s;
+        a.Hout[R * H + cw] = h;
+      }
+    }
+  };
+
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    F3_TG_STAMP(0);
     // x_t -> X[., ., 0:Din], h -> X[., ., Din:Din+H]
-    for (int i = tid; i < BT * V * Din; i += GRU_THREADS) {
-      const int b = i / (V * Din), rem = i - b * V * Din, n = rem / Din, c = rem - n * Din;
-      const float v = (b0 + b < a.B) ? a.x[((size_t)(b0 + b) * T + t) * V * Din + rem] : 0.f;
-      X[(n * BT + b) * XS + c] = (TT)v;
-    }
+    if (Din % 4 == 0) {  // float4 loads, several in flight per thread
+#pragma unroll 4
+      for (int i = tid; i < BT * V * (Din / 4); i += GRU_THREADS) {
+        const int b = i / (V * (Din / 4)), rem = i - b * V * (Din / 4), n = rem / (Din / 4), c = (rem - n * (Din / 4)) * 4;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (b0 + b < a.B) v = *reinterpret_cast<const f32x4*>(a.x + ((size_t)(b0 + b) * T + t) * V * Din + rem * 4);
+        TT* d = X + (n * BT + b) * XS + c;
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      int q = wave + GRU_WAVES * jj;
-      asm volatile("" : "+s"(q));  // per step: keep job addresses and biases out of loop-invariant registers
-      if (q < njobs) {
-        const int n = q >> 2, j = q & 3;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = rq * 4 + r;
-          if (b < BT) X[(n * BT + b) * XS + Din + 16 * j + col] = (TT)hreg[jj][r];
-        }
+        for (int e = 0; e < 4; ++e) d[e] = (TT)v[e];
+      }
+    } else {
+#pragma unroll 4
+      for (int i = tid; i < BT * V * Din; i += GRU_THREADS) {
+        const int b = i / (V * Din), rem = i - b * V * Din, n = rem / Din, c = rem - n * Din;
+        const float v = (b0 + b < a.B) ? a.x[((size_t)(b0 + b) * T + t) * V * Din + rem] : 0.f;
+        X[(n * BT + b) * XS + c] = (TT)v;
       }
     }
+    for (int i = tid; i < V * BT * (H / 4); i += GRU_THREADS) {
+      const int row = i / (H / 4), c = (i - row * (H / 4)) * 4;
+      const f32x4 h = *reinterpret_cast<const f32x4*>(Hs + row * H + c);
+      TT* d = X + row * XS + Din + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = (TT)h[e];
+    }
     __syncthreads();
+    F3_TG_STAMP(1);
     node_mix<TT, BT, XS, false, false, GRU_THREADS>(X, Y, Sl, V, I, tid);
     __syncthreads();
+    F3_TG_STAMP(2);
     store_rows<TT, BT, XS, GRU_THREADS>(X, a.XI, V, a.B, b0, t, tid);
     store_rows<TT, BT, XS, GRU_THREADS>(Y, a.XG, V, a.B, b0, t, tid);
-    // gate: zr = sigmoid(S.x W_n + b_n + silu(cs*x Lin^T + b))   (EmbGCN.py:78-89, GRU.py:22)
+    F3_TG_STAMP(7);
+    {
+      GateJob<B16> JA, JB;
+      gate_load(0, JA);
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      int q = wave + GRU_WAVES * jj;
-      asm volatile("" : "+s"(q));  // per step: keep job addresses and biases out of loop-invariant registers
-      if (q < njobs) {
-        const int n = q >> 2, j = q & 3, cz = 16 * j + col;
-        f32x4 gz = {0.f, 0.f, 0.f, 0.f}, gr = gz, sz = gz, sr = gz;
-        const TT* ay = Y + (n * BT + arow) * XS + kofs;
-        const TT* ax = X + (n * BT + arow) * XS + kofs;
-        const TT* wz = gWf + ((size_t)n * 2 * H + cz) * IP + kofs;
-        const TT* wr = wz + (size_t)H * IP;
-        const TT* lz = gLf + (size_t)cz * IP + kofs;
-        const TT* lr = lz + (size_t)H * IP;
-#pragma unroll 1
-        for (int ks = 0; ks < nks; ++ks) {
-          const int o = ks * KS;
-          gz = mma<B16>(ay + o, wz + o, gz);
-          gr = mma<B16>(ay + o, wr + o, gr);
-          sz = mma<B16>(ax + o, lz + o, sz);
-          sr = mma<B16>(ax + o, lr + o, sr);
-        }
-        const float csn = csl[n];
-        const float bnz = a.g.bn[n * 2 * H + cz], bnr = a.g.bn[n * 2 * H + H + cz];
-        const float blz = a.g.bl[cz], blr = a.g.bl[H + cz];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = rq * 4 + r;
-          const float s_z = sz[r] * csn + blz, s_r = sr[r] * csn + blr;
-          const float z = sigmoidf_(gz[r] + bnz + s_z * sigmoidf_(s_z));
-          const float rr = sigmoidf_(gr[r] + bnr + s_r * sigmoidf_(s_r));
-          zreg[jj][r] = z;
-          rreg[jj][r] = rr;
-          if (b < BT && b0 + b < a.B) {
-            const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-            a.ZR[R * 2 * H + cz] = z;
-            a.ZR[R * 2 * H + H + cz] = rr;
-            a.SG[R * 2 * H + cz] = s_z;
-            a.SG[R * 2 * H + H + cz] = s_r;
-          }
-        }
+      for (int jj = 0; jj < NJ; jj += 2) {
+        if (jj + 1 < NJ) gate_load(jj + 1, JB);
+        gate_compute(jj, JA, t);
+        if (jj + 2 < NJ) gate_load(jj + 2, JA);
+        if (jj + 1 < NJ) gate_compute(jj + 1, JB, t);
       }
     }
     __syncthreads();
+    F3_TG_STAMP(3);
     // candidate input [x, r*h] (GRU.py:24)
+    for (int i = tid; i < V * BT * (H / 4); i += GRU_THREADS) {
+      const int row = i / (H / 4), c = (i - row * (H / 4)) * 4;
+      const f32x4 h = *reinterpret_cast<const f32x4*>(Hs + row * H + c);
+      const f32x4 r = *reinterpret_cast<const f32x4*>(Rs + row * H + c);
+      TT* d = X + row * XS + Din + c;
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      int q = wave + GRU_WAVES * jj;
-      asm volatile("" : "+s"(q));  // per step: keep job addresses and biases out of loop-invariant registers
-      if (q < njobs) {
-        const int n = q >> 2, j = q & 3;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = rq * 4 + r;
-          if (b < BT) X[(n * BT + b) * XS + Din + 16 * j + col] = (TT)(rreg[jj][r] * hreg[jj][r]);
-        }
-      }
+      for (int e = 0; e < 4; ++e) d[e] = (TT)(r[e] * h[e]);
     }
     __syncthreads();
+    F3_TG_STAMP(4);
     node_mix<TT, BT, XS, false, false, GRU_THREADS>(X, Y, Sl, V, I, tid);
     __syncthreads();
+    F3_TG_STAMP(5);
     store_rows<TT, BT, XS, GRU_THREADS>(X, a.UI, V, a.B, b0, t, tid);
     store_rows<TT, BT, XS, GRU_THREADS>(Y, a.UG, V, a.B, b0, t, tid);
-    // update: hc = tanh(EmbGCN_u([x, r*h])); h = z*h + (1-z)*hc   (GRU.py:25-26)
+    {
+      UpdJob<B16> JA, JB;
+      upd_load(0, JA);
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      int q = wave + GRU_WAVES * jj;
-      asm volatile("" : "+s"(q));  // per step: keep job addresses and biases out of loop-invariant registers
-      if (q < njobs) {
-        const int n = q >> 2, j = q & 3, c = 16 * j + col;
-        f32x4 gu = {0.f, 0.f, 0.f, 0.f}, su = gu;
-        const TT* ay = Y + (n * BT + arow) * XS + kofs;
-        const TT* ax = X + (n * BT + arow) * XS + kofs;
-        const TT* wu = uWf + ((size_t)n * H + c) * IP + kofs;
-        const TT* lu = uLf + (size_t)c * IP + kofs;
-#pragma unroll 1
-        for (int ks = 0; ks < nks; ++ks) {
-          const int o = ks * KS;
-          gu = mma<B16>(ay + o, wu + o, gu);
-          su = mma<B16>(ax + o, lu + o, su);
-        }
-        const float csn = csl[n], bnu = a.u.bn[n * H + c], blu = a.u.bl[c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = rq * 4 + r;
-          const float s = su[r] * csn + blu;
-          const float hc = tanhf(gu[r] + bnu + s * sigmoidf_(s));
-          const float z = zreg[jj][r];
-          const float h = z * hreg[jj][r] + (1.f - z) * hc;
-          hreg[jj][r] = h;
-          if (b < BT && b0 + b < a.B) {
-            const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-            a.HC[R * H + c] = hc;
-            a.SU[R * H + c] = s;
-            a.Hout[R * H + c] = h;
-          }
-        }
+      for (int jj = 0; jj < NJ; jj += 2) {
+        if (jj + 1 < NJ) upd_load(jj + 1, JB);
+        upd_compute(jj, JA, t);
+        if (jj + 2 < NJ) upd_load(jj + 2, JA);
+        if (jj + 1 < NJ) upd_compute(jj + 1, JB, t);
       }
     }
     __syncthreads();
+    F3_TG_STAMP(6);
   }
 }
 
@@ -303,7 +460,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
   const int arow = (lane & 15) % BT;
   const int kofs = B16 ? 8 * (lane >> 4) : (lane >> 4);
   const int njobs = 4 * V;
-  const int nit = (I + 15) / 16;
+  const int nit2 = (I + 31) / 32;  // jobs of two 16-column input tiles
   const bool has_dx = a.dX != nullptr && Din == H;
   const TT* gWb = reinterpret_cast<const TT*>(a.g.Wb);
   const TT* gLb = reinterpret_cast<const TT*>(a.g.Lb);
@@ -355,25 +512,51 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
     }
     __syncthreads();
     // update EmbGCN input gradient: GX = dU . W_n^T, DX = (cs dSu) . Lin
-    for (int q = wave; q < V * nit; q += GRU_WAVES) {
-      const int n = q / nit, i = 16 * (q - n * nit) + col;
-      f32x4 gx = {0.f, 0.f, 0.f, 0.f}, sx = gx;
+    for (int q = wave; q < V * nit2; q += GRU_WAVES) {
+      const int n = q / nit2, i0 = 32 * (q - n * nit2) + col, i1 = i0 + 16;
+      f32x4 gx0 = {0.f, 0.f, 0.f, 0.f}, gx1 = gx0, sx0 = gx0, sx1 = gx0;
       const TT* aa = AG + (n * BT + arow) * XS + kofs;
       const TT* as = AS + (n * BT + arow) * XS + kofs;
-      const TT* wb = uWb + ((size_t)n * IP + i) * H + kofs;
-      const TT* lb = uLb + (size_t)i * H + kofs;
+      const TT* wb0 = uWb + ((size_t)n * IP + i0) * H + kofs;
+      const TT* wb1 = uWb + ((size_t)n * IP + i1) * H + kofs;
+      const TT* lb0 = uLb + (size_t)i0 * H + kofs;
+      const TT* lb1 = uLb + (size_t)i1 * H + kofs;
+      if constexpr (B16) {  // all weight fragments of the job in flight before the first MFMA
+        constexpr int NK = (H) / 32;
+        bf16x8_t w0[NK], w1[NK], l0[NK], l1[NK];
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+          w0[ks] = ld8(wb0 + 32 * ks);
+          w1[ks] = ld8(wb1 + 32 * ks);
+          l0[ks] = ld8(lb0 + 32 * ks);
+          l1[ks] = ld8(lb1 + 32 * ks);
+        }
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+          const bf16x8_t ga = ld8(aa + 32 * ks), sa = ld8(as + 32 * ks);
+          gx0 = mfma8(ga, w0[ks], gx0);
+          gx1 = mfma8(ga, w1[ks], gx1);
+          sx0 = mfma8(sa, l0[ks], sx0);
+          sx1 = mfma8(sa, l1[ks], sx1);
+        }
+      } else {
 #pragma unroll 1
-      for (int ks = 0; ks < H / KS; ++ks) {
-        const int o = ks * KS;
-        gx = mma<B16>(aa + o, wb + o, gx);
-        sx = mma<B16>(as + o, lb + o, sx);
+        for (int ks = 0; ks < (H) / KS; ++ks) {
+          const int o = ks * KS;
+          gx0 = mma<B16>(aa + o, wb0 + o, gx0);
+          gx1 = mma<B16>(aa + o, wb1 + o, gx1);
+          sx0 = mma<B16>(as + o, lb0 + o, sx0);
+          sx1 = mma<B16>(as + o, lb1 + o, sx1);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rq * 4 + r;
         if (b < BT) {
-          GX[(n * BT + b) * XS + i] = (TT)gx[r];
-          DX[(n * BT + b) * XS + i] = (TT)sx[r];
+          GX[(n * BT + b) * XS + i0] = (TT)gx0[r];
+          DX[(n * BT + b) * XS + i0] = (TT)sx0[r];
+          GX[(n * BT + b) * XS + i1] = (TT)gx1[r];
+          DX[(n * BT + b) * XS + i1] = (TT)sx1[r];
         }
       }
     }
@@ -420,25 +603,51 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
     }
     __syncthreads();
     // gate EmbGCN input gradient (K = 2H)
-    for (int q = wave; q < V * nit; q += GRU_WAVES) {
-      const int n = q / nit, i = 16 * (q - n * nit) + col;
-      f32x4 gx = {0.f, 0.f, 0.f, 0.f}, sx = gx;
+    for (int q = wave; q < V * nit2; q += GRU_WAVES) {
+      const int n = q / nit2, i0 = 32 * (q - n * nit2) + col, i1 = i0 + 16;
+      f32x4 gx0 = {0.f, 0.f, 0.f, 0.f}, gx1 = gx0, sx0 = gx0, sx1 = gx0;
       const TT* aa = AG + (n * BT + arow) * XS + kofs;
       const TT* as = AS + (n * BT + arow) * XS + kofs;
-      const TT* wb = gWb + ((size_t)n * IP + i) * 2 * H + kofs;
-      const TT* lb = gLb + (size_t)i * 2 * H + kofs;
+      const TT* wb0 = gWb + ((size_t)n * IP + i0) * 2 * H + kofs;
+      const TT* wb1 = gWb + ((size_t)n * IP + i1) * 2 * H + kofs;
+      const TT* lb0 = gLb + (size_t)i0 * 2 * H + kofs;
+      const TT* lb1 = gLb + (size_t)i1 * 2 * H + kofs;
+      if constexpr (B16) {  // all weight fragments of the job in flight before the first MFMA
+        constexpr int NK = (2 * H) / 32;
+        bf16x8_t w0[NK], w1[NK], l0[NK], l1[NK];
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+          w0[ks] = ld8(wb0 + 32 * ks);
+          w1[ks] = ld8(wb1 + 32 * ks);
+          l0[ks] = ld8(lb0 + 32 * ks);
+          l1[ks] = ld8(lb1 + 32 * ks);
+        }
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+          const bf16x8_t ga = ld8(aa + 32 * ks), sa = ld8(as + 32 * ks);
+          gx0 = mfma8(ga, w0[ks], gx0);
+          gx1 = mfma8(ga, w1[ks], gx1);
+          sx0 = mfma8(sa, l0[ks], sx0);
+          sx1 = mfma8(sa, l1[ks], sx1);
+        }
+      } else {
 #pragma unroll 1
-      for (int ks = 0; ks < 2 * H / KS; ++ks) {
-        const int o = ks * KS;
-        gx = mma<B16>(aa + o, wb + o, gx);
-        sx = mma<B16>(as + o, lb + o, sx);
+        for (int ks = 0; ks < (2 * H) / KS; ++ks) {
+          const int o = ks * KS;
+          gx0 = mma<B16>(aa + o, wb0 + o, gx0);
+          gx1 = mma<B16>(aa + o, wb1 + o, gx1);
+          sx0 = mma<B16>(as + o, lb0 + o, sx0);
+          sx1 = mma<B16>(as + o, lb1 + o, sx1);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rq * 4 + r;
         if (b < BT) {
-          GX[(n * BT + b) * XS + i] = (TT)gx[r];
-          DX[(n * BT + b) * XS + i] = (TT)sx[r];
+          GX[(n * BT + b) * XS + i0] = (TT)gx0[r];
+          DX[(n * BT + b) * XS + i0] = (TT)sx0[r];
+          GX[(n * BT + b) * XS + i1] = (TT)gx1[r];
+          DX[(n * BT + b) * XS + i1] = (TT)sx1[r];
         }
       }
     }
@@ -492,27 +701,27 @@ __global__ __launch_bounds__(256) void tg_supports_kernel(const float* __restric
     for (int m = 0; m < V; ++m) s += expf(Z[n * V + m] - mx);
     for (int m = 0; m < V; ++m) S[n * V + m] = expf(Z[n * V + m] - mx) / s + (m == n ? 1.f : 0.f);
   }
-  if (tid == 0) {  // static adjacency with adj = ones (TRAGCN.py:191)
+  // static adjacency with adj = ones (TRAGCN.py:191): softmax(dim=1) at init, softmax(dim=-1)
+  // in forward (one row per thread), then column sums
+  __shared__ float M[VMAX * VMAX];
+  if (tid < V) {
+    const int n = tid;
     const double dgn = 1.0 / ((double)V + 0.5), sq = sqrt(dgn);
-    float M[VMAX * VMAX];
-    for (int n = 0; n < V; ++n)
-      for (int m = 0; m < V; ++m) M[n * V + m] = (float)(sq * ((n == m ? 1.5 : 1.0) * sq));
-    for (int pass = 0; pass < 2; ++pass)  // softmax(dim=1) at init, softmax(dim=-1) in forward
-      for (int n = 0; n < V; ++n) {
-        float mx = -INFINITY, s = 0.f;
-        for (int m = 0; m < V; ++m) mx = fmaxf(mx, M[n * V + m]);
-        for (int m = 0; m < V; ++m) s += expf(M[n * V + m] - mx);
-        for (int m = 0; m < V; ++m) M[n * V + m] = expf(M[n * V + m] - mx) / s;
-      }
-    for (int m = 0; m < V; ++m) {
-      float s = 0.f;
-      for (int n = 0; n < V; ++n) s += M[n * V + m];
-      cs[m] = s;
+    for (int m = 0; m < V; ++m) M[n * V + m] = (float)(sq * ((n == m ? 1.5 : 1.0) * sq));
+    for (int pass = 0; pass < 2; ++pass) {
+      float mx = -INFINITY, s = 0.f;
+      for (int m = 0; m < V; ++m) mx = fmaxf(mx, M[n * V + m]);
+      for (int m = 0; m < V; ++m) s += expf(M[n * V + m] - mx);
+      for (int m = 0; m < V; ++m) M[n * V + m] = expf(M[n * V + m] - mx) / s;
     }
   }
+  __syncthreads();
+  if (tid < V) {
+    float s = 0.f;
+    for (int n = 0; n < V; ++n) s += M[n * V + tid];
+    cs[tid] = s;
+  }
 }
-
-
 
 // one thread per (n, i, o) of W_n (i < IP, zero padding for i >= I), plus the linear packs
 template <bool B16>
@@ -1188,7 +1397,7 @@ template <bool B16>
 int gru_lds(int V, bool bwd) {
   using TT = typename Op<B16>::T;
   const int bt = bwd ? Op<B16>::BTB : Op<B16>::BTF;
-  return (bwd ? 4 : 2) * V * bt * Op<B16>::XS * (int)sizeof(TT) + (V * V + V) * 4;
+  return (bwd ? 4 : 2) * V * bt * Op<B16>::XS * (int)sizeof(TT) + (bwd ? 0 : 3 * V * bt * H * 4) + (V * V + V) * 4;
 }
 }  // namespace
 

@@ -301,7 +301,23 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     g.Hout = at<float>(ws, p.H[l]); g.ZR = at<float>(ws, p.ZR[l]); g.SG = at<float>(ws, p.SG[l]);
     g.HC = at<float>(ws, p.HC[l]); g.SU = at<float>(ws, p.SU[l]);
     g.XG = at<void>(ws, p.XG[l]); g.XI = at<void>(ws, p.XI[l]); g.UG = at<void>(ws, p.UG[l]); g.UI = at<void>(ws, p.UI[l]);
+    static long long* prof = nullptr;
+    if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
+    g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
     TG_TRY(f3_tg_gru_fwd(&g, b16, s));
+    if (g.prof) {  // debugging aid: per-phase microseconds of workgroup 0, averaged over the steps
+      long long h[T * 8];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost);
+      double ph[8] = {0};
+      // stamps: 0 step start, 1 fill, 2 mix, 7 row stores, 3 gate, 4 r*h, 5 mix, 6 update
+      const int ord[8] = {0, 1, 2, 7, 3, 4, 5, 6};
+      for (int t = 0; t < T; ++t)
+        for (int k = 1; k < 8; ++k) ph[k] += (h[t * 8 + ord[k]] - h[t * 8 + ord[k - 1]]) * 0.01 / T;  // 100 MHz
+      fprintf(stderr, "gru_fwd layer %d per-step phases (us) fill/mix/stores/gate/rh/mix/stores+update:", l);
+      for (int k = 1; k < 8; ++k) fprintf(stderr, " %.2f", ph[k]);
+      fprintf(stderr, "\n");
+    }
   }
   for (int l = 0; l < 2; ++l) {  // transformer_layer (TA.py:101-108)
     TaArgs a = ta_args(net, l, B, params);
