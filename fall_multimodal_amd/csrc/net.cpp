@@ -119,16 +119,17 @@ struct f3_net {
     entries.push_back(e);
     return (int)entries.size() - 1;
   }
-  void finalize_offsets() {
+  void finalize_offsets() {  // phase-1 parameters first; every entry 16-B aligned (float4 RMSprop)
     int64_t off = 0;
     for (int ph = 1; ph <= 2; ++ph) {
       for (auto& e : entries)
         if (e.kind == F3_ENTRY_PARAM && e.phase == ph) {
           e.offset = off;
-          off += e.numel;
+          off += (e.numel + 3) / 4 * 4;
         }
       if (ph == 1) nparam_phase1 = off;
     }
+    nparam = off;  // includes the alignment padding (zero gradients, RMSprop leaves it at 0)
   }
   BnIdx add_bn(const std::string& p, int C) {
     BnIdx b;
@@ -1145,12 +1146,10 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     // main queues should already hold their next layer by then. F3_SIDE_LAG=0: same layer.
     static const int lag = getenv("F3_SIDE_LAG") ? atoi(getenv("F3_SIDE_LAG")) : 1;
     const bool defer = lag && br.side() != br.s;
-    // F3_TAIL_SIDE=0 runs the first layer's weight gradients on the stream's own queue (idle
-    // after its input gradient) instead of the side queues: measured neutral to 1 % slower
-    // (6.50-6.57 vs 6.49-6.56 ms), so the side queues stay the default.
-    static const bool tail_side = !getenv("F3_TAIL_SIDE") || atoi(getenv("F3_TAIL_SIDE")) != 0;
-    // (only with the slab wgrad: the atomic form's unpack launch runs on the side queue)
-    auto side_of = [&](int si, int l) { return l == 0 && !tail_side && wgrad_slab() ? br.at(si) : br.side(si); };
+    // Every layer's weight gradients run on the side queues. (A former F3_TAIL_SIDE=0 option ran
+    // layer 0's on the stream's own queue: measured neutral to 1 % slower, and it raced with the
+    // side queue's layer-1 launch on the stream's shared split-K slab, so it is gone.)
+    auto side_of = [&](int si, int) { return br.side(si); };
     for (int l = l_hi; l >= l_lo; --l) {
       for (int si = 0; si < net->nstreams; ++si) {
         F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], side_of(si, l), l_hi,

@@ -68,6 +68,7 @@ struct GruBwdArgs {
   void* DSU;          // [R][H]
   void* DXG;          // [R][IP] d(mixed gate input)
   void* DUG;          // [R][IP] d(mixed update input)
+  long long* prof;    // optional phase stamps (F3_TG_PROF), [T][8]
 };
 
 struct TaArgs {

@@ -37,7 +37,8 @@ struct Op<true> {
                                       // time of a workgroup is set by its weight stream, not its row
                                       // count, and fewer clips per workgroup spread the per-step
                                       // stores over more CUs (64 workgroups at B = 256)
-  static constexpr int BTB = 4;       // backward (four [node][clip][k] buffers in LDS)
+  static constexpr int BTB = 3;       // backward (four [node][clip][k] buffers + the step's staged
+                                      // fp32 inputs in LDS)
 };
 template <>
 struct Op<false> {
@@ -45,7 +46,7 @@ struct Op<false> {
   static constexpr int KS = 4;        // v_mfma_f32_16x16x4_f32 (exact fp32 products)
   static constexpr int XS = IP + 4;
   static constexpr int BTF = 4;
-  static constexpr int BTB = 4;
+  static constexpr int BTB = 1;
 };
 
 template <bool B16>
@@ -146,8 +147,9 @@ F3_DEV void store_rows(const TY* L, void* dst, int V, int B, int b0, int t, int 
     const int n = row / BT, b = row - n * BT;
     if (b0 + b >= B) continue;
     const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(L + row * XS) + ch * 16);
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + R * IP * sizeof(TY) + ch * 16) = v;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(L + row * XS) + ch * 16);
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(reinterpret_cast<char*>(dst) + R * IP * sizeof(TY) + ch * 16));
   }
 }
 
@@ -287,10 +289,10 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
       Rs[(n * BT + b) * H + cw] = rr;
       if (b0 + b < a.B) {
         const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-        a.ZR[R * 2 * H + cw] = z;
-        a.ZR[R * 2 * H + H + cw] = rr;
-        a.SG[R * 2 * H + cw] = s_z;
-        a.SG[R * 2 * H + H + cw] = s_r;
+        __builtin_nontemporal_store(z, &a.ZR[R * 2 * H + cw]);
+        __builtin_nontemporal_store(rr, &a.ZR[R * 2 * H + H + cw]);
+        __builtin_nontemporal_store(s_z, &a.SG[R * 2 * H + cw]);
+        __builtin_nontemporal_store(s_r, &a.SG[R * 2 * H + H + cw]);
       }
     }
   };
@@ -345,9 +347,9 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
       hs = h;
       if (b0 + b < a.B) {
         const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-        a.HC[R * H + cw] = hc;
-        a.SU[R * H + cw] = s;
-        a.Hout[R * H + cw] = h;
+        __builtin_nontemporal_store(hc, &a.HC[R * H + cw]);
+        __builtin_nontemporal_store(s, &a.SU[R * H + cw]);
+        __builtin_nontemporal_store(h, &a.Hout[R * H + cw]);
       }
     }
   };
@@ -449,7 +451,10 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
   TT* AS = AG + V * BT * XS;              // cs * d static pre-activation (static A operand)
   TT* GX = AS + V * BT * XS;              // d mixed input (unmixed gconv input gradient)
   TT* DX = GX + V * BT * XS;              // d input = static part + S^T . GX
-  float* Sl = reinterpret_cast<float*>(DX + V * BT * XS);
+  // [7][V*BT][H] fp32: slots 0-4 this step's staged inputs (z; hc / r; su / s_z; h_{t-1}; dH / s_r),
+  // 5 dz, 6 the update path's x gradient
+  float* ST = reinterpret_cast<float*>(DX + V * BT * XS);
+  float* Sl = ST + 7 * V * BT * H;
   float* csl = Sl + V * V;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b0 = blockIdx.x * BT;
@@ -470,13 +475,52 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
   TT* DSG = reinterpret_cast<TT*>(a.DSG);
   TT* DU = reinterpret_cast<TT*>(a.DU);
   TT* DSU = reinterpret_cast<TT*>(a.DSU);
-  float dh[NJ][4], dz[NJ][4], dxr[NJ][4];
+  float dh[NJ][4];
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dh[jj][r] = dz[jj][r] = dxr[jj][r] = 0.f;
+    for (int r = 0; r < 4; ++r) dh[jj][r] = 0.f;
+  // Stage up to 5 per-row 64-float slices of this step's saved tensors into ST[slot] with every
+  // 16-B load issued before the first LDS write (one round trip per phase instead of one per job).
+  struct Src {
+    const float* p;
+    int ld, coff, tshift, slot;
+  };
+  auto stage = [&](const Src* src, int nsrc, int t) {
+    constexpr int MAXK = (5 * VMAX * BT * (H / 4) + GRU_THREADS - 1) / GRU_THREADS;
+    const int per = V * BT * (H / 4), total = nsrc * per;
+    f32x4 v[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+      const int i = tid + k * GRU_THREADS;
+      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < total) {
+        const int si = i / per, rem = i - si * per, row = rem / (H / 4), c4 = rem - row * (H / 4);
+        const int n = row / BT, b = row - n * BT, tt = t + src[si].tshift;
+        if (b0 + b < a.B && tt >= 0) {
+          const size_t R = ((size_t)(b0 + b) * T + tt) * V + n;
+          v[k] = *reinterpret_cast<const f32x4*>(src[si].p + R * src[si].ld + src[si].coff + 4 * c4);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+      const int i = tid + k * GRU_THREADS;
+      if (i < total) {
+        const int si = i / per, rem = i - si * per;
+        *reinterpret_cast<f32x4*>(ST + (size_t)src[si].slot * V * BT * H + rem * 4) = v[k];
+      }
+    }
+  };
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
+    F3_TG_STAMP(0);
+    {  // z, hc, su, h_{t-1}, dH of this step
+      const Src src[5] = {{a.ZR, 2 * H, 0, 0, 0}, {a.HC, H, 0, 0, 1}, {a.SU, H, 0, 0, 2}, {a.Hout, H, 0, -1, 3},
+                          {a.dH, H, 0, 0, 4}};
+      stage(src, 5, t);
+    }
+    __syncthreads();
     // h = z*hp + (1-z)*hc: dz, dhc -> dU (tanh), cs*dSu (silu)
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
@@ -491,17 +535,15 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
           float dU = 0.f, dsu = 0.f;
           if (b < BT && b0 + b < a.B) {
             const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-            const float g = dh[jj][r] + a.dH[R * H + c];
-            const float z = a.ZR[R * 2 * H + c], hc = a.HC[R * H + c], su = a.SU[R * H + c];
-            const float hp = t > 0 ? a.Hout[(R - V) * H + c] : 0.f;
-            dz[jj][r] = g * (hp - hc);
+            const int o = (n * BT + b) * H + c, sl = V * BT * H;
+            const float g = dh[jj][r] + ST[4 * sl + o];
+            const float z = ST[o], hc = ST[sl + o], su = ST[2 * sl + o], hp = ST[3 * sl + o];
+            ST[5 * sl + o] = g * (hp - hc);  // dz
             dU = g * (1.f - z) * (1.f - hc * hc);
             dsu = dU * silu_grad(su) * csn;
             dh[jj][r] = g * z;
-            DU[R * H + c] = (TT)dU;
-            DSU[R * H + c] = (TT)dsu;
-          } else {
-            dz[jj][r] = 0.f;
+            __builtin_nontemporal_store((TT)dU, &DU[R * H + c]);
+            __builtin_nontemporal_store((TT)dsu, &DSU[R * H + c]);
           }
           if (b < BT) {
             AG[(n * BT + b) * XS + c] = (TT)dU;
@@ -511,6 +553,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
       }
     }
     __syncthreads();
+    F3_TG_STAMP(1);
     // update EmbGCN input gradient: GX = dU . W_n^T, DX = (cs dSu) . Lin
     for (int q = wave; q < V * nit2; q += GRU_WAVES) {
       const int n = q / nit2, i0 = 32 * (q - n * nit2) + col, i1 = i0 + 16;
@@ -561,8 +604,15 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
       }
     }
     __syncthreads();
+    F3_TG_STAMP(2);
     node_mix<TT, BT, XS, true, true, GRU_THREADS>(GX, DX, Sl, V, I, tid);
     store_rows<TT, BT, XS, GRU_THREADS>(GX, a.DUG, V, a.B, b0, t, tid);
+    __syncthreads();
+    F3_TG_STAMP(3);
+    {  // r, gate static pre-activations (z and h_{t-1} stay staged)
+      const Src src[3] = {{a.ZR, 2 * H, H, 0, 1}, {a.SG, 2 * H, 0, 0, 2}, {a.SG, 2 * H, H, 0, 4}};
+      stage(src, 3, t);
+    }
     __syncthreads();
     // d(r*h) -> dr, dh; gate pre-activation gradients
 #pragma unroll
@@ -578,19 +628,19 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
           float dPz = 0.f, dPr = 0.f, dsz = 0.f, dsr = 0.f;
           if (b < BT && b0 + b < a.B) {
             const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+            const int o = (n * BT + b) * H + c, sl = V * BT * H;
             const float drh = (float)DX[(n * BT + b) * XS + Din + c];
-            const float z = a.ZR[R * 2 * H + c], rr = a.ZR[R * 2 * H + H + c];
-            const float hp = t > 0 ? a.Hout[(R - V) * H + c] : 0.f;
+            const float z = ST[o], rr = ST[sl + o], hp = ST[3 * sl + o];
             dh[jj][r] += drh * rr;
-            if (has_dx) dxr[jj][r] = (float)DX[(n * BT + b) * XS + c];
-            dPz = dz[jj][r] * z * (1.f - z);
+            if (has_dx) ST[6 * sl + o] = (float)DX[(n * BT + b) * XS + c];
+            dPz = ST[5 * sl + o] * z * (1.f - z);
             dPr = drh * hp * rr * (1.f - rr);
-            dsz = dPz * silu_grad(a.SG[R * 2 * H + c]) * csn;
-            dsr = dPr * silu_grad(a.SG[R * 2 * H + H + c]) * csn;
-            DP[R * 2 * H + c] = (TT)dPz;
-            DP[R * 2 * H + H + c] = (TT)dPr;
-            DSG[R * 2 * H + c] = (TT)dsz;
-            DSG[R * 2 * H + H + c] = (TT)dsr;
+            dsz = dPz * silu_grad(ST[2 * sl + o]) * csn;
+            dsr = dPr * silu_grad(ST[4 * sl + o]) * csn;
+            __builtin_nontemporal_store((TT)dPz, &DP[R * 2 * H + c]);
+            __builtin_nontemporal_store((TT)dPr, &DP[R * 2 * H + H + c]);
+            __builtin_nontemporal_store((TT)dsz, &DSG[R * 2 * H + c]);
+            __builtin_nontemporal_store((TT)dsr, &DSG[R * 2 * H + H + c]);
           }
           if (b < BT) {
             AG[(n * BT + b) * XS + c] = (TT)dPz;
@@ -602,6 +652,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
       }
     }
     __syncthreads();
+    F3_TG_STAMP(4);
     // gate EmbGCN input gradient (K = 2H)
     for (int q = wave; q < V * nit2; q += GRU_WAVES) {
       const int n = q / nit2, i0 = 32 * (q - n * nit2) + col, i1 = i0 + 16;
@@ -652,9 +703,11 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
       }
     }
     __syncthreads();
+    F3_TG_STAMP(5);
     node_mix<TT, BT, XS, true, true, GRU_THREADS>(GX, DX, Sl, V, I, tid);
     store_rows<TT, BT, XS, GRU_THREADS>(GX, a.DXG, V, a.B, b0, t, tid);
     __syncthreads();
+    F3_TG_STAMP(6);
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
       int q = wave + GRU_WAVES * jj;
@@ -668,7 +721,8 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
             dh[jj][r] += (float)DX[(n * BT + b) * XS + Din + c];
             if (has_dx) {
               const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
-              a.dX[R * H + c] = dxr[jj][r] + (float)DX[(n * BT + b) * XS + c];
+              __builtin_nontemporal_store(ST[6 * V * BT * H + (n * BT + b) * H + c] + (float)DX[(n * BT + b) * XS + c],
+                                          &a.dX[R * H + c]);
             }
           }
         }
@@ -1397,7 +1451,7 @@ template <bool B16>
 int gru_lds(int V, bool bwd) {
   using TT = typename Op<B16>::T;
   const int bt = bwd ? Op<B16>::BTB : Op<B16>::BTF;
-  return (bwd ? 4 : 2) * V * bt * Op<B16>::XS * (int)sizeof(TT) + (bwd ? 0 : 3 * V * bt * H * 4) + (V * V + V) * 4;
+  return (bwd ? 4 : 2) * V * bt * Op<B16>::XS * (int)sizeof(TT) + (bwd ? 7 : 3) * V * bt * H * 4 + (V * V + V) * 4;
 }
 }  // namespace
 

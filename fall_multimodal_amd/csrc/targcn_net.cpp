@@ -386,7 +386,21 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     g.dX = l == 1 ? at<float>(ws, p.dH0) : nullptr;
     g.DP = at<void>(ws, p.DP); g.DSG = at<void>(ws, p.DSG); g.DU = at<void>(ws, p.DU); g.DSU = at<void>(ws, p.DSU);
     g.DXG = at<void>(ws, p.DXG); g.DUG = at<void>(ws, p.DUG);
+    static long long* prof = nullptr;
+    if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
+    g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
     TG_TRY(f3_tg_gru_bwd(&g, b16, s));
+    if (g.prof) {
+      long long h[T * 8];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost);
+      double ph[8] = {0};
+      for (int t = 0; t < T; ++t)
+        for (int k = 1; k < 7; ++k) ph[k] += (h[t * 8 + k] - h[t * 8 + k - 1]) * 0.01 / T;
+      fprintf(stderr, "gru_bwd layer %d per-step phases (us) upd-epi/upd-gemm/mixT/gate-epi/gate-gemm/mixT:", l);
+      for (int k = 1; k < 7; ++k) fprintf(stderr, " %.2f", ph[k]);
+      fprintf(stderr, "\n");
+    }
     // per-node weight gradients over the B*T rows of each node (grouped GEMMs, one group per node)
     struct Job { size_t dy, x; int O; size_t dw, db; };
     const Job jobs[4] = {{p.DP, p.XG[l], 2 * H, p.dW[l][0][0], p.dW[l][0][1]},

@@ -62,9 +62,8 @@ def predict(model, loader):
     return torch.cat(outs), torch.cat(labs)
 
 
-@torch.no_grad()
-def valid(model, loader, loss_fn=None, top_k=(1, 5)):
-    """model/main.py:148-197: mean batch loss and top-k accuracy of the whole split."""
+def _eval_pass(model, loader, loss_fn=None):
+    """One eval-mode pass: concatenated outputs and labels, per-batch losses."""
     was_training = model.training
     model.eval()
     outs, labs, losses = [], [], []
@@ -76,16 +75,23 @@ def valid(model, loader, loss_fn=None, top_k=(1, 5)):
         labs.append(label)
     if was_training:
         model.train()
-    out, lab = torch.cat(outs), torch.cat(labs)
+    return torch.cat(outs), torch.cat(labs), losses
+
+
+@torch.no_grad()
+def valid(model, loader, loss_fn=None, top_k=(1, 5)):
+    """model/main.py:148-197: mean batch loss and top-k accuracy of the whole split."""
+    out, lab, losses = _eval_pass(model, loader, loss_fn)
     return {"loss": float(np.mean(losses)) if losses else None, "top_k": cal_top_k_accuracy(out, lab, top_k)}
 
 
 @torch.no_grad()
 def test(model, loader, loss_fn=None, top_k=(1, 5), num_classes: int | None = None):
-    """model/main.py:199-245 (+ main_cross_validation.py:247): valid() plus the per-class
-    metrics of argmax predictions against argmax labels."""
-    res = valid(model, loader, loss_fn, top_k)
-    out, lab = predict(model, loader)
+    """model/main.py:199-245 (+ main_cross_validation.py:247): loss, top-k and the per-class
+    metrics of argmax predictions against argmax labels, from ONE pass over the loader as the
+    reference's test() makes (a second pass would also draw an extra shuffle seed)."""
+    out, lab, losses = _eval_pass(model, loader, loss_fn)
+    res = {"loss": float(np.mean(losses)) if losses else None, "top_k": cal_top_k_accuracy(out, lab, top_k)}
     pred = out.argmax(1).cpu().numpy()
     true = (lab if lab.dim() == 1 else lab.argmax(1)).cpu().numpy()
     res.update(class_metrics(pred, true, num_classes or out.shape[1]))

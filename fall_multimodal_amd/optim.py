@@ -6,6 +6,8 @@ the sgd/adam/adamw branches delegate to torch.optim (PyTorch's own fused HIP ker
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from ._lib import check, lib, ptr, require_device, stream_handle
@@ -42,6 +44,54 @@ class RMSprop(torch.optim.Optimizer):
         return loss
 
 
+class CosineLRScheduler:
+    """timm.scheduler.CosineLRScheduler as the reference builds it (model/optimizer.py:31; timm is
+    not installed here, so its published schedule is restated): cycle_mul 1, decay_rate 1,
+    cycle_limit 1, k_decay 1, warmup_prefix False, no noise.
+      t <  warmup_t : lr = warmup_lr_init + t * (base_lr - warmup_lr_init) / warmup_t
+      t <  t_initial: lr = lr_min + (base_lr - lr_min) * (1 + cos(pi * t / t_initial)) / 2
+      otherwise     : lr = lr_min
+    The warm-up value is applied at construction (so epoch 0 trains at warmup_lr_init) and
+    step(epoch) sets the value for `epoch` (t_in_epochs; step_update(num_updates) otherwise)."""
+
+    def __init__(self, optimizer, t_initial, lr_min=0.0, t_in_epochs=True, warmup_t=0, warmup_lr_init=0.0):
+        self.optimizer = optimizer
+        self.t_initial, self.lr_min, self.t_in_epochs = t_initial, lr_min, t_in_epochs
+        self.warmup_t, self.warmup_lr_init = warmup_t, warmup_lr_init
+        for g in optimizer.param_groups:
+            g.setdefault("initial_lr", g["lr"])
+        self.base_values = [g["initial_lr"] for g in optimizer.param_groups]
+        self.warmup_steps = [(v - warmup_lr_init) / warmup_t for v in self.base_values] if warmup_t else []
+        if warmup_t:
+            self._set([warmup_lr_init] * len(self.base_values))
+
+    def _get_lr(self, t):
+        if t < self.warmup_t:
+            return [self.warmup_lr_init + t * s for s in self.warmup_steps]
+        if t < self.t_initial:
+            return [self.lr_min + 0.5 * (v - self.lr_min) * (1 + math.cos(math.pi * t / self.t_initial))
+                    for v in self.base_values]
+        return [self.lr_min for _ in self.base_values]
+
+    def _set(self, values):
+        for g, v in zip(self.optimizer.param_groups, values):
+            g["lr"] = v
+
+    def step(self, epoch, metric=None):
+        if self.t_in_epochs:
+            self._set(self._get_lr(epoch))
+
+    def step_update(self, num_updates, metric=None):
+        if not self.t_in_epochs:
+            self._set(self._get_lr(num_updates))
+
+    def state_dict(self):
+        return {k: v for k, v in self.__dict__.items() if k != "optimizer"}
+
+    def load_state_dict(self, state):
+        self.__dict__.update(state)
+
+
 def build_optimizer(model, config):
     t = config.OPTIM.TYPE
     if t == "rmsprop":
@@ -60,7 +110,7 @@ def build_optimizer(model, config):
     if config.LR_SCHEDULER.TYPE is None:
         return opt, None
     if config.LR_SCHEDULER.TYPE == "cosine":
-        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=config.LR_SCHEDULER.T_INITIAL,
-                                                           eta_min=config.LR_SCHEDULER.LR_MIN)
-        return opt, sched
+        c = config.LR_SCHEDULER
+        return opt, CosineLRScheduler(opt, t_initial=c.T_INITIAL, lr_min=c.LR_MIN, t_in_epochs=c.T_IN_EPOCHS,
+                                      warmup_t=c.WARMUP_T, warmup_lr_init=c.WARMUP_LR_INIT)
     raise RuntimeError(f"LR Scheduler type [{config.LR_SCHEDULER.TYPE}] is not implemented.")

@@ -54,10 +54,15 @@ class GradSync:
 
 
 class TrainStep:
-    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None):
+    """`optimizer` (optional, e.g. fall3 RMSprop driven by a CosineLRScheduler): its
+    param_groups[0] lr / alpha / eps are read at every step, so a scheduler's step(epoch) takes
+    effect as with the reference's optimizer.step() (model/main.py:127, 321-322)."""
+
+    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None, optimizer=None):
         self.model = model
         self.N = batch
         self.lr, self.alpha, self.eps = lr, alpha, eps
+        self.optimizer = optimizer
         dev = model.flat_parameters().device
         nat = model._native
         self.grads = torch.zeros(nat.nparam, dtype=torch.float32, device=dev)
@@ -76,6 +81,28 @@ class TrainStep:
         self._static = None
 
     # -- the pieces ------------------------------------------------------------
+    def prepare(self, skel, sensor, label):
+        """Validate a batch against the step's preallocated buffers (batch N, contiguous fp32 on the
+        device) and turn 1-D class-index labels into one-hot targets as model/main.py:104-109 does."""
+        m = self.model
+        m.check_inputs(skel, sensor)
+        for t, what in ((skel, "skel"), (sensor, "sensor")):
+            if t is None:
+                continue
+            if t.shape[0] != self.N:
+                raise ValueError(f"TrainStep was built for batch {self.N}, got {what} with batch {t.shape[0]}")
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"TrainStep: {what} must be contiguous fp32")
+        dev = m.flat_parameters().device
+        if label.dim() == 1:
+            label = torch.nn.functional.one_hot(label.to(dev).long(), num_classes=m.spec.num_class).float()
+        if tuple(label.shape) != (self.N, m.spec.num_class):
+            raise ValueError(f"TrainStep: label must be [{self.N},{m.spec.num_class}] (or [{self.N}] class indices), "
+                             f"got {tuple(label.shape)}")
+        if label.device != dev or label.dtype != torch.float32 or not label.is_contiguous():
+            label = label.to(device=dev, dtype=torch.float32).contiguous()
+        return label
+
     def forward_loss(self, skel, sensor, label):
         L = lib()
         st = stream_handle()
@@ -95,6 +122,9 @@ class TrainStep:
         self.backward_phase(0)
 
     def optimizer_step(self):
+        if self.optimizer is not None:
+            g = self.optimizer.param_groups[0]
+            self.lr, self.alpha, self.eps = g["lr"], g.get("alpha", self.alpha), g.get("eps", self.eps)
         scale = 1.0 / self.world
         check(lib().f3_rmsprop_step(ptr(self.model.flat_parameters()), ptr(self.square_avg), ptr(self.grads),
                                     self.grads.numel(), self.lr, self.alpha, self.eps, scale, stream_handle()),
@@ -117,6 +147,7 @@ class TrainStep:
         self.optimizer_step()
 
     def __call__(self, skel, sensor, label):
+        label = self.prepare(skel, sensor, label)
         if self.graph is None:
             self._eager(skel, sensor, label)
             return self.loss
