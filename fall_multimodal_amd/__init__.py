@@ -13,7 +13,7 @@ evaluate (valid / test loops, top-k, macro P/R/F1, best-model checkpoints).
 """
 from .config import CfgNode, get_cfg_defaults
 from .graph import Graph
-from .model import (BiLSTM, Fall3Net, NetSpec, STGCAN, TwoStreamSpatialTemporalGraph, TwoStreamSTGCAN,
+from .model import (BiLSTM, CNN_BiLSTM, Fall3Net, NetSpec, STGCAN, TwoStreamSpatialTemporalGraph, TwoStreamSTGCAN,
                     TwoStreamSTGCAN_BiLSTM, build_model)
 from .optim import RMSprop, build_optimizer
 from .train import TrainStep
@@ -21,5 +21,5 @@ from .targcn import TARGCN, TargcnStep
 from . import data, evaluate
 
 __all__ = ["build_model", "build_optimizer", "get_cfg_defaults", "CfgNode", "Graph", "Fall3Net", "NetSpec",
-           "STGCAN", "BiLSTM", "TwoStreamSTGCAN", "TwoStreamSTGCAN_BiLSTM", "TwoStreamSpatialTemporalGraph",
+           "STGCAN", "BiLSTM", "CNN_BiLSTM", "TwoStreamSTGCAN", "TwoStreamSTGCAN_BiLSTM", "TwoStreamSpatialTemporalGraph",
            "RMSprop", "TrainStep", "TARGCN", "TargcnStep", "data", "evaluate"]

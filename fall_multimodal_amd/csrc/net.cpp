@@ -990,6 +990,12 @@ int f3_net_create(const f3_config* cfg, f3_net** out) {
       break;
     case F3_MODEL_BILSTM:
       n->has_sensor = true;
+      if (cfg->sensor == F3_SENSOR_CNN_BILSTM) {  // sensor-only CNN_BiLSTM (GSTCAN_UR_sensor.ipynb:572-586)
+        n->has_cnn = true;
+        n->add_cnn("cnn.", cfg->sensor_dim, cfg->sensor_frames);
+        n->add_bilstm("bilstm.", 32, cfg->num_class);
+        break;
+      }
       if (cfg->sensor_dim > 32) { delete n; return F3_EINVAL; }
       n->add_bilstm("", cfg->sensor_dim, cfg->num_class);
       break;

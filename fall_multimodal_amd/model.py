@@ -63,7 +63,7 @@ class NativeNet:
         c.model = MODEL_IDS[spec.model]
         c.num_node, c.num_partition, c.num_class = V, K, spec.num_class
         c.in_channels = spec.in_channels
-        c.sensor = SENSOR_IDS[spec.sensor if spec.model == "two_stgcan_bilstm" else "none"]
+        c.sensor = SENSOR_IDS[spec.sensor if spec.model in ("two_stgcan_bilstm", "bilstm") else "none"]
         c.sensor_dim = spec.sensor_dim
         c.sensor_classes = spec.sensor_classes or 0
         c.softmax_output = int(spec.softmax_output)
@@ -329,6 +329,21 @@ class BiLSTM(Fall3Net):
             raise NotImplementedError("fall3 implements the reference configuration: H=64, 1 layer, mean feature")
         super().__init__(NetSpec(model="bilstm", num_class=num_classes, sensor="bilstm", sensor_dim=input_size,
                                  sensor_frames=sensor_frames), device)
+
+
+class CNN_BiLSTM(Fall3Net):
+    """Sensor-only CNN1D -> BiLSTM (GSTCAN_UR_sensor.ipynb:493-586; BASELINE config 1): the notebook's
+    class takes (hidden_size, num_layers, dropout_prob, num_classes, feature) but builds a fixed
+    BiLSTM(input_size=32, hidden_size=64, num_classes=2, feature='mean') on CNN1D(4) (:577-578), so
+    the module always has 2 outputs; the same arguments are accepted and ignored here."""
+
+    def __init__(self, hidden_size=16, num_layers=1, dropout_prob=0.3, num_classes=1, feature="last", device=None,
+                 sensor_dim=4, sensor_frames=30):
+        super().__init__(NetSpec(model="bilstm", num_class=2, sensor="cnn_bilstm", sensor_dim=sensor_dim,
+                                 sensor_frames=sensor_frames), device)
+
+    def forward(self, x):
+        return super().forward(None, x)
 
 
 class TwoStreamSTGCAN(Fall3Net):

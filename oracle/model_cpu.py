@@ -14,6 +14,7 @@ It follows, op for op (file:line relative to /root/reference):
 * Channel_Attention                        Multimodal_Fall3/model/stgcan.py:59-74
 * BiLSTM sensor branch                     Multimodal_Fall3/model/bilstm.py:21-59
 * CNN1D / CNN_BiLSTM (UR notebook)         GSTCAN_UR_conv.ipynb cell 2 (:493-586)
+* sensor-only CNN_BiLSTM (BASELINE cfg 1)  GSTCAN_UR_sensor.ipynb cell 2 (:493-586)
 * TwoStreamSTGCAN(_BiLSTM) fusion          Multimodal_Fall3/model/combination.py:9-46
 * notebook 3-stream (+softmax)             GSTCAN_HAR_conv_10kfold.ipynb:390-444
 * CE with soft targets                     Multimodal_Fall3/model/main.py:113,280
@@ -204,6 +205,10 @@ def param_shapes(spec: Spec, sensor_frames: int = 30) -> "OrderedDict[str, tuple
     if spec.model == "stgcn":
         return stream_shapes("", spec.in_channels, K, V, spec, spec.num_class)
     if spec.model == "bilstm":
+        if spec.sensor == "cnn_bilstm":  # sensor-only CNN_BiLSTM (GSTCAN_UR_sensor.ipynb:572-586)
+            out = cnn1d_shapes("cnn.", spec.sensor_dim, sensor_frames)
+            out.update(bilstm_shapes("bilstm.", 32, 64, spec.num_class))
+            return out
         return bilstm_shapes("", spec.sensor_dim, 64, spec.num_class)
     p1, p2, ps, pf = prefixes(spec)
     out = OrderedDict()
@@ -366,6 +371,8 @@ def forward(st, spec: Spec, skel, sensor=None, training=True):
     if spec.model == "stgcn":
         return stgcan_stream(S, "", skel, spec, spec.num_class)
     if spec.model == "bilstm":
+        if spec.sensor == "cnn_bilstm":
+            return bilstm_head(S, "bilstm.", cnn1d(S, "cnn.", sensor))
         return bilstm_head(S, "", sensor)
     p1, p2, ps, pf = prefixes(spec)
     mot = skel[:, :2, 1:] - skel[:, :2, :-1]  # combination.py:39

@@ -55,6 +55,7 @@ SPECS = [
     oc.Spec(model="bilstm", num_class=11, sensor_dim=15),
     oc.Spec(model="two_stgcan_bilstm", layout="coco_cut", num_class=2, sensor="cnn_bilstm", sensor_dim=4,
             sensor_classes=2, softmax_output=True, naming="notebook"),
+    oc.Spec(model="bilstm", num_class=2, sensor="cnn_bilstm", sensor_dim=4),  # BASELINE config 1
 ]
 
 
@@ -108,3 +109,34 @@ def test_param_offsets_tile_flat_buffer_phase1_first(spec):
         m = re.search(r"(?:st_gc[a]?n_networks|edge_importance)\.(\d+)", n)
         phase1 = (m is None and "data_bn" not in n) or (m is not None and int(m.group(1)) >= 4)
         assert (b <= split) == phase1, n
+
+
+@pytest.mark.parametrize("V", [14, 17, 18])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_targcn_entry_table_matches_reference_state_dict(V, precision):
+    """f3_targcn_entry: TARGCN(adj=None, num_nodes=V)'s exact state_dict keys, order and shapes
+    (TRAGCN.py:177-205; pinned by the oracle's table and the reference's parameter counts), 16-B
+    aligned parameter offsets, positive workspace."""
+    from oracle import targcn_cpu as tg
+    from fall_multimodal_amd.targcn import _NativeTargcn
+    net = _NativeTargcn(V, 11, precision)
+    ref = tg.param_shapes(V)
+    assert [n for n, k, sh, off in net.entries] == list(ref.keys())
+    for n, kind, sh, off in net.entries:
+        assert tuple(sh) == tuple(ref[n]), n
+        assert (kind == 1) == tg.is_buffer(n), n
+        if kind == 0:
+            assert off % 4 == 0, n
+    assert net.workspace_bytes(256) > net.workspace_bytes(4) > 0
+
+
+def test_targcn_rejects_unsupported_configs():
+    from fall_multimodal_amd.targcn import TARGCN, _NativeTargcn
+    with pytest.raises(RuntimeError):
+        _NativeTargcn(40, 11, "fp32")  # beyond the per-tile LDS layout (V <= 18)
+    with pytest.raises(ValueError):
+        _NativeTargcn(14, 11, "fp8")
+    with pytest.raises(NotImplementedError):
+        TARGCN(rnn_units=32, device="cpu")
+    with pytest.raises(ValueError):
+        TARGCN(adj=np.ones((14, 14)), device="cpu")

@@ -12,7 +12,7 @@ from tests.golden_util import check_grads_conditioned, check_packed, check_post,
 
 pytestmark = pytest.mark.gpu
 
-TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb"]
+TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb", "ur_sensor"]
 
 
 def dev():
@@ -26,6 +26,9 @@ def build_from_spec(spec, device):
     g = {"layout": spec.layout, "strategy": spec.strategy}
     if spec.model == "stgcn":
         return f3.STGCAN(spec.in_channels, g, spec.num_class, device=device)
+    if spec.model == "bilstm" and spec.sensor == "cnn_bilstm":
+        return f3.CNN_BiLSTM(hidden_size=16, num_layers=1, dropout_prob=0.3, num_classes=2, feature="mean",
+                             device=device)
     if spec.model == "bilstm":
         return f3.BiLSTM(spec.sensor_dim, num_classes=spec.num_class, device=device)
     if spec.model == "two_stgcan":
@@ -39,6 +42,8 @@ def build_from_spec(spec, device):
 def call(model, spec, skel, sensor):
     if spec.naming == "notebook":
         return model((skel, skel[:, :2, 1:] - skel[:, :2, :-1], sensor))
+    if spec.model == "bilstm" and spec.sensor == "cnn_bilstm":
+        return model(sensor)
     if spec.model == "bilstm":
         return model(None, sensor)
     return model(skel, sensor)
@@ -223,7 +228,7 @@ def test_fused_train_step_vs_oracle(layout, S, B):
     check_grads_conditioned(fake, ours, env, what=f"{layout} B={B}")
 
 
-@pytest.mark.parametrize("tag", ["har", "ur_nb", "stgcn", "bilstm"])
+@pytest.mark.parametrize("tag", ["har", "ur_nb", "stgcn", "bilstm", "ur_sensor"])
 def test_workspace_poison_no_uninitialized_reads(tag):
     """Every workspace byte a step reads must have been written by that step: with the
     workspace pre-filled with NaN (0xFF) or huge (0x7F) bytes the outputs and gradients

@@ -9,7 +9,7 @@ import torch
 from oracle import model_cpu as oc
 from tests.golden_util import GOLDEN, check_packed, check_post, load
 
-TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb"]
+TAGS = ["har", "ns", "two", "stgcn", "bilstm", "ur_nb", "ur_sensor"]
 
 
 def test_param_counts_match_reference_kats():
@@ -19,6 +19,7 @@ def test_param_counts_match_reference_kats():
     assert kat["ur_nb"] == 4311324        # GSTCAN_UR_conv.ipynb:797
     assert kat["two"] == 4250783          # GSTCAN_HAR_skeleton_10kfold.ipynb:954
     assert kat["bilstm"] == 47387         # GSTCAN_HAR_sensor(lstm)_10kfold.ipynb:968
+    assert kat["ur_sensor"] == 65154      # GSTCAN_UR_sensor.ipynb:796 (BASELINE config 1)
     for tag in TAGS:
         d, spec = load(tag)
         n = sum(int(np.prod(s)) for k, s in oc.param_shapes(spec).items() if not oc.is_buffer(k))

@@ -202,6 +202,14 @@ def main():
                   spec, lambda m, sk, se: m((sk, sk[:, :2, 1:] - sk[:, :2, :-1], se)), 4, 6789))
     for tag, mod, spec, fn, b, seed in cases:
         kat[tag] = run_case(tag, mod, spec, fn, b, seed)
+    # BASELINE config 1: the sensor-only CNN_BiLSTM of GSTCAN_UR_sensor.ipynb (cell 2, called at :4142)
+    nbs = json.load(open(REF + "/GSTCAN_UR_sensor.ipynb"))
+    nss = {"__name__": "nbsensor", "device": torch.device("cpu")}
+    exec(compile("".join(nbs["cells"][2]["source"]), "nb_ur_sensor", "exec"), nss)
+    spec = oc.Spec(model="bilstm", num_class=2, sensor="cnn_bilstm", sensor_dim=4)
+    kat["ur_sensor"] = run_case("ur_sensor", nss["CNN_BiLSTM"](hidden_size=16, num_layers=1, dropout_prob=0.3,
+                                                              num_classes=2, feature="mean"),
+                                spec, lambda m, sk, se: m(se), 8, 7890)
     T = import_targcn()
     kat["targcn_v14"] = run_targcn_case("v14", T, 14, 4, 7001)
     kat["targcn_v17"] = run_targcn_case("v17", T, 17, 3, 7002)
