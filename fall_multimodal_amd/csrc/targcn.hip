@@ -520,6 +520,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
                           {a.dH, H, 0, 0, 4}};
       stage(src, 5, t);
     }
+    F3_TG_STAMP(7);
     __syncthreads();
     // h = z*hp + (1-z)*hc: dz, dhc -> dU (tanh), cs*dSu (silu)
 #pragma unroll

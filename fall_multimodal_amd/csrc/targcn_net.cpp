@@ -395,10 +395,11 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
       (void)hipStreamSynchronize(s);
       (void)hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost);
       double ph[8] = {0};
+      const int ord[8] = {0, 7, 1, 2, 3, 4, 5, 6};
       for (int t = 0; t < T; ++t)
-        for (int k = 1; k < 7; ++k) ph[k] += (h[t * 8 + k] - h[t * 8 + k - 1]) * 0.01 / T;
-      fprintf(stderr, "gru_bwd layer %d per-step phases (us) upd-epi/upd-gemm/mixT/gate-epi/gate-gemm/mixT:", l);
-      for (int k = 1; k < 7; ++k) fprintf(stderr, " %.2f", ph[k]);
+        for (int k = 1; k < 8; ++k) ph[k] += (h[t * 8 + ord[k]] - h[t * 8 + ord[k - 1]]) * 0.01 / T;
+      fprintf(stderr, "gru_bwd layer %d per-step phases (us) stage/upd-epi/upd-gemm/mixT/gate-epi/gate-gemm/mixT:", l);
+      for (int k = 1; k < 8; ++k) fprintf(stderr, " %.2f", ph[k]);
       fprintf(stderr, "\n");
     }
     // per-node weight gradients over the B*T rows of each node (grouped GEMMs, one group per node)
