@@ -144,6 +144,31 @@ def eval_throughput(model, sk, se, reps=20):
     return {"clips_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3), "batch": B}
 
 
+def autograd_path_bench(model, sk, se, lb, steps=5):
+    """The reference driver's loop body unchanged (model/main.py:112-127): out = model(data, sensor)
+    through the fall3::net_forward custom op, CrossEntropyLoss, loss.backward() (fall3::net_backward),
+    optimizer.step() with fall3 RMSprop per parameter tensor (fall3::rmsprop_), zero_grad."""
+    import fall_multimodal_amd as f3
+    opt = f3.RMSprop(model.parameters(), lr=1e-3)
+    loss_fn = torch.nn.CrossEntropyLoss()
+
+    def one():
+        opt.zero_grad()
+        loss = loss_fn(model(sk, se), lb)
+        loss.backward()
+        opt.step()
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"ms_per_step": round(dt * 1e3, 3), "clips_per_s": round(sk.shape[0] / dt, 1), "steps": steps,
+            "path": "model(data, sensor) -> CrossEntropyLoss -> backward -> RMSprop.step (torch.library ops)"}
+
+
 def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_seconds=0.0):
     """BASELINE config 2: skeleton-only TARGCN (TRAGCN.py:177-224, V=17 joints, T=30, bf16 GEMM
     operands) training step (fwd + CE + bwd + RMSprop) at B=256 on one GPU, synthetic clips,
@@ -255,6 +280,7 @@ def main():
         dt = float(t.item())
     loss = float(step.loss.item())
     ev = eval_throughput(model, sk, se) if rank == 0 else None
+    agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     if rank == 0:
@@ -279,6 +305,7 @@ def main():
             "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
             "eval_forward": ev,
+            "main_py_autograd_path": agp,
             "cfg2_targcn": tgrec,
             "cpu_baseline": cpu,
         }

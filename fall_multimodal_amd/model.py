@@ -15,7 +15,8 @@ Every module's state_dict has the reference's exact keys, order and shapes (the 
 comes from the native plan, f3_net_entry). Parameters are views into one flat fp32
 buffer and gradients come back as views into one flat gradient buffer, so the optimizer
 and the data-parallel all-reduce each touch one contiguous array. The whole model's
-forward is one native call and its backward another (one autograd node).
+forward is one native call and its backward another: the custom ops fall3::net_forward /
+fall3::net_backward (ops.py, torch.library, with fake kernels and autograd registration).
 """
 from __future__ import annotations
 
@@ -27,7 +28,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, ops
 from ._lib import ENTRY_BUFFER, ENTRY_COUNTER, ENTRY_PARAM, check, lib, ptr, require_device, stream_handle
 from .graph import STRATEGY_PARTITIONS, Graph
 
@@ -129,6 +130,7 @@ class Fall3Net(nn.Module):
         graph = Graph(spec.layout, spec.strategy)
         A = graph.A
         object.__setattr__(self, "_native", NativeNet(spec, A.shape[0], A.shape[1]))
+        object.__setattr__(self, "_op_id", ops.register(self))
         object.__setattr__(self, "num_node", A.shape[1])
         if device is None:
             device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
@@ -238,17 +240,27 @@ class Fall3Net(nn.Module):
         return skel, sensor
 
     def forward(self, *args, **kwargs):
+        """One fall3::net_forward custom op (its autograd calls fall3::net_backward)."""
         skel, sensor = self._inputs(args, kwargs)
-        params = [p for p in self.parameters()]
-        return _Fall3Fn.apply(self, skel, sensor, *params)
+        skel, sensor = _prep(skel), _prep(sensor)
+        self.check_inputs(skel, sensor)
+        out, _, buffers, counters = torch.ops.fall3.net_forward(self._op_id, list(self.parameters()),
+                                                                self._flat_buffers, self._flat_counters, skel,
+                                                                sensor, self.training)
+        if self.training:  # BatchNorm running statistics / num_batches_tracked (nn.BatchNorm semantics)
+            with torch.no_grad():
+                self._flat_buffers.copy_(buffers)
+                self._flat_counters.copy_(counters)
+        return out
 
-    def native_forward(self, skel, sensor, out, workspace, training, stream=None):
+    def native_forward(self, skel, sensor, out, workspace, training, stream=None, buffers=None, counters=None):
         nat = self._native
         N = (skel if skel is not None else sensor).shape[0]
         st = stream if stream is not None else stream_handle()
-        check(lib().f3_net_forward(nat.h, N, int(training), ptr(self._flat_params), ptr(self._flat_buffers),
-                                   ptr(self._flat_counters), ptr(skel), ptr(sensor), ptr(out), ptr(workspace),
-                                   st), "fall3 forward")
+        buffers = self._flat_buffers if buffers is None else buffers
+        counters = self._flat_counters if counters is None else counters
+        check(lib().f3_net_forward(nat.h, N, int(training), ptr(self._flat_params), ptr(buffers), ptr(counters),
+                                   ptr(skel), ptr(sensor), ptr(out), ptr(workspace), st), "fall3 forward")
 
     def native_backward(self, N, dout, grads, workspace, stream=None):
         st = stream if stream is not None else stream_handle()
@@ -275,31 +287,6 @@ class Fall3Net(nn.Module):
 
 def _prep(t):
     return None if t is None else t.detach().contiguous().float()
-
-
-class _Fall3Fn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, module, skel, sensor, *params):
-        skel, sensor = _prep(skel), _prep(sensor)
-        module.check_inputs(skel, sensor)
-        ref = skel if skel is not None else sensor
-        N = ref.shape[0]
-        training = module.training
-        ws = torch.empty(module._native.workspace_bytes(N), dtype=torch.uint8, device=ref.device)
-        out = torch.empty(N, module.spec.num_class, dtype=torch.float32, device=ref.device)
-        module.native_forward(skel, sensor, out, ws, training)
-        ctx.module, ctx.ws, ctx.training, ctx.N = module, ws, training, N
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        if not ctx.training:
-            raise RuntimeError("fall3: backward through an eval-mode forward is not supported")
-        module = ctx.module
-        grads = torch.empty(module._native.nparam, dtype=torch.float32, device=dout.device)
-        module.native_backward(ctx.N, dout.contiguous().float(), grads, ctx.ws)
-        views = [grads[off:off + int(np.prod(shape))].view(shape) for _, shape, off in module.param_views()]
-        return (None, None, None, *views)
 
 
 # ----------------------------------------------------------------------------

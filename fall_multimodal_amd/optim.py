@@ -10,13 +10,13 @@ import math
 
 import torch
 
-from ._lib import check, lib, ptr, require_device, stream_handle
+from . import ops  # noqa: F401  (registers fall3::rmsprop_)
+from ._lib import require_device
 
 
 class RMSprop(torch.optim.Optimizer):
     """torch.optim.RMSprop(lr, alpha=0.99, eps=1e-8) — no momentum, not centred, no
-    weight decay — as one f3_rmsprop_step launch per parameter tensor (or one launch
-    over a flat buffer via `step_flat`)."""
+    weight decay — as one fall3::rmsprop_ custom op (f3_rmsprop_step) per parameter tensor."""
 
     def __init__(self, params, lr=1e-2, alpha=0.99, eps=1e-8):
         super().__init__(params, dict(lr=lr, alpha=alpha, eps=eps))
@@ -24,8 +24,6 @@ class RMSprop(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        L = lib()
-        st = stream_handle()
         for group in self.param_groups:
             for p in group["params"]:
                 if p.grad is None:
@@ -39,8 +37,7 @@ class RMSprop(torch.optim.Optimizer):
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 if not p.is_contiguous():
                     raise RuntimeError("fall3 RMSprop needs contiguous parameters")
-                check(L.f3_rmsprop_step(ptr(p), ptr(state["square_avg"]), ptr(g), p.numel(), group["lr"],
-                                        group["alpha"], group["eps"], 1.0, st), "rmsprop")
+                torch.ops.fall3.rmsprop_(p, state["square_avg"], g, group["lr"], group["alpha"], group["eps"], 1.0)
         return loss
 
 

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, ops
 from ._lib import ENTRY_PARAM, check, lib, ptr, require_device, stream_handle
 
 PRECISION_IDS = {"fp32": 0, "bf16": 1}
@@ -90,6 +90,7 @@ class TARGCN(nn.Module):
         object.__setattr__(self, "num_class", num_classes)
         object.__setattr__(self, "precision", precision)
         object.__setattr__(self, "_native", _NativeTargcn(num_nodes, num_classes, precision))
+        object.__setattr__(self, "_op_id", ops.register(self))
         if device is None:
             device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
         nat = self._native
@@ -184,28 +185,11 @@ class TARGCN(nn.Module):
                                        ptr(dout), ptr(grads), ptr(workspace), st), "targcn backward")
 
     def forward(self, source):
-        return _TargcnFn.apply(self, source, *self.parameters())
-
-
-class _TargcnFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, module, source, *params):
+        """One fall3::targcn_forward custom op (its autograd calls fall3::targcn_backward)."""
         source = source.detach().contiguous().float()
-        module.check_inputs(source)
-        B = source.shape[0]
-        ws = torch.empty(module._native.workspace_bytes(B), dtype=torch.uint8, device=source.device)
-        out = torch.empty(B, module.num_class, dtype=torch.float32, device=source.device)
-        module.native_forward(source, out, ws)
-        ctx.module, ctx.ws, ctx.B = module, ws, B
+        self.check_inputs(source)
+        out, _ = torch.ops.fall3.targcn_forward(self._op_id, list(self.parameters()), self._flat_buffers, source)
         return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        m = ctx.module
-        grads = torch.empty(m._native.nparam, dtype=torch.float32, device=dout.device)
-        m.native_backward(ctx.B, dout.contiguous().float(), grads, ctx.ws)
-        views = [grads[off:off + int(np.prod(shape))].view(shape) for _, shape, off in m.param_views()]
-        return (None, None, *views)
 
 
 class TargcnStep:

@@ -140,3 +140,26 @@ def test_targcn_rejects_unsupported_configs():
         TARGCN(rnn_units=32, device="cpu")
     with pytest.raises(ValueError):
         TARGCN(adj=np.ones((14, 14)), device="cpu")
+
+
+def test_custom_ops_registered_with_fake_kernels():
+    """the native step is reachable as torch.library custom ops with fake kernels,
+    so shapes propagate under FakeTensor tracing (torch.compile) without a device."""
+    import torch
+    from torch._subclasses import FakeTensorMode
+    import fall_multimodal_amd as f3
+    for op in ("net_forward", "net_backward", "targcn_forward", "targcn_backward", "rmsprop_"):
+        assert hasattr(torch.ops.fall3, op), op
+    m = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device="cpu")
+    t = f3.TARGCN(num_nodes=17, device="cpu")
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        out, ws, nb, nc = torch.ops.fall3.net_forward(m._op_id, list(m.parameters()), m._flat_buffers,
+                                                      m._flat_counters, torch.empty(8, 3, 30, 18),
+                                                      torch.empty(8, 30, 6), True)
+        assert tuple(out.shape) == (8, 11) and ws.numel() == m._native.workspace_bytes(8)
+        assert nb.shape == m._flat_buffers.shape and nc.shape == m._flat_counters.shape
+        g = torch.ops.fall3.net_backward(m._op_id, list(m.parameters()), out, ws)
+        assert g.numel() == m._native.nparam
+        o2, w2 = torch.ops.fall3.targcn_forward(t._op_id, list(t.parameters()), t._flat_buffers,
+                                                torch.empty(4, 30, 17, 3))
+        assert tuple(o2.shape) == (4, 11) and w2.numel() == t._native.workspace_bytes(4)

@@ -537,3 +537,18 @@ def test_cfg3_two_stream_bf16_parity():
     print(rec)
     assert err < BF16_CFG3_LOGIT_GATE and agree >= BF16_B256_ARGMAX_GATE
     assert cos >= BF16_CFG3_COS_GATE
+
+
+def test_custom_ops_opcheck():
+    """torch.library.opcheck on the native ops (schema, fake kernel vs real kernel, autograd
+    registration) at a small batch."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_mmpose", num_class=11, sensor_dim=6)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d)
+    model.load_state_dict(oc.init_state(spec, 5))
+    skel, sensor, _ = synthetic_batch(4, 18, 11, 6, 6)
+    args = (model._op_id, list(model.parameters()), model._flat_buffers, model._flat_counters,
+            torch.from_numpy(skel).to(d), torch.from_numpy(sensor).to(d), True)
+    torch.library.opcheck(torch.ops.fall3.net_forward.default, args,
+                          test_utils=("test_schema", "test_faketensor", "test_autograd_registration"))
