@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 PEAK_MFMA_TFLOPS = {"fp32": 157.3,    # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
                     "bf16": 2500.0}   # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 PEAK_HBM_GBS = 8000.0
+FLOP_PER_CLIP = {(18, 6): 5.118e9, (14, 15): 3.946e9}  # 3-stream fwd+bwd GEMM FLOPs per clip
 
 
 def parse():
@@ -75,12 +76,16 @@ def _time_launch(fn, reps=20):
 
 
 def roofline_kernels(dev, batch, V, precision):
-    """The step's GEMM kernels on the layer-6 tcn shape (C=256, T=8, 9 taps, B clips):
-    * "wgrad": the tcn weight gradient, wgrad_glds_bf16<128,128> — the kernel with the largest
-      share of the step's GPU time (profiles/r01_bf16_kernel_summary.txt), launched alone
-      through f3_conv_wgrad_packed exactly as the step launches it;
-    * "tcn_fwd": the forward implicit GEMM (igemm_big<1,1,8>: the step's launch is igemm_big<13,1,8>, the same GEMM with the BN-statistics and pooling epilogue), weight operand pre-packed.
-    Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for both."""
+    """The step's GEMM kernels on the layer-6 tcn shape (C=256, T=8, 9 taps, B clips), each
+    launched alone through the C ABI exactly as the step launches it:
+    * "wgrad": the tcn weight gradient as the step computes it: wgrad_big<4,2,4,4,64> (split-K
+      partials into the slab) + wgrad_slab_reduce (partials summed into dW[Cout][Cin][KT]);
+      f3_conv_backward_weight(bf16). The headline roofline (the step's largest kernel share,
+      profiles/r01_bf16_kernel_summary.txt);
+    * "wgrad_kernel": wgrad_big alone (partials left in the slab), for the kernel's own fraction;
+    * "tcn_fwd": the forward implicit GEMM igemm_big<1,1,8> with bf16 output (the step writes
+      the tcn output bf16; its launch igemm_big<13,1,8> adds the BN-statistics/pool epilogue).
+    Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for all three."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
     N, T, C, KT = batch, 8, 256, 9
@@ -90,28 +95,33 @@ def roofline_kernels(dev, batch, V, precision):
     out = {}
     x = torch.randn(N, T, V, C, device=dev)
     dy = torch.randn(N, T, V, C, device=dev)
-    if precision == "bf16":  # the network's bf16 GEMM operand tensors are bf16 in HBM
+    bf = precision == "bf16"
+    if bf:  # the network's bf16 GEMM operand tensors are bf16 in HBM
         x, dy = x.to(torch.bfloat16), dy.to(torch.bfloat16)
     w = torch.randn(C, C, KT, device=dev) / 48.0
     b = torch.zeros(C, device=dev)
-    y = torch.empty(N, T, V, C, device=dev)
+    y = torch.empty(N, T, V, C, device=dev, dtype=torch.bfloat16 if bf else torch.float32)
     wp = torch.empty(C * KT * C, device=dev)
-    prec = 1 if precision == "bf16" else 0
+    prec = 3 if bf else 0  # F3_CONV_BF16_OUT: bf16 in, bf16 out (as the step)
     L.check(lib.f3_conv_forward(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1, 4, prec, st),
             "conv")  # packs w into wp; the timed launches reuse it (the GEMM alone)
     ms = _time_launch(lambda: lib.f3_conv_forward(L.ptr(x), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1,
                                                   4, prec, st))
-    out["tcn_fwd"] = {"kernel": f"{'igemm_big<1,1,8>' if prec else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, N={N}, V={V})",
-                      "ms": ms}
-    if prec:
+    out["tcn_fwd"] = {"kernel": f"{'igemm_big<1,1,8> bf16-out' if bf else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, "
+                                f"N={N}, V={V})", "ms": ms}
+    if bf:
+        dw = torch.empty(C, C, KT, device=dev)
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight(L.ptr(dy), L.ptr(x), L.ptr(dw), None, N, T, V, C, C, KT,
+                                                              1, 4, 1, st))
+        out["wgrad"] = {"kernel": f"wgrad_big<4,2,4,4,64> + wgrad_slab_reduce (tcn 9x1 weight gradient incl. the "
+                                  f"split-K reduce, C=256, T=8, N={N}, V={V})", "ms": ms}
         cap = 512 * 128 * 128 * max(1, int(os.environ.get("F3_SLAB_X", "1")))  # the step's slab (net.cpp wgrad_slab_floats)
         slab = torch.empty(cap, device=dev)
         L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4, st), "wgrad")
         ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4,
                                                            st))
-        kname = "wgrad_big<4,2,4,4,64>" if os.environ.get("F3_WGRAD_BIG", "1") != "0" else "wgrad_glds_bf16<128,128>"
-        out["wgrad"] = {"kernel": f"{kname} (tcn 9x1 weight gradient, C=256, T=8, N={N}, V={V})",
-                        "ms": ms}
+        out["wgrad_kernel"] = {"kernel": f"wgrad_big<4,2,4,4,64> alone (partials left in the slab, C=256, T=8, N={N}, "
+                                         f"V={V})", "ms": ms}
     pmc = {}
     if os.path.exists(ROOFLINE_PMC):
         with open(ROOFLINE_PMC) as f:
@@ -124,6 +134,77 @@ def roofline_kernels(dev, batch, V, precision):
         res[key] = {"kernel": r["kernel"], "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                     "flop_per_launch": flop, "ms_per_launch": round(r["ms"], 4)}
+    return res
+
+
+def mix_roofline(dev, batch, V, precision):
+    """Graph mix of a st_gcan block (stgcan.py:54; R-GCN's A-contraction, HBM-bound) on the
+    layer-1 shape (Cin=64, K=3, T=30, B clips), launched alone with the step's operand types.
+    Algorithmic bytes: fwd = x + z (+A); bwd = x + dz + dx (+A, dA)."""
+    import fall_multimodal_amd._lib as L
+    lib = L.lib()
+    K, Cin, T = 3, 64, 30
+    frames = batch * T
+    bf = precision == "bf16"
+    et = torch.bfloat16 if bf else torch.float32
+    es = 2 if bf else 4
+    A = torch.rand(K, V, V, device=dev) / V
+    x = torch.randn(frames, V, Cin, device=dev).to(et)
+    z = torch.empty(frames, V, K, Cin, device=dev, dtype=et)
+    dx = torch.empty(frames, V, Cin, device=dev)
+    dA = torch.empty(K, V, V, device=dev)
+    st = L.stream_handle()
+    ffl = (1 if bf else 0) | (2 if bf else 0)
+    ms_f = _time_launch(lambda: lib.f3_graph_mix_forward_ex(L.ptr(A), L.ptr(x), L.ptr(z), frames, K, V, Cin, ffl, st))
+    ms_b = _time_launch(lambda: lib.f3_graph_mix_backward_ex(L.ptr(A), L.ptr(x), L.ptr(z), L.ptr(dx), L.ptr(dA), frames,
+                                                             K, V, Cin, 1 if bf else 0, st))
+    nx = frames * V * Cin
+    bytes_f = nx * es + nx * K * es + K * V * V * 4
+    bytes_b = nx * es + nx * K * es + nx * 4 + 2 * K * V * V * 4
+    res = {}
+    for key, byt, ms, kern in (("fwd", bytes_f, ms_f, "mix_fwd_lds"), ("bwd", bytes_b, ms_b, "mix_bwd_lds + colsum")):
+        gbs = byt / (ms * 1e-3) / 1e9
+        res[key] = {"kernel": f"{kern} (K=3, V={V}, Cin=64, frames={frames}, {precision})", "bound": "hbm",
+                    "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": byt, "ms_per_launch": round(ms, 4)}
+    return res
+
+
+def sensor_bench(dev, precision="fp32"):
+    """The sensor models on their own: BASELINE config 1 (sensor-only CNN_BiLSTM, UR-Fall, S=4,
+    B=32, GSTCAN_UR_sensor.ipynb:572-586) training-step throughput, and the north-star sensor
+    branch's BiLSTM (bilstm.py:21-59, S=6, T=30, B=256) per-recurrent-step latency: the
+    BiLSTM-only model's forward and fwd+bwd step divided by the 30 dependent steps (each
+    direction runs concurrently; the head kernels are included, so these are upper bounds)."""
+    import fall_multimodal_amd as f3
+    res = {}
+    g = torch.Generator().manual_seed(5)
+    for name, model, B, S in (("cfg1_cnn_bilstm", f3.CNN_BiLSTM(device=dev), 32, 4),
+                              ("bilstm_S6", f3.BiLSTM(6, num_classes=11, device=dev), 256, 6)):
+        C = model.spec.num_class
+        x = torch.randn(B, 30, S, generator=g).to(dev)
+        lab = torch.softmax(torch.randn(B, C, generator=g), 1).to(dev)
+        step = f3.TrainStep(model, B, lr=1e-3)
+        out = torch.empty(B, C, device=dev)
+        ws = step.ws
+        for _ in range(3):
+            step(None, x, lab)
+        torch.cuda.synchronize()
+        reps = 50
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step(None, x, lab)
+        torch.cuda.synchronize()
+        dt_step = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            model.native_forward(None, x, out, ws, True)
+        torch.cuda.synchronize()
+        dt_fwd = (time.perf_counter() - t0) / reps
+        res[name] = {"batch": B, "sensor_dim": S, "clips_per_s": round(B / dt_step, 1),
+                     "ms_per_step": round(dt_step * 1e3, 4), "fwd_ms": round(dt_fwd * 1e3, 4),
+                     "lstm_fwd_us_per_recurrent_step": round(dt_fwd * 1e6 / 30, 2),
+                     "lstm_step_us_per_recurrent_step": round(dt_step * 1e6 / 30, 2)}
     return res
 
 
@@ -194,14 +275,14 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
                       "gru_layers": 2, "hidden": 64, "ta_layers": 2},
            "final_loss": round(float(step.loss.item()), 5)}
     if cpu_seconds > 0:  # the oracle (pinned bit-exactly to the reference) on this host's cores
-        threads = min(os.cpu_count() or 1, 64)
+        threads = cpu_threads()
         torch.set_num_threads(threads)
         st = tg.init_state(V, 7)
-        Bc = 64
+        Bc = B
         s_c, l_c = (torch.from_numpy(a) for a in tg.synthetic_source(Bc, V, 11, 1))
         tg.train_step(st, s_c, l_c)
         t0, n = time.perf_counter(), 0
-        while time.perf_counter() - t0 < cpu_seconds and n < 20:
+        while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 20):
             tg.train_step(st, s_c, l_c)
             n += 1
         rec["cpu_baseline"] = {"value": round(Bc * n / (time.perf_counter() - t0), 2), "unit": "clips/s",
@@ -210,20 +291,29 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
     return rec
 
 
+def cpu_threads():
+    """The CPU share this process may use: OMP_NUM_THREADS (16 on the GPU box, whose nproc shows
+    the whole machine), else every core here."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(env))) if env and env.isdigit() else n
+
+
 def cpu_baseline(layout, V, S, seconds):
-    """The oracle (CPU PyTorch restatement, pinned to the reference) on this host's cores."""
+    """The oracle (CPU PyTorch restatement, pinned to the reference) on this host's cores, at the
+    benchmarked batch (B=256)."""
     from oracle import model_cpu as oc
     from oracle.prng import synthetic_batch
-    threads = min(os.cpu_count() or 1, 64)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     spec = oc.Spec(model="two_stgcan_bilstm", layout=layout, num_class=11, sensor_dim=S)
     st = oc.init_state(spec, 7)
-    B = 64
+    B = 256
     sk, se, lb = (torch.from_numpy(x) for x in synthetic_batch(B, V, 11, S, 1))
-    oc.train_step(st, spec, sk, se, lb)  # warm-up
+    oc.train_step(st, spec, *(torch.from_numpy(x) for x in synthetic_batch(16, V, 11, S, 2)))  # warm-up
     t0 = time.perf_counter()
     n = 0
-    while time.perf_counter() - t0 < seconds and n < 50:
+    while n < 1 or (time.perf_counter() - t0 < seconds and n < 50):
         oc.train_step(st, spec, sk, se, lb)
         n += 1
     dt = time.perf_counter() - t0
@@ -283,6 +373,8 @@ def main():
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
+    sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
         rec = {
@@ -303,7 +395,15 @@ def main():
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5)},
             "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
+            "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
+            "roofline_graph_mix": mix,
+            "step_mfma": {"flop_per_clip": FLOP_PER_CLIP.get((V, S)), "achieved_tflops": None if FLOP_PER_CLIP.get(
+                (V, S)) is None else round(B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12, 2),
+                "peak": PEAK_MFMA_TFLOPS[a.precision], "frac": None if FLOP_PER_CLIP.get((V, S)) is None else round(
+                    B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12 / PEAK_MFMA_TFLOPS[a.precision], 4),
+                "note": "whole step (fwd+bwd conv/einsum/addmm FLOPs, SURVEY 8d) / ms_per_step / dense peak"},
+            "sensor": sens,
             "eval_forward": ev,
             "main_py_autograd_path": agp,
             "cfg2_targcn": tgrec,

@@ -1242,7 +1242,9 @@ static float* test_scratch(size_t n) {
 int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
                     int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (precision < 0 || precision > 2) return F3_EINVAL;
+  if (precision < 0 || precision > F3_CONV_BF16_OUT) return F3_EINVAL;
+  const bool bf_out = precision == F3_CONV_BF16_OUT;
+  if (bf_out) precision = F3_PRECISION_BF16;
   const int hb = precision != F3_PRECISION_FP32;
   if (w) {  // w == NULL: wpack already holds the packed operand (timing the GEMM alone)
     PrepTable t;
@@ -1261,6 +1263,7 @@ int f3_conv_forward(const void* x, const float* w, const float* bias, float* out
     a.in = (const float*)x;
   }
   a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias;
+  if (bf_out) a.outb = reinterpret_cast<unsigned short*>(out);
   return f3_conv_gemm(&a, 0, EPI_BIAS, s);
 }
 
@@ -1347,6 +1350,39 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
   std::memset(&m, 0, sizeof(m));
   m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = x; m.z = const_cast<float*>(dz);
   m.dx = dx; m.dA = dA; m.accumulate = 0;
+  static float* part = nullptr;  // test entry only: scratch kept for the process lifetime
+  if (!part && hipMalloc(&part, sizeof(float) * kMixParts * 1024) != hipSuccess) return F3_EHIP;
+  m.part = part;
+  return f3_mix_bwd(&m, s);
+}
+
+int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int frames, int K, int V, int Cin, int flags,
+                            void* stream) {
+  if (!A_eff || !x || !z || frames < 0 || (flags & ~3)) return F3_EINVAL;
+  MixArgs m;
+  std::memset(&m, 0, sizeof(m));
+  m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff;
+  m.x = static_cast<const float*>(x); m.x16 = flags & F3_MIX_X_BF16;
+  m.z = static_cast<float*>(z);
+  if (flags & F3_MIX_Z_BF16) m.zb = static_cast<unsigned short*>(z);
+  return f3_mix_fwd(&m, (hipStream_t)stream);
+}
+
+int f3_graph_mix_backward_ex(const float* A_eff, const void* x, const void* dz, float* dx, float* dA, int frames, int K,
+                             int V, int Cin, int flags, void* stream) {
+  if (!A_eff || !x || !dz || !dx || !dA || frames < 0 || (flags & ~1)) return F3_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(dA, 0, sizeof(float) * K * V * V, s) != hipSuccess) return F3_EHIP;
+  MixArgs m;
+  std::memset(&m, 0, sizeof(m));
+  m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = static_cast<const float*>(x);
+  m.dx = dx; m.dA = dA; m.accumulate = 0;
+  if (flags & F3_MIX_X_BF16) {
+    m.x16 = 1;
+    m.dzb = static_cast<const unsigned short*>(dz);
+  } else {
+    m.z = const_cast<float*>(static_cast<const float*>(dz));
+  }
   static float* part = nullptr;  // test entry only: scratch kept for the process lifetime
   if (!part && hipMalloc(&part, sizeof(float) * kMixParts * 1024) != hipSuccess) return F3_EHIP;
   m.part = part;

@@ -107,7 +107,9 @@ int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_
  * (stgcan.py:24-31 tcn Conv2d). wpack is scratch of Cout*KT*Cin floats for the packed
  * operand; w == NULL reuses what a previous call packed there. precision = F3_PRECISION_*:
  * FP32 -> x/dy are fp32; BF16 -> x/dy are bf16 (the network's bf16 operand tensors);
- * BF16_FP32IN -> fp32 x/dy rounded to bf16 while staging. */
+ * BF16_FP32IN -> fp32 x/dy rounded to bf16 while staging. f3_conv_forward also takes
+ * F3_CONV_BF16_OUT (bf16 x, out written as bf16 [N,T_out,V,Cout]: the step's tcn output type). */
+enum { F3_CONV_BF16_OUT = 3 };
 int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
                     int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream);
 
@@ -129,6 +131,13 @@ int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frame
                          void* stream);
 int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, float* dx, float* dA, int frames, int K,
                           int V, int Cin, void* stream);
+/* The same with the bf16 mode's operand types: F3_MIX_X_BF16 -> x (and, backward, dz) bf16;
+ * F3_MIX_Z_BF16 -> forward z written bf16 (the gcn GEMM's operand, as the step stores it). */
+enum { F3_MIX_X_BF16 = 1, F3_MIX_Z_BF16 = 2 };
+int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int frames, int K, int V, int Cin, int flags,
+                            void* stream);
+int f3_graph_mix_backward_ex(const float* A_eff, const void* x, const void* dz, float* dx, float* dA, int frames, int K,
+                             int V, int Cin, int flags, void* stream);
 
 const char* f3_status_string(int status);
 
