@@ -90,3 +90,57 @@ def test_targcn_oracle_train_step_matches_reference(tag):
         check_packed(d, "grad:" + name, g.numpy(), rtol=1e-4, atol=1e-7)
     for name, g in grads.items():
         check_packed(d, "post:" + name, st[name].numpy(), rtol=1e-5, atol=1e-7)
+
+
+SKTR_TAGS = ["m1", "m2"]
+
+
+def test_sktr_param_count_matches_reference_kat():
+    from oracle import sktr_cpu as sk
+    kat = json.load(open(os.path.join(GOLDEN, "param_counts.json")))
+    assert kat["sktr"] == 262091   # GSTCAN_HAR_conv_kfold_trans.ipynb:938
+    n = sum(int(np.prod(s)) for k, s in sk.param_shapes().items() if not sk.is_buffer(k))
+    assert n == kat["sktr"]
+
+
+@pytest.mark.parametrize("tag", SKTR_TAGS)
+def test_sktr_oracle_train_step_matches_reference(tag):
+    """The SkeletonTransformer restatement vs the reference module (stochastic depth identity,
+    FFN dropout p=0): eval logits, train logits, loss, gradients, post-RMSprop params, BN running stats."""
+    from oracle import sktr_cpu as sk
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    z = np.load(os.path.join(GOLDEN, f"sktr_{tag}.npz"))
+    d = {k: z[k] for k in z.files}
+    st = sk.init_state(int(d["seed"][0]), int(d["V"][0]), int(d["T"][0]))
+    x = torch.from_numpy(d["x"])
+    with torch.no_grad():  # eval mode of the initial model (running statistics 0 / 1)
+        ev = sk.forward(st, x, training=False)
+    np.testing.assert_allclose(ev.numpy(), d["eval_out"], rtol=0, atol=1e-5)
+    out, loss, grads = sk.train_step(st, x, torch.from_numpy(d["label"]), lr=float(d["lr"][0]))
+    np.testing.assert_allclose(out.numpy(), d["out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(loss.item(), d["loss"][0], rtol=1e-6, atol=1e-6)
+    for name, g in grads.items():
+        # fp32 reassociation through six BatchNorm backward passes: 1e-3 of the tensor's max |g|, floored
+        # at 1e-5 for the biases that feed a BatchNorm directly (zero gradient up to rounding)
+        check_packed(d, "grad:" + name, g.numpy(), rtol=1e-4, atol=1e-3 * max(float(g.abs().max()), 1e-2))
+        # RMSprop's first step moves an element by ~10*lr*sign(g) whatever |g|, so tensors whose
+        # exact gradient is zero (biases feeding a BatchNorm; the key part of w_qkv.bias, a per-row
+        # constant under the softmax) move by rounding noise: their post-step values are not compared
+        # (elements with |g| near rounding level move by up to 10*lr as well: atol 0.1*lr)
+        if not name.endswith("w_qkv.bias") and float(g.abs().max()) > 1e-5:
+            check_packed(d, "post:" + name, st[name].numpy(), rtol=1e-5, atol=0.1 * float(d["lr"][0]))
+    for name in st:
+        if name.endswith(("running_mean", "running_var")):
+            check_packed(d, "buf:" + name, st[name].numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_sktr_dropout_mask_statistics():
+    """The counter-hash dropout mask keeps ~half the elements, independently per block and seed."""
+    from oracle import sktr_cpu as sk
+    a = sk.dropout_keep(123, 0, 1 << 16, 0.5)
+    b = sk.dropout_keep(123, 1, 1 << 16, 0.5)
+    c = sk.dropout_keep(124, 0, 1 << 16, 0.5)
+    for m in (a, b, c):
+        assert abs(m.mean() - 0.5) < 0.01
+    assert abs((a == b).mean() - 0.5) < 0.01 and abs((a == c).mean() - 0.5) < 0.01
+    assert sk.dropout_keep(5, 2, 100, 0.0).all()

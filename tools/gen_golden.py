@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate golden vectors by running the REFERENCE's own modules (build container only).
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--targcn-only]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--targcn-only | --sktr-only]
 Writes: tests/golden/*.npz  (small, committed; the reference itself never travels).
 
 How the reference is imported: the packaged 3-stream model lives in
@@ -32,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 from oracle import model_cpu as oc  # noqa: E402
+from oracle import sktr_cpu as sk  # noqa: E402
 from oracle import targcn_cpu as tg  # noqa: E402
 from oracle.prng import synthetic_batch  # noqa: E402
 
@@ -153,8 +154,85 @@ def run_targcn_case(tag, T, V, batch, seed, lr=1e-5):
     return nparams
 
 
+def import_sktr():
+    """skeleton_transformer.py imports torchvision (absent here) for ops.StochasticDepth: stub it as
+    the identity, which is what the reference computes in eval mode and what a
+    train-mode step computes with every stochastic-depth draw kept at scale 1."""
+    tv = types.ModuleType("torchvision")
+    ops = types.ModuleType("torchvision.ops")
+
+    class StochasticDepth(torch.nn.Module):
+        def __init__(self, p, mode):
+            super().__init__()
+            self.p, self.mode = p, mode
+
+        def forward(self, x):
+            return x
+
+    ops.StochasticDepth = StochasticDepth
+    tv.ops = ops
+    sys.modules.setdefault("torchvision", tv)
+    sys.modules.setdefault("torchvision.ops", ops)
+    sys.path.insert(0, REF)
+    return importlib.import_module("skeleton_transformer")
+
+
+def run_sktr_case(tag, S, batch, seed, M=1, V=14, T=30, lr=1e-3):
+    """SkeletonTransformer(3, V, T, 11, 32, 6, 16, 8) train step (GSTCAN_HAR_conv_kfold_trans.ipynb):
+    CE(out, soft labels), RMSprop(lr). Stochastic depth = identity (torchvision stub) and the FFN
+    Dropout(0.5) set to p=0, so the step is deterministic; the oracle covers both with explicit
+    draws. Also records eval-mode logits of the initial model (running statistics 0 / 1): after
+    the step the biases that feed a BatchNorm have moved by RMSprop's +-10*lr on rounding-level
+    gradients, which eval mode (no batch statistics to cancel them) would amplify."""
+    torch.manual_seed(0)
+    model = S.SkeletonTransformer(3, V, T, 11, 32, 6, 16, 8)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    state = sk.init_state(seed, V, T)
+    assert list(model.state_dict().keys()) == list(state.keys()), "oracle state_dict order differs"
+    model.load_state_dict(state, strict=True)
+    xs, label = sk.synthetic_clips(batch, V, 11, seed + 1, T=T, M=M)
+    x, lb = torch.from_numpy(xs), torch.from_numpy(label)
+    model.eval()
+    with torch.no_grad():
+        eval_out = model(x).numpy()
+    model.train()
+    opt = torch.optim.RMSprop(model.parameters(), lr=lr)
+    opt.zero_grad()
+    out = model(x)
+    loss = torch.nn.CrossEntropyLoss()(out, lb)
+    loss.backward()
+    d = {"seed": np.array([seed]), "V": np.array([V]), "T": np.array([T]), "M": np.array([M]), "x": xs,
+         "label": label, "lr": np.array([lr]), "out": out.detach().numpy(), "loss": np.array([loss.item()])}
+    nparams = 0
+    for name, p in model.named_parameters():
+        nparams += p.numel()
+        pack("grad:" + name, d, p.grad)
+    opt.step()
+    for name, p in model.named_parameters():
+        pack("post:" + name, d, p)
+    for name, b in model.named_buffers():
+        if name.endswith(("running_mean", "running_var")):
+            pack("buf:" + name, d, b)
+    d["eval_out"] = eval_out
+    d["nparams"] = np.array([nparams])
+    path = os.path.join(OUT, f"sktr_{tag}.npz")
+    np.savez_compressed(path, **d)
+    print(f"sktr {tag}: params={nparams} loss={loss.item():.6f} -> {path} ({os.path.getsize(path)//1024} KB)")
+    return nparams
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--sktr-only" in sys.argv:
+        S = import_sktr()
+        kat = json.load(open(os.path.join(OUT, "param_counts.json")))
+        kat["sktr"] = run_sktr_case("m1", S, 4, 8001)
+        run_sktr_case("m2", S, 3, 8002, M=2)
+        with open(os.path.join(OUT, "param_counts.json"), "w") as f:
+            json.dump(kat, f, indent=1, sort_keys=True)
+        return
     if "--targcn-only" in sys.argv:
         T = import_targcn()
         kat = json.load(open(os.path.join(OUT, "param_counts.json")))
@@ -213,6 +291,9 @@ def main():
     T = import_targcn()
     kat["targcn_v14"] = run_targcn_case("v14", T, 14, 4, 7001)
     kat["targcn_v17"] = run_targcn_case("v17", T, 17, 3, 7002)
+    S = import_sktr()
+    kat["sktr"] = run_sktr_case("m1", S, 4, 8001)
+    run_sktr_case("m2", S, 3, 8002, M=2)
     with open(os.path.join(OUT, "param_counts.json"), "w") as f:
         json.dump(kat, f, indent=1, sort_keys=True)
 
