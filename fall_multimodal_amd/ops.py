@@ -10,6 +10,10 @@ under torch.compile / FakeTensor tracing and composes with the rest of an autogr
   fall3::targcn_forward(net, params, buffers, source) -> (out, workspace)
         model(pts.permute(0,2,3,1)), TARGCN_HAR_conv_10kfold.ipynb cell 3 (TRAGCN.py:207-224)
   fall3::targcn_backward(net, params, buffers, dout, workspace) -> grads
+  fall3::sktr_forward(net, params, buffers, counters, x, training, sd, seed)
+        -> (out, workspace, new running buffers, new counters)
+        model(x), skeleton_transformer.py:418-435 (BASELINE config 5)
+  fall3::sktr_backward(net, params, dout, workspace) -> grads
   fall3::rmsprop_(param!, square_avg!, grad, lr, alpha, eps, scale)
         optimizer.step(), model/optimizer.py:21 (torch.optim.RMSprop semantics)
 
@@ -158,6 +162,61 @@ def _tg_backward(ctx, dout, dws):
 
 
 targcn_forward.register_autograd(_tg_backward, setup_context=_tg_setup)
+
+
+# ---------------------------------------------------------------------------------------------
+# SkeletonTransformer (f3_sktr)
+# ---------------------------------------------------------------------------------------------
+@torch.library.custom_op("fall3::sktr_forward", mutates_args=())
+def sktr_forward(net: int, params: List[Tensor], buffers: Tensor, counters: Tensor, x: Tensor, training: bool,
+                 sd: List[float], seed: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Functional like net_forward: returns the new BatchNorm3d running statistics / counters."""
+    m = _module(net)
+    N = x.shape[0]
+    ws = torch.empty(m._native.workspace_bytes(N), dtype=torch.uint8, device=x.device)
+    out = torch.empty(N, m.num_classes, dtype=torch.float32, device=x.device)
+    nb, nc = buffers.clone(), counters.clone()
+    m.native_forward(x, out, ws, training, sd, seed, buffers=nb, counters=nc)
+    return out, ws, nb, nc
+
+
+@sktr_forward.register_fake
+def _(net, params, buffers, counters, x, training, sd, seed):
+    m = _module(net)
+    N = x.shape[0]
+    return (x.new_empty(N, m.num_classes, dtype=torch.float32),
+            x.new_empty(m._native.workspace_bytes(N), dtype=torch.uint8), torch.empty_like(buffers),
+            torch.empty_like(counters))
+
+
+@torch.library.custom_op("fall3::sktr_backward", mutates_args=())
+def sktr_backward(net: int, params: List[Tensor], dout: Tensor, workspace: Tensor) -> Tensor:
+    m = _module(net)
+    grads = torch.empty(m._native.nparam, dtype=torch.float32, device=dout.device)
+    m.native_backward(dout.shape[0], dout.contiguous(), grads, workspace)
+    return grads
+
+
+@sktr_backward.register_fake
+def _(net, params, dout, workspace):
+    return dout.new_empty(_module(net)._native.nparam, dtype=torch.float32)
+
+
+def _sk_setup(ctx, inputs, output):
+    ctx.net, ctx.training = inputs[0], inputs[5]
+    ctx.save_for_backward(output[1])
+
+
+def _sk_backward(ctx, dout, dws, dbuf, dcnt):
+    if not ctx.training:
+        raise RuntimeError("fall3: backward through an eval-mode forward is not supported")
+    (ws,) = ctx.saved_tensors
+    m = _module(ctx.net)
+    grads = torch.ops.fall3.sktr_backward(ctx.net, list(m.parameters()), dout.float(), ws)
+    return None, _split_grads(m, grads), None, None, None, None, None, None
+
+
+sktr_forward.register_autograd(_sk_backward, setup_context=_sk_setup)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -179,6 +179,44 @@ int f3_targcn_backward(f3_targcn* net, int batch, const float* params, const flo
  * dout = dloss/dout. loss is overwritten. */
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream);
 
+/* ---- SkeletonTransformer (BASELINE config 5; skeleton_transformer.py) ----
+ * f3_sktr_create     <- SkeletonTransformer(3, V, T, num_class, 32, 6, 16, 8)   :360-416
+ *                       (GSTCAN_HAR_conv_kfold_trans.ipynb; V=14, T=30, 11 classes)
+ * f3_sktr_entry      <- model.state_dict() keys/shapes (same names, order, shapes): PARAM
+ *                       (16-B aligned offsets), BUFFER (BatchNorm3d running stats), COUNTER
+ *                       (num_batches_tracked, int64)
+ * f3_sktr_forward    <- out = model(x), x f32[N,3,T,V,M]                          :418-435
+ * f3_sktr_backward   <- loss.backward()
+ * Train mode randomness is explicit: sd = 18 stochastic-depth factors [block][spatial, temporal,
+ * ffn] (torchvision StochasticDepth(p, "batch"): 0 or 1/(1-p); NULL = all 1), and the FFN
+ * Dropout(dropout_p) mask comes from a counter hash of (dropout_seed, block, element) that the
+ * oracle reproduces (oracle/sktr_cpu.py dropout_keep). Eval mode: running statistics, no
+ * randomness. fp32 arithmetic throughout (fp32 MFMA GEMMs). */
+typedef struct f3_sktr_config {
+  int num_joint;   /* V: spatial attention length (14, 17, 18, 30, 32 supported) */
+  int frames;      /* T: temporal attention length (same set) */
+  int persons;     /* M >= 1 */
+  int num_class;   /* <= 64 */
+} f3_sktr_config;
+
+typedef struct f3_sktr f3_sktr;
+
+int f3_sktr_create(const f3_sktr_config* cfg, f3_sktr** out);
+void f3_sktr_destroy(f3_sktr* net);
+int f3_sktr_num_entries(const f3_sktr* net);
+int f3_sktr_entry(const f3_sktr* net, int i, const char** name, int* kind, int* ndim, int64_t* shape8,
+                  int64_t* offset);
+int64_t f3_sktr_param_count(const f3_sktr* net);
+int64_t f3_sktr_buffer_count(const f3_sktr* net);
+int64_t f3_sktr_counter_count(const f3_sktr* net);
+int64_t f3_sktr_workspace_bytes(const f3_sktr* net, int batch);
+int f3_sktr_forward(f3_sktr* net, int batch, int training, const float* params, float* buffers, int64_t* counters,
+                    const float* x, float* out, void* workspace, const float* sd, unsigned dropout_seed,
+                    float dropout_p, void* stream);
+/* grads (flat, params layout) are OVERWRITTEN; needs the last forward to have been a training one. */
+int f3_sktr_backward(f3_sktr* net, int batch, const float* params, const float* buffers, const float* dout,
+                     float* grads, void* workspace, void* stream);
+
 /* Debug accessor for tools/tests: device pointer of a per-layer workspace tensor
  * ("x","z","g","h","r","out","att","dh","dv","dg","dZ","dres","bn1_fsum",...) or NULL. */
 void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, int layer, const char* what);

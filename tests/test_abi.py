@@ -148,7 +148,8 @@ def test_custom_ops_registered_with_fake_kernels():
     import torch
     from torch._subclasses import FakeTensorMode
     import fall_multimodal_amd as f3
-    for op in ("net_forward", "net_backward", "targcn_forward", "targcn_backward", "rmsprop_"):
+    for op in ("net_forward", "net_backward", "targcn_forward", "targcn_backward", "sktr_forward", "sktr_backward",
+               "rmsprop_"):
         assert hasattr(torch.ops.fall3, op), op
     m = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device="cpu")
     t = f3.TARGCN(num_nodes=17, device="cpu")
@@ -163,3 +164,45 @@ def test_custom_ops_registered_with_fake_kernels():
         o2, w2 = torch.ops.fall3.targcn_forward(t._op_id, list(t.parameters()), t._flat_buffers,
                                                 torch.empty(4, 30, 17, 3))
         assert tuple(o2.shape) == (4, 11) and w2.numel() == t._native.workspace_bytes(4)
+        k = f3.SkeletonTransformer(device="cpu")
+        o3, w3, b3, c3 = torch.ops.fall3.sktr_forward(k._op_id, list(k.parameters()), k._flat_buffers, k._counters,
+                                                      torch.empty(6, 3, 30, 14, 1), True, [1.0] * 18, 7)
+        assert tuple(o3.shape) == (6, 11) and w3.numel() == k._native.workspace_bytes(6)
+        assert torch.ops.fall3.sktr_backward(k._op_id, list(k.parameters()), o3, w3).numel() == k._native.nparam
+
+
+@pytest.mark.parametrize("V,T,M", [(14, 30, 1), (17, 30, 2), (18, 32, 1)])
+def test_sktr_entry_table_matches_reference_state_dict(V, T, M):
+    """f3_sktr_entry: SkeletonTransformer(3, V, T, 11, 32, 6, 16, 8)'s exact state_dict keys, order and
+    shapes (skeleton_transformer.py:360-416, checked against the reference module by
+    tools/gen_golden.py), 262,091 parameters at V=14/T=30, 16-B aligned parameter offsets, BatchNorm3d
+    running statistics as buffers and num_batches_tracked as int64 counters."""
+    from oracle import sktr_cpu as sk
+    from fall_multimodal_amd.sktr import _NativeSktr
+    net = _NativeSktr(V, T, M, 11)
+    ref = sk.param_shapes(V, T)
+    assert [n for n, k, sh, off in net.entries] == list(ref.keys())
+    nparam = 0
+    for n, kind, sh, off in net.entries:
+        assert tuple(sh) == tuple(ref[n]), n
+        if n.endswith("num_batches_tracked"):
+            assert kind == 2, n
+        else:
+            assert (kind == 1) == sk.is_buffer(n), n
+        if kind == 0:
+            assert off % 4 == 0, n
+            nparam += int(np.prod(sh))
+    if (V, T) == (14, 30):
+        assert nparam == 262091
+    assert net.ncnt == 18 and net.nbuf == 18 * 2 * 32
+    assert net.workspace_bytes(64) > net.workspace_bytes(4) > 0
+
+
+def test_sktr_rejects_unsupported_configs():
+    from fall_multimodal_amd.sktr import SkeletonTransformer, _NativeSktr
+    with pytest.raises(RuntimeError):
+        _NativeSktr(20, 30, 1, 11)   # attention length without a compiled kernel
+    with pytest.raises(RuntimeError):
+        _NativeSktr(14, 30, 0, 11)
+    with pytest.raises(NotImplementedError):
+        SkeletonTransformer(embedding_dim=64, device="cpu")

@@ -1,0 +1,151 @@
+"""SkeletonTransformer (BASELINE config 5) HIP path vs the reference's golden vectors and the CPU oracle.
+
+Golden fixtures come from the reference's own SkeletonTransformer (tools/gen_golden.py, stochastic
+depth = identity, FFN dropout p=0); the oracle (oracle/sktr_cpu.py) is pinned to them by
+tests/test_oracle_golden.py and reproduces the kernels' dropout mask and stochastic-depth draws.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sktr_cpu as sk
+from tests.golden_util import GOLDEN, check_packed
+
+pytestmark = pytest.mark.gpu
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda")
+
+
+def _golden(tag):
+    z = np.load(os.path.join(GOLDEN, f"sktr_{tag}.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def _grad_tol(g):
+    # 1e-3 of the tensor's max |g| (fp32 reassociation through six BatchNorm3d backward passes),
+    # floored at 1e-5 for the biases that feed a BatchNorm (exact gradient zero, rounding noise)
+    return 1e-3 * max(float(np.abs(g).max()), 1e-2)
+
+
+@pytest.mark.parametrize("tag", ["m1", "m2"])
+def test_sktr_train_step_matches_reference_golden(tag):
+    """The drop-in module driven as the notebook drives it (model(x) -> CrossEntropyLoss ->
+    backward -> RMSprop) vs the reference's own outputs: eval logits of the initial model, train
+    logits within 1e-3 with identical argmax, loss 1e-5, gradients, BatchNorm3d running stats."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    g = _golden(tag)
+    V, T, M = int(g["V"][0]), int(g["T"][0]), int(g["M"][0])
+    st = sk.init_state(int(g["seed"][0]), V, T)
+    model = f3.SkeletonTransformer(n_joints=V, seq_len=T, persons=M, device=d, dropout_p=0.0,
+                                   stochastic_depth=False)
+    model.load_state_dict(st, strict=True)
+    x = torch.from_numpy(g["x"]).to(d)
+    label = torch.from_numpy(g["label"]).to(d)
+    model.eval()
+    with torch.no_grad():
+        ev = model(x).cpu().numpy()
+    assert np.abs(ev - g["eval_out"]).max() < 1e-3
+    model.train()
+    out = model(x)
+    o = out.detach().cpu().numpy()
+    err = float(np.abs(o - g["out"]).max())
+    assert err < 1e-3, err
+    assert (o.argmax(1) == g["out"].argmax(1)).all()
+    loss = torch.nn.CrossEntropyLoss()(out, label)
+    np.testing.assert_allclose(loss.item(), g["loss"][0], rtol=0, atol=1e-5)
+    opt = f3.RMSprop(model.parameters(), lr=float(g["lr"][0]))
+    opt.zero_grad()
+    loss.backward()
+    for name, p in model.named_parameters():
+        gr = p.grad.detach().cpu().numpy()
+        check_packed(g, "grad:" + name, gr, rtol=1e-3, atol=_grad_tol(gr), what=tag + " ")
+    for name, b in model.named_buffers():
+        if name.endswith(("running_mean", "running_var")):
+            check_packed(g, "buf:" + name, b.cpu().numpy(), rtol=1e-4, atol=1e-6, what=tag + " ")
+        if name.endswith("num_batches_tracked"):
+            assert int(b.item()) == 1
+    print(f"sktr {tag}: max|dlogit| {err:.2e}, eval max|dlogit| {np.abs(ev - g['eval_out']).max():.2e}")
+
+
+def _oracle(st, x, label, sd, seed, lr=1e-3):
+    return sk.train_step({k: v.clone() for k, v in st.items()}, torch.from_numpy(x), torch.from_numpy(label),
+                         lr=lr, sd=[sd[3 * b:3 * b + 3] for b in range(6)], dropout_seed=seed)
+
+
+@pytest.mark.parametrize("B", [16, 256])
+def test_sktr_step_with_dropout_and_stochastic_depth_vs_oracle(B):
+    """SktrStep with the reference's train-mode randomness (FFN Dropout(0.5) hash mask, stochastic
+    depth draws incl. dropped branches) vs the oracle given the same draws: logits within 1e-3,
+    identical argmax, loss 1e-5, every gradient within 2e-3 of its tensor's max (floored), whole-
+    gradient cosine >= 0.99999."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    st = sk.init_state(31)
+    x, label = sk.synthetic_clips(B, 14, 11, 77)
+    model = f3.SkeletonTransformer(device=d)
+    model.load_state_dict(st)
+    step = f3.SktrStep(model, B)
+    sd = [1.0, 1.0, 1.0, 0.0, 1.25, 1.25, 1.5, 1.5, 0.0, 2.0, 0.0, 2.0, 1.0 / 0.6, 1.0 / 0.6, 1.0 / 0.6, 0.0, 2.0, 2.0]
+    seed = 12345
+    step.forward_backward(torch.from_numpy(x).to(d), torch.from_numpy(label).to(d), sd=sd, seed=seed)
+    out_ref, loss_ref, grads_ref = _oracle(st, x, label, sd, seed)
+    out = step.out.cpu().numpy()
+    err = float(np.abs(out - out_ref.numpy()).max())
+    ours = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters()}
+    rel = {k: float(np.abs(ours[k] - grads_ref[k].numpy()).max() / max(np.abs(grads_ref[k].numpy()).max(), 1e-2))
+           for k in grads_ref}
+    a = np.concatenate([ours[k].reshape(-1) for k in grads_ref]).astype(np.float64)
+    r = np.concatenate([grads_ref[k].numpy().reshape(-1) for k in grads_ref]).astype(np.float64)
+    cos = float(a @ r / (np.linalg.norm(a) * np.linalg.norm(r)))
+    worst = max(rel, key=rel.get)
+    print(f"sktr step B={B}: max|dlogit| {err:.2e}, loss {step.loss.item():.6f} vs {loss_ref.item():.6f}, "
+          f"grad cosine {cos:.7f}, worst grad rel {rel[worst]:.2e} ({worst})")
+    assert err < 1e-3 and (out.argmax(1) == out_ref.numpy().argmax(1)).all()
+    assert abs(step.loss.item() - loss_ref.item()) < 1e-5
+    assert rel[worst] < 2e-3, (worst, rel[worst])
+    assert cos >= 0.99999
+
+
+def test_sktr_training_tracks_oracle():
+    """Five fused steps (RMSprop lr 1e-3, dropout + stochastic depth drawn by the module): the loss
+    trajectory follows the oracle's (1e-4) and the trained models agree on held-out clips (train-
+    mode logits without randomness, 1e-3). Eval mode is not compared after training: the biases
+    that feed a BatchNorm have exactly zero gradient, so RMSprop moves them by +-10*lr on rounding
+    noise, differently in any two implementations; batch statistics cancel that, running ones do not."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    B, steps = 12, 5
+    st = sk.init_state(41)
+    batches = [sk.synthetic_clips(B, 14, 11, 500 + i) for i in range(2)]
+    model = f3.SkeletonTransformer(device=d, seed=3)
+    model.load_state_dict(st)
+    step = f3.SktrStep(model, B)
+    ref = {k: v.clone() for k, v in st.items()}
+    sq = None
+    for i in range(steps):
+        x, lab = batches[i % 2]
+        loss = step(torch.from_numpy(x).to(d), torch.from_numpy(lab).to(d)).item()
+        sd, seed = step.last_draws
+        if sq is None:
+            sq = {k: torch.zeros_like(v) for k, v in ref.items() if not sk.is_buffer(k)}
+        _, loss_ref, _ = sk.train_step(ref, torch.from_numpy(x), torch.from_numpy(lab), sq=sq,
+                                       sd=[sd[3 * b:3 * b + 3] for b in range(6)], dropout_seed=seed)
+        assert abs(loss - loss_ref.item()) < 1e-4, (i, loss, loss_ref.item())
+    object.__setattr__(model, "dropout_p", 0.0)
+    object.__setattr__(model, "stochastic_depth", False)
+    x, _ = sk.synthetic_clips(32, 14, 11, 999)
+    with torch.no_grad():
+        out = model(torch.from_numpy(x).to(d)).cpu().numpy()
+        out_ref = sk.forward(ref, torch.from_numpy(x), training=True).numpy()
+    err = float(np.abs(out - out_ref).max())
+    print(f"sktr after {steps} steps: held-out max|dlogit| {err:.2e}")
+    assert err < 1e-3 and (out.argmax(1) == out_ref.argmax(1)).all()
