@@ -50,9 +50,9 @@ def parse():
                         "step: 10.1 vs 8.15 ms at B=256; see DESIGN.md)")
     p.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old commands
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--model", default="fall3", choices=("fall3", "targcn"),
-                   help="fall3: the headline 3-stream step (default). targcn: BASELINE config 2 alone")
-    p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN line in the default run")
+    p.add_argument("--model", default="fall3", choices=("fall3", "targcn", "sktr"),
+                   help="fall3: the headline 3-stream step (default). targcn / sktr: BASELINE config 2 / 5 alone")
+    p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN and config-5 lines in the default run")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
 
@@ -291,6 +291,46 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
     return rec
 
 
+def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
+    """BASELINE config 5: SkeletonTransformer(3, 14, 30, 11, 32, 6, 16, 8) training step (fwd + CE +
+    bwd + RMSprop, train-mode FFN dropout and stochastic depth) at B=256 on one GPU, fp32 (fp32 MFMA
+    GEMMs), synthetic clips, random-init weights. The 10-fold CV shards folds over GPUs as independent
+    replicas (no collective), so per-GPU throughput is the whole story."""
+    import fall_multimodal_amd as f3
+    from oracle import sktr_cpu as sk
+    x, lab = sk.synthetic_clips(B, 14, 11, 3)
+    model = f3.SkeletonTransformer(device=dev)
+    step = f3.SktrStep(model, B)
+    xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
+    for _ in range(warmup):
+        step(xd, yd)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(xd, yd)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    rec = {"metric": "clips/sec (fwd+bwd) SkeletonTransformer, B=256, 1 GPU (one CV fold)", "value": round(B / dt, 1),
+           "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32", "steps": steps,
+           "config": {"workload": f"sktr_V14_T30_M1_B{B}", "global_batch": B, "joints": 14, "frames": 30,
+                      "blocks": 6, "heads": 8, "parallelism": "replicas (10-fold CV, one fold per GPU)"},
+           "final_loss": round(float(step.loss.item()), 5)}
+    if cpu_seconds > 0:  # the oracle (pinned to the reference) on this host's cores
+        threads = cpu_threads()
+        torch.set_num_threads(threads)
+        st = sk.init_state(7)
+        xc, lc = torch.from_numpy(x), torch.from_numpy(lab)
+        sk.train_step(st, xc[:16], lc[:16])
+        t0, n = time.perf_counter(), 0
+        while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 10):
+            sk.train_step(st, xc, lc)
+            n += 1
+        rec["cpu_baseline"] = {"value": round(B * n / (time.perf_counter() - t0), 2), "unit": "clips/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{n} oracle train steps of B={B}, fp32, torch CPU"}
+    return rec
+
+
 def cpu_threads():
     """The CPU share this process may use: OMP_NUM_THREADS (16 on the GPU box, whose nproc shows
     the whole machine), else every core here."""
@@ -341,6 +381,11 @@ def main():
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
+    if a.model == "sktr":
+        rec = sktr_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        return
     V = 18 if a.layout == "coco_mmpose" else 14
     B, S, C = a.batch, a.sensor_dim, 11
     model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev,
@@ -373,6 +418,7 @@ def main():
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    skrec = sktr_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
     if rank == 0:
@@ -407,6 +453,7 @@ def main():
             "eval_forward": ev,
             "main_py_autograd_path": agp,
             "cfg2_targcn": tgrec,
+            "cfg5_sktr": skrec,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

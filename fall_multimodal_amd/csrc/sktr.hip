@@ -150,6 +150,38 @@ F3_DEV long long seq_row(const AttnArgs& a, int s, int l, int L) {
   return (long long)s * L + l;
 }
 
+// one thread per (head, query) row, rounded up to whole waves (the launch's block size)
+constexpr int attn_threads(int L) { return (HEADS * L + 63) / 64 * 64; }
+
+// 16-wide rows in LDS are read as four 16-B vectors (ds_read_b128)
+F3_DEV f32x4 l4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+F3_DEV void load16(f32x4 (&r)[4], const float* p) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r[u] = l4(p + 4 * u);
+}
+F3_DEV float dot16(const f32x4 (&a)[4], const float* p) {  // four independent chains
+  f32x4 acc = a[0] * l4(p);
+#pragma unroll
+  for (int u = 1; u < 4; ++u) {
+    const f32x4 b = l4(p + 4 * u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = fmaf(a[u][e], b[e], acc[e]);
+  }
+  return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+F3_DEV void axpy16(f32x4 (&acc)[4], float s, const float* p) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const f32x4 b = l4(p + 4 * u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[u][e] = fmaf(s, b[e], acc[u][e]);
+  }
+}
+F3_DEV void zero16(f32x4 (&r)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 template <int L>
 __global__ __launch_bounds__(256) void sk_attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -159,37 +191,37 @@ __global__ __launch_bounds__(256) void sk_attn_fwd_kernel(AttnArgs a) {
   float* Tb = Vs + L * DM;             // [2L-1][16]
   float* Ps = Tb + (2 * L - 1) * HD;   // [H][L][L+1] score / probability rows
   const int s = blockIdx.x;
-  for (int e = threadIdx.x; e < L * 64; e += blockDim.x) {
-    const int l = e >> 6, c4 = e & 63;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(a.qkv + seq_row(a, s, l, L) * QKV + DM + c4 * 4);
-    float* dst = c4 < 32 ? Ks + l * DM + c4 * 4 : Vs + l * DM + (c4 - 32) * 4;
-    *reinterpret_cast<f32x4*>(dst) = v;
+  {  // all of the thread's 16-B loads in flight before the LDS writes
+    constexpr int NPT = (L * 64 + attn_threads(L) - 1) / attn_threads(L);
+    f32x4 buf[NPT];
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = min((int)threadIdx.x + q * (int)blockDim.x, L * 64 - 1);
+      const int l = e >> 6, c4 = e & 63;
+      buf[q] = *reinterpret_cast<const f32x4*>(a.qkv + seq_row(a, s, l, L) * QKV + DM + c4 * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = threadIdx.x + q * blockDim.x;
+      if (e < L * 64) {
+        const int l = e >> 6, c4 = e & 63;
+        float* dst = c4 < 32 ? Ks + l * DM + c4 * 4 : Vs + l * DM + (c4 - 32) * 4;
+        *reinterpret_cast<f32x4*>(dst) = buf[q];
+      }
+    }
   }
   for (int e = threadIdx.x; e < (2 * L - 1) * HD; e += blockDim.x) Tb[e] = a.table[e];
   __syncthreads();
   const int h = threadIdx.x / L, i = threadIdx.x - h * L;
   if (h >= HEADS) return;
   const long long ri = seq_row(a, s, i, L);
-  float q[HD];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const f32x4 t = *reinterpret_cast<const f32x4*>(a.qkv + ri * QKV + h * HD + 4 * u);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) q[4 * u + e] = t[e];
-  }
+  f32x4 q[4];
+  load16(q, a.qkv + ri * QKV + h * HD);
   float* Sr = Ps + (h * L + i) * LP;
   float mx = -INFINITY;
 #pragma unroll 2
   for (int j = 0; j < L; ++j) {
-    const float* kr = Ks + j * DM + h * HD;
-    const float* tr = Tb + (i - j + L - 1) * HD;
-    float d1 = 0.f, d2 = 0.f;
-#pragma unroll
-    for (int d = 0; d < HD; ++d) {
-      d1 = fmaf(q[d], kr[d], d1);
-      d2 = fmaf(q[d], tr[d], d2);
-    }
-    const float sc = d1 * a.scale + d2;
+    const float sc = dot16(q, Ks + j * DM + h * HD) * a.scale + dot16(q, Tb + (i - j + L - 1) * HD);
     Sr[j] = sc;
     mx = fmaxf(mx, sc);
   }
@@ -201,19 +233,12 @@ __global__ __launch_bounds__(256) void sk_attn_fwd_kernel(AttnArgs a) {
     sum += e;
   }
   const float inv = 1.f / sum;
-  float o[HD];
-#pragma unroll
-  for (int d = 0; d < HD; ++d) o[d] = 0.f;
+  f32x4 o[4];
+  zero16(o);
 #pragma unroll 2
-  for (int j = 0; j < L; ++j) {
-    const float p = Sr[j] * inv;
-    const float* vr = Vs + j * DM + h * HD;
+  for (int j = 0; j < L; ++j) axpy16(o, Sr[j] * inv, Vs + j * DM + h * HD);
 #pragma unroll
-    for (int d = 0; d < HD; ++d) o[d] = fmaf(p, vr[d], o[d]);
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    *reinterpret_cast<f32x4*>(a.o + ri * DM + h * HD + 4 * u) = f32x4{o[4 * u], o[4 * u + 1], o[4 * u + 2], o[4 * u + 3]};
+  for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4*>(a.o + ri * DM + h * HD + 4 * u) = o[u];
 }
 
 template <int L>
@@ -226,7 +251,8 @@ constexpr size_t attn_bwd_lds() {
 }
 
 // backward: phase 1 rows (h, i): P, dP = dO v^T, dS = P (dP - rowsum(P dP)), dq;
-// phase 2 columns (h, j): dk = scale dS^T q, dv = P^T dO; phase 3: table partial sums.
+// phase 2 columns (h, j): dk = scale dS^T q, dv = P^T dO; phase 3 (r, h): the table gradient
+// sum_{i, j = i - r + L - 1} dS[h][i][j] q_i, summed over heads with LDS atomics.
 template <int L>
 __global__ __launch_bounds__(256) void sk_attn_bwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -234,44 +260,46 @@ __global__ __launch_bounds__(256) void sk_attn_bwd_kernel(AttnArgs a) {
   float* Ks = Qs + L * DM;
   float* Vs = Ks + L * DM;
   float* Os = Vs + L * DM;              // dO
-  float* Tb = Os + L * DM;              // [2L-1][16]
+  float* Tb = Os + L * DM;              // [2L-1][16]; the table gradient after phase 1
   float* Ps = Tb + (2 * L - 1) * HD;    // [H][L][L+1]
   float* Ss = Ps + HEADS * L * (L + 1); // [H][L][L+1]
-  constexpr int LP = L + 1;
+  constexpr int LP = L + 1, NT = (2 * L - 1) * HD;
   const int s = blockIdx.x;
-  for (int e = threadIdx.x; e < L * 128; e += blockDim.x) {
-    const int l = e >> 7, c4 = e & 127;
-    const long long r = seq_row(a, s, l, L);
-    if (c4 < 96) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(a.qkv + r * QKV + c4 * 4);
-      const int part = c4 >> 5, c = (c4 & 31) * 4;
-      *reinterpret_cast<f32x4*>(Qs + part * L * DM + l * DM + c) = v;
-    } else {
-      const int c = (c4 - 96) * 4;
-      *reinterpret_cast<f32x4*>(Os + l * DM + c) = *reinterpret_cast<const f32x4*>(a.dout + r * DM + c);
+  {  // all of the thread's 16-B loads in flight before the LDS writes
+    constexpr int NPT = (L * 128 + attn_threads(L) - 1) / attn_threads(L);
+    f32x4 buf[NPT];
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = min((int)threadIdx.x + q * (int)blockDim.x, L * 128 - 1);
+      const int l = e >> 7, c4 = e & 127;
+      const long long r = seq_row(a, s, l, L);
+      buf[q] = c4 < 96 ? *reinterpret_cast<const f32x4*>(a.qkv + r * QKV + c4 * 4)
+                       : *reinterpret_cast<const f32x4*>(a.dout + r * DM + (c4 - 96) * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = threadIdx.x + q * blockDim.x;
+      if (e < L * 128) {
+        const int l = e >> 7, c4 = e & 127;
+        float* dst = c4 < 96 ? Qs + (c4 >> 5) * L * DM + l * DM + (c4 & 31) * 4 : Os + l * DM + (c4 - 96) * 4;
+        *reinterpret_cast<f32x4*>(dst) = buf[q];
+      }
     }
   }
-  for (int e = threadIdx.x; e < (2 * L - 1) * HD; e += blockDim.x) Tb[e] = a.table[e];
+  for (int e = threadIdx.x; e < NT; e += blockDim.x) Tb[e] = a.table[e];
   __syncthreads();
   const int h = threadIdx.x / L, i = threadIdx.x - h * L;
   const bool act = h < HEADS;
   if (act) {
-    const float* q = Qs + i * DM + h * HD;
-    const float* go = Os + i * DM + h * HD;
+    f32x4 q[4], go[4];
+    load16(q, Qs + i * DM + h * HD);
+    load16(go, Os + i * DM + h * HD);
     float* Pr = Ps + (h * L + i) * LP;
     float* Sr = Ss + (h * L + i) * LP;
     float mx = -INFINITY;
 #pragma unroll 2
     for (int j = 0; j < L; ++j) {
-      const float* kr = Ks + j * DM + h * HD;
-      const float* tr = Tb + (i - j + L - 1) * HD;
-      float d1 = 0.f, d2 = 0.f;
-#pragma unroll
-      for (int d = 0; d < HD; ++d) {
-        d1 = fmaf(q[d], kr[d], d1);
-        d2 = fmaf(q[d], tr[d], d2);
-      }
-      const float sc = d1 * a.scale + d2;
+      const float sc = dot16(q, Ks + j * DM + h * HD) * a.scale + dot16(q, Tb + (i - j + L - 1) * HD);
       Pr[j] = sc;
       mx = fmaxf(mx, sc);
     }
@@ -288,67 +316,58 @@ __global__ __launch_bounds__(256) void sk_attn_bwd_kernel(AttnArgs a) {
     for (int j = 0; j < L; ++j) {
       const float p = Pr[j] * inv;
       Pr[j] = p;
-      const float* vr = Vs + j * DM + h * HD;
-      float dp = 0.f;
-#pragma unroll
-      for (int d = 0; d < HD; ++d) dp = fmaf(go[d], vr[d], dp);
+      const float dp = dot16(go, Vs + j * DM + h * HD);
       Sr[j] = dp;
       dsum = fmaf(p, dp, dsum);
     }
-    float dq[HD];
-#pragma unroll
-    for (int d = 0; d < HD; ++d) dq[d] = 0.f;
+    f32x4 dq[4], dqt[4];
+    zero16(dq);
+    zero16(dqt);
 #pragma unroll 2
     for (int j = 0; j < L; ++j) {
       const float ds = Pr[j] * (Sr[j] - dsum);
       Sr[j] = ds;
-      const float* kr = Ks + j * DM + h * HD;
-      const float* tr = Tb + (i - j + L - 1) * HD;
-#pragma unroll
-      for (int d = 0; d < HD; ++d) dq[d] = fmaf(ds, fmaf(a.scale, kr[d], tr[d]), dq[d]);
+      axpy16(dq, ds, Ks + j * DM + h * HD);
+      axpy16(dqt, ds, Tb + (i - j + L - 1) * HD);
     }
     const long long ri = seq_row(a, s, i, L);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      *reinterpret_cast<f32x4*>(a.dqkv + ri * QKV + h * HD + 4 * u) =
-          f32x4{dq[4 * u], dq[4 * u + 1], dq[4 * u + 2], dq[4 * u + 3]};
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4*>(a.dqkv + ri * QKV + h * HD + 4 * u) = dq[u] * a.scale + dqt[u];
   }
   __syncthreads();
   if (act) {
     const int j = i;
-    float dk[HD], dv[HD];
-#pragma unroll
-    for (int d = 0; d < HD; ++d) dk[d] = dv[d] = 0.f;
+    f32x4 dk[4], dv[4];
+    zero16(dk);
+    zero16(dv);
 #pragma unroll 2
     for (int ii = 0; ii < L; ++ii) {
-      const float sv = Ss[(h * L + ii) * LP + j], pv = Ps[(h * L + ii) * LP + j];
-      const float* q = Qs + ii * DM + h * HD;
-      const float* go = Os + ii * DM + h * HD;
-#pragma unroll
-      for (int d = 0; d < HD; ++d) {
-        dk[d] = fmaf(sv, q[d], dk[d]);
-        dv[d] = fmaf(pv, go[d], dv[d]);
-      }
+      axpy16(dk, Ss[(h * L + ii) * LP + j], Qs + ii * DM + h * HD);
+      axpy16(dv, Ps[(h * L + ii) * LP + j], Os + ii * DM + h * HD);
     }
     const long long rj = seq_row(a, s, j, L);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      *reinterpret_cast<f32x4*>(a.dqkv + rj * QKV + DM + h * HD + 4 * u) =
-          f32x4{dk[4 * u] * a.scale, dk[4 * u + 1] * a.scale, dk[4 * u + 2] * a.scale, dk[4 * u + 3] * a.scale};
-      *reinterpret_cast<f32x4*>(a.dqkv + rj * QKV + 2 * DM + h * HD + 4 * u) =
-          f32x4{dv[4 * u], dv[4 * u + 1], dv[4 * u + 2], dv[4 * u + 3]};
+      *reinterpret_cast<f32x4*>(a.dqkv + rj * QKV + DM + h * HD + 4 * u) = dk[u] * a.scale;
+      *reinterpret_cast<f32x4*>(a.dqkv + rj * QKV + 2 * DM + h * HD + 4 * u) = dv[u];
     }
   }
-  // d table[r][d] = sum_{h, i, j = i - r + L - 1} dS[h][i][j] q_i[h*16 + d]
-  float* dt = a.dtab + (long long)s * (2 * L - 1) * HD;
-  for (int idx = threadIdx.x; idx < (2 * L - 1) * HD; idx += blockDim.x) {
-    const int r = idx / HD, d = idx - r * HD;
+  for (int e = threadIdx.x; e < NT; e += blockDim.x) Tb[e] = 0.f;   // table gradient accumulator
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < (2 * L - 1) * HEADS; idx += blockDim.x) {
+    const int r = idx / HEADS, hh = idx - r * HEADS;
     const int i0 = max(0, r - L + 1), i1 = min(L - 1, r);
-    float acc = 0.f;
-    for (int hh = 0; hh < HEADS; ++hh)
-      for (int ii = i0; ii <= i1; ++ii) acc = fmaf(Ss[(hh * L + ii) * LP + ii - r + L - 1], Qs[ii * DM + hh * HD + d], acc);
-    dt[idx] = acc;
+    f32x4 acc[4];
+    zero16(acc);
+    for (int ii = i0; ii <= i1; ++ii) axpy16(acc, Ss[(hh * L + ii) * LP + ii - r + L - 1], Qs + ii * DM + hh * HD);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(Tb + r * HD + 4 * u + e, acc[u][e]);
   }
+  __syncthreads();
+  float* dt = a.dtab + (long long)s * NT;
+  for (int e = threadIdx.x; e < NT; e += blockDim.x) dt[e] = Tb[e];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -564,7 +583,7 @@ static int launch_attn(const AttnArgs& a, bool bwd, hipStream_t s) {
     return true;
   }();
   (void)once;
-  const int threads = (HEADS * L + 63) / 64 * 64;
+  const int threads = attn_threads(L);
   if (bwd)
     hipLaunchKernelGGL(sk_attn_bwd_kernel<L>, dim3(a.nseq), dim3(threads), attn_bwd_lds<L>(), s, a);
   else
