@@ -414,6 +414,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(step.loss.item())
+    phased = None
+    if world == 1 and rank == 0:  # the data-parallel two-phase backward's own cost, measured on one GPU
+        step.phased = True
+        for _ in range(2):
+            step(sk, se, lb)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            step(sk, se, lb)
+        torch.cuda.synchronize()
+        step.phased = False
+        pm = (time.perf_counter() - t1) / a.steps * 1e3
+        phased = {"ms_per_step": round(pm, 3), "vs_phase0": round(pm / (dt / a.steps * 1e3), 4),
+                  "note": "backward as phase 1 (head, sensor, layers 4-6) + phase 2 (layers 0-3), the DP path "
+                          "without the collective; phase 0 = the one-pass backward the N=1 value uses"}
     ev = eval_throughput(model, sk, se) if rank == 0 else None
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
@@ -451,6 +466,7 @@ def main():
                 "note": "whole step (fwd+bwd conv/einsum/addmm FLOPs, SURVEY 8d) / ms_per_step / dense peak"},
             "sensor": sens,
             "eval_forward": ev,
+            "dp_phased_backward": phased,
             "main_py_autograd_path": agp,
             "cfg2_targcn": tgrec,
             "cfg5_sktr": skrec,

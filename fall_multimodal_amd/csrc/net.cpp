@@ -83,10 +83,16 @@ struct f3_net {
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_main[2][7] = {};  // per (skeleton stream, layer) main -> side hand-offs
+  // end of backward phase 1 on each queue it used ([0..2] aux, [3] the caller's stream): the
+  // gradient all-reduce of the phase-1 bucket waits on these instead of the caller's stream
+  // joining every queue, so phase 2's critical path starts while phase 1's weight gradients drain
+  hipEvent_t ev_p1[4] = {nullptr, nullptr, nullptr, nullptr};
+  int p1_mask = 0;  // bit i: ev_p1[i] recorded by the last phase-1 backward
   bool par_init = false, par_ok = false;
   ~f3_net() {
     for (auto& a : aux) if (a) (void)hipStreamDestroy(a);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ev_p1) if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i)
       for (int l = 0; l < 7; ++l) {
         if (ev_main[i][l]) (void)hipEventDestroy(ev_main[i][l]);
@@ -915,6 +921,7 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   bool ok = true;
   for (auto& a : n.aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
   for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < 2; ++i)
     for (int l = 0; l < 7; ++l) {
       ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], hipEventDisableTiming) == hipSuccess;
@@ -960,7 +967,29 @@ struct Branches {
     }
     return F3_OK;
   }
+  // end of backward phase 1: record where every queue is instead of joining them into s
+  int mark_phase1() {
+    n.p1_mask = 0;
+    for (auto& e : n.ev_p1)  // (serial mode never created the branch events)
+      if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return F3_EHIP;
+    for (int i = 0; i < 3 && par; ++i) {
+      if (!(mask >> i & 1)) continue;
+      if (hipEventRecord(n.ev_p1[i], n.aux[i]) != hipSuccess) return F3_EHIP;
+      n.p1_mask |= 1 << i;
+    }
+    if (hipEventRecord(n.ev_p1[3], s) != hipSuccess) return F3_EHIP;
+    n.p1_mask |= 8;
+    return F3_OK;
+  }
 };
+
+// stream `t` waits for everything backward phase 1 queued (no-op after a serial phase 1, whose
+// work is all on the caller's stream)
+int wait_phase1(f3_net& n, hipStream_t t) {
+  for (int i = 0; i < 4; ++i)
+    if ((n.p1_mask >> i & 1) && hipStreamWaitEvent(t, n.ev_p1[i], 0) != hipSuccess) return F3_EHIP;
+  return F3_OK;
+}
 
 }  // namespace
 
@@ -1176,10 +1205,16 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
   };
   if (phase == 2) {
     Branches br{*net, s, ensure_parallel(*net, s)};
-    br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->nstreams > 0 ? BR_SIDE : 0);
+    // the same queue assignment as phase 1 (mask incl. the sensor queue, which carries the motion
+    // stream's weight gradients): a stream's split-K slab is then only ever used from one queue,
+    // so phase 2's weight gradients cannot overlap phase 1's still-draining ones on that slab
+    br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) |
+              (net->nstreams > 0 ? BR_SIDE : 0);
     F3_TRY(br.fork());
     F3_TRY(skeleton(br, kSplitLayer - 1, 0));
     F3_TRY(br.join());
+    F3_TRY(wait_phase1(*net, s));  // phase 1's queues (e.g. the sensor queue) are done too
+    net->p1_mask = 0;
     return F3_OK;
   }
   if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
@@ -1211,8 +1246,14 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     }
   }
   F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0));
+  if (phase == 1) return br.mark_phase1();  // the caller orders its all-reduce after f3_net_wait_phase1
   F3_TRY(br.join());
   return F3_OK;
+}
+
+int f3_net_wait_phase1(f3_net* net, void* stream) {
+  if (!net) return F3_EINVAL;
+  return wait_phase1(*net, (hipStream_t)stream);
 }
 
 int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_t n, float lr, float alpha,

@@ -6,12 +6,16 @@ buffer preallocated, so it can be captured into HIP graphs and replayed per batc
 
 Data parallel: one process per GPU. Gradients live in ONE flat fp32 buffer whose layout
 puts the parameters the first backward phase finalises (head, sensor branch, skeleton
-layers 4-6; f3_net_grad_split) first. Their all-reduce (RCCL, sum) is issued as soon as
-phase 1 ends and runs on the process group's communication stream WHILE phase 2 (layers
-0-3, data_bn) computes; the remainder follows. 1/world is applied inside the RMSprop
-kernel. BatchNorm statistics stay per-rank (the reference's per-device batch semantics).
+layers 4-6; f3_net_grad_split) first. Phase 1 returns without joining its private queues:
+the head bucket's all-reduce (RCCL, sum) is issued from a side stream that waits on phase
+1's per-queue events (f3_net_wait_phase1), so phase 2's critical path (layers 0-3, data_bn)
+starts at once while phase 1's weight gradients drain and the all-reduce runs; the remainder
+follows phase 2. 1/world is applied inside the RMSprop kernel. BatchNorm statistics stay
+per-rank (the reference's per-device batch semantics).
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 import torch
@@ -22,12 +26,16 @@ from ._lib import check, lib, ptr, stream_handle
 
 class GradSync:
     """Two-bucket gradient all-reduce over a flat buffer: `head` = grads[:split] (final after
-    backward phase 1), `tail` = grads[split:]. Both are issued async on the group's
-    communication stream; `finish()` orders the caller's stream after them."""
+    backward phase 1), `tail` = grads[split:]. Both are issued async; `finish()` orders the
+    caller's stream after them. `wait_phase1(stream_handle)` (optional) makes a stream wait for
+    the phase-1 gradients: the head bucket is then issued from a side stream ordered after them
+    rather than after everything on the caller's stream."""
 
-    def __init__(self, grads: torch.Tensor, split: int, group=None):
+    def __init__(self, grads: torch.Tensor, split: int, group=None, wait_phase1=None):
         self.grads, self.split, self.group = grads, int(split), group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.wait_phase1 = wait_phase1
+        self._side = torch.cuda.Stream(device=grads.device) if (self.world > 1 and grads.is_cuda) else None
         self._work = []
 
     def _reduce(self, t):
@@ -35,7 +43,13 @@ class GradSync:
             self._work.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def start_head(self):
-        if self.world > 1:
+        if self.world <= 1:
+            return
+        if self.wait_phase1 is None or self._side is None:
+            self._reduce(self.grads[:self.split])
+            return
+        self.wait_phase1(ctypes.c_void_p(self._side.cuda_stream))
+        with torch.cuda.stream(self._side):
             self._reduce(self.grads[:self.split])
 
     def start_tail(self):
@@ -58,7 +72,8 @@ class TrainStep:
     param_groups[0] lr / alpha / eps are read at every step, so a scheduler's step(epoch) takes
     effect as with the reference's optimizer.step() (model/main.py:127, 321-322)."""
 
-    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None, optimizer=None):
+    def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None, optimizer=None,
+                 phased=None):
         self.model = model
         self.N = batch
         self.lr, self.alpha, self.eps = lr, alpha, eps
@@ -72,8 +87,12 @@ class TrainStep:
         self.dout = torch.empty_like(self.out)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.pg = process_group
-        self.sync = GradSync(self.grads, lib().f3_net_grad_split(nat.h), process_group)
+        h = nat.h
+        self.sync = GradSync(self.grads, lib().f3_net_grad_split(h), process_group,
+                             wait_phase1=lambda st: check(lib().f3_net_wait_phase1(h, st), "wait phase 1"))
         self.world = self.sync.world
+        # phased=True runs the two-phase backward even on one rank (times its cost against phase 0)
+        self.phased = self.world > 1 if phased is None else bool(phased)
         # expose the flat gradient through the usual .grad attributes
         for (name, shape, off), p in zip(model.param_views(), model.parameters()):
             p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
@@ -136,9 +155,9 @@ class TrainStep:
     # -- one step ----------------------------------------------------------------
     def _eager(self, skel, sensor, label):
         self.forward_loss(skel, sensor, label)
-        if self.world > 1:
+        if self.phased:
             self.backward_phase(1)
-            self.sync.start_head()       # overlaps phase 2
+            self.sync.start_head()       # after phase 1's queues, concurrent with phase 2
             self.backward_phase(2)
             self.sync.start_tail()
             self.sync.finish()
@@ -161,6 +180,7 @@ class TrainStep:
         g_head, g_tail, g_opt = self.graph
         g_head.replay()
         if g_tail is not None:
+            check(lib().f3_net_wait_phase1(self.model._native.h, stream_handle()), "wait phase 1")
             self.sync.start_head()       # RCCL on the comm stream, concurrent with phase 2
             g_tail.replay()
             self.sync.start_tail()
@@ -183,7 +203,7 @@ class TrainStep:
         torch.cuda.synchronize()
         g_head = torch.cuda.CUDAGraph()
         g_tail = None
-        if self.world > 1:
+        if self.phased:
             with torch.cuda.graph(g_head):
                 self.forward_loss(skel, sensor, label)
                 self.backward_phase(1)

@@ -89,12 +89,17 @@ int f3_net_backward(f3_net* net, int batch, const float* params, const float* do
 
 /* The same backward in two phases, for overlapping the data-parallel gradient all-reduce
  * with compute: phase 1 = zero grads, head, sensor branch and skeleton layers 4-6 (their
- * gradients, params[0 .. f3_net_grad_split) in the flat buffer, are final when it ends);
- * phase 2 = skeleton layers 0-3 and data_bn (the rest). phase 0 = both (f3_net_backward).
- * Parameter offsets are laid out phase-1-first; state_dict order is unchanged. */
+ * gradients, params[0 .. f3_net_grad_split) in the flat buffer); phase 2 = skeleton layers 0-3
+ * and data_bn (the rest). phase 0 = both (f3_net_backward). Parameter offsets are laid out
+ * phase-1-first; state_dict order is unchanged.
+ * Phase 1 returns WITHOUT ordering `stream` after its private queues (the weight-gradient queues
+ * keep draining while phase 2's critical path starts): make the all-reduce stream wait with
+ * f3_net_wait_phase1 before reducing params[0 .. split). Phase 2 ends with `stream` ordered after
+ * all work of both phases. */
 int f3_net_backward_phase(f3_net* net, int batch, const float* params, const float* dout, float* grads,
                           void* workspace, int phase, void* stream);
 int64_t f3_net_grad_split(const f3_net* net);
+int f3_net_wait_phase1(f3_net* net, void* stream);
 
 /* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
  * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):

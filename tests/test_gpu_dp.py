@@ -1,7 +1,10 @@
 """Data parallel on the device (needs an MI355X): two ranks (torchrun, both on cuda:0, gloo
 reducing the device gradients through the host) train their own clip shards through
-TrainStep — backward in two phases, the head bucket's all-reduce overlapping phase 2, RMSprop
-with the 1/world scale — and must end with bit-identical parameters (tools/dp_check.py).
+TrainStep — backward in two phases, the head bucket's all-reduce ordered after phase 1's
+per-queue events and overlapping phase 2, RMSprop with the 1/world scale. The first step's
+reduced gradient must equal the mean of the per-shard gradients (each computed alone, within
+10x the backward's run-to-run floor) and its update RMSprop on it; the replicas must end with
+bit-identical parameters (tools/dp_check.py).
 The 8-GPU RCCL run is the driver's scaling bench; this checks the same code path on one GPU."""
 import json
 import os
@@ -35,3 +38,6 @@ def test_two_rank_replicas_stay_identical():
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(lines[-1])
     assert res["world"] == 2 and res["replicas_identical"] and res["max_param_change"] > 0
+    s1 = res["first_step_vs_mean_of_shard_grads"]
+    print(s1)
+    assert s1["ok"], s1

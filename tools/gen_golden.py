@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate golden vectors by running the REFERENCE's own modules (build container only).
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--targcn-only | --sktr-only]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--targcn-only | --sktr-only | --musa-only]
 Writes: tests/golden/*.npz  (small, committed; the reference itself never travels).
 
 How the reference is imported: the packaged 3-stream model lives in
@@ -32,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 from oracle import model_cpu as oc  # noqa: E402
+from oracle import musa_cpu as mu  # noqa: E402
 from oracle import sktr_cpu as sk  # noqa: E402
 from oracle import targcn_cpu as tg  # noqa: E402
 from oracle.prng import synthetic_batch  # noqa: E402
@@ -223,8 +224,77 @@ def run_sktr_case(tag, S, batch, seed, M=1, V=14, T=30, lr=1e-3):
     return nparams
 
 
+def import_musa():
+    sys.path.insert(0, REF + "/Multimodal_Fall3/model")
+    return importlib.import_module("musa_model")
+
+
+def run_musa_case(tag, Mm, batch, seed, lr=1e-3):
+    """musa_model.Model as root Multimodal_Fall3/main.py:307-320 builds it, one train step with
+    CrossEntropyLoss and RMSprop(lr). DropBlock off (keep_prob = 1 on every block, so the modules
+    return their input) and the classifier's Dropout p = 0: the step is deterministic; the oracle
+    covers the random parts with hash draws shared with the kernels."""
+    import warnings
+    torch.manual_seed(0)
+    g = Mm.adjGraph(layout="coco_cut", strategy="uniform")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = Mm.Model(num_class=11, num_point=14, max_frame=300, graph=g, bias=True, edge=True, block_size=41,
+                         embed_dim=64, n_stage=1, act_type="tanh")
+    for m in model.modules():
+        if hasattr(m, "keep_prob"):
+            m.keep_prob = 1.0
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    state = mu.init_state(seed)
+    assert list(model.state_dict().keys()) == list(state.keys()), "oracle state_dict order differs"
+    for k, v in model.state_dict().items():
+        assert tuple(v.shape) == tuple(state[k].shape), k
+        if k.endswith(".A"):
+            assert torch.equal(v, state[k]), "adjGraph A differs from the oracle's"
+    model.load_state_dict(state, strict=True)
+    skel, _, label = synthetic_batch(batch, 14, 11, 1, seed + 1)
+    x, lb = torch.from_numpy(skel), torch.from_numpy(label)
+    model.eval()
+    with torch.no_grad():
+        eval_out = model(x).numpy()
+    model.train()
+    opt = torch.optim.RMSprop([p for p in model.parameters() if p.requires_grad], lr=lr)
+    opt.zero_grad()
+    out = model(x)
+    loss = torch.nn.CrossEntropyLoss()(out, lb)
+    loss.backward()
+    d = {"seed": np.array([seed]), "x": skel, "label": label, "lr": np.array([lr]), "out": out.detach().numpy(),
+         "loss": np.array([loss.item()]), "eval_out": eval_out}
+    nparams = 0
+    for name, p in model.named_parameters():
+        nparams += p.numel()
+        if p.grad is None:
+            d["nograd:" + name] = np.array([1])
+            continue
+        pack("grad:" + name, d, p.grad)
+    opt.step()
+    for name, p in model.named_parameters():
+        pack("post:" + name, d, p)
+    for name, b in model.named_buffers():
+        if name.endswith(("running_mean", "running_var")):
+            pack("buf:" + name, d, b)
+    d["nparams"] = np.array([nparams])
+    path = os.path.join(OUT, f"musa_{tag}.npz")
+    np.savez_compressed(path, **d)
+    print(f"musa {tag}: params={nparams} loss={loss.item():.6f} -> {path} ({os.path.getsize(path)//1024} KB)")
+    return nparams
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--musa-only" in sys.argv:
+        Mm = import_musa()
+        kat = json.load(open(os.path.join(OUT, "param_counts.json")))
+        kat["musa"] = run_musa_case("b4", Mm, 4, 9001)
+        with open(os.path.join(OUT, "param_counts.json"), "w") as f:
+            json.dump(kat, f, indent=1, sort_keys=True)
+        return
     if "--sktr-only" in sys.argv:
         S = import_sktr()
         kat = json.load(open(os.path.join(OUT, "param_counts.json")))
@@ -294,6 +364,7 @@ def main():
     S = import_sktr()
     kat["sktr"] = run_sktr_case("m1", S, 4, 8001)
     run_sktr_case("m2", S, 3, 8002, M=2)
+    kat["musa"] = run_musa_case("b4", import_musa(), 4, 9001)
     with open(os.path.join(OUT, "param_counts.json"), "w") as f:
         json.dump(kat, f, indent=1, sort_keys=True)
 
