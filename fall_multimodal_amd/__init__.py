@@ -8,7 +8,8 @@ Public surface mirrors the reference (Multimodal_Fall3/model/):
     get_cfg_defaults()           -> model/config.py
 plus TrainStep, the fused multi-stream step used by bench.py, the skeleton-only TARGCN model
 (BASELINE config 2: TRAGCN.py / EmbGCN.py / GRU.py / TA.py) with its fused TargcnStep, the
-SkeletonTransformer (BASELINE config 5: skeleton_transformer.py) with SktrStep, and the steps either side of it
+SkeletonTransformer (BASELINE config 5: skeleton_transformer.py) with SktrStep, musa.Model (the model
+the root Multimodal_Fall3/main.py trains: musa_model.py) with musa.MusaStep, and the steps either side of it
 (SURVEY §8f): data (window files, video-wise splits, pinned double-buffered loader) and
 evaluate (valid / test loops, top-k, macro P/R/F1, best-model checkpoints).
 """
@@ -20,8 +21,9 @@ from .optim import RMSprop, build_optimizer
 from .train import TrainStep
 from .targcn import TARGCN, TargcnStep
 from .sktr import SkeletonTransformer, SktrStep
+from . import musa
 from . import data, evaluate
 
 __all__ = ["build_model", "build_optimizer", "get_cfg_defaults", "CfgNode", "Graph", "Fall3Net", "NetSpec",
            "STGCAN", "BiLSTM", "CNN_BiLSTM", "TwoStreamSTGCAN", "TwoStreamSTGCAN_BiLSTM", "TwoStreamSpatialTemporalGraph",
-           "RMSprop", "TrainStep", "TARGCN", "TargcnStep", "SkeletonTransformer", "SktrStep", "data", "evaluate"]
+           "RMSprop", "TrainStep", "TARGCN", "TargcnStep", "SkeletonTransformer", "SktrStep", "musa", "data", "evaluate"]

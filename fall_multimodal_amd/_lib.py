@@ -26,6 +26,8 @@ EXPORTS = (
     "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_soft_ce",
     "f3_sktr_create", "f3_sktr_destroy", "f3_sktr_num_entries", "f3_sktr_entry", "f3_sktr_param_count",
     "f3_sktr_buffer_count", "f3_sktr_counter_count", "f3_sktr_workspace_bytes", "f3_sktr_forward", "f3_sktr_backward",
+    "f3_musa_create", "f3_musa_destroy", "f3_musa_num_entries", "f3_musa_entry", "f3_musa_param_count",
+    "f3_musa_buffer_count", "f3_musa_counter_count", "f3_musa_workspace_bytes", "f3_musa_forward", "f3_musa_backward",
 )
 
 F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE = 0, 1001, 1002, 1003, 1004
@@ -34,6 +36,10 @@ ENTRY_PARAM, ENTRY_BUFFER, ENTRY_COUNTER = 0, 1, 2
 
 class F3TargcnConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("num_node", "num_class", "precision")]
+
+
+class F3MusaConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("num_point", "frames", "num_class")]
 
 
 class F3SktrConfig(ctypes.Structure):
@@ -106,6 +112,17 @@ def lib():
         "f3_sktr_workspace_bytes": (I64, [P, I]),
         "f3_sktr_forward": (I, [P, I, I, P, P, P, P, P, P, P, ctypes.c_uint, F, P]),
         "f3_sktr_backward": (I, [P, I, P, P, P, P, P, P]),
+        "f3_musa_create": (I, [ctypes.POINTER(F3MusaConfig), ctypes.POINTER(P)]),
+        "f3_musa_destroy": (None, [P]),
+        "f3_musa_num_entries": (I, [P]),
+        "f3_musa_entry": (I, [P, I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(I), ctypes.POINTER(I),
+                              ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "f3_musa_param_count": (I64, [P]),
+        "f3_musa_buffer_count": (I64, [P]),
+        "f3_musa_counter_count": (I64, [P]),
+        "f3_musa_workspace_bytes": (I64, [P, I]),
+        "f3_musa_forward": (I, [P, I, I, P, P, P, P, P, P, ctypes.c_uint, I, P]),
+        "f3_musa_backward": (I, [P, I, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

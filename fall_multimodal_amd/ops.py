@@ -14,6 +14,9 @@ under torch.compile / FakeTensor tracing and composes with the rest of an autogr
         -> (out, workspace, new running buffers, new counters)
         model(x), skeleton_transformer.py:418-435 (BASELINE config 5)
   fall3::sktr_backward(net, params, dout, workspace) -> grads
+  fall3::musa_forward(net, params, buffers, counters, x, training, seed) -> (out, workspace, buffers, counters)
+        model(data), Multimodal_Fall3/model/musa_model.py:561-589 (root main.py:97-99)
+  fall3::musa_backward(net, params, dout, workspace) -> grads
   fall3::rmsprop_(param!, square_avg!, grad, lr, alpha, eps, scale)
         optimizer.step(), model/optimizer.py:21 (torch.optim.RMSprop semantics)
 
@@ -217,6 +220,58 @@ def _sk_backward(ctx, dout, dws, dbuf, dcnt):
 
 
 sktr_forward.register_autograd(_sk_backward, setup_context=_sk_setup)
+
+
+# ---------------------------------------------------------------------------------------------
+# musa_model.Model (f3_musa)
+# ---------------------------------------------------------------------------------------------
+@torch.library.custom_op("fall3::musa_forward", mutates_args=())
+def musa_forward(net: int, params: List[Tensor], buffers: Tensor, counters: Tensor, x: Tensor, training: bool,
+                 seed: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    m = _module(net)
+    N = x.shape[0]
+    ws = torch.empty(m._native.workspace_bytes(N), dtype=torch.uint8, device=x.device)
+    out = torch.empty(N, m.num_classes, dtype=torch.float32, device=x.device)
+    nb, nc = buffers.clone(), counters.clone()
+    m.native_forward(x, out, ws, training, seed, buffers=nb, counters=nc)
+    return out, ws, nb, nc
+
+
+@musa_forward.register_fake
+def _(net, params, buffers, counters, x, training, seed):
+    m = _module(net)
+    N = x.shape[0]
+    return (x.new_empty(N, m.num_classes, dtype=torch.float32),
+            x.new_empty(m._native.workspace_bytes(N), dtype=torch.uint8), torch.empty_like(buffers),
+            torch.empty_like(counters))
+
+
+@torch.library.custom_op("fall3::musa_backward", mutates_args=())
+def musa_backward(net: int, params: List[Tensor], dout: Tensor, workspace: Tensor) -> Tensor:
+    m = _module(net)
+    grads = torch.empty(m._native.nparam, dtype=torch.float32, device=dout.device)
+    m.native_backward(dout.shape[0], dout.contiguous(), grads, workspace)
+    return grads
+
+
+@musa_backward.register_fake
+def _(net, params, dout, workspace):
+    return dout.new_empty(_module(net)._native.nparam, dtype=torch.float32)
+
+
+def _mu_backward(ctx, dout, dws, dbuf, dcnt):
+    if not ctx.training:
+        raise RuntimeError("fall3: backward through an eval-mode forward is not supported")
+    (ws,) = ctx.saved_tensors
+    m = _module(ctx.net)
+    grads = torch.ops.fall3.musa_backward(ctx.net, list(m.parameters()), dout.float(), ws)
+    gl = _split_grads(m, grads)
+    # parameters that do not require grad (A) get None, as autograd expects
+    gl = [g if p.requires_grad else None for g, p in zip(gl, m.parameters())]
+    return None, gl, None, None, None, None, None
+
+
+musa_forward.register_autograd(_mu_backward, setup_context=_sk_setup)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -184,6 +184,40 @@ int f3_targcn_backward(f3_targcn* net, int batch, const float* params, const flo
  * dout = dloss/dout. loss is overwritten. */
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream);
 
+/* ---- musa_model.Model (the model root Multimodal_Fall3/main.py trains; model/musa_model.py) ----
+ * f3_musa_create   <- Model(num_class=11, num_point=14, max_frame=300, graph=adjGraph('coco_cut',
+ *                     'uniform'), bias=True, edge=True, block_size=41, embed_dim=64, n_stage=1,
+ *                     act_type='tanh')                                      main.py:307-320, :492-559
+ * f3_musa_entry    <- model.state_dict() keys/shapes (A included: a Parameter, requires_grad False)
+ * f3_musa_forward  <- pred = model(data), x f32[N,3,T,V]                   musa_model.py:561-589
+ * f3_musa_backward <- loss.backward()
+ * Train mode: dropout != 0 enables the DropBlocks (keep_prob 0.9, block 41) and the head's
+ * Dropout(0.2), all drawn from a counter hash of `seed` (oracle/musa_cpu.py reproduces it);
+ * dropout == 0 is the reference with keep_prob 1 and p = 0. fp32 arithmetic (fp32 MFMA GEMMs). */
+typedef struct f3_musa_config {
+  int num_point;   /* V (13..18; 14 = coco_cut) */
+  int frames;      /* T (8..64; the motion stream has T-1) */
+  int num_class;   /* <= 64 */
+} f3_musa_config;
+
+typedef struct f3_musa f3_musa;
+
+int f3_musa_create(const f3_musa_config* cfg, f3_musa** out);
+void f3_musa_destroy(f3_musa* net);
+int f3_musa_num_entries(const f3_musa* net);
+int f3_musa_entry(const f3_musa* net, int i, const char** name, int* kind, int* ndim, int64_t* shape8,
+                  int64_t* offset);
+int64_t f3_musa_param_count(const f3_musa* net);
+int64_t f3_musa_buffer_count(const f3_musa* net);
+int64_t f3_musa_counter_count(const f3_musa* net);
+int64_t f3_musa_workspace_bytes(const f3_musa* net, int batch);
+int f3_musa_forward(f3_musa* net, int batch, int training, const float* params, float* buffers, int64_t* counters,
+                    const float* x, float* out, void* workspace, unsigned seed, int dropout, void* stream);
+/* grads (flat, params layout) are OVERWRITTEN; A and the SepTemporal blocks' edge get zeros (the
+ * reference leaves their .grad None: A is frozen, those edges only shape DropBlock masks). */
+int f3_musa_backward(f3_musa* net, int batch, const float* params, const float* buffers, const float* dout,
+                     float* grads, void* workspace, void* stream);
+
 /* ---- SkeletonTransformer (BASELINE config 5; skeleton_transformer.py) ----
  * f3_sktr_create     <- SkeletonTransformer(3, V, T, num_class, 32, 6, 16, 8)   :360-416
  *                       (GSTCAN_HAR_conv_kfold_trans.ipynb; V=14, T=30, 11 classes)

@@ -149,7 +149,7 @@ def test_custom_ops_registered_with_fake_kernels():
     from torch._subclasses import FakeTensorMode
     import fall_multimodal_amd as f3
     for op in ("net_forward", "net_backward", "targcn_forward", "targcn_backward", "sktr_forward", "sktr_backward",
-               "rmsprop_"):
+               "musa_forward", "musa_backward", "rmsprop_"):
         assert hasattr(torch.ops.fall3, op), op
     m = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device="cpu")
     t = f3.TARGCN(num_nodes=17, device="cpu")
@@ -195,6 +195,26 @@ def test_sktr_entry_table_matches_reference_state_dict(V, T, M):
     if (V, T) == (14, 30):
         assert nparam == 262091
     assert net.ncnt == 18 and net.nbuf == 18 * 2 * 32
+    assert net.workspace_bytes(64) > net.workspace_bytes(4) > 0
+
+
+def test_musa_entry_table_matches_reference_state_dict():
+    """f3_musa_entry: musa_model.Model's exact state_dict keys, order and shapes (checked against the
+    reference module by tools/gen_golden.py), 427,107 trainable parameters (+ the frozen A)."""
+    from oracle import musa_cpu as mu
+    from fall_multimodal_amd.musa import _NativeMusa
+    net = _NativeMusa(14, 30, 11)
+    ref = mu.param_shapes()
+    assert [n for n, k, sh, off in net.entries] == list(ref.keys())
+    n_train = 0
+    for n, kind, sh, off in net.entries:
+        assert tuple(sh) == tuple(ref[n]), n
+        assert kind == (2 if n.endswith("num_batches_tracked") else 1 if mu.is_buffer(n) else 0), n
+        if kind == 0:
+            assert off % 4 == 0
+            if not mu.is_frozen(n):
+                n_train += int(np.prod(sh))
+    assert n_train == 427107 and net.ncnt == 22
     assert net.workspace_bytes(64) > net.workspace_bytes(4) > 0
 
 
