@@ -50,8 +50,9 @@ def parse():
                         "step: 10.1 vs 8.15 ms at B=256; see DESIGN.md)")
     p.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old commands
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--model", default="fall3", choices=("fall3", "targcn", "sktr"),
-                   help="fall3: the headline 3-stream step (default). targcn / sktr: BASELINE config 2 / 5 alone")
+    p.add_argument("--model", default="fall3", choices=("fall3", "targcn", "sktr", "musa"),
+                   help="fall3: the headline 3-stream step (default). targcn / sktr: BASELINE config 2 / 5 alone; "
+                        "musa: the root main.py's musa_model")
     p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN and config-5 lines in the default run")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -331,6 +332,73 @@ def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     return rec
 
 
+def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
+    """The model the root Multimodal_Fall3/main.py trains (musa_model.Model, main.py:307-320: 14 joints,
+    30 frames, two streams, DropBlocks, RMSprop) — training step (fwd + CE + bwd + RMSprop) at B=256 on
+    one GPU, fp32, synthetic clips; plus the HBM roofline of its depthwise temporal Conv1D."""
+    import fall_multimodal_amd as f3
+    import fall_multimodal_amd._lib as L
+    from oracle.prng import synthetic_batch
+    x, _, lab = synthetic_batch(B, 14, 11, 1, 9)
+    model = f3.musa.Model(11, 14, 300, f3.musa.adjGraph("coco_cut", "uniform"), True, True, 41, device=dev)
+    step = f3.musa.MusaStep(model, B)
+    xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
+    for _ in range(warmup):
+        step(xd, yd)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(xd, yd)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    rec = {"metric": "clips/sec (fwd+bwd) musa_model.Model (root Multimodal_Fall3/main.py), B=256, 1 GPU",
+           "value": round(B / dt, 1), "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32",
+           "steps": steps, "config": {"workload": f"musa_V14_T30_B{B}", "global_batch": B, "joints": 14,
+                                      "frames": 30, "dropblock": True},
+           "final_loss": round(float(step.loss.item()), 5)}
+    # depthwise temporal conv roofline (SepTemporal_Block depth_conv, C=128, V=14, T=30, B clips):
+    # algorithmic bytes = x + y (+ w, b); the BatchNorm sums are fused in the epilogue
+    lib, st = L.lib(), L.stream_handle()
+    roofs = {}
+    for K, S in ((3, 1), (5, 2)):
+        C, T, V = 128, 30, 14
+        xin = torch.randn(B, T, V, C, device=dev)
+        To = (T + (K - 1) - K) // S + 1
+        y = torch.empty(B, To, V, C, device=dev)
+        w = torch.randn(C, K, device=dev)
+        bb = torch.randn(C, device=dev)
+        sums = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+        fn = lambda: lib.f3_dwconv_t_forward(L.ptr(xin), L.ptr(w), L.ptr(bb), L.ptr(y), L.ptr(sums), B, T, V, C, K,  # noqa: E731
+                                             S, (K - 1) // 2, st)
+        L.check(fn(), "dwconv")
+        ms = _time_launch(fn)
+        ms_nosum = _time_launch(lambda: lib.f3_dwconv_t_forward(L.ptr(xin), L.ptr(w), L.ptr(bb), L.ptr(y), None, B, T,
+                                                                V, C, K, S, (K - 1) // 2, st))
+        byt = 4 * (xin.numel() + y.numel() + w.numel() + bb.numel())
+        gbs = byt / (ms * 1e-3) / 1e9
+        roofs[f"k{K}_s{S}"] = {"kernel": f"mu_dwconv_fwd_kernel<{K}> (C={C}, V={V}, T={T}->{To}, N={B}, fp32, "
+                                         f"BN sums fused)", "bound": "hbm", "achieved": round(gbs, 1),
+                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                               "bytes_per_launch": byt, "ms_per_launch": round(ms, 4),
+                               "ms_without_bn_sums": round(ms_nosum, 4)}
+    rec["roofline_dwconv_t"] = roofs
+    if cpu_seconds > 0:  # the oracle (pinned to the reference) on this host's cores
+        from oracle import musa_cpu as mu
+        threads = cpu_threads()
+        torch.set_num_threads(threads)
+        stc = mu.init_state(7)
+        xc, lc = torch.from_numpy(x), torch.from_numpy(lab)
+        mu.train_step(stc, xc[:16], lc[:16])
+        t0, n = time.perf_counter(), 0
+        while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 10):
+            mu.train_step(stc, xc, lc, draws=n + 1)
+            n += 1
+        rec["cpu_baseline"] = {"value": round(B * n / (time.perf_counter() - t0), 2), "unit": "clips/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{n} oracle train steps of B={B}, fp32, torch CPU"}
+    return rec
+
+
 def cpu_threads():
     """The CPU share this process may use: OMP_NUM_THREADS (16 on the GPU box, whose nproc shows
     the whole machine), else every core here."""
@@ -378,6 +446,11 @@ def main():
     if a.model == "targcn":
         rec = targcn_bench(dev, steps=a.steps, warmup=a.warmup, precision=a.precision,
                            cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        return
+    if a.model == "musa":
+        rec = musa_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
@@ -434,6 +507,7 @@ def main():
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
     tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     skrec = sktr_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    murec = musa_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
     if rank == 0:
@@ -470,6 +544,7 @@ def main():
             "main_py_autograd_path": agp,
             "cfg2_targcn": tgrec,
             "cfg5_sktr": skrec,
+            "musa_model": murec,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

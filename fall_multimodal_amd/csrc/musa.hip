@@ -7,6 +7,8 @@
 // block call, every intermediate in LDS, draws from the counter hash of oracle/musa_cpu.py.
 #include <math.h>
 
+#include <algorithm>
+
 #include "musa.h"
 
 namespace f3 {
@@ -58,22 +60,38 @@ struct QuadLayout {
   }
 };
 
-// per-channel sums of this workgroup's threads -> fp64 global accumulators (C <= 256)
-F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], const float (&s2)[4], double* g1,
-                          double* g2) {
+// per-channel sums of this workgroup's threads -> its fp64 lane (lanes[l][0..C) and [C..2C))
+F3_DEV void channel_flush(int C, int q, bool act, const float (&s1)[4], const float (&s2)[4], double* lanes) {
   __shared__ float r1[256], r2[256];
   for (int c = threadIdx.x; c < C; c += blockDim.x) r1[c] = r2[c] = 0.f;
   __syncthreads();
-  if (L.act)
+  if (act)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      atomicAdd(r1 + 4 * L.q + e, s1[e]);
-      atomicAdd(r2 + 4 * L.q + e, s2[e]);
+      atomicAdd(r1 + 4 * q + e, s1[e]);
+      atomicAdd(r2 + 4 * q + e, s2[e]);
     }
   __syncthreads();
+  double* l = lanes + (size_t)(blockIdx.x % kLanes) * 2 * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    if (g1) atomicAdd(g1 + c, (double)r1[c]);
-    if (g2) atomicAdd(g2 + c, (double)r2[c]);
+    atomicAdd(l + c, (double)r1[c]);
+    atomicAdd(l + C + c, (double)r2[c]);
+  }
+}
+F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], const float (&s2)[4], double* lanes) {
+  channel_flush(C, L.q, L.act, s1, s2, lanes);
+}
+
+// totals of the lanes: g1[c] += sum_l lanes[l][c], g2[c] += sum_l lanes[l][C + c]; lanes re-zeroed
+__global__ __launch_bounds__(512) void mu_lane_finalize_kernel(double* lanes, int C, double* g1, double* g2) {
+  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+    double s = 0.0;
+    for (int l = 0; l < kLanes; ++l) {
+      s += lanes[(size_t)l * 2 * C + c];
+      lanes[(size_t)l * 2 * C + c] = 0.0;
+    }
+    if (c < C) g1[c] += s;
+    else g2[c - C] += s;
   }
 }
 
@@ -83,41 +101,65 @@ F3_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 // ------------------------------------------------------------------------------------------
 // depthwise temporal conv (SepTemporal_Block depth_conv / Sep_TCN sep31, sep11; :163-166, 429-436)
 // ------------------------------------------------------------------------------------------
-template <int K>
+// One thread per (clip n, joint v, channel quad q, chunk of TC output frames): the K-frame input
+// window slides in registers (one new 16-B row load per output at stride 1, two at stride 2, the
+// next step's loads issued before this step's FMAs), so every input row is read once per chunk and
+// consecutive threads read consecutive 16-B pieces of a row (joint-major rows of C channels: a wave
+// covers 64 quads of one or two joints' rows). 32-bit index math; chunks keep ~28 waves per CU busy.
+constexpr int kDwChunk = 8;
+
+template <int K, int S>
 __global__ __launch_bounds__(256) void mu_dwconv_fwd_kernel(DwConvArgs a) {
-  const QuadLayout L(a.C);
+  const int nq = a.C >> 2;
+  const int nchunk = (a.T_out + kDwChunk - 1) / kDwChunk;
+  const int total = a.N * a.V * nq * nchunk;
+  // blockDim is a multiple of nq, so a thread's channel quad is the same for every item it takes
+  const int g0 = blockIdx.x * blockDim.x + threadIdx.x, G = gridDim.x * blockDim.x;
+  const int q = g0 % nq;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  if (L.act) {
-    f32x4 w[K];
-    const f32x4 b = ld4(a.b + 4 * L.q);
+  f32x4 w[K];
+  const f32x4 b = ld4(a.b + 4 * q);
 #pragma unroll
-    for (int k = 0; k < K; ++k)
+  for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) w[k][e] = a.w[(4 * L.q + e) * K + k];
-    const long long rows = (long long)a.N * a.T_out * a.V;
-    for (long long r = (long long)blockIdx.x * L.rs + L.rl; r < rows; r += (long long)gridDim.x * L.rs) {
-      const int v = (int)(r % a.V);
-      const long long nt = r / a.V;
-      const int to = (int)(nt % a.T_out), n = (int)(nt / a.T_out);
+    for (int e = 0; e < 4; ++e) w[k][e] = a.w[(4 * q + e) * K + k];
+  const int rstride = a.V * a.C;  // floats between consecutive frames of one joint
+  for (int g = g0; g < total; g += G) {
+    int rest = g / nq;
+    const int v = rest % a.V;
+    rest /= a.V;
+    const int ch = rest % nchunk, n = rest / nchunk;
+    const float* xb = a.x + ((size_t)n * a.T_in * a.V + v) * a.C + 4 * q;
+    float* yb = a.y + ((size_t)n * a.T_out * a.V + v) * a.C + 4 * q;
+    auto load = [&](int ti) -> f32x4 {
+      return (ti >= 0 && ti < a.T_in) ? ld4(xb + (size_t)ti * rstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    const int t0 = ch * kDwChunk, t1 = min(a.T_out, t0 + kDwChunk);
+    f32x4 xw[K];  // xw[k] = x[to*S + k - P]
+#pragma unroll
+    for (int k = 0; k < K; ++k) xw[k] = load(t0 * S + k - a.P);
+    for (int to = t0; to < t1; ++to) {
+      f32x4 nx[S];  // the next output's new window rows, in flight during this output's FMAs
+#pragma unroll
+      for (int j = 0; j < S; ++j) nx[j] = load((to + 1) * S + K - S + j - a.P);
       f32x4 acc = b;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int ti = to * a.S + k - a.P;
-        if (ti >= 0 && ti < a.T_in) {
-          const f32x4 x = ld4(a.x + (((size_t)n * a.T_in + ti) * a.V + v) * a.C + 4 * L.q);
+      for (int k = 0; k < K; ++k)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[e] = fmaf(w[k][e], x[e], acc[e]);
-        }
-      }
-      st4(a.y + (size_t)r * a.C + 4 * L.q, acc);
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w[k][e], xw[k][e], acc[e]);
+      st4(yb + (size_t)to * rstride, acc);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s1[e] += acc[e];
         s2[e] = fmaf(acc[e], acc[e], s2[e]);
       }
+#pragma unroll
+      for (int k = 0; k < K - S; ++k) xw[k] = xw[k + S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) xw[K - S + j] = nx[j];
     }
   }
-  if (a.sum) channel_flush(a.C, L, s1, s2, a.sum, a.sumsq);
+  if (a.sum) channel_flush(a.C, q, g0 < total, s1, s2, a.lanes);
 }
 
 // dx[n][ti][v][c] = sum_k dy[n][to][v][c] w[c][k], ti = to*S + k - P
@@ -234,7 +276,7 @@ __global__ __launch_bounds__(256) void mu_bn_act_bwd_reduce_kernel(BnActBwdArgs 
       }
     }
   }
-  channel_flush(a.C, L, s1, s2, a.s_dz, a.s_dzx);
+  channel_flush(a.C, L, s1, s2, a.lanes);
 }
 
 __global__ __launch_bounds__(256) void mu_bn_act_bwd_apply_kernel(BnActBwdArgs a) {
@@ -279,7 +321,7 @@ __global__ __launch_bounds__(256) void mu_colstat_kernel(ColStatArgs a) {
         s2[e] = fmaf(x[e], x[e], s2[e]);
       }
     }
-  channel_flush(a.C, L, s1, s2, a.sum, a.sumsq);
+  channel_flush(a.C, L, s1, s2, a.lanes);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -485,10 +527,10 @@ __global__ __launch_bounds__(256) void mu_merge_bwd_reduce_kernel(MergeArgs a) {
       }
     }
   }
-  channel_flush(a.C, L, p1, q1, a.s1_dz, a.s1_dzx);
+  channel_flush(a.C, L, p1, q1, a.lanes);
   if (a.bn2_on) {
     __syncthreads();
-    channel_flush(a.C, L, p2, q2, a.s2_dz, a.s2_dzx);
+    channel_flush(a.C, L, p2, q2, a.lanes + kLaneDoubles);
   }
 }
 
@@ -710,20 +752,37 @@ using namespace f3::mu;
 
 static bool c_ok(int C) { return C % 4 == 0 && C >= 16 && C <= 256; }
 
+#define F3_TRY_MU(x)              \
+  do {                            \
+    const int _st = (x);          \
+    if (_st != F3_OK) return _st; \
+  } while (0)
+
+static int lane_finalize(double* lanes, int C, double* g1, double* g2, hipStream_t s) {
+  hipLaunchKernelGGL(mu_lane_finalize_kernel, dim3(1), dim3(512), 0, s, lanes, C, g1, g2);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
 int f3_mu_dwconv_part_rows(const DwConvArgs* a) {
   return quad_grid((long long)a->N * a->T_out * a->V, a->C, 512);
 }
 
 int f3_mu_dwconv_fwd(const DwConvArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
-  const int grid = quad_grid((long long)a->N * a->T_out * a->V, a->C, 2048);
-  switch (a->K) {
-    case 1: hipLaunchKernelGGL(mu_dwconv_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, *a); break;
-    case 3: hipLaunchKernelGGL(mu_dwconv_fwd_kernel<3>, dim3(grid), dim3(256), 0, s, *a); break;
-    case 5: hipLaunchKernelGGL(mu_dwconv_fwd_kernel<5>, dim3(grid), dim3(256), 0, s, *a); break;
-    default: return F3_EINVAL;
-  }
+  const long long total = (long long)a->N * a->V * (a->C / 4) * ((a->T_out + kDwChunk - 1) / kDwChunk);
+  if (total >= (1LL << 31)) return F3_EINVAL;
+  const int nq = a->C / 4, block = 256 / nq * nq;  // a multiple of nq (the thread's quad stays fixed)
+  const long long want = (total + block - 1) / block;
+  const int grid = (int)std::min<long long>(want, 1024);  // <= 1024 workgroup flushes into the lanes
+  if (a->K == 1 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<1, 1>), dim3(grid), dim3(block), 0, s, *a);
+  else if (a->K == 3 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<3, 1>), dim3(grid), dim3(block), 0, s, *a);
+  else if (a->K == 5 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<5, 1>), dim3(grid), dim3(block), 0, s, *a);
+  else if (a->K == 3 && a->S == 2) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<3, 2>), dim3(grid), dim3(block), 0, s, *a);
+  else if (a->K == 5 && a->S == 2) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<5, 2>), dim3(grid), dim3(block), 0, s, *a);
+  else return F3_EINVAL;
   F3_LAUNCH_CHECK();
+  if (a->sum) return lane_finalize(a->lanes, a->C, a->sum, a->sumsq, s);
   return F3_OK;
 }
 
@@ -759,6 +818,7 @@ int f3_mu_bn_act_bwd(const BnActBwdArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
   hipLaunchKernelGGL(mu_bn_act_bwd_reduce_kernel, dim3(quad_grid(a->R, a->C, 1024)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
+  F3_TRY_MU(lane_finalize(a->lanes, a->C, a->s_dz, a->s_dzx, s));
   hipLaunchKernelGGL(mu_bn_act_bwd_apply_kernel, dim3(grid_for(a->R * a->C / 4)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
@@ -768,7 +828,7 @@ int f3_mu_colstat(const ColStatArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
   hipLaunchKernelGGL(mu_colstat_kernel, dim3(quad_grid(a->R, a->C, 1024)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  return F3_OK;
+  return lane_finalize(a->lanes, a->C, a->sum, a->sumsq, s);
 }
 
 int f3_mu_absstat(const AbsStatArgs* a, hipStream_t s) {
@@ -805,6 +865,8 @@ int f3_mu_merge_bwd(const MergeArgs* a, hipStream_t s) {
   const long long R = (long long)a->N * a->T * a->V;
   hipLaunchKernelGGL(mu_merge_bwd_reduce_kernel, dim3(quad_grid(R, a->C, 1024)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
+  F3_TRY_MU(lane_finalize(a->lanes, a->C, a->s1_dz, a->s1_dzx, s));
+  if (a->bn2_on) F3_TRY_MU(lane_finalize(a->lanes + kLaneDoubles, a->C, a->s2_dz, a->s2_dzx, s));
   hipLaunchKernelGGL(mu_merge_bwd_apply_kernel, dim3(grid_for(R * a->C / 4)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;

@@ -121,6 +121,7 @@ struct Plan {
   size_t ga, gb, gc, gd;  // backward scratch [R][256]
   size_t part;         // depthwise weight-gradient partials
   size_t mixpart;      // graph-mix dA partial rows
+  size_t lanes;        // per-channel reduction lanes (2 * kLaneDoubles; finalize re-zeroes them)
   size_t total;
 };
 
@@ -171,6 +172,7 @@ Plan plan(const f3_musa* net, int N) {
   p.gd = take(4 * Rmax * C2);
   p.part = take(4 * 512 * (size_t)CM * 6);
   p.mixpart = take(4 * (size_t)kMixParts * 1024);
+  p.lanes = take(8 * 2 * kLaneDoubles);
   p.total = o;
   return p;
 }
@@ -247,6 +249,7 @@ struct Ctx {
     return r;
   }
   float* f(size_t off) const { return at<float>(ws, off); }
+  double* lanes() const { return at<double>(ws, p.lanes); }
 };
 
 int gemm_fwd(const Ctx& c, ConvGemmArgs a, const BnOff* stats) {
@@ -320,6 +323,7 @@ int stream_forward(const Ctx& c, int si) {
     if (c.train) {
       ColStatArgs cs;
       cs.R = R; cs.C = C1; cs.x = c.f(w.h); cs.sum = c.fsum(o.bn_h); cs.sumsq = cs.sum + 256;
+      cs.lanes = c.lanes();
       MU_TRY(f3_mu_colstat(&cs, c.s));
     }
     if (c.train && net->drop) {
@@ -346,6 +350,7 @@ int stream_forward(const Ctx& c, int si) {
     if (c.train) {
       dw.sum = c.fsum(o.bn_d[b]);
       dw.sumsq = dw.sum + 256;
+      dw.lanes = c.lanes();
     }
     MU_TRY(f3_mu_dwconv_fwd(&dw, c.s));
     BnActArgs ba;
@@ -379,7 +384,7 @@ int stream_forward(const Ctx& c, int si) {
     std::memset(&dw, 0, sizeof(dw));
     dw.N = N; dw.T_in = T2; dw.T_out = T2; dw.V = V; dw.C = C1; dw.K = 3; dw.S = 1; dw.P = 1;
     dw.x = x; dw.w = P + o.d1_w; dw.b = P + o.d1_b; dw.y = c.f(w.td1);
-    if (c.train) { dw.sum = c.fsum(o.bn1); dw.sumsq = dw.sum + 256; }
+    if (c.train) { dw.sum = c.fsum(o.bn1); dw.sumsq = dw.sum + 256; dw.lanes = c.lanes(); }
     MU_TRY(f3_mu_dwconv_fwd(&dw, c.s));
     BnActArgs ba;
     std::memset(&ba, 0, sizeof(ba));
@@ -391,7 +396,7 @@ int stream_forward(const Ctx& c, int si) {
     std::memset(&dw, 0, sizeof(dw));
     dw.N = N; dw.T_in = T2; dw.T_out = T2; dw.V = V; dw.C = CM; dw.K = 1; dw.S = 1; dw.P = 0;
     dw.x = c.f(w.te2); dw.w = P + o.d2_w; dw.b = P + o.d2_b; dw.y = c.f(w.td2);
-    if (c.train) { dw.sum = c.fsum(o.bn3); dw.sumsq = dw.sum + 256; }
+    if (c.train) { dw.sum = c.fsum(o.bn3); dw.sumsq = dw.sum + 256; dw.lanes = c.lanes(); }
     MU_TRY(f3_mu_dwconv_fwd(&dw, c.s));
     ba.C = CM; ba.u = c.f(w.td2); ba.bn = c.bn(o.bn3, R2); ba.act = ACT_LEAKY; ba.y = c.f(w.te3);
     MU_TRY(f3_mu_bn_act(&ba, c.s));
@@ -409,6 +414,7 @@ int bn_act_bwd(const Ctx& c, const BnOff& b, long long R, int C, const float* dy
   std::memset(&a, 0, sizeof(a));
   a.R = R; a.C = C; a.dy = dy; a.u = u; a.bn = c.bn(b, R); a.act = act;
   a.s_dz = c.bsum(b); a.s_dzx = a.s_dz + 256;
+  a.lanes = c.lanes();
   a.du = du; a.add = add;
   a.g_gamma = c.grads + b.w; a.g_beta = c.grads + b.b;
   return f3_mu_bn_act_bwd(&a, c.s);
@@ -470,6 +476,7 @@ int stream_backward(const Ctx& c, int si, float* dres2T) {
     const int k1 = 2 + 2 * b;
     MergeArgs m = merge_args(c, To, C1, c.f(b == 0 ? w.p1 : w.p2), o.bn_p[b], res, rbn, w, k1, Ro);
     m.dout = gd;
+    m.lanes = c.lanes();
     m.s1_dz = c.bsum(o.bn_p[b]); m.s1_dzx = m.s1_dz + 256;
     if (rbn) { m.s2_dz = c.bsum(*rbn); m.s2_dzx = m.s2_dz + 256; }
     m.du1 = ga;                              // d p
@@ -494,6 +501,7 @@ int stream_backward(const Ctx& c, int si, float* dres2T) {
   {
     MergeArgs m = merge_args(c, T, C1, c.f(w.h), o.bn_h, c.f(w.r0), &o.bn_r0, w, 0, R);
     m.dout = gd;
+    m.lanes = c.lanes();
     m.s1_dz = c.bsum(o.bn_h); m.s1_dzx = m.s1_dz + 256;
     m.s2_dz = c.bsum(o.bn_r0); m.s2_dzx = m.s2_dz + 256;
     m.du1 = ga; m.du2 = gb; m.du2_add = 0;
@@ -633,6 +641,7 @@ int f3_musa_forward(f3_musa* net, int N, int training, const float* params, floa
   net->drop = training && dropout;
   Ctx c{net, p, workspace, params, buffers, nullptr, training != 0, N, s};
   if (training && hipMemsetAsync(at<char>(workspace, p.fsum), 0, 8 * 22 * 512, s) != hipSuccess) return F3_EHIP;
+  if (training && hipMemsetAsync(at<char>(workspace, p.lanes), 0, 8 * 2 * kLaneDoubles, s) != hipSuccess) return F3_EHIP;
   TokenArgs tk;
   std::memset(&tk, 0, sizeof(tk));
   tk.N = N; tk.T = net->T; tk.V = net->V; tk.x = x; tk.pos = c.f(p.s[0].tok); tk.mot = c.f(p.s[1].tok);
@@ -697,6 +706,7 @@ int f3_musa_backward(f3_musa* net, int N, const float* params, const float* buff
   Ctx c{net, p, workspace, params, const_cast<float*>(buffers), grads, true, N, s};
   if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
   if (hipMemsetAsync(at<char>(workspace, p.bsum), 0, 8 * 22 * 512, s) != hipSuccess) return F3_EHIP;
+  if (hipMemsetAsync(at<char>(workspace, p.lanes), 0, 8 * 2 * kLaneDoubles, s) != hipSuccess) return F3_EHIP;
   float* dres2T[2];
   {  // transposed 1x1 weights ([I][O] from [O][I]) for the input-gradient GEMMs
     PrepTable t;
@@ -735,6 +745,25 @@ int f3_musa_backward(f3_musa* net, int N, const float* params, const float* buff
                        s));
   for (int si = 0; si < 2; ++si) MU_TRY(stream_backward(c, si, dres2T[si]));
   return F3_OK;
+}
+
+int f3_dwconv_t_forward(const float* x, const float* w, const float* b, float* y, double* sums, int N, int T_in,
+                        int V, int C, int K, int S, int P, void* stream) {
+  if (!x || !w || !b || !y || N < 1 || T_in < 1 || V < 1 || S < 1 || P < 0) return F3_EINVAL;
+  DwConvArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.N = N; a.T_in = T_in; a.T_out = (T_in + 2 * P - K) / S + 1; a.V = V; a.C = C; a.K = K; a.S = S; a.P = P;
+  if (a.T_out < 1) return F3_EINVAL;
+  a.x = x; a.w = w; a.b = b; a.y = y;
+  if (sums) {
+    static double* lanes = nullptr;  // test / bench entry only: lane scratch kept for the process lifetime
+    if (!lanes) {
+      if (hipMalloc(&lanes, sizeof(double) * kLaneDoubles) != hipSuccess) return F3_EHIP;
+      if (hipMemset(lanes, 0, sizeof(double) * kLaneDoubles) != hipSuccess) return F3_EHIP;
+    }
+    a.sum = sums; a.sumsq = sums + C; a.lanes = lanes;
+  }
+  return f3_mu_dwconv_fwd(&a, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -217,6 +217,11 @@ int f3_musa_forward(f3_musa* net, int batch, int training, const float* params, 
  * reference leaves their .grad None: A is frozen, those edges only shape DropBlock masks). */
 int f3_musa_backward(f3_musa* net, int batch, const float* params, const float* buffers, const float* dout,
                      float* grads, void* workspace, void* stream);
+/* Kernel-level entry (tests, bench.py roofline): the depthwise temporal conv of SepTemporal_Block /
+ * Sep_TCN, Conv2d(C, C, (K,1), (S,1), (P,0), groups=C) on channels-last x [N,T_in,V,C] -> y
+ * [N,T_out,V,C], w [C][K], b [C]; sums (optional, [2C] fp64, accumulated): BatchNorm batch sums of y. */
+int f3_dwconv_t_forward(const float* x, const float* w, const float* b, float* y, double* sums, int N, int T_in,
+                        int V, int C, int K, int S, int P, void* stream);
 
 /* ---- SkeletonTransformer (BASELINE config 5; skeleton_transformer.py) ----
  * f3_sktr_create     <- SkeletonTransformer(3, V, T, num_class, 32, 6, 16, 8)   :360-416

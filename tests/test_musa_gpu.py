@@ -114,3 +114,31 @@ def test_musa_step_with_dropblock_vs_oracle(B):
     assert err < 1e-3 and (out.argmax(1) == out_ref.numpy().argmax(1)).all()
     assert abs(step.loss.item() - loss_ref.item()) < 1e-4
     assert cos >= 0.9999 and worst < 5e-2
+
+
+@pytest.mark.parametrize("K,S,C,T", [(3, 1, 128, 30), (5, 2, 128, 29), (1, 1, 192, 15), (3, 2, 256, 30),
+                                     (5, 1, 64, 17)])
+def test_dwconv_kernel_matches_torch(K, S, C, T):
+    """f3_dwconv_t_forward (the model's HBM-bound depthwise temporal Conv1D, with the BatchNorm sums
+    fused) vs torch's grouped Conv2d in fp64: output within 1e-5 of max |y|; the per-channel sums
+    (fp32 per thread and per workgroup, fp64 across workgroups) within 1e-5 of sum |y| (of y^2)."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    torch.manual_seed(K * 100 + C)
+    N, V, P = 7, 14, (K - 1) // 2
+    x = torch.randn(N, T, V, C, dtype=torch.float64)
+    w = torch.randn(C, 1, K, 1, dtype=torch.float64)
+    b = torch.randn(C, dtype=torch.float64)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride=(S, 1), padding=(P, 0), groups=C)
+    ref = ref.permute(0, 2, 3, 1).contiguous()
+    xd, wd, bd = x.float().to(d), w.reshape(C, K).float().contiguous().to(d), b.float().to(d)
+    y = torch.empty(ref.shape, device=d)
+    sums = torch.zeros(2 * C, dtype=torch.float64, device=d)
+    L.check(L.lib().f3_dwconv_t_forward(L.ptr(xd), L.ptr(wd), L.ptr(bd), L.ptr(y), L.ptr(sums), N, T, V, C, K, S, P,
+                                        L.stream_handle()), "dwconv")
+    got = y.cpu().double()
+    assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    s = sums.cpu()
+    flat = got.reshape(-1, C)
+    assert np.all(np.abs(s[:C].numpy() - flat.sum(0).numpy()) <= 1e-5 * flat.abs().sum(0).numpy())
+    assert np.all(np.abs(s[C:].numpy() - (flat * flat).sum(0).numpy()) <= 1e-5 * (flat * flat).sum(0).numpy())
