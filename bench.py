@@ -251,6 +251,31 @@ def autograd_path_bench(model, sk, se, lb, steps=5):
             "path": "model(data, sensor) -> CrossEntropyLoss -> backward -> RMSprop.step (torch.library ops)"}
 
 
+def replica_seconds(fn, steps, warmup):
+    """Seconds per step of fn over `steps` timed calls after `warmup`, bracketed by barrier +
+    synchronize on both sides and maxed over ranks when torch.distributed is initialised (the
+    replicas-only configs: every rank runs its own independent step, no collective)."""
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt / steps, world
+
+
 def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_seconds=0.0):
     """BASELINE config 2: skeleton-only TARGCN (TRAGCN.py:177-224, V=17 joints, T=30, bf16 GEMM
     operands) training step (fwd + CE + bwd + RMSprop) at B=256 on one GPU, synthetic clips,
@@ -262,18 +287,12 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
     model = f3.TARGCN(num_nodes=V, device=dev, precision=precision)
     step = f3.TargcnStep(model, B, lr=1e-5)
     x, y = torch.from_numpy(src).to(dev), torch.from_numpy(lab).to(dev)
-    for _ in range(warmup):
-        step(x, y)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(x, y)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    rec = {"metric": "clips/sec (fwd+bwd) TARGCN skeleton-only, B=256, 1 GPU", "value": round(B / dt, 1),
-           "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": precision, "steps": steps,
-           "config": {"workload": f"targcn_V{V}_T30_B{B}", "global_batch": B, "joints": V, "frames": 30,
-                      "gru_layers": 2, "hidden": 64, "ta_layers": 2},
+    dt, world = replica_seconds(lambda: step(x, y), steps, warmup)
+    rec = {"metric": "clips/sec (fwd+bwd) TARGCN skeleton-only, B=256, 1 GPU", "value": round(world * B / dt, 1),
+           "unit": "clips/s", "n_gpus": world, "scaling": "weak", "ms_per_step": round(dt * 1e3, 3),
+           "dtype": precision, "steps": steps,
+           "config": {"workload": f"targcn_V{V}_T30_B{B}", "global_batch": world * B, "joints": V, "frames": 30,
+                      "gru_layers": 2, "hidden": 64, "ta_layers": 2, "parallelism": f"replicas{world}"},
            "final_loss": round(float(step.loss.item()), 5)}
     if cpu_seconds > 0:  # the oracle (pinned bit-exactly to the reference) on this host's cores
         threads = cpu_threads()
@@ -303,18 +322,13 @@ def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     model = f3.SkeletonTransformer(device=dev)
     step = f3.SktrStep(model, B)
     xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
-    for _ in range(warmup):
-        step(xd, yd)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(xd, yd)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    rec = {"metric": "clips/sec (fwd+bwd) SkeletonTransformer, B=256, 1 GPU (one CV fold)", "value": round(B / dt, 1),
-           "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32", "steps": steps,
-           "config": {"workload": f"sktr_V14_T30_M1_B{B}", "global_batch": B, "joints": 14, "frames": 30,
-                      "blocks": 6, "heads": 8, "parallelism": "replicas (10-fold CV, one fold per GPU)"},
+    dt, world = replica_seconds(lambda: step(xd, yd), steps, warmup)
+    rec = {"metric": "clips/sec (fwd+bwd) SkeletonTransformer, B=256, 1 GPU (one CV fold)",
+           "value": round(world * B / dt, 1), "unit": "clips/s", "n_gpus": world, "scaling": "weak",
+           "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32", "steps": steps,
+           "config": {"workload": f"sktr_V14_T30_M1_B{B}", "global_batch": world * B, "joints": 14, "frames": 30,
+                      "blocks": 6, "heads": 8,
+                      "parallelism": f"replicas{world} (10-fold CV, one fold per GPU)"},
            "final_loss": round(float(step.loss.item()), 5)}
     if cpu_seconds > 0:  # the oracle (pinned to the reference) on this host's cores
         threads = cpu_threads()
@@ -343,19 +357,15 @@ def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     model = f3.musa.Model(11, 14, 300, f3.musa.adjGraph("coco_cut", "uniform"), True, True, 41, device=dev)
     step = f3.musa.MusaStep(model, B)
     xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
-    for _ in range(warmup):
-        step(xd, yd)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(xd, yd)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
+    dt, world = replica_seconds(lambda: step(xd, yd), steps, warmup)
     rec = {"metric": "clips/sec (fwd+bwd) musa_model.Model (root Multimodal_Fall3/main.py), B=256, 1 GPU",
-           "value": round(B / dt, 1), "unit": "clips/s", "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32",
-           "steps": steps, "config": {"workload": f"musa_V14_T30_B{B}", "global_batch": B, "joints": 14,
-                                      "frames": 30, "dropblock": True},
+           "value": round(world * B / dt, 1), "unit": "clips/s", "n_gpus": world, "scaling": "weak",
+           "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32",
+           "steps": steps, "config": {"workload": f"musa_V14_T30_B{B}", "global_batch": world * B, "joints": 14,
+                                      "frames": 30, "dropblock": True, "parallelism": f"replicas{world}"},
            "final_loss": round(float(step.loss.item()), 5)}
+    if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+        return rec
     # depthwise temporal conv roofline (SepTemporal_Block depth_conv, C=128, V=14, T=30, B clips):
     # algorithmic bytes = x + y (+ w, b); the BatchNorm sums are fused in the epilogue
     lib, st = L.lib(), L.stream_handle()
@@ -445,17 +455,17 @@ def main():
 
     if a.model == "targcn":
         rec = targcn_bench(dev, steps=a.steps, warmup=a.warmup, precision=a.precision,
-                           cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+                           cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
     if a.model == "musa":
-        rec = musa_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+        rec = musa_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
     if a.model == "sktr":
-        rec = sktr_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0)
+        rec = sktr_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return

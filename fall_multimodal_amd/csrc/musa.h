@@ -19,9 +19,11 @@ namespace mu {
 enum : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_LEAKY = 3 };
 constexpr float kLeaky = 0.01f;
 // Per-channel batch sums are reduced workgroup -> one of kLanes fp64 lanes (blockIdx % kLanes) ->
-// the fp64 total in a one-workgroup finalize: thousands of workgroups adding into the same C
-// addresses serialise at L2 (measured: 37 us of a 57 us depthwise-conv launch).
-constexpr int kLanes = 32;
+// the fp64 total in a small finalize launch: thousands of workgroups adding into the same C
+// addresses serialise (measured: 37 us of a 57 us depthwise-conv launch), and so do 32 lanes in
+// a 64 KB block (7 us of a 27 us launch): the atomics execute memory-side, per channel, so the
+// lanes spread them over 256 rows (2 MB with the second set).
+constexpr int kLanes = 256;
 constexpr size_t kLaneDoubles = (size_t)kLanes * 2 * 256;   // lane scratch per reduction (C <= 256)
 
 // depthwise temporal convolution (Conv2d(C, C, (K,1), (S,1), (P,0), groups=C)) over [N][T][V][C]
@@ -78,6 +80,7 @@ struct DropMaskArgs {
   unsigned seed; int call;
   float keep_prob; int block_size;
   float* fS; float* fT;
+  float* scr;          // f3_mu_dropmask_scratch_floats(N, T, V) floats
 };
 
 // out = tanh(f1 * z1 + f2 * z2), z1 = BN1(u1), z2 = BN2(u2) or u2; f = fS[n][v] * fT[n][t] (or 1)
@@ -147,6 +150,7 @@ int f3_mu_bn_act(const f3::mu::BnActArgs* a, hipStream_t s);
 int f3_mu_bn_act_bwd(const f3::mu::BnActBwdArgs* a, hipStream_t s);
 int f3_mu_absstat(const f3::mu::AbsStatArgs* a, hipStream_t s);
 int f3_mu_dropmask(const f3::mu::DropMaskArgs* a, hipStream_t s);
+int f3_mu_dropmask_scratch_floats(int N, int T, int V);
 int f3_mu_merge_fwd(const f3::mu::MergeArgs* a, hipStream_t s);
 int f3_mu_merge_bwd(const f3::mu::MergeArgs* a, hipStream_t s);
 int f3_mu_colstat(const f3::mu::ColStatArgs* a, hipStream_t s);

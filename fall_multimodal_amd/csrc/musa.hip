@@ -82,14 +82,32 @@ F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], cons
   channel_flush(C, L.q, L.act, s1, s2, lanes);
 }
 
-// totals of the lanes: g1[c] += sum_l lanes[l][c], g2[c] += sum_l lanes[l][C + c]; lanes re-zeroed
-__global__ __launch_bounds__(512) void mu_lane_finalize_kernel(double* lanes, int C, double* g1, double* g2) {
-  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
-    double s = 0.0;
-    for (int l = 0; l < kLanes; ++l) {
-      s += lanes[(size_t)l * 2 * C + c];
-      lanes[(size_t)l * 2 * C + c] = 0.0;
+// totals of the lanes: g1[c] += sum_l lanes[l][c], g2[c] += sum_l lanes[l][C + c]; lanes re-zeroed.
+// Workgroup w owns columns [64w, 64w + 64) of the 2C; its 16 lane groups of 64 threads walk every
+// 16th lane with all loads independent (one memory round trip), then the groups are summed in a
+// fixed order.
+constexpr int kFinCols = 64, kFinGroups = 16;
+__global__ __launch_bounds__(kFinCols * kFinGroups) void mu_lane_finalize_kernel(double* lanes, int C, double* g1,
+                                                                                 double* g2) {
+  __shared__ double red[kFinGroups][kFinCols];
+  const int n2 = 2 * C, j = threadIdx.x % kFinCols, grp = threadIdx.x / kFinCols;
+  const int c = blockIdx.x * kFinCols + j;
+  double s = 0.0;
+  if (c < n2) {
+    constexpr int kPer = kLanes / kFinGroups;
+    double v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) v[i] = lanes[(size_t)(grp + i * kFinGroups) * n2 + c];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      lanes[(size_t)(grp + i * kFinGroups) * n2 + c] = 0.0;
+      s += v[i];
     }
+  }
+  red[grp][j] = s;
+  __syncthreads();
+  if (grp == 0 && c < n2) {
+    for (int k = 1; k < kFinGroups; ++k) s += red[k][j];
     if (c < C) g1[c] += s;
     else g2[c - C] += s;
   }
@@ -367,73 +385,121 @@ F3_DEV float block_sum(float v, float* scratch) {  // 1024 threads
   return t;
 }
 
-__global__ __launch_bounds__(1024) void mu_dropmask_kernel(DropMaskArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int N = a.N, T = a.T, V = a.V, NV = N * V, NT = N * T;
-  float* sS = sm;            // [NV] dropS input_abs, then the S mask
-  float* bT = sS + NV;       // [NT] dropT input_abs
-  float* mT = bT + NT;       // [NT] seed mask, then the permuted max-pool
-  float* pT = mT + NT;       // [NT] max-pooled
-  __shared__ float Ae[32 * 32], scratch[32];
-  __shared__ int idx[64];
-  __shared__ float keys[64];
+// The two DropBlocks run as three launches (one workgroup per clip for the per-clip reductions
+// over a, then one workgroup for the global draws). The S-mask's rescale cS cancels in the T
+// block's probabilities (bT / sum bT), so the per-clip T statistics use the 0/1 S mask.
+// Scratch (DropMaskArgs::scr): sS [NV], rowS [N], mS [NV], rowM [N], bT [NT], rowT [N].
+struct DropScr {
+  float *sS, *rowS, *mS, *rowM, *bT, *rowT;
+  F3_DEV DropScr(const DropMaskArgs& a) {
+    const int NV = a.N * a.V, NT = a.N * a.T;
+    sS = a.scr; rowS = sS + NV; mS = rowS + a.N; rowM = mS + NV; bT = rowM + a.N; rowT = bT + NT;
+  }
+};
+
+// fixed-order sum of x[0..n) (identical in every workgroup of the same blockDim)
+F3_DEV float ordered_sum(const float* x, int n, float* red) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float t = red[0];
+  __syncthreads();
+  return t;
+}
+
+// Randomized_DropBlock_Ske input_abs per (n, v) = mean_{c,t} |z|, and its per-clip total
+__global__ __launch_bounds__(256) void mu_drop_s_kernel(DropMaskArgs a) {
+  __shared__ float sA[64 * 32];
+  const DropScr d(a);
+  const int n = blockIdx.x, TV = a.T * a.V;
+  for (int i = threadIdx.x; i < TV; i += blockDim.x) sA[i] = a.a[(size_t)n * TV + i];
+  __syncthreads();
+  __shared__ float sv[32];
+  if ((int)threadIdx.x < a.V) {
+    const int v = threadIdx.x;
+    float s = 0.f;
+    for (int t = 0; t < a.T; ++t) s += sA[t * a.V + v];
+    s /= (float)(a.C * a.T);
+    sv[v] = s;
+    d.sS[n * a.V + v] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int v = 0; v < a.V; ++v) s += sv[v];
+    d.rowS[n] = s;
+  }
+}
+
+// per clip: the S seed draws, M = (seed @ Ae) > 0.001, the 0/1 S mask, and the T block's
+// input_abs per (n, t) = mean_{c,v} |z| * mask_S (unscaled)
+__global__ __launch_bounds__(256) void mu_drop_t_kernel(DropMaskArgs a) {
+  __shared__ float sA[64 * 32], Ae[32 * 32], red[256], seedm[32], msk[32], bt[64];
+  const DropScr d(a);
+  const int n = blockIdx.x, TV = a.T * a.V, V = a.V, NV = a.N * a.V;
+  for (int i = threadIdx.x; i < TV; i += blockDim.x) sA[i] = a.a[(size_t)n * TV + i];
   for (int i = threadIdx.x; i < V * V; i += blockDim.x) Ae[i] = a.Ae[i];
-  // --- Randomized_DropBlock_Ske: input_abs = mean_{c,t} |z| per (n, v)
-  float loc = 0.f;
-  for (int i = threadIdx.x; i < NV; i += blockDim.x) {
-    const int n = i / V, v = i - n * V;
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += a.a[((size_t)n * T + t) * V + v];
-    s /= (float)(a.C * T);
-    sS[i] = s;
-    loc += s;
-  }
-  const float totS = block_sum(loc, scratch);
+  const float totS = ordered_sum(d.rowS, a.N, red);
   const float gamma = (1.f - a.keep_prob) / (1.f + 1.92f);
-  for (int i = threadIdx.x; i < NV; i += blockDim.x) {
-    const float p = fminf(sS[i] / totS * (float)NV * gamma, 1.f);
-    sS[i] = uni24(a.seed, 2 * a.call, (unsigned)i) < p ? 1.f : 0.f;   // M_seed
+  if ((int)threadIdx.x < V) {
+    const int i = n * V + threadIdx.x;
+    const float p = fminf(d.sS[i] / totS * (float)NV * gamma, 1.f);
+    seedm[threadIdx.x] = uni24(a.seed, 2 * a.call, (unsigned)i) < p ? 1.f : 0.f;
   }
   __syncthreads();
-  // M = (M_seed @ A) > 0.001 ; mask = 1 - M
-  float* fS = bT;  // reuse as scratch for the mask before bT is needed
-  loc = 0.f;
-  for (int i = threadIdx.x; i < NV; i += blockDim.x) {
-    const int n = i / V, w = i - n * V;
+  if ((int)threadIdx.x < V) {
+    const int w = threadIdx.x;
     float m = 0.f;
-    for (int v = 0; v < V; ++v) m += sS[n * V + v] * Ae[v * V + w];
+    for (int v = 0; v < V; ++v) m += seedm[v] * Ae[v * V + w];
     const float mask = m > 0.001f ? 0.f : 1.f;
-    fS[i] = mask;
-    loc += mask;
-  }
-  const float sumS = block_sum(loc, scratch);
-  const float cS = (float)NV / sumS;
-  for (int i = threadIdx.x; i < NV; i += blockDim.x) {
-    const float f = fS[i] * cS;
-    a.fS[i] = f;
-    sS[i] = f;
+    msk[w] = mask;
+    d.mS[n * V + w] = mask;
   }
   __syncthreads();
-  // --- Randomized_DropBlockT_1d on the S-masked input: input_abs = mean_{c,v} |z * fS| per (n, t)
-  loc = 0.f;
-  for (int i = threadIdx.x; i < NT; i += blockDim.x) {
-    const int n = i / T, t = i - n * T;
+  if ((int)threadIdx.x < a.T) {
+    const int t = threadIdx.x;
     float s = 0.f;
-    for (int v = 0; v < V; ++v) s += sS[n * V + v] * a.a[((size_t)n * T + t) * V + v];
+    for (int v = 0; v < V; ++v) s += msk[v] * sA[t * V + v];
     s /= (float)(a.C * V);
-    bT[i] = s;
-    loc += s;
+    bt[t] = s;
+    d.bT[n * a.T + t] = s;
   }
-  const float totT = block_sum(loc, scratch);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.f, s = 0.f;
+    for (int v = 0; v < V; ++v) m += msk[v];
+    for (int t = 0; t < a.T; ++t) s += bt[t];
+    d.rowM[n] = m;
+    d.rowT[n] = s;
+  }
+}
+
+// global part: fS = mask_S * NV / sum(mask_S); the T seed draws, the frame permutation (argsort of
+// hashed keys: the reference's torch.randperm), max_pool1d, fT = mask_T * NT / sum(mask_T)
+__global__ __launch_bounds__(1024) void mu_drop_final_kernel(DropMaskArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, T = a.T, NV = N * a.V, NT = N * T;
+  const DropScr d(a);
+  float* mT = sm;        // [NT] seed mask, then the permuted max-pool mask
+  float* pT = mT + NT;   // [NT] max-pooled
+  __shared__ float red[1024], keys[64];
+  __shared__ int idx[64];
+  const float cS = (float)NV / ordered_sum(d.rowM, N, red);
+  for (int i = threadIdx.x; i < NV; i += blockDim.x) a.fS[i] = d.mS[i] * cS;
+  const float totT = ordered_sum(d.rowT, N, red);
   const float gT = (1.f - a.keep_prob) / (float)a.block_size;
   for (int i = threadIdx.x; i < NT; i += blockDim.x) {
-    const float p = fminf(bT[i] / totT * (float)NT * gT, 1.f);
+    const float p = fminf(d.bT[i] / totT * (float)NT * gT, 1.f);
     mT[i] = uni24(a.seed, 2 * a.call + 1, (unsigned)i) < p ? 1.f : 0.f;
   }
-  // frame permutation: argsort of hashed keys (the reference's torch.randperm)
-  if (threadIdx.x < T) keys[threadIdx.x] = uni24(a.seed ^ 0x5BD1E995u, a.call, threadIdx.x);
+  if ((int)threadIdx.x < T) keys[threadIdx.x] = uni24(a.seed ^ 0x5BD1E995u, a.call, threadIdx.x);
   __syncthreads();
-  if (threadIdx.x < T) {
+  if ((int)threadIdx.x < T) {
     const int t = threadIdx.x;
     int rank = 0;
     for (int j = 0; j < T; ++j) rank += (keys[j] < keys[t]) || (keys[j] == keys[t] && j < t);
@@ -447,15 +513,14 @@ __global__ __launch_bounds__(1024) void mu_dropmask_kernel(DropMaskArgs a) {
     pT[i] = m;
   }
   __syncthreads();
-  loc = 0.f;
+  float loc = 0.f;
   for (int i = threadIdx.x; i < NT; i += blockDim.x) {
     const int n = i / T, t = i - n * T;
     const float mask = 1.f - pT[n * T + idx[t]];
     mT[i] = mask;
     loc += mask;
   }
-  const float sumT = block_sum(loc, scratch);
-  const float cT = (float)NT / sumT;
+  const float cT = (float)NT / block_sum(loc, red);
   for (int i = threadIdx.x; i < NT; i += blockDim.x) a.fT[i] = mT[i] * cT;
 }
 
@@ -759,7 +824,8 @@ static bool c_ok(int C) { return C % 4 == 0 && C >= 16 && C <= 256; }
   } while (0)
 
 static int lane_finalize(double* lanes, int C, double* g1, double* g2, hipStream_t s) {
-  hipLaunchKernelGGL(mu_lane_finalize_kernel, dim3(1), dim3(512), 0, s, lanes, C, g1, g2);
+  hipLaunchKernelGGL(mu_lane_finalize_kernel, dim3((2 * C + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0,
+                     s, lanes, C, g1, g2);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -838,17 +904,23 @@ int f3_mu_absstat(const AbsStatArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
+int f3_mu_dropmask_scratch_floats(int N, int T, int V) { return 2 * N * V + N * T + 3 * N; }
+
 int f3_mu_dropmask(const DropMaskArgs* a, hipStream_t s) {
-  const size_t lds = sizeof(float) * ((size_t)a->N * a->V + 3 * (size_t)a->N * a->T);
-  if (a->V > 32 || a->T > 64 || lds > 150 * 1024) return F3_EINVAL;
+  const size_t lds = sizeof(float) * 2 * (size_t)a->N * a->T;
+  if (a->V > 32 || a->T > 64 || a->T * a->V > 64 * 32 || lds > 150 * 1024 || !a->scr) return F3_EINVAL;
   static bool once = [] {
-    (void)hipFuncSetAttribute((const void*)mu_dropmask_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)mu_drop_final_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               150 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL(mu_dropmask_kernel, dim3(1), dim3(1024), lds, s, *a);
+  hipLaunchKernelGGL(mu_drop_s_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mu_drop_t_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mu_drop_final_kernel, dim3(1), dim3(1024), lds, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

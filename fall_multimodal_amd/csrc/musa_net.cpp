@@ -121,6 +121,7 @@ struct Plan {
   size_t ga, gb, gc, gd;  // backward scratch [R][256]
   size_t part;         // depthwise weight-gradient partials
   size_t mixpart;      // graph-mix dA partial rows
+  size_t dmscr;        // DropBlock scratch (f3_mu_dropmask_scratch_floats)
   size_t lanes;        // per-channel reduction lanes (2 * kLaneDoubles; finalize re-zeroes them)
   size_t total;
 };
@@ -172,6 +173,7 @@ Plan plan(const f3_musa* net, int N) {
   p.gd = take(4 * Rmax * C2);
   p.part = take(4 * 512 * (size_t)CM * 6);
   p.mixpart = take(4 * (size_t)kMixParts * 1024);
+  p.dmscr = take(4 * (size_t)f3_mu_dropmask_scratch_floats(N, net->T, V));
   p.lanes = take(8 * 2 * kLaneDoubles);
   p.total = o;
   return p;
@@ -275,6 +277,7 @@ int drop_masks(const Ctx& c, const StreamWs& w, const float* u, const BnOff* bn,
   dm.N = c.N; dm.T = T; dm.V = c.net->V; dm.C = C; dm.a = as.a; dm.Ae = Ae;
   dm.seed = c.net->seed; dm.call = call; dm.keep_prob = kKeepProb; dm.block_size = kBlockSize;
   dm.fS = fS; dm.fT = fT;
+  dm.scr = c.f(c.p.dmscr);
   (void)w;
   return f3_mu_dropmask(&dm, c.s);
 }

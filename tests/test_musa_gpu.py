@@ -142,3 +142,31 @@ def test_dwconv_kernel_matches_torch(K, S, C, T):
     flat = got.reshape(-1, C)
     assert np.all(np.abs(s[:C].numpy() - flat.sum(0).numpy()) <= 1e-5 * flat.abs().sum(0).numpy())
     assert np.all(np.abs(s[C:].numpy() - (flat * flat).sum(0).numpy()) <= 1e-5 * (flat * flat).sum(0).numpy())
+
+
+@pytest.mark.parametrize("fill", [0xFF, 0x7F])
+def test_musa_workspace_poison_no_uninitialized_reads(fill):
+    """The step's workspace filled with NaN (0xFF bytes) or huge (0x7F) patterns before the step: every
+    region the step reads must have been written (or zeroed) by the step itself, so the results stay
+    at the oracle's (same gates as the DropBlock test at B=16)."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    from oracle.prng import synthetic_batch
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    B = 16
+    st = mu.init_state(78)
+    x, _, label = synthetic_batch(B, 14, 11, 1, 321)
+    model = _model(d, st, dropblock=True)
+    step = f3.musa.MusaStep(model, B)
+    step.ws.fill_(fill)
+    step.grads.fill_(float("nan"))
+    seed = 99
+    step.forward_backward(torch.from_numpy(x).to(d), torch.from_numpy(label).to(d), seed=seed)
+    out_ref, loss_ref, grads_ref = _oracle64(st, x, label, seed)
+    out = step.out.cpu().numpy()
+    ours = {n: step.grads[off:off + int(np.prod(shape))].view(shape).cpu().numpy()
+            for n, shape, off in model.param_views()}
+    assert all(np.isfinite(v).all() for v in ours.values())
+    err, cos, worst = _compare(ours, out, out_ref.numpy(), grads_ref, f"poison 0x{fill:02X}")
+    assert err < 1e-3 and (out.argmax(1) == out_ref.numpy().argmax(1)).all()
+    assert cos >= 0.9999 and worst < 5e-2
