@@ -28,6 +28,7 @@ EXPORTS = (
     "f3_sktr_buffer_count", "f3_sktr_counter_count", "f3_sktr_workspace_bytes", "f3_sktr_forward", "f3_sktr_backward",
     "f3_musa_create", "f3_musa_destroy", "f3_musa_num_entries", "f3_musa_entry", "f3_musa_param_count",
     "f3_musa_buffer_count", "f3_musa_counter_count", "f3_musa_workspace_bytes", "f3_musa_forward", "f3_musa_backward",
+    "f3_musa_guards",
     "f3_dwconv_t_forward",
 )
 
@@ -122,6 +123,7 @@ def lib():
         "f3_musa_buffer_count": (I64, [P]),
         "f3_musa_counter_count": (I64, [P]),
         "f3_musa_workspace_bytes": (I64, [P, I]),
+        "f3_musa_guards": (I, [P, I, ctypes.POINTER(I64), I]),
         "f3_musa_forward": (I, [P, I, I, P, P, P, P, P, P, ctypes.c_uint, I, P]),
         "f3_musa_backward": (I, [P, I, P, P, P, P, P, P]),
         "f3_dwconv_t_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, P]),

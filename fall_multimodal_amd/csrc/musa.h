@@ -18,13 +18,13 @@ namespace mu {
 
 enum : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_LEAKY = 3 };
 constexpr float kLeaky = 0.01f;
-// Per-channel batch sums are reduced workgroup -> one of kLanes fp64 lanes (blockIdx % kLanes) ->
-// the fp64 total in a small finalize launch: thousands of workgroups adding into the same C
-// addresses serialise (measured: 37 us of a 57 us depthwise-conv launch), and so do 32 lanes in
-// a 64 KB block (7 us of a 27 us launch): the atomics execute memory-side, per channel, so the
-// lanes spread them over 256 rows (2 MB with the second set).
-constexpr int kLanes = 256;
-constexpr size_t kLaneDoubles = (size_t)kLanes * 2 * 256;   // lane scratch per reduction (C <= 256)
+// Per-channel batch sums are reduced workgroup (LDS) -> one of kLanes fp32 lane rows (blockIdx %
+// kLanes; memory-side f32 adds) -> fp64 totals in a small finalize launch that re-zeroes the
+// lanes. Measured history (depthwise conv, C=128, B=256): thousands of workgroups adding into 2C
+// fp64 addresses serialised (37 us of a 57 us launch); an in-kernel ticketed finalize (last
+// arriver per XCD group, then last group) cost more than the separate launch (39.7 vs 27 + 5 us).
+constexpr int kLanes = 256, kLaneRow = 512;   // 2C <= kLaneRow
+constexpr size_t kLaneFloats = (size_t)kLanes * kLaneRow;
 
 // depthwise temporal convolution (Conv2d(C, C, (K,1), (S,1), (P,0), groups=C)) over [N][T][V][C]
 struct DwConvArgs {
@@ -34,11 +34,12 @@ struct DwConvArgs {
   const float* b;      // [C]
   float* y;            // fwd out [N][T_out][V][C]
   double* sum; double* sumsq;   // fwd: BatchNorm batch sums of y (accumulated)
-  double* lanes;       // fwd: lane scratch (kLaneDoubles) when sum is set
+  float* lanes;        // fwd: lane scratch (kLaneFloats) when sum is set
   const float* dy;     // bwd in
   float* dx; int dx_add;        // bwd: input gradient (overwrite or +=)
   float* part;         // bwd: per-workgroup weight-gradient partial rows [grid][C*(K+1)]
   int part_rows;       // (out) rows written to part
+  int grid, block;     // set by the launcher (kernels must not read gridDim / blockDim after their stores)
 };
 
 // y = act(BN(u)) (+ add)
@@ -59,9 +60,10 @@ struct BnActBwdArgs {
   BnRef bn;
   int act;
   double* s_dz; double* s_dzx;  // [C] each (zeroed by the caller)
-  double* lanes;                // lane scratch (kLaneDoubles)
+  float* lanes;                 // lane scratch (kLaneFloats)
   float* du; const float* add;
   float* g_gamma; float* g_beta;
+  int grid;            // set by the launcher
 };
 
 // a[r] = sum_c |z[r][c]|, z = BN(u) (or u when bn_on == 0): DropBlock statistics
@@ -92,9 +94,10 @@ struct MergeArgs {
   // backward
   const float* dout;
   double* s1_dz; double* s1_dzx; double* s2_dz; double* s2_dzx;
-  double* lanes;       // lane scratch (2 * kLaneDoubles)
+  float* lanes;        // lane scratch (2 * kLaneFloats)
   float* du1; float* du2; int du2_add;
   float* g_gamma1; float* g_beta1; float* g_gamma2; float* g_beta2;
+  int grid;            // set by the launcher
 };
 
 // column sums of rows (BatchNorm batch statistics of a tensor no producer epilogue covers)
@@ -102,7 +105,8 @@ struct ColStatArgs {
   long long R; int C;
   const float* x;
   double* sum; double* sumsq;
-  double* lanes;       // lane scratch (kLaneDoubles)
+  float* lanes;        // lane scratch (kLaneFloats)
+  int grid;            // set by the launcher
 };
 
 // tokens: pos [R][4] = (x, y, score, 0); mot [Rm][4] = (x[t] - x[t+1], y[t] - y[t+1], 0, 0)

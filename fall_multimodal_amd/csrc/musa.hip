@@ -8,6 +8,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "musa.h"
 
@@ -60,56 +61,69 @@ struct QuadLayout {
   }
 };
 
-// per-channel sums of this workgroup's threads -> its fp64 lane (lanes[l][0..C) and [C..2C))
-F3_DEV void channel_flush(int C, int q, bool act, const float (&s1)[4], const float (&s2)[4], double* lanes) {
-  __shared__ float r1[256], r2[256];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) r1[c] = r2[c] = 0.f;
-  __syncthreads();
+// per-channel sums of this workgroup's threads -> its fp32 lane (lanes[l][0..C) and [C..2C)),
+// totalled in fp64 by mu_lane_finalize_kernel. Straight-line code behind raw barriers, and nb (the
+// block size) from a kernel argument: a loop, a __syncthreads fence or a blockDim read (a vector
+// load from the dispatch packet) ahead of the lane adds made hipcc wait vmcnt(0) for the
+// workgroup's row stores first (7 us of a 27 us conv launch). Needs C <= 256 and nb >= C.
+F3_DEV void channel_flush(int C, int q, bool act, const float (&s1)[4], const float (&s2)[4], float* lanes, int nb) {
+  __shared__ float r[512];
+  const int t = threadIdx.x, n2 = 2 * C;
+  if (t < n2) r[t] = 0.f;
+  if (t + nb < n2) r[t + nb] = 0.f;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   if (act)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      atomicAdd(r1 + 4 * q + e, s1[e]);
-      atomicAdd(r2 + 4 * q + e, s2[e]);
+      atomicAdd(r + 4 * q + e, s1[e]);
+      atomicAdd(r + C + 4 * q + e, s2[e]);
     }
-  __syncthreads();
-  double* l = lanes + (size_t)(blockIdx.x % kLanes) * 2 * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(l + c, (double)r1[c]);
-    atomicAdd(l + C + c, (double)r2[c]);
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // one wave issues the lane adds (the others end here)
+  if (t >= 64) return;
+  float* l = lanes + (size_t)(blockIdx.x % kLanes) * kLaneRow;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = t + 64 * i < n2 ? r[t + 64 * i] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (t + 64 * i < n2) atomicAdd(l + t + 64 * i, v[i]);
 }
-F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], const float (&s2)[4], double* lanes) {
-  channel_flush(C, L.q, L.act, s1, s2, lanes);
+F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], const float (&s2)[4], float* lanes) {
+  channel_flush(C, L.q, L.act, s1, s2, lanes, 256);  // QuadLayout kernels run 256 threads
 }
 
-// totals of the lanes: g1[c] += sum_l lanes[l][c], g2[c] += sum_l lanes[l][C + c]; lanes re-zeroed.
-// Workgroup w owns columns [64w, 64w + 64) of the 2C; its 16 lane groups of 64 threads walk every
-// 16th lane with all loads independent (one memory round trip), then the groups are summed in a
-// fixed order.
+// totals of the lanes: g1[c] += sum_l lanes[l][c], g2[c] += sum_l lanes[l][C + c] (fp64); lanes
+// re-zeroed. Workgroup w owns columns [64w, 64w + 64) of the 2C; its 16 lane groups of 64 threads
+// walk every 16th lane with all loads independent (and the g1 / g2 read issued with them: one
+// memory round trip), then the groups are summed in a fixed order.
 constexpr int kFinCols = 64, kFinGroups = 16;
-__global__ __launch_bounds__(kFinCols * kFinGroups) void mu_lane_finalize_kernel(double* lanes, int C, double* g1,
+__global__ __launch_bounds__(kFinCols * kFinGroups) void mu_lane_finalize_kernel(float* lanes, int C, double* g1,
                                                                                  double* g2) {
   __shared__ double red[kFinGroups][kFinCols];
   const int n2 = 2 * C, j = threadIdx.x % kFinCols, grp = threadIdx.x / kFinCols;
   const int c = blockIdx.x * kFinCols + j;
-  double s = 0.0;
+  double s = 0.0, g = 0.0;
   if (c < n2) {
     constexpr int kPer = kLanes / kFinGroups;
-    double v[kPer];
+    float v[kPer];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) v[i] = lanes[(size_t)(grp + i * kFinGroups) * n2 + c];
+    for (int i = 0; i < kPer; ++i) v[i] = lanes[(size_t)(grp + i * kFinGroups) * kLaneRow + c];
+    if (grp == 0) g = c < C ? g1[c] : g2[c - C];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      lanes[(size_t)(grp + i * kFinGroups) * n2 + c] = 0.0;
-      s += v[i];
+      lanes[(size_t)(grp + i * kFinGroups) * kLaneRow + c] = 0.f;
+      s += (double)v[i];
     }
   }
   red[grp][j] = s;
   __syncthreads();
   if (grp == 0 && c < n2) {
     for (int k = 1; k < kFinGroups; ++k) s += red[k][j];
-    if (c < C) g1[c] += s;
-    else g2[c - C] += s;
+    if (c < C) g1[c] = g + s;
+    else g2[c - C] = g + s;
   }
 }
 
@@ -119,15 +133,16 @@ F3_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 // ------------------------------------------------------------------------------------------
 // depthwise temporal conv (SepTemporal_Block depth_conv / Sep_TCN sep31, sep11; :163-166, 429-436)
 // ------------------------------------------------------------------------------------------
-// One thread per (clip n, joint v, channel quad q, chunk of TC output frames): the K-frame input
-// window slides in registers (one new 16-B row load per output at stride 1, two at stride 2, the
-// next step's loads issued before this step's FMAs), so every input row is read once per chunk and
-// consecutive threads read consecutive 16-B pieces of a row (joint-major rows of C channels: a wave
-// covers 64 quads of one or two joints' rows). 32-bit index math; chunks keep ~28 waves per CU busy.
+// One thread per (clip n, joint v, channel quad q, chunk of 8 output frames): the chunk's
+// (8-1)*S + K input rows are loaded at once into registers, so every input row is read once per
+// chunk (plus the K-S overlap with the neighbouring chunk) and consecutive threads read
+// consecutive 16-B pieces of a row (joint-major rows of C channels: a wave covers 64 quads of one
+// or two joints' rows). The grid is capped (1024 workgroups) and walks the items with a stride
+// that is a multiple of the quad count, so a thread's BN partial sums stay per channel quad.
 constexpr int kDwChunk = 8;
 
 template <int K, int S>
-__global__ __launch_bounds__(256) void mu_dwconv_fwd_kernel(DwConvArgs a) {
+__global__ __launch_bounds__(512) void mu_dwconv_fwd_kernel(DwConvArgs a) {
   const int nq = a.C >> 2;
   const int nchunk = (a.T_out + kDwChunk - 1) / kDwChunk;
   const int total = a.N * a.V * nq * nchunk;
@@ -149,35 +164,38 @@ __global__ __launch_bounds__(256) void mu_dwconv_fwd_kernel(DwConvArgs a) {
     const int ch = rest % nchunk, n = rest / nchunk;
     const float* xb = a.x + ((size_t)n * a.T_in * a.V + v) * a.C + 4 * q;
     float* yb = a.y + ((size_t)n * a.T_out * a.V + v) * a.C + 4 * q;
-    auto load = [&](int ti) -> f32x4 {
-      return (ti >= 0 && ti < a.T_in) ? ld4(xb + (size_t)ti * rstride) : f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    const int t0 = ch * kDwChunk, t1 = min(a.T_out, t0 + kDwChunk);
-    f32x4 xw[K];  // xw[k] = x[to*S + k - P]
+    // the chunk's whole input window is loaded up front (clamped frames, zeroed after): every
+    // load is in flight at once, and no load is conditional (a conditional load makes hipcc
+    // wait vmcnt(0) per output)
+    constexpr int NIN = (kDwChunk - 1) * S + K;
+    const int t0 = ch * kDwChunk, nout = min(a.T_out - t0, kDwChunk);
+    const int tb = t0 * S - a.P;
+    f32x4 xw[NIN];
 #pragma unroll
-    for (int k = 0; k < K; ++k) xw[k] = load(t0 * S + k - a.P);
-    for (int to = t0; to < t1; ++to) {
-      f32x4 nx[S];  // the next output's new window rows, in flight during this output's FMAs
+    for (int i = 0; i < NIN; ++i) xw[i] = ld4(xb + (size_t)min(max(tb + i, 0), a.T_in - 1) * rstride);
 #pragma unroll
-      for (int j = 0; j < S; ++j) nx[j] = load((to + 1) * S + K - S + j - a.P);
-      f32x4 acc = b;
+    for (int i = 0; i < NIN; ++i)
+      if (tb + i < 0 || tb + i >= a.T_in) xw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < K; ++k)
+    for (int o = 0; o < kDwChunk; ++o) {
+      if (o < nout) {
+        f32x4 acc = b;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w[k][e], xw[k][e], acc[e]);
-      st4(yb + (size_t)to * rstride, acc);
+        for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s1[e] += acc[e];
-        s2[e] = fmaf(acc[e], acc[e], s2[e]);
+          for (int e = 0; e < 4; ++e) acc[e] = fmaf(w[k][e], xw[o * S + k][e], acc[e]);
+        st4(yb + (size_t)(t0 + o) * rstride, acc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += acc[e];
+          s2[e] = fmaf(acc[e], acc[e], s2[e]);
+        }
       }
-#pragma unroll
-      for (int k = 0; k < K - S; ++k) xw[k] = xw[k + S];
-#pragma unroll
-      for (int j = 0; j < S; ++j) xw[K - S + j] = nx[j];
     }
   }
-  if (a.sum) channel_flush(a.C, q, g0 < total, s1, s2, a.lanes);
+  if (a.sum) {
+    channel_flush(a.C, q, g0 < total, s1, s2, a.lanes, a.block);
+  }
 }
 
 // dx[n][ti][v][c] = sum_k dy[n][to][v][c] w[c][k], ti = to*S + k - P
@@ -247,9 +265,9 @@ __global__ __launch_bounds__(256) void mu_dwconv_dw_kernel(DwConvArgs a) {
     }
   }
   __syncthreads();
-  const size_t G = gridDim.x;
-  for (int i = threadIdx.x; i < a.C * K; i += blockDim.x) a.part[(size_t)blockIdx.x * a.C * K + i] = red[i];
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) a.part[G * a.C * K + (size_t)blockIdx.x * a.C + c] = red[a.C * K + c];
+  const size_t G = a.part_rows;  // == gridDim.x (set by the launcher)
+  for (int i = threadIdx.x; i < a.C * K; i += 256) a.part[(size_t)blockIdx.x * a.C * K + i] = red[i];
+  for (int c = threadIdx.x; c < a.C; c += 256) a.part[G * a.C * K + (size_t)blockIdx.x * a.C + c] = red[a.C * K + c];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -595,7 +613,7 @@ __global__ __launch_bounds__(256) void mu_merge_bwd_reduce_kernel(MergeArgs a) {
   channel_flush(a.C, L, p1, q1, a.lanes);
   if (a.bn2_on) {
     __syncthreads();
-    channel_flush(a.C, L, p2, q2, a.lanes + kLaneDoubles);
+    channel_flush(a.C, L, p2, q2, a.lanes + kLaneFloats);
   }
 }
 
@@ -823,7 +841,8 @@ static bool c_ok(int C) { return C % 4 == 0 && C >= 16 && C <= 256; }
     if (_st != F3_OK) return _st; \
   } while (0)
 
-static int lane_finalize(double* lanes, int C, double* g1, double* g2, hipStream_t s) {
+
+static int lane_finalize(float* lanes, int C, double* g1, double* g2, hipStream_t s) {
   hipLaunchKernelGGL(mu_lane_finalize_kernel, dim3((2 * C + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0,
                      s, lanes, C, g1, g2);
   F3_LAUNCH_CHECK();
@@ -838,9 +857,21 @@ int f3_mu_dwconv_fwd(const DwConvArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
   const long long total = (long long)a->N * a->V * (a->C / 4) * ((a->T_out + kDwChunk - 1) / kDwChunk);
   if (total >= (1LL << 31)) return F3_EINVAL;
-  const int nq = a->C / 4, block = 256 / nq * nq;  // a multiple of nq (the thread's quad stays fixed)
+  // F3_DW_BLOCK: threads per workgroup (rounded down to a multiple of the quad count, so a
+  // thread's channel quad stays fixed over its grid-stride walk)
+  static const int bt = getenv("F3_DW_BLOCK") ? std::min(512, std::max(256, atoi(getenv("F3_DW_BLOCK")))) : 256;
+  const int nq = a->C / 4, block = bt / nq * nq;
   const long long want = (total + block - 1) / block;
-  const int grid = (int)std::min<long long>(want, 1024);  // <= 1024 workgroup flushes into the lanes
+  // F3_DW_GRID: the workgroup cap. Measured (C=128, V=14, T=30, B=256, k3): the BN-sum epilogue
+  // costs ~2.3 ns per wave of the grid at the launch's end (1024 x 256 threads: 28.3 vs 18.8 us
+  // without sums; 512 x 256: 24.9 vs 19.9; 512-thread blocks or one wave issuing the lane adds:
+  // the same), so 512 workgroups of 256 threads
+  static const int cap = getenv("F3_DW_GRID") ? std::max(64, atoi(getenv("F3_DW_GRID"))) : 512;
+  const int grid = (int)std::min<long long>(want, cap);
+  DwConvArgs b = *a;
+  b.grid = grid;
+  b.block = block;
+  a = &b;
   if (a->K == 1 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<1, 1>), dim3(grid), dim3(block), 0, s, *a);
   else if (a->K == 3 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<3, 1>), dim3(grid), dim3(block), 0, s, *a);
   else if (a->K == 5 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<5, 1>), dim3(grid), dim3(block), 0, s, *a);
@@ -882,7 +913,9 @@ int f3_mu_bn_act(const BnActArgs* a, hipStream_t s) {
 
 int f3_mu_bn_act_bwd(const BnActBwdArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
-  hipLaunchKernelGGL(mu_bn_act_bwd_reduce_kernel, dim3(quad_grid(a->R, a->C, 1024)), dim3(256), 0, s, *a);
+  BnActBwdArgs b = *a;
+  b.grid = quad_grid(a->R, a->C, 1024);
+  hipLaunchKernelGGL(mu_bn_act_bwd_reduce_kernel, dim3(b.grid), dim3(256), 0, s, b);
   F3_LAUNCH_CHECK();
   F3_TRY_MU(lane_finalize(a->lanes, a->C, a->s_dz, a->s_dzx, s));
   hipLaunchKernelGGL(mu_bn_act_bwd_apply_kernel, dim3(grid_for(a->R * a->C / 4)), dim3(256), 0, s, *a);
@@ -892,7 +925,9 @@ int f3_mu_bn_act_bwd(const BnActBwdArgs* a, hipStream_t s) {
 
 int f3_mu_colstat(const ColStatArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
-  hipLaunchKernelGGL(mu_colstat_kernel, dim3(quad_grid(a->R, a->C, 1024)), dim3(256), 0, s, *a);
+  ColStatArgs b = *a;
+  b.grid = quad_grid(a->R, a->C, 1024);
+  hipLaunchKernelGGL(mu_colstat_kernel, dim3(b.grid), dim3(256), 0, s, b);
   F3_LAUNCH_CHECK();
   return lane_finalize(a->lanes, a->C, a->sum, a->sumsq, s);
 }
@@ -935,10 +970,12 @@ int f3_mu_merge_fwd(const MergeArgs* a, hipStream_t s) {
 int f3_mu_merge_bwd(const MergeArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
   const long long R = (long long)a->N * a->T * a->V;
-  hipLaunchKernelGGL(mu_merge_bwd_reduce_kernel, dim3(quad_grid(R, a->C, 1024)), dim3(256), 0, s, *a);
+  MergeArgs b = *a;
+  b.grid = quad_grid(R, a->C, 1024);
+  hipLaunchKernelGGL(mu_merge_bwd_reduce_kernel, dim3(b.grid), dim3(256), 0, s, b);
   F3_LAUNCH_CHECK();
   F3_TRY_MU(lane_finalize(a->lanes, a->C, a->s1_dz, a->s1_dzx, s));
-  if (a->bn2_on) F3_TRY_MU(lane_finalize(a->lanes + kLaneDoubles, a->C, a->s2_dz, a->s2_dzx, s));
+  if (a->bn2_on) F3_TRY_MU(lane_finalize(a->lanes + kLaneFloats, a->C, a->s2_dz, a->s2_dzx, s));
   hipLaunchKernelGGL(mu_merge_bwd_apply_kernel, dim3(grid_for(R * a->C / 4)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;

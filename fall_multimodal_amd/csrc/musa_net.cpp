@@ -14,6 +14,7 @@
 // block merges: musa.hip.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -122,18 +123,30 @@ struct Plan {
   size_t part;         // depthwise weight-gradient partials
   size_t mixpart;      // graph-mix dA partial rows
   size_t dmscr;        // DropBlock scratch (f3_mu_dropmask_scratch_floats)
-  size_t lanes;        // per-channel reduction lanes (2 * kLaneDoubles; finalize re-zeroes them)
+  size_t lanes;        // per-channel reduction lanes (2 * kLaneFloats; finalize re-zeroes them)
   size_t total;
 };
 
 constexpr int kPackPerStream = C1 * E * 2 + C1 * C1 * 3 + CM * C1 + C2 * CM + C2 * C1;
 
-Plan plan(const f3_musa* net, int N) {
+// F3_MU_GUARD=<bytes> (debugging): a guard band after every region; f3_musa_guards lists them so a
+// tool can fill the workspace with a pattern and find any kernel writing outside its region
+size_t guard_bytes() {
+  static const size_t g = getenv("F3_MU_GUARD") ? (size_t)atol(getenv("F3_MU_GUARD")) / 256 * 256 : 0;
+  return g;
+}
+
+Plan plan(const f3_musa* net, int N, std::vector<size_t>* guards = nullptr) {
   Plan p;
   size_t o = 0;
+  const size_t gb = guard_bytes();
   auto take = [&](size_t bytes) {
     const size_t at = o;
     o += (bytes + 255) / 256 * 256;
+    if (gb) {
+      if (guards) guards->push_back(o);
+      o += gb;
+    }
     return at;
   };
   const int V = net->V;
@@ -174,7 +187,7 @@ Plan plan(const f3_musa* net, int N) {
   p.part = take(4 * 512 * (size_t)CM * 6);
   p.mixpart = take(4 * (size_t)kMixParts * 1024);
   p.dmscr = take(4 * (size_t)f3_mu_dropmask_scratch_floats(N, net->T, V));
-  p.lanes = take(8 * 2 * kLaneDoubles);
+  p.lanes = take(4 * 2 * kLaneFloats);
   p.total = o;
   return p;
 }
@@ -251,7 +264,7 @@ struct Ctx {
     return r;
   }
   float* f(size_t off) const { return at<float>(ws, off); }
-  double* lanes() const { return at<double>(ws, p.lanes); }
+  float* lanes() const { return at<float>(ws, p.lanes); }
 };
 
 int gemm_fwd(const Ctx& c, ConvGemmArgs a, const BnOff* stats) {
@@ -644,7 +657,7 @@ int f3_musa_forward(f3_musa* net, int N, int training, const float* params, floa
   net->drop = training && dropout;
   Ctx c{net, p, workspace, params, buffers, nullptr, training != 0, N, s};
   if (training && hipMemsetAsync(at<char>(workspace, p.fsum), 0, 8 * 22 * 512, s) != hipSuccess) return F3_EHIP;
-  if (training && hipMemsetAsync(at<char>(workspace, p.lanes), 0, 8 * 2 * kLaneDoubles, s) != hipSuccess) return F3_EHIP;
+  if (training && hipMemsetAsync(at<char>(workspace, p.lanes), 0, 4 * 2 * kLaneFloats, s) != hipSuccess) return F3_EHIP;
   TokenArgs tk;
   std::memset(&tk, 0, sizeof(tk));
   tk.N = N; tk.T = net->T; tk.V = net->V; tk.x = x; tk.pos = c.f(p.s[0].tok); tk.mot = c.f(p.s[1].tok);
@@ -709,7 +722,7 @@ int f3_musa_backward(f3_musa* net, int N, const float* params, const float* buff
   Ctx c{net, p, workspace, params, const_cast<float*>(buffers), grads, true, N, s};
   if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
   if (hipMemsetAsync(at<char>(workspace, p.bsum), 0, 8 * 22 * 512, s) != hipSuccess) return F3_EHIP;
-  if (hipMemsetAsync(at<char>(workspace, p.lanes), 0, 8 * 2 * kLaneDoubles, s) != hipSuccess) return F3_EHIP;
+  if (hipMemsetAsync(at<char>(workspace, p.lanes), 0, 4 * 2 * kLaneFloats, s) != hipSuccess) return F3_EHIP;
   float* dres2T[2];
   {  // transposed 1x1 weights ([I][O] from [O][I]) for the input-gradient GEMMs
     PrepTable t;
@@ -750,6 +763,14 @@ int f3_musa_backward(f3_musa* net, int N, const float* params, const float* buff
   return F3_OK;
 }
 
+int f3_musa_guards(const f3_musa* net, int batch, int64_t* offsets, int max) {
+  if (!net || batch < 1) return -1;
+  std::vector<size_t> g;
+  (void)plan(net, batch, &g);
+  for (int i = 0; i < (int)g.size() && i < max; ++i) offsets[i] = (int64_t)g[i];
+  return (int)g.size();
+}
+
 int f3_dwconv_t_forward(const float* x, const float* w, const float* b, float* y, double* sums, int N, int T_in,
                         int V, int C, int K, int S, int P, void* stream) {
   if (!x || !w || !b || !y || N < 1 || T_in < 1 || V < 1 || S < 1 || P < 0) return F3_EINVAL;
@@ -759,10 +780,10 @@ int f3_dwconv_t_forward(const float* x, const float* w, const float* b, float* y
   if (a.T_out < 1) return F3_EINVAL;
   a.x = x; a.w = w; a.b = b; a.y = y;
   if (sums) {
-    static double* lanes = nullptr;  // test / bench entry only: lane scratch kept for the process lifetime
+    static float* lanes = nullptr;  // test / bench entry only: lane scratch kept for the process lifetime
     if (!lanes) {
-      if (hipMalloc(&lanes, sizeof(double) * kLaneDoubles) != hipSuccess) return F3_EHIP;
-      if (hipMemset(lanes, 0, sizeof(double) * kLaneDoubles) != hipSuccess) return F3_EHIP;
+      if (hipMalloc(&lanes, sizeof(float) * kLaneFloats) != hipSuccess) return F3_EHIP;
+      if (hipMemset(lanes, 0, sizeof(float) * kLaneFloats) != hipSuccess) return F3_EHIP;
     }
     a.sum = sums; a.sumsq = sums + C; a.lanes = lanes;
   }

@@ -217,6 +217,9 @@ int f3_musa_forward(f3_musa* net, int batch, int training, const float* params, 
  * reference leaves their .grad None: A is frozen, those edges only shape DropBlock masks). */
 int f3_musa_backward(f3_musa* net, int batch, const float* params, const float* buffers, const float* dout,
                      float* grads, void* workspace, void* stream);
+/* Debug: with F3_MU_GUARD=<bytes> set before the library loads, the workspace plan puts a guard band
+ * of that size after every region; this lists the guard offsets (returns the count; -1 on error). */
+int f3_musa_guards(const f3_musa* net, int batch, int64_t* offsets, int max);
 /* Kernel-level entry (tests, bench.py roofline): the depthwise temporal conv of SepTemporal_Block /
  * Sep_TCN, Conv2d(C, C, (K,1), (S,1), (P,0), groups=C) on channels-last x [N,T_in,V,C] -> y
  * [N,T_out,V,C], w [C][K], b [C]; sums (optional, [2C] fp64, accumulated): BatchNorm batch sums of y. */
