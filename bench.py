@@ -79,11 +79,12 @@ def _time_launch(fn, reps=20):
 def roofline_kernels(dev, batch, V, precision):
     """The step's GEMM kernels on the layer-6 tcn shape (C=256, T=8, 9 taps, B clips), each
     launched alone through the C ABI exactly as the step launches it:
-    * "wgrad": the tcn weight gradient as the step computes it: wgrad_big<4,2,4,4,64> (split-K
-      partials into the slab) + wgrad_slab_reduce (partials summed into dW[Cout][Cin][KT]);
+    * "wgrad": the tcn weight gradient as the step computes it: wgrad_taps<5> (all 9 taps of a
+      64x64 tile from one staged copy of each clip; split-K partials into the slab; F3_WGRAD_TAPS=0:
+      the per-tap wgrad_big<4,2,4,4,64>) + wgrad_slab_reduce (partials summed into dW[Cout][Cin][KT]);
       f3_conv_backward_weight(bf16). The headline roofline (the step's largest kernel share,
       profiles/r01_bf16_kernel_summary.txt);
-    * "wgrad_kernel": wgrad_big alone (partials left in the slab), for the kernel's own fraction;
+    * "wgrad_kernel": the GEMM kernel alone (partials left in the slab), for the kernel's own fraction;
     * "tcn_fwd": the forward implicit GEMM igemm_big<1,1,8> with bf16 output (the step writes
       the tcn output bf16; its launch igemm_big<13,1,8> adds the BN-statistics/pool epilogue).
     Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for all three."""
@@ -114,14 +115,17 @@ def roofline_kernels(dev, batch, V, precision):
         dw = torch.empty(C, C, KT, device=dev)
         ms = _time_launch(lambda: lib.f3_conv_backward_weight(L.ptr(dy), L.ptr(x), L.ptr(dw), None, N, T, V, C, C, KT,
                                                               1, 4, 1, st))
-        out["wgrad"] = {"kernel": f"wgrad_big<4,2,4,4,64> + wgrad_slab_reduce (tcn 9x1 weight gradient incl. the "
+        taps = os.environ.get("F3_WGRAD_TAPS", "1") != "0" and V % 2 == 0
+        kname = "wgrad_taps<5>" if taps else "wgrad_big<4,2,4,4,64>"
+        out["wgrad"] = {"kernel": f"{kname} + wgrad_slab_reduce (tcn 9x1 weight gradient incl. the "
                                   f"split-K reduce, C=256, T=8, N={N}, V={V})", "ms": ms}
-        cap = 512 * 128 * 128 * max(1, int(os.environ.get("F3_SLAB_X", "1")))  # the step's slab (net.cpp wgrad_slab_floats)
+        # the step's slab (net.cpp wgrad_slab_floats)
+        cap = max(512 * 128 * 128, 16 * 256 * 256 * 9) * max(1, int(os.environ.get("F3_SLAB_X", "1")))
         slab = torch.empty(cap, device=dev)
         L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4, st), "wgrad")
         ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4,
                                                            st))
-        out["wgrad_kernel"] = {"kernel": f"wgrad_big<4,2,4,4,64> alone (partials left in the slab, C=256, T=8, N={N}, "
+        out["wgrad_kernel"] = {"kernel": f"{kname} alone (partials left in the slab, C=256, T=8, N={N}, "
                                          f"V={V})", "ms": ms}
     pmc = {}
     if os.path.exists(ROOFLINE_PMC):

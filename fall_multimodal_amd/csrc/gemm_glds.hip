@@ -919,6 +919,271 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// wgrad_taps: the stride-1 (9,1) tcn weight gradient with all 9 taps of a 64 co x 64 ci tile
+// computed from ONE staged copy of each clip's rows. wgrad_big restages the dY and input rows
+// once per tap (each tap is its own workgroup tile), so its L2 -> LDS fill is ~12x the
+// algorithmic bytes and bounds it; here a workgroup stages a whole clip's dY rows [T*V][64 co]
+// and input rows [T*V][64 ci] once, and tap dt reads the input tile shifted by dt*V rows. The
+// input region keeps 4V zero rows above and below the clip (written once, never staged into),
+// so a shifted window needs no masking; the dY region's rows past T*V (up to a 32-row multiple)
+// stay zero, so the padded k steps add nothing. Fragments come from the same swizzled layout and
+// transposed LDS reads as wgrad_big; the swizzle of a shifted row is taken per tap (it stays
+// bank-conflict-free for any shift, checked exhaustively for V = 14 / 18).
+// Waves: w & 3 picks the 16-column ci slice, w >> 2 the tap half (taps 0-4 or 5-8): the two waves
+// sharing a SIMD issue 20 + 16 MFMAs per k step. Split-K over clips into slab[split] (plain
+// stores), summed by wgrad_slab_reduce_kernel. One workgroup per CU (118 KiB of LDS), two stages.
+// Needs: bf16 operands, forward geometry with S = 1, KT = 9, P = 4, T_in = T_out, V even,
+// T*V % 8 == 0, roundup(T*V, 32) == 32*NKS, Nc % 64 == 0, Kc % 64 == 0.
+// ----------------------------------------------------------------------------
+template <int NKS, int PAD = 0>
+__global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
+  constexpr int R = 128;                    // row bytes of both tiles (64 bf16)
+  constexpr int TVP = 32 * NKS;             // padded clip rows
+  constexpr int VMAX = 18;
+  constexpr int Y_BYTES = TVP * R, X_BYTES = (TVP + 8 * VMAX) * R, STAGE = Y_BYTES + X_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 64 * 4 + PAD];
+  if (PAD && blockIdx.x == (1u << 30)) smem[2 * STAGE + 256 + PAD - 1] = 1;
+  float* dbs = reinterpret_cast<float*>(smem + 2 * STAGE);  // [64]
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int V = g.V, TV = g.T_out * g.V;
+  const int jt = g.Nc / 64, tiles = jt * (g.Kc / 64);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a split's tiles stay on one XCD
+  const int bz = lin / tiles, tile = lin - bz * tiles;
+  const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
+  const int n_begin = bz * a.rows_per_split;          // rows_per_split holds clips per split here
+  const int n_end = min(g.M / TV, n_begin + a.rows_per_split);
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+
+  // zero both stages once: the halo / padding rows are never staged into
+  for (int o = tid * 16; o < 2 * STAGE; o += 512 * 16) *reinterpret_cast<f32x4*>(smem + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- staging: 1-KiB pieces (8 rows), dY pieces then input pieces; a lane's slots are fixed ----
+  const int npy = TV / 8, np = 2 * npy, ppw = (np + 7) / 8;
+  const int sub = lane >> 3, ph = lane & 7;
+  constexpr int PPW_MAX = (2 * TVP / 8 + 7) / 8;
+  unsigned ldso[PPW_MAX];
+  long long srco[PPW_MAX];
+  bool isy[PPW_MAX];
+#pragma unroll
+  for (int k = 0; k < PPW_MAX; ++k) {
+    int piece = k * 8 + wave;
+    if (piece >= np) piece %= np;  // the last round re-issues earlier pieces: same bytes, same place
+    const bool y = piece < npy;
+    const int pr = y ? piece : piece - npy;           // piece index within its tile
+    const int crow = pr * 8 + sub;                    // clip-local row
+    const int brow = y ? crow : 4 * V + crow;         // buffer row in its region
+    const int u = (ph >> 1) ^ wswz<4>(brow);
+    const int col = (u * 2 + (ph & 1)) * 8;
+    isy[k] = y;
+    ldso[k] = (unsigned)((y ? 0 : Y_BYTES) + brow * R + ph * 16);
+    srco[k] = y ? (long long)crow * a.ldy + j0 + col : (long long)crow * g.lda + i0 + col;
+  }
+  auto stage = [&](int n, int buf) {
+    const long long by = (long long)n * TV * a.ldy, bx = (long long)n * TV * g.lda;
+#pragma unroll
+    for (int k = 0; k < PPW_MAX; ++k) {
+      if (k < ppw) {
+        const __bf16* src = isy[k] ? dyb + by + srco[k] : xb + bx + srco[k];
+        // the DMA writes lane L's 16 B at (M0 + instruction offset) + 16 L: pass the piece base
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (lds_void_t*)(size_t)(lds0 + buf * STAGE + ldso[k] - lane * 16), 16, 0, 0);
+      }
+    }
+  };
+
+  // ---- fragment lanes ----
+  const int wi = wave & 3, kh = wave >> 2;
+  const int ntap = kh == 0 ? 5 : 4, dt0 = kh * 5;
+  const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
+  const int r0 = 8 * fg + tq;
+  const int fa = wswz<4>(r0);  // unchanged at r0 + 4 and r0 + 32*ks
+  unsigned offa[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) offa[x] = r0 * R + ((x ^ fa) * 32) + tp * 8;
+  unsigned offl[5], offh[5];
+  // every wave issues 5 tap reads (the second half's 5th repeats its 4th, unused): a read under a
+  // wave-varying condition let hipcc repack the other reads' destination registers before the
+  // lgkmcnt wait (measured: garbage in taps 2-3 whenever the LDS was slow, i.e. inside the step)
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt) {
+    const int rl = r0 + (dt0 + min(tt, ntap - 1)) * V, rh = rl + 4;
+    offl[tt] = Y_BYTES + rl * R + ((wi ^ wswz<4>(rl)) * 32) + tp * 8;
+    offh[tt] = Y_BYTES + rh * R + ((wi ^ wswz<4>(rh)) * 32) + tp * 8;
+  }
+
+  f32x4 acc[5][4];
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[tt][x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_db = a.db && i0 == 0 && wi == 0 && kh == 0;
+  float dbp[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nst = n_end - n_begin;
+  if (nst > 0) {
+    stage(n_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < nst; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nst) stage(n_begin + t + 1, buf ^ 1);
+    const unsigned base = lds0 + buf * STAGE;
+    // k step ks + 1's 26 fragment reads are issued before k step ks's MFMAs (two register sets);
+    // the loop is branch-free between every read and its wait, so no read destination can be
+    // touched early (the second half's 5th tap is computed into an accumulator it discards)
+    s16x4_t lo[2][9], hi[2][9];
+    auto issue = [&](int ks, s16x4_t (&l)[9], s16x4_t (&h)[9]) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const unsigned p = base + offa[x] + ks * 32 * R;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[x]) : "v"(p));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(h[x]) : "v"(p), "n"(4 * R));
+      }
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[4 + tt]) : "v"(base + offl[tt] + ks * 32 * R));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(h[4 + tt]) : "v"(base + offh[tt] + ks * 32 * R));
+      }
+    };
+    issue(0, lo[0], hi[0]);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int c = ks & 1;
+      tr_wait(lo[c], hi[c]);
+      bf16x8 fa_[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        fa_[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][x], hi[c][x], 0, 1, 2, 3, 4, 5, 6, 7));
+      if (do_db) {  // before the next reads are issued: no branch while they are in flight
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dbp[x] += (float)fa_[x][e];
+      }
+      if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        const bf16x8 fb =
+            __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fb, acc[tt][x]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (a.db && i0 == 0) {
+    if (do_db) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        dbp[x] += __shfl_xor(dbp[x], 16, 64);
+        dbp[x] += __shfl_xor(dbp[x], 32, 64);
+      }
+      if (fg == 0)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) dbs[x * 16 + fr] = dbp[x];
+    }
+    __syncthreads();
+    if (tid < 64 && nst > 0) atomic_add_f(a.db + j0 + tid, dbs[tid]);
+  }
+  float* slab = a.slab + (size_t)bz * g.Nc * 9 * g.Kc;
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt) {
+    if (tt < ntap) {
+      const int dt = dt0 + tt;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = j0 + x * 16 + fg * 4 + r, i = i0 + wi * 16 + fr;
+          slab[(size_t)j * 9 * g.Kc + (size_t)dt * g.Kc + i] = acc[tt][x][r];
+        }
+    }
+  }
+}
+
+// dw_ref[j][i][dt] += sum_s slab[s][j][dt*Kc + i] for wgrad_taps' 9-tap slab. Thread (j, i) keeps
+// the 9 tap sums, walks the splits four at a time (36 independent loads, each wave reading 256
+// contiguous bytes per tap), and writes its 9 consecutive outputs (a wave writes 64 * 36 contiguous
+// bytes). Workgroup = 4 output rows j x 64 columns i.
+__global__ __launch_bounds__(256) void wgrad_taps_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
+                                                                 int Kc, float* __restrict__ dw_ref) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63), j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const size_t per = (size_t)Nc * 9 * Kc;
+  const float* p = slab + (size_t)j * 9 * Kc + i;
+  float acc[9];
+#pragma unroll
+  for (int d = 0; d < 9; ++d) acc[d] = 0.f;
+  int sp = 0;
+  for (; sp + 4 <= splits; sp += 4) {
+    float v[4][9];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int d = 0; d < 9; ++d) v[q][d] = p[(size_t)(sp + q) * per + (size_t)d * Kc];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int d = 0; d < 9; ++d) acc[d] += v[q][d];
+  }
+  for (; sp < splits; ++sp)
+#pragma unroll
+    for (int d = 0; d < 9; ++d) acc[d] += p[(size_t)sp * per + (size_t)d * Kc];
+  float* o = dw_ref + ((size_t)j * Kc + i) * 9;
+#pragma unroll
+  for (int d = 0; d < 9; ++d) o[d] += acc[d];
+}
+
+// wgrad_taps applies (see its comment); nks = padded clip rows / 32
+static int wgrad_taps_nks(const WgradArgs& a) {
+  const ConvGeom& g = a.g;
+  if (!a.dyb || !a.inb || !a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || g.transposed) return 0;
+  if (g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out || g.V % 2 || g.V > 18) return 0;
+  if (g.Nc % 64 || g.Kc % 64 || a.ldy % 8 || g.lda % 8) return 0;
+  const int TV = g.T_out * g.V;
+  if (TV % 8 || g.M % TV) return 0;
+  const int nks = (TV + 31) / 32;
+  return nks == 4 || nks == 5 ? nks : 0;
+}
+
+static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
+  const int TV = a.g.T_out * a.g.V, clips = a.g.M / TV;
+  const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
+  const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
+  static const int target = getenv("F3_TAPS_WGS") ? atoi(getenv("F3_TAPS_WGS")) : 256;  // one per CU
+  int splits = std::max(1, std::min(clips, target / tiles));
+  splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
+  if (splits < 1) return F3_EINVAL;
+  const int cps = (clips + splits - 1) / splits;
+  splits = (clips + cps - 1) / cps;
+  a.rows_per_split = cps;  // clips per split
+  static const int priv = getenv("F3_TAPS_PRIVATE") ? atoi(getenv("F3_TAPS_PRIVATE")) : 0;  // debugging
+  if (priv) {
+    static float* ps = nullptr;
+    if (!ps && hipMalloc(&ps, sizeof(float) * 16 * 256 * 256 * 9) != hipSuccess) return F3_EHIP;
+    a.slab = ps;
+  }
+  const dim3 grid(tiles * splits);
+  static const int pad = getenv("F3_TAPS_PAD") ? atoi(getenv("F3_TAPS_PAD")) : 0;  // debugging: LDS footprint
+  if (nks == 5 && pad) hipLaunchKernelGGL((wgrad_taps<5, 30000>), grid, dim3(512), 0, s, a);
+  else if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
+  F3_LAUNCH_CHECK();
+  if (a.dw_ref) {
+    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(a.g.Kc / 64, a.g.Nc / 4), dim3(256), 0, s, a.slab, splits,
+                       a.g.Nc, a.g.Kc, a.dw_ref);
+    F3_LAUNCH_CHECK();
+  }
+  return F3_OK;
+}
+
 bool f3_wgrad_glds_ok(const WgradArgs& a) {
   return a.dyb && a.inb && a.zero && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && a.ldy % 8 == 0 && a.g.lda % 8 == 0;
 }
@@ -949,7 +1214,8 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   const long long per_split = (long long)a.g.Nc * a.g.KT * a.g.Kc;
   if (to_slab) {
     if (a.slab_cap < per_split) return F3_EINVAL;
-    splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
+    // (the slab grew for wgrad_taps; these tiles keep their measured split count)
+    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, 512LL * 128 * 128) / per_split);
   }
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + 63) / 64) * 64;
@@ -981,6 +1247,12 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
   if (a.groups > 1 && (a.g.transposed || a.slab)) return F3_EINVAL;  // grouped: wgrad_big + atomics only
   const int bigv = a.groups > 1 ? 1 : big;
+  // F3_WGRAD_TAPS=0: the per-tap wgrad_big tiles for the stride-1 clip-sized layers too
+  static const int taps_env = getenv("F3_WGRAD_TAPS") ? atoi(getenv("F3_WGRAD_TAPS")) : 1;
+  if (taps_env && bigv) {
+    const int nks = wgrad_taps_nks(a);
+    if (nks) return launch_wgrad_taps(a, nks, s);
+  }
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once

@@ -241,10 +241,12 @@ struct Arena {
   }
 };
 
-// slab capacity: one round of resident 128x128 weight-gradient tiles (2 per CU x 256 CUs); the
-// launcher caps the split count to it
+// slab capacity: one round of resident 128x128 weight-gradient tiles (2 per CU x 256 CUs), or 16
+// splits of the 256 x 256 x 9 tcn weight (wgrad_taps: 16 tiles x 16 splits = one workgroup per
+// CU); the launchers cap the split count to it
 long long wgrad_slab_floats() {  // F3_SLAB_X: capacity multiplier (A/B of split count vs slab traffic)
-  static const long long v = 512LL * 128 * 128 * (getenv("F3_SLAB_X") ? std::max(1, atoi(getenv("F3_SLAB_X"))) : 1);
+  static const long long v = std::max(512LL * 128 * 128, 16LL * 256 * 256 * 9) *
+                             (getenv("F3_SLAB_X") ? std::max(1, atoi(getenv("F3_SLAB_X"))) : 1);
   return v;
 }
 #define kWgradSlabFloats wgrad_slab_floats()
@@ -1445,6 +1447,7 @@ void* f3_net_debug_tensor(f3_net* net, int batch, void* workspace, int stream, i
   if (k == "out") return X.out;
   if (k == "att") return X.att;
   if (k == "dh") return X.dh;
+  if (k == "u") return X.u;
   if (k == "dv") return W.dv;
   if (k == "dg") return X.dg;
   if (k == "dZ") return W.dZ;

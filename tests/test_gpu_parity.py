@@ -95,7 +95,9 @@ def test_conv_kernel_matches_torch(precision):
 CONV_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
                (4, 29, 14, 128, 128, 9, 2, 4), (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4),
                (2, 30, 14, 9, 64, 1, 1, 0), (2, 30, 18, 64, 192, 1, 1, 0), (3, 30, 18, 192, 64, 1, 1, 0),
-               (2, 15, 14, 256, 128, 9, 1, 4), (2, 15, 18, 128, 128, 9, 1, 4)]
+               (2, 15, 14, 256, 128, 9, 1, 4), (2, 15, 18, 128, 128, 9, 1, 4),
+               # the tap-reuse weight gradient (wgrad_taps): T*V = 144 (5 k steps, 16 splits) and 112 (4)
+               (40, 8, 18, 256, 256, 9, 1, 4), (5, 8, 14, 128, 64, 9, 1, 4)]
 
 
 @pytest.mark.parametrize("precision", PRECISIONS, ids=PREC_IDS)
