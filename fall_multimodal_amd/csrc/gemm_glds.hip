@@ -936,14 +936,13 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
 // Needs: bf16 operands, forward geometry with S = 1, KT = 9, P = 4, T_in = T_out, V even,
 // T*V % 8 == 0, roundup(T*V, 32) == 32*NKS, Nc % 64 == 0, Kc % 64 == 0.
 // ----------------------------------------------------------------------------
-template <int NKS, int PAD = 0>
+template <int NKS>
 __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   constexpr int R = 128;                    // row bytes of both tiles (64 bf16)
   constexpr int TVP = 32 * NKS;             // padded clip rows
   constexpr int VMAX = 18;
   constexpr int Y_BYTES = TVP * R, X_BYTES = (TVP + 8 * VMAX) * R, STAGE = Y_BYTES + X_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 64 * 4 + PAD];
-  if (PAD && blockIdx.x == (1u << 30)) smem[2 * STAGE + 256 + PAD - 1] = 1;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 64 * 4];
   float* dbs = reinterpret_cast<float*>(smem + 2 * STAGE);  // [64]
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1033,7 +1032,7 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   }
   for (int t = 0; t < nst; ++t) {
     const int buf = t & 1;
-    if (t + 1 < nst) stage(n_begin + t + 1, buf ^ 1);
+    if (t + 1 < nst && a.dbg != 2) stage(n_begin + t + 1, buf ^ 1);
     const unsigned base = lds0 + buf * STAGE;
     // k step ks + 1's 26 fragment reads are issued before k step ks's MFMAs (two register sets);
     // the loop is branch-free between every read and its wait, so no read destination can be
@@ -1068,12 +1067,14 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
           for (int e = 0; e < 8; ++e) dbp[x] += (float)fa_[x][e];
       }
       if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
+      if (a.dbg != 1) {
 #pragma unroll
-      for (int tt = 0; tt < 5; ++tt) {
-        const bf16x8 fb =
-            __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
+        for (int tt = 0; tt < 5; ++tt) {
+          const bf16x8 fb =
+              __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fb, acc[tt][x]);
+          for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fb, acc[tt][x]);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1164,16 +1165,10 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const int cps = (clips + splits - 1) / splits;
   splits = (clips + cps - 1) / cps;
   a.rows_per_split = cps;  // clips per split
-  static const int priv = getenv("F3_TAPS_PRIVATE") ? atoi(getenv("F3_TAPS_PRIVATE")) : 0;  // debugging
-  if (priv) {
-    static float* ps = nullptr;
-    if (!ps && hipMalloc(&ps, sizeof(float) * 16 * 256 * 256 * 9) != hipSuccess) return F3_EHIP;
-    a.slab = ps;
-  }
+  static const int dbg = getenv("F3_TAPS_DBG") ? atoi(getenv("F3_TAPS_DBG")) : 0;
+  a.dbg = dbg;
   const dim3 grid(tiles * splits);
-  static const int pad = getenv("F3_TAPS_PAD") ? atoi(getenv("F3_TAPS_PAD")) : 0;  // debugging: LDS footprint
-  if (nks == 5 && pad) hipLaunchKernelGGL((wgrad_taps<5, 30000>), grid, dim3(512), 0, s, a);
-  else if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
+  if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
   F3_LAUNCH_CHECK();
   if (a.dw_ref) {

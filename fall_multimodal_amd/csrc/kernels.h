@@ -75,6 +75,7 @@ struct WgradArgs {
   // dw + q*gs_dw, db + q*gs_db. groups <= 1: one problem. Atomics path only (slab == null).
   int groups;
   long long gs_dy, gs_in, gs_dw, gs_db;
+  int dbg;                    // measurement knob of wgrad_taps (F3_TAPS_DBG): 1 no MFMA, 2 no restaging
 };
 
 // Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).
