@@ -10,6 +10,7 @@
 #include "layers.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace f3 {
 
@@ -345,6 +346,106 @@ __global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {  // regis
         *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8) = u0;
         *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8 + 4) = u1;
       }
+    }
+  }
+}
+
+// Wave-per-frame graph mix forward: each wave owns whole frames (no workgroup barrier, so the 3
+// barriers per frame of mix_fwd_lds_kernel are gone), keeps its frame's [V][Cin] input in a
+// wave-private LDS slab (bf16 when x is bf16), prefetches the next frame's input into registers
+// during the MFMAs, and writes Z one 16-channel tile at a time through a [64][20] fp32 LDS tile
+// as 16-B row pieces (L2 merges a wave's consecutive tiles into whole lines).
+template <int CIN> struct MixWaveCap {
+  static constexpr int PX = (18 * CIN / 4 + 63) / 64;  // 8-B (bf16) or 16-B (fp32) input pieces per lane
+};
+
+template <int KS, int CIN, bool XB>
+__global__ __launch_bounds__(256) void mix_fwd_wave_kernel(MixArgs a) {
+  using T = typename std::conditional<XB, unsigned short, float>::type;
+  constexpr int PX = MixWaveCap<CIN>::PX;
+  constexpr int S = CIN + (XB ? 8 : 4);    // LDS row stride (elements)
+  constexpr int ZS = 20;                    // zt row stride (floats)
+  constexpr int XW = 18 * S * (int)sizeof(T), ZW = 64 * ZS * 4;  // bytes per wave
+  extern __shared__ __attribute__((aligned(16))) char smw[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T* xs = reinterpret_cast<T*>(smw + wave * (XW + ZW));
+  float* zt = reinterpret_cast<float*>(smw + wave * (XW + ZW) + XW);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  float af[4][KS];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg);
+  const int n4 = V * CIN / 4, C4 = CIN / 4;
+  u32x2 rb[XB ? PX : 1];
+  f32x4 rf[XB ? 1 : PX];
+  auto prefetch = [&](int f) {  // unconditional loads from clamped indices
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = min(lane + q * 64, n4 - 1);
+      if constexpr (XB) rb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * CIN)[i];
+      else rf[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * CIN)[i];
+    }
+  };
+  const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+  if (gw < a.frames) prefetch(gw);
+  for (int f = gw; f < a.frames; f += nw) {
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = lane + q * 64;
+      if (i < n4) {
+        const int v = i / C4, c = (i - v * C4) * 4;
+        if constexpr (XB) *reinterpret_cast<u32x2*>(xs + v * S + c) = rb[q];
+        else *reinterpret_cast<f32x4*>(xs + v * S + c) = rf[q];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (f + nw < a.frames) prefetch(f + nw);
+    const size_t zoff = (size_t)f * KV * CIN;
+#pragma unroll 1
+    for (int t = 0; t < CIN / 16; ++t) {
+      const int ci0 = t * 16;
+      float b[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int v = 4 * ks + fg;
+        const T raw = xs[min(v, V - 1) * S + ci0 + fr];
+        float xv;
+        if constexpr (XB) xv = __uint_as_float((unsigned)raw << 16);
+        else xv = raw;
+        b[ks] = v < V ? xv : 0.f;
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b[ks], acc[mt]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zt[(16 * mt + 4 * fg + r) * ZS + fr] = acc[mt][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (a.zb) {  // 16-B pieces: (row wk, half h) -> 8 bf16
+        for (int p = lane; p < 2 * KV; p += 64) {
+          const int wk = p >> 1, h = p & 1;
+          const f32x4 u0 = *reinterpret_cast<const f32x4*>(zt + wk * ZS + 8 * h);
+          const f32x4 u1 = *reinterpret_cast<const f32x4*>(zt + wk * ZS + 8 * h + 4);
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o[e] = (__bf16)u0[e]; o[4 + e] = (__bf16)u1[e]; }
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.zb) + zoff + (size_t)wk * CIN + ci0 + 8 * h) = o;
+        }
+      } else {  // fp32 z: (row wk, quarter h) -> 4 floats
+        for (int p = lane; p < 4 * KV; p += 64) {
+          const int wk = p >> 2, h = p & 3;
+          *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)wk * CIN + ci0 + 4 * h) =
+              *reinterpret_cast<const f32x4*>(zt + wk * ZS + 4 * h);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zt is rewritten by the next tile
     }
   }
 }
@@ -1208,8 +1309,19 @@ static size_t mix_lds_bwd2(const MixArgs& a) {
 
 template <int KS, int CIN, bool XB>
 static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN, XB>), true);
+  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN, XB>),
+                      allow_big_lds((const void*)mix_fwd_wave_kernel<KS, CIN, XB>), true);
   (void)once;
+  // F3_MIX_WAVE=0: the workgroup-per-frame kernel
+  static const int wave_env = getenv("F3_MIX_WAVE") ? atoi(getenv("F3_MIX_WAVE")) : 1;
+  if (wave_env) {
+    const size_t per_wave = 18 * (CIN + (XB ? 8 : 4)) * (XB ? 2 : 4) + 64 * 20 * 4;
+    static const int wcap = getenv("F3_MIX_WGRID") ? atoi(getenv("F3_MIX_WGRID")) : 1024;
+    const int grid = std::max(1, std::min((a->frames + 3) / 4, wcap));
+    hipLaunchKernelGGL((mix_fwd_wave_kernel<KS, CIN, XB>), dim3(grid), dim3(256), 4 * per_wave, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   // resident workgroups loop over frames; measured (serial step, 256-1024-4096 swept with
   // F3_MIX_GRID): 1024 best for 64/128 channels, 512 for 256 (30.4 vs 32.7 us)
   static const int env = getenv("F3_MIX_GRID") ? atoi(getenv("F3_MIX_GRID")) : 0;
