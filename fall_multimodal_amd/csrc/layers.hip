@@ -372,11 +372,19 @@ __global__ __launch_bounds__(256) void mix_fwd_wave_kernel(MixArgs a) {
   float* zt = reinterpret_cast<float*>(smw + wave * (XW + ZW) + XW);
   const int fr = lane & 15, fg = lane >> 4;
   const int K = a.K, V = a.V, KV = K * V;
+  // A_eff once per workgroup through LDS (coalesced), then each lane's 4*KS fragment values:
+  // gathering them straight from global memory cost every wave 20 scattered loads
+  {
+    float* As = reinterpret_cast<float*>(smw + 4 * (XW + ZW));
+    for (int i = threadIdx.x; i < K * V * V; i += 256) As[i] = a.A[i];
+    __syncthreads();
+  }
+  const float* As = reinterpret_cast<const float*>(smw + 4 * (XW + ZW));
   float af[4][KS];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg);
+    for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(As, K, V, 16 * mt + fr, 4 * ks + fg);
   const int n4 = V * CIN / 4, C4 = CIN / 4;
   u32x2 rb[XB ? PX : 1];
   f32x4 rf[XB ? 1 : PX];
@@ -1318,7 +1326,8 @@ static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
     const size_t per_wave = 18 * (CIN + (XB ? 8 : 4)) * (XB ? 2 : 4) + 64 * 20 * 4;
     static const int wcap = getenv("F3_MIX_WGRID") ? atoi(getenv("F3_MIX_WGRID")) : 1024;
     const int grid = std::max(1, std::min((a->frames + 3) / 4, wcap));
-    hipLaunchKernelGGL((mix_fwd_wave_kernel<KS, CIN, XB>), dim3(grid), dim3(256), 4 * per_wave, s, *a);
+    const size_t lds = 4 * per_wave + sizeof(float) * a->K * a->V * a->V;
+    hipLaunchKernelGGL((mix_fwd_wave_kernel<KS, CIN, XB>), dim3(grid), dim3(256), lds, s, *a);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }

@@ -106,23 +106,39 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
   for (int u = 0; u < H; ++u) gwh[u] = 0.f;
 #pragma unroll
   for (int s = 0; s < 32; ++s) gwi[s] = 0.f;
+  // the saved gates / cell / h of (clip cb, unit cu) at the time a processing step handles,
+  // loaded one step ahead (unconditional loads from a clamped clip index: the recurrence chain
+  // then never waits on global memory)
+  struct StepVals { float gi, gf, gg, go, ct, cp, hprev; };
+  const int cbc = min(n0 + cb, a.N - 1);
+  auto load_step = [&](int step) {
+    StepVals r;
+    const int t = dir ? T - 1 - step : step, tp = dir ? t + 1 : t - 1;
+    const int tpc = min(max(tp, 0), T - 1);
+    const size_t nt = (size_t)cbc * T + t, ntp = (size_t)cbc * T + tpc;
+    const float* gsv = a.gates + ((size_t)dir * a.N * T + nt) * G4;
+    r.gi = gsv[cu]; r.gf = gsv[H + cu]; r.gg = gsv[2 * H + cu]; r.go = gsv[3 * H + cu];
+    r.ct = a.cell[((size_t)dir * a.N * T + nt) * H + cu];
+    r.cp = a.cell[((size_t)dir * a.N * T + ntp) * H + cu];
+    r.hprev = a.seq[ntp * 2 * H + dir * H + cu];
+    return r;
+  };
+  StepVals nxt = load_step(T - 1);
   __syncthreads();
   for (int step = T - 1; step >= 0; --step) {
     const int t = dir ? T - 1 - step : step;           // time of this processing step
-    const int tp = dir ? t + 1 : t - 1;                // time of the previous step's state
     const bool has_prev = step > 0;
+    const StepVals cur = nxt;
+    if (step > 0) nxt = load_step(step - 1);
     // (b, u): cell backward
     {
       float gi = 0, gf = 0, gg = 0, go = 0, ct = 0, cp = 0;
       if (valid) {
-        const size_t nt = (size_t)(n0 + cb) * T + t;
-        const float* gsv = a.gates + ((size_t)dir * a.N * T + nt) * G4;
-        gi = gsv[cu]; gf = gsv[H + cu]; gg = gsv[2 * H + cu]; go = gsv[3 * H + cu];
-        ct = a.cell[((size_t)dir * a.N * T + nt) * H + cu];
+        gi = cur.gi; gf = cur.gf; gg = cur.gg; go = cur.go;
+        ct = cur.ct;
         if (has_prev) {
-          const size_t ntp = (size_t)(n0 + cb) * T + tp;
-          cp = a.cell[((size_t)dir * a.N * T + ntp) * H + cu];
-          hp[cb * H + cu] = a.seq[ntp * 2 * H + dir * H + cu];
+          cp = cur.cp;
+          hp[cb * H + cu] = cur.hprev;
         } else {
           hp[cb * H + cu] = 0.f;
         }
@@ -247,6 +263,73 @@ __global__ __launch_bounds__(1024) void shead_fwd_kernel(SHeadArgs a) {
     const float* w = a.W3 + (size_t)k * HC;
     for (int c = 0; c < HC; ++c) q += w[c] * y[c] * at[c];
     a.out[(size_t)n * a.out_ld + k] = q;
+  }
+}
+
+// The same head as two launches: the BatchNorm1d batch statistics (one workgroup, 8 row slices
+// per channel, fp64) and one workgroup of 128 threads per clip for BN -> CA -> Linear (the single
+// workgroup above walked every [N x 128] stage alone: 127 us at N = 256).
+__global__ __launch_bounds__(1024) void shead_stats_kernel(SHeadArgs a) {
+  __shared__ double rs[8][HC], rq[8][HC];
+  const int c = threadIdx.x % HC, part = threadIdx.x / HC;
+  double sum = 0.0, sq = 0.0;
+  for (int n = part; n < a.N; n += 8) {
+    const double v = a.hmean[(size_t)n * HC + c];
+    sum += v;
+    sq += v * v;
+  }
+  rs[part][c] = sum;
+  rq[part][c] = sq;
+  __syncthreads();
+  if (part == 0) {
+    for (int p = 1; p < 8; ++p) {
+      sum += rs[p][c];
+      sq += rq[p][c];
+    }
+    a.bn_sum[c] = sum;
+    a.bn_sq[c] = sq;
+  }
+}
+
+__global__ __launch_bounds__(128) void shead_clip_kernel(SHeadArgs a) {
+  __shared__ float y[HC], h1[HR], yt[HC];
+  const int n = blockIdx.x, c = threadIdx.x;
+  float mean, rstd;
+  if (a.bn.eval) {
+    mean = a.bn.rmean[c];
+    rstd = rsqrtf(a.bn.rvar[c] + kBnEps);
+  } else {
+    const double m = a.bn_sum[c] / a.N;
+    double var = a.bn_sq[c] / a.N - m * m;
+    if (var < 0) var = 0;
+    mean = (float)m;
+    rstd = (float)(1.0 / sqrt(var + kBnEps));
+  }
+  const float sc = a.bn.gamma[c] * rstd, sh = a.bn.beta[c] - mean * sc;
+  const float yv = a.hmean[(size_t)n * HC + c] * sc + sh;
+  a.ybn[(size_t)n * HC + c] = yv;
+  y[c] = yv;
+  __syncthreads();
+  if (c < HR) {
+    float q = a.b1[c];
+    for (int k = 0; k < HC; ++k) q += a.W1[c * HC + k] * y[k];
+    q = fmaxf(q, 0.f);
+    h1[c] = q;
+    a.a1[(size_t)n * HR + c] = q;
+  }
+  __syncthreads();
+  float q = a.b2[c];
+#pragma unroll
+  for (int j = 0; j < HR; ++j) q += a.W2[c * HR + j] * h1[j];
+  const float at = sigmoidf_(q);
+  a.att[(size_t)n * HC + c] = at;
+  yt[c] = yv * at;
+  __syncthreads();
+  for (int k = c; k < a.Cs; k += HC) {
+    float o = a.b3[k];
+    const float* w = a.W3 + (size_t)k * HC;
+    for (int j = 0; j < HC; ++j) o += w[j] * yt[j];
+    a.out[(size_t)n * a.out_ld + k] = o;
   }
 }
 
@@ -583,7 +666,17 @@ int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
 }
 
 int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(shead_fwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+  static const bool one_wg = getenv("F3_SHEAD_1WG") != nullptr;  // the single-workgroup form (A/B)
+  if (one_wg) {
+    hipLaunchKernelGGL(shead_fwd_kernel, dim3(1), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
+  if (!a->bn.eval) {
+    hipLaunchKernelGGL(shead_stats_kernel, dim3(1), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(shead_clip_kernel, dim3(a->N), dim3(HC), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
