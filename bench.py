@@ -58,7 +58,7 @@ def parse():
     return p.parse_args()
 
 
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r01_roofline_pmc.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
 
 
 def _time_launch(fn, reps=20):
@@ -117,7 +117,7 @@ def roofline_kernels(dev, batch, V, precision):
                                                               1, 4, 1, st))
         taps = os.environ.get("F3_WGRAD_TAPS", "1") != "0" and V % 2 == 0
         kname = "wgrad_taps<5>" if taps else "wgrad_big<4,2,4,4,64>"
-        out["wgrad"] = {"kernel": f"{kname} + wgrad_slab_reduce (tcn 9x1 weight gradient incl. the "
+        out["wgrad"] = {"kernel": f"{kname} + slab reduce (tcn 9x1 weight gradient incl. the "
                                   f"split-K reduce, C=256, T=8, N={N}, V={V})", "ms": ms}
         # the step's slab (net.cpp wgrad_slab_floats)
         cap = max(512 * 128 * 128, 16 * 256 * 256 * 9) * max(1, int(os.environ.get("F3_SLAB_X", "1")))
@@ -413,6 +413,43 @@ def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     return rec
 
 
+def loader_bench(model, dev, B=256, V=18, S=6, C=11, n=20480):
+    """The data step in front of the hot path: data.WindowLoader over synthetic
+    windows in the reference's format (n windows, shuffled, drop_last), timed alone (gather into
+    pinned buffers + async H2D on a copy stream) and feeding the training step, per epoch."""
+    import fall_multimodal_amd as f3
+    from fall_multimodal_amd.data import Windows, WindowLoader
+    rng = np.random.default_rng(3)
+    w = Windows([f"v{i // 40}" for i in range(n)], rng.standard_normal((n, 30, V, 3), dtype=np.float32),
+                rng.standard_normal((n, 30, S), dtype=np.float32),
+                np.eye(C, dtype=np.float32)[rng.integers(0, C, n)])
+    loader = WindowLoader(w, B, shuffle=True, drop_last=True, device=dev, generator=torch.Generator().manual_seed(1))
+    for _ in loader:  # warm the pinned allocator
+        pass
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nb = 0
+    for sk, se, lb in loader:
+        nb += 1
+    torch.cuda.synchronize()
+    t_load = time.perf_counter() - t0
+    step = f3.TrainStep(model, B, lr=1e-3)
+    it = iter(loader)
+    step(*next(it))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ns = 0
+    for sk, se, lb in it:
+        step(sk, se, lb)
+        ns += 1
+    torch.cuda.synchronize()
+    t_fed = time.perf_counter() - t0
+    return {"windows": n, "batch": B, "loader_only_clips_per_s": round(nb * B / t_load, 1),
+            "train_fed_clips_per_s": round(ns * B / t_fed, 1),
+            "note": "one epoch of data.WindowLoader (shuffle, drop_last, pinned gather + async H2D) alone, "
+                    "then feeding TrainStep batch by batch"}
+
+
 def cpu_threads():
     """The CPU share this process may use: OMP_NUM_THREADS (16 on the GPU box, whose nproc shows
     the whole machine), else every core here."""
@@ -524,6 +561,7 @@ def main():
     murec = musa_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
+    ldr = loader_bench(model, dev, B, V, S, C) if (rank == 0 and world == 1 and not a.no_targcn) else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
         rec = {
@@ -553,6 +591,7 @@ def main():
                     B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12 / PEAK_MFMA_TFLOPS[a.precision], 4),
                 "note": "whole step (fwd+bwd conv/einsum/addmm FLOPs, SURVEY 8d) / ms_per_step / dense peak"},
             "sensor": sens,
+            "loader": ldr,
             "eval_forward": ev,
             "dp_phased_backward": phased,
             "main_py_autograd_path": agp,

@@ -19,8 +19,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-_WG = "wgrad_big<4, 2, 4, 4, 64>" if os.environ.get("F3_WGRAD_BIG", "1") != "0" else "wgrad_glds_bf16<128, 128>"
-KERNELS = {"wgrad": _WG, "tcn_fwd": "igemm_big<1, 1, 8>"}
+_TAPS = os.environ.get("F3_WGRAD_TAPS", "1") != "0"
+_WG = "wgrad_taps<5>" if _TAPS else "wgrad_big<4, 2, 4, 4, 64>"
+_RED = "wgrad_taps_reduce_kernel" if _TAPS else "wgrad_slab_reduce_kernel"
+# bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
+KERNELS = {"wgrad": [_WG, _RED], "wgrad_kernel": [_WG], "tcn_fwd": ["igemm_big<1, 1, 8>"]}
+_SHAPE = "C=256, T=8, N=256, V=18"
+_KN = _WG.replace(", ", ",")
+NAMES = {"wgrad": f"{_KN} + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, {_SHAPE})",
+         "wgrad_kernel": f"{_KN} alone (partials left in the slab, {_SHAPE})",
+         "tcn_fwd": f"igemm_big<1,1,8> bf16-out (tcn 9x1 fwd, {_SHAPE})"}
 
 
 def run():
@@ -38,19 +46,23 @@ def per_launch(db, counter, pattern):
 
 
 def summarize(d):
-    import torch  # noqa: F401  (bench imports torch)
-    import bench
-    names = {"wgrad": KERNELS["wgrad"].replace(", ", ",") + " (tcn 9x1 weight gradient, C=256, T=8, N=256, V=18)",
-             "tcn_fwd": "igemm_big<1,1,8> (tcn 9x1 fwd, C=256, T=8, N=256, V=18)"}
     out = {}
-    for key, pat in KERNELS.items():
-        f, nf = per_launch(os.path.join(d, "rpmc_FETCH_SIZE", "run_results.db"), "FETCH_SIZE", pat)
-        w, nw = per_launch(os.path.join(d, "rpmc_WRITE_SIZE", "run_results.db"), "WRITE_SIZE", pat)
-        if f is None or w is None:
-            continue
-        out[key] = {"kernel": names[key], "fetch_bytes": 2.0 * f, "write_bytes": w,
-                    "bytes_per_launch": round(2.0 * f + w), "launches": [nf, nw],
-                    "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, mean over launches"}
+    for key, pats in KERNELS.items():
+        fetch = write = 0.0
+        launches = []
+        for pat in pats:
+            f, nf = per_launch(os.path.join(d, "rpmc_FETCH_SIZE", "run_results.db"), "FETCH_SIZE", pat)
+            w, nw = per_launch(os.path.join(d, "rpmc_WRITE_SIZE", "run_results.db"), "WRITE_SIZE", pat)
+            if f is None or w is None:
+                break
+            fetch += 2.0 * f
+            write += w
+            launches.append([pat, nf, nw])
+        else:
+            out[key] = {"kernel": NAMES[key], "fetch_bytes": fetch, "write_bytes": write,
+                        "bytes_per_launch": round(fetch + write), "launches": launches,
+                        "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, mean over launches, "
+                                "summed over the kernels of one launch"}
     print(json.dumps(out, indent=1))
 
 
