@@ -83,14 +83,14 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
 __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int dir = blockIdx.y, n0 = blockIdx.x * LSTM_NB, S = a.S, T = a.T;
-  float* whs = sm;                        // [4H][H+1]
-  float* wis = whs + G4 * (H + 1);        // [4H][S]
+  float* whs = sm;                        // W_hh^T [H][4H + 4] (a unit's row of all gates: float4 reads)
+  float* wis = whs + G4 * (H + 1);        // [4H][S]   (H * (4H + 4) == 4H * (H + 1))
   float* xs = wis + G4 * S;               // [NB][T][S]
   float* hp = xs + LSTM_NB * T * S;       // [NB][H] h_{prev}
   float* dgs = hp + LSTM_NB * H;          // [NB][4H]
   float* dhr = dgs + LSTM_NB * G4;        // [NB][H] recurrent dh
   const int tid = threadIdx.x;
-  for (int i = tid; i < G4 * H; i += 256) whs[(i / H) * (H + 1) + (i % H)] = a.w_hh[dir][i];
+  for (int i = tid; i < G4 * H; i += 256) whs[(i % H) * (G4 + 4) + i / H] = a.w_hh[dir][i];
   for (int i = tid; i < G4 * S; i += 256) wis[i] = a.w_ih[dir][i];
   for (int i = tid; i < LSTM_NB * T * S; i += 256) {
     const int b = i / (T * S), r = i - b * T * S;
@@ -167,15 +167,22 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
 #pragma unroll
       for (int s = 0; s < 32; ++s)
         if (s < S) gwi[s] += d * xr[s];
-      const float* hr = hp + b * H;
+      const f32x4* hr = reinterpret_cast<const f32x4*>(hp + b * H);
 #pragma unroll
-      for (int u = 0; u < H; ++u) gwh[u] += d * hr[u];
+      for (int u4 = 0; u4 < H / 4; ++u4) {
+        const f32x4 h = hr[u4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gwh[4 * u4 + e] += d * h[e];
+      }
     }
-    // (b, u'): recurrent dh
+    // (b, u'): recurrent dh = sum_g dgates[g] W_hh[g][u'] (16-B reads of both rows)
     {
-      float acc = 0.f;
-      const float* dg = dgs + cb * G4;
-      for (int g = 0; g < G4; ++g) acc += dg[g] * whs[g * (H + 1) + cu];
+      const f32x4* dg = reinterpret_cast<const f32x4*>(dgs + cb * G4);
+      const f32x4* wr = reinterpret_cast<const f32x4*>(whs + cu * (G4 + 4));
+      f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int j = 0; j < G4 / 4; ++j) acc4 += dg[j] * wr[j];
+      const float acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
       __syncthreads();  // everyone finished reading dhr of this step (dh above)
       dhr[cb * H + cu] = acc;
     }
