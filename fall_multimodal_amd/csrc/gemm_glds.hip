@@ -942,8 +942,7 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   constexpr int TVP = 32 * NKS;             // padded clip rows
   constexpr int VMAX = 18;
   constexpr int Y_BYTES = TVP * R, X_BYTES = (TVP + 8 * VMAX) * R, STAGE = Y_BYTES + X_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 64 * 4];
-  float* dbs = reinterpret_cast<float*>(smem + 2 * STAGE);  // [64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int V = g.V, TV = g.T_out * g.V;
@@ -956,11 +955,6 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
   const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
   const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
-
-  // zero both stages once: the halo / padding rows are never staged into
-  for (int o = tid * 16; o < 2 * STAGE; o += 512 * 16) *reinterpret_cast<f32x4*>(smem + o) = f32x4{0.f, 0.f, 0.f, 0.f};
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
 
   // ---- staging: 1-KiB pieces (8 rows), dY pieces then input pieces; a lane's slots are fixed ----
   const int npy = TV / 8, np = 2 * npy, ppw = (np + 7) / 8;
@@ -1021,15 +1015,29 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   for (int tt = 0; tt < 5; ++tt)
 #pragma unroll
     for (int x = 0; x < 4; ++x) acc[tt][x] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_db = a.db && i0 == 0 && wi == 0 && kh == 0;
-  float dbp[4] = {0.f, 0.f, 0.f, 0.f};
+  // The second tap half has a free 5th MFMA column: with an all-ones B fragment it sums dY over
+  // the rows, i.e. the bias gradient, at no extra issue (the first version summed the fragments
+  // on the VALU in one wave, which held its workgroup's SIMD ~60 % longer per k step).
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const unsigned ones_m = kh ? 0xffffffffu : 0u;
+  const u32x4_t ones_v = {0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m};
+  const u32x4_t keep_v = {~ones_m, ~ones_m, ~ones_m, ~ones_m};
 
   const int nst = n_end - n_begin;
-  if (nst > 0) {
-    stage(n_begin, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  if (nst > 0) stage(n_begin, 0);
+  // zero the rows no stage ever writes (dY padding past T*V, the input halo and tail), in both
+  // buffers, while the first clip's DMA is in flight (disjoint bytes)
+  {
+    const int zr[3][2] = {{TV * R, Y_BYTES}, {Y_BYTES, Y_BYTES + 4 * V * R}, {Y_BYTES + (4 * V + TV) * R, STAGE}};
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int z = 0; z < 3; ++z)
+        for (int o = zr[z][0] + tid * 16; o < zr[z][1]; o += 512 * 16)
+          *reinterpret_cast<f32x4*>(smem + b * STAGE + o) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int t = 0; t < nst; ++t) {
     const int buf = t & 1;
     if (t + 1 < nst && a.dbg != 2) stage(n_begin + t + 1, buf ^ 1);
@@ -1060,86 +1068,75 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
 #pragma unroll
       for (int x = 0; x < 4; ++x)
         fa_[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][x], hi[c][x], 0, 1, 2, 3, 4, 5, 6, 7));
-      if (do_db) {  // before the next reads are issued: no branch while they are in flight
+      bf16x8 fbs[5];
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dbp[x] += (float)fa_[x][e];
-      }
+      for (int tt = 0; tt < 5; ++tt)
+        fbs[tt] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
+      // second half: the 5th column is the ones fragment (bit select, no branch)
+      fbs[4] = __builtin_bit_cast(bf16x8, (__builtin_bit_cast(u32x4_t, fbs[4]) & keep_v) | ones_v);
       if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
       if (a.dbg != 1) {
 #pragma unroll
-        for (int tt = 0; tt < 5; ++tt) {
-          const bf16x8 fb =
-              __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
+        for (int tt = 0; tt < 5; ++tt)
 #pragma unroll
-          for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fb, acc[tt][x]);
-        }
+          for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fbs[tt], acc[tt][x]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (a.db && i0 == 0) {
-    if (do_db) {
+  // bias gradient: the ones column of wave (kh 1, wi 0) in the i0 == 0 tiles; lane (fg, fr = 0)
+  // holds co = x*16 + fg*4 + r (all 16 columns carry the same sum)
+  if (a.db && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        dbp[x] += __shfl_xor(dbp[x], 16, 64);
-        dbp[x] += __shfl_xor(dbp[x], 32, 64);
-      }
-      if (fg == 0)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int x = 0; x < 4; ++x) dbs[x * 16 + fr] = dbp[x];
-    }
-    __syncthreads();
-    if (tid < 64 && nst > 0) atomic_add_f(a.db + j0 + tid, dbs[tid]);
+      for (int r = 0; r < 4; ++r) atomic_add_f(a.db + j0 + x * 16 + fg * 4 + r, acc[4][x][r]);
   }
-  float* slab = a.slab + (size_t)bz * g.Nc * 9 * g.Kc;
+  // partials in fragment order, slab[split][tile][wi][dt][x][lane] as 16-B pieces: each store is
+  // one contiguous KiB per wave (the reference-layout scatter took 80 4-B stores per lane at
+  // the kernel's end, when every CU stores at once); wgrad_taps_reduce_kernel reorders
+  f32x4* slab = reinterpret_cast<f32x4*>(a.slab) + ((size_t)(bz * tiles + tile) * 4 + wi) * 9 * 4 * 64 + lane;
 #pragma unroll
   for (int tt = 0; tt < 5; ++tt) {
     if (tt < ntap) {
-      const int dt = dt0 + tt;
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = j0 + x * 16 + fg * 4 + r, i = i0 + wi * 16 + fr;
-          slab[(size_t)j * 9 * g.Kc + (size_t)dt * g.Kc + i] = acc[tt][x][r];
-        }
+      for (int x = 0; x < 4; ++x) slab[((dt0 + tt) * 4 + x) * 64] = acc[tt][x];
     }
   }
 }
 
-// dw_ref[j][i][dt] += sum_s slab[s][j][dt*Kc + i] for wgrad_taps' 9-tap slab. Thread (j, i) keeps
-// the 9 tap sums, walks the splits four at a time (36 independent loads, each wave reading 256
-// contiguous bytes per tap), and writes its 9 consecutive outputs (a wave writes 64 * 36 contiguous
-// bytes). Workgroup = 4 output rows j x 64 columns i.
-__global__ __launch_bounds__(256) void wgrad_taps_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
+// dw_ref[j][i][dt] += sum_s (wgrad_taps' fragment-order slab). Workgroup = one (tile, wi, x)
+// block: 16 co x 16 ci x 9 taps. Wave dt, lane L sums the 16-B piece [dt][x][L] over the splits
+// (each load a contiguous KiB per wave, 8 in flight), drops its 4 values into an LDS image
+// [16 co][16 ci][9] that is exactly the reference layout of those 16 output rows (144
+// contiguous floats each), and the workgroup adds it into dw_ref as 16-B pieces.
+__global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
                                                                  int Kc, float* __restrict__ dw_ref) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63), j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const size_t per = (size_t)Nc * 9 * Kc;
-  const float* p = slab + (size_t)j * 9 * Kc + i;
-  float acc[9];
-#pragma unroll
-  for (int d = 0; d < 9; ++d) acc[d] = 0.f;
+  __shared__ __attribute__((aligned(16))) float img[16 * 16 * 9];
+  const int tiles = (Nc / 64) * (Kc / 64), jt = Nc / 64;
+  const int b = blockIdx.x, tile = b >> 4, wi = (b >> 2) & 3, x = b & 3;
+  const int j0 = (tile % jt) * 64 + x * 16, i0 = (tile / jt) * 64 + wi * 16;
+  const int tid = threadIdx.x, dt = tid >> 6, lane = tid & 63, fr = lane & 15, fg = lane >> 4;
+  const f32x4* p = reinterpret_cast<const f32x4*>(slab) + (((size_t)tile * 4 + wi) * 9 + dt) * 4 * 64 + x * 64 + lane;
+  const size_t per = (size_t)tiles * 4 * 9 * 4 * 64;  // f32x4 per split
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   int sp = 0;
-  for (; sp + 4 <= splits; sp += 4) {
-    float v[4][9];
+  for (; sp + 8 <= splits; sp += 8) {
+    f32x4 v[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 8; ++q) v[q] = p[(size_t)(sp + q) * per];
 #pragma unroll
-      for (int d = 0; d < 9; ++d) v[q][d] = p[(size_t)(sp + q) * per + (size_t)d * Kc];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int d = 0; d < 9; ++d) acc[d] += v[q][d];
+    for (int q = 0; q < 8; ++q) s += v[q];
   }
-  for (; sp < splits; ++sp)
+  for (; sp < splits; ++sp) s += p[(size_t)sp * per];
 #pragma unroll
-    for (int d = 0; d < 9; ++d) acc[d] += p[(size_t)sp * per + (size_t)d * Kc];
-  float* o = dw_ref + ((size_t)j * Kc + i) * 9;
-#pragma unroll
-  for (int d = 0; d < 9; ++d) o[d] += acc[d];
+  for (int r = 0; r < 4; ++r) img[((fg * 4 + r) * 16 + fr) * 9 + dt] = s[r];
+  __syncthreads();
+  // 16 rows x 36 float4 = 576 pieces, one per thread
+  const int row = tid / 36, c4 = tid - row * 36;
+  f32x4* o = reinterpret_cast<f32x4*>(dw_ref + ((size_t)(j0 + row) * Kc + i0) * 9) + c4;
+  *o += *reinterpret_cast<const f32x4*>(img + row * 144 + c4 * 4);
 }
 
 // wgrad_taps applies (see its comment); nks = padded clip rows / 32
@@ -1172,8 +1169,8 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
   F3_LAUNCH_CHECK();
   if (a.dw_ref) {
-    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(a.g.Kc / 64, a.g.Nc / 4), dim3(256), 0, s, a.slab, splits,
-                       a.g.Nc, a.g.Kc, a.dw_ref);
+    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
+                       a.dw_ref);
     F3_LAUNCH_CHECK();
   }
   return F3_OK;
