@@ -233,7 +233,7 @@ def eval_throughput(model, sk, se, reps=20):
 def autograd_path_bench(model, sk, se, lb, steps=5):
     """The reference driver's loop body unchanged (model/main.py:112-127): out = model(data, sensor)
     through the fall3::net_forward custom op, CrossEntropyLoss, loss.backward() (fall3::net_backward),
-    optimizer.step() with fall3 RMSprop per parameter tensor (fall3::rmsprop_), zero_grad."""
+    optimizer.step() with fall3 RMSprop (one fall3::rmsprop_ over the flat parameter range), zero_grad."""
     import fall_multimodal_amd as f3
     opt = f3.RMSprop(model.parameters(), lr=1e-3)
     loss_fn = torch.nn.CrossEntropyLoss()

@@ -14,17 +14,75 @@ from . import ops  # noqa: F401  (registers fall3::rmsprop_)
 from ._lib import require_device
 
 
+def _flat_view(t, start, n):
+    """1-D view of n elements of t's storage from element `start`."""
+    return torch.empty(0, dtype=t.dtype, device=t.device).set_(t.untyped_storage(), start, (n,))
+
+
 class RMSprop(torch.optim.Optimizer):
     """torch.optim.RMSprop(lr, alpha=0.99, eps=1e-8) — no momentum, not centred, no
-    weight decay — as one fall3::rmsprop_ custom op (f3_rmsprop_step) per parameter tensor."""
+    weight decay — as fall3::rmsprop_ custom ops (f3_rmsprop_step).
+
+    Flat path: the fall3 modules keep their parameters as views of ONE flat buffer and
+    loss.backward() hands back their gradients as views of ONE flat gradient buffer in the
+    same layout (ops.py `_split_grads`). When a group's parameters, gradients and square_avg
+    states are laid out that way, step() is one launch over the whole range (the 16-B
+    alignment pads between tensors carry zero gradients, so they stay unchanged), and the
+    group shares one `step` counter tensor. Anything else (a user-built group, states loaded
+    from a state_dict, gradients that autograd copied) takes the per-tensor path."""
 
     def __init__(self, params, lr=1e-2, alpha=0.99, eps=1e-8):
         super().__init__(params, dict(lr=lr, alpha=alpha, eps=eps))
+
+    def _flat(self, group):
+        """(params, square_avg, grads) flat views covering the group, or None."""
+        ps = group["params"]
+        if not ps or any(p.grad is None for p in ps):
+            return None
+        ps = sorted(ps, key=lambda t: t.storage_offset())  # module order is not the flat order
+        p0, g0 = ps[0], ps[0].grad
+        if p0.dtype != torch.float32 or g0.dtype != torch.float32:
+            return None
+        pst, gst = p0.untyped_storage().data_ptr(), g0.untyped_storage().data_ptr()
+        pbase, gbase = p0.storage_offset(), g0.storage_offset()
+        st0 = self.state[p0]
+        sq0 = st0.get("square_avg")
+        sst = sq0.untyped_storage().data_ptr() if sq0 is not None else None
+        sbase = sq0.storage_offset() if sq0 is not None else 0
+        end = pbase
+        for p in ps:
+            g = p.grad
+            if (p.untyped_storage().data_ptr() != pst or g.untyped_storage().data_ptr() != gst
+                    or not p.is_contiguous() or not g.is_contiguous() or g.shape != p.shape
+                    or p.storage_offset() < end or g.storage_offset() - gbase != p.storage_offset() - pbase):
+                return None
+            s = self.state[p].get("square_avg")
+            if (s is None) != (sq0 is None) or (s is not None and (
+                    s.untyped_storage().data_ptr() != sst or s.storage_offset() - sbase != p.storage_offset() - pbase)):
+                return None
+            end = p.storage_offset() + p.numel()
+        n = end - pbase
+        if sq0 is None:  # first step: one flat square_avg, per-tensor views as the states
+            flat_sq = torch.zeros(n, dtype=torch.float32, device=p0.device)
+            step = torch.zeros((), dtype=torch.float32)
+            for p in ps:
+                o = p.storage_offset() - pbase
+                self.state[p]["square_avg"] = flat_sq[o:o + p.numel()].view_as(p)
+                self.state[p]["step"] = step
+        else:
+            flat_sq = _flat_view(sq0, sbase, n)
+        return _flat_view(p0, pbase, n), flat_sq, _flat_view(g0, gbase, n)
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         for group in self.param_groups:
+            flat = self._flat(group)
+            if flat is not None:
+                require_device(flat[0], "parameter")
+                self.state[group["params"][0]]["step"] += 1  # one counter shared by the group
+                torch.ops.fall3.rmsprop_(flat[0], flat[1], flat[2], group["lr"], group["alpha"], group["eps"], 1.0)
+                continue
             for p in group["params"]:
                 if p.grad is None:
                     continue
