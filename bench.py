@@ -166,12 +166,27 @@ def mix_roofline(dev, batch, V, precision):
     nx = frames * V * Cin
     bytes_f = nx * es + nx * K * es + K * V * V * 4
     bytes_b = nx * es + nx * K * es + nx * 4 + 2 * K * V * V * 4
+    bwd_kern = ("mix_bwd_bf16 (bf16 MFMA) + colsum" if bf and os.environ.get("F3_MIX_BWD_BF16", "1") != "0"
+                else "mix_bwd_lds (fp32 MFMA) + colsum")
     res = {}
-    for key, byt, ms, kern in (("fwd", bytes_f, ms_f, "mix_fwd_lds"), ("bwd", bytes_b, ms_b, "mix_bwd_lds + colsum")):
+    for key, byt, ms, kern in (("fwd", bytes_f, ms_f, "mix_fwd_wave"), ("bwd", bytes_b, ms_b, bwd_kern)):
         gbs = byt / (ms * 1e-3) / 1e9
         res[key] = {"kernel": f"{kern} (K=3, V={V}, Cin=64, frames={frames}, {precision})", "bound": "hbm",
                     "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": byt, "ms_per_launch": round(ms, 4)}
+    # the backward at the other two layer shapes of the step (128 ch at T=15, 256 ch at T=8)
+    res["bwd_other_shapes"] = {}
+    for cin, t in ((128, 15), (256, 8)):
+        fr = batch * t
+        x2 = torch.randn(fr, V, cin, device=dev).to(et)
+        z2 = torch.randn(fr, V, K, cin, device=dev).to(et)
+        dx2 = torch.empty(fr, V, cin, device=dev)
+        ms2 = _time_launch(lambda: lib.f3_graph_mix_backward_ex(L.ptr(A), L.ptr(x2), L.ptr(z2), L.ptr(dx2), L.ptr(dA),
+                                                                fr, K, V, cin, 1 if bf else 0, st))
+        n2 = fr * V * cin
+        b2 = n2 * es + n2 * K * es + n2 * 4 + 2 * K * V * V * 4
+        res["bwd_other_shapes"][f"Cin{cin}_T{t}"] = {"ms_per_launch": round(ms2, 4), "bytes_per_launch": b2,
+                                                     "frac": round(b2 / (ms2 * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
     return res
 
 

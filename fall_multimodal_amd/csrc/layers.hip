@@ -607,6 +607,144 @@ __global__ __launch_bounds__(256) void mix_bwd_lds_kernel(MixArgs a) {  // ACC: 
   for (int i = tid; i < KVV; i += 256) row[i] = red[i];
 }
 
+// ----------------------------------------------------------------------------
+// Graph-mix backward of the bf16 mode on bf16 MFMA (16x16x32). x and dZ are stored bf16, so
+// dA = sum_{f,c} X_f[v][c] dZ_f[wk][c] takes them as MFMA operands with exact products and fp32
+// accumulation (what the fp32 16x16x4 kernel computed, at 8x the MFMA rate); for
+// dX = A~ . dZ the fp32 A~ is split into bf16 hi + lo (hi = its top 16 bits, lo = the rest
+// rounded: |A~ - hi - lo| <= 2^-17 |A~|), two MFMAs per product. The fp32 16x16x4 kernel was
+// bound by its MFMA work (~4 GFLOP padded per layer = ~25 us at the fp32 MFMA rate) and ran
+// 53-107 us. One frame per loop trip: the frame's x [V][C] and dZ [KV][C] rows (bf16, prefetched
+// into registers one frame ahead) land in LDS rows of 2C + 16 bytes (conflict-free 16-B row
+// reads); dX's dZ fragments are transposed LDS reads (ds_read_b64_tr_b16), dA's fragments plain
+// 16-B reads. dZ rows KV..63 are zero (they meet A~'s zero columns; garbage there could be NaN).
+// Wave w: dX tiles nt = w, w + 4, ..; dA column tile wk 16w..16w+15 (all K*V <= 64) for both
+// v tiles, accumulated over the workgroup's frames into one partial row (f3_colsum after).
+// ----------------------------------------------------------------------------
+typedef short mx_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const char mx_lds_t;
+F3_DEV f32x4 mfma_bf16x(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
+F3_DEV void a_split(float t, __bf16& hi, __bf16& lo) {
+  const float h = __uint_as_float(__float_as_uint(t) & 0xffff0000u);
+  hi = __builtin_bit_cast(__bf16, (unsigned short)(__float_as_uint(h) >> 16));
+  lo = (__bf16)(t - h);
+}
+
+template <int CIN, bool ACC>
+__global__ __launch_bounds__(256) void mix_bwd_bf16_kernel(MixArgs a) {
+  constexpr int RB = 2 * CIN + 16, XR = 32, ZR = 64, C8 = CIN / 8;
+  constexpr int PX = (18 * C8 + 255) / 256, PZ = (54 * C8 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smb[];
+  char* xs = smb;            // [32][RB]
+  char* zs = smb + XR * RB;  // [64][RB]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  const int nx = V * C8, nz = KV * C8;
+  // A~ as the dX A operand: lane holds rows v = 16 mt + fr, k = wk = 32 ks + 8 fg + e
+  bf16x8 ahi[2][2], alo[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 h, l;
+        a_split(atil(a.A, K, V, 32 * ks + 8 * fg + e, 16 * mt + fr), h, l);
+        ahi[mt][ks][e] = h;
+        alo[mt][ks][e] = l;
+      }
+  for (int o = KV * RB + tid * 16; o < ZR * RB; o += 256 * 16)
+    *reinterpret_cast<f32x4*>(zs + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  f32x4 rx[PX], rz[PZ];  // 16-B bf16 pieces of the next frame (unconditional, clamped loads)
+  auto prefetch = [&](int f) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * CIN);
+    const f32x4* zg = reinterpret_cast<const f32x4*>(reinterpret_cast<const __bf16*>(a.dzb) + (size_t)f * KV * CIN);
+#pragma unroll
+    for (int q = 0; q < PX; ++q) rx[q] = xg[min(tid + q * 256, nx - 1)];
+#pragma unroll
+    for (int q = 0; q < PZ; ++q) rz[q] = zg[min(tid + q * 256, nz - 1)];
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame's reads of xs / zs are done
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = tid + q * 256;
+      if (i < nx) *reinterpret_cast<f32x4*>(xs + (i / C8) * RB + (i % C8) * 16) = rx[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PZ; ++q) {
+      const int i = tid + q * 256;
+      if (i < nz) *reinterpret_cast<f32x4*>(zs + (i / C8) * RB + (i % C8) * 16) = rz[q];
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
+    // dX_f[v][c] = sum_wk A~[v][wk] dZ_f[wk][c]
+    float* dxf = a.dx + (size_t)f * V * CIN;
+    for (int nt = wave; nt < CIN / 16; nt += 4) {
+      bf16x8 b[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const unsigned p = (unsigned)(size_t)(mx_lds_t*)(zs + (32 * ks + 8 * fg + (fr >> 2)) * RB + 32 * nt + 8 * (fr & 3));
+        mx_s16x4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(p));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(p), "n"(4 * RB));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi)::"memory");
+        b[ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          acc[mt] = mfma_bf16x(ahi[mt][ks], b[ks], acc[mt]);
+          acc[mt] = mfma_bf16x(alo[mt][ks], b[ks], acc[mt]);
+        }
+      // lane holds v = 16 mt + 4 fg + r, c = 16 nt + fr; old values (identity residual) first
+      float old[2][4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = min(16 * mt + 4 * fg + r, V - 1);
+          old[mt][r] = ACC ? dxf[(size_t)v * CIN + 16 * nt + fr] : 0.f;
+        }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = 16 * mt + 4 * fg + r;
+          if (v < V) dxf[(size_t)v * CIN + 16 * nt + fr] = acc[mt][r] + old[mt][r];
+        }
+    }
+    // dA[v][wk] += sum_c X_f[v][c] dZ_f[wk][c]: this wave's wk tile, both v tiles
+#pragma unroll 4
+    for (int ks = 0; ks < CIN / 32; ++ks) {
+      const int cb = (32 * ks + 8 * fg) * 2;
+      const bf16x8 zb = *reinterpret_cast<const bf16x8*>(zs + (16 * wave + fr) * RB + cb);
+      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xs + fr * RB + cb);
+      const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xs + (16 + fr) * RB + cb);
+      dacc[0] = mfma_bf16x(x0, zb, dacc[0]);
+      dacc[1] = mfma_bf16x(x1, zb, dacc[1]);
+    }
+  }
+  // partial row of dA in the reference layout [k][v][w]: every (v < V, wk < KV) has one owner
+  float* row = a.part + (size_t)blockIdx.x * K * V * V;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = 16 * mt + 4 * fg + r, wk = 16 * wave + fr;
+      if (v < V && wk < KV) {
+        const int w = wk / K, k = wk - w * K;
+        row[(k * V + v) * V + w] = dacc[mt][r];
+      }
+    }
+}
+
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
 __global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
@@ -1387,8 +1525,51 @@ static int launch_mix_bwd(const MixArgs* a, hipStream_t s) {
   return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
 }
 
+// bf16 mode: the bf16-MFMA kernel (F3_MIX_BWD_BF16=0: the fp32 16x16x4 kernel). Grid = one
+// round of resident workgroups (each loops over frames with its next frame prefetched), capped at
+// 768 partial rows.
+static bool mix_bwd_bf16_on() {
+  static const bool v = !getenv("F3_MIX_BWD_BF16") || atoi(getenv("F3_MIX_BWD_BF16")) != 0;
+  return v;
+}
+template <int CIN>
+static size_t mix_bf16_lds() { return (size_t)96 * (2 * CIN + 16); }
+template <int CIN>
+static int mix_bwd_bf16_grid(const MixArgs* a) {
+  static const int slots = [] {
+    int per_cu = 0, dev = 0, cus = 256;
+    (void)hipFuncSetAttribute((const void*)mix_bwd_bf16_kernel<CIN, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)mix_bf16_lds<CIN>());
+    (void)hipFuncSetAttribute((const void*)mix_bwd_bf16_kernel<CIN, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)mix_bf16_lds<CIN>());
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mix_bwd_bf16_kernel<CIN, true>, 256,
+                                                     mix_bf16_lds<CIN>()) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    return per_cu * cus;
+  }();
+  return std::min(std::min(a->frames, 768), slots);
+}
+template <int CIN>
+static int launch_mix_bwd_bf16(const MixArgs* a, hipStream_t s) {
+  if (a->K * a->V > 64 || a->V > 32) return -1;
+  const int grid = mix_bwd_bf16_grid<CIN>(a);
+  if (a->accumulate)
+    hipLaunchKernelGGL((mix_bwd_bf16_kernel<CIN, true>), dim3(grid), dim3(256), mix_bf16_lds<CIN>(), s, *a);
+  else
+    hipLaunchKernelGGL((mix_bwd_bf16_kernel<CIN, false>), dim3(grid), dim3(256), mix_bf16_lds<CIN>(), s, *a);
+  F3_LAUNCH_CHECK();
+  if (a->no_colsum) return F3_OK;
+  return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
+}
+
 template <int CIN, bool ZB16>
 static int mix_bwd_ks(const MixArgs* a, hipStream_t s) {
+  if (ZB16 && mix_bwd_bf16_on()) {
+    const int r = launch_mix_bwd_bf16<CIN>(a, s);
+    if (r >= 0) return r;
+  }
   switch ((a->K * a->V + 3) / 4) {
     case 4: return launch_mix_bwd<4, CIN, ZB16>(a, s);
     case 5: return launch_mix_bwd<5, CIN, ZB16>(a, s);
@@ -1406,7 +1587,12 @@ static int mix_bwd_cin(const MixArgs* a, hipStream_t s) {
   return a->dzb ? mix_bwd_ks<CIN, true>(a, s) : mix_bwd_ks<CIN, false>(a, s);
 }
 
-int f3_mix_bwd_parts(const MixArgs* a) { return mix_lds_ok(*a) ? std::min(a->frames, 768) : 0; }
+int f3_mix_bwd_parts(const MixArgs* a) {  // rows of `part` the launch leaves (no_colsum callers sum them)
+  if (!mix_lds_ok(*a)) return 0;
+  if (a->dzb && mix_bwd_bf16_on() && a->K * a->V <= 64 && a->V <= 32)
+    return a->Cin == 64 ? mix_bwd_bf16_grid<64>(a) : a->Cin == 128 ? mix_bwd_bf16_grid<128>(a) : mix_bwd_bf16_grid<256>(a);
+  return std::min(a->frames, 768);
+}
 
 int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
   if (mix_lds_ok(*a)) {

@@ -651,8 +651,16 @@ static size_t lstm_bwd_lds(const LstmArgs& a) {
   return ((size_t)G4 * (H + 1) + G4 * a.S + LSTM_NB * a.T * a.S + LSTM_NB * H + LSTM_NB * G4 + LSTM_NB * H) * 4;
 }
 
+// F3_DBG_NO_LSTM=1 (timing experiments only; results are wrong): skip both LSTM launches, to
+// measure what the recurrences' CU and LDS occupancy costs the concurrent skeleton streams
+static bool dbg_no_lstm() {
+  static const bool v = getenv("F3_DBG_NO_LSTM") && atoi(getenv("F3_DBG_NO_LSTM")) != 0;
+  return v;
+}
+
 int f3_lstm_fwd(const LstmArgs* a, hipStream_t s) {
   if (a->S > 32 || a->S < 1) return F3_EINVAL;
+  if (dbg_no_lstm()) return F3_OK;
   dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
   hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), lstm_fwd_lds(*a), s, *a);
   F3_LAUNCH_CHECK();
@@ -661,6 +669,7 @@ int f3_lstm_fwd(const LstmArgs* a, hipStream_t s) {
 
 int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
   if (a->S > 32 || a->S < 1) return F3_EINVAL;
+  if (dbg_no_lstm()) return F3_OK;
   dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
   const size_t lds = lstm_bwd_lds(*a);
   if (lds > 160 * 1024) return F3_EINVAL;

@@ -177,6 +177,50 @@ def test_graph_mix_bf16_forward(V, Cin, F):
     assert bool(((got - ref).abs() <= tol).all()), float(((got - ref).abs() - tol).max())
 
 
+@pytest.mark.parametrize("V,K,Cin,F", [(18, 3, 64, 300), (14, 3, 128, 77), (18, 3, 256, 41), (17, 1, 64, 5),
+                                        (18, 3, 64, 7680)])
+@pytest.mark.parametrize("bf16_kernel", [True, False], ids=["bf16mfma", "fp32mfma"])
+def test_graph_mix_bf16_backward(V, K, Cin, F, bf16_kernel, monkeypatch):
+    """The bf16-mode mix backward (x, dZ bf16; dx fp32, dA fp32) against fp64 on the same bf16
+    operands, for the bf16-MFMA kernel (A~ split into bf16 hi + lo: |A~ - hi - lo| <= 2^-17 |A~|)
+    and the fp32 16x16x4 kernel (F3_MIX_BWD_BF16=0, a fresh process reads the knob): dx within
+    2e-5 of its max, dA (exact bf16 products, fp32 sums over F*Cin terms) within 1e-5 of its max.
+    F=7680 is the benchmarked 64-channel layer (B=256, T=30)."""
+    d = dev()
+    import subprocess
+    import sys
+    if not bf16_kernel:
+        code = (f"import sys; sys.path.insert(0, {os.getcwd()!r}); import tests.test_gpu_parity as t; "
+                f"t._mix_bwd_bf16_check({V}, {K}, {Cin}, {F})")
+        env = dict(os.environ, F3_MIX_BWD_BF16="0")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return
+    _mix_bwd_bf16_check(V, K, Cin, F, d)
+
+
+def _mix_bwd_bf16_check(V, K, Cin, F, d=None):
+    import fall_multimodal_amd._lib as L
+    d = d or torch.device("cuda")
+    torch.manual_seed(V * 7 + Cin + F)
+    A = torch.rand(K, V, V, dtype=torch.float64) / V            # fp32 A_eff (not bf16-representable)
+    A = A.float().double().requires_grad_(True)
+    x = torch.randn(F, V, Cin).to(torch.bfloat16).double().requires_grad_(True)
+    z = torch.einsum("kvw,fvc->fwkc", A, x)
+    dz = torch.randn_like(z).to(torch.bfloat16).double()
+    z.backward(dz)
+    Ag = A.detach().float().contiguous().to(d)
+    xg = x.detach().to(torch.bfloat16).contiguous().to(d)
+    dzg = dz.to(torch.bfloat16).contiguous().to(d)
+    dx = torch.empty(F, V, Cin, device=d)
+    dA = torch.empty(K, V, V, device=d)
+    L.check(L.lib().f3_graph_mix_backward_ex(L.ptr(Ag), L.ptr(xg), L.ptr(dzg), L.ptr(dx), L.ptr(dA), F, K, V, Cin, 1,
+                                             L.stream_handle()), "mixbwd")
+    for got, ref, rel in ((dx, x.grad, 2e-5), (dA, A.grad, 1e-5)):
+        r = ref.numpy()
+        np.testing.assert_allclose(got.cpu().double().numpy(), r, rtol=0, atol=rel * np.abs(r).max())
+
+
 @pytest.mark.parametrize("tag", TAGS)
 def test_train_step_matches_reference_golden(tag):
     """fp32 path vs the reference's own outputs (golden, B=4):
