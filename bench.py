@@ -169,7 +169,9 @@ def mix_roofline(dev, batch, V, precision):
     bwd_kern = ("mix_bwd_bf16 (bf16 MFMA) + colsum" if bf and os.environ.get("F3_MIX_BWD_BF16", "1") != "0"
                 else "mix_bwd_lds (fp32 MFMA) + colsum")
     res = {}
-    for key, byt, ms, kern in (("fwd", bytes_f, ms_f, "mix_fwd_wave"), ("bwd", bytes_b, ms_b, bwd_kern)):
+    fwd_kern = ("mix_fwd_bf16 (bf16 MFMA)" if bf and os.environ.get("F3_MIX_FWD_BF16", "1") != "0"
+                else "mix_fwd_wave (fp32 MFMA)")
+    for key, byt, ms, kern in (("fwd", bytes_f, ms_f, fwd_kern), ("bwd", bytes_b, ms_b, bwd_kern)):
         gbs = byt / (ms * 1e-3) / 1e9
         res[key] = {"kernel": f"{kern} (K=3, V={V}, Cin=64, frames={frames}, {precision})", "bound": "hbm",
                     "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -745,6 +745,77 @@ __global__ __launch_bounds__(256) void mix_bwd_bf16_kernel(MixArgs a) {
     }
 }
 
+// Graph-mix forward of the bf16 mode on bf16 MFMA 16x16x32, in the backward kernel's form: one
+// frame per loop trip (its x rows prefetched into registers one frame ahead, staged in LDS rows
+// of 2C + 16 bytes), Z^T tiles out[c][wk] = sum_v x[v][c] A~[wk][v] with x fragments as
+// transposed LDS reads and A~ (fp32) as bf16 hi + lo fragments held in registers, the tile
+// written into an LDS image of the frame's Z [KV][C] (bf16, 8-B pieces: 4 channels of one row)
+// and copied out as 16-B pieces of the contiguous frame. x rows V..31 are zero (they meet
+// A~'s zero rows). Wave w: channel tiles w, w + 4, ...
+template <int CIN>
+__global__ __launch_bounds__(256) void mix_fwd_bf16_kernel(MixArgs a) {
+  constexpr int RB = 2 * CIN + 16, XR = 32, C8 = CIN / 8;
+  constexpr int PX = (18 * C8 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smb[];
+  char* xs = smb;            // [32][RB]
+  char* zt = smb + XR * RB;  // [64][RB]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  const int nx = V * C8, nz = KV * C8;
+  // B operand: lane holds k = v = 8 fg + e, n = wk = 16 nt + fr
+  bf16x8 bhi[4], blo[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 h, l;
+      a_split(atil(a.A, K, V, 16 * nt + fr, 8 * fg + e), h, l);
+      bhi[nt][e] = h;
+      blo[nt][e] = l;
+    }
+  for (int o = V * RB + tid * 16; o < XR * RB; o += 256 * 16)
+    *reinterpret_cast<f32x4*>(xs + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rx[PX];
+  auto prefetch = [&](int f) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * CIN);
+#pragma unroll
+    for (int q = 0; q < PX; ++q) rx[q] = xg[min(tid + q * 256, nx - 1)];
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame's xs reads and zt copy-out are done
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = tid + q * 256;
+      if (i < nx) *reinterpret_cast<f32x4*>(xs + (i / C8) * RB + (i % C8) * 16) = rx[q];
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
+    for (int mt = wave; mt < CIN / 16; mt += 4) {
+      const unsigned p = (unsigned)(size_t)(mx_lds_t*)(xs + (8 * fg + (fr >> 2)) * RB + 32 * mt + 8 * (fr & 3));
+      mx_s16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(p));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(p), "n"(4 * RB));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi)::"memory");
+      const bf16x8 xa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4 acc = mfma_bf16x(xa, bhi[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+        acc = mfma_bf16x(xa, blo[nt], acc);
+        // lane holds Z[wk = 16 nt + fr][c = 16 mt + 4 fg + r], r = 0..3: one 8-B piece
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[r];
+        *reinterpret_cast<bf16x4*>(zt + (16 * nt + fr) * RB + (16 * mt + 4 * fg) * 2) = o;
+      }
+    }
+    __syncthreads();
+    f32x4* zg = reinterpret_cast<f32x4*>(a.zb + (size_t)f * KV * CIN);
+    for (int i = tid; i < nz; i += 256) zg[i] = *reinterpret_cast<const f32x4*>(zt + (i / C8) * RB + (i % C8) * 16);
+  }
+}
+
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
 __global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
@@ -1496,7 +1567,34 @@ bool f3_mix_lds_ok(int K, int V, int Cin) {
 }
 static bool mix_lds_ok(const MixArgs& a) { return f3_mix_lds_ok(a.K, a.V, a.Cin); }
 
+// bf16 mode (x and Z bf16): the bf16-MFMA kernel; F3_MIX_FWD_BF16=0 keeps the fp32-MFMA kernels
+template <int CIN>
+static int launch_mix_fwd_bf16(const MixArgs* a, hipStream_t s) {
+  constexpr size_t lds = (size_t)96 * (2 * CIN + 16);
+  static const int slots = [] {
+    int per_cu = 0, dev = 0, cus = 256;
+    (void)hipFuncSetAttribute((const void*)mix_fwd_bf16_kernel<CIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mix_fwd_bf16_kernel<CIN>, 256, lds) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    return per_cu * cus;
+  }();
+  const int grid = std::max(1, std::min(a->frames, slots));
+  hipLaunchKernelGGL(mix_fwd_bf16_kernel<CIN>, dim3(grid), dim3(256), lds, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
+  static const bool fwd_bf16 = !getenv("F3_MIX_FWD_BF16") || atoi(getenv("F3_MIX_FWD_BF16")) != 0;
+  if (fwd_bf16 && mix_lds_ok(*a) && a->x16 && a->zb && a->K * a->V <= 64 && a->V <= 32) {
+    if (a->frames <= 0) return F3_OK;
+    return a->Cin == 64 ? launch_mix_fwd_bf16<64>(a, s) : a->Cin == 128 ? launch_mix_fwd_bf16<128>(a, s)
+                                                           : launch_mix_fwd_bf16<256>(a, s);
+  }
   if (mix_lds_ok(*a)) {
     const int r = a->Cin == 64 ? mix_fwd_ks<64>(a, s) : a->Cin == 128 ? mix_fwd_ks<128>(a, s) : mix_fwd_ks<256>(a, s);
     if (r >= 0) return r;

@@ -1,0 +1,34 @@
+"""The bench's 3-stream training step alone (B=256, V=18, S=6, bf16, eager), for kernel traces:
+    rocprofv3 --kernel-trace -d gpurun_out/step -o run -- python tools/step_only.py [steps]
+    python tools/timeline.py gpurun_out/step/run_results.db --list"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    import fall_multimodal_amd as f3
+    from oracle.prng import synthetic_batch
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    dev = torch.device("cuda")
+    B, V, S, C = 256, 18, 6, 11
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, C, S, device=dev,
+                                      precision="bf16")
+    step = f3.TrainStep(model, B, lr=1e-3)
+    sk, se, lb = (torch.from_numpy(x).to(dev) for x in synthetic_batch(B, V, C, S, 100))
+    for _ in range(3):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    print(f"{(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step")
+
+
+if __name__ == "__main__":
+    main()
