@@ -1435,10 +1435,22 @@ __global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
   for (int c = threadIdx.x; c < C; c += 256) {
     float sc, sh, mu, rs;
     bn_coeff(a.bn2, c, sc, sh, mu, rs);
+    // W1's column c read once for all the workgroup's clips (the clip loop outside re-read it
+    // per clip: 4 dependent 64-long load chains); per clip the k order is unchanged
+    float dgs[kCaB3Clips];
+#pragma unroll
+    for (int nn = 0; nn < kCaB3Clips; ++nn) dgs[nn] = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < H; ++k) {
+      const float wk = a.W1[(size_t)k * C + c];
+#pragma unroll
+      for (int nn = 0; nn < kCaB3Clips; ++nn) dgs[nn] += dq[nn][k] * wk;
+    }
     double s1 = 0.0, s2 = 0.0, r1 = 0.0, r2 = 0.0;
-    for (int nn = 0; nn < kCaB3Clips && n0 + nn < N; ++nn) {
-      float dg = 0.f;
-      for (int k = 0; k < H; ++k) dg += dq[nn][k] * a.W1[(size_t)k * C + c];
+#pragma unroll
+    for (int nn = 0; nn < kCaB3Clips; ++nn) {
+      if (n0 + nn >= N) break;
+      const float dg = dgs[nn];
       const size_t o = (size_t)(n0 + nn) * C + c;
       a.e[o] = dg * a.inv_tv;
       const float at = a.att[o];
