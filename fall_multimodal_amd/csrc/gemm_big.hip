@@ -25,24 +25,30 @@ namespace f3 {
 constexpr int BG_MT = 9, BG_NT = 2, BG_NST = 3;  // per-wave MFMA tiles (rows x cols), LDS stages
 constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 
-template <int WM, int WN>
+// BD (B direct): the weight fragments are loaded from global memory straight into registers one
+// k chunk ahead instead of through the LDS stages, which then carry the A rows only (the stages
+// are bound by the L2 -> LDS fill rate, ~12 B/cycle/CU: 50 KB per chunk with B, 18 KB without).
+template <int WM, int WN, bool BD = false>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
-  static constexpr int AP = BM / 8, BP = BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
-  static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;     // pieces per wave
+  static constexpr int AP = BM / 8, BP = BD ? 0 : BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
+  static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;              // pieces per wave
   static constexpr int STAGE = NP * 1024;
-  static constexpr int SMEM = BG_NST * STAGE + 4 * BN * 4;
+  // the epilogue's output image (16 KiB + BM x (BN + 8) bf16) reuses the stages' bytes
+  static constexpr int OT_NEED = 16 * 1024 + BM * (BN + 8) * 2;
+  static constexpr int EPI_OFF = BG_NST * STAGE > OT_NEED ? BG_NST * STAGE : OT_NEED;
+  static constexpr int SMEM = EPI_OFF + 4 * BN * 4;
 };
 
-template <int EPI, int WM, int WN>
+template <int EPI, int WM, int WN, bool BD = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
-  using Cfg = BigCfg<WM, WN>;
+  using Cfg = BigCfg<WM, WN, BD>;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
   static_assert(WM * WN == BG_WAVES, "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
   // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code)
   __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
-  float* epi_sc = reinterpret_cast<float*>(smem + BG_NST * STAGE);
+  float* epi_sc = reinterpret_cast<float*>(smem + Cfg::EPI_OFF);
   float* epi_sh = epi_sc + BN;
   float* epi_mu = epi_sh + BN;
   float* epi_rs = epi_mu + BN;
@@ -130,11 +136,24 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // BD: this lane's B fragments of chunk t, [ks][y] = W[wn*32 + y*16 + fr][k0 + (ks*4 + fg)*8 ..+8]
+  bf16x8 fbr[2][BG_NT];
+  auto load_b = [&](int t, bf16x8 (&f)[2][BG_NT]) {
+    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    const int dt = par ? dt0 + 2 * tap : tap;
+    const int k0 = dt * g.Kc + i0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y)
+        f[ks][y] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(wn * 32 + y * 16 + fr) * Ktot + k0 + (ks * 4 + fg) * 8);
+  };
 
   if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
     if (EPI & EPI_ADD) return;
     __syncthreads();
   } else {
+    if (BD) load_b(0, fbr);
     stage(0, 0);
     if (nchunk > 1) {
       stage(1, 1);
@@ -146,6 +165,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   }
   for (int t = 0; t < nchunk; ++t) {
     const int buf = t % 3;
+    bf16x8 fbn[2][BG_NT];
+    if (BD && t + 1 < nchunk) load_b(t + 1, fbn);  // issued before the stage: one vmcnt serves both
     if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
     const char* sa = smem + buf * STAGE;
     const char* sb = sa + AP * 1024;
@@ -156,7 +177,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
       for (int y = 0; y < BG_NT; ++y) {
         const int r = wn * 32 + y * 16 + fr;
-        fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+        fb[y] = BD ? fbr[ks][y] : *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
       }
 #pragma unroll
       for (int x = 0; x < BG_MT; ++x) {
@@ -172,6 +193,12 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (BD && t + 1 < nchunk) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) fbr[ks][y] = fbn[ks][y];
+    }
   }
   __syncthreads();
 
@@ -340,11 +367,14 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
     const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
     tiles = (M0 + BM - 1) / BM + (M1 + BM - 1) / BM;
   }
-#define F3_BCASE(E)                                                                 \
-  if (epi == (E)) {                                                                \
-    hipLaunchKernelGGL((igemm_big<(E), WM, WN>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    F3_LAUNCH_CHECK();                                                              \
-    return F3_OK;                                                                   \
+  // F3_BIG_BDIRECT=1: weight fragments straight to registers (BD), A rows only through LDS
+  static const int bd = getenv("F3_BIG_BDIRECT") ? atoi(getenv("F3_BIG_BDIRECT")) : 0;
+#define F3_BCASE(E)                                                                        \
+  if (epi == (E)) {                                                                       \
+    if (bd) hipLaunchKernelGGL((igemm_big<(E), WM, WN, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);   \
+    F3_LAUNCH_CHECK();                                                                     \
+    return F3_OK;                                                                          \
   }
   F3_BCASE(EPI_BIASV | EPI_STATS)            // gcn forward
   F3_BCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
