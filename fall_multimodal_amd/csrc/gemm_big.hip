@@ -28,21 +28,31 @@ constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 // BD (B direct): the weight fragments are loaded from global memory straight into registers one
 // k chunk ahead instead of through the LDS stages, which then carry the A rows only (the stages
 // are bound by the L2 -> LDS fill rate, ~12 B/cycle/CU: 50 KB per chunk with B, 18 KB without).
-template <int WM, int WN, bool BD = false>
+// WIN (clip window): for stride-1 temporal convs whose clips are exactly 144 rows (T*V = 144,
+// the 256-channel layers at T = 8) a workgroup owns two whole clips x BN = 128 output channels.
+// Each channel chunk's 288 input rows are staged ONCE (two 36-KiB A buffers) and all KT taps
+// read them shifted by (dt - P) frames, rows falling outside the clip read as zero; only the
+// weights are staged per (chunk, tap) step (16 KiB). Per workgroup that is 4 x 36 + 36 x 16 =
+// 720 KiB of L2 -> LDS fill instead of 36 x 50 KiB = 1.8 MiB for the 144 x 256 tile.
+constexpr int WIN_APS = 6;  // A pieces of the next chunk carried by one step (steps 2..7 of 9)
+template <int WM, int WN, bool BD = false, bool WIN = false>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
-  static constexpr int AP = BM / 8, BP = BD ? 0 : BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
+  static constexpr int AP = WIN ? WIN_APS : BM / 8, BP = BD ? 0 : BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
   static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;              // pieces per wave
-  static constexpr int STAGE = NP * 1024;
+  static constexpr int STAGE = WIN ? BN * 128 : NP * 1024;
+  static constexpr int AWIN = WIN ? BM * 128 : 0;    // one A window buffer (WIN: two of them)
+  static constexpr int SOFF = 2 * AWIN;              // byte offset of the per-step stages
   // the epilogue's output image (16 KiB + BM x (BN + 8) bf16) reuses the stages' bytes
   static constexpr int OT_NEED = 16 * 1024 + BM * (BN + 8) * 2;
-  static constexpr int EPI_OFF = BG_NST * STAGE > OT_NEED ? BG_NST * STAGE : OT_NEED;
+  static constexpr int EPI_OFF = SOFF + BG_NST * STAGE > OT_NEED ? SOFF + BG_NST * STAGE : OT_NEED;
   static constexpr int SMEM = EPI_OFF + 4 * BN * 4;
 };
 
-template <int EPI, int WM, int WN, bool BD = false>
+template <int EPI, int WM, int WN, bool BD = false, bool WIN = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
-  using Cfg = BigCfg<WM, WN, BD>;
+  using Cfg = BigCfg<WM, WN, BD, WIN>;
+  static_assert(!(WIN && (BD || WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips, weights through LDS");
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
   static_assert(WM * WN == BG_WAVES, "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
@@ -57,7 +67,13 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const bool par = igemm_parity(g);
+  int n0 = 0;  // first output channel of the tile (WIN: Nc / BN column tiles, neighbours share rows)
+  if (WIN) {
+    const int ncol = g.Nc / BN;
+    n0 = (tile % ncol) * BN;
+    tile /= ncol;
+  }
+  const bool par = !WIN && igemm_parity(g);
   int p = 0, Tp = g.T_out, Mp = g.M;
   if (par) {
     const int nclip = g.M / (g.T_out * g.V), T0 = (g.T_out + 1) >> 1;
@@ -83,7 +99,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   if (EPI & EPI_RELUMASK) {
     for (int t = tid; t < BN; t += BG_THREADS) {
       float sc, sh, mu, rs;
-      bn_coeff(a.epi_bn, t, sc, sh, mu, rs);
+      bn_coeff(a.epi_bn, n0 + t, sc, sh, mu, rs);
       epi_sc[t] = sc; epi_sh[t] = sh; epi_mu[t] = mu; epi_rs[t] = rs;
     }
   }
@@ -96,6 +112,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   int boff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
+    if (WIN) break;
     const int q = (wave + BG_WAVES * i) % NP;
     amap[i].base = -1;
     amap[i].q = 0;
@@ -149,55 +166,139 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         f[ks][y] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(wn * 32 + y * 16 + fr) * Ktot + k0 + (ks * 4 + fg) * 8);
   };
 
-  if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
-    if (EPI & EPI_ADD) return;
-    __syncthreads();
-  } else {
-    if (BD) load_b(0, fbr);
-    stage(0, 0);
-    if (nchunk > 1) {
-      stage(1, 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-  }
-  for (int t = 0; t < nchunk; ++t) {
-    const int buf = t % 3;
-    bf16x8 fbn[2][BG_NT];
-    if (BD && t + 1 < nchunk) load_b(t + 1, fbn);  // issued before the stage: one vmcnt serves both
-    if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
-    const char* sa = smem + buf * STAGE;
-    const char* sb = sa + AP * 1024;
+  if constexpr (WIN) {
+    // step u = (chunk c, tap dt), chunk-major: c = u / KT, dt = u % KT. Per step every wave
+    // issues PPW DMAs: its B pieces of step u's weight stage, the 6 A pieces of chunk c + 1 that
+    // step u carries (steps 2..7 of a chunk: the buffer they fill was last read in step c*KT - 1,
+    // and a step is issued two steps ahead), and otherwise a re-issue of its first B piece.
+    constexpr int KTW = 9;
+    const int nstep = KTW * kpt;
+    const int sgn = g.transposed ? -1 : 1;
+    auto stage_w = [&](int u, int buf) {
+      const int c = u / KTW, dt = u - c * KTW;
+      const int k0 = dt * g.Kc + c * G_BK;
+      char* sbase = smem + Cfg::SOFF + buf * STAGE;
+      const void* src0 = wb + (size_t)(n0 + wave * 8 + sub) * Ktot + k0 + swz(wave * 8 + sub, pch) * 8;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[BG_MT], fb[BG_NT];
-      const int c = ks * 4 + fg;
-#pragma unroll
-      for (int y = 0; y < BG_NT; ++y) {
-        const int r = wn * 32 + y * 16 + fr;
-        fb[y] = BD ? fbr[ks][y] : *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+      for (int i = 0; i < PPW; ++i) {
+        const int q = wave + BG_WAVES * i;
+        const void* src = src0;
+        char* dst = sbase + wave * 1024;
+        if (q < Cfg::BP) {
+          src = wb + (size_t)(n0 + q * 8 + sub) * Ktot + k0 + swz(q * 8 + sub, pch) * 8;
+          dst = sbase + q * 1024;
+        } else if (q < NP && dt >= 2 && c + 1 < kpt) {
+          const int pa = (dt - 2) * WIN_APS + (q - Cfg::BP);  // A piece of chunk c + 1
+          if (pa < BM / 8) {
+            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + (c + 1) * G_BK + swz(pa * 8 + sub, pch) * 8;
+            dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
+          }
+        }
+        __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
       }
+    };
+    // chunk 0's A rows, then steps 0 and 1
+    constexpr int A0W = (BM / 8 + BG_WAVES - 1) / BG_WAVES;
+#pragma unroll
+    for (int i = 0; i < A0W; ++i) {
+      const int pa = (wave + BG_WAVES * i) % (BM / 8);
+      __builtin_amdgcn_global_load_lds(in + (size_t)(m0 + pa * 8 + sub) * g.lda + swz(pa * 8 + sub, pch) * 8,
+                                       (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
+    }
+    stage_w(0, 0);
+    stage_w(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const int wrow = wm * 144;  // this wave's clip in the tile
+    for (int u = 0; u < nstep; ++u) {
+      const int c = u / KTW, dt = u - c * KTW;
+      const int sh = sgn * (dt - g.P) * g.V;  // row shift of this tap inside the clip
+      if (u + 2 < nstep) stage_w(u + 2, (u + 2) % 3);
+      const char* sa = smem + (c & 1) * Cfg::AWIN;
+      const char* sb = smem + Cfg::SOFF + (u % 3) * STAGE;
+      int arow[BG_MT];
+      bool aok[BG_MT];
 #pragma unroll
       for (int x = 0; x < BG_MT; ++x) {
-        const int r = wm * 144 + x * 16 + fr;
-        fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+        const int rs = x * 16 + fr + sh;
+        aok[x] = rs >= 0 && rs < 144;
+        arow[x] = wrow + min(max(rs, 0), 143);
       }
 #pragma unroll
-      for (int x = 0; x < BG_MT; ++x)
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[BG_MT], fb[BG_NT];
+        const int cc = ks * 4 + fg;
 #pragma unroll
-        for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+        for (int y = 0; y < BG_NT; ++y) {
+          const int r = wn * 32 + y * 16 + fr;
+          fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, cc) * 16);
+        }
+#pragma unroll
+        for (int x = 0; x < BG_MT; ++x) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + arow[x] * 128 + swz(arow[x], cc) * 16);
+          fa[x] = aok[x] ? v : bf16x8{};
+        }
+#pragma unroll
+        for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+      }
+      if (u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
-    if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (BD && t + 1 < nchunk) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int y = 0; y < BG_NT; ++y) fbr[ks][y] = fbn[ks][y];
+  } else {
+    if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
+      if (EPI & EPI_ADD) return;
+      __syncthreads();
+    } else {
+      if (BD) load_b(0, fbr);
+      stage(0, 0);
+      if (nchunk > 1) {
+        stage(1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    for (int t = 0; t < nchunk; ++t) {
+      const int buf = t % 3;
+      bf16x8 fbn[2][BG_NT];
+      if (BD && t + 1 < nchunk) load_b(t + 1, fbn);  // issued before the stage: one vmcnt serves both
+      if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
+      const char* sa = smem + buf * STAGE;
+      const char* sb = sa + AP * 1024;
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[BG_MT], fb[BG_NT];
+        const int c = ks * 4 + fg;
+  #pragma unroll
+        for (int y = 0; y < BG_NT; ++y) {
+          const int r = wn * 32 + y * 16 + fr;
+          fb[y] = BD ? fbr[ks][y] : *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+        }
+  #pragma unroll
+        for (int x = 0; x < BG_MT; ++x) {
+          const int r = wm * 144 + x * 16 + fr;
+          fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+        }
+  #pragma unroll
+        for (int x = 0; x < BG_MT; ++x)
+  #pragma unroll
+          for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+      }
+      if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (BD && t + 1 < nchunk) {
+  #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+  #pragma unroll
+          for (int y = 0; y < BG_NT; ++y) fbr[ks][y] = fbn[ks][y];
+      }
     }
   }
   __syncthreads();
@@ -224,7 +325,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const bool aux16 = a.auxb != nullptr;
   float biasj[BG_NT];  // EPI_BIAS: one value per column, loaded once
 #pragma unroll
-  for (int y = 0; y < BG_NT; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(wn * 32 + y * 16 + fr, g.Nc - 1)] : 0.f;
+  for (int y = 0; y < BG_NT; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1)] : 0.f;
   // all groups' operands first: a load issued after the group's stores would make its first
   // use wait (vmcnt counts stores too) for every store before it
   float pre[BG_MT][4][BG_NT];
@@ -235,7 +336,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int mc = max(phys(m0 + wm * 144 + x * 16 + fg * 4 + r), 0);
 #pragma unroll
-        for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(wn * 32 + y * 16 + fr, g.Nc - 1));
+        for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1));
       }
   };
   if (EPI & EPI_RELUMASK) {
@@ -253,7 +354,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     for (int r = 0; r < 4; ++r) mrow[r] = phys(m0 + wm * 144 + x * 16 + fg * 4 + r);
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) {
-      const int j = wn * 32 + y * 16 + fr;
+      const int jl = wn * 32 + y * 16 + fr, j = n0 + jl;  // tile-local / global column
       const bool jok = j < g.Nc;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -264,8 +365,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         if (EPI & EPI_BIASV) v += pre[x][r][y];
         if (EPI & EPI_RELUMASK) {
           const float gv = pre[x][r][y];
-          if (gv * epi_sc[j] + epi_sh[j] <= 0.f) v = 0.f;
-          const float xh = (gv - epi_mu[j]) * epi_rs[j];
+          if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
+          const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
           ssum[y] += v;
           ssq[y] += v * xh;
         } else if (EPI & EPI_STATS) {
@@ -279,7 +380,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
           else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
         }
         if (!(EPI & EPI_ADD) && a.outb) {
-          if (stage_out) ot[(wm * 144 + x * 16 + fg * 4 + r) * OTS + j] = (__bf16)v;
+          if (stage_out) ot[(wm * 144 + x * 16 + fg * 4 + r) * OTS + jl] = (__bf16)v;
           else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
         } else {
           float* o = a.out + (size_t)m * g.ldo + j;
@@ -312,7 +413,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     }
     __syncthreads();
     for (int t = tid; t < BN; t += BG_THREADS) {
-      if (t >= g.Nc) continue;
+      if (n0 + t >= g.Nc) continue;
       float s0 = 0.f, s1 = 0.f, g0 = 0.f, g1 = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
@@ -322,12 +423,12 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         g1 += gred[(w * 2 + 1) * BN + t];
       }
       if (EPI & (EPI_STATS | EPI_RELUMASK)) {
-        atomic_add_d(a.st_sum + t, (double)s0);
-        atomic_add_d(a.st_sq + t, (double)s1);
+        atomic_add_d(a.st_sum + n0 + t, (double)s0);
+        atomic_add_d(a.st_sq + n0 + t, (double)s1);
       }
       if (EPI & EPI_GAP) {
-        atomic_add_f(a.gap + (size_t)nlo * g.Nc + t, g0);
-        if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + t, g1);
+        atomic_add_f(a.gap + (size_t)nlo * g.Nc + n0 + t, g0);
+        if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + n0 + t, g1);
       }
     }
   }
@@ -336,7 +437,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     constexpr int CPR = BN / 8;  // 16-B chunks per tile row
     for (int q = tid; q < BM * CPR; q += blockDim.x) {
       const int rl = q / CPR, c = q - rl * CPR;
-      const int m = phys(m0 + rl), j = 0 + c * 8;
+      const int m = phys(m0 + rl), j = n0 + c * 8;
       if (m < 0 || j >= g.Nc) continue;
       *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
           *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
@@ -387,10 +488,34 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   return F3_EINVAL;
 }
 
+// Clip-window form (WIN): stride-1 9-tap temporal convs (forward or input gradient) of the
+// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows. F3_BIG_WIN=1 turns it
+// on (default off until measured on the step; A/B against the 144 x 256 tile).
+static bool big_win_ok(const ConvGemmArgs& a) {
+  static const int on = getenv("F3_BIG_WIN") ? atoi(getenv("F3_BIG_WIN")) : 0;
+  const ConvGeom& g = a.g;
+  return on && g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
+         g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % G_BK == 0 && g.Kc / G_BK >= 2 && !igemm_parity(g);
+}
+
 int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
+  if (big_win_ok(a)) {
+    const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
+#define F3_WCASE(E)                                                                        \
+    if (epi == (E)) {                                                                     \
+      hipLaunchKernelGGL((igemm_big<(E), 2, 4, false, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+      F3_LAUNCH_CHECK();                                                                   \
+      return F3_OK;                                                                        \
+    }
+    F3_WCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
+    F3_WCASE(EPI_RELUMASK)                     // tcn dgrad
+    F3_WCASE(EPI_BIAS)                         // plain conv (tests)
+    F3_WCASE(0)                                // plain input gradient (tests)
+#undef F3_WCASE
+  }
   if (a.g.Nc == 256) return launch_big<1, 8>(a, epi, s);
   return launch_big<2, 4>(a, epi, s);
 }
