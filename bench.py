@@ -88,7 +88,7 @@ def roofline_kernels(dev, batch, V, precision):
     * "tcn_fwd": the forward implicit GEMM with bf16 output (the step writes the tcn output bf16;
       its launch adds the BN-statistics/pool epilogue, EPI 13): igemm_big<1,2,4,false,true>, the
       clip-window form (two clips x 128 channels per workgroup, each channel chunk's rows staged
-      once for all 9 taps) under F3_BIG_WIN=1, else the 144 x 256 tile igemm_big<1,1,8>.
+      once for all 9 taps); F3_BIG_WIN=0: the 144 x 256 tile igemm_big<1,1,8>.
     Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for all three."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
@@ -111,7 +111,7 @@ def roofline_kernels(dev, batch, V, precision):
             "conv")  # packs w into wp; the timed launches reuse it (the GEMM alone)
     ms = _time_launch(lambda: lib.f3_conv_forward(L.ptr(x), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1,
                                                   4, prec, st))
-    win = os.environ.get("F3_BIG_WIN", "0") == "1" and (N * T * V) % 288 == 0 and T * V == 144
+    win = os.environ.get("F3_BIG_WIN", "1") != "0" and (N * T * V) % 288 == 0 and T * V == 144
     fname = "igemm_big<1,2,4,false,true> (clip window)" if win else "igemm_big<1,1,8>"
     out["tcn_fwd"] = {"kernel": f"{fname + ' bf16-out' if bf else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, "
                                 f"N={N}, V={V})", "ms": ms}

@@ -34,6 +34,7 @@ constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 // read them shifted by (dt - P) frames, rows falling outside the clip read as zero; only the
 // weights are staged per (chunk, tap) step (16 KiB). Per workgroup that is 4 x 36 + 36 x 16 =
 // 720 KiB of L2 -> LDS fill instead of 36 x 50 KiB = 1.8 MiB for the 144 x 256 tile.
+typedef __attribute__((address_space(3))) const char lds_cchar_t;
 constexpr int WIN_APS = 6;  // A pieces of the next chunk carried by one step (steps 2..7 of 9)
 template <int WM, int WN, bool BD = false, bool WIN = false>
 struct BigCfg {
@@ -46,10 +47,11 @@ struct BigCfg {
   // the epilogue's output image (16 KiB + BM x (BN + 8) bf16) reuses the stages' bytes
   static constexpr int OT_NEED = 16 * 1024 + BM * (BN + 8) * 2;
   static constexpr int EPI_OFF = SOFF + BG_NST * STAGE > OT_NEED ? SOFF + BG_NST * STAGE : OT_NEED;
-  static constexpr int SMEM = EPI_OFF + 4 * BN * 4;
+  static constexpr int ZOFF = EPI_OFF + 4 * BN * 4;  // WIN: one zero row, read for out-of-clip taps
+  static constexpr int SMEM = ZOFF + (WIN ? 128 : 0);
 };
 
-template <int EPI, int WM, int WN, bool BD = false, bool WIN = false>
+template <int EPI, int WM, int WN, bool BD = false, bool WIN = false, bool ARD = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, BD, WIN>;
   static_assert(!(WIN && (BD || WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips, weights through LDS");
@@ -207,45 +209,61 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     }
     stage_w(0, 0);
     stage_w(1, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
     __builtin_amdgcn_s_barrier();
     const int wrow = wm * 144;  // this wave's clip in the tile
+    // fragment reads as inline asm: hipcc otherwise issues each ds_read_b128 just before the MFMA
+    // that consumes it with its own lgkmcnt(0), exposing the LDS latency ~14 times per step. Both
+    // k halves' 22 reads are issued at once; each half is released by a counted wait whose asm
+    // also passes the fragments through (nothing can use them earlier). Out-of-clip tap rows read
+    // a zero row instead of being masked.
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+    const unsigned zaddr = lds0 + Cfg::ZOFF + fg * 16;
     for (int u = 0; u < nstep; ++u) {
       const int c = u / KTW, dt = u - c * KTW;
       const int sh = sgn * (dt - g.P) * g.V;  // row shift of this tap inside the clip
       if (u + 2 < nstep) stage_w(u + 2, (u + 2) % 3);
-      const char* sa = smem + (c & 1) * Cfg::AWIN;
-      const char* sb = smem + Cfg::SOFF + (u % 3) * STAGE;
-      int arow[BG_MT];
-      bool aok[BG_MT];
-#pragma unroll
-      for (int x = 0; x < BG_MT; ++x) {
-        const int rs = x * 16 + fr + sh;
-        aok[x] = rs >= 0 && rs < 144;
-        arow[x] = wrow + min(max(rs, 0), 143);
-      }
+      const unsigned sa = lds0 + (c & 1) * Cfg::AWIN;
+      const unsigned sb = lds0 + Cfg::SOFF + (u % 3) * STAGE;
+      u32x4_t f[2][BG_NT + BG_MT];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[BG_MT], fb[BG_NT];
         const int cc = ks * 4 + fg;
 #pragma unroll
         for (int y = 0; y < BG_NT; ++y) {
           const int r = wn * 32 + y * 16 + fr;
-          fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, cc) * 16);
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(sb + r * 128 + swz(r, cc) * 16));
         }
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x) {
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + arow[x] * 128 + swz(arow[x], cc) * 16);
-          fa[x] = aok[x] ? v : bf16x8{};
+          const int rs = x * 16 + fr + sh, r = wrow + rs;
+          const unsigned ad = (rs >= 0 && rs < 144) ? sa + r * 128 + swz(r, cc) * 16 : zaddr;
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][BG_NT + x]) : "v"(ad));
         }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < BG_NT + BG_MT; ++q) asm volatile("" : "+v"(f[ks][q]));
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+          for (int y = 0; y < BG_NT; ++y)
+            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[ks][y]),
+                                   acc[x][y]);
+        if (ks == 0) {  // pin the first half's MFMAs above the second wait (hipcc sinks them below it)
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+        }
       }
       if (u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
   } else {
@@ -270,23 +288,63 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
       const char* sa = smem + buf * STAGE;
       const char* sb = sa + AP * 1024;
-  #pragma unroll
+      if constexpr (!BD && ARD) {
+        // ARD (F3_BIG_ASM=1): as the WIN loop: both k halves' 22 fragment reads issued at once (inline asm), each half
+        // released by a counted wait; hipcc's own schedule waits lgkmcnt(0) before every MFMA pair
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        const unsigned la = (unsigned)(size_t)(lds_cchar_t*)sa, lb = (unsigned)(size_t)(lds_cchar_t*)sb;
+        u32x4_t f[2][BG_NT + BG_MT];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + fg;
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) {
+            const int r = wn * 32 + y * 16 + fr;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(lb + r * 128 + swz(r, c) * 16));
+          }
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x) {
+            const int r = wm * 144 + x * 16 + fr;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][BG_NT + x]) : "v"(la + r * 128 + swz(r, c) * 16));
+          }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int q = 0; q < BG_NT + BG_MT; ++q) asm volatile("" : "+v"(f[ks][q]));
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[ks][y]),
+                                     acc[x][y]);
+          if (ks == 0) {
+#pragma unroll
+            for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+              for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+          }
+        }
+      } else
+#pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 fa[BG_MT], fb[BG_NT];
         const int c = ks * 4 + fg;
-  #pragma unroll
+#pragma unroll
         for (int y = 0; y < BG_NT; ++y) {
           const int r = wn * 32 + y * 16 + fr;
           fb[y] = BD ? fbr[ks][y] : *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
         }
-  #pragma unroll
+#pragma unroll
         for (int x = 0; x < BG_MT; ++x) {
           const int r = wm * 144 + x * 16 + fr;
           fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
         }
-  #pragma unroll
+#pragma unroll
         for (int x = 0; x < BG_MT; ++x)
-  #pragma unroll
+#pragma unroll
           for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
       }
       if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
@@ -294,9 +352,9 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (BD && t + 1 < nchunk) {
-  #pragma unroll
+#pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-  #pragma unroll
+#pragma unroll
           for (int y = 0; y < BG_NT; ++y) fbr[ks][y] = fbn[ks][y];
       }
     }
@@ -470,9 +528,12 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   }
   // F3_BIG_BDIRECT=1: weight fragments straight to registers (BD), A rows only through LDS
   static const int bd = getenv("F3_BIG_BDIRECT") ? atoi(getenv("F3_BIG_BDIRECT")) : 0;
+  // F3_BIG_ASM=1: the batched inline-asm fragment reads of the WIN loop in the regular loop too
+  static const int ard = getenv("F3_BIG_ASM") ? atoi(getenv("F3_BIG_ASM")) : 0;
 #define F3_BCASE(E)                                                                        \
   if (epi == (E)) {                                                                       \
     if (bd) hipLaunchKernelGGL((igemm_big<(E), WM, WN, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else if (ard) hipLaunchKernelGGL((igemm_big<(E), WM, WN, false, false, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
     else hipLaunchKernelGGL((igemm_big<(E), WM, WN, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);   \
     F3_LAUNCH_CHECK();                                                                     \
     return F3_OK;                                                                          \
@@ -489,10 +550,10 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
 }
 
 // Clip-window form (WIN): stride-1 9-tap temporal convs (forward or input gradient) of the
-// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows. F3_BIG_WIN=1 turns it
-// on (default off until measured on the step; A/B against the 144 x 256 tile).
+// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows. F3_BIG_WIN=0 turns it
+// off (A/B against the 144 x 256 tile).
 static bool big_win_ok(const ConvGemmArgs& a) {
-  static const int on = getenv("F3_BIG_WIN") ? atoi(getenv("F3_BIG_WIN")) : 0;
+  static const int on = getenv("F3_BIG_WIN") ? atoi(getenv("F3_BIG_WIN")) : 1;
   const ConvGeom& g = a.g;
   return on && g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
          g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % G_BK == 0 && g.Kc / G_BK >= 2 && !igemm_parity(g);
