@@ -11,6 +11,9 @@ branch, so none is built or timed.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`bench.py --gpus N` without a torch.distributed environment starts the N ranks itself (one per
+GPU, torch.distributed.run as a child process) and fails if the node has fewer than N GPUs.
+
 Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
 ranks), the roofline of the dominant kernel (the temporal-conv weight-gradient GEMM, measured
 live with HIP events on the stream it runs on; HBM traffic from profiles/r01_roofline_pmc.json) and the CPU baseline (the oracle timed on this
@@ -55,7 +58,44 @@ def parse():
                         "musa: the root main.py's musa_model")
     p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN and config-5 lines in the default run")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the --gpus N ranks exactly as a bench run does, all-reduce each rank's id over gloo and "
+                        "print the ranks seen; touches no GPU (tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def launch_ranks(a):
+    """`bench.py --gpus N` with no torch.distributed environment: start N ranks (one per GPU) with
+    torch.distributed.run as a CHILD process and exit with its status (never exec: this process
+    must not have touched the GPU, and it has not - torch.cuda.device_count() does not initialise
+    it). Fails loudly when the node has fewer than N GPUs instead of silently timing one."""
+    import socket
+    import subprocess
+    if not a.launch_check:
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            raise SystemExit(f"bench.py --gpus {a.gpus}: this node has {have} GPU(s); refusing to report a "
+                             f"{a.gpus}-GPU number from fewer ranks")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(world, rank):
+    """Each rank contributes its id over gloo: rank 0 prints the world and the ranks seen."""
+    dist.init_process_group("gloo")
+    ids = torch.zeros(world, dtype=torch.int64)
+    ids[rank] = rank + 1
+    dist.all_reduce(ids)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world": dist.get_world_size(),
+                          "ranks_seen": [int(i) - 1 for i in ids.tolist()]}), flush=True)
+    dist.destroy_process_group()
 
 
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
@@ -503,9 +543,16 @@ def cpu_baseline(layout, V, S, seconds):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
+    if a.launch_check:
+        launch_check(world, rank)
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
@@ -601,7 +648,8 @@ def main():
             "config": {"workload": f"fall3_3stream_{a.layout}_V{V}_S{S}_B{B}_per_gpu",
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
-                       "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5)},
+                       "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
+                       "ranks": world, "collective": "rccl all_reduce (2 buckets)" if world > 1 else None},
             "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
             "roofline_tcn_fwd": roofs["tcn_fwd"],

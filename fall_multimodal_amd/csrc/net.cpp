@@ -969,9 +969,15 @@ struct Branches {
     }
     return F3_OK;
   }
-  // end of backward phase 1: record where every queue is instead of joining them into s
+  // end of backward phase 1: record where every queue is instead of joining them into s. Under
+  // stream capture the queues are joined instead: a capture must end with every forked queue
+  // joined back, and events recorded inside one capture are not re-recorded by its replay (the
+  // caller orders its all-reduce after the replaying stream, train.py TrainStep.__call__).
   int mark_phase1() {
     n.p1_mask = 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) return F3_EHIP;
+    if (cs != hipStreamCaptureStatusNone) return join();
     for (auto& e : n.ev_p1)  // (serial mode never created the branch events)
       if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return F3_EHIP;
     for (int i = 0; i < 3 && par; ++i) {

@@ -19,6 +19,7 @@ draws); `dropblock=False` runs the reference with keep_prob 1 and p 0.
 from __future__ import annotations
 
 import ctypes
+import re
 import math
 
 import numpy as np
@@ -223,6 +224,17 @@ class Model(nn.Module):
         return out
 
 
+_NONE_GRAD = re.compile(r"(^|\.)A$|^stream_(pos|mot)\.[12]\.edge$")
+
+
+def grad_is_none(name):
+    """True for the parameters whose .grad the reference leaves None after backward: the frozen
+    graphs `A` and the SepTemporal blocks' `edge`, which only shape the DropBlock masks
+    (musa_model.py:148-199; f3_musa_backward zero-fills their slots). Adam/AdamW with weight
+    decay would otherwise move them on a zero gradient."""
+    return bool(_NONE_GRAD.search(name))
+
+
 class MusaStep:
     """Fused musa_model training step: forward -> soft-target CE -> backward -> RMSprop on one HIP
     stream with preallocated buffers (main.py's train loop body with RMSprop(lr=1e-3))."""
@@ -242,7 +254,7 @@ class MusaStep:
         # A (frozen) and the SepTemporal blocks' edge get zero gradients, which RMSprop maps to a
         # zero update (square_avg stays 0): they stay put, as torch.optim skips their None grads
         for (name, shape, off), p in zip(model.param_views(), model.parameters()):
-            if p.requires_grad:
+            if not grad_is_none(name):
                 p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
 
     def forward_backward(self, x, label, seed=None):

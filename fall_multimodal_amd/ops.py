@@ -265,9 +265,9 @@ def _mu_backward(ctx, dout, dws, dbuf, dcnt):
     (ws,) = ctx.saved_tensors
     m = _module(ctx.net)
     grads = torch.ops.fall3.musa_backward(ctx.net, list(m.parameters()), dout.float(), ws)
-    gl = _split_grads(m, grads)
-    # parameters that do not require grad (A) get None, as autograd expects
-    gl = [g if p.requires_grad else None for g, p in zip(gl, m.parameters())]
+    from .musa import grad_is_none
+    # A (frozen) and the SepTemporal edges get None, as the reference's autograd leaves them
+    gl = [None if grad_is_none(name) else g for g, (name, _, _) in zip(_split_grads(m, grads), m.param_views())]
     return None, gl, None, None, None, None, None
 
 

@@ -50,11 +50,15 @@ class RMSprop(torch.optim.Optimizer):
         sst = sq0.untyped_storage().data_ptr() if sq0 is not None else None
         sbase = sq0.storage_offset() if sq0 is not None else 0
         end = pbase
-        for p in ps:
+        for i, p in enumerate(ps):
             g = p.grad
+            # every tensor starts exactly at the previous one's end rounded up to 16 B: a larger gap
+            # could hold a tensor outside this group (another param_group, a frozen parameter), which
+            # one launch over [first, last] would update with this group's lr
             if (p.untyped_storage().data_ptr() != pst or g.untyped_storage().data_ptr() != gst
                     or not p.is_contiguous() or not g.is_contiguous() or g.shape != p.shape
-                    or p.storage_offset() < end or g.storage_offset() - gbase != p.storage_offset() - pbase):
+                    or (i > 0 and p.storage_offset() != (end + 3) // 4 * 4)
+                    or g.storage_offset() - gbase != p.storage_offset() - pbase):
                 return None
             s = self.state[p].get("square_avg")
             if (s is None) != (sq0 is None) or (s is not None and (

@@ -42,8 +42,15 @@ class GradSync:
         if t.numel():
             self._work.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
-    def start_head(self):
+    def start_head(self, after_current=False):
+        """after_current: order the bucket after everything on the caller's stream (a replayed
+        graph, whose phase 1 joined its queues) instead of after phase 1's per-queue events."""
         if self.world <= 1:
+            return
+        if after_current and self._side is not None:
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                self._reduce(self.grads[:self.split])
             return
         if self.wait_phase1 is None or self._side is None:
             self._reduce(self.grads[:self.split])
@@ -180,8 +187,9 @@ class TrainStep:
         g_head, g_tail, g_opt = self.graph
         g_head.replay()
         if g_tail is not None:
-            check(lib().f3_net_wait_phase1(self.model._native.h, stream_handle()), "wait phase 1")
-            self.sync.start_head()       # RCCL on the comm stream, concurrent with phase 2
+            # the captured phase 1 joined its queues into the capturing stream (net.cpp
+            # mark_phase1), so the head bucket is ordered after the replay itself
+            self.sync.start_head(after_current=True)  # RCCL on the comm stream, concurrent with phase 2
             g_tail.replay()
             self.sync.start_tail()
             self.sync.finish()

@@ -34,7 +34,7 @@ def _worker(rank, world, port, n, split, q):
         grads[split:] += 0.0          # "phase 2" compute touching only the tail
         sync.start_tail()
         sync.finish()
-        q.put((rank, mine, grads.clone()))
+        q.put((rank, mine.numpy(), grads.numpy().copy()))  # by value: a shared tensor dies with its sender
     finally:
         dist.destroy_process_group()
 
@@ -55,9 +55,9 @@ def test_gradsync_two_buckets_gloo(split):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    total = res[0][0] + res[1][0]
+    total = torch.from_numpy(res[0][0] + res[1][0])
     for r in range(world):
-        torch.testing.assert_close(res[r][1], total, rtol=0, atol=1e-6)
+        torch.testing.assert_close(torch.from_numpy(res[r][1]), total, rtol=0, atol=1e-6)
 
 
 def test_rmsprop_grad_scale_is_gradient_average():

@@ -47,3 +47,37 @@ def test_flat_layout_rejected():
     ps[1].grad = ps[1].grad.clone()  # a copied gradient
     opt = RMSprop(ps, lr=1e-3)
     assert opt._flat(opt.param_groups[0]) is None
+
+
+def test_flat_rejects_gap_holding_other_tensors():
+    """A gap wider than the 16-B pad may hold a tensor outside the group (a second param_group with
+    its own lr, or a frozen parameter): the flat launch would update it, so the per-tensor path runs."""
+    flat = torch.zeros(24)
+    G = torch.arange(24.)
+    a = torch.nn.Parameter(flat[0:3])
+    b = torch.nn.Parameter(flat[4:8])     # another group's tensor between a and c
+    c = torch.nn.Parameter(flat[8:11])
+    for p, (lo, hi) in ((a, (0, 3)), (b, (4, 8)), (c, (8, 11))):
+        p.grad = G[lo:hi]
+    opt = RMSprop([{"params": [a, c], "lr": 1e-3}, {"params": [b], "lr": 5e-2}])
+    assert opt._flat(opt.param_groups[0]) is None
+    assert opt._flat(opt.param_groups[1]) is not None   # one tensor: trivially flat
+    # a frozen parameter (filtered out of the optimizer) between two trainable ones
+    opt = RMSprop([p for p in (a, b, c) if p is not b], lr=1e-3)
+    assert opt._flat(opt.param_groups[0]) is None
+    # adjacent groups each covering an exact range are both flat
+    opt = RMSprop([{"params": [a, b]}, {"params": [c], "lr": 5e-2}], lr=1e-3)
+    assert opt._flat(opt.param_groups[0]) is not None and opt._flat(opt.param_groups[1]) is not None
+
+
+def test_flat_per_tensor_update_matches_torch_cpu_layout():
+    """The flat-path decision never changes the update: with two groups, every tensor gets its own
+    group's lr (checked on the layout decision alone; the update kernel is GPU-only)."""
+    flat = torch.zeros(16)
+    a = torch.nn.Parameter(flat[0:4])
+    b = torch.nn.Parameter(flat[4:8])
+    a.grad, b.grad = torch.ones(4), torch.ones(4)
+    opt = RMSprop([{"params": [a]}, {"params": [b], "lr": 0.5}], lr=1e-3)
+    fa, fb = opt._flat(opt.param_groups[0]), opt._flat(opt.param_groups[1])
+    assert fa[0].numel() == 4 and fb[0].numel() == 4
+    assert fa[0].storage_offset() == 0 and fb[0].storage_offset() == 4

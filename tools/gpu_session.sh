@@ -1,0 +1,90 @@
+#!/bin/bash
+# One GPU-box session: runs the named steps in order, each under its own time limit, output under
+# gpurun_out/. A step that FAILS (exit 1: a test or check failed) does not stop the session; a
+# step that faults, aborts or hits its limit (exit >= 124, 134, 139) ends it at once.
+#   tools/gpu_session.sh tests step_prof bench [pytest args for "tests" via PYTEST_ARGS]
+# Steps:
+#   tests       pytest -m gpu (PYTEST_ARGS overrides the selection)      -> gpurun_out/gpu_tests.log
+#   step_prof   rocprofv3 kernel trace + stats of the bench step alone  -> gpurun_out/step_kernels.txt
+#   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
+#   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches  -> gpurun_out/roof_kernels.txt
+#   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the roofline launches -> gpurun_out/roofline_pmc.json
+#   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
+#   bench_fp32  bench.py --precision fp32 --no-targcn                   -> gpurun_out/bench_fp32.json
+#   smoke       __graft_entry__.smoke()
+#   py:<file>   python <file> (a tool script)                           -> gpurun_out/<name>.log
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+rc_all=0
+run() {  # name limit cmd...
+  local name=$1 lim=$2
+  shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@"
+  local rc=$?
+  echo "== $name rc=$rc ($(date +%T))"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "== stopping: $name ended with $rc"
+    exit $rc
+  fi
+  [ $rc -ne 0 ] && rc_all=1
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests)
+      run tests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+        ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+      tail -5 gpurun_out/gpu_tests.log ;;
+    step_prof)
+      run step_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step -o run -- \
+        python tools/step_only.py 8 > gpurun_out/step_prof.log 2>&1
+      python tools/prof_summary.py gpurun_out/step/run_results.db --per-step 11 --top 60 \
+        > gpurun_out/step_kernels.txt 2>&1
+      python tools/timeline.py gpurun_out/step/run_results.db --list > gpurun_out/step_timeline.txt 2>&1
+      head -25 gpurun_out/step_kernels.txt ;;
+    step_pmc)
+      for C in FETCH_SIZE WRITE_SIZE; do
+        rm -rf gpurun_out/pmc_$C
+        run pmc_$C 120 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run -- python tools/step_only.py 2 \
+          > gpurun_out/step_pmc_$C.log 2>&1
+        db=$(find gpurun_out/pmc_$C -name "*.db" | head -1)
+        [ -n "$db" ] && [ "$db" != "gpurun_out/pmc_$C/run_results.db" ] && mv "$db" gpurun_out/pmc_$C/run_results.db
+      done
+      python tools/pmc_summary.py gpurun_out --top 60 > gpurun_out/step_hbm_traffic.txt 2>&1
+      head -30 gpurun_out/step_hbm_traffic.txt ;;
+    roof_prof)
+      run roof_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof -o run -- \
+        python tools/roofline_pmc.py run > gpurun_out/roof_prof.log 2>&1
+      python tools/prof_summary.py gpurun_out/roof/run_results.db --top 30 > gpurun_out/roof_kernels.txt 2>&1
+      head -20 gpurun_out/roof_kernels.txt ;;
+    roof_pmc)
+      for C in FETCH_SIZE WRITE_SIZE; do
+        rm -rf gpurun_out/rpmc_$C
+        run rpmc_$C 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/rpmc_$C -o run -- python tools/roofline_pmc.py run \
+          > gpurun_out/roof_pmc_$C.log 2>&1
+        db=$(find gpurun_out/rpmc_$C -name "*.db" | head -1)
+        [ -n "$db" ] && [ "$db" != "gpurun_out/rpmc_$C/run_results.db" ] && mv "$db" gpurun_out/rpmc_$C/run_results.db
+      done
+      python tools/roofline_pmc.py summarize gpurun_out > gpurun_out/roofline_pmc.json 2>&1
+      cat gpurun_out/roofline_pmc.json | head -40 ;;
+    bench)
+      run bench 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
+      cut -c1-600 gpurun_out/bench.json ;;
+    bench_fp32)
+      run bench_fp32 300 python bench.py --steps 20 --warmup 5 --precision fp32 --no-targcn --no-cpu-baseline \
+        > gpurun_out/bench_fp32.json 2> gpurun_out/bench_fp32.err
+      cut -c1-400 gpurun_out/bench_fp32.json ;;
+    smoke)
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    py:*)
+      f=${step#py:}
+      n=$(basename "$f" .py)
+      run "$n" 600 python -u $f > "gpurun_out/$n.log" 2>&1
+      tail -15 "gpurun_out/$n.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit $rc_all
