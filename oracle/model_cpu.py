@@ -306,7 +306,120 @@ def st_gcan_block(S, p, x, A_eff, cin, cout, stride, res_kind):
     return F.relu(h * a + res)
 
 
-def stgcan_stream(S, prefix, x, spec, num_class=None):
+# --------------------------------------------------------------------------
+# bf16-storage restatement (test infrastructure for the HIP path's bf16 mode)
+#
+# The reference computes in fp32 throughout; the build's bf16 mode keeps its
+# arithmetic in fp32 but STORES these tensors as bf16 (round-to-nearest-even of the fp32 value):
+#   forward : data_bn output, Z = graph mix of the block input, g = gcn output, u = relu(bn1(g)),
+#             h = tcn output, r = residual-conv output, the block output; the packed gcn / tcn /
+#             residual weights are bf16 GEMM operands;
+#   backward: dZ, dg (gcn output gradient), dv (gradient of bn1's output, after the ReLU mask),
+#             dh (tcn output gradient), dres (residual-conv output gradient).
+# BatchNorm statistics are taken from the fp32 values before rounding (GEMM epilogues), and the
+# channel-attention pool from the fp32 h; the normalised values are computed from the stored
+# (rounded) tensors. The gcn runs in the build's order (graph mix, then the 1x1 GEMM with the
+# graph-mixed bias), which is the reference's arithmetic reassociated (stgcan.py:50-56).
+# Run in fp64 this isolates the effect of the storage rounding; the HIP bf16 path is compared
+# with it per gradient tensor (tests/test_gpu_parity.py::test_bf16_storage_parity).
+# --------------------------------------------------------------------------
+def _to_bf16(t):
+    """Round through fp32 to bf16 (RNE), as a kernel rounds its fp32 result, back in t's dtype."""
+    return t.float().to(torch.bfloat16).to(t.dtype)
+
+
+class _RoundValue(torch.autograd.Function):
+    """Forward: the stored (rounded) value. Backward: the gradient passes unchanged."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return _to_bf16(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """Forward: identity. Backward: the gradient is stored as bf16."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _to_bf16(g)
+
+
+_rv, _rg = _RoundValue.apply, _RoundGrad.apply
+
+
+def _bn_split(S, stat_src, values, p):
+    """BatchNorm whose batch statistics come from `stat_src` (the unrounded tensor) applied to
+    `values` (the stored one); running statistics updated as nn.BatchNorm does."""
+    rm, rv = S[p + ".running_mean"], S[p + ".running_var"]
+    shape = [1, -1] + [1] * (values.dim() - 2)
+    if S.training:
+        dims = [0] + list(range(2, stat_src.dim()))
+        mean = stat_src.mean(dims)
+        var = stat_src.var(dims, unbiased=False)
+        n = stat_src.numel() // stat_src.shape[1]
+        with torch.no_grad():
+            rm.mul_(0.9).add_(0.1 * mean.detach().to(rm.dtype))
+            rv.mul_(0.9).add_(0.1 * (var.detach() * n / (n - 1)).to(rv.dtype))
+            S[p + ".num_batches_tracked"].add_(1)
+    else:
+        mean, var = rm, rv
+    inv = torch.rsqrt(var + 1e-5)
+    return (values - mean.view(shape)) * (inv * S[p + ".weight"]).view(shape) + S[p + ".bias"].view(shape)
+
+
+def st_gcan_block_bf16(S, p, x, A_eff, cin, cout, stride, res_kind):
+    """st_gcan block (stgcan.py:79-144) with the bf16 mode's storage rounding. `x` is the stored
+    (bf16-valued) block input. Returns (out fp32, out as stored)."""
+    N, _, T, V = x.shape
+    K = A_eff.shape[0]
+    if res_kind == "none":
+        res = 0
+    elif res_kind == "id":
+        res = x
+    else:
+        r = _rg(F.conv2d(x, _rv(S[p + "residual.0.weight"]), S[p + "residual.0.bias"], stride=(stride, 1)))
+        res = _bn_split(S, r, _rv(r), p + "residual.1")
+    # gcn: Z = graph mix of x (stored bf16, dZ bf16), g = W_bf16 . Z + graph-mixed bias
+    Z = _rv(_rg(torch.einsum("nctv,kvw->nkctw", x, A_eff)))
+    W = _rv(S[p + "gcn.conv.weight"]).view(K, cout, cin)
+    b = S[p + "gcn.conv.bias"].view(K, cout)
+    g = torch.einsum("nkitw,kci->nctw", Z, W) + torch.einsum("kc,kw->cw", b, A_eff.sum(1)).view(1, cout, 1, V)
+    g = _rg(g)
+    # tcn: u = relu(bn1(g_bf16)) stored bf16 (dv bf16), conv, h stored bf16 (dh bf16)
+    u = _rv(F.relu(_rg(_bn_split(S, g, _rv(g), p + "tcn.0"))))
+    h = _rg(F.conv2d(u, _rv(S[p + "tcn.2.weight"]), S[p + "tcn.2.bias"], stride=(stride, 1), padding=(4, 0)))
+    hn_pool = _bn_split(S, h, h, p + "tcn.3")            # the pool reads the fp32 h
+    hn = _bn_reuse(S, h, _rv(h), p + "tcn.3")
+    q = p + "channel_attention_module.atten."
+    a = F.adaptive_avg_pool2d(hn_pool, (1, 1))
+    a = F.conv2d(a, S[q + "1.weight"], S[q + "1.bias"])
+    a = F.relu(S.bn(a, q + "2"))
+    a = torch.sigmoid(F.conv2d(a, S[q + "4.weight"], S[q + "4.bias"]))
+    out = F.relu(hn * a + res)
+    return out, _rv(out)
+
+
+def _bn_reuse(S, stat_src, values, p):
+    """The same BatchNorm applied a second time in one forward (no second running-stat update)."""
+    shape = [1, -1] + [1] * (values.dim() - 2)
+    if S.training:
+        dims = [0] + list(range(2, stat_src.dim()))
+        mean, var = stat_src.mean(dims), stat_src.var(dims, unbiased=False)
+    else:
+        mean, var = S[p + ".running_mean"], S[p + ".running_var"]
+    inv = torch.rsqrt(var + 1e-5)
+    return (values - mean.view(shape)) * (inv * S[p + ".weight"]).view(shape) + S[p + ".bias"].view(shape)
+
+
+def stgcan_stream(S, prefix, x, spec, num_class=None, storage="fp32"):
     layers = "st_gcn_networks" if spec.naming == "notebook" else "st_gcan_networks"
     N, C, T, V = x.shape
     # data_bn over V*C channels, V-major (stgcan.py:213-218)
@@ -314,10 +427,18 @@ def stgcan_stream(S, prefix, x, spec, num_class=None):
     z = S.bn(z, prefix + "data_bn")
     x = z.view(N, V, C, T).permute(0, 2, 3, 1).contiguous()
     A = S[prefix + "A"]
-    for i, (ci, co, s, res) in enumerate(STREAM_CHANNELS):
-        ci = C if ci is None else ci
-        A_eff = A * S[f"{prefix}edge_importance.{i}"]
-        x = st_gcan_block(S, f"{prefix}{layers}.{i}.", x, A_eff, ci, co, s, res)
+    if storage == "bf16":
+        x = _rv(x)
+        for i, (ci, co, s, res) in enumerate(STREAM_CHANNELS):
+            ci = C if ci is None else ci
+            A_eff = A * S[f"{prefix}edge_importance.{i}"]
+            out, x = st_gcan_block_bf16(S, f"{prefix}{layers}.{i}.", x, A_eff, ci, co, s, res)
+        x = out  # the pool reads the fp32 block output
+    else:
+        for i, (ci, co, s, res) in enumerate(STREAM_CHANNELS):
+            ci = C if ci is None else ci
+            A_eff = A * S[f"{prefix}edge_importance.{i}"]
+            x = st_gcan_block(S, f"{prefix}{layers}.{i}.", x, A_eff, ci, co, s, res)
     x = F.avg_pool2d(x, x.shape[2:])
     if num_class is not None:
         x = F.conv2d(x, S[prefix + "cls.weight"], S[prefix + "cls.bias"])
@@ -365,18 +486,19 @@ def cnn1d(S, p, x):
     return z.permute(0, 2, 1)
 
 
-def forward(st, spec: Spec, skel, sensor=None, training=True):
-    """Returns the module output (logits, or softmax for the notebook form)."""
+def forward(st, spec: Spec, skel, sensor=None, training=True, storage="fp32"):
+    """Returns the module output (logits, or softmax for the notebook form). storage="bf16":
+    the skeleton streams with the build's bf16-mode storage rounding (st_gcan_block_bf16)."""
     S = _State(st, training)
     if spec.model == "stgcn":
-        return stgcan_stream(S, "", skel, spec, spec.num_class)
+        return stgcan_stream(S, "", skel, spec, spec.num_class, storage)
     if spec.model == "bilstm":
         if spec.sensor == "cnn_bilstm":
             return bilstm_head(S, "bilstm.", cnn1d(S, "cnn.", sensor))
         return bilstm_head(S, "", sensor)
     p1, p2, ps, pf = prefixes(spec)
     mot = skel[:, :2, 1:] - skel[:, :2, :-1]  # combination.py:39
-    feats = [stgcan_stream(S, p1, skel, spec), stgcan_stream(S, p2, mot, spec)]
+    feats = [stgcan_stream(S, p1, skel, spec, storage=storage), stgcan_stream(S, p2, mot, spec, storage=storage)]
     if spec.model == "two_stgcan_bilstm":
         if spec.sensor == "cnn_bilstm":
             feats.append(bilstm_head(S, ps + "bilstm.", cnn1d(S, ps + "cnn.", sensor)))
@@ -401,7 +523,7 @@ def rmsprop_step(params, grads, sq, lr=1e-3, alpha=0.99, eps=1e-8):
         params[k].addcdiv_(g, sq[k].sqrt().add_(eps), value=-lr)
 
 
-def train_step(st, spec, skel, sensor, label, lr=1e-3, sq=None):
+def train_step(st, spec, skel, sensor, label, lr=1e-3, sq=None, storage="fp32"):
     """One reference training step: forward -> CE -> backward -> RMSprop.
 
     Mutates `st` (params updated, BN running stats updated). Returns
@@ -410,7 +532,7 @@ def train_step(st, spec, skel, sensor, label, lr=1e-3, sq=None):
     names = [k for k in st if not is_buffer(k)]
     for k in names:
         st[k] = st[k].detach().clone().requires_grad_(True)
-    out = forward(st, spec, skel, sensor, training=True)
+    out = forward(st, spec, skel, sensor, training=True, storage=storage)
     loss = soft_ce(out, label)
     gl = torch.autograd.grad(loss, [st[k] for k in names], allow_unused=True)
     # unused parameters (CNN1D.fc, GSTCAN_UR_conv.ipynb cell 2) get no gradient: RMSprop skips them
