@@ -511,6 +511,39 @@ def loader_bench(model, dev, B=256, V=18, S=6, C=11, n=20480):
                     "then feeding TrainStep batch by batch"}
 
 
+# The reference's own code timed on CPU: a reported, non-target figure
+REFERENCE_CPU = {"value": 77.4, "unit": "clips/s", "cores": 8, "kind": "reference",
+                 "sample": "reference TwoStreamSTGCAN_BiLSTM (HAR V=14, S=15, 11 classes) fwd+bwd+RMSprop at B=256, "
+                           "torch CPU fp32, 3.308 s/step, timed in the survey container (BASELINE.md 2a)"}
+
+
+def fp32_mode_bench(dev, a, V, S, C, sk, se, lb, steps=10, warmup=3):
+    """The parity mode's throughput: the same step with every GEMM on fp32 MFMA and fp32 activations
+    (logits within 1e-3 of the reference, identical argmax; tests/test_gpu_parity.py), same config."""
+    import fall_multimodal_amd as f3
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev,
+                                      precision="fp32")
+    step = f3.TrainStep(model, sk.shape[0], lr=1e-3)
+    for _ in range(warmup):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(sk, se, lb)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    B = sk.shape[0]
+    fl = FLOP_PER_CLIP.get((V, S))
+    res = {"ms_per_step": round(dt * 1e3, 3), "clips_per_s": round(B / dt, 1), "steps": steps, "dtype": "fp32",
+           "note": "parity mode: fp32 MFMA GEMMs (v_mfma_f32_16x16x4_f32), fp32 activations; logits within 1e-3 of "
+                   "the reference CPU run with identical argmax"}
+    if fl:
+        res["step_mfma_frac_of_fp32_peak"] = round(B * fl / dt / 1e12 / PEAK_MFMA_TFLOPS["fp32"], 4)
+    del step, model
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_threads():
     """The CPU share this process may use: OMP_NUM_THREADS (16 on the GPU box, whose nproc shows
     the whole machine), else every core here."""
@@ -621,6 +654,7 @@ def main():
         phased = {"ms_per_step": round(pm, 3), "vs_phase0": round(pm / (dt / a.steps * 1e3), 4),
                   "note": "backward as phase 1 (head, sensor, layers 4-6) + phase 2 (layers 0-3), the DP path "
                           "without the collective; phase 0 = the one-pass backward the N=1 value uses"}
+    fp32m = fp32_mode_bench(dev, a, V, S, C, sk, se, lb) if (rank == 0 and world == 1 and a.precision == "bf16") else None
     ev = eval_throughput(model, sk, se) if rank == 0 else None
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
@@ -667,7 +701,9 @@ def main():
             "cfg2_targcn": tgrec,
             "cfg5_sktr": skrec,
             "musa_model": murec,
+            "fp32_mode": fp32m,
             "cpu_baseline": cpu,
+            "reference_cpu_published": REFERENCE_CPU,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -1106,6 +1106,192 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// wgrad_seg<NKS, S>: wgrad_taps' tap reuse for every (9,1) tcn layer, not only the clips that fit
+// one staged window. A work unit is (clip, segment of kSegFrames = 8 output frames); output frame
+// t, tap dt reads input frame S*t + dt - 4, so a unit stages
+//   dY rows of output frames [t0, t0 + 8)                      -> Y rows [0, 8V)
+//   S = 1: input frames t0-4 .. t0+11 (real halo frames of the same clip)  -> X rows [0, 16V);
+//          tap dt reads X row m + dt*V (m = dY row within the unit)
+//   S = 2: the input frames de-interleaved by parity: even frames 2t0-4, 2t0-2, ... -> E rows,
+//          odd frames 2t0-3, 2t0-1, ... -> O rows (12 frames each); tap dt reads E row
+//          m + (dt/2)*V (dt even) or O row m + ((dt-1)/2)*V (dt odd): a uniform row shift again.
+// Rows outside the clip (frame < 0 or >= T) and the dY rows past a short last segment are DMA'd
+// from the zero page, so no unit sees another unit's rows and no masking is needed. Fragments,
+// waves, the MFMA schedule (all reads unconditional, nothing but address arithmetic and MFMAs
+// between a read and its wait), the bias column and the slab format are wgrad_taps'.
+// Needs: bf16 operands, forward geometry, KT = 9, P = 4, S in {1, 2}, V even, V <= 18,
+// 8V % 8 == 0, roundup(8V, 32) == 32*NKS, Nc % 64 == 0, Kc % 64 == 0.
+// ----------------------------------------------------------------------------
+constexpr int kSegFrames = 8;
+
+template <int NKS, int S>
+__global__ __launch_bounds__(512) void wgrad_seg(WgradArgs a) {
+  constexpr int R = 128;                                      // row bytes of every region (64 bf16)
+  constexpr int TVP = 32 * NKS;                               // padded dY rows of a unit
+  constexpr int VMAX = 18;
+  constexpr int NREG = S == 1 ? 1 : 2;                        // input regions (X, or E and O)
+  constexpr int RR = S == 1 ? TVP + 8 * VMAX : TVP + 4 * VMAX;  // rows of one input region
+  constexpr int Y_BYTES = TVP * R, STAGE = Y_BYTES + NREG * RR * R;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int V = g.V, SV = kSegFrames * V;
+  const int nseg = (g.T_out + kSegFrames - 1) / kSegFrames;
+  const int jt = g.Nc / 64, tiles = jt * (g.Kc / 64);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a split's tiles stay on one XCD
+  const int bz = lin / tiles, tile = lin - bz * tiles;
+  const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
+  const int nunits = g.M / (g.T_out * V) * nseg;
+  const int u_begin = bz * a.rows_per_split;                // rows_per_split holds units per split
+  const int u_end = min(nunits, u_begin + a.rows_per_split);
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const __bf16* zp = reinterpret_cast<const __bf16*>(a.zero);
+  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+
+  // ---- staging: 1-KiB pieces (8 rows); a lane's rows are fixed, their source frame per unit ----
+  const int xrows = (S == 1 ? kSegFrames + 8 : kSegFrames + 4) * V;
+  const int npy = SV / 8, npx = xrows / 8, np = npy + NREG * npx, ppw = (np + 7) / 8;
+  const int sub = lane >> 3, ph = lane & 7;
+  constexpr int PPW_MAX = (TVP / 8 + NREG * (RR / 8) + 7) / 8;
+  unsigned ldso[PPW_MAX];
+  long long rowoff[PPW_MAX];  // source offset from the unit's first dY row / first input frame
+  int rfr[PPW_MAX];           // the row's frame offset within the unit's window
+  bool isy[PPW_MAX];
+#pragma unroll
+  for (int k = 0; k < PPW_MAX; ++k) {
+    int piece = k * 8 + wave;
+    if (piece >= np) piece %= np;  // the last round re-issues earlier pieces: same bytes, same place
+    const bool y = piece < npy;
+    const int q = piece - npy, kd = y ? 0 : 1 + (q >= npx);   // 0 dY, 1 X / E, 2 O
+    const int pr = y ? piece : q - (kd - 1) * npx;
+    const int crow = pr * 8 + sub;                            // row within its region
+    const int qf = crow / V, vv = crow - qf * V;
+    const int u = (ph >> 1) ^ wswz<4>(crow);
+    const int col = (u * 2 + (ph & 1)) * 8;
+    isy[k] = y;
+    ldso[k] = (unsigned)((y ? 0 : Y_BYTES + (kd - 1) * RR * R) + crow * R + ph * 16);
+    rfr[k] = y ? qf : S * qf + (kd - 1);
+    rowoff[k] = y ? (long long)crow * a.ldy + j0 + col : (long long)(rfr[k] * V + vv) * g.lda + i0 + col;
+  }
+  auto stage = [&](int unit, int buf) {
+    const int n = unit / nseg, t0 = (unit - n * nseg) * kSegFrames, fb = S * t0 - 4;
+    const __bf16* yb = dyb + ((long long)n * g.T_out + t0) * V * a.ldy;
+    const __bf16* xbase = xb + ((long long)n * g.T_in + fb) * V * g.lda;  // dereferenced only in range
+#pragma unroll
+    for (int k = 0; k < PPW_MAX; ++k) {
+      if (k < ppw) {
+        const int f = isy[k] ? t0 + rfr[k] : fb + rfr[k];
+        const bool ok = isy[k] ? f < g.T_out : (f >= 0 && f < g.T_in);
+        const __bf16* src = ok ? (isy[k] ? yb : xbase) + rowoff[k] : zp;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (lds_void_t*)(size_t)(lds0 + buf * STAGE + ldso[k] - lane * 16), 16, 0, 0);
+      }
+    }
+  };
+
+  // ---- fragment lanes (wgrad_taps') ----
+  const int wi = wave & 3, kh = wave >> 2;
+  const int ntap = kh == 0 ? 5 : 4, dt0 = kh * 5;
+  const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
+  const int r0 = 8 * fg + tq;
+  const int fa = wswz<4>(r0);
+  unsigned offa[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) offa[x] = r0 * R + ((x ^ fa) * 32) + tp * 8;
+  unsigned offl[5], offh[5];
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt) {
+    const int dt = dt0 + min(tt, ntap - 1);
+    const int reg = S == 1 ? 0 : (dt & 1), sh = S == 1 ? dt : (dt >> 1);
+    const int rl = r0 + sh * V, rh = rl + 4;
+    const unsigned rb = Y_BYTES + reg * RR * R;
+    offl[tt] = rb + rl * R + ((wi ^ wswz<4>(rl)) * 32) + tp * 8;
+    offh[tt] = rb + rh * R + ((wi ^ wswz<4>(rh)) * 32) + tp * 8;
+  }
+
+  f32x4 acc[5][4];
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[tt][x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const unsigned ones_m = kh ? 0xffffffffu : 0u;
+  const u32x4_t ones_v = {0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m};
+  const u32x4_t keep_v = {~ones_m, ~ones_m, ~ones_m, ~ones_m};
+
+  const int nst = u_end - u_begin;
+  if (nst > 0) stage(u_begin, 0);
+  // zero the rows no unit ever stages (dY padding past 8V; each input region past its staged
+  // rows), in both buffers, while the first unit's DMA is in flight (disjoint bytes)
+  for (int b = 0; b < 2; ++b) {
+    for (int o = SV * R + tid * 16; o < Y_BYTES; o += 512 * 16)
+      *reinterpret_cast<f32x4*>(smem + b * STAGE + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < NREG; ++r)
+      for (int o = xrows * R + tid * 16; o < RR * R; o += 512 * 16)
+        *reinterpret_cast<f32x4*>(smem + b * STAGE + Y_BYTES + r * RR * R + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nst; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nst) stage(u_begin + t + 1, buf ^ 1);
+    const unsigned base = lds0 + buf * STAGE;
+    s16x4_t lo[2][9], hi[2][9];
+    auto issue = [&](int ks, s16x4_t (&l)[9], s16x4_t (&h)[9]) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const unsigned p = base + offa[x] + ks * 32 * R;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[x]) : "v"(p));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(h[x]) : "v"(p), "n"(4 * R));
+      }
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[4 + tt]) : "v"(base + offl[tt] + ks * 32 * R));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(h[4 + tt]) : "v"(base + offh[tt] + ks * 32 * R));
+      }
+    };
+    issue(0, lo[0], hi[0]);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int c = ks & 1;
+      tr_wait(lo[c], hi[c]);
+      bf16x8 fa_[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        fa_[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][x], hi[c][x], 0, 1, 2, 3, 4, 5, 6, 7));
+      bf16x8 fbs[5];
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt)
+        fbs[tt] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
+      fbs[4] = __builtin_bit_cast(bf16x8, (__builtin_bit_cast(u32x4_t, fbs[4]) & keep_v) | ones_v);
+      if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fbs[tt], acc[tt][x]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (a.db && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomic_add_f(a.db + j0 + x * 16 + fg * 4 + r, acc[4][x][r]);
+  }
+  f32x4* slab = reinterpret_cast<f32x4*>(a.slab) + ((size_t)(bz * tiles + tile) * 4 + wi) * 9 * 4 * 64 + lane;
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt) {
+    if (tt < ntap) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) slab[((dt0 + tt) * 4 + x) * 64] = acc[tt][x];
+    }
+  }
+}
+
 // dw_ref[j][i][dt] += sum_s (wgrad_taps' fragment-order slab). Workgroup = one (tile, wi, x)
 // block: 16 co x 16 ci x 9 taps. Wave dt, lane L sums the 16-B piece [dt][x][L] over the splits
 // (each load a contiguous KiB per wave, 8 in flight), drops its 4 values into an LDS image
@@ -1167,6 +1353,50 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const dim3 grid(tiles * splits);
   if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
+  F3_LAUNCH_CHECK();
+  if (a.dw_ref) {
+    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
+                       a.dw_ref);
+    F3_LAUNCH_CHECK();
+  }
+  return F3_OK;
+}
+
+// wgrad_seg applies (see its comment): its NKS (4 or 5), 0 if not. F3_WGRAD_SEG: bit 0 stride-1
+// layers, bit 1 stride-2 layers (default both).
+static int wgrad_seg_nks(const WgradArgs& a) {
+  static const int on = getenv("F3_WGRAD_SEG") ? atoi(getenv("F3_WGRAD_SEG")) : 3;
+  const ConvGeom& g = a.g;
+  if (!a.dyb || !a.inb || !a.slab || !a.zero || a.outmap != WG_OUT_CONV || a.groups > 1 || g.transposed) return 0;
+  if (g.KT != 9 || g.P != 4 || (g.S != 1 && g.S != 2) || !((on >> (g.S - 1)) & 1)) return 0;
+  if (g.T_out != (g.T_in + 2 * g.P - g.KT) / g.S + 1) return 0;
+  if (g.V % 2 || g.V > 18 || g.Nc % 64 || g.Kc % 64 || a.ldy % 8 || g.lda % 8) return 0;
+  const int SV = kSegFrames * g.V;
+  if (SV % 8 || g.M % (g.T_out * g.V)) return 0;
+  const int nks = (SV + 31) / 32;
+  return nks == 4 || nks == 5 ? nks : 0;
+}
+
+static int launch_wgrad_seg(WgradArgs a, int nks, hipStream_t s) {
+  const int nseg = (a.g.T_out + kSegFrames - 1) / kSegFrames;
+  const int units = a.g.M / (a.g.T_out * a.g.V) * nseg;
+  const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
+  const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
+  static const int target = getenv("F3_SEG_WGS") ? atoi(getenv("F3_SEG_WGS")) : 256;  // one per CU
+  int splits = std::max(1, std::min(units, target / tiles));
+  splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
+  if (splits < 1) return F3_EINVAL;
+  const int ups = (units + splits - 1) / splits;
+  splits = (units + ups - 1) / ups;
+  a.rows_per_split = ups;  // units per split
+  const dim3 grid(tiles * splits);
+  if (a.g.S == 1) {
+    if (nks == 5) hipLaunchKernelGGL((wgrad_seg<5, 1>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_seg<4, 1>), grid, dim3(512), 0, s, a);
+  } else {
+    if (nks == 5) hipLaunchKernelGGL((wgrad_seg<5, 2>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_seg<4, 2>), grid, dim3(512), 0, s, a);
+  }
   F3_LAUNCH_CHECK();
   if (a.dw_ref) {
     hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
@@ -1244,6 +1474,8 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   if (taps_env && bigv) {
     const int nks = wgrad_taps_nks(a);
     if (nks) return launch_wgrad_taps(a, nks, s);
+    const int nseg = wgrad_seg_nks(a);  // every other (9,1) layer: clip segments, stride 2 by parity
+    if (nseg) return launch_wgrad_seg(a, nseg, s);
   }
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is

@@ -323,8 +323,22 @@ def st_gcan_block(S, p, x, A_eff, cin, cout, stride, res_kind):
 # Run in fp64 this isolates the effect of the storage rounding; the HIP bf16 path is compared
 # with it per gradient tensor (tests/test_gpu_parity.py::test_bf16_storage_parity).
 # --------------------------------------------------------------------------
+_JITTER = {"eps": 0.0, "gen": None}
+
+
+def storage_jitter(eps, seed):
+    """Relative noise `eps` applied to every value just before it is rounded to bf16 (eps=0: off).
+    eps ~ 2^-23 stands in for another valid fp32 evaluation order: it moves a value across a bf16
+    rounding boundary exactly where a different fp32 accumulation would. The spread of gradients
+    over such runs is the restatement's own envelope for the bf16 mode (test_bf16_storage_parity)."""
+    _JITTER["eps"] = float(eps)
+    _JITTER["gen"] = torch.Generator().manual_seed(int(seed)) if eps else None
+
+
 def _to_bf16(t):
     """Round through fp32 to bf16 (RNE), as a kernel rounds its fp32 result, back in t's dtype."""
+    if _JITTER["eps"]:
+        t = t * (1 + _JITTER["eps"] * torch.randn(t.shape, generator=_JITTER["gen"], dtype=t.dtype))
     return t.float().to(torch.bfloat16).to(t.dtype)
 
 

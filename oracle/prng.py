@@ -50,7 +50,7 @@ def param_value(name: str, shape, seed: int) -> np.ndarray:
 
 def synthetic_batch(batch: int, num_node: int, num_class: int, sensor_dim: int,
                     seed: int, frames: int = 30, sensor_frames: int | None = None,
-                    center: int | None = None):
+                    center: int | None = None, separation: float = 0.8, spread: float = 0.5):
     """Synthetic clip batch in the reference's loader format.
 
     skel  f32[N,3,T,V]: x,y ~ U(-1,1) (post scale_pose range,
@@ -60,7 +60,9 @@ def synthetic_batch(batch: int, num_node: int, num_class: int, sensor_dim: int,
     sensor f32[N,Ts,S]: N(0,0.5^2) + 1.0 on every third axis (gravity).
     label f32[N,C]: smoothed one-hot (eps 0.1) scaled by a score in U(0.5,1) —
           rows do not sum to 1 (har_create4_sensor.py:99-101,128-136).
-    A class-conditional shift on joints 0..3 makes the data separable.
+    A class-conditional shift on joints 0..3 makes the data separable: x of those joints is
+    spread * U(-1,1) + (cls/(C-1) - 1/2) * separation (defaults: the bench / parity data;
+    the convergence test uses a wider separation so training reaches a plateau quickly).
     """
     rng = np.random.default_rng([int(seed), 0xC11B5])
     ts = frames if sensor_frames is None else sensor_frames
@@ -68,8 +70,8 @@ def synthetic_batch(batch: int, num_node: int, num_class: int, sensor_dim: int,
     skel = np.empty((batch, 3, frames, num_node), np.float32)
     skel[:, :2] = rng.uniform(-1, 1, size=(batch, 2, frames, num_node))
     skel[:, 2] = rng.uniform(0.3, 1.0, size=(batch, frames, num_node))
-    shift = (cls[:, None, None].astype(np.float32) / max(num_class - 1, 1) - 0.5) * 0.8
-    skel[:, 0, :, :4] = np.clip(skel[:, 0, :, :4] * 0.5 + shift, -1, 1)
+    shift = (cls[:, None, None].astype(np.float32) / max(num_class - 1, 1) - 0.5) * np.float32(separation)
+    skel[:, 0, :, :4] = np.clip(skel[:, 0, :, :4] * np.float32(spread) + shift, -1, 1)
     if center is None:
         center = num_node - 1
     if num_node == 14:

@@ -97,7 +97,10 @@ CONV_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 
                (2, 30, 14, 9, 64, 1, 1, 0), (2, 30, 18, 64, 192, 1, 1, 0), (3, 30, 18, 192, 64, 1, 1, 0),
                (2, 15, 14, 256, 128, 9, 1, 4), (2, 15, 18, 128, 128, 9, 1, 4),
                # the tap-reuse weight gradient (wgrad_taps): T*V = 144 (5 k steps, 16 splits) and 112 (4)
-               (40, 8, 18, 256, 256, 9, 1, 4), (5, 8, 14, 128, 64, 9, 1, 4)]
+               (40, 8, 18, 256, 256, 9, 1, 4), (5, 8, 14, 128, 64, 9, 1, 4),
+               # its clip-segment / stride-2 form (wgrad_seg): the motion stream's T = 29 layers,
+               # layer 5's 15 -> 8 stride 2 at V = 18, and enough clips for multi-unit splits
+               (6, 29, 18, 64, 64, 9, 1, 4), (3, 15, 18, 256, 256, 9, 2, 4), (12, 30, 18, 64, 64, 9, 1, 4)]
 
 
 @pytest.mark.parametrize("precision", PRECISIONS, ids=PREC_IDS)
@@ -644,21 +647,34 @@ BF16_CFG3_LOGIT_GATE = 9e-3
 BF16_CFG3_COS_GATE = 0.993
 
 
+def _progress(msg):
+    """A line in gpurun_out/progress.log for long oracle runs (shows the box the run is alive)."""
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "progress.log"), "a") as f:
+        f.write(msg + "\n")
+
+
 def test_bf16_storage_parity():
     """The benchmarked bf16 step (TrainStep, B=256, V=18, S=6) gated PER GRADIENT TENSOR against
-    the oracle's bf16-storage restatement (oracle/model_cpu.py st_gcan_block_bf16: the same
-    tensors rounded to bf16 where the kernels store them, arithmetic in fp64).
+    the oracle's bf16-storage restatement (oracle/model_cpu.py st_gcan_block_bf16: the tensors the
+    kernels store in bf16 rounded at the same points, arithmetic in fp64).
 
-    Against the plain fp64 oracle the bf16 step's worst per-tensor error is ~0.4 of the tensor's
-    max (e.g. edge_importance, data_bn.weight; profiles/r02_parity_record.jsonl). The restatement
-    shows where that comes from: the same rounding alone moves those tensors as far (e_emu64), it
-    is the forward activations' rounding (gradient-storage rounding alone: <= 0.012 of max at
-    B=64), and the train-mode BatchNorms amplify it. Against the restatement the HIP path is
-    within ~a tenth of that, the residue of fp32-vs-fp64 arithmetic flipping the rounding of a
-    few elements. Gates (per tensor, biases feeding a train-mode BN on the cosine only):
-      e_hip_emu <= 0.25 * e_emu64 + 0.01 and e_hip_emu <= 0.1 (the HIP path is the restatement),
-      e_hip64   <= 1.5 * e_emu64 + 0.02          (the error vs fp64 is the storage rounding),
-      logits within 1.5e-3 of the restatement, identical argmax, gradient cosine >= 0.9995."""
+    What the restatement shows (profiles/r03_parity_record.jsonl): the bf16 step's per-tensor
+    gradient errors against the plain fp64 oracle (worst ~0.4 of the tensor's max, e.g.
+    edge_importance / data_bn.weight in round 2) are the storage rounding itself — the restatement
+    moves as far from fp64 (median 0.11, worst 0.4 at B=256), almost all of it from rounding the
+    forward activations (rounding only the stored gradients: <= 0.012 at B=64). And the bf16-mode
+    gradient is CHAOTIC at the rounding boundaries: perturbing every value by 2^-24 (half an fp32
+    ulp) before it is rounded — what any other valid fp32 summation order does — moves the
+    restatement's own gradients by a median 0.1 of max and its logits by ~1.7e-3 (train-mode BNs
+    amplify the 1-ulp bf16 flips). A per-tensor bound tighter than that envelope cannot hold for
+    any fp32 implementation of this step, so the gate is the envelope, measured per tensor from
+    two jittered restatement runs (env):
+      |g_hip - g_storage| / max|g_storage| <= 2.5 env + 0.02     for every gradient tensor,
+      logits within 2.5x the envelope's logit spread, identical argmax,
+      gradient cosine >= 1 - 2.5 (1 - the envelope's worst cosine),
+      |g_hip - g_fp64| <= |g_storage - g_fp64| + 2.5 env + 0.02 (the error vs fp64 IS the rounding).
+    Biases feeding a train-mode BN (true gradient ~0) are on the cosine only."""
     d = dev()
     import fall_multimodal_amd as f3
     torch.set_num_threads(min(32, os.cpu_count() or 1))
@@ -676,34 +692,58 @@ def test_bf16_storage_parity():
     def d64():
         return {k: (v.double() if v.dtype == torch.float32 else v.clone()) for k, v in st.items()}
     x64 = [torch.from_numpy(x).double() for x in batch]
+    _progress("bf16_storage_parity: storage oracle")
     out_e, loss_e, g_e = oc.train_step(d64(), spec, *x64, storage="bf16")
+    _progress("bf16_storage_parity: fp64 oracle")
     out_64, _, g_64 = oc.train_step(d64(), spec, *x64)
-    rel_e, cos = _flat_grad_errors(model, g_e)
-    rel_64, _ = _flat_grad_errors(model, g_64)
-    e_emu64 = {n: float((g_e[n] - g_64[n]).abs().max() / g_64[n].abs().max()) for n in rel_64}
-    names = [n for n in rel_e if not n.endswith(_ZERO_GRAD)]
+    names = [n for n in g_e if not n.endswith(_ZERO_GRAD) and float(g_e[n].abs().max()) > 0]
+
+    def rel(a, b):
+        return {n: float((a[n] - b[n]).abs().max() / b[n].abs().max()) for n in names}
+
+    def cosine(a, b):
+        x = torch.cat([a[n].reshape(-1) for n in g_e])
+        y = torch.cat([b[n].reshape(-1) for n in g_e])
+        return float(x @ y / (x.norm() * y.norm()))
+    env, env_logit, env_cos = {n: 0.0 for n in names}, 0.0, 1.0
+    for seed in (1, 2):
+        _progress(f"bf16_storage_parity: jittered storage oracle {seed}")
+        oc.storage_jitter(2.0 ** -24, seed)
+        try:
+            out_j, _, g_j = oc.train_step(d64(), spec, *x64, storage="bf16")
+        finally:
+            oc.storage_jitter(0.0, 0)
+        r = rel(g_j, g_e)
+        env = {n: max(env[n], r[n]) for n in names}
+        env_logit = max(env_logit, float((out_j - out_e).abs().max()))
+        env_cos = min(env_cos, cosine(g_j, g_e))
+    ours = {n: p.grad.detach().cpu().double() for n, p in model.named_parameters()}
+    rel_e, rel_64, e_emu64 = rel(ours, g_e), rel(ours, g_64), rel(g_e, g_64)
+    cos = cosine(ours, g_e)
     dlog = float((out - out_e).abs().max())
     agree = float((out.argmax(1) == out_e.argmax(1)).double().mean())
-    worst_e = max(names, key=lambda n: rel_e[n] / (0.25 * e_emu64[n] + 0.01))
-    worst_64 = max(names, key=lambda n: rel_64[n] / (1.5 * e_emu64[n] + 0.02))
+    ratio = {n: rel_e[n] / (2.5 * env[n] + 0.02) for n in names}
+    worst = max(names, key=ratio.get)
     rec = {"precision": "bf16", "B": B, "max_abs_dlogit_vs_storage_oracle": dlog,
+           "envelope_dlogit": env_logit, "envelope_cosine": env_cos,
            "max_abs_dlogit_storage_oracle_vs_fp64": float((out_e - out_64).abs().max()),
            "max_abs_dlogit_vs_fp64": float((out - out_64).abs().max()), "argmax_agreement": agree,
            "grad_cosine_vs_storage_oracle": cos, "loss": float(step.loss.item()), "loss_storage_oracle": float(loss_e),
-           "worst_hip_vs_storage": [worst_e, rel_e[worst_e], e_emu64[worst_e]],
-           "worst_hip_vs_fp64": [worst_64, rel_64[worst_64], e_emu64[worst_64]],
+           "worst_ratio_to_gate": [worst, ratio[worst], rel_e[worst], env[worst]],
            "median_hip_vs_storage": float(np.median([rel_e[n] for n in names])),
+           "median_envelope": float(np.median([env[n] for n in names])),
            "median_storage_vs_fp64": float(np.median([e_emu64[n] for n in names])),
            "median_hip_vs_fp64": float(np.median([rel_64[n] for n in names])),
-           "per_tensor": {n: [round(rel_e[n], 5), round(rel_64[n], 5), round(e_emu64[n], 5)] for n in names}}
+           "per_tensor_hip_vs_storage_hip_vs_fp64_storage_vs_fp64_envelope": {
+               n: [round(rel_e[n], 5), round(rel_64[n], 5), round(e_emu64[n], 5), round(env[n], 5)] for n in names}}
     _record("bf16_storage_parity", rec)
-    print({k: v for k, v in rec.items() if k != "per_tensor"})
-    assert dlog < 1.5e-3 and agree == 1.0, (dlog, agree)
-    assert cos >= 0.9995, cos
+    print({k: v for k, v in rec.items() if not k.startswith("per_tensor")})
+    assert dlog <= 2.5 * env_logit and agree == 1.0, (dlog, env_logit, agree)
+    assert cos >= 1 - 2.5 * (1 - env_cos), (cos, env_cos)
     assert abs(float(step.loss.item()) - float(loss_e)) < 5e-4
     for n in names:
-        assert rel_e[n] <= min(0.25 * e_emu64[n] + 0.01, 0.1), (n, rel_e[n], e_emu64[n])
-        assert rel_64[n] <= 1.5 * e_emu64[n] + 0.02, (n, rel_64[n], e_emu64[n])
+        assert rel_e[n] <= 2.5 * env[n] + 0.02, (n, rel_e[n], env[n])
+        assert rel_64[n] <= e_emu64[n] + 2.5 * env[n] + 0.02, (n, rel_64[n], e_emu64[n], env[n])
 
 
 def test_cfg3_two_stream_bf16_parity():

@@ -11,6 +11,7 @@
 #   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the roofline launches -> gpurun_out/roofline_pmc.json
 #   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
 #   bench_fp32  bench.py --precision fp32 --no-targcn                   -> gpurun_out/bench_fp32.json
+#   ab          tools/ab.sh env $AB_CFGS (eager bench A/B, optional serial profiles) -> gpurun_out/ab.log
 #   smoke       __graft_entry__.smoke()
 #   py:<file>   python <file> (a tool script)                           -> gpurun_out/<name>.log
 set -o pipefail
@@ -77,6 +78,9 @@ for step in "$@"; do
       run bench_fp32 300 python bench.py --steps 20 --warmup 5 --precision fp32 --no-targcn --no-cpu-baseline \
         > gpurun_out/bench_fp32.json 2> gpurun_out/bench_fp32.err
       cut -c1-400 gpurun_out/bench_fp32.json ;;
+    ab)   # eager bench A/B over AB_CFGS (tools/ab.sh env; SERIAL_PROF / PAT / ROUNDS pass through)
+      run ab 900 bash tools/ab.sh env ${AB_CFGS:--} > gpurun_out/ab.log 2>&1
+      grep -E "ms/step|==" gpurun_out/ab.log | head -40 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     py:*)
