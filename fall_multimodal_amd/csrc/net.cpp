@@ -647,7 +647,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
 }
 
 // debugging aid: F3_DEBUG_BWD_STOP="stream,layer" ends the backward right after that
-// layer's tcn input-gradient so its scratch tensors can be inspected (tools/diag_layer.py)
+// layer's tcn input-gradient so its scratch tensors can be inspected (f3_net_debug_tensor)
 bool debug_stop(int si, int l) {
   static const char* e = getenv("F3_DEBUG_BWD_STOP");
   if (!e) return false;
@@ -1197,7 +1197,7 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
       for (int si = 0; si < net->nstreams; ++si) {
         F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], side_of(si, l), l_hi,
                                defer ? 1 : 3));
-        if (debug_stop(si, l)) return F3_OK;  // tools/diag_layer.py: leave the scratch as is
+        if (debug_stop(si, l)) return F3_OK;  // leave the scratch as is for f3_net_debug_tensor
       }
       if (defer && l < l_hi)
         for (int si = 0; si < net->nstreams; ++si)
