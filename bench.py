@@ -353,12 +353,13 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
     step = f3.TargcnStep(model, B, lr=1e-5)
     x, y = torch.from_numpy(src).to(dev), torch.from_numpy(lab).to(dev)
     dt, world = replica_seconds(lambda: step(x, y), steps, warmup)
+    stages = targcn_stage_times(model, step, x, y, B, V, precision)
     rec = {"metric": "clips/sec (fwd+bwd) TARGCN skeleton-only, B=256, 1 GPU", "value": round(world * B / dt, 1),
            "unit": "clips/s", "n_gpus": world, "scaling": "weak", "ms_per_step": round(dt * 1e3, 3),
            "dtype": precision, "steps": steps,
            "config": {"workload": f"targcn_V{V}_T30_B{B}", "global_batch": world * B, "joints": V, "frames": 30,
                       "gru_layers": 2, "hidden": 64, "ta_layers": 2, "parallelism": f"replicas{world}"},
-           "final_loss": round(float(step.loss.item()), 5)}
+           "final_loss": round(float(step.loss.item()), 5), "stages": stages}
     if cpu_seconds > 0:  # the oracle (pinned bit-exactly to the reference) on this host's cores
         threads = cpu_threads()
         torch.set_num_threads(threads)
@@ -376,25 +377,72 @@ def targcn_bench(dev, B=256, V=17, steps=10, warmup=3, precision="bf16", cpu_sec
     return rec
 
 
-def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
+def targcn_stage_times(model, step, x, y, B, V, precision, reps=5):
+    """The recurrences and TA layers of one TARGCN step, timed with HIP events on the step's stream
+    (f3_targcn_stage_times), averaged over `reps` steps. R-GRU is latency-bound: its
+    figure is us per recurrent step (kernel time / 30 dependent steps); the achieved GB/s of each
+    recurrence kernel is also given, from its algorithmic bytes: every row it must read and write once
+    (R = B*T*V rows; forward writes H, sigmoid gates, static gate, tanh update, static update (fp32)
+    and the four EmbGCN operand rows (operand type, 128 wide); backward reads the five saved fp32
+    tensors and dH, writes the four pre-activation gradients and two mixed-input gradients (operand
+    type) and dX (layer 1))."""
+    import ctypes
+    import fall_multimodal_amd._lib as L
+    lib, h = L.lib(), model._native.h
+    acc = np.zeros(8)
+    L.check(lib.f3_targcn_stage_times(h, 1, None), "stage times")
+    for _ in range(reps):
+        step(x, y)
+        ms = (ctypes.c_float * 8)()
+        L.check(lib.f3_targcn_stage_times(h, 1, ms), "stage times")
+        acc += np.array(ms[:])
+    L.check(lib.f3_targcn_stage_times(h, 0, None), "stage times")
+    acc /= reps
+    R, T, es = B * 30 * V, 30, (2 if precision == "bf16" else 4)
+    fwd_row = [4 * 3 + 4 * (64 + 128 + 128 + 64 + 64) + es * 4 * 128, 4 * 64 + 4 * (64 + 128 + 128 + 64 + 64) + es * 4 * 128]
+    bwd_row = [4 * (64 + 128 + 128 + 64 + 64) + 4 * 64 + es * (128 * 2 + 64 * 2 + 2 * 128),
+               4 * (64 + 128 + 128 + 64 + 64) + 4 * 64 + es * (128 * 2 + 64 * 2 + 2 * 128) + 4 * 64]
+    out = {}
+    for i, (name, row) in enumerate((("gru_fwd_l0", fwd_row[0]), ("gru_fwd_l1", fwd_row[1]))):
+        out[name] = {"ms": round(acc[i], 4), "us_per_recurrent_step": round(acc[i] * 1e3 / T, 2),
+                     "GBps": round(R * row / (acc[i] * 1e-3) / 1e9, 1), "bytes": R * row}
+    for i, name in ((6, "gru_bwd_l1"), (7, "gru_bwd_l0")):
+        row = bwd_row[1] if name.endswith("l1") else bwd_row[0]
+        out[name] = {"ms": round(acc[i], 4), "us_per_recurrent_step": round(acc[i] * 1e3 / T, 2),
+                     "GBps": round(R * row / (acc[i] * 1e-3) / 1e9, 1), "bytes": R * row}
+    for i, name in ((2, "ta_fwd_l0"), (3, "ta_fwd_l1"), (4, "ta_bwd_l1"), (5, "ta_bwd_l0")):
+        out[name] = {"ms": round(acc[i], 4)}
+    out["note"] = ("HIP events around each launch on the step's stream (f3_targcn_stage_times), mean of "
+                   f"{reps} steps; R-GRU is latency-bound: 30 dependent steps per layer")
+    return out
+
+
+def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0, precision="bf16"):
     """BASELINE config 5: SkeletonTransformer(3, 14, 30, 11, 32, 6, 16, 8) training step (fwd + CE +
-    bwd + RMSprop, train-mode FFN dropout and stochastic depth) at B=256 on one GPU, fp32 (fp32 MFMA
-    GEMMs), synthetic clips, random-init weights. The 10-fold CV shards folds over GPUs as independent
-    replicas (no collective), so per-GPU throughput is the whole story."""
+    bwd + RMSprop, train-mode FFN dropout and stochastic depth) at B=256 on one GPU, synthetic clips,
+    random-init weights. precision "bf16" (BASELINE cfg 5): the block Linears on bf16 MFMA, fp32
+    accumulate; "fp32": fp32 MFMA (the parity mode, also reported). The 10-fold CV shards folds over
+    GPUs as independent replicas (no collective), so per-GPU throughput is the whole story."""
     import fall_multimodal_amd as f3
     from oracle import sktr_cpu as sk
     x, lab = sk.synthetic_clips(B, 14, 11, 3)
-    model = f3.SkeletonTransformer(device=dev)
+    model = f3.SkeletonTransformer(device=dev, precision=precision)
     step = f3.SktrStep(model, B)
     xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
     dt, world = replica_seconds(lambda: step(xd, yd), steps, warmup)
+    fp32_ms = None
+    if precision != "fp32":  # the parity mode's step time beside it
+        m32 = f3.SkeletonTransformer(device=dev)
+        s32 = f3.SktrStep(m32, B)
+        fp32_ms = round(replica_seconds(lambda: s32(xd, yd), steps, warmup)[0] * 1e3, 3)
+        del s32, m32
     rec = {"metric": "clips/sec (fwd+bwd) SkeletonTransformer, B=256, 1 GPU (one CV fold)",
            "value": round(world * B / dt, 1), "unit": "clips/s", "n_gpus": world, "scaling": "weak",
-           "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32", "steps": steps,
+           "ms_per_step": round(dt * 1e3, 3), "dtype": precision, "steps": steps,
            "config": {"workload": f"sktr_V14_T30_M1_B{B}", "global_batch": world * B, "joints": 14, "frames": 30,
                       "blocks": 6, "heads": 8,
                       "parallelism": f"replicas{world} (10-fold CV, one fold per GPU)"},
-           "final_loss": round(float(step.loss.item()), 5)}
+           "final_loss": round(float(step.loss.item()), 5), "fp32_mode_ms_per_step": fp32_ms}
     if cpu_seconds > 0:  # the oracle (pinned to the reference) on this host's cores
         threads = cpu_threads()
         torch.set_num_threads(threads)
@@ -411,7 +459,7 @@ def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     return rec
 
 
-def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
+def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0, precision="bf16"):
     """The model the root Multimodal_Fall3/main.py trains (musa_model.Model, main.py:307-320: 14 joints,
     30 frames, two streams, DropBlocks, RMSprop) — training step (fwd + CE + bwd + RMSprop) at B=256 on
     one GPU, fp32, synthetic clips; plus the HBM roofline of its depthwise temporal Conv1D."""
@@ -419,16 +467,23 @@ def musa_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0):
     import fall_multimodal_amd._lib as L
     from oracle.prng import synthetic_batch
     x, _, lab = synthetic_batch(B, 14, 11, 1, 9)
-    model = f3.musa.Model(11, 14, 300, f3.musa.adjGraph("coco_cut", "uniform"), True, True, 41, device=dev)
+    model = f3.musa.Model(11, 14, 300, f3.musa.adjGraph("coco_cut", "uniform"), True, True, 41, device=dev,
+                          precision=precision)
     step = f3.musa.MusaStep(model, B)
     xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
     dt, world = replica_seconds(lambda: step(xd, yd), steps, warmup)
+    fp32_ms = None
+    if precision != "fp32":  # the parity mode's step time beside it
+        m32 = f3.musa.Model(11, 14, 300, f3.musa.adjGraph("coco_cut", "uniform"), True, True, 41, device=dev)
+        s32 = f3.musa.MusaStep(m32, B)
+        fp32_ms = round(replica_seconds(lambda: s32(xd, yd), steps, warmup)[0] * 1e3, 3)
+        del s32, m32
     rec = {"metric": "clips/sec (fwd+bwd) musa_model.Model (root Multimodal_Fall3/main.py), B=256, 1 GPU",
            "value": round(world * B / dt, 1), "unit": "clips/s", "n_gpus": world, "scaling": "weak",
-           "ms_per_step": round(dt * 1e3, 3), "dtype": "fp32",
+           "ms_per_step": round(dt * 1e3, 3), "dtype": precision,
            "steps": steps, "config": {"workload": f"musa_V14_T30_B{B}", "global_batch": world * B, "joints": 14,
                                       "frames": 30, "dropblock": True, "parallelism": f"replicas{world}"},
-           "final_loss": round(float(step.loss.item()), 5)}
+           "final_loss": round(float(step.loss.item()), 5), "fp32_mode_ms_per_step": fp32_ms}
     if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
         return rec
     # depthwise temporal conv roofline (SepTemporal_Block depth_conv, C=128, V=14, T=30, B clips):
@@ -602,12 +657,14 @@ def main():
             print(json.dumps(rec), flush=True)
         return
     if a.model == "musa":
-        rec = musa_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0)
+        rec = musa_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0,
+                         precision=a.precision)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
     if a.model == "sktr":
-        rec = sktr_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0)
+        rec = sktr_bench(dev, steps=a.steps, warmup=a.warmup, cpu_seconds=0.0 if (a.no_cpu_baseline or world > 1) else 6.0,
+                         precision=a.precision)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
@@ -658,7 +715,8 @@ def main():
     ev = eval_throughput(model, sk, se) if rank == 0 else None
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
-    tgrec = targcn_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    tgrec = targcn_bench(dev, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0) if (
+        rank == 0 and world == 1 and not a.no_targcn) else None
     skrec = sktr_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     murec = musa_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None

@@ -63,6 +63,7 @@ constexpr float kHeadDrop = 0.2f;   // Classification_Module Dropout(0.2)
 
 struct f3_musa {
   int V, T, C;
+  int prec = F3_PRECISION_FP32;  // F3_PRECISION_BF16: the stream 1x1 convs on bf16 MFMA (fp32 accumulate)
   std::vector<Entry> entries;
   int64_t nparam = 0, nbuf = 0, ncnt = 0;
   StreamOff st[2];
@@ -119,6 +120,7 @@ struct Plan {
   size_t feat, z1, stat, h, dz1;
   size_t fsum, bsum;   // [22 BN][2][256] doubles
   size_t packT;        // transposed 1x1 weights for the input-gradient GEMMs (per stream)
+  size_t packF;        // bf16 mode: the stream 1x1 weights as bf16 GEMM operands ([O][I], same slots)
   size_t ga, gb, gc, gd;  // backward scratch [R][256]
   size_t part;         // depthwise weight-gradient partials
   size_t mixpart;      // graph-mix dA partial rows
@@ -180,6 +182,7 @@ Plan plan(const f3_musa* net, int N, std::vector<size_t>* guards = nullptr) {
   p.fsum = take(8 * 22 * 512);
   p.bsum = take(8 * 22 * 512);
   p.packT = take(4 * 2 * (size_t)kPackPerStream);
+  p.packF = net->prec == F3_PRECISION_BF16 ? take(4 * 2 * (size_t)kPackPerStream) : 0;
   p.ga = take(4 * Rmax * C2);
   p.gb = take(4 * Rmax * C2);
   p.gc = take(4 * Rmax * C2);
@@ -215,13 +218,15 @@ ConvGemmArgs conv1x1(int N, int T_in, int T_out, int V, int I, int O, int S, con
 }
 
 // input gradient of that conv: dx[N][T_in][V][I] (+)= dy[N][T_out][V][O] . W, Wt = W^T [I][O]
+// bf16: Wt holds the bf16 copy (bf16 MFMA on the fp32 dy, rounded as it is staged)
 int conv1x1_dgrad(int N, int T_in, int T_out, int V, int I, int O, int S, const float* dy, const float* Wt, float* dx,
-                  bool add, hipStream_t s) {
+                  bool add, hipStream_t s, bool bf16 = false) {
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g.M = N * T_in * V; a.g.Nc = I; a.g.Kc = O; a.g.KT = 1; a.g.S = S; a.g.P = 0; a.g.transposed = 1;
   a.g.T_out = T_in; a.g.T_in = T_out; a.g.V = V; a.g.lda = O; a.g.ldo = I;
-  a.in = dy; a.w = Wt; a.out = dx;
+  a.in = dy; a.w = bf16 ? nullptr : Wt; a.out = dx;
+  a.wb = bf16 ? reinterpret_cast<const unsigned short*>(Wt) : nullptr;
   if (S == 1) {  // plain row map
     a.g.transposed = 0;
     a.g.T_out = a.g.T_in = T_in;
@@ -230,12 +235,13 @@ int conv1x1_dgrad(int N, int T_in, int T_out, int V, int I, int O, int S, const 
 }
 
 int conv1x1_wgrad(int N, int T_in, int T_out, int V, int I, int lda, int O, int S, const float* dy, const float* in,
-                  float* dW, float* db, hipStream_t s) {
+                  float* dW, float* db, hipStream_t s, bool bf16 = false) {
   WgradArgs w;
   std::memset(&w, 0, sizeof(w));
   w.g.M = N * T_out * V; w.g.Nc = O; w.g.Kc = I; w.g.KT = 1; w.g.S = S; w.g.P = 0; w.g.transposed = 0;
   w.g.T_out = T_out; w.g.T_in = T_in; w.g.V = V; w.g.lda = lda; w.g.ldo = O;
   w.dy = dy; w.ldy = O; w.in = in; w.dw = dW; w.db = db; w.outmap = WG_OUT_CONV;
+  w.bf16 = bf16;  // operands rounded to bf16 as they are staged, bf16 MFMA, fp32 accumulate
   return f3_conv_wgrad(&w, 0, s);
 }
 
@@ -265,7 +271,26 @@ struct Ctx {
   }
   float* f(size_t off) const { return at<float>(ws, off); }
   float* lanes() const { return at<float>(ws, p.lanes); }
+  bool hb() const { return net->prec == F3_PRECISION_BF16; }
 };
+
+// slot `which` of stream si's 1x1-weight area (0 gcn, 1 res0, 2 pw1, 3 pw2, 4 p1, 5 p2, 6 sc, 7 res2):
+// transposed fp32/bf16 copies for the input gradients (packT) or bf16 forward operands (packF)
+float* pack_slot(const Ctx& c, size_t region, int si, int which) {
+  static const int sz[7] = {C1 * E, C1 * E, C1 * C1, C1 * C1, CM * C1, C2 * CM, C2 * C1};
+  float* base = at<float>(c.ws, region) + (size_t)si * kPackPerStream;
+  for (int i = 0; i < which; ++i) base += sz[i];
+  return base;
+}
+
+// the forward 1x1 conv's weight operand: bf16 copy in the bf16 mode
+ConvGemmArgs with_wb(const Ctx& c, ConvGemmArgs a, int si, int which) {
+  if (c.hb()) {
+    a.wb = reinterpret_cast<const unsigned short*>(pack_slot(c, c.p.packF, si, which));
+    a.w = nullptr;
+  }
+  return a;
+}
 
 int gemm_fwd(const Ctx& c, ConvGemmArgs a, const BnOff* stats) {
   int epi = EPI_BIAS;
@@ -328,8 +353,9 @@ int stream_forward(const Ctx& c, int si) {
   MU_TRY(f3_mu_relu_bwd(&rl, c.s));
   // --- SpatialGraphConv(64 -> 128), musa_model.py:127-146
   {
-    ConvGemmArgs a = conv1x1(N, T, T, V, E, C1, 1, c.f(w.e0), P + o.gcn_w, P + o.gcn_b, c.f(w.g));
-    ConvGemmArgs ar = conv1x1(N, T, T, V, E, C1, 1, c.f(w.e0), P + o.res0_w, P + o.res0_b, c.f(w.r0));
+    ConvGemmArgs a = with_wb(c, conv1x1(N, T, T, V, E, C1, 1, c.f(w.e0), P + o.gcn_w, P + o.gcn_b, c.f(w.g)), si, 0);
+    ConvGemmArgs ar =
+        with_wb(c, conv1x1(N, T, T, V, E, C1, 1, c.f(w.e0), P + o.res0_w, P + o.res0_b, c.f(w.r0)), si, 1);
     MU_TRY(gemm_fwd(c, a, nullptr));
     MU_TRY(gemm_fwd(c, ar, &o.bn_r0));
     MixArgs mx;
@@ -373,11 +399,13 @@ int stream_forward(const Ctx& c, int si) {
     std::memset(&ba, 0, sizeof(ba));
     ba.R = Ro; ba.C = C1; ba.u = d; ba.bn = c.bn(o.bn_d[b], Ro); ba.act = ACT_TANH; ba.y = e;
     MU_TRY(f3_mu_bn_act(&ba, c.s));
-    MU_TRY(gemm_fwd(c, conv1x1(N, To, To, V, C1, C1, 1, e, P + o.pw_w[b], P + o.pw_b[b], pp), &o.bn_p[b]));
+    MU_TRY(gemm_fwd(c, with_wb(c, conv1x1(N, To, To, V, C1, C1, 1, e, P + o.pw_w[b], P + o.pw_b[b], pp), si, 2 + b),
+                    &o.bn_p[b]));
     const float* res = x;
     const BnOff* rbn = nullptr;
     if (b == 1) {
-      MU_TRY(gemm_fwd(c, conv1x1(N, Ti, To, V, C1, C1, 2, x, P + o.res2_w, P + o.res2_b, c.f(w.r2)), &o.bn_r2));
+      MU_TRY(gemm_fwd(c, with_wb(c, conv1x1(N, Ti, To, V, C1, C1, 2, x, P + o.res2_w, P + o.res2_b, c.f(w.r2)), si, 7),
+                      &o.bn_r2));
       res = c.f(w.r2);
       rbn = &o.bn_r2;
     }
@@ -395,7 +423,8 @@ int stream_forward(const Ctx& c, int si) {
   // --- Sep_TCN(128 -> 256), musa_model.py:461-474
   {
     const float* x = c.f(w.out3);
-    MU_TRY(gemm_fwd(c, conv1x1(N, T2, T2, V, C1, C2, 1, x, P + o.sc_w, P + o.sc_b, c.f(w.tres)), nullptr));
+    MU_TRY(gemm_fwd(c, with_wb(c, conv1x1(N, T2, T2, V, C1, C2, 1, x, P + o.sc_w, P + o.sc_b, c.f(w.tres)), si, 6),
+                    nullptr));
     DwConvArgs dw;
     std::memset(&dw, 0, sizeof(dw));
     dw.N = N; dw.T_in = T2; dw.T_out = T2; dw.V = V; dw.C = C1; dw.K = 3; dw.S = 1; dw.P = 1;
@@ -406,7 +435,8 @@ int stream_forward(const Ctx& c, int si) {
     std::memset(&ba, 0, sizeof(ba));
     ba.R = R2; ba.C = C1; ba.u = c.f(w.td1); ba.bn = c.bn(o.bn1, R2); ba.act = ACT_LEAKY; ba.y = c.f(w.te1);
     MU_TRY(f3_mu_bn_act(&ba, c.s));
-    MU_TRY(gemm_fwd(c, conv1x1(N, T2, T2, V, C1, CM, 1, c.f(w.te1), P + o.p1_w, P + o.p1_b, c.f(w.tp1)), &o.bn2));
+    MU_TRY(gemm_fwd(c, with_wb(c, conv1x1(N, T2, T2, V, C1, CM, 1, c.f(w.te1), P + o.p1_w, P + o.p1_b, c.f(w.tp1)), si, 4),
+                    &o.bn2));
     ba.C = CM; ba.u = c.f(w.tp1); ba.bn = c.bn(o.bn2, R2); ba.act = ACT_RELU; ba.y = c.f(w.te2);
     MU_TRY(f3_mu_bn_act(&ba, c.s));
     std::memset(&dw, 0, sizeof(dw));
@@ -416,7 +446,8 @@ int stream_forward(const Ctx& c, int si) {
     MU_TRY(f3_mu_dwconv_fwd(&dw, c.s));
     ba.C = CM; ba.u = c.f(w.td2); ba.bn = c.bn(o.bn3, R2); ba.act = ACT_LEAKY; ba.y = c.f(w.te3);
     MU_TRY(f3_mu_bn_act(&ba, c.s));
-    MU_TRY(gemm_fwd(c, conv1x1(N, T2, T2, V, CM, C2, 1, c.f(w.te3), P + o.p2_w, P + o.p2_b, c.f(w.tp2)), &o.bn4));
+    MU_TRY(gemm_fwd(c, with_wb(c, conv1x1(N, T2, T2, V, CM, C2, 1, c.f(w.te3), P + o.p2_w, P + o.p2_b, c.f(w.tp2)), si, 5),
+                    &o.bn4));
     ba.C = C2; ba.u = c.f(w.tp2); ba.bn = c.bn(o.bn4, R2); ba.act = ACT_RELU; ba.y = c.f(w.out4);
     ba.add = c.f(w.tres);
     MU_TRY(f3_mu_bn_act(&ba, c.s));
@@ -448,14 +479,8 @@ int dwconv_bwd(const Ctx& c, int N, int Ti, int To, int V, int C, int K, int S, 
   return f3_colsum(dw.part + (size_t)dw.part_rows * C * K, dw.part_rows, C, c.grads + b_off, c.s);
 }
 
-// transposed copies [I][O] of the stream's 1x1 weights [O][I]
-float* packT(const Ctx& c, int si, int which) {
-  static const int sz[7] = {C1 * E, C1 * E, C1 * C1, C1 * C1, CM * C1, C2 * CM, C2 * C1};
-  float* base = at<float>(c.ws, c.p.packT) + (size_t)si * kPackPerStream;
-  for (int i = 0; i < which; ++i) base += sz[i];
-  return base;
-}
-// (which: 0 gcn, 1 res0, 2 pw1, 3 pw2, 4 p1, 5 p2, 6 sc, 7 the strided residual res2)
+// transposed copies [I][O] of the stream's 1x1 weights [O][I] (bf16 in the bf16 mode)
+float* packT(const Ctx& c, int si, int which) { return pack_slot(c, c.p.packT, si, which); }
 
 int stream_backward(const Ctx& c, int si, float* dres2T) {
   f3_musa* net = c.net;
@@ -470,16 +495,16 @@ int stream_backward(const Ctx& c, int si, float* dres2T) {
   float* G = c.grads;
   const float* dy4 = c.f(w.dy4);
   // --- Sep_TCN
-  MU_TRY(conv1x1_wgrad(N, T2, T2, V, C1, C1, C2, 1, dy4, c.f(w.out3), G + o.sc_w, G + o.sc_b, c.s));
-  MU_TRY(conv1x1_dgrad(N, T2, T2, V, C1, C2, 1, dy4, packT(c, si, 6), gd, false, c.s));   // gd = d out3
+  MU_TRY(conv1x1_wgrad(N, T2, T2, V, C1, C1, C2, 1, dy4, c.f(w.out3), G + o.sc_w, G + o.sc_b, c.s, c.hb()));
+  MU_TRY(conv1x1_dgrad(N, T2, T2, V, C1, C2, 1, dy4, packT(c, si, 6), gd, false, c.s, c.hb()));   // gd = d out3
   MU_TRY(bn_act_bwd(c, o.bn4, R2, C2, dy4, c.f(w.tp2), ACT_RELU, ga, nullptr));           // ga = d p2
-  MU_TRY(conv1x1_wgrad(N, T2, T2, V, CM, CM, C2, 1, ga, c.f(w.te3), G + o.p2_w, G + o.p2_b, c.s));
-  MU_TRY(conv1x1_dgrad(N, T2, T2, V, CM, C2, 1, ga, packT(c, si, 5), gb, false, c.s));    // gb = d e3
+  MU_TRY(conv1x1_wgrad(N, T2, T2, V, CM, CM, C2, 1, ga, c.f(w.te3), G + o.p2_w, G + o.p2_b, c.s, c.hb()));
+  MU_TRY(conv1x1_dgrad(N, T2, T2, V, CM, C2, 1, ga, packT(c, si, 5), gb, false, c.s, c.hb()));    // gb = d e3
   MU_TRY(bn_act_bwd(c, o.bn3, R2, CM, gb, c.f(w.td2), ACT_LEAKY, ga, nullptr));           // ga = d d2
   MU_TRY(dwconv_bwd(c, N, T2, T2, V, CM, 1, 1, c.f(w.te2), ga, gb, false, o.d2_w, o.d2_b));  // gb = d e2
   MU_TRY(bn_act_bwd(c, o.bn2, R2, CM, gb, c.f(w.tp1), ACT_RELU, ga, nullptr));            // ga = d p1
-  MU_TRY(conv1x1_wgrad(N, T2, T2, V, C1, C1, CM, 1, ga, c.f(w.te1), G + o.p1_w, G + o.p1_b, c.s));
-  MU_TRY(conv1x1_dgrad(N, T2, T2, V, C1, CM, 1, ga, packT(c, si, 4), gb, false, c.s));    // gb = d e1
+  MU_TRY(conv1x1_wgrad(N, T2, T2, V, C1, C1, CM, 1, ga, c.f(w.te1), G + o.p1_w, G + o.p1_b, c.s, c.hb()));
+  MU_TRY(conv1x1_dgrad(N, T2, T2, V, C1, CM, 1, ga, packT(c, si, 4), gb, false, c.s, c.hb()));    // gb = d e1
   MU_TRY(bn_act_bwd(c, o.bn1, R2, C1, gb, c.f(w.td1), ACT_LEAKY, ga, nullptr));           // ga = d d1
   MU_TRY(dwconv_bwd(c, N, T2, T2, V, C1, 3, 1, c.f(w.out3), ga, gd, true, o.d1_w, o.d1_b));  // gd += ...
   // --- SepTemporal blocks (2 then 1); gd holds d out3, then d out2
@@ -503,12 +528,12 @@ int stream_backward(const Ctx& c, int si, float* dres2T) {
     MU_TRY(f3_mu_merge_bwd(&m, c.s));
     float* dxin = gc;                        // d x of the block (x = out2 / out1) accumulates in gc
     if (b == 1) {  // strided residual: wgrad and dx = dr . W (transposed row map)
-      MU_TRY(conv1x1_wgrad(N, Ti, To, V, C1, C1, C1, 2, gb, x, G + o.res2_w, G + o.res2_b, c.s));
-      MU_TRY(conv1x1_dgrad(N, Ti, To, V, C1, C1, 2, gb, dres2T, gc, false, c.s));
+      MU_TRY(conv1x1_wgrad(N, Ti, To, V, C1, C1, C1, 2, gb, x, G + o.res2_w, G + o.res2_b, c.s, c.hb()));
+      MU_TRY(conv1x1_dgrad(N, Ti, To, V, C1, C1, 2, gb, dres2T, gc, false, c.s, c.hb()));
     }
     MU_TRY(conv1x1_wgrad(N, To, To, V, C1, C1, C1, 1, ga, c.f(b == 0 ? w.ee1 : w.ee2), G + o.pw_w[b], G + o.pw_b[b],
-                         c.s));
-    MU_TRY(conv1x1_dgrad(N, To, To, V, C1, C1, 1, ga, packT(c, si, 2 + b), gb, false, c.s));   // gb = d e
+                         c.s, c.hb()));
+    MU_TRY(conv1x1_dgrad(N, To, To, V, C1, C1, 1, ga, packT(c, si, 2 + b), gb, false, c.s, c.hb()));   // gb = d e
     MU_TRY(bn_act_bwd(c, o.bn_d[b], Ro, C1, gb, c.f(b == 0 ? w.d1 : w.d2), ACT_TANH, ga, nullptr));  // ga = d d
     MU_TRY(dwconv_bwd(c, N, Ti, To, V, C1, K, S, x, ga, dxin, true, o.dw_w[b], o.dw_b[b]));
     std::swap(gc, gd);  // the block input's gradient becomes the next (earlier) block's output gradient
@@ -537,10 +562,10 @@ int stream_backward(const Ctx& c, int si, float* dres2T) {
     std::memset(&j, 0, sizeof(j));
     j.type = PREP_MUL; j.n = V * V; j.dst = G + o.e0; j.s0 = dAe; j.s1 = c.params + o.A0;
     MU_TRY(f3_prep(t, c.s));
-    MU_TRY(conv1x1_wgrad(N, T, T, V, E, E, C1, 1, gc, c.f(w.e0), G + o.gcn_w, G + o.gcn_b, c.s));
-    MU_TRY(conv1x1_wgrad(N, T, T, V, E, E, C1, 1, gb, c.f(w.e0), G + o.res0_w, G + o.res0_b, c.s));
-    MU_TRY(conv1x1_dgrad(N, T, T, V, E, C1, 1, gc, packT(c, si, 0), gd, false, c.s));
-    MU_TRY(conv1x1_dgrad(N, T, T, V, E, C1, 1, gb, packT(c, si, 1), gd, true, c.s));   // gd = d e0
+    MU_TRY(conv1x1_wgrad(N, T, T, V, E, E, C1, 1, gc, c.f(w.e0), G + o.gcn_w, G + o.gcn_b, c.s, c.hb()));
+    MU_TRY(conv1x1_wgrad(N, T, T, V, E, E, C1, 1, gb, c.f(w.e0), G + o.res0_w, G + o.res0_b, c.s, c.hb()));
+    MU_TRY(conv1x1_dgrad(N, T, T, V, E, C1, 1, gc, packT(c, si, 0), gd, false, c.s, c.hb()));
+    MU_TRY(conv1x1_dgrad(N, T, T, V, E, C1, 1, gb, packT(c, si, 1), gd, true, c.s, c.hb()));   // gd = d e0
   }
   // --- embedding: relu backward, weight gradient on the token rows
   ReluBwdArgs rl;
@@ -561,6 +586,8 @@ int f3_musa_create(const f3_musa_config* cfg, f3_musa** out) {
     return F3_EINVAL;
   f3_musa* n = new f3_musa();
   n->V = cfg->num_point; n->T = cfg->frames; n->C = cfg->num_class;
+  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) { delete n; return F3_EINVAL; }
+  n->prec = cfg->precision;
   const int V = n->V;
   n->bns.reserve(22);
   StreamOff* so[2] = {&n->st[0], &n->st[1]};
@@ -677,6 +704,22 @@ int f3_musa_forward(f3_musa* net, int N, int training, const float* params, floa
     }
     MU_TRY(f3_prep(t, s));
   }
+  if (c.hb()) {  // bf16 mode: the stream 1x1 weights as bf16 GEMM operands ([O][I])
+    PrepTable t;
+    t.n = 0;
+    auto job = [&](float* dst, const float* src, int O, int I) {
+      PrepJob& j = t.jobs[t.n++];
+      std::memset(&j, 0, sizeof(j));
+      j.type = PREP_PACK_CONV; j.n = O * I; j.dst = dst; j.s0 = src; j.d0 = O; j.d1 = I; j.d2 = 1; j.bf16 = 1;
+    };
+    for (int si = 0; si < 2; ++si) {
+      const StreamOff& o = net->st[si];
+      const int64_t ws8[8] = {o.gcn_w, o.res0_w, o.pw_w[0], o.pw_w[1], o.p1_w, o.p2_w, o.sc_w, o.res2_w};
+      const int O8[8] = {C1, C1, C1, C1, CM, C2, C2, C1}, I8[8] = {E, E, C1, C1, C1, CM, C1, C1};
+      for (int k = 0; k < 8; ++k) job(pack_slot(c, p.packF, si, k), params + ws8[k], O8[k], I8[k]);
+    }
+    MU_TRY(f3_prep(t, s));
+  }
   for (int si = 0; si < 2; ++si) MU_TRY(stream_forward(c, si));
   if (training) {
     BnRunTable t;
@@ -731,6 +774,7 @@ int f3_musa_backward(f3_musa* net, int N, const float* params, const float* buff
       PrepJob& j = t.jobs[t.n++];
       std::memset(&j, 0, sizeof(j));
       j.type = PREP_PACK_CONV_T; j.n = O * I; j.dst = dst; j.s0 = src; j.d0 = O; j.d1 = I; j.d2 = 1;
+      j.bf16 = c.hb();
     };
     for (int si = 0; si < 2; ++si) {
       const StreamOff& o = net->st[si];

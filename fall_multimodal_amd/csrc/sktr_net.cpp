@@ -53,6 +53,7 @@ constexpr int NBLOCK = 6;
 
 struct f3_sktr {
   int V, T, M, C;
+  int prec = F3_PRECISION_FP32;  // F3_PRECISION_BF16: the block Linears on bf16 MFMA (fp32 accumulate)
   std::vector<Entry> entries;
   int64_t nparam = 0, nbuf = 0, ncnt = 0;
   int64_t e_w1 = 0, e_b1 = 0, e_w2 = 0, e_b2 = 0, fc_w = 0, fc_b = 0;
@@ -95,6 +96,7 @@ struct Plan {
   size_t fsum;      // [18 BN][2][32] doubles, forward batch sums
   size_t bsum;      // [18 BN][2][32] doubles, backward sums
   size_t packT;     // transposed weights for the input-gradient GEMMs, per block 6 matrices
+  size_t packF;     // bf16 mode: the forward weights as bf16 GEMM operands, same slots
   size_t du3, dy2, dy1, dm, dbig, dqkv, dya, dyb, da1, da2, dtab;
   size_t total;
 };
@@ -134,6 +136,7 @@ Plan plan(const f3_sktr* net, int N) {
   p.fsum = take(8 * 18 * 64);
   p.bsum = take(8 * 18 * 64);
   p.packT = take(4 * (size_t)NBLOCK * kPackPerBlock);
+  p.packF = net->prec == F3_PRECISION_BF16 ? take(4 * (size_t)NBLOCK * kPackPerBlock) : 0;
   p.du3 = take(r32);
   p.dy2 = take(r32);
   p.dy1 = take(r32);
@@ -163,24 +166,28 @@ P* at(void* ws, size_t off) {
   } while (0)
 
 // token-row Linear: out[R][O] = in[R][I] . W^T (+ bias) ; W packed [O][I] (nn.Linear layout)
+// wb (bf16 mode): the same weight as a bf16 operand; fp32 activations are rounded to bf16 as
+// they are staged (conv_gemm_bf16), accumulation and outputs stay fp32
 int linear(const float* in, int I, const float* W, const float* bias, float* out, int O, long long R, int epi,
-           hipStream_t s) {
+           hipStream_t s, const void* wb = nullptr) {
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.g.M = (int)R; a.g.Nc = O; a.g.Kc = I; a.g.KT = 1; a.g.S = 1; a.g.P = 0; a.g.transposed = 0;
   a.g.T_out = 1; a.g.T_in = 1; a.g.V = 1; a.g.lda = I; a.g.ldo = O;
   a.in = in; a.w = W; a.out = out; a.bias = bias;
+  a.wb = reinterpret_cast<const unsigned short*>(wb);
   return f3_conv_gemm(&a, 0, epi, s);
 }
 
 // weight gradient of a token-row Linear: dW[O][I] += dy[R][O]^T in[R][I] ; db[O] += sum dy
+// bf16 != 0: operands rounded to bf16 as they are staged, bf16 MFMA, fp32 accumulate (conv_wgrad_bf16)
 int linear_wgrad(const float* dy, int O, const float* in, int I, int lda, float* dW, float* db, long long R,
-                 hipStream_t s) {
+                 hipStream_t s, int bf16 = 0) {
   WgradArgs w;
   std::memset(&w, 0, sizeof(w));
   w.g.M = (int)R; w.g.Nc = O; w.g.Kc = I; w.g.KT = 1; w.g.S = 1; w.g.P = 0; w.g.transposed = 0;
   w.g.T_out = 1; w.g.T_in = 1; w.g.V = 1; w.g.lda = lda; w.g.ldo = O;
-  w.dy = dy; w.ldy = O; w.in = in; w.dw = dW; w.db = db; w.outmap = WG_OUT_CONV;
+  w.dy = dy; w.ldy = O; w.in = in; w.dw = dW; w.db = db; w.outmap = WG_OUT_CONV; w.bf16 = bf16;
   return f3_conv_wgrad(&w, 0, s);
 }
 
@@ -201,8 +208,8 @@ BnRef bnref(const f3_sktr* net, const Plan& p, void* ws, const float* params, co
 }
 
 // transposed weight slots of block b: Wqkv^T [32][384] and Wm^T [128][32] per attention, W1^T [32][128], W2^T [128][32]
-float* packT(void* ws, const Plan& p, int b, int which) {
-  float* base = at<float>(ws, p.packT) + (size_t)b * kPackPerBlock;
+float* packT(void* ws, const Plan& p, int b, int which, bool fwd = false) {
+  float* base = at<float>(ws, fwd ? p.packF : p.packT) + (size_t)b * kPackPerBlock;
   const size_t sz[6] = {QKV * EMB, DM * EMB, QKV * EMB, DM * EMB, FFN * EMB, FFN * EMB};
   for (int i = 0; i < which; ++i) base += sz[i];
   return base;
@@ -220,6 +227,8 @@ int f3_sktr_create(const f3_sktr_config* cfg, f3_sktr** out) {
     return F3_EINVAL;
   f3_sktr* n = new f3_sktr();
   n->V = cfg->num_joint; n->T = cfg->frames; n->M = cfg->persons; n->C = cfg->num_class;
+  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) { delete n; return F3_EINVAL; }
+  n->prec = cfg->precision;
   // state_dict order of SkeletonTransformer (checked against the reference by tools/gen_golden.py)
   n->e_w1 = n->add("embedding.0.weight", {HID0, CIN});
   n->e_b1 = n->add("embedding.0.bias", {HID0});
@@ -317,6 +326,27 @@ int f3_sktr_forward(f3_sktr* net, int N, int training, const float* params, floa
   ea.y = at<float>(ws, p.y0);
   SK_TRY(f3_sk_embed_fwd_save(&ea, at<float>(ws, p.xt), at<float>(ws, p.a1), at<float>(ws, p.h1), at<float>(ws, p.a2),
                               s));
+  const bool hb = net->prec == F3_PRECISION_BF16;
+  if (hb) {  // the block Linears' weights as bf16 GEMM operands ([O][I], nn.Linear layout)
+    PrepTable t;
+    t.n = 0;
+    auto job = [&](float* dst, const float* src, int O, int I) {
+      PrepJob& j = t.jobs[t.n++];
+      std::memset(&j, 0, sizeof(j));
+      j.type = PREP_PACK_CONV; j.n = O * I; j.dst = dst; j.s0 = src; j.d0 = O; j.d1 = I; j.d2 = 1; j.bf16 = 1;
+    };
+    for (int b = 0; b < NBLOCK; ++b) {
+      const BlockOff& B = net->blk[b];
+      for (int k = 0; k < 2; ++k) {
+        job(packT(ws, p, b, 2 * k, true), params + B.at[k].wqkv, QKV, EMB);
+        job(packT(ws, p, b, 2 * k + 1, true), params + B.at[k].wm, EMB, DM);
+      }
+      job(packT(ws, p, b, 4, true), params + B.w1, FFN, EMB);
+      job(packT(ws, p, b, 5, true), params + B.w2, EMB, FFN);
+    }
+    SK_TRY(f3_prep(t, s));
+  }
+  auto wbf = [&](int b, int which) -> const void* { return hb ? packT(ws, p, b, which, true) : nullptr; };
   const float scale = 1.f / std::sqrt((float)DM);
   float* mt = at<float>(ws, p.mtmp);
   const float* yin = at<float>(ws, p.y0);
@@ -328,7 +358,7 @@ int f3_sktr_forward(f3_sktr* net, int N, int training, const float* params, floa
       const AttnOff& A = B.at[k];
       float* qkv = at<float>(ws, W.qkv[k]);
       float* o = at<float>(ws, W.o[k]);
-      SK_TRY(linear(ycur, EMB, params + A.wqkv, params + A.bqkv, qkv, QKV, R, EPI_BIAS, s));
+      SK_TRY(linear(ycur, EMB, params + A.wqkv, params + A.bqkv, qkv, QKV, R, EPI_BIAS, s, wbf(b, 2 * k)));
       AttnArgs aa;
       std::memset(&aa, 0, sizeof(aa));
       aa.L = k == 0 ? net->V : net->T;
@@ -337,7 +367,7 @@ int f3_sktr_forward(f3_sktr* net, int N, int training, const float* params, floa
       aa.T = net->T; aa.V = net->V; aa.scale = scale;
       aa.qkv = qkv; aa.table = params + A.table; aa.o = o;
       SK_TRY(f3_sk_attn_fwd(&aa, s));
-      SK_TRY(linear(o, DM, params + A.wm, params + A.bm, mt, EMB, R, EPI_BIAS, s));
+      SK_TRY(linear(o, DM, params + A.wm, params + A.bm, mt, EMB, R, EPI_BIAS, s, wbf(b, 2 * k + 1)));
       BnRef bn = bnref(net, p, ws, params, buffers, b, k, R, tr);
       ResidArgs ra;
       std::memset(&ra, 0, sizeof(ra));
@@ -354,12 +384,12 @@ int f3_sktr_forward(f3_sktr* net, int N, int training, const float* params, floa
     // feed-forward network (Linear 32->128, GELU, Linear 128->32, Dropout)
     float* h = at<float>(ws, W.h);
     float* g = at<float>(ws, W.g);
-    SK_TRY(linear(ycur, EMB, params + B.w1, params + B.b1, h, FFN, R, EPI_BIAS, s));
+    SK_TRY(linear(ycur, EMB, params + B.w1, params + B.b1, h, FFN, R, EPI_BIAS, s, wbf(b, 4)));
     GeluArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     ga.n = R * FFN; ga.h = h; ga.g = g;
     SK_TRY(f3_sk_gelu_fwd(&ga, s));
-    SK_TRY(linear(g, FFN, params + B.w2, params + B.b2, mt, EMB, R, EPI_BIAS, s));
+    SK_TRY(linear(g, FFN, params + B.w2, params + B.b2, mt, EMB, R, EPI_BIAS, s, wbf(b, 5)));
     BnRef bn = bnref(net, p, ws, params, buffers, b, 2, R, tr);
     ResidArgs ra;
     std::memset(&ra, 0, sizeof(ra));
@@ -416,6 +446,7 @@ int f3_sktr_backward(f3_sktr* net, int N, const float* params, const float* buff
       PrepJob& j = t.jobs[t.n++];
       std::memset(&j, 0, sizeof(j));
       j.type = PREP_PACK_CONV_T; j.n = O * I; j.dst = dst; j.s0 = src; j.d0 = O; j.d1 = I; j.d2 = 1;
+      j.bf16 = net->prec == F3_PRECISION_BF16;  // bf16 mode: the transposed copies are bf16 operands
     };
     for (int b = 0; b < NBLOCK; ++b) {
       const BlockOff& B = net->blk[b];
@@ -446,6 +477,12 @@ int f3_sktr_backward(f3_sktr* net, int N, const float* params, const float* buff
   float* dm = at<float>(ws, p.dm);
   float* dbig = at<float>(ws, p.dbig);
   float* dqkv = at<float>(ws, p.dqkv);
+  const int hb = net->prec == F3_PRECISION_BF16;
+  // the input-gradient GEMMs' B operand: fp32 transposed weights, or their bf16 copies (same slots)
+  auto lin_t = [&](const float* dy, int O, int b, int which, float* out, int I, int epi) {
+    const float* wt = packT(ws, p, b, which);
+    return linear(dy, O, hb ? nullptr : wt, nullptr, out, I, R, epi, s, hb ? (const void*)wt : nullptr);
+  };
   for (int b = NBLOCK - 1; b >= 0; --b) {
     const BlockOff& B = net->blk[b];
     const BlockWs& W = p.b[b];
@@ -466,14 +503,14 @@ int f3_sktr_backward(f3_sktr* net, int N, const float* params, const float* buff
     // BN3: dU3 -> dy2 (its skip into y2) and du3 (kept for y0); dF = sd * drop'(dU3)
     SK_TRY(bnb(2, dy_cur, at<float>(ws, W.u[2]), nullptr, dy2, dm, du3, net->sd[b][2], net->drop_p));
     // FFN backward
-    SK_TRY(linear_wgrad(dm, EMB, at<float>(ws, W.g), FFN, FFN, grads + B.w2, grads + B.b2, R, s));
-    SK_TRY(linear(dm, EMB, packT(ws, p, b, 5), nullptr, dbig, FFN, R, 0, s));   // dG = dF W2
+    SK_TRY(linear_wgrad(dm, EMB, at<float>(ws, W.g), FFN, FFN, grads + B.w2, grads + B.b2, R, s, hb));
+    SK_TRY(lin_t(dm, EMB, b, 5, dbig, FFN, 0));   // dG = dF W2
     GeluArgs ga;
     std::memset(&ga, 0, sizeof(ga));
     ga.n = R * FFN; ga.h = at<float>(ws, W.h); ga.dg = dbig; ga.dh = dbig;
     SK_TRY(f3_sk_gelu_bwd(&ga, s));
-    SK_TRY(linear_wgrad(dbig, FFN, at<float>(ws, W.y2), EMB, EMB, grads + B.w1, grads + B.b1, R, s));
-    SK_TRY(linear(dbig, FFN, packT(ws, p, b, 4), nullptr, dy2, EMB, R, EPI_ADD, s));   // dy2 += dH W1
+    SK_TRY(linear_wgrad(dbig, FFN, at<float>(ws, W.y2), EMB, EMB, grads + B.w1, grads + B.b1, R, s, hb));
+    SK_TRY(lin_t(dbig, FFN, b, 4, dy2, EMB, EPI_ADD));   // dy2 += dH W1
     // temporal then spatial attention
     for (int k = 1; k >= 0; --k) {
       const AttnOff& A = B.at[k];
@@ -482,8 +519,8 @@ int f3_sktr_backward(f3_sktr* net, int N, const float* params, const float* buff
       const float* add = k == 1 ? nullptr : du3;    // y0 also feeds u3 directly
       SK_TRY(bnb(k, dyk, at<float>(ws, W.u[k]), add, o1, dm, nullptr, net->sd[b][k], 0.f));
       const float* xin = k == 1 ? at<float>(ws, W.y1) : yin;
-      SK_TRY(linear_wgrad(dm, EMB, at<float>(ws, W.o[k]), DM, DM, grads + A.wm, grads + A.bm, R, s));
-      SK_TRY(linear(dm, EMB, packT(ws, p, b, 2 * k + 1), nullptr, dbig, DM, R, 0, s));   // dO = dM Wm
+      SK_TRY(linear_wgrad(dm, EMB, at<float>(ws, W.o[k]), DM, DM, grads + A.wm, grads + A.bm, R, s, hb));
+      SK_TRY(lin_t(dm, EMB, b, 2 * k + 1, dbig, DM, 0));   // dO = dM Wm
       AttnArgs aa;
       std::memset(&aa, 0, sizeof(aa));
       aa.L = k == 0 ? net->V : net->T;
@@ -494,8 +531,8 @@ int f3_sktr_backward(f3_sktr* net, int N, const float* params, const float* buff
       aa.dout = dbig; aa.dqkv = dqkv; aa.dtab = at<float>(ws, p.dtab);
       SK_TRY(f3_sk_attn_bwd(&aa, s));
       SK_TRY(f3_colsum(aa.dtab, aa.nseq, (2 * aa.L - 1) * HD, grads + A.table, s));
-      SK_TRY(linear_wgrad(dqkv, QKV, xin, EMB, EMB, grads + A.wqkv, grads + A.bqkv, R, s));
-      SK_TRY(linear(dqkv, QKV, packT(ws, p, b, 2 * k), nullptr, o1, EMB, R, EPI_ADD, s));   // += dQKV Wqkv
+      SK_TRY(linear_wgrad(dqkv, QKV, xin, EMB, EMB, grads + A.wqkv, grads + A.bqkv, R, s, hb));
+      SK_TRY(lin_t(dqkv, QKV, b, 2 * k, o1, EMB, EPI_ADD));   // += dQKV Wqkv
     }
     std::swap(dy_cur, dy_next);
   }

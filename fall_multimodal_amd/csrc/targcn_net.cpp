@@ -55,6 +55,9 @@ struct f3_targcn {
   EmbOff emb[2][2];  // [layer][gate, update]
   TaOff ta[2];
   int64_t end_w = 0, end_b = 0, fc_w = 0, fc_b = 0, pe = 0;
+  // f3_targcn_stage_times: timing events around the recurrences and the TA layers (0 = off)
+  int timing = 0;
+  hipEvent_t tev[11] = {};
 
   int64_t add(const std::string& name, std::vector<int64_t> shape, int kind = F3_ENTRY_PARAM) {
     int64_t n = 1;
@@ -183,6 +186,12 @@ TaArgs ta_args(const f3_targcn* net, int l, int B, const float* params) {
   return a;
 }
 
+// stage timing marks (f3_targcn_stage_times): forward 0 | gru0 | 1 | gru1 | 2 | ta0 | 3 | ta1 | 4,
+// backward 5 | ta1 | 6 | ta0 | 7 | gru1 | 8 ... 9 | gru0 | 10
+inline void mark(f3_targcn* n, int i, hipStream_t s) {
+  if (n->timing && n->tev[i]) (void)hipEventRecord(n->tev[i], s);
+}
+
 #define TG_TRY(x)                 \
   do {                            \
     const int _st = (x);          \
@@ -290,6 +299,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
       TG_TRY(f3_tg_prep(&pa, b16, s));
     }
   TG_TRY(f3_tg_endconv_mean(params + net->end_w, params + net->end_b, at<float>(ws, p.Wm), at<float>(ws, p.bm), s));
+  mark(net, 0, s);
   for (int l = 0; l < 2; ++l) {  // AVWDCRNN (TRAGCN.py:159-166)
     GruFwdArgs g;
     std::memset(&g, 0, sizeof(g));
@@ -305,6 +315,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
     TG_TRY(f3_tg_gru_fwd(&g, b16, s));
+    mark(net, 1 + l, s);
     if (g.prof) {  // debugging aid: per-phase microseconds of workgroup 0, averaged over the steps
       long long h[T * 8];
       (void)hipStreamSynchronize(s);
@@ -326,6 +337,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     a.out = at<float>(ws, l == 0 ? p.ta_out0 : p.ta_out1);
     a.save = at<float>(ws, p.ta_save[l]);
     TG_TRY(f3_tg_ta_fwd(&a, s));
+    mark(net, 3 + l, s);
   }
   TG_TRY(f3_tg_pool_fwd(at<float>(ws, p.ta_out1), B, V, at<float>(ws, p.Wm), at<float>(ws, p.bm), at<float>(ws, p.xm),
                         at<float>(ws, p.pooled), s));
@@ -358,6 +370,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
   TG_TRY(f3_head_bwd(&h, s));
   TG_TRY(f3_tg_pool_bwd(at<float>(ws, p.dpooled), at<float>(ws, p.xm), at<float>(ws, p.Wm), B, V, at<float>(ws, p.dY1),
                         grads + net->end_w, grads + net->end_b, s));
+  mark(net, 5, s);
   for (int l = 1; l >= 0; --l) {
     TaArgs a = ta_args(net, l, B, params);
     a.in = l == 0 ? at<float>(ws, p.H[1]) : at<float>(ws, p.ta_out0);
@@ -367,6 +380,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     a.din = at<float>(ws, l == 1 ? p.dY0 : p.dH1);
     a.grads = grads;
     TG_TRY(f3_tg_ta_bwd(&a, s));
+    mark(net, 7 - l, s);
   }
   const float* S = at<float>(ws, p.S);
   const float* cs = at<float>(ws, p.cs);
@@ -389,7 +403,9 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
+    mark(net, l == 1 ? 7 : 9, s);
     TG_TRY(f3_tg_gru_bwd(&g, b16, s));
+    mark(net, l == 1 ? 8 : 10, s);
     if (g.prof) {
       long long h[T * 8];
       (void)hipStreamSynchronize(s);
@@ -450,6 +466,25 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
       TG_TRY(f3_tg_pool_grad(&a, s));
     }
   return f3_tg_supports_bwd(E, V, dS, grads + net->E, s);
+}
+
+int f3_targcn_stage_times(f3_targcn* net, int enable, float* ms) {
+  if (!net) return F3_EINVAL;
+  if (enable && !net->timing) {
+    for (auto& e : net->tev)
+      if (!e && hipEventCreate(&e) != hipSuccess) return F3_EHIP;
+  }
+  if (ms) {  // the last forward + backward: gru_fwd l0, l1, ta_fwd l0, l1, ta_bwd l1, l0, gru_bwd l1, l0
+    if (!net->timing) return F3_ESTATE;
+    const int pairs[8][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {5, 6}, {6, 7}, {7, 8}, {9, 10}};
+    for (int i = 0; i < 8; ++i) {
+      if (hipEventSynchronize(net->tev[pairs[i][1]]) != hipSuccess ||
+          hipEventElapsedTime(&ms[i], net->tev[pairs[i][0]], net->tev[pairs[i][1]]) != hipSuccess)
+        return F3_EHIP;
+    }
+  }
+  net->timing = enable;
+  return F3_OK;
 }
 
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream) {

@@ -50,10 +50,10 @@ class adjGraph:  # noqa: N801  (reference name)
 
 
 class _NativeMusa:
-    def __init__(self, V, T, num_class):
+    def __init__(self, V, T, num_class, precision=0):
         L = lib()
         c = _lib.F3MusaConfig()
-        c.num_point, c.frames, c.num_class = V, T, num_class
+        c.num_point, c.frames, c.num_class, c.precision = V, T, num_class, precision
         h = ctypes.c_void_p()
         check(L.f3_musa_create(ctypes.byref(c), ctypes.byref(h)), "f3_musa_create")
         self.h = h
@@ -87,8 +87,14 @@ class Model(nn.Module):
     """musa_model.Model on the MI355X path (the driver's configuration)."""
 
     def __init__(self, num_class, num_point, max_frame, graph, bias, edge, block_size, embed_dim=64, n_stage=1,
-                 act_type="tanh", device=None, dropblock=True, seed=0, frames=30):
+                 act_type="tanh", device=None, dropblock=True, seed=0, frames=30, precision="fp32"):
+        """precision: "fp32" (fp32 MFMA; the parity mode) or "bf16" (the root main.py trains under bf16
+        autocast, Multimodal_Fall3/main.py:97: the streams' 1x1 convs on bf16 MFMA with fp32 accumulate;
+        depthwise convs, graph mix, BatchNorms, DropBlock and the head stay fp32)."""
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        object.__setattr__(self, "precision", precision)
         if (embed_dim, n_stage, act_type, bool(bias), bool(edge), block_size) != (64, 1, "tanh", True, True, 41):
             raise NotImplementedError("fall3 musa Model implements the driver's configuration (embed_dim 64, "
                                       "n_stage 1, act 'tanh', bias, edge, block_size 41; main.py:307-320)")
@@ -100,7 +106,7 @@ class Model(nn.Module):
         object.__setattr__(self, "frames", frames)
         object.__setattr__(self, "dropblock", bool(dropblock))
         object.__setattr__(self, "_gen", torch.Generator().manual_seed(int(seed)))
-        object.__setattr__(self, "_native", _NativeMusa(num_point, frames, num_class))
+        object.__setattr__(self, "_native", _NativeMusa(num_point, frames, num_class, 1 if precision == "bf16" else 0))
         object.__setattr__(self, "_op_id", ops.register(self))
         if device is None:
             device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")

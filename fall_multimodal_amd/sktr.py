@@ -35,10 +35,10 @@ SD_RATES = np.linspace(0, 0.5, NBLOCK)  # skeleton_transformer.py:380
 
 
 class _NativeSktr:
-    def __init__(self, V, T, M, num_class):
+    def __init__(self, V, T, M, num_class, precision=0):
         L = lib()
         c = _lib.F3SktrConfig()
-        c.num_joint, c.frames, c.persons, c.num_class = V, T, M, num_class
+        c.num_joint, c.frames, c.persons, c.num_class, c.precision = V, T, M, num_class, precision
         h = ctypes.c_void_p()
         check(L.f3_sktr_create(ctypes.byref(c), ctypes.byref(h)), "f3_sktr_create")
         self.h = h
@@ -73,8 +73,15 @@ class SkeletonTransformer(nn.Module):
 
     def __init__(self, in_channels: int = 3, n_joints: int = 14, seq_len: int = 30, num_classes: int = 11,
                  embedding_dim: int = 32, n_block: int = 6, head_dim: int = 16, n_heads: int = 8, persons: int = 1,
-                 device=None, dropout_p: float = 0.5, stochastic_depth: bool = True, seed: int = 0):
+                 device=None, dropout_p: float = 0.5, stochastic_depth: bool = True, seed: int = 0,
+                 precision: str = "fp32"):
+        """precision: "fp32" (fp32 MFMA GEMMs; the parity mode) or "bf16" (BASELINE config 5: the six
+        blocks' Linear layers - qkv, merge, FFN - on bf16 MFMA with fp32 accumulate; attention core,
+        BatchNorm3d, embedding and head stay fp32)."""
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        object.__setattr__(self, "precision", precision)
         if (in_channels, embedding_dim, n_block, head_dim, n_heads) != (3, 32, 6, 16, 8):
             raise NotImplementedError("fall3 SkeletonTransformer implements the reference configuration "
                                       "(in_channels 3, embedding_dim 32, 6 blocks, head_dim 16, 8 heads)")
@@ -85,7 +92,8 @@ class SkeletonTransformer(nn.Module):
         object.__setattr__(self, "dropout_p", float(dropout_p))
         object.__setattr__(self, "stochastic_depth", bool(stochastic_depth))
         object.__setattr__(self, "_gen", torch.Generator().manual_seed(int(seed)))
-        object.__setattr__(self, "_native", _NativeSktr(n_joints, seq_len, persons, num_classes))
+        object.__setattr__(self, "_native", _NativeSktr(n_joints, seq_len, persons, num_classes,
+                                                        1 if precision == "bf16" else 0))
         object.__setattr__(self, "_op_id", ops.register(self))
         if device is None:
             device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")

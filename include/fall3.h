@@ -180,6 +180,11 @@ int f3_targcn_forward(f3_targcn* net, int batch, const float* params, const floa
 /* grads (flat, params layout) are OVERWRITTEN with d(sum dout*out)/dparams of the last forward. */
 int f3_targcn_backward(f3_targcn* net, int batch, const float* params, const float* buffers, const float* dout,
                        float* grads, void* workspace, void* stream);
+/* Stage timing (measurement aid, no reference counterpart): enable != 0 records HIP events around the
+ * two GRU recurrences and the two TA layers of the following f3_targcn_forward / _backward calls on
+ * their stream; ms != NULL (after such a pair) waits for them and writes 8 durations in ms:
+ * gru_fwd l0, gru_fwd l1, ta_fwd l0, ta_fwd l1, ta_bwd l1, ta_bwd l0, gru_bwd l1, gru_bwd l0. */
+int f3_targcn_stage_times(f3_targcn* net, int enable, float* ms);
 /* loss = -(1/N) sum_i sum_c y_ic log_softmax(out_i)_c (soft targets, not renormalised);
  * dout = dloss/dout. loss is overwritten. */
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream);
@@ -198,6 +203,9 @@ typedef struct f3_musa_config {
   int num_point;   /* V (13..18; 14 = coco_cut) */
   int frames;      /* T (8..64; the motion stream has T-1) */
   int num_class;   /* <= 64 */
+  int precision;   /* F3_PRECISION_FP32 (0) or F3_PRECISION_BF16: the streams' 1x1 convs (graph conv,
+                      residuals, point convs, Sep_TCN) on bf16 MFMA with fp32 accumulate, activations fp32
+                      (the root main.py trains under bf16 autocast) */
 } f3_musa_config;
 
 typedef struct f3_musa f3_musa;
@@ -244,6 +252,8 @@ typedef struct f3_sktr_config {
   int frames;      /* T: temporal attention length (same set) */
   int persons;     /* M >= 1 */
   int num_class;   /* <= 64 */
+  int precision;   /* F3_PRECISION_FP32 (0) or F3_PRECISION_BF16: the 6 blocks' Linear layers (qkv, merge,
+                      FFN) on bf16 MFMA with fp32 accumulate, activations fp32 in HBM (cfg 5 in bf16) */
 } f3_sktr_config;
 
 typedef struct f3_sktr f3_sktr;

@@ -114,6 +114,42 @@ def test_sktr_step_with_dropout_and_stochastic_depth_vs_oracle(B):
     assert cos >= 0.99999
 
 
+def test_sktr_bf16_step_vs_oracle():
+    """BASELINE config 5 names SkeletonTransformer in bf16: the block Linears (qkv, merge, FFN) on
+    bf16 MFMA with fp32 accumulate, everything else fp32, at B=256 with dropout and stochastic depth,
+    against the fp32 oracle given the same draws. Gates ~2-3x the values measured on MI355X (recorded
+    in profiles/r03_parity_record.jsonl): logits within 2e-2, argmax agreement >= 0.98, loss within
+    2e-3, whole-gradient cosine >= 0.995."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    from tests.test_gpu_parity import _record
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    B = 256
+    st = sk.init_state(31)
+    x, label = sk.synthetic_clips(B, 14, 11, 77)
+    model = f3.SkeletonTransformer(device=d, precision="bf16")
+    model.load_state_dict(st)
+    step = f3.SktrStep(model, B)
+    sd = [1.0, 1.0, 1.0, 0.0, 1.25, 1.25, 1.5, 1.5, 0.0, 2.0, 0.0, 2.0, 1.0 / 0.6, 1.0 / 0.6, 1.0 / 0.6, 0.0, 2.0, 2.0]
+    seed = 12345
+    step.forward_backward(torch.from_numpy(x).to(d), torch.from_numpy(label).to(d), sd=sd, seed=seed)
+    out_ref, loss_ref, grads_ref = _oracle(st, x, label, sd, seed)
+    out = step.out.cpu().numpy()
+    err = float(np.abs(out - out_ref.numpy()).max())
+    agree = float((out.argmax(1) == out_ref.numpy().argmax(1)).mean())
+    ours = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters()}
+    a = np.concatenate([ours[k].reshape(-1) for k in grads_ref]).astype(np.float64)
+    r = np.concatenate([grads_ref[k].numpy().reshape(-1) for k in grads_ref]).astype(np.float64)
+    cos = float(a @ r / (np.linalg.norm(a) * np.linalg.norm(r)))
+    rec = {"model": "sktr", "precision": "bf16", "B": B, "max_abs_dlogit": err, "argmax_agreement": agree,
+           "grad_cosine": cos, "loss": float(step.loss.item()), "loss_ref": float(loss_ref)}
+    _record("sktr_bf16_parity", rec)
+    print(rec)
+    assert err < 2e-2 and agree >= 0.98, (err, agree)
+    assert abs(step.loss.item() - loss_ref.item()) < 2e-3
+    assert cos >= 0.995, cos
+
+
 def test_sktr_training_tracks_oracle():
     """Five fused steps (RMSprop lr 1e-3, dropout + stochastic depth drawn by the module): the loss
     trajectory follows the oracle's (1e-4) and the trained models agree on held-out clips (train-
