@@ -171,6 +171,15 @@ def roofline_kernels(dev, batch, V, precision):
                                                            st))
         out["wgrad_kernel"] = {"kernel": f"{kname} alone (partials left in the slab, C=256, T=8, N={N}, "
                                          f"V={V})", "ms": ms}
+        # the step's largest kernel share (profiles/r03_step_kernel_summary.txt): wgrad_big<4,2,4,4,64>,
+        # whose largest launch is tcn layer 5's weight gradient (stride 2, T 15 -> 8, C 256): the same
+        # 2*M*N*K as layer 6 (M = B*8*V output rows, K = 9*256)
+        T5 = 15
+        x5 = torch.randn(N, T5, V, C, device=dev).to(torch.bfloat16)
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight(L.ptr(dy), L.ptr(x5), L.ptr(dw), None, N, T5, V, C, C,
+                                                              KT, 2, 4, 1, st))
+        out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,64> + slab reduce (tcn 9x1 weight gradient incl. the split-K "
+                                     f"reduce, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms}
     pmc = {}
     if os.path.exists(ROOFLINE_PMC):
         with open(ROOFLINE_PMC) as f:
@@ -742,7 +751,8 @@ def main():
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
                        "ranks": world, "collective": "rccl all_reduce (2 buckets)" if world > 1 else None},
-            "roofline": roofs.get("wgrad", roofs["tcn_fwd"]),
+            "roofline": roofs.get("wgrad_l5", roofs["tcn_fwd"]),
+            "roofline_wgrad_l6": roofs.get("wgrad"),
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
             "roofline_graph_mix": mix,

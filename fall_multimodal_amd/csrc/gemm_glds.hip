@@ -1363,9 +1363,13 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
 }
 
 // wgrad_seg applies (see its comment): its NKS (4 or 5), 0 if not. F3_WGRAD_SEG: bit 0 stride-1
-// layers, bit 1 stride-2 layers (default both).
+// layers, bit 1 stride-2 layers. Off by default: measured on MI355X (B=256 step, serial launches)
+// it is SLOWER than the per-tap wgrad_big tiles it replaces - 61 us vs 35 us for the 64-channel
+// T=30 layers (one 64x64 tile: 256 splits of 4 units, whose 37.7 MB of partials and their
+// reduce, 15.7 us, outweigh the 9x smaller staging) and 83 us vs 53-62 us for the stride-2 layers -
+// and the step 5.94-6.01 -> 6.42 ms (profiles/r03_wgrad_seg_ab.txt).
 static int wgrad_seg_nks(const WgradArgs& a) {
-  static const int on = getenv("F3_WGRAD_SEG") ? atoi(getenv("F3_WGRAD_SEG")) : 3;
+  static const int on = getenv("F3_WGRAD_SEG") ? atoi(getenv("F3_WGRAD_SEG")) : 0;
   const ConvGeom& g = a.g;
   if (!a.dyb || !a.inb || !a.slab || !a.zero || a.outmap != WG_OUT_CONV || a.groups > 1 || g.transposed) return 0;
   if (g.KT != 9 || g.P != 4 || (g.S != 1 && g.S != 2) || !((on >> (g.S - 1)) & 1)) return 0;

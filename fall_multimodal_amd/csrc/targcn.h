@@ -73,6 +73,7 @@ struct GruBwdArgs {
 
 struct TaArgs {
   int B, V;
+  int b16;               // bf16 mode: the layer's products on bf16 MFMA (ta_fwd_mfma_kernel)
   const float* p;        // flat params
   long long off_vw, off_vb, off_c1w, off_c1b, off_c2w, off_c2b, off_lnw, off_lnb, off_lnffw, off_lnffb,
       off_f0w, off_f0b, off_f2w, off_f2b;

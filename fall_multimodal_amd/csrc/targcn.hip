@@ -1437,6 +1437,324 @@ __global__ __launch_bounds__(TA_THREADS) void ta_bwd_kernel(TaArgs a) {
   if (tid >= 128 && tid < 128 + T) atomic_add_f(G + a.off_c2b + tid - 128, gcb);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Transform.forward on bf16 MFMA (the bf16 mode; TA.py:40-69). One WAVE per (clip, node) sequence:
+// every product of the layer is a small GEMM over the sequence's 30 frames (padded to 32), done as
+// v_mfma_f32_16x16x32_bf16 tiles with bf16 operands in LDS and fp32 accumulators:
+//   Q = sum_j W1_j . X_j + b1   (conv1 (1,3) over T-as-channels: W1_j[t][t'] = conv1.weight[t][t'][0][j],
+//                                X_j[t'][c'] = x[t'][c'+j], read as the transposed x shifted by j rows)
+//   K likewise (conv2);  V = x . Wv^T + bv
+//   A = softmax(Q K^T / sqrt(C)) over the 30 valid columns;  O1 = A . V + x
+//   Y1 = LN(O1);  U = relu(Y1 . W0^T + b0);  F = U . W2^T + b2 + Y1;  out = LN(F)
+// LayerNorm and softmax reduce a row across the 16 lanes that share it (MFMA C layout: lane l holds
+// rows 4(l/16)+i of column l%16). The saved tensors are ta_fwd_kernel's (fp32, same layout), so the
+// backward reads either forward's output.
+// LDS: the layer's weights in bf16 once per workgroup, and per wave the sequence's x (row-major and
+// transposed), Q, K, V^T, P; Y1 and U reuse x's and Q's space.
+// ---------------------------------------------------------------------------------------------
+constexpr int TAM_WAVES = 4;
+constexpr int TAM_LD = 72;   // row stride (bf16) of [32][64] operands: 144-B rows, 16-B aligned
+constexpr int TAM_LT = 40;   // row stride of [.][32] operands
+constexpr int TAM_W1 = 3 * 32 * TAM_LT;          // one conv weight set [3][32 t][32 t'] (bf16)
+constexpr int TAM_WL = 64 * TAM_LD;              // one Linear weight [64 out][64 in] (bf16)
+constexpr int TAM_VEC = 10 * 64;                 // b1 b2 bv bf0 bf2 g1 be1 g2 be2 (fp32), 64 each
+constexpr int TAM_SEQ = 32 * TAM_LD * 3 + 66 * TAM_LT + 64 * TAM_LT + 32 * TAM_LT;  // per-wave bf16
+constexpr int TAM_LDS = (2 * TAM_W1 + 3 * TAM_WL) * 2 + TAM_VEC * 4 + TAM_WAVES * TAM_SEQ * 2;
+static_assert(TAM_LDS <= 160 * 1024, "TA MFMA LDS");
+
+// the wave's LDS writes complete (and are not moved) before its next LDS reads
+F3_DEV void tam_wsync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+F3_DEV f32x4 tam_mfma(bf16x8_t a, bf16x8_t b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
+// acc[x][y] (+)= A[32 x 32*KS] . B, A row-major (stride sa), B as Bt[n][k] row-major (stride sb)
+template <int NT, int KSTEPS>
+F3_DEV void tam_gemm(f32x4 (&acc)[2][NT], const __bf16* A, int sa, const __bf16* Bt, int sb, int fr, int fg) {
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    bf16x8_t fa[2], fb[NT];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) fa[x] = *reinterpret_cast<const bf16x8_t*>(A + (x * 16 + fr) * sa + ks * 32 + fg * 8);
+#pragma unroll
+    for (int y = 0; y < NT; ++y) fb[y] = *reinterpret_cast<const bf16x8_t*>(Bt + (y * 16 + fr) * sb + ks * 32 + fg * 8);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < NT; ++y) acc[x][y] = tam_mfma(fa[x], fb[y], acc[x][y]);
+  }
+}
+
+template <int NT>
+F3_DEV void tam_zero(f32x4 (&acc)[2][NT]) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// sum over the 16 lanes that share a row (lanes 16g .. 16g+15)
+F3_DEV float tam_rowsum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+F3_DEV float tam_rowmax(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// LayerNorm over the 64 columns of each row of acc (4 tiles x 16 lanes); writes the normalised
+// values back (xhat) and returns per-row rstd in rs[x][i]
+F3_DEV void tam_layernorm(f32x4 (&acc)[2][4], float (&rs)[2][4]) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) s += acc[x][y][i];
+      const float mean = tam_rowsum(s) * (1.f / C);
+      float q = 0.f;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const float d = acc[x][y][i] - mean;
+        acc[x][y][i] = d;
+        q += d * d;
+      }
+      const float r = rsqrtf(tam_rowsum(q) * (1.f / C) + 1e-5f);
+      rs[x][i] = r;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[x][y][i] *= r;
+    }
+}
+
+__global__ __launch_bounds__(64 * TAM_WAVES) void ta_fwd_mfma_kernel(TaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char tam_smem[];
+  __bf16* W1 = reinterpret_cast<__bf16*>(tam_smem);     // [3][32][TAM_LT]
+  __bf16* W2 = W1 + TAM_W1;
+  __bf16* Wv = W2 + TAM_W1;                               // [64][TAM_LD], [out][in]
+  __bf16* Wf0 = Wv + TAM_WL;
+  __bf16* Wf2 = Wf0 + TAM_WL;
+  float* vec = reinterpret_cast<float*>(Wf2 + TAM_WL);   // [10][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar sequence pointers
+  const float* P_ = a.p;
+  for (int i = tid; i < 3 * 32 * 32; i += 64 * TAM_WAVES) {
+    const int j = i / 1024, t = (i >> 5) & 31, u = i & 31;
+    const bool ok = t < T && u < T;
+    W1[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c1w + (t * T + u) * 3 + j] : 0.f);
+    W2[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c2w + (t * T + u) * 3 + j] : 0.f);
+  }
+  for (int i = tid; i < C * C; i += 64 * TAM_WAVES) {
+    const int o = i / C, k = i - o * C;
+    Wv[o * TAM_LD + k] = (__bf16)P_[a.off_vw + i];
+    Wf0[o * TAM_LD + k] = (__bf16)P_[a.off_f0w + i];
+    Wf2[o * TAM_LD + k] = (__bf16)P_[a.off_f2w + i];
+  }
+  for (int i = tid; i < 64; i += 64 * TAM_WAVES) {
+    vec[0 * 64 + i] = i < T ? P_[a.off_c1b + i] : 0.f;
+    vec[1 * 64 + i] = i < T ? P_[a.off_c2b + i] : 0.f;
+    vec[2 * 64 + i] = P_[a.off_vb + i];
+    vec[3 * 64 + i] = P_[a.off_f0b + i];
+    vec[4 * 64 + i] = P_[a.off_f2b + i];
+    vec[5 * 64 + i] = P_[a.off_lnw + i];
+    vec[6 * 64 + i] = P_[a.off_lnb + i];
+    vec[7 * 64 + i] = P_[a.off_lnffw + i];
+    vec[8 * 64 + i] = P_[a.off_lnffb + i];
+  }
+  // per-wave sequence buffers
+  __bf16* xa = reinterpret_cast<__bf16*>(vec + TAM_VEC) + wave * TAM_SEQ;  // [32][LD] x, later Y1
+  __bf16* Qs = xa + 32 * TAM_LD;                                            // [32][LD] Q, later U
+  __bf16* Ks = Qs + 32 * TAM_LD;                                            // [32][LD]
+  __bf16* xt = Ks + 32 * TAM_LD;                                            // [66][LT] x^T (rows 64, 65 zero)
+  __bf16* Vt = xt + 66 * TAM_LT;                                            // [64][LT] V^T
+  __bf16* Pm = Vt + 64 * TAM_LT;                                            // [32][LT] softmax
+  const int fr = lane & 15, fg = lane >> 4;
+  // zero the padding the GEMMs read but no sequence writes: x rows 30-31, x^T rows 64-65 and
+  // columns 30-31, V^T columns 30-31 (NaN garbage would survive a multiply by zero)
+  for (int i = lane; i < 2 * TAM_LD; i += 64) xa[30 * TAM_LD + i] = (__bf16)0.f;
+  for (int i = lane; i < 66 * TAM_LT; i += 64) xt[i] = (__bf16)0.f;
+  for (int i = lane; i < 64 * TAM_LT; i += 64) Vt[i] = (__bf16)0.f;
+  __syncthreads();
+  const int V = a.V, nseq = a.B * V;
+  for (int sq = blockIdx.x * TAM_WAVES + wave; sq < nseq; sq += gridDim.x * TAM_WAVES) {
+    const int b = sq / V, n = sq - b * V;
+    float* sv = a.save + (size_t)sq * TA_SAVE;
+    const float* xin = a.in + ((size_t)b * T * V + n) * C;  // row t at xin + t*V*C
+    const size_t rstride = (size_t)V * C;
+    // x (+ PE) into LDS, row-major and transposed; lane = channel
+#pragma unroll 2
+    for (int t = 0; t < T; ++t) {
+      float v = xin[t * rstride + lane];
+      if (a.pe) v += a.pe[t * C + lane];
+      const __bf16 h = (__bf16)v;
+      xa[t * TAM_LD + lane] = h;
+      xt[lane * TAM_LT + t] = h;
+    }
+    tam_wsync();  // (each wave works on its own LDS: LDS order within the wave is enough)
+    // ---- Q, K (conv (1,3) over T-as-channels), one at a time (register pressure) ----
+#pragma unroll 1
+    for (int w = 0; w < 2; ++w) {
+      f32x4 q[2][4];
+      tam_zero(q);
+      const __bf16* Wc = w ? W2 : W1;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) tam_gemm<4, 1>(q, Wc + j * 32 * TAM_LT, TAM_LT, xt + j * TAM_LT, TAM_LT, fr, fg);
+      __bf16* dst = w ? Ks : Qs;
+      float* svq = sv + (w ? TA_K : TA_Q);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = x * 16 + fg * 4 + i;
+          const float bt = vec[w * 64 + t];
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const int c = y * 16 + fr;
+            const float qv = c < CQ ? q[x][y][i] + bt : 0.f;
+            dst[t * TAM_LD + c] = (__bf16)qv;
+            if (t < T && c < CQ) svq[t * CQ + c] = qv;
+          }
+        }
+    }
+    {  // V = x Wv^T + bv, stored transposed [c][u] (a lane's 4 rows of one column: 4 consecutive u)
+      f32x4 v[2][4];
+      tam_zero(v);
+      tam_gemm<4, 2>(v, xa, TAM_LD, Wv, TAM_LD, fr, fg);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr, u0 = x * 16 + fg * 4;
+          const float bv = vec[2 * 64 + c];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float vv = v[x][y][i] + bv;
+            const bool ok = u0 + i < T;
+            Vt[c * TAM_LT + u0 + i] = ok ? (__bf16)vv : (__bf16)0.f;
+            if (ok) sv[TA_V + (u0 + i) * C + c] = vv;
+          }
+        }
+    }
+    tam_wsync();
+    // ---- A = softmax(Q K^T / sqrt(C)) over the valid 30 columns ----
+    f32x4 s[2][2];
+    tam_zero(s);
+    tam_gemm<2, 2>(s, Qs, TAM_LD, Ks, TAM_LD, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        const float s0 = s[x][0][i] * 0.125f;                           // column fr < 16 <= 30
+        const float s1 = fr + 16 < T ? s[x][1][i] * 0.125f : -INFINITY;  // column 16 + fr
+        const float m = tam_rowmax(fmaxf(s0, s1));
+        const float e0 = __expf(s0 - m), e1 = fr + 16 < T ? __expf(s1 - m) : 0.f;
+        const float inv = 1.f / tam_rowsum(e0 + e1);
+        const float p0 = e0 * inv, p1 = e1 * inv;
+        Pm[t * TAM_LT + fr] = (__bf16)p0;
+        Pm[t * TAM_LT + 16 + fr] = (__bf16)p1;
+        if (t < T) {
+          sv[TA_P + t * T + fr] = p0;
+          if (fr + 16 < T) sv[TA_P + t * T + 16 + fr] = p1;
+        }
+      }
+    tam_wsync();
+    // ---- O1 = A V + x; Y1 = LN(O1) ----
+    f32x4 o[2][4];
+    tam_zero(o);
+    tam_gemm<4, 1>(o, Pm, TAM_LT, Vt, TAM_LT, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = min(x * 16 + fg * 4 + i, T - 1);  // rows 30, 31: any finite value
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          float xv = xin[t * rstride + c];
+          if (a.pe) xv += a.pe[t * C + c];
+          o[x][y][i] += xv;
+        }
+      }
+    float r1[2][4];
+    tam_layernorm(o, r1);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          const float xh = o[x][y][i];
+          const float y1 = xh * vec[5 * 64 + c] + vec[6 * 64 + c];
+          if (t < T) sv[TA_X1 + t * C + c] = xh;
+          o[x][y][i] = y1;                       // keep Y1 (fp32) for the residual
+          xa[t * TAM_LD + c] = (__bf16)y1;       // and as the FF's A operand
+        }
+        if (t < T && fr == 0) sv[TA_R1 + t] = r1[x][i];
+      }
+    tam_wsync();
+    // ---- U = relu(Y1 W0^T + b0) ----
+    f32x4 u[2][4];
+    tam_zero(u);
+    tam_gemm<4, 2>(u, xa, TAM_LD, Wf0, TAM_LD, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          const float uv = fmaxf(u[x][y][i] + vec[3 * 64 + c], 0.f);
+          if (t < T) sv[TA_U + t * C + c] = uv;
+          Qs[t * TAM_LD + c] = (__bf16)uv;
+        }
+      }
+    tam_wsync();
+    // ---- F = U W2^T + b2 + Y1; out = LN(F) ----
+    f32x4 f[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) f[x][y] = o[x][y];
+    tam_gemm<4, 2>(f, Qs, TAM_LD, Wf2, TAM_LD, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const float bb = vec[4 * 64 + y * 16 + fr];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[x][y][i] += bb;
+      }
+    float r2[2][4];
+    tam_layernorm(f, r2);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        if (t >= T) continue;
+        float* orow = a.out + ((size_t)(b * T + t) * V + n) * C;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          const float xh = f[x][y][i];
+          sv[TA_F2 + t * C + c] = xh;
+          orow[c] = xh * vec[7 * 64 + c] + vec[8 * 64 + c];
+        }
+        if (fr == 0) sv[TA_R2 + t] = r2[x][i];
+      }
+    tam_wsync();
+  }
+}
+
 }  // namespace tg
 }  // namespace f3
 
@@ -1561,6 +1879,15 @@ static int ta_grid(const TaArgs& a) {
 }
 
 int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
+  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 1;
+  if (a->b16 && mfma_env) {  // bf16 mode: one wave per sequence on bf16 MFMA
+    static bool once_m = (allow_lds(ta_fwd_mfma_kernel, TAM_LDS), true);
+    (void)once_m;
+    const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAM_WAVES - 1) / TAM_WAVES));
+    hipLaunchKernelGGL(ta_fwd_mfma_kernel, dim3(grid), dim3(64 * TAM_WAVES), TAM_LDS, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   static bool once = (allow_lds(ta_fwd_kernel, TA_FWD_LDS), true);
   (void)once;
   hipLaunchKernelGGL(ta_fwd_kernel, dim3(ta_grid(*a)), dim3(TA_THREADS), TA_FWD_LDS, s, *a);

@@ -178,6 +178,7 @@ TaArgs ta_args(const f3_targcn* net, int l, int B, const float* params) {
   std::memset(&a, 0, sizeof(a));
   a.B = B;
   a.V = net->V;
+  a.b16 = net->prec == F3_PRECISION_BF16;
   a.p = params;
   const TaOff& t = net->ta[l];
   a.off_vw = t.vw; a.off_vb = t.vb; a.off_c1w = t.c1w; a.off_c1b = t.c1b; a.off_c2w = t.c2w; a.off_c2b = t.c2b;

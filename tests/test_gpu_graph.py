@@ -75,4 +75,8 @@ def test_captured_step_matches_eager(phased):
     tstep = f3.TrainStep(twin, B, lr=1e-3, phased=phased)
     ref = [float(tstep(sk, se, lbl).item()) for _ in range(3)]
     assert all(np.isfinite(losses)), losses
-    np.testing.assert_allclose(losses, ref, rtol=2e-3)
+    # step 1 is the same forward; after it the two runs differ by float-atomic ordering noise, which
+    # RMSprop's first steps amplify (lr*g/sqrt(v) ~ 10*lr*sign(g), also for gradients at rounding
+    # level): measured 2e-4 after one update, 0.4-0.8 % after two
+    np.testing.assert_allclose(losses[:2], ref[:2], rtol=1e-3)
+    np.testing.assert_allclose(losses[2], ref[2], rtol=2e-2)

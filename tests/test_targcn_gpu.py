@@ -78,10 +78,10 @@ def _oracle_grads(st, src, label):
 def test_targcn_step_vs_oracle(precision, B):
     """TargcnStep (native fwd + CE + bwd + RMSprop) vs the oracle on a ragged multi-tile batch.
     fp32: logits 1e-3 / identical argmax / every gradient within 2e-3 of its max (measured
-    4.5e-8 / 2e-6). bf16 (GEMM operands bf16, fp32 accumulate and state), gates ~4x the values
-    measured on MI355X (B=40 / 256: max|dlogit| 4.2e-5 / 4.8e-5, argmax agreement 1.0 / 1.0,
-    whole-gradient cosine 0.999995 / 0.999996): logits within 2e-4, argmax agreement >= 0.996,
-    cosine >= 0.9999."""
+    4.5e-8 / 2e-6). bf16 (GEMM operands bf16, fp32 accumulate and state; since round 3 the TA layers'
+    products too, on bf16 MFMA): logits within 5e-3, argmax agreement >= 0.99, cosine >= 0.999
+    (round 2, TA in fp32: 4.2e-5 / 4.8e-5, 1.0, 0.999995; the round-3 values are recorded in
+    profiles/r03_parity_record.jsonl)."""
     d = dev()
     import fall_multimodal_amd as f3
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -109,9 +109,13 @@ def test_targcn_step_vs_oracle(precision, B):
         assert rel[worst] < 2e-3, (worst, rel[worst])
         assert abs(step.loss.item() - loss_ref) < 1e-5
     else:
-        assert err < 2e-4 and agree >= 0.996
-        assert cos >= 0.9999
-        assert abs(step.loss.item() - loss_ref) < 1e-4
+        from tests.test_gpu_parity import _record
+        _record("targcn_bf16_parity", {"B": B, "max_abs_dlogit": err, "argmax_agreement": agree, "grad_cosine": cos,
+                                       "worst_grad_rel": [worst, rel[worst]], "loss": float(step.loss.item()),
+                                       "loss_ref": float(loss_ref)})
+        assert err < 5e-3 and agree >= 0.99
+        assert cos >= 0.999
+        assert abs(step.loss.item() - loss_ref) < 1e-3
 
 
 def test_targcn_training_tracks_oracle():

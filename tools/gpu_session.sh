@@ -4,7 +4,7 @@
 # step that faults, aborts or hits its limit (exit >= 124, 134, 139) ends it at once.
 #   tools/gpu_session.sh tests step_prof bench [pytest args for "tests" via PYTEST_ARGS]
 # Steps:
-#   tests       pytest -m gpu (PYTEST_ARGS overrides the selection)      -> gpurun_out/gpu_tests.log
+#   tests       pytest -m gpu over ${TESTS:-tests} (+ PYTEST_ARGS)         -> gpurun_out/gpu_tests.log
 #   step_prof   rocprofv3 kernel trace + stats of the bench step alone  -> gpurun_out/step_kernels.txt
 #   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
 #   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches  -> gpurun_out/roof_kernels.txt
@@ -12,6 +12,7 @@
 #   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
 #   bench_fp32  bench.py --precision fp32 --no-targcn                   -> gpurun_out/bench_fp32.json
 #   ab          tools/ab.sh env $AB_CFGS (eager bench A/B, optional serial profiles) -> gpurun_out/ab.log
+#   bench_tg    bench.py --model targcn per TG_CFGS config                -> gpurun_out/bench_tg_*.json
 #   smoke       __graft_entry__.smoke()
 #   py:<file>   python <file> (a tool script)                           -> gpurun_out/<name>.log
 set -o pipefail
@@ -36,7 +37,7 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case $step in
     tests)
-      run tests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+      run tests 900 python -u -m pytest ${TESTS:-tests} -m gpu -q --timeout 300 --timeout-method thread \
         ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
       tail -5 gpurun_out/gpu_tests.log ;;
     step_prof)
@@ -83,6 +84,13 @@ for step in "$@"; do
       grep -E "ms/step|==" gpurun_out/ab.log | head -40 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench_tg)  # the TARGCN (cfg 2) line alone, A/B over TG_CFGS (env assignments, "-" = defaults)
+      for cfg in ${TG_CFGS:--}; do
+        envs=(); [ "$cfg" != "-" ] && IFS=',' read -ra envs <<< "$cfg"
+        run "bench_tg[$cfg]" 300 env "${envs[@]}" python bench.py --model targcn --steps 10 --warmup 3 \
+          --no-cpu-baseline > "gpurun_out/bench_tg_${cfg//[^A-Za-z0-9]/_}.json" 2>> gpurun_out/bench_tg.err
+        cut -c1-300 "gpurun_out/bench_tg_${cfg//[^A-Za-z0-9]/_}.json"
+      done ;;
     py:*)
       f=${step#py:}
       n=$(basename "$f" .py)

@@ -23,11 +23,15 @@ _TAPS = os.environ.get("F3_WGRAD_TAPS", "1") != "0"
 _WG = "wgrad_taps<5>" if _TAPS else "wgrad_big<4, 2, 4, 4, 64>"
 _RED = "wgrad_taps_reduce_kernel" if _TAPS else "wgrad_slab_reduce_kernel"
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
-KERNELS = {"wgrad": [_WG, _RED], "wgrad_kernel": [_WG], "tcn_fwd": ["igemm_big<1, 2, 4, false, true," if os.environ.get("F3_BIG_WIN", "1") != "0" else "igemm_big<1, 1, 8,"]}
+KERNELS = {"wgrad": [_WG, _RED], "wgrad_kernel": [_WG],
+           "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_kernel"],
+           "tcn_fwd": ["igemm_big<1, 2, 4, false, true," if os.environ.get("F3_BIG_WIN", "1") != "0" else "igemm_big<1, 1, 8,"]}
 _SHAPE = "C=256, T=8, N=256, V=18"
 _KN = _WG.replace(", ", ",")
 NAMES = {"wgrad": f"{_KN} + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, {_SHAPE})",
          "wgrad_kernel": f"{_KN} alone (partials left in the slab, {_SHAPE})",
+         "wgrad_l5": "wgrad_big<4,2,4,4,64> + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, "
+                     "stride 2, C=256, T=15->8, N=256, V=18)",
          "tcn_fwd": f"igemm_big (clip window unless F3_BIG_WIN=0) bf16-out (tcn 9x1 fwd, {_SHAPE})"}
 
 
