@@ -1755,6 +1755,473 @@ __global__ __launch_bounds__(64 * TAM_WAVES) void ta_fwd_mfma_kernel(TaArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Transform backward on bf16 MFMA (the bf16 mode). One wave per sequence again, two waves per
+// workgroup. Every operand is kept ONCE, row-major, in LDS: a product that reduces over the rows of
+// an operand (the weight gradients, P^T dO, dS^T Q, the conv weight gradient) reads that operand's
+// fragments with gfx950's transposed LDS read (ds_read_b64_tr_b16: lane i of a 16-lane group gets
+// column i of 8 consecutive rows) instead of keeping transposed copies. The weight gradients of the
+// layer accumulate in each wave's registers across its sequences and are added once per wave at the
+// end (fp32 atomics); the input gradient is written per sequence.
+//   FF:   dF = LN2'(dY);  dU = (dF Wf2) . [U > 0];  dY1 = dU Wf0 + dF;  dO1 = LN1'(dY1)
+//         dWf2 += dF^T U;  dWf0 += dU^T Y1
+//   attn: dP = dO1 V^T;  dV = P^T dO1;  dS = P . (dP - rowsum(P . dP)) / sqrt(C)
+//         dQ = dS K;  dK = dS^T Q;  dWv += dV^T x;  dx = dO1 + dV Wv
+//   conv: dW1_j += dQ X_j^T (X_j[t'][c'] = x[t'][c'+j]);  dx[t'][c] += sum_j,t W1_j[t][t'] dQ[t][c-j]
+//         (and K with W2)
+// ---------------------------------------------------------------------------------------------
+constexpr int TAB_WAVES = 2;
+constexpr int TAB_R72 = 32 * TAM_LD;   // a [32][72] row-major operand (bf16)
+constexpr int TAB_R40 = 32 * TAM_LT;   // a [32][40] operand
+constexpr int TAB_T66 = 66 * TAM_LT;   // a [66][40] operand (two zero rows of padding)
+constexpr int TAB_SEQ = 6 * TAB_R72 + 2 * TAB_R40 + 3 * TAB_T66;
+constexpr int TAB_VEC = 4 * 64;        // g1, be1, g2 (fp32)
+constexpr int TAB_LDS = (2 * TAM_W1 + 3 * TAM_WL) * 2 + TAB_VEC * 4 + TAB_WAVES * TAB_SEQ * 2;
+static_assert(TAB_LDS <= 160 * 1024, "TA MFMA backward LDS");
+
+typedef short tab_s16x4 __attribute__((ext_vector_type(4)));
+
+// the two transposed reads of a B-style fragment: rows k0 + 8 fg .. +7 of column c0 + fr of a
+// row-major bf16 matrix with row stride ld (elements). The builtin (unlike inline asm) lets the
+// compiler fold the constant part of the address into the instruction's offset field and place the
+// lgkmcnt waits itself; with asm every fragment address became a live VGPR hoisted out of the
+// sequence loop and the kernel spilled. No global loads are in flight around these reads, so the
+// conservative vmcnt wait the builtin brings costs nothing here.
+typedef __attribute__((address_space(3))) tab_s16x4 tab_lds_s16x4;
+F3_DEV void tab_tr(const __bf16* base, int ld, int k0, int c0, int fr, int fg, tab_s16x4& lo, tab_s16x4& hi) {
+  const int tq = fr >> 2, tp = fr & 3;
+  const __bf16* p0 = base + (k0 + 8 * fg + tq) * ld + c0 + 4 * tp;
+  lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tab_lds_s16x4*)(p0));
+  hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tab_lds_s16x4*)(p0 + 4 * ld));
+}
+template <int N>
+F3_DEV void tab_trwait(tab_s16x4 (&)[N], tab_s16x4 (&)[N]) {}
+F3_DEV bf16x8_t tab_join(tab_s16x4 lo, tab_s16x4 hi) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// acc[x][y] (+)= A . B over K = 32*KSTEPS. Fragments: A either normal (A row-major [m][k], stride
+// sa) or transposed (A^T stored row-major [k][m]); B either normal (Bt row-major [n][k]) or
+// transposed (B stored row-major [k][n]). MT x NT tiles of 16.
+template <int MT, int NT, int KSTEPS, bool AT, bool BT>
+F3_DEV void tab_gemm(f32x4 (&acc)[MT][NT], const __bf16* A, int sa, const __bf16* B, int sb, int fr, int fg,
+                     int a_k0 = 0, int b_k0 = 0) {
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    bf16x8_t fa[MT], fb[NT];
+    tab_s16x4 lo[MT + NT], hi[MT + NT];
+#pragma unroll
+    for (int x = 0; x < MT; ++x) {
+      if (AT) tab_tr(A, sa, a_k0 + ks * 32, x * 16, fr, fg, lo[x], hi[x]);
+      else fa[x] = *reinterpret_cast<const bf16x8_t*>(A + (x * 16 + fr) * sa + a_k0 + ks * 32 + fg * 8);
+    }
+#pragma unroll
+    for (int y = 0; y < NT; ++y) {
+      if (BT) tab_tr(B, sb, b_k0 + ks * 32, y * 16, fr, fg, lo[MT + y], hi[MT + y]);
+      else fb[y] = *reinterpret_cast<const bf16x8_t*>(B + (y * 16 + fr) * sb + b_k0 + ks * 32 + fg * 8);
+    }
+    if (AT || BT) tab_trwait(lo, hi);
+#pragma unroll
+    for (int x = 0; x < MT; ++x)
+      if (AT) fa[x] = tab_join(lo[x], hi[x]);
+#pragma unroll
+    for (int y = 0; y < NT; ++y)
+      if (BT) fb[y] = tab_join(lo[MT + y], hi[MT + y]);
+#pragma unroll
+    for (int x = 0; x < MT; ++x)
+#pragma unroll
+      for (int y = 0; y < NT; ++y) acc[x][y] = tam_mfma(fa[x], fb[y], acc[x][y]);
+  }
+}
+
+template <int MT, int NT>
+F3_DEV void tab_zero(f32x4 (&acc)[MT][NT]) {
+#pragma unroll
+  for (int x = 0; x < MT; ++x)
+#pragma unroll
+    for (int y = 0; y < NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// store a [32 rows][16*NT cols] accumulator (rows x*16+4fg+i, cols y*16+fr) row-major as bf16
+template <int NT>
+F3_DEV void tab_store(__bf16* dst, int ld, const f32x4 (&acc)[2][NT], int fr, int fg) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < NT; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[(x * 16 + fg * 4 + i) * ld + y * 16 + fr] = (__bf16)acc[x][y][i];
+}
+// the same accumulator transposed ([col + roff][row], 4 consecutive rows of a lane = one 8-B store)
+template <int NT>
+F3_DEV void tab_store_t(__bf16* dst, int ld, int roff, const f32x4 (&acc)[2][NT], int fr, int fg) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < NT; ++y) {
+      bf16x4_t v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (__bf16)acc[x][y][i];
+      *reinterpret_cast<bf16x4_t*>(dst + (y * 16 + fr + roff) * ld + x * 16 + fg * 4) = v;
+    }
+}
+// load an fp32 [rows < nrow][ncol] matrix (row stride lds) into the accumulator layout, 0 outside
+template <int NT>
+F3_DEV void tab_load(f32x4 (&acc)[2][NT], const float* src, int lds, int nrow, int ncol, int fr, int fg) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < NT; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = x * 16 + fg * 4 + i, c = y * 16 + fr;
+        acc[x][y][i] = (r < nrow && c < ncol) ? src[r * lds + c] : 0.f;
+      }
+}
+
+// add a per-lane column accumulator (summed over the lane's rows) across the 4 row groups, then
+// one atomic per column
+F3_DEV void tab_flush_cols(float v, float* dst, int fg) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  if (fg == 0) atomic_add_f(dst, v);
+}
+
+// PART 1: the FF half (LN2', FF weight gradients, LN1') -> dO1 written into din (scratch);
+// PART 2: the attention and conv half, reading dO1 from din and overwriting it with dx. Two launches
+// keep each half's weight-gradient accumulators in registers without spilling.
+template <int PART>
+__global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char tab_smem[];
+  __bf16* W1 = reinterpret_cast<__bf16*>(tab_smem);     // [3][32 t][LT t'] (row-major W_j[t][t'])
+  __bf16* W2 = W1 + TAM_W1;
+  __bf16* Wv = W2 + TAM_W1;                               // [64 out][LD in]
+  __bf16* Wf0 = Wv + TAM_WL;
+  __bf16* Wf2 = Wf0 + TAM_WL;
+  float* vec = reinterpret_cast<float*>(Wf2 + TAM_WL);   // g1, be1, g2
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* P_ = a.p;
+  constexpr int NTH = 64 * TAB_WAVES;
+  for (int i = tid; i < 3 * 32 * 32; i += NTH) {
+    const int j = i / 1024, t = (i >> 5) & 31, u = i & 31;
+    const bool ok = t < T && u < T;
+    W1[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c1w + (t * T + u) * 3 + j] : 0.f);
+    W2[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c2w + (t * T + u) * 3 + j] : 0.f);
+  }
+  for (int i = tid; i < C * C; i += NTH) {
+    const int o = i / C, k = i - o * C;
+    Wv[o * TAM_LD + k] = (__bf16)P_[a.off_vw + i];
+    Wf0[o * TAM_LD + k] = (__bf16)P_[a.off_f0w + i];
+    Wf2[o * TAM_LD + k] = (__bf16)P_[a.off_f2w + i];
+  }
+  for (int i = tid; i < 64; i += NTH) {
+    vec[i] = P_[a.off_lnw + i];
+    vec[64 + i] = P_[a.off_lnb + i];
+    vec[128 + i] = P_[a.off_lnffw + i];
+  }
+  __bf16* sq0 = reinterpret_cast<__bf16*>(vec + TAB_VEC) + wave * TAB_SEQ;
+  __bf16* Bk = sq0;                 // K   (FF phase: dF)
+  __bf16* Bq = Bk + TAB_R72;        // Q   (FF phase: U)
+  __bf16* Bdv = Bq + TAB_R72;       // dV  (FF phase: dU)
+  __bf16* Bx = Bdv + TAB_R72;       // x   (FF phase: Y1)
+  __bf16* Bdo = Bx + TAB_R72;       // dO1
+  __bf16* Bv = Bdo + TAB_R72;       // V
+  __bf16* Bp = Bv + TAB_R72;        // P   [32][40]
+  __bf16* Bds = Bp + TAB_R40;       // dS  [32][40]
+  __bf16* Bxt = Bds + TAB_R40;      // x^T [66][40] (rows 64, 65 zero)
+  __bf16* Bdqt = Bxt + TAB_T66;     // dQ^T at rows 2.. [66][40] (rows 0, 1 zero)
+  __bf16* Bdkt = Bdqt + TAB_T66;    // dK^T likewise
+  __bf16* BdF = Bk;
+  __bf16* BU = Bq;
+  __bf16* BdU = Bdv;
+  __bf16* BY1 = Bx;
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int i = lane; i < TAB_SEQ; i += 64) sq0[i] = (__bf16)0.f;  // padding rows / columns stay zero
+  __syncthreads();
+  // weight-gradient accumulators (this wave's sequences)
+  f32x4 gA[4][4], gB[4][4];                 // PART 1: dWf2, dWf0;  PART 2: dWv (gA)
+  f32x4 gC1[PART == 2 ? 3 : 1][2][2], gC2[PART == 2 ? 3 : 1][2][2];
+  tab_zero(gA);
+  tab_zero(gB);
+#pragma unroll
+  for (int j = 0; j < (PART == 2 ? 3 : 1); ++j) {
+    tab_zero(gC1[j]);
+    tab_zero(gC2[j]);
+  }
+  float cg2[4] = {}, cbe2[4] = {}, cbf2[4] = {}, cbf0[4] = {}, cg1[4] = {}, cbe1[4] = {}, cbv[4] = {};
+  float rb1[2][4] = {}, rb2[2][4] = {};  // conv bias gradients per row t (summed over c')
+  const int V = a.V, nseq = a.B * V;
+  const size_t rstride = (size_t)V * C;
+#pragma unroll 1
+  for (int sq = blockIdx.x * TAB_WAVES + wave; sq < nseq; sq += gridDim.x * TAB_WAVES) {
+    // opaque copies of the lane coordinates: every lane-derived address is then recomputed per
+    // sequence instead of being hoisted out of the loop (dozens of live 64-bit offsets -> spills)
+    int fr = lane & 15, fg = lane >> 4;
+    asm volatile("" : "+v"(fr), "+v"(fg));
+    const int b = sq / V, n = sq - b * V;
+    const float* sv = a.save + (size_t)sq * TA_SAVE;
+    const float* xin = a.in + ((size_t)b * T * V + n) * C;
+    const float* dout = a.dout + ((size_t)b * T * V + n) * C;
+    f32x4 dF[2][4];
+    if constexpr (PART == 1) {
+    // ---------------- FF ----------------
+    f32x4 fh[2][4];
+    tab_load(fh, sv + TA_F2, C, T, C, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        const float r2 = t < T ? sv[TA_R2 + t] : 0.f;
+        float g[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          const float dy = t < T ? dout[t * rstride + c] : 0.f;
+          cg2[y] += dy * fh[x][y][i];
+          cbe2[y] += dy;
+          g[y] = dy * vec[128 + c];
+          s1 += g[y];
+          s2 += g[y] * fh[x][y][i];
+        }
+        const float m1 = tam_rowsum(s1) * (1.f / C), m2 = tam_rowsum(s2) * (1.f / C);
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          dF[x][y][i] = r2 * (g[y] - m1 - fh[x][y][i] * m2);
+          cbf2[y] += dF[x][y][i];
+        }
+      }
+    {
+      f32x4 u[2][4];
+      tab_load(u, sv + TA_U, C, T, C, fr, fg);
+      tab_store(BU, TAM_LD, u, fr, fg);  // the ReLU mask below reads U back (bf16 keeps the sign)
+    }
+    tab_store(BdF, TAM_LD, dF, fr, fg);
+    tam_wsync();
+    tab_gemm<4, 4, 1, true, true>(gA, BdF, TAM_LD, BU, TAM_LD, fr, fg);  // dWf2[c][k'] += sum_t dF[t][c] U[t][k']
+    f32x4 du[2][4];
+    tab_zero(du);
+    tab_gemm<2, 4, 2, false, true>(du, BdF, TAM_LD, Wf2, TAM_LD, fr, fg);  // dF Wf2
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool on = (float)BU[(x * 16 + fg * 4 + i) * TAM_LD + y * 16 + fr] > 0.f;
+          du[x][y][i] = on ? du[x][y][i] : 0.f;
+          cbf0[y] += du[x][y][i];
+        }
+    f32x4 y1[2][4];
+    tab_load(y1, sv + TA_X1, C, T, C, fr, fg);  // xhat1 -> Y1 = g1 xhat1 + be1
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y1[x][y][i] = y1[x][y][i] * vec[y * 16 + fr] + vec[64 + y * 16 + fr];
+    tam_wsync();  // all lanes read their U before dU / Y1 overwrite the neighbouring buffers
+    tab_store(BdU, TAM_LD, du, fr, fg);
+    tab_store(BY1, TAM_LD, y1, fr, fg);
+    tam_wsync();
+    tab_gemm<4, 4, 1, true, true>(gB, BdU, TAM_LD, BY1, TAM_LD, fr, fg);  // dWf0[k'][c] += sum_t dU[t][k'] Y1[t][c]
+    tab_gemm<2, 4, 2, false, true>(dF, BdU, TAM_LD, Wf0, TAM_LD, fr, fg);  // dY1 = dF + dU Wf0
+    // LN1 backward -> dO1 (into dF); y1 <- xhat1 again
+    tab_load(y1, sv + TA_X1, C, T, C, fr, fg);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        const float r1 = t < T ? sv[TA_R1 + t] : 0.f;
+        float g[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int c = y * 16 + fr;
+          cg1[y] += dF[x][y][i] * y1[x][y][i];
+          cbe1[y] += dF[x][y][i];
+          g[y] = dF[x][y][i] * vec[c];
+          s1 += g[y];
+          s2 += g[y] * y1[x][y][i];
+        }
+        const float m1 = tam_rowsum(s1) * (1.f / C), m2 = tam_rowsum(s2) * (1.f / C);
+#pragma unroll
+        for (int y = 0; y < 4; ++y) dF[x][y][i] = r1 * (g[y] - m1 - y1[x][y][i] * m2);
+      }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        if (t >= T) continue;
+        float* drow = a.din + ((size_t)(b * T + t) * V + n) * C;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) drow[y * 16 + fr] = dF[x][y][i];  // dO1 (scratch for PART 2)
+      }
+    tam_wsync();
+    continue;
+    } else {
+    // dO1 from PART 1 (din is overwritten with dx below, by this same wave)
+    tab_load(dF, a.din + ((size_t)b * T * V + n) * C, V * C, T, C, fr, fg);
+    }
+    // ---------------- attention ----------------
+    tab_store(Bdo, TAM_LD, dF, fr, fg);
+    {
+      f32x4 t4[2][4];
+      tab_load(t4, sv + TA_V, C, T, C, fr, fg);
+      tab_store(Bv, TAM_LD, t4, fr, fg);
+      tab_load(t4, sv + TA_K, CQ, T, CQ, fr, fg);
+      tab_store(Bk, TAM_LD, t4, fr, fg);
+      tab_load(t4, sv + TA_Q, CQ, T, CQ, fr, fg);
+      tab_store(Bq, TAM_LD, t4, fr, fg);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = min(x * 16 + fg * 4 + i, T - 1);
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            float xv = xin[t * rstride + y * 16 + fr];
+            if (a.pe) xv += a.pe[t * C + y * 16 + fr];
+            t4[x][y][i] = x * 16 + fg * 4 + i < T ? xv : 0.f;
+          }
+        }
+      tab_store(Bx, TAM_LD, t4, fr, fg);
+      tab_store_t(Bxt, TAM_LT, 0, t4, fr, fg);
+    }
+    f32x4 p[2][2];
+    tab_load(p, sv + TA_P, T, T, T, fr, fg);
+    tab_store(Bp, TAM_LT, p, fr, fg);
+    tam_wsync();
+    f32x4 dp[2][2];
+    tab_zero(dp);
+    tab_gemm<2, 2, 2, false, false>(dp, Bdo, TAM_LD, Bv, TAM_LD, fr, fg);  // dP = dO1 V^T
+    f32x4 dv[2][4];
+    tab_zero(dv);
+    tab_gemm<2, 4, 1, true, true>(dv, Bp, TAM_LT, Bdo, TAM_LD, fr, fg);   // dV = P^T dO1
+    // softmax backward (rows t, columns u; P is 0 outside the 30 x 30 block)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dot = tam_rowsum(p[x][0][i] * dp[x][0][i] + p[x][1][i] * dp[x][1][i]);
+#pragma unroll
+        for (int y = 0; y < 2; ++y) dp[x][y][i] = p[x][y][i] * (dp[x][y][i] - dot) * 0.125f;
+      }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cbv[y] += dv[x][y][i];
+    tab_store(Bds, TAM_LT, dp, fr, fg);
+    tab_store(Bdv, TAM_LD, dv, fr, fg);
+    tam_wsync();
+    tab_gemm<4, 4, 1, true, true>(gA, Bdv, TAM_LD, Bx, TAM_LD, fr, fg);  // dWv[c][c2] += sum_u dV[u][c] x[u][c2]
+    {
+      f32x4 dq[2][4];  // dQ = dS K, then dK = dS^T Q in the same registers
+      tab_zero(dq);
+      tab_gemm<2, 4, 1, false, true>(dq, Bds, TAM_LT, Bk, TAM_LD, fr, fg);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // summed over this lane's columns; the 16 lanes of a row add up at the end
+          rb1[x][i] += dq[x][0][i] + dq[x][1][i] + dq[x][2][i] + dq[x][3][i];
+      tab_store_t(Bdqt, TAM_LT, 2, dq, fr, fg);
+      tab_zero(dq);
+      tab_gemm<2, 4, 1, true, true>(dq, Bds, TAM_LT, Bq, TAM_LD, fr, fg);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb2[x][i] += dq[x][0][i] + dq[x][1][i] + dq[x][2][i] + dq[x][3][i];
+      tab_store_t(Bdkt, TAM_LT, 2, dq, fr, fg);
+    }
+    tam_wsync();
+    // conv weight gradients: dW_j[t][t'] += sum_c' dQ[t][c'] x[t'][c'+j] (A = dQ^T rows c'+2, B = x^T rows c'+j)
+#pragma unroll
+    for (int j = 0; j < (PART == 2 ? 3 : 0); ++j) {
+      tab_gemm<2, 2, 2, true, true>(gC1[j], Bdqt, TAM_LT, Bxt, TAM_LT, fr, fg, 2, j);
+      tab_gemm<2, 2, 2, true, true>(gC2[j], Bdkt, TAM_LT, Bxt, TAM_LT, fr, fg, 2, j);
+    }
+    // dx = dO1 (O1 = A V + x) + dV Wv + conv input gradients; dO1 in fp32 from din
+    f32x4 dx[2][4];
+    tab_load(dx, a.din + ((size_t)b * T * V + n) * C, V * C, T, C, fr, fg);
+    tab_gemm<2, 4, 2, false, true>(dx, Bdv, TAM_LD, Wv, TAM_LD, fr, fg);
+    // conv input gradients: dx[t'][c] += sum_j sum_t W_j[t][t'] dQ[t][c-j]  (B^T rows c-j+2 of dQ^T)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      tab_gemm<2, 4, 1, true, false>(dx, W1 + j * 32 * TAM_LT, TAM_LT, Bdqt + (2 - j) * TAM_LT, TAM_LT, fr, fg);
+      tab_gemm<2, 4, 1, true, false>(dx, W2 + j * 32 * TAM_LT, TAM_LT, Bdkt + (2 - j) * TAM_LT, TAM_LT, fr, fg);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = x * 16 + fg * 4 + i;
+        if (t >= T) continue;
+        float* drow = a.din + ((size_t)(b * T + t) * V + n) * C;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) drow[y * 16 + fr] = dx[x][y][i];
+      }
+    tam_wsync();
+  }
+  // ---------------- flush this wave's weight gradients ----------------
+  float* G = a.grads;
+  auto flush64 = [&](const f32x4 (&g)[4][4], long long off) {  // g rows = out (m), cols = in (n)
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomic_add_f(G + off + (x * 16 + fg * 4 + i) * C + y * 16 + fr, g[x][y][i]);
+  };
+  if constexpr (PART == 1) {
+    flush64(gA, a.off_f2w);
+    flush64(gB, a.off_f0w);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int c = y * 16 + fr;
+      tab_flush_cols(cg2[y], G + a.off_lnffw + c, fg);
+      tab_flush_cols(cbe2[y], G + a.off_lnffb + c, fg);
+      tab_flush_cols(cbf2[y], G + a.off_f2b + c, fg);
+      tab_flush_cols(cbf0[y], G + a.off_f0b + c, fg);
+      tab_flush_cols(cg1[y], G + a.off_lnw + c, fg);
+      tab_flush_cols(cbe1[y], G + a.off_lnb + c, fg);
+    }
+    return;
+  }
+  flush64(gA, a.off_vw);
+#pragma unroll
+  for (int j = 0; j < (PART == 2 ? 3 : 0); ++j)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = x * 16 + fg * 4 + i, u = y * 16 + fr;
+          if (t < T && u < T) {
+            atomic_add_f(G + a.off_c1w + (t * T + u) * 3 + j, gC1[j][x][y][i]);
+            atomic_add_f(G + a.off_c2w + (t * T + u) * 3 + j, gC2[j][x][y][i]);
+          }
+        }
+#pragma unroll
+  for (int y = 0; y < 4; ++y) tab_flush_cols(cbv[y], G + a.off_vb + y * 16 + fr, fg);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = x * 16 + fg * 4 + i;
+      const float s1 = tam_rowsum(rb1[x][i]), s2 = tam_rowsum(rb2[x][i]);
+      if (fr == 0 && t < T) {
+        atomic_add_f(G + a.off_c1b + t, s1);
+        atomic_add_f(G + a.off_c2b + t, s2);
+      }
+    }
+}
+
 }  // namespace tg
 }  // namespace f3
 
@@ -1879,8 +2346,9 @@ static int ta_grid(const TaArgs& a) {
 }
 
 int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
-  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 1;
-  if (a->b16 && mfma_env) {  // bf16 mode: one wave per sequence on bf16 MFMA
+  // F3_TA_MFMA (bf16 mode): bit 0 the MFMA forward, bit 1 the MFMA backward (default both)
+  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
+  if (a->b16 && (mfma_env & 1)) {  // bf16 mode: one wave per sequence on bf16 MFMA
     static bool once_m = (allow_lds(ta_fwd_mfma_kernel, TAM_LDS), true);
     (void)once_m;
     const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAM_WAVES - 1) / TAM_WAVES));
@@ -1896,6 +2364,17 @@ int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
 }
 
 int f3_tg_ta_bwd(const TaArgs* a, hipStream_t s) {
+  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
+  if (a->b16 && (mfma_env & 2)) {  // bf16 mode: one wave per sequence on bf16 MFMA
+    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, TAB_LDS), allow_lds(ta_bwd_mfma_kernel<2>, TAB_LDS), true);
+    (void)once_m;
+    const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAB_WAVES - 1) / TAB_WAVES));
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS, s, *a);
+    F3_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   static bool once = (allow_lds(ta_bwd_kernel, TA_BWD_LDS), true);
   (void)once;
   hipLaunchKernelGGL(ta_bwd_kernel, dim3(ta_grid(*a)), dim3(TA_THREADS), TA_BWD_LDS, s, *a);

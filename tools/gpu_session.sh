@@ -6,6 +6,9 @@
 # Steps:
 #   tests       pytest -m gpu over ${TESTS:-tests} (+ PYTEST_ARGS)         -> gpurun_out/gpu_tests.log
 #   step_prof   rocprofv3 kernel trace + stats of the bench step alone  -> gpurun_out/step_kernels.txt
+#   step_prof_ag  the same for the reference loop body through the custom ops -> gpurun_out/step_ag_*.txt
+#   step_prof_serial  the bench step with every queue joined (F3_SERIAL=1): per-kernel alone times
+#                     -> gpurun_out/step_serial_kernels.txt
 #   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
 #   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches  -> gpurun_out/roof_kernels.txt
 #   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the roofline launches -> gpurun_out/roofline_pmc.json
@@ -47,6 +50,21 @@ for step in "$@"; do
         > gpurun_out/step_kernels.txt 2>&1
       python tools/timeline.py gpurun_out/step/run_results.db --list > gpurun_out/step_timeline.txt 2>&1
       head -25 gpurun_out/step_kernels.txt ;;
+    step_prof_ag)
+      run step_prof_ag 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step_ag -o run -- \
+        python tools/step_only.py 8 autograd > gpurun_out/step_prof_ag.log 2>&1
+      python tools/prof_summary.py gpurun_out/step_ag/run_results.db --per-step 11 --top 60 \
+        > gpurun_out/step_ag_kernels.txt 2>&1
+      python tools/timeline.py gpurun_out/step_ag/run_results.db --list > gpurun_out/step_ag_timeline.txt 2>&1
+      head -25 gpurun_out/step_ag_kernels.txt ;;
+    step_prof_serial)
+      export F3_SERIAL=1
+      run step_prof_serial 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step_serial -o run -- \
+        python tools/step_only.py 8 > gpurun_out/step_prof_serial.log 2>&1
+      unset F3_SERIAL
+      python tools/prof_summary.py gpurun_out/step_serial/run_results.db --per-step 11 --top 80 \
+        > gpurun_out/step_serial_kernels.txt 2>&1
+      head -25 gpurun_out/step_serial_kernels.txt ;;
     step_pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         rm -rf gpurun_out/pmc_$C
