@@ -280,7 +280,58 @@ def sensor_bench(dev, precision="fp32"):
                      "ms_per_step": round(dt_step * 1e3, 4), "fwd_ms": round(dt_fwd * 1e3, 4),
                      "lstm_fwd_us_per_recurrent_step": round(dt_fwd * 1e6 / 30, 2),
                      "lstm_step_us_per_recurrent_step": round(dt_step * 1e6 / 30, 2)}
+        if name == "cfg1_cnn_bilstm":
+            res[name]["cnn1d"] = cnn1d_stage_times(model, step, x, lab, B, S)
+    m256 = f3.CNN_BiLSTM(device=dev)
+    x256 = torch.randn(256, 30, 4, generator=g).to(dev)
+    lab256 = torch.softmax(torch.randn(256, m256.spec.num_class, generator=g), 1).to(dev)
+    res["cnn1d_B256"] = cnn1d_stage_times(m256, f3.TrainStep(m256, 256, lr=1e-3), x256, lab256, 256, 4)
     return res
+
+
+def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
+    """GB/s of the sensor CNN1D launches (GSTCAN_UR_conv.ipynb:493-514: Conv1d(S->16,k5) BN ReLU
+    MaxPool, Conv1d(16->32,k5) BN ReLU MaxPool), from HIP events around each launch on the sensor
+    queue (f3_net_sensor_times), mean over `reps` steps. Algorithmic bytes (fp32, each tensor once):
+    conv fwd x + w + y; pool fwd y + p; conv bwd y + dp + x (+ dx for conv2) + dW. The tensors are
+    0.02-0.5 MB, so these launches are latency-bound (a few us each): the GB/s says how close to
+    launch latency they run, not to the 8 TB/s roofline."""
+    import ctypes
+    import fall_multimodal_amd._lib as FL
+    L, check = FL.lib(), FL.check
+    h = model._native.h
+    f32 = 4
+    shapes = [(T, S, 16), (T // 2, 16, 32)]  # (T_in, Ci, Co) per conv layer
+    acc = [0.0] * 6
+    check(L.f3_net_sensor_times(h, 1, None), "sensor times on")
+    for _ in range(3):
+        step(None, x, lab)
+    torch.cuda.synchronize()
+    ms = (ctypes.c_float * 6)()
+    for _ in range(reps):
+        step(None, x, lab)
+        check(L.f3_net_sensor_times(h, 1, ms), "sensor times")
+        for i in range(6):
+            acc[i] += ms[i] / reps
+    check(L.f3_net_sensor_times(h, 0, None), "sensor times off")
+    out = {}
+    names = ["conv1_fwd", "pool1_fwd", "conv2_fwd", "pool2_fwd", "conv2_bwd", "conv1_bwd"]
+    for i, nm in enumerate(names):
+        layer = 0 if nm.startswith(("conv1", "pool1")) else 1
+        Tl, Ci, Co = shapes[layer]
+        x_b, y_b, p_b, w_b = B * Tl * Ci * f32, B * Tl * Co * f32, B * (Tl // 2) * Co * f32, Co * Ci * 5 * f32
+        if nm.startswith("conv") and nm.endswith("fwd"):
+            nb = x_b + w_b + y_b
+        elif nm.startswith("pool"):
+            nb = y_b + p_b
+        else:
+            nb = y_b + p_b + x_b + 2 * w_b + (x_b if layer == 1 else 0)
+        us = acc[i] * 1e3
+        out[nm] = {"us": round(us, 2), "bytes": nb, "GBps": round(nb / (us * 1e-6) / 1e9, 1)}
+    out["batch"] = B
+    out["note"] = ("HIP events around each launch on the sensor queue; latency-bound (tensors of "
+                   "0.02-0.5 MB): GB/s against 8 TB/s is not a meaningful fraction at this size")
+    return out
 
 
 def eval_throughput(model, sk, se, reps=20):

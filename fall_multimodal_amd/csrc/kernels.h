@@ -108,6 +108,9 @@ int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);
 int f3_conv_gemm_bf16(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
 bool f3_igemm_ok(const f3::ConvGemmArgs& a);
 int f3_igemm_bf16(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
+// weight-stationary 64-channel 9-tap tcn (tcn64.hip); f3_igemm_bf16 dispatches to it
+bool f3_tcn64_ok(const f3::ConvGemmArgs& a, int epi);
+int f3_tcn64(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_igemm_big_ok(const f3::ConvGemmArgs& a);
 int f3_igemm_big(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_wgrad_glds_ok(const f3::WgradArgs& a);

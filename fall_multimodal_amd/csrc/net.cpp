@@ -89,7 +89,15 @@ struct f3_net {
   hipEvent_t ev_p1[4] = {nullptr, nullptr, nullptr, nullptr};
   int p1_mask = 0;  // bit i: ev_p1[i] recorded by the last phase-1 backward
   bool par_init = false, par_ok = false;
+  // f3_net_sensor_times: events around the sensor CNN1D launches (0 = off). Forward
+  // 0 | conv1 | 1 | pool1 | 2 | conv2 | 3 | pool2 | 4, backward 5 | conv2' | 6 | conv1' | 7
+  int stiming = 0;
+  hipEvent_t sev[8] = {};
+  void smark(int i, hipStream_t s) {
+    if (stiming && sev[i]) (void)hipEventRecord(sev[i], s);
+  }
   ~f3_net() {
+    for (auto& e : sev) if (e) (void)hipEventDestroy(e);
     for (auto& a : aux) if (a) (void)hipStreamDestroy(a);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : ev_p1) if (e) (void)hipEventDestroy(e);
@@ -1124,10 +1132,15 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     Conv1dArgs c1, c2;
     sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
     if (net->has_cnn) {
+      net->smark(0, ss);
       F3_TRY(f3_conv1d_fwd(&c1, ss));
+      net->smark(1, ss);
       F3_TRY(f3_bnrelupool_fwd(&c1, ss));
+      net->smark(2, ss);
       F3_TRY(f3_conv1d_fwd(&c2, ss));
+      net->smark(3, ss);
       F3_TRY(f3_bnrelupool_fwd(&c2, ss));
+      net->smark(4, ss);
       if (training) {
         add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
         add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
@@ -1249,13 +1262,36 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     F3_TRY(f3_shead_bwd(&sa, ss));
     F3_TRY(f3_lstm_bwd(&la, ss));
     if (net->has_cnn) {
+      net->smark(5, ss);
       F3_TRY(f3_conv1d_bwd(&c2, ss));
+      net->smark(6, ss);
       F3_TRY(f3_conv1d_bwd(&c1, ss));
+      net->smark(7, ss);
     }
   }
   F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0));
   if (phase == 1) return br.mark_phase1();  // the caller orders its all-reduce after f3_net_wait_phase1
   F3_TRY(br.join());
+  return F3_OK;
+}
+
+int f3_net_sensor_times(f3_net* net, int enable, float* ms) {
+  if (!net) return F3_EINVAL;
+  if (!net->has_cnn) return F3_EINVAL;
+  if (enable && !net->stiming) {
+    for (auto& e : net->sev)
+      if (!e && hipEventCreate(&e) != hipSuccess) return F3_EHIP;
+  }
+  if (ms) {  // conv1 fwd, pool1 fwd, conv2 fwd, pool2 fwd, conv2 bwd, conv1 bwd (ms)
+    if (!net->stiming) return F3_ESTATE;
+    const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {5, 6}, {6, 7}};
+    for (int i = 0; i < 6; ++i) {
+      if (hipEventSynchronize(net->sev[pairs[i][1]]) != hipSuccess ||
+          hipEventElapsedTime(&ms[i], net->sev[pairs[i][0]], net->sev[pairs[i][1]]) != hipSuccess)
+        return F3_EHIP;
+    }
+  }
+  net->stiming = enable;
   return F3_OK;
 }
 

@@ -11,6 +11,8 @@
 #include "common.h"
 #include "sensor.h"
 
+#include <algorithm>
+
 namespace f3 {
 
 constexpr int H = 64, G4 = 256;
@@ -536,107 +538,159 @@ __global__ __launch_bounds__(1024) void shead_bwd_p4(SHeadArgs a) {  // BatchNor
 
 // ----------------------------------------------------------------------------
 // CNN1D: Conv1d(k5,p2) -> BN (batch stats) -> ReLU -> MaxPool1d(2), twice
-// layout: [N][T][C] rows (time-major, channel contiguous)
+// (GSTCAN_UR_conv.ipynb:493-514; layout [N][T][C] rows, time-major, channel contiguous).
+// The tensors are tiny (B=256: 0.1-0.5 MB each), so these kernels are latency-bound; what they
+// avoid is contention: a block walks several clips with a FIXED channel per thread
+// (blockDim % Co == 0), keeps its BN / bias / weight-gradient partials in registers and adds
+// them to HBM once per block (the first version added fp64 per element: 2 atomics x N*T*Co on
+// Co addresses).
 // ----------------------------------------------------------------------------
-__global__ void conv1d_fwd_kernel(Conv1dArgs a) {
-  const int n = blockIdx.x;
-  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
-    const int t = i / a.Co, o = i - t * a.Co;
-    float acc = a.b[o];
+constexpr int C1D_THREADS = 256;
+constexpr int C1D_GRID = 128;   // conv backward: blocks (each walks N / 128 clips)
+constexpr int C1D_WMAX = 10;    // weight-gradient elements per thread: Co*Ci*5 <= 2560
+
+// sum v over the threads of one channel (tid % Co == o) and add it to dst[o] (fp64)
+F3_DEV void c1d_flush(float v, double* dst, float* red, int Co) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  red[tid] = v;
+  __syncthreads();
+  if (tid < Co) {
+    float s = 0.f;
+    for (int i = tid; i < C1D_THREADS; i += Co) s += red[i];
+    atomic_add_d(dst + tid, (double)s);
+  }
+}
+
+// one block per clip; the clip's input rows and the weights in LDS
+__global__ __launch_bounds__(C1D_THREADS) void conv1d_fwd_kernel(Conv1dArgs a) {
+  extern __shared__ float c1d_sm[];
+  float* ws = c1d_sm;                       // [Co][Ci][5]
+  float* xs = ws + a.Co * a.Ci * 5;         // [T][Ci]
+  float* red = xs + a.T * a.Ci;             // [256]
+  const int tid = threadIdx.x, n = blockIdx.x, o = tid % a.Co, TCo = a.T * a.Co, TCi = a.T * a.Ci;
+  for (int i = tid; i < a.Co * a.Ci * 5; i += C1D_THREADS) ws[i] = a.w[i];
+  for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  const float bo = a.b[o];
+  for (int i = tid; i < TCo; i += C1D_THREADS) {  // i % Co == o for every i of this thread
+    const int t = i / a.Co;
+    float acc = bo;
     for (int k = 0; k < 5; ++k) {
       const int ti = t + k - 2;
       if (ti < 0 || ti >= a.T) continue;
-      const float* xr = a.x + ((size_t)n * a.T + ti) * a.Ci;
-      for (int s = 0; s < a.Ci; ++s) acc += a.w[(o * a.Ci + s) * 5 + k] * xr[s];
+      const float* xr = xs + ti * a.Ci;
+      const float* wr = ws + o * a.Ci * 5 + k;
+      for (int c = 0; c < a.Ci; ++c) acc += wr[c * 5] * xr[c];
     }
-    a.y[((size_t)n * a.T + t) * a.Co + o] = acc;
-    atomic_add_d(a.st_sum + o, (double)acc);
-    atomic_add_d(a.st_sq + o, (double)acc * acc);
+    a.y[(size_t)n * TCo + i] = acc;
+    s1 += acc;
+    s2 += acc * acc;
+  }
+  c1d_flush(s1, a.st_sum, red, a.Co);
+  c1d_flush(s2, a.st_sq, red, a.Co);
+}
+
+__global__ __launch_bounds__(C1D_THREADS) void bnrelupool_fwd_kernel(Conv1dArgs a) {
+  const int Tp = a.T / 2, tot = a.N * Tp * a.Co;
+  for (int i = blockIdx.x * C1D_THREADS + threadIdx.x; i < tot; i += gridDim.x * C1D_THREADS) {
+    const int o = i % a.Co, r = i / a.Co, n = r / Tp, tp = r - n * Tp;
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn, o, sc, sh, mu, rs);
+    const float* y = a.y + ((size_t)n * a.T + 2 * tp) * a.Co + o;
+    a.p[i] = fmaxf(fmaxf(y[0] * sc + sh, 0.f), fmaxf(y[a.Co] * sc + sh, 0.f));
   }
 }
 
-__global__ void bnrelupool_fwd_kernel(Conv1dArgs a) {
-  const int n = blockIdx.x, Tp = a.T / 2;
-  for (int i = threadIdx.x; i < Tp * a.Co; i += blockDim.x) {
-    const int tp = i / a.Co, o = i - tp * a.Co;
-    float sc, sh, mu, rs;
-    bn_coeff(a.bn, o, sc, sh, mu, rs);
-    const float v0 = fmaxf(a.y[((size_t)n * a.T + 2 * tp) * a.Co + o] * sc + sh, 0.f);
-    const float v1 = fmaxf(a.y[((size_t)n * a.T + 2 * tp + 1) * a.Co + o] * sc + sh, 0.f);
-    a.p[((size_t)n * Tp + tp) * a.Co + o] = fmaxf(v0, v1);
-  }
-}
-
-// gradient through MaxPool + ReLU to the BN output, with BN-backward sums
-__global__ void bnrelupool_bwd_kernel(Conv1dArgs a) {
-  const int n = blockIdx.x, Tp = a.T / 2;
-  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
-    const int t = i / a.Co, o = i - t * a.Co;
-    float sc, sh, mu, rs;
-    bn_coeff(a.bn, o, sc, sh, mu, rs);
-    const float yv = a.y[((size_t)n * a.T + t) * a.Co + o];
+// gradient through MaxPool + ReLU to the BN output, with the BN-backward sums (one block per clip)
+__global__ __launch_bounds__(C1D_THREADS) void bnrelupool_bwd_kernel(Conv1dArgs a) {
+  __shared__ float red[C1D_THREADS];
+  const int tid = threadIdx.x, o = tid % a.Co, Tp = a.T / 2, TCo = a.T * a.Co, n = blockIdx.x;
+  float sc, sh, mu, rs;
+  bn_coeff(a.bn, o, sc, sh, mu, rs);
+  float s1 = 0.f, s2 = 0.f;
+  const float* yc = a.y + (size_t)n * TCo;
+  for (int i = tid; i < TCo; i += C1D_THREADS) {
+    const int t = i / a.Co;
+    const float yv = yc[i];
     float d = 0.f;
-    const int tp = t / 2;
+    const int tp = t >> 1;
     if (tp < Tp) {
-      const float v0 = fmaxf(a.y[((size_t)n * a.T + 2 * tp) * a.Co + o] * sc + sh, 0.f);
-      const float v1 = fmaxf(a.y[((size_t)n * a.T + 2 * tp + 1) * a.Co + o] * sc + sh, 0.f);
+      const float v0 = fmaxf(yc[(2 * tp) * a.Co + o] * sc + sh, 0.f);
+      const float v1 = fmaxf(yc[(2 * tp + 1) * a.Co + o] * sc + sh, 0.f);
       const int win = (v1 > v0) ? 1 : 0;  // first max wins ties (max_pool1d)
       const float me = fmaxf(yv * sc + sh, 0.f);
       if ((t & 1) == win && me > 0.f) d = a.dp[((size_t)n * Tp + tp) * a.Co + o];
     }
-    a.dy[((size_t)n * a.T + t) * a.Co + o] = d;
-    atomic_add_d(a.bsum + o, (double)d);
-    atomic_add_d(a.bsq + o, (double)d * ((yv - mu) * rs));
+    a.dy[(size_t)n * TCo + i] = d;
+    s1 += d;
+    s2 += d * ((yv - mu) * rs);
   }
+  c1d_flush(s1, a.bsum, red, a.Co);
+  c1d_flush(s2, a.bsq, red, a.Co);
 }
 
-// BN apply backward then conv1d backward (dx += , dW, db via atomics)
-__global__ void conv1d_bwd_kernel(Conv1dArgs a) {
-  extern __shared__ float dcs[];  // [T][Co]
-  const int n = blockIdx.x;
+// BN apply backward, then the conv1d backward: dx per clip, dW and db as per-thread register
+// partials over the block's clips (thread tid owns weight elements tid, tid + 256, ...)
+__global__ __launch_bounds__(C1D_THREADS) void conv1d_bwd_kernel(Conv1dArgs a) {
+  extern __shared__ float c1d_sm[];
+  float* dcs = c1d_sm;                    // [T][Co] pre-BN gradient of the clip
+  float* xs = dcs + a.T * a.Co;           // [T][Ci] the clip's conv input
+  float* ws = xs + a.T * a.Ci;            // [Co][Ci][5]
+  const int tid = threadIdx.x, TCo = a.T * a.Co, TCi = a.T * a.Ci, NW = a.Co * a.Ci * 5;
   const float M = a.bn.count;
-  for (int i = threadIdx.x; i < a.T * a.Co; i += blockDim.x) {
-    const int o = i % a.Co;
-    float sc, sh, mu, rs;
-    bn_coeff(a.bn, o, sc, sh, mu, rs);
-    const float yv = a.y[(size_t)n * a.T * a.Co + i];
-    const float xh = (yv - mu) * rs;
-    const float d = a.dy[(size_t)n * a.T * a.Co + i];
-    dcs[i] = a.bn.gamma[o] * rs * (d - (float)a.bsum[o] / M - xh * (float)a.bsq[o] / M);
-  }
-  __syncthreads();
-  if (n == 0) {
-    for (int o = threadIdx.x; o < a.Co; o += blockDim.x) {
+  float gw[C1D_WMAX], gb = 0.f;
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) gw[e] = 0.f;
+  for (int i = tid; i < NW; i += C1D_THREADS) ws[i] = a.w[i];
+  if (blockIdx.x == 0) {
+    for (int o = tid; o < a.Co; o += C1D_THREADS) {
       a.g_gamma[o] += (float)a.bsq[o];
       a.g_beta[o] += (float)a.bsum[o];
     }
   }
-  for (int i = threadIdx.x; i < a.Co; i += blockDim.x) {
-    float acc = 0.f;
-    for (int t = 0; t < a.T; ++t) acc += dcs[t * a.Co + i];
-    atomic_add_f(a.g_b + i, acc);
-  }
-  for (int i = threadIdx.x; i < a.Co * a.Ci * 5; i += blockDim.x) {
-    const int o = i / (a.Ci * 5), r = i - o * a.Ci * 5, s = r / 5, k = r - s * 5;
-    float acc = 0.f;
-    for (int t = 0; t < a.T; ++t) {
-      const int ti = t + k - 2;
-      if (ti < 0 || ti >= a.T) continue;
-      acc += dcs[t * a.Co + o] * a.x[((size_t)n * a.T + ti) * a.Ci + s];
+  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
+    __syncthreads();  // the previous clip's readers are done
+    for (int i = tid; i < TCo; i += C1D_THREADS) {
+      const int o = i % a.Co;
+      float sc, sh, mu, rs;
+      bn_coeff(a.bn, o, sc, sh, mu, rs);
+      const float xh = (a.y[(size_t)n * TCo + i] - mu) * rs;
+      const float d = a.dy[(size_t)n * TCo + i];
+      dcs[i] = a.bn.gamma[o] * rs * (d - (float)a.bsum[o] / M - xh * (float)a.bsq[o] / M);
     }
-    atomic_add_f(a.g_w + i, acc);
-  }
-  if (a.dx) {
-    for (int i = threadIdx.x; i < a.T * a.Ci; i += blockDim.x) {
-      const int ti = i / a.Ci, s = i - ti * a.Ci;
+    for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
+    __syncthreads();
+    if (tid < a.Co)
+      for (int t = 0; t < a.T; ++t) gb += dcs[t * a.Co + tid];
+#pragma unroll
+    for (int e = 0; e < C1D_WMAX; ++e) {
+      const int i = tid + e * C1D_THREADS;
+      if (i >= NW) break;
+      const int o = i / (a.Ci * 5), r = i - o * a.Ci * 5, c = r / 5, k = r - c * 5;
       float acc = 0.f;
-      for (int k = 0; k < 5; ++k) {
-        const int t = ti - k + 2;
-        if (t < 0 || t >= a.T) continue;
-        for (int o = 0; o < a.Co; ++o) acc += dcs[t * a.Co + o] * a.w[(o * a.Ci + s) * 5 + k];
-      }
-      a.dx[((size_t)n * a.T + ti) * a.Ci + s] = acc;
+      for (int t = max(0, 2 - k); t < min(a.T, a.T + 2 - k); ++t) acc += dcs[t * a.Co + o] * xs[(t + k - 2) * a.Ci + c];
+      gw[e] += acc;
     }
+    if (a.dx) {
+      for (int i = tid; i < TCi; i += C1D_THREADS) {
+        const int ti = i / a.Ci, c = i - ti * a.Ci;
+        float acc = 0.f;
+        for (int k = 0; k < 5; ++k) {
+          const int t = ti - k + 2;
+          if (t < 0 || t >= a.T) continue;
+          for (int o = 0; o < a.Co; ++o) acc += dcs[t * a.Co + o] * ws[(o * a.Ci + c) * 5 + k];
+        }
+        a.dx[(size_t)n * TCi + i] = acc;
+      }
+    }
+  }
+  if (tid < a.Co) atomic_add_f(a.g_b + tid, gb);
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) {
+    const int i = tid + e * C1D_THREADS;
+    if (i < NW) atomic_add_f(a.g_w + i, gw[e]);
   }
 }
 
@@ -717,22 +771,34 @@ int f3_shead_bwd(const SHeadArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
+static int c1d_grid(const Conv1dArgs& a) { return std::max(1, std::min(a.N, C1D_GRID)); }
+static bool c1d_ok(const Conv1dArgs& a) {
+  return a.Co >= 1 && C1D_THREADS % a.Co == 0 && a.Co * a.Ci * 5 <= C1D_WMAX * C1D_THREADS && a.T >= 1;
+}
+
 int f3_conv1d_fwd(const Conv1dArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(conv1d_fwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  if (!c1d_ok(*a)) return F3_EINVAL;
+  const size_t lds = ((size_t)a->Co * a->Ci * 5 + (size_t)a->T * a->Ci + C1D_THREADS) * 4;
+  hipLaunchKernelGGL(conv1d_fwd_kernel, dim3(a->N), dim3(C1D_THREADS), lds, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
 
 int f3_bnrelupool_fwd(const Conv1dArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(bnrelupool_fwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  const int tot = a->N * (a->T / 2) * a->Co;
+  if (tot <= 0) return F3_OK;
+  hipLaunchKernelGGL(bnrelupool_fwd_kernel, dim3(std::min((tot + C1D_THREADS - 1) / C1D_THREADS, 1024)),
+                     dim3(C1D_THREADS), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
 
 int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(bnrelupool_bwd_kernel, dim3(a->N), dim3(256), 0, s, *a);
+  if (!c1d_ok(*a)) return F3_EINVAL;
+  hipLaunchKernelGGL(bnrelupool_bwd_kernel, dim3(a->N), dim3(C1D_THREADS), 0, s, *a);
   F3_LAUNCH_CHECK();
-  hipLaunchKernelGGL(conv1d_bwd_kernel, dim3(a->N), dim3(256), (size_t)a->T * a->Co * 4, s, *a);
+  hipLaunchKernelGGL(conv1d_bwd_kernel, dim3(c1d_grid(*a)), dim3(C1D_THREADS),
+                     ((size_t)a->T * (a->Co + a->Ci) + (size_t)a->Co * a->Ci * 5) * 4, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -1770,14 +1770,22 @@ __global__ __launch_bounds__(64 * TAM_WAVES) void ta_fwd_mfma_kernel(TaArgs a) {
 //   conv: dW1_j += dQ X_j^T (X_j[t'][c'] = x[t'][c'+j]);  dx[t'][c] += sum_j,t W1_j[t][t'] dQ[t][c-j]
 //         (and K with W2)
 // ---------------------------------------------------------------------------------------------
-constexpr int TAB_WAVES = 2;
+constexpr int TAB_WAVES = 4;           // both halves use 256 VGPRs + ~220-256 AGPRs: one wave per SIMD
 constexpr int TAB_R72 = 32 * TAM_LD;   // a [32][72] row-major operand (bf16)
 constexpr int TAB_R40 = 32 * TAM_LT;   // a [32][40] operand
 constexpr int TAB_T66 = 66 * TAM_LT;   // a [66][40] operand (two zero rows of padding)
-constexpr int TAB_SEQ = 6 * TAB_R72 + 2 * TAB_R40 + 3 * TAB_T66;
 constexpr int TAB_VEC = 4 * 64;        // g1, be1, g2 (fp32)
-constexpr int TAB_LDS = (2 * TAM_W1 + 3 * TAM_WL) * 2 + TAB_VEC * 4 + TAB_WAVES * TAB_SEQ * 2;
-static_assert(TAB_LDS <= 160 * 1024, "TA MFMA backward LDS");
+// PART 1: Wf0, Wf2, vec shared; per wave two [32][72] slots (dF then Y1; U then dU)
+// PART 2: W1, W2, Wv shared; per wave S1..S3 [32][72], S4 [32][40], Sxt / Sdqt / Sdkt [66][40]
+//         (S1: dO1 then dV;  S2: V then K;  S3: x;  S4: P then dS;  Sdkt: Q then dK^T)
+constexpr int TAB_SH1 = 2 * TAM_WL * 2 + TAB_VEC * 4;
+constexpr int TAB_SEQ1 = 2 * TAB_R72;
+constexpr int TAB_SH2 = (2 * TAM_W1 + TAM_WL) * 2;
+constexpr int TAB_SEQ2 = 3 * TAB_R72 + TAB_R40 + 3 * TAB_T66;
+constexpr int TAB_LDS1 = TAB_SH1 + TAB_WAVES * TAB_SEQ1 * 2;
+constexpr int TAB_LDS2 = TAB_SH2 + TAB_WAVES * TAB_SEQ2 * 2;
+static_assert(TAB_LDS1 <= 160 * 1024 && TAB_LDS2 <= 160 * 1024, "TA MFMA backward LDS");
+static_assert(TAB_R72 <= TAB_T66, "Q is staged in the dK^T slot");
 
 typedef short tab_s16x4 __attribute__((ext_vector_type(4)));
 
@@ -1894,51 +1902,59 @@ F3_DEV void tab_flush_cols(float v, float* dst, int fg) {
 template <int PART>
 __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char tab_smem[];
-  __bf16* W1 = reinterpret_cast<__bf16*>(tab_smem);     // [3][32 t][LT t'] (row-major W_j[t][t'])
-  __bf16* W2 = W1 + TAM_W1;
-  __bf16* Wv = W2 + TAM_W1;                               // [64 out][LD in]
-  __bf16* Wf0 = Wv + TAM_WL;
-  __bf16* Wf2 = Wf0 + TAM_WL;
-  float* vec = reinterpret_cast<float*>(Wf2 + TAM_WL);   // g1, be1, g2
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* P_ = a.p;
   constexpr int NTH = 64 * TAB_WAVES;
-  for (int i = tid; i < 3 * 32 * 32; i += NTH) {
-    const int j = i / 1024, t = (i >> 5) & 31, u = i & 31;
-    const bool ok = t < T && u < T;
-    W1[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c1w + (t * T + u) * 3 + j] : 0.f);
-    W2[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c2w + (t * T + u) * 3 + j] : 0.f);
+  __bf16 *W1 = nullptr, *W2 = nullptr, *Wv = nullptr, *Wf0 = nullptr, *Wf2 = nullptr, *sq0;
+  float* vec = nullptr;
+  if constexpr (PART == 1) {
+    Wf0 = reinterpret_cast<__bf16*>(tab_smem);  // [64 out][LD in]
+    Wf2 = Wf0 + TAM_WL;
+    vec = reinterpret_cast<float*>(Wf2 + TAM_WL);  // g1, be1, g2
+    sq0 = reinterpret_cast<__bf16*>(tab_smem + TAB_SH1) + wave * TAB_SEQ1;
+    for (int i = tid; i < C * C; i += NTH) {
+      const int o = i / C, k = i - o * C;
+      Wf0[o * TAM_LD + k] = (__bf16)P_[a.off_f0w + i];
+      Wf2[o * TAM_LD + k] = (__bf16)P_[a.off_f2w + i];
+    }
+    for (int i = tid; i < 64; i += NTH) {
+      vec[i] = P_[a.off_lnw + i];
+      vec[64 + i] = P_[a.off_lnb + i];
+      vec[128 + i] = P_[a.off_lnffw + i];
+    }
+  } else {
+    W1 = reinterpret_cast<__bf16*>(tab_smem);  // [3][32 t][LT t'] (row-major W_j[t][t'])
+    W2 = W1 + TAM_W1;
+    Wv = W2 + TAM_W1;                         // [64 out][LD in]
+    sq0 = reinterpret_cast<__bf16*>(tab_smem + TAB_SH2) + wave * TAB_SEQ2;
+    for (int i = tid; i < 3 * 32 * 32; i += NTH) {
+      const int j = i / 1024, t = (i >> 5) & 31, u = i & 31;
+      const bool ok = t < T && u < T;
+      W1[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c1w + (t * T + u) * 3 + j] : 0.f);
+      W2[j * 32 * TAM_LT + t * TAM_LT + u] = (__bf16)(ok ? P_[a.off_c2w + (t * T + u) * 3 + j] : 0.f);
+    }
+    for (int i = tid; i < C * C; i += NTH) Wv[(i / C) * TAM_LD + i % C] = (__bf16)P_[a.off_vw + i];
   }
-  for (int i = tid; i < C * C; i += NTH) {
-    const int o = i / C, k = i - o * C;
-    Wv[o * TAM_LD + k] = (__bf16)P_[a.off_vw + i];
-    Wf0[o * TAM_LD + k] = (__bf16)P_[a.off_f0w + i];
-    Wf2[o * TAM_LD + k] = (__bf16)P_[a.off_f2w + i];
-  }
-  for (int i = tid; i < 64; i += NTH) {
-    vec[i] = P_[a.off_lnw + i];
-    vec[64 + i] = P_[a.off_lnb + i];
-    vec[128 + i] = P_[a.off_lnffw + i];
-  }
-  __bf16* sq0 = reinterpret_cast<__bf16*>(vec + TAB_VEC) + wave * TAB_SEQ;
-  __bf16* Bk = sq0;                 // K   (FF phase: dF)
-  __bf16* Bq = Bk + TAB_R72;        // Q   (FF phase: U)
-  __bf16* Bdv = Bq + TAB_R72;       // dV  (FF phase: dU)
-  __bf16* Bx = Bdv + TAB_R72;       // x   (FF phase: Y1)
-  __bf16* Bdo = Bx + TAB_R72;       // dO1
-  __bf16* Bv = Bdo + TAB_R72;       // V
-  __bf16* Bp = Bv + TAB_R72;        // P   [32][40]
-  __bf16* Bds = Bp + TAB_R40;       // dS  [32][40]
-  __bf16* Bxt = Bds + TAB_R40;      // x^T [66][40] (rows 64, 65 zero)
-  __bf16* Bdqt = Bxt + TAB_T66;     // dQ^T at rows 2.. [66][40] (rows 0, 1 zero)
-  __bf16* Bdkt = Bdqt + TAB_T66;    // dK^T likewise
-  __bf16* BdF = Bk;
-  __bf16* BU = Bq;
-  __bf16* BdU = Bdv;
-  __bf16* BY1 = Bx;
+  // PART 1 slots
+  __bf16* BdF = sq0;               // dF, then Y1
+  __bf16* BU = sq0 + TAB_R72;      // U, then dU
+  __bf16* BY1 = BdF;
+  __bf16* BdU = BU;
+  // PART 2 slots
+  __bf16* Bdo = sq0;                       // S1: dO1, then dV
+  __bf16* Bdv = Bdo;
+  __bf16* Bv = sq0 + TAB_R72;              // S2: V, then K
+  __bf16* Bk = Bv;
+  __bf16* Bx = sq0 + 2 * TAB_R72;          // S3: x
+  __bf16* Bp = sq0 + 3 * TAB_R72;          // S4: P [32][40], then dS
+  __bf16* Bds = Bp;
+  __bf16* Bxt = Bp + TAB_R40;              // x^T [66][40] (rows 64, 65 zero)
+  __bf16* Bdqt = Bxt + TAB_T66;            // dQ^T at rows 2.. (rows 0, 1 zero)
+  __bf16* Bdkt = Bdqt + TAB_T66;           // Q [32][72] first, then dK^T like dQ^T
+  __bf16* Bq = Bdkt;
   const int fr = lane & 15, fg = lane >> 4;
-  for (int i = lane; i < TAB_SEQ; i += 64) sq0[i] = (__bf16)0.f;  // padding rows / columns stay zero
+  for (int i = lane; i < (PART == 1 ? TAB_SEQ1 : TAB_SEQ2); i += 64) sq0[i] = (__bf16)0.f;
   __syncthreads();
   // weight-gradient accumulators (this wave's sequences)
   f32x4 gA[4][4], gB[4][4];                 // PART 1: dWf2, dWf0;  PART 2: dWv (gA)
@@ -2022,7 +2038,7 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int i = 0; i < 4; ++i) y1[x][y][i] = y1[x][y][i] * vec[y * 16 + fr] + vec[64 + y * 16 + fr];
-    tam_wsync();  // all lanes read their U before dU / Y1 overwrite the neighbouring buffers
+    tam_wsync();  // all lanes read their U (and the dF fragments) before dU / Y1 overwrite them
     tab_store(BdU, TAM_LD, du, fr, fg);
     tab_store(BY1, TAM_LD, y1, fr, fg);
     tam_wsync();
@@ -2068,29 +2084,23 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
     }
     // ---------------- attention ----------------
     tab_store(Bdo, TAM_LD, dF, fr, fg);
-    {
-      f32x4 t4[2][4];
-      tab_load(t4, sv + TA_V, C, T, C, fr, fg);
-      tab_store(Bv, TAM_LD, t4, fr, fg);
-      tab_load(t4, sv + TA_K, CQ, T, CQ, fr, fg);
-      tab_store(Bk, TAM_LD, t4, fr, fg);
-      tab_load(t4, sv + TA_Q, CQ, T, CQ, fr, fg);
-      tab_store(Bq, TAM_LD, t4, fr, fg);
+    f32x4 t4[2][4];
+    tab_load(t4, sv + TA_V, C, T, C, fr, fg);
+    tab_store(Bv, TAM_LD, t4, fr, fg);
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = min(x * 16 + fg * 4 + i, T - 1);
+      for (int i = 0; i < 4; ++i) {
+        const int t = min(x * 16 + fg * 4 + i, T - 1);
 #pragma unroll
-          for (int y = 0; y < 4; ++y) {
-            float xv = xin[t * rstride + y * 16 + fr];
-            if (a.pe) xv += a.pe[t * C + y * 16 + fr];
-            t4[x][y][i] = x * 16 + fg * 4 + i < T ? xv : 0.f;
-          }
+        for (int y = 0; y < 4; ++y) {
+          float xv = xin[t * rstride + y * 16 + fr];
+          if (a.pe) xv += a.pe[t * C + y * 16 + fr];
+          t4[x][y][i] = x * 16 + fg * 4 + i < T ? xv : 0.f;
         }
-      tab_store(Bx, TAM_LD, t4, fr, fg);
-      tab_store_t(Bxt, TAM_LT, 0, t4, fr, fg);
-    }
+      }
+    tab_store(Bx, TAM_LD, t4, fr, fg);
+    tab_store_t(Bxt, TAM_LT, 0, t4, fr, fg);
     f32x4 p[2][2];
     tab_load(p, sv + TA_P, T, T, T, fr, fg);
     tab_store(Bp, TAM_LT, p, fr, fg);
@@ -2116,8 +2126,13 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int i = 0; i < 4; ++i) cbv[y] += dv[x][y][i];
+    tam_wsync();  // dO1 / V / P fragments read by every lane: S1, S2, S4 are reused below
     tab_store(Bds, TAM_LT, dp, fr, fg);
     tab_store(Bdv, TAM_LD, dv, fr, fg);
+    tab_load(t4, sv + TA_K, CQ, T, CQ, fr, fg);
+    tab_store(Bk, TAM_LD, t4, fr, fg);
+    tab_load(t4, sv + TA_Q, CQ, T, CQ, fr, fg);
+    tab_store(Bq, TAM_LD, t4, fr, fg);
     tam_wsync();
     tab_gemm<4, 4, 1, true, true>(gA, Bdv, TAM_LD, Bx, TAM_LD, fr, fg);  // dWv[c][c2] += sum_u dV[u][c] x[u][c2]
     {
@@ -2136,7 +2151,9 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
       for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int i = 0; i < 4; ++i) rb2[x][i] += dq[x][0][i] + dq[x][1][i] + dq[x][2][i] + dq[x][3][i];
+      tam_wsync();  // Q read by every lane before dK^T replaces it
       tab_store_t(Bdkt, TAM_LT, 2, dq, fr, fg);
+      for (int i = lane; i < 2 * TAM_LT; i += 64) Bdkt[i] = (__bf16)0.f;  // the zero rows Q covered
     }
     tam_wsync();
     // conv weight gradients: dW_j[t][t'] += sum_c' dQ[t][c'] x[t'][c'+j] (A = dQ^T rows c'+2, B = x^T rows c'+j)
@@ -2366,12 +2383,12 @@ int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
 int f3_tg_ta_bwd(const TaArgs* a, hipStream_t s) {
   static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
   if (a->b16 && (mfma_env & 2)) {  // bf16 mode: one wave per sequence on bf16 MFMA
-    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, TAB_LDS), allow_lds(ta_bwd_mfma_kernel<2>, TAB_LDS), true);
+    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, TAB_LDS1), allow_lds(ta_bwd_mfma_kernel<2>, TAB_LDS2), true);
     (void)once_m;
     const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAB_WAVES - 1) / TAB_WAVES));
-    hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS, s, *a);
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS1, s, *a);
     F3_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS, s, *a);
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS2, s, *a);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }

@@ -33,13 +33,16 @@ def _view(ws, ptr, n, dtype):
     return ws[off:off + n * es].view(dtype)
 
 
-def test_asm_wait_kernels_inside_the_step():
+@pytest.mark.parametrize("layer,C,T", [(6, 256, 8), (1, 64, 30)])  # T: the position stream's frames
+def test_asm_wait_kernels_inside_the_step(layer, C, T):
+    """layer 6: igemm_big clip window + wgrad_taps; layer 1 (64 channels, T=30): the
+    weight-stationary tcn64 forward / input gradient (tcn64.hip) and wgrad_big."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import fall_multimodal_amd as f3
     import fall_multimodal_amd._lib as L
     d = torch.device("cuda")
-    B, V, S, C, T = 256, 18, 6, 256, 8
+    B, V, S = 256, 18, 6
     model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, S, device=d,
                                       precision="bf16")
     step = f3.TrainStep(model, B, lr=0.0)
@@ -49,10 +52,12 @@ def test_asm_wait_kernels_inside_the_step():
     torch.cuda.synchronize()
     lib, h = L.lib(), model._native.h
     params = dict(model.named_parameters())
-    M = B * T * V
     for si, pre in ((0, "stgcan_1"), (1, "stgcan_2")):
+        if T == 30:
+            T = 30 - si  # the motion stream (frame differences) has one frame less (combination.py:39)
+        M = B * T * V
         def t(what, n=M * C, dtype=torch.bfloat16):
-            p = lib.f3_net_debug_tensor(h, B, L.ptr(step.ws), si, 6, what.encode())
+            p = lib.f3_net_debug_tensor(h, B, L.ptr(step.ws), si, layer, what.encode())
             assert p, what
             return _view(step.ws, p, n, dtype)
 
@@ -61,7 +66,7 @@ def test_asm_wait_kernels_inside_the_step():
         dh = t("dh").float().view(B, T, V, C).permute(0, 3, 1, 2)
         g = t("g").float().view(B, T, V, C).permute(0, 3, 1, 2)
         dg = t("dg").float().view(B, T, V, C).permute(0, 3, 1, 2)
-        p = f"{pre}.st_gcan_networks.6."
+        p = f"{pre}.st_gcan_networks.{layer}."
         W = params[p + "tcn.2.weight"].detach().to(torch.bfloat16).float()
         bias = params[p + "tcn.2.bias"].detach()
         # forward (igemm_big clip window), bf16 output
