@@ -48,7 +48,15 @@ struct GruFwdArgs {
   void* UG;           // [R][IP] mixed update input S.[x,r*h]
   void* UI;           // [R][IP] update input [x,r*h]
   long long* prof;    // optional phase stamps (F3_TG_PROF), [T][8]
+  // node-partitioned recurrence (gru_fwd_node_kernel, bf16): per-step exchange of h and r*h
+  // between the workgroups of a clip group, and the groups' barrier counters (zeroed per launch)
+  unsigned short* hx;   // [B][V][H] bf16 h_t of every node
+  unsigned short* rhx;  // [B][V][H] bf16 r*h of every node
+  int* gsync;           // [GN_MAXG] counters, then an error flag
 };
+
+constexpr int GN_BT = 32;     // clips per group of the node-partitioned recurrence
+constexpr int GN_MAXG = 64;   // groups supported (B <= 2048)
 
 struct GruBwdArgs {
   int B, V, Din, I;
@@ -69,6 +77,11 @@ struct GruBwdArgs {
   void* DXG;          // [R][IP] d(mixed gate input)
   void* DUG;          // [R][IP] d(mixed update input)
   long long* prof;    // optional phase stamps (F3_TG_PROF), [T][8]
+  // node-partitioned backward (gru_bwd_node_kernel, bf16): the two per-step exchanges of every
+  // node's d(mixed input) rows, and the group barrier counters (zeroed per launch)
+  unsigned short* gx1;  // [B][V][IP] bf16 (update part)
+  unsigned short* gx2;  // [B][V][IP] bf16 (gate part)
+  int* gsync;           // [GN_MAXG] counters, then an error flag
 };
 
 struct TaArgs {

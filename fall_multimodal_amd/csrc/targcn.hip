@@ -437,6 +437,248 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Node-partitioned forward recurrence (bf16 mode; F3_GRU_NODE, default on). gru_fwd_kernel keeps
+// a clip tile and ALL nodes in one workgroup and re-streams the 17 node weight matrices from L2
+// every step (816 KB per step; measured 19 us of gate GEMM + 14 us of update GEMM per 42 us step,
+// profiles/r03_gru_phases.txt). Here a GROUP of V workgroups shares a tile of GN_BT clips and
+// workgroup (g, n) owns node n: its W_n tiles (gate z, r and update) and the Linear tiles of the
+// static branch stay in registers for all 30 steps (each of the 4 waves owns 16 hidden columns:
+// 6 x 4 bf16x8 fragments = 96 VGPRs). The node mixing S.[x, h] needs every node's h, so h and r*h
+// are exchanged through memory (hx, rhx) with two group barriers per step. The launch is
+// cooperative (all workgroups co-resident, or the launch fails and the clip-tile kernel runs);
+// a barrier that does not complete within ~2^22 polls sets the error flag and stops waiting, so a
+// fault shows as wrong results and a flag, never as a hang.
+// Numerics are those of gru_fwd_kernel: X = bf16([x, h]), Y = bf16(sum_m S[n][m] X_m) in fp32
+// in m order, fp32 MFMA accumulation, fp32 epilogue and saved tensors.
+// ---------------------------------------------------------------------------------------------
+constexpr int GN_THREADS = 256;
+constexpr int GN_XS = IP + 8;  // LDS row stride (bf16): 272-B rows
+
+F3_DEV void gn_barrier(int* cnt, int target, int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's exchange stores have reached L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // agent-scope release: the group's other XCDs see the stores
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int polls = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++polls > (1 << 22)) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __threadfence();  // acquire: no stale lines of the exchanged rows survive in this CU / XCD
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(GN_THREADS) void gru_fwd_node_kernel(GruFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ys[GN_BT * GN_XS];  // S.[x, h] (gate) / S.[x, r*h] (update)
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[GN_BT * GN_XS];  // [x, h] / [x, r*h] of node n
+  __shared__ float Sn[VMAX];
+  const int V = a.V, Din = a.Din, I = a.I;
+  const int NG = gridDim.x / V;
+  const int g = blockIdx.x % NG, n = blockIdx.x / NG;
+  const int b0 = g * GN_BT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, rq = lane >> 4, cw = 16 * w + col, kofs = 8 * rq;
+  int* cnt = a.gsync + g;
+  int* err = a.gsync + GN_MAXG;
+  for (int i = tid; i < GN_BT * GN_XS; i += GN_THREADS) {
+    Ys[i] = (__bf16)0.f;
+    Xs[i] = (__bf16)0.f;
+  }
+  for (int i = tid; i < V; i += GN_THREADS) Sn[i] = a.S[n * V + i];
+  // resident weight fragments of this wave's columns (B operands: lane holds W[k = kofs + j][col])
+  const __bf16* gWf = reinterpret_cast<const __bf16*>(a.g.Wf);
+  const __bf16* gLf = reinterpret_cast<const __bf16*>(a.g.Lf);
+  const __bf16* uWf = reinterpret_cast<const __bf16*>(a.u.Wf);
+  const __bf16* uLf = reinterpret_cast<const __bf16*>(a.u.Lf);
+  bf16x8_t wz[IP / 32], wr[IP / 32], wu[IP / 32], lz[IP / 32], lr[IP / 32], lu[IP / 32];
+#pragma unroll
+  for (int ks = 0; ks < IP / 32; ++ks) {
+    wz[ks] = ld8(gWf + ((size_t)n * 2 * H + cw) * IP + kofs + 32 * ks);
+    wr[ks] = ld8(gWf + ((size_t)n * 2 * H + H + cw) * IP + kofs + 32 * ks);
+    wu[ks] = ld8(uWf + ((size_t)n * H + cw) * IP + kofs + 32 * ks);
+    lz[ks] = ld8(gLf + (size_t)cw * IP + kofs + 32 * ks);
+    lr[ks] = ld8(gLf + (size_t)(H + cw) * IP + kofs + 32 * ks);
+    lu[ks] = ld8(uLf + (size_t)cw * IP + kofs + 32 * ks);
+  }
+  const float bz = a.g.bn[n * 2 * H + cw], br = a.g.bn[n * 2 * H + H + cw], bu = a.u.bn[n * H + cw];
+  const float blz = a.g.bl[cw], blr = a.g.bl[H + cw], blu = a.u.bl[cw];
+  const float csn = a.cs[n];
+  float h[2][4], z[2][4];  // own node's h and z of this lane's column, rows x*16 + 4rq + i
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[x][i] = z[x][i] = 0.f;
+  __syncthreads();
+  int nbar = 0;
+
+  // Y h-part (columns Din..Din+H) = sum_m S[n][m] src[m] (bf16 rows [B][V][H]); one (clip, 8-column
+  // chunk) per thread (GN_BT * H / 8 = 256)
+  auto mix_h = [&](const unsigned short* src, bool zero) {
+    const int b = tid >> 3, c8 = (tid & 7) * 8;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    if (!zero && b0 + b < a.B) {
+      const unsigned short* row = src + (size_t)(b0 + b) * V * H + c8;
+#pragma unroll 2
+      for (int m = 0; m < V; ++m) {
+        const bf16x8_t v = ld8(reinterpret_cast<const __bf16*>(row + (size_t)m * H));
+        const float sm = Sn[m];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += sm * (float)v[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Ys[b * GN_XS + Din + c8 + e] = (__bf16)acc[e];
+  };
+  // Y x-part and X x-part of step t (x rows [B][T][V][Din] fp32, rounded to bf16 as X is)
+  auto mix_x = [&](int t) {
+    if (Din % 4 == 0) {  // 16-B rows pieces (layer 1: x = layer 0's h)
+      const int D4 = Din / 4;
+      for (int q = tid; q < GN_BT * D4; q += GN_THREADS) {
+        const int b = q / D4, c = (q - b * D4) * 4;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f}, own[4] = {0.f, 0.f, 0.f, 0.f};
+        if (b0 + b < a.B) {
+          const float* xr = a.x + ((size_t)(b0 + b) * T + t) * V * Din + c;
+#pragma unroll 3
+          for (int m = 0; m < V; ++m) {
+            const f32x4 v4 = *reinterpret_cast<const f32x4*>(xr + (size_t)m * Din);
+            const float sm = Sn[m];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = (float)(__bf16)v4[e];
+              acc[e] += sm * v;
+              if (m == n) own[e] = v;
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          Ys[b * GN_XS + c + e] = (__bf16)acc[e];
+          Xs[b * GN_XS + c + e] = (__bf16)own[e];
+        }
+      }
+      return;
+    }
+    for (int q = tid; q < GN_BT * Din; q += GN_THREADS) {
+      const int b = q / Din, c = q - b * Din;
+      float acc = 0.f, own = 0.f;
+      if (b0 + b < a.B) {
+        const float* xr = a.x + ((size_t)(b0 + b) * T + t) * V * Din + c;
+        for (int m = 0; m < V; ++m) {
+          const float v = (float)(__bf16)xr[(size_t)m * Din];
+          acc += Sn[m] * v;
+          if (m == n) own = v;
+        }
+      }
+      Ys[b * GN_XS + c] = (__bf16)acc;
+      Xs[b * GN_XS + c] = (__bf16)own;
+    }
+  };
+  // rows of Xs / Ys -> the saved [R][IP] operand rows of this node (16-B pieces)
+  auto save_rows = [&](const __bf16* L, void* dst, int t) {
+    for (int q = tid; q < GN_BT * (IP / 8); q += GN_THREADS) {
+      const int b = q / (IP / 8), c = q - b * (IP / 8);
+      if (b0 + b >= a.B) continue;
+      const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(L + b * GN_XS + c * 8);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(reinterpret_cast<__bf16*>(dst) + R * IP + c * 8));
+    }
+  };
+
+  for (int t = 0; t < T; ++t) {
+    // ---- gate input: X = [x_t, h_{t-1}] of node n, Y = S.[x_t, h_{t-1}] ----
+    mix_x(t);
+    mix_h(a.hx, t == 0);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Xs[(x * 16 + 4 * rq + i) * GN_XS + Din + cw] = (__bf16)h[x][i];
+    __syncthreads();
+    save_rows(Xs, a.XI, t);
+    save_rows(Ys, a.XG, t);
+    // ---- gate: z, r of this wave's 16 columns ----
+    float rh[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      f32x4 gz = {0.f, 0.f, 0.f, 0.f}, gr = gz, sz = gz, sr = gz;
+      const __bf16* ay = Ys + (x * 16 + col) * GN_XS + kofs;
+      const __bf16* ax = Xs + (x * 16 + col) * GN_XS + kofs;
+#pragma unroll
+      for (int ks = 0; ks < IP / 32; ++ks) {
+        const bf16x8_t ya = ld8(ay + 32 * ks), xa = ld8(ax + 32 * ks);
+        gz = mfma8(ya, wz[ks], gz);
+        gr = mfma8(ya, wr[ks], gr);
+        sz = mfma8(xa, lz[ks], sz);
+        sr = mfma8(xa, lr[ks], sr);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = x * 16 + 4 * rq + i;
+        const float s_z = sz[i] * csn + blz, s_r = sr[i] * csn + blr;
+        const float zz = sigmoidf_(gz[i] + bz + s_z * sigmoidf_(s_z));
+        const float rr = sigmoidf_(gr[i] + br + s_r * sigmoidf_(s_r));
+        z[x][i] = zz;
+        rh[x][i] = rr * h[x][i];
+        if (b0 + b < a.B) {
+          const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+          __builtin_nontemporal_store(zz, &a.ZR[R * 2 * H + cw]);
+          __builtin_nontemporal_store(rr, &a.ZR[R * 2 * H + H + cw]);
+          __builtin_nontemporal_store(s_z, &a.SG[R * 2 * H + cw]);
+          __builtin_nontemporal_store(s_r, &a.SG[R * 2 * H + H + cw]);
+          a.rhx[((size_t)(b0 + b) * V + n) * H + cw] = __builtin_bit_cast(unsigned short, (__bf16)rh[x][i]);
+        }
+      }
+    }
+    gn_barrier(cnt, V * ++nbar, err);  // every node's r*h (and every wave's reads of Xs / Ys) done
+    // ---- update input: X = [x_t, r*h] of node n, Y = S.[x_t, r*h] (x parts unchanged) ----
+    mix_h(a.rhx, false);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Xs[(x * 16 + 4 * rq + i) * GN_XS + Din + cw] = (__bf16)rh[x][i];
+    __syncthreads();
+    save_rows(Xs, a.UI, t);
+    save_rows(Ys, a.UG, t);
+    // ---- update: hc, h ----
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      f32x4 gu = {0.f, 0.f, 0.f, 0.f}, su = gu;
+      const __bf16* ay = Ys + (x * 16 + col) * GN_XS + kofs;
+      const __bf16* ax = Xs + (x * 16 + col) * GN_XS + kofs;
+#pragma unroll
+      for (int ks = 0; ks < IP / 32; ++ks) {
+        gu = mfma8(ld8(ay + 32 * ks), wu[ks], gu);
+        su = mfma8(ld8(ax + 32 * ks), lu[ks], su);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = x * 16 + 4 * rq + i;
+        const float sv = su[i] * csn + blu;
+        const float hc = tanhf(gu[i] + bu + sv * sigmoidf_(sv));
+        const float hn = z[x][i] * h[x][i] + (1.f - z[x][i]) * hc;
+        h[x][i] = hn;
+        if (b0 + b < a.B) {
+          const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+          __builtin_nontemporal_store(hc, &a.HC[R * H + cw]);
+          __builtin_nontemporal_store(sv, &a.SU[R * H + cw]);
+          __builtin_nontemporal_store(hn, &a.Hout[R * H + cw]);
+          a.hx[((size_t)(b0 + b) * V + n) * H + cw] = __builtin_bit_cast(unsigned short, (__bf16)hn);
+        }
+      }
+    }
+    gn_barrier(cnt, V * ++nbar, err);  // every node's h_t (and every wave's reads of Xs / Ys) done
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Backward recurrence (BPTT) of one GRU layer: the input-gradient chain only. Per step the
 // pre-activation gradients (dP, cs*dSg, dU, cs*dSu) and the unmixed input gradients of both
 // EmbGCN products (dXG, dUG) go to HBM for the post-recurrence weight / support gradients.
@@ -729,6 +971,223 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
         }
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Node-partitioned backward recurrence (bf16 mode; F3_GRU_NODE bit 2, default on): the layout of
+// gru_fwd_node_kernel applied to gru_bwd_kernel's step. Workgroup (g, n) owns node n of a tile of
+// GN_BT clips: its Wb / Lb tiles (the input-gradient B operands of both EmbGCN products) stay in
+// registers, the element-wise epilogues touch only node n's rows, and the two S^T mixes of the
+// d(mixed input) rows (update, then gate) read every node's rows from the exchange buffers gx1 /
+// gx2 after a group barrier. Wave w owns hidden columns [16w, 16w+16) for the epilogues and
+// input-gradient columns [32w, 32w+32) for the GEMMs. Numerics as gru_bwd_kernel: bf16 A operands
+// and stored gradients, fp32 accumulation, DX = bf16(bf16(static) + sum_m S[m][n] GX_m).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(GN_THREADS) void gru_bwd_node_kernel(GruBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 AG[GN_BT * GN_XS];  // d pre-activation (gconv A)
+  __shared__ __attribute__((aligned(16))) __bf16 AS[GN_BT * GN_XS];  // cs * d static pre-activation
+  __shared__ __attribute__((aligned(16))) __bf16 GXs[GN_BT * GN_XS]; // this node's d mixed input
+  __shared__ __attribute__((aligned(16))) __bf16 DXs[GN_BT * GN_XS]; // this node's d input
+  __shared__ float Sc[VMAX];                                          // column n of S
+  const int V = a.V, Din = a.Din, I = a.I;
+  const int NG = gridDim.x / V;
+  const int g = blockIdx.x % NG, n = blockIdx.x / NG;
+  const int b0 = g * GN_BT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, rq = lane >> 4, cw = 16 * w + col, kofs = 8 * rq;
+  const bool has_dx = a.dX != nullptr && Din == H;
+  int* cnt = a.gsync + g;
+  int* err = a.gsync + GN_MAXG;
+  for (int i = tid; i < GN_BT * GN_XS; i += GN_THREADS) {
+    AG[i] = (__bf16)0.f;
+    AS[i] = (__bf16)0.f;
+    GXs[i] = (__bf16)0.f;
+    DXs[i] = (__bf16)0.f;
+  }
+  for (int i = tid; i < V; i += GN_THREADS) Sc[i] = a.S[i * V + n];
+  // resident B fragments: output columns i = 32w + 16y + col, k = o (update: H, gate: 2H)
+  const __bf16* gWb = reinterpret_cast<const __bf16*>(a.g.Wb);
+  const __bf16* gLb = reinterpret_cast<const __bf16*>(a.g.Lb);
+  const __bf16* uWb = reinterpret_cast<const __bf16*>(a.u.Wb);
+  const __bf16* uLb = reinterpret_cast<const __bf16*>(a.u.Lb);
+  bf16x8_t wu[2][H / 32], lu[2][H / 32], wg[2][2 * H / 32], lg[2][2 * H / 32];
+#pragma unroll
+  for (int y = 0; y < 2; ++y) {
+    const int i = 32 * w + 16 * y + col;
+#pragma unroll
+    for (int ks = 0; ks < H / 32; ++ks) {
+      wu[y][ks] = ld8(uWb + ((size_t)n * IP + i) * H + kofs + 32 * ks);
+      lu[y][ks] = ld8(uLb + (size_t)i * H + kofs + 32 * ks);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2 * H / 32; ++ks) {
+      wg[y][ks] = ld8(gWb + ((size_t)n * IP + i) * 2 * H + kofs + 32 * ks);
+      lg[y][ks] = ld8(gLb + (size_t)i * 2 * H + kofs + 32 * ks);
+    }
+  }
+  const float csn = a.cs[n];
+  __bf16* DP = reinterpret_cast<__bf16*>(a.DP);
+  __bf16* DSG = reinterpret_cast<__bf16*>(a.DSG);
+  __bf16* DU = reinterpret_cast<__bf16*>(a.DU);
+  __bf16* DSU = reinterpret_cast<__bf16*>(a.DSU);
+  float dh[2][4], dz[2][4], dxu[2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dh[x][i] = dz[x][i] = dxu[x][i] = 0.f;
+  __syncthreads();
+  int nbar = 0;
+
+  // GEMM: out[b][i] (i = 32w + 16y + col) = sum_k A[b][k] B[k][i] for the two products of one part
+  // (gconv A=AG with Wb, static A=AS with Lb), then GXs / DXs (bf16) and the exchange / save rows
+  auto part_gemm = [&](auto& wt, auto& lt, auto ksteps_tag) {
+    constexpr int KS = decltype(ksteps_tag)::value;
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      f32x4 gx[2], sx[2];
+#pragma unroll
+      for (int y = 0; y < 2; ++y) gx[y] = sx[y] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const __bf16* aa = AG + (x * 16 + col) * GN_XS + kofs;
+      const __bf16* as = AS + (x * 16 + col) * GN_XS + kofs;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8_t ga = ld8(aa + 32 * ks), sa = ld8(as + 32 * ks);
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          gx[y] = mfma8(ga, wt[y][ks], gx[y]);
+          sx[y] = mfma8(sa, lt[y][ks], sx[y]);
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = x * 16 + 4 * rq + i, c = 32 * w + 16 * y + col;
+          GXs[b * GN_XS + c] = (__bf16)gx[y][i];
+          DXs[b * GN_XS + c] = (__bf16)sx[y][i];
+        }
+    }
+  };
+  // this node's GXs rows -> the exchange buffer and the saved [R][IP] rows (16-B pieces)
+  auto emit_gx = [&](unsigned short* xch, void* save, int t) {
+    for (int q = tid; q < GN_BT * (IP / 8); q += GN_THREADS) {
+      const int b = q / (IP / 8), c = q - b * (IP / 8);
+      if (b0 + b >= a.B) continue;
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(GXs + b * GN_XS + c * 8);
+      *reinterpret_cast<u32x4*>(xch + ((size_t)(b0 + b) * V + n) * IP + c * 8) = v;
+      const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(reinterpret_cast<__bf16*>(save) + R * IP + c * 8));
+    }
+  };
+  // DXs[b][i] = bf16(DXs + sum_m S[m][n] GX_m[b][i]) over every node's exchanged rows (fp32 sum in m order)
+  auto mix_t = [&](const unsigned short* xch) {
+    for (int q = tid; q < GN_BT * (IP / 8); q += GN_THREADS) {
+      const int b = q / (IP / 8), c = (q - b * (IP / 8)) * 8;
+      float acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+      if (b0 + b < a.B && c < I) {
+        const unsigned short* rows = xch + (size_t)(b0 + b) * V * IP + c;
+#pragma unroll 2
+        for (int m = 0; m < V; ++m) {
+          const bf16x8_t v = ld8(reinterpret_cast<const __bf16*>(rows + (size_t)m * IP));
+          const float sm = Sc[m];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += sm * (float)v[e];
+        }
+      }
+      bf16x8_t o = ld8(DXs + b * GN_XS + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)o[e] + acc[e]);
+      *reinterpret_cast<bf16x8_t*>(DXs + b * GN_XS + c) = o;
+    }
+  };
+
+  for (int t = T - 1; t >= 0; --t) {
+    // ---- update part: h = z*hp + (1-z)*hc ----
+    float z[2][4], hp[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = x * 16 + 4 * rq + i;
+        float dU = 0.f, dsu = 0.f;
+        z[x][i] = hp[x][i] = 0.f;
+        if (b0 + b < a.B) {
+          const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+          const float zz = a.ZR[R * 2 * H + cw], hc = a.HC[R * H + cw], su = a.SU[R * H + cw];
+          const float hpp = t > 0 ? a.Hout[(R - V) * H + cw] : 0.f;
+          const float gg = dh[x][i] + a.dH[R * H + cw];
+          z[x][i] = zz;
+          hp[x][i] = hpp;
+          dz[x][i] = gg * (hpp - hc);
+          dU = gg * (1.f - zz) * (1.f - hc * hc);
+          dsu = dU * silu_grad(su) * csn;
+          dh[x][i] = gg * zz;
+          __builtin_nontemporal_store((__bf16)dU, &DU[R * H + cw]);
+          __builtin_nontemporal_store((__bf16)dsu, &DSU[R * H + cw]);
+        }
+        AG[b * GN_XS + cw] = (__bf16)dU;
+        AS[b * GN_XS + cw] = (__bf16)dsu;
+      }
+    __syncthreads();
+    part_gemm(wu, lu, std::integral_constant<int, H / 32>{});
+    __syncthreads();
+    emit_gx(a.gx1, a.DUG, t);
+    gn_barrier(cnt, V * ++nbar, err);  // every node's update-part GX rows
+    mix_t(a.gx1);
+    __syncthreads();
+    // ---- gate part ----
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = x * 16 + 4 * rq + i;
+        float dPz = 0.f, dPr = 0.f, dsz = 0.f, dsr = 0.f;
+        if (b0 + b < a.B) {
+          const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+          const float rr = a.ZR[R * 2 * H + H + cw], sgz = a.SG[R * 2 * H + cw], sgr = a.SG[R * 2 * H + H + cw];
+          const float drh = (float)DXs[b * GN_XS + Din + cw];
+          dh[x][i] += drh * rr;
+          if (has_dx) dxu[x][i] = (float)DXs[b * GN_XS + cw];
+          dPz = dz[x][i] * z[x][i] * (1.f - z[x][i]);
+          dPr = drh * hp[x][i] * rr * (1.f - rr);
+          dsz = dPz * silu_grad(sgz) * csn;
+          dsr = dPr * silu_grad(sgr) * csn;
+          __builtin_nontemporal_store((__bf16)dPz, &DP[R * 2 * H + cw]);
+          __builtin_nontemporal_store((__bf16)dPr, &DP[R * 2 * H + H + cw]);
+          __builtin_nontemporal_store((__bf16)dsz, &DSG[R * 2 * H + cw]);
+          __builtin_nontemporal_store((__bf16)dsr, &DSG[R * 2 * H + H + cw]);
+        }
+        AG[b * GN_XS + cw] = (__bf16)dPz;
+        AG[b * GN_XS + H + cw] = (__bf16)dPr;
+        AS[b * GN_XS + cw] = (__bf16)dsz;
+        AS[b * GN_XS + H + cw] = (__bf16)dsr;
+      }
+    __syncthreads();
+    part_gemm(wg, lg, std::integral_constant<int, 2 * H / 32>{});
+    __syncthreads();
+    emit_gx(a.gx2, a.DXG, t);
+    gn_barrier(cnt, V * ++nbar, err);  // every node's gate-part GX rows
+    mix_t(a.gx2);
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = x * 16 + 4 * rq + i;
+        if (b0 + b < a.B) {
+          dh[x][i] += (float)DXs[b * GN_XS + Din + cw];
+          if (has_dx) {
+            const size_t R = ((size_t)(b0 + b) * T + t) * V + n;
+            __builtin_nontemporal_store(dxu[x][i] + (float)DXs[b * GN_XS + cw], &a.dX[R * H + cw]);
+          }
+        }
+      }
+    __syncthreads();  // DXs / AG / AS are rewritten by the next step
   }
 }
 
@@ -2300,13 +2759,60 @@ static int gru_bwd_launch(const GruBwdArgs& a, hipStream_t s) {
   return F3_OK;
 }
 
+// node-partitioned forward (see gru_fwd_node_kernel): bf16 mode, exchange buffers present, a
+// cooperative launch of V x ceil(B / GN_BT) workgroups. Returns false (caller falls back to the
+// clip-tile kernel) when off (F3_GRU_NODE=0) or when the cooperative launch is refused.
+static bool gru_fwd_node(const GruFwdArgs& a, hipStream_t s) {
+  static const int on = getenv("F3_GRU_NODE") ? atoi(getenv("F3_GRU_NODE")) : 3;
+  const int NG = (a.B + GN_BT - 1) / GN_BT;
+  if (!(on & 1) || !a.hx || !a.rhx || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipMemsetAsync(a.gsync, 0, sizeof(int) * NG, s) != hipSuccess) return false;
+  GruFwdArgs arg = a;
+  void* params[] = {&arg};
+  const hipError_t e = hipLaunchCooperativeKernel((const void*)gru_fwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS),
+                                                  params, 0, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
+}
+
 int f3_tg_gru_fwd(const GruFwdArgs* a, int b16, hipStream_t s) {
   if (!f3_tg_gru_lds_ok(a->V) || a->I > IP || a->B < 1) return F3_EINVAL;
+  if (b16 && gru_fwd_node(*a, s)) return F3_OK;
   return b16 ? gru_fwd_launch<true>(*a, s) : gru_fwd_launch<false>(*a, s);
+}
+
+static bool gru_bwd_node(const GruBwdArgs& a, hipStream_t s) {
+  static const int on = getenv("F3_GRU_NODE") ? atoi(getenv("F3_GRU_NODE")) : 3;
+  const int NG = (a.B + GN_BT - 1) / GN_BT;
+  if (!(on & 2) || !a.gx1 || !a.gx2 || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipMemsetAsync(a.gsync, 0, sizeof(int) * NG, s) != hipSuccess) return false;
+  GruBwdArgs arg = a;
+  void* params[] = {&arg};
+  const hipError_t e = hipLaunchCooperativeKernel((const void*)gru_bwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS),
+                                                  params, 0, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
 }
 
 int f3_tg_gru_bwd(const GruBwdArgs* a, int b16, hipStream_t s) {
   if (!f3_tg_gru_lds_ok(a->V) || a->I > IP || a->B < 1) return F3_EINVAL;
+  if (b16 && gru_bwd_node(*a, s)) return F3_OK;
   return b16 ? gru_bwd_launch<true>(*a, s) : gru_bwd_launch<false>(*a, s);
 }
 

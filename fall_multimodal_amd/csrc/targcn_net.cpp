@@ -83,6 +83,7 @@ struct Plan {
   size_t ops[2][2][5];  // Wf, Wb, Lf, Lb, bn
   size_t H[2], ZR[2], SG[2], HC[2], SU[2], XG[2], XI[2], UG[2], UI[2];
   size_t ta_out0, ta_out1, ta_save[2], xm, pooled;
+  size_t hx, rhx, gsync, gx1, gx2;  // node-partitioned recurrences: exchange buffers, barrier counters
   // backward
   size_t dlog, dpooled, dY0, dH1, dH0, DP, DSG, DU, DSU, DXG, DUG;
   size_t zero_begin, dW[2][2][4], dS, dY1, zpage, zero_end;
@@ -124,6 +125,11 @@ Plan plan(const f3_targcn* net, int B) {
     p.UG[l] = take(es * R * IP);
     p.UI[l] = take(es * R * IP);
   }
+  p.hx = take(2 * (size_t)B * V * H);
+  p.rhx = take(2 * (size_t)B * V * H);
+  p.gsync = take(4 * (GN_MAXG + 1));
+  p.gx1 = take(2 * (size_t)B * V * IP);
+  p.gx2 = take(2 * (size_t)B * V * IP);
   p.ta_out0 = take(4 * R * C);
   p.ta_out1 = take(4 * R * C);
   for (int l = 0; l < 2; ++l) p.ta_save[l] = take(4 * (size_t)B * V * TA_SAVE);
@@ -312,6 +318,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     g.Hout = at<float>(ws, p.H[l]); g.ZR = at<float>(ws, p.ZR[l]); g.SG = at<float>(ws, p.SG[l]);
     g.HC = at<float>(ws, p.HC[l]); g.SU = at<float>(ws, p.SU[l]);
     g.XG = at<void>(ws, p.XG[l]); g.XI = at<void>(ws, p.XI[l]); g.UG = at<void>(ws, p.UG[l]); g.UI = at<void>(ws, p.UI[l]);
+    g.hx = at<unsigned short>(ws, p.hx); g.rhx = at<unsigned short>(ws, p.rhx); g.gsync = at<int>(ws, p.gsync);
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
@@ -401,6 +408,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     g.dX = l == 1 ? at<float>(ws, p.dH0) : nullptr;
     g.DP = at<void>(ws, p.DP); g.DSG = at<void>(ws, p.DSG); g.DU = at<void>(ws, p.DU); g.DSU = at<void>(ws, p.DSU);
     g.DXG = at<void>(ws, p.DXG); g.DUG = at<void>(ws, p.DUG);
+    g.gx1 = at<unsigned short>(ws, p.gx1); g.gx2 = at<unsigned short>(ws, p.gx2); g.gsync = at<int>(ws, p.gsync);
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
