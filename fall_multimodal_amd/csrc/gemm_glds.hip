@@ -432,6 +432,7 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
   if (f3_tcn64_ok(a, epi)) return f3_tcn64(args, epi, s);
+  if (f3_pw_ok(a, epi)) return f3_pw_gemm(args, epi, s);
   if (igemm_win_ok(a, epi)) {
     if (a.g.Nc == 128) return launch_igemm<4, 2, true>(a, epi, s);
     return launch_igemm<2, 2, true>(a, epi, s);

@@ -111,6 +111,9 @@ int f3_igemm_bf16(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 // weight-stationary 64-channel 9-tap tcn (tcn64.hip); f3_igemm_bf16 dispatches to it
 bool f3_tcn64_ok(const f3::ConvGemmArgs& a, int epi);
 int f3_tcn64(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
+// weight-stationary persistent 1x1 GEMM (pw_gemm.hip): gcn forward / input gradient, residual conv
+bool f3_pw_ok(const f3::ConvGemmArgs& a, int epi);
+int f3_pw_gemm(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_igemm_big_ok(const f3::ConvGemmArgs& a);
 int f3_igemm_big(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_wgrad_glds_ok(const f3::WgradArgs& a);

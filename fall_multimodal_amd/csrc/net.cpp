@@ -1375,6 +1375,29 @@ int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpac
   return f3_conv_gemm(&a, 0, 0, s);
 }
 
+int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void* out, int out_bf16, double* st_sum,
+                      double* st_sq, int N, int T_in, int T_out, int V, int Cin, int Cout, int stride, int transposed,
+                      int epi, void* stream) {
+  if (!x || !wpack || !out || N <= 0 || T_in <= 0 || T_out <= 0 || V <= 0 || (stride != 1 && stride != 2)) return F3_EINVAL;
+  if (epi != 0 && epi != EPI_BIAS && epi != (EPI_BIAS | EPI_STATS) && epi != (EPI_BIASV | EPI_STATS) && epi != EPI_ADD)
+    return F3_EINVAL;
+  if (transposed ? (T_in != (T_out - 1) / stride + 1) : (T_out != (T_in - 1) / stride + 1)) return F3_EINVAL;
+  if ((epi & EPI_ADD) && out_bf16) return F3_EINVAL;
+  if ((epi & EPI_STATS) && (!st_sum || !st_sq)) return F3_EINVAL;
+  if ((epi & (EPI_BIAS | EPI_BIASV)) && !bias) return F3_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, Cout, Cin, 1, stride, 0, transposed, T_out, T_in, V, Cin, Cout);
+  a.inb = (const unsigned short*)x;
+  a.wb = (const unsigned short*)wpack;
+  a.zero = test_zero_page();
+  if (out_bf16) a.outb = (unsigned short*)out;
+  else a.out = (float*)out;
+  a.bias = bias; a.st_sum = st_sum; a.st_sq = st_sq;
+  if (!f3_igemm_ok(a)) return F3_EINVAL;
+  return f3_igemm_bf16(&a, epi, (hipStream_t)stream);
+}
+
 int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;

@@ -112,14 +112,21 @@ def _net_setup(ctx, inputs, output):
 
 
 def _split_grads(m, grads):
-    """Views of the flat gradient in parameter order (the (offset, numel, shape) table is built once
-    per module)."""
+    """Views of the flat gradient in parameter order (the (shape, stride, offset) table is built once
+    per module; as_strided is the cheapest per-view call, ~1.3 us against ~3 us for slice + view)."""
     table = getattr(m, "_f3_grad_table", None)
     if table is None:
-        import numpy as np
-        table = [(off, int(np.prod(shape)), tuple(shape)) for _, shape, off in m.param_views()]
+        table = []
+        for _, shape, off in m.param_views():
+            shape = tuple(int(d) for d in shape)
+            stride, acc = [], 1
+            for d in reversed(shape):
+                stride.append(acc)
+                acc *= d
+            table.append((shape, tuple(reversed(stride)), int(off)))
         object.__setattr__(m, "_f3_grad_table", table)
-    return [grads[off:off + n].view(shape) for off, n, shape in table]
+    o0 = grads.storage_offset()
+    return [grads.as_strided(shape, stride, o0 + off) for shape, stride, off in table]
 
 
 def _net_backward(ctx, dout, dws, dbuf, dcnt):

@@ -35,10 +35,42 @@ class RMSprop(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, alpha=alpha, eps=eps))
 
     def _flat(self, group):
-        """(params, square_avg, grads) flat views covering the group, or None."""
+        """(params, square_avg, grads) flat views covering the group, or None. The full layout check
+        below is ~7 us of Python per parameter; once it has passed, the group remembers the layout
+        and later steps only check that the gradients are still views of one buffer at the same
+        relative offsets (the parameters and the flat square_avg do not move between steps)."""
         ps = group["params"]
         if not ps or any(p.grad is None for p in ps):
             return None
+        caches = self.__dict__.setdefault("_f3_flat", {})  # per group (not in param_groups: state_dict)
+        cache = caches.get(id(group))
+        if cache is not None:
+            hit = self._flat_cached(ps, cache)
+            if hit is not None:
+                return hit
+            del caches[id(group)]
+        flat = self._flat_full(ps)
+        if flat is not None:
+            p0 = min(ps, key=lambda t: t.storage_offset())
+            caches[id(group)] = (tuple(map(id, ps)), [p.storage_offset() - p0.storage_offset() for p in ps], flat[0],
+                                 flat[1], self.state[p0]["square_avg"], p0)
+        return flat
+
+    def _flat_cached(self, ps, cache):
+        ids, rel, flat_p, flat_sq, sq0, p0 = cache
+        if tuple(map(id, ps)) != ids or self.state[p0].get("square_avg") is not sq0:
+            return None
+        g0 = p0.grad
+        base = g0._base if g0._base is not None else g0
+        gbase = g0.storage_offset()
+        for p, r in zip(ps, rel):
+            g = p.grad
+            if (g._base if g._base is not None else g) is not base or g.storage_offset() - gbase != r \
+                    or not g.is_contiguous():
+                return None
+        return flat_p, flat_sq, _flat_view(g0, gbase, flat_p.numel())
+
+    def _flat_full(self, ps):
         ps = sorted(ps, key=lambda t: t.storage_offset())  # module order is not the flat order
         p0, g0 = ps[0], ps[0].grad
         if p0.dtype != torch.float32 or g0.dtype != torch.float32:

@@ -138,6 +138,18 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
 int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long slab_floats, int N, int T_in, int V,
                          int Cin, int Cout, int KT, int stride, int pad, void* stream);
 
+/* The 1x1 conv GEMM of the bf16 step with the step's epilogues (stgcan.py:50-56 gcn conv, its
+ * input gradient; stgcan.py:123-144 stride-2 residual conv and its input gradient), through the
+ * step's own dispatch (the weight-stationary pw_gemm kernel where the shape allows, else igemm).
+ * x bf16 [N,T_in,V,Cin] rows; wpack bf16 [Cout][Cin]; out [N,T_out,V,Cout], bf16 (out_bf16 = 1) or
+ * fp32. transposed = 0: forward, T_out = (T_in - 1) / stride + 1; transposed = 1: input gradient of a
+ * stride-`stride` 1x1 conv whose input had T_out frames. epi: 0 plain, 1 + bias[Cout], 5 + bias with
+ * BN sums, 6 + per-joint bias[V][Cout] with BN sums, 32 out += (fp32 out). st_sum / st_sq: fp64
+ * [Cout] sums of the fp32 outputs, accumulated (+=). */
+int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void* out, int out_bf16, double* st_sum,
+                      double* st_sq, int N, int T_in, int T_out, int V, int Cin, int Cout, int stride, int transposed,
+                      int epi, void* stream);
+
 /* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):
  * z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci]; backward gives dx and dA_eff (overwritten). */
 int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frames, int K, int V, int Cin,
