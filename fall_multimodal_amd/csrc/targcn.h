@@ -98,7 +98,20 @@ struct TaArgs {
   const float* dout;     // [B][T][V][C]
   float* din;            // [B][T][V][C]
   float* grads;          // flat grads (same offsets as p), accumulated
+  int dbg;               // measurement knob (F3_TA_DBG): 1 = skip the backward's weight-gradient flush
+  // backward weight gradients: each workgroup adds its waves' sums through LDS and stores them to
+  // part[blockIdx][TA_PART] (plain stores); ta_part_reduce then adds the workgroups' rows into grads.
+  // (Every wave's atomics into the same 64x64 matrices serialised at the end of the kernel.)
+  float* part;           // [TA_MAX_WG][TA_PART] or null (per-wave atomics)
 };
+
+// the backward's per-workgroup gradient row (PART 1 fields, then reused by PART 2):
+//   PART 1: dWf2 [64][64] | dWf0 [64][64] | lnffw lnffb f2b f0b lnw lnb [64] each
+//   PART 2: dWv [64][64] | dW conv1 [T][T][3] | dW conv2 [T][T][3] | vb [64] | c1b [32] | c2b [32]
+constexpr int TA_MAX_WG = 1024;
+constexpr int TA_PART1 = 2 * 4096 + 6 * 64;
+constexpr int TA_PART2 = 4096 + 2 * T * T * 3 + 64 + 2 * 32;
+constexpr int TA_PART = (TA_PART2 > TA_PART1 ? TA_PART2 : TA_PART1) + 32;
 
 // per-sequence saved block: q, k [T][CQ], v [T][C], P [T][T], xhat1 [T][C], u [T][C],
 // fhat2 [T][C], rstd1 [T], rstd2 [T]

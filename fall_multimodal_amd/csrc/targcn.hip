@@ -19,6 +19,7 @@
 #include "targcn.h"
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 namespace f3 {
@@ -2041,16 +2042,27 @@ __global__ __launch_bounds__(64 * TAM_WAVES) void ta_fwd_mfma_kernel(TaArgs a) {
   __syncthreads();
   const int V = a.V, nseq = a.B * V;
   for (int sq = blockIdx.x * TAM_WAVES + wave; sq < nseq; sq += gridDim.x * TAM_WAVES) {
+    // opaque copies of the lane coordinates (as in ta_bwd_mfma_kernel): the weight fragments are read
+    // from LDS per sequence instead of being hoisted out of the loop, which held ~180 registers and
+    // left none for the x rows below
+    int fr = lane & 15, fg = lane >> 4;
+    asm volatile("" : "+v"(fr), "+v"(fg));
     const int b = sq / V, n = sq - b * V;
     float* sv = a.save + (size_t)sq * TA_SAVE;
     const float* xin = a.in + ((size_t)b * T * V + n) * C;  // row t at xin + t*V*C
     const size_t rstride = (size_t)V * C;
-    // x (+ PE) into LDS, row-major and transposed; lane = channel
-#pragma unroll 2
+    // x (+ PE) into LDS, row-major and transposed; lane = channel. All 30 rows are loaded before the
+    // first is used (one memory round trip per sequence instead of 15 dependent pairs)
+    float xr[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) xr[t] = xin[t * rstride + lane];
+    if (a.pe) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) xr[t] += a.pe[t * C + lane];
+    }
+#pragma unroll
     for (int t = 0; t < T; ++t) {
-      float v = xin[t * rstride + lane];
-      if (a.pe) v += a.pe[t * C + lane];
-      const __bf16 h = (__bf16)v;
+      const __bf16 h = (__bf16)xr[t];
       xa[t * TAM_LD + lane] = h;
       xt[lane * TAM_LT + t] = h;
     }
@@ -2243,6 +2255,7 @@ constexpr int TAB_SH2 = (2 * TAM_W1 + TAM_WL) * 2;
 constexpr int TAB_SEQ2 = 3 * TAB_R72 + TAB_R40 + 3 * TAB_T66;
 constexpr int TAB_LDS1 = TAB_SH1 + TAB_WAVES * TAB_SEQ1 * 2;
 constexpr int TAB_LDS2 = TAB_SH2 + TAB_WAVES * TAB_SEQ2 * 2;
+constexpr int TAB_RED_LDS = (4 * 4096 + 4 * 64 + 2 * 4 * 32) * 4;  // the workgroup gradient reduction
 static_assert(TAB_LDS1 <= 160 * 1024 && TAB_LDS2 <= 160 * 1024, "TA MFMA backward LDS");
 static_assert(TAB_R72 <= TAB_T66, "Q is staged in the dK^T slot");
 
@@ -2644,6 +2657,94 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
     tam_wsync();
   }
   // ---------------- flush this wave's weight gradients ----------------
+  if (a.dbg & 1) return;  // measurement only (F3_TA_DBG=1): results are wrong
+  if (a.part) {  // workgroup sums through LDS -> this workgroup's row of the partial slab
+    float* red = reinterpret_cast<float*>(tab_smem);  // [4 waves][4096] (the sequence slots are done)
+    float* row = a.part + (size_t)blockIdx.x * TA_PART;
+    auto wg_matrix = [&](const f32x4 (&g)[4][4], int field) {
+      __syncthreads();
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[wave * 4096 + (x * 16 + fg * 4 + i) * C + y * 16 + fr] = g[x][y][i];
+      __syncthreads();
+      for (int e = tid; e < 4096; e += NTH) row[field + e] = (red[e] + red[4096 + e]) + (red[8192 + e] + red[12288 + e]);
+    };
+    auto wg_cols = [&](float v, int field, int c) {  // column sums over the lane's rows -> [64]
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (fg == 0) red[16384 + wave * 64 + c] = v;
+      return field;
+    };
+    auto wg_cols_out = [&](int field) {  // after a barrier: the 4 waves' column sums
+      for (int e = tid; e < 64; e += NTH)
+        row[field + e] = (red[16384 + e] + red[16384 + 64 + e]) + (red[16384 + 128 + e] + red[16384 + 192 + e]);
+    };
+    if constexpr (PART == 1) {
+      wg_matrix(gA, 0);
+      wg_matrix(gB, 4096);
+      auto cols = [&](const float (&v)[4], int q) {  // (by reference: a pointer table forced scratch)
+        __syncthreads();
+#pragma unroll
+        for (int y = 0; y < 4; ++y) wg_cols(v[y], 0, y * 16 + fr);
+        __syncthreads();
+        wg_cols_out(8192 + q * 64);
+      };
+      cols(cg2, 0);
+      cols(cbe2, 1);
+      cols(cbf2, 2);
+      cols(cbf0, 3);
+      cols(cg1, 4);
+      cols(cbe1, 5);
+    } else {
+      wg_matrix(gA, 0);
+#pragma unroll
+      for (int cv = 0; cv < 2; ++cv) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          __syncthreads();
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                red[wave * 1024 + (x * 16 + fg * 4 + i) * 32 + y * 16 + fr] = cv ? gC2[j][x][y][i] : gC1[j][x][y][i];
+          __syncthreads();
+          for (int e = tid; e < T * T; e += NTH) {
+            const int t = e / T, u = e - t * T, k = t * 32 + u;
+            row[4096 + cv * T * T * 3 + e * 3 + j] = (red[k] + red[1024 + k]) + (red[2048 + k] + red[3072 + k]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int y = 0; y < 4; ++y) wg_cols(cbv[y], 0, y * 16 + fr);
+      // conv bias gradients: per-row sums of the 16 lanes of each row group
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = x * 16 + fg * 4 + i;
+          const float s1 = tam_rowsum(rb1[x][i]), s2 = tam_rowsum(rb2[x][i]);
+          if (fr == 0) {
+            red[16384 + 256 + wave * 32 + t] = s1;
+            red[16384 + 384 + wave * 32 + t] = s2;
+          }
+        }
+      __syncthreads();
+      const int fb = 4096 + 2 * T * T * 3;
+      wg_cols_out(fb);
+      for (int e = tid; e < 64; e += NTH) {
+        const int which = e >> 5, t = e & 31;
+        const float* r = red + 16384 + 256 + which * 128;
+        row[fb + 64 + e] = t < T ? (r[t] + r[32 + t]) + (r[64 + t] + r[96 + t]) : 0.f;
+      }
+    }
+    return;
+  }
   float* G = a.grads;
   auto flush64 = [&](const f32x4 (&g)[4][4], long long off) {  // g rows = out (m), cols = in (n)
 #pragma unroll
@@ -2861,6 +2962,39 @@ int f3_tg_pool_bwd(const float* dpooled, const float* xm, const float* Wm, int B
   return F3_OK;
 }
 
+// grads[seg.goff + e - seg.start] += sum over the workgroups' rows of part[.][e], for the fields of one
+// backward half. Block = 64 fields x 4 row groups (each sums every 4th workgroup), LDS combine.
+struct TaSeg {
+  int start, len;
+  long long goff;
+};
+struct TaSegs {
+  TaSeg s[8];
+  int n, total;
+};
+__global__ __launch_bounds__(256) void ta_part_reduce_kernel(const float* __restrict__ part, int nblk, TaSegs sg,
+                                                             float* __restrict__ grads) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  float acc0 = 0.f, acc1 = 0.f;
+  if (e < sg.total) {
+    int b = rg;
+    for (; b + 4 < nblk; b += 8) {
+      acc0 += part[(size_t)b * TA_PART + e];
+      acc1 += part[(size_t)(b + 4) * TA_PART + e];
+    }
+    if (b < nblk) acc0 += part[(size_t)b * TA_PART + e];
+  }
+  red[rg][lane] = acc0 + acc1;
+  __syncthreads();
+  if (rg == 0 && e < sg.total) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    for (int k = 0; k < sg.n; ++k)
+      if (e >= sg.s[k].start && e < sg.s[k].start + sg.s[k].len) grads[sg.s[k].goff + (e - sg.s[k].start)] += v;
+  }
+}
+
 static int ta_grid(const TaArgs& a) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -2886,16 +3020,48 @@ int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_tg_ta_bwd(const TaArgs* a, hipStream_t s) {
+int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
   static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
+  static const int dbg_env = getenv("F3_TA_DBG") ? atoi(getenv("F3_TA_DBG")) : 0;
+  TaArgs ad = *a_;
+  ad.dbg = dbg_env;
+  const TaArgs* a = &ad;
   if (a->b16 && (mfma_env & 2)) {  // bf16 mode: one wave per sequence on bf16 MFMA
-    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, TAB_LDS1), allow_lds(ta_bwd_mfma_kernel<2>, TAB_LDS2), true);
+    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, std::max(TAB_LDS1, TAB_RED_LDS)),
+                          allow_lds(ta_bwd_mfma_kernel<2>, std::max(TAB_LDS2, TAB_RED_LDS)), true);
     (void)once_m;
-    const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAB_WAVES - 1) / TAB_WAVES));
-    hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS1, s, *a);
+    const int grid = std::max(1, std::min({ta_grid(*a), (a->B * a->V + TAB_WAVES - 1) / TAB_WAVES, TA_MAX_WG}));
+    // the workgroup reduction reuses the LDS as [4 waves][4096] + column sums
+    const int lds1 = a->part ? std::max(TAB_LDS1, TAB_RED_LDS) : TAB_LDS1;
+    const int lds2 = a->part ? std::max(TAB_LDS2, TAB_RED_LDS) : TAB_LDS2;
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), lds1, s, *a);
     F3_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), TAB_LDS2, s, *a);
+    if (a->part && !(a->dbg & 1)) {
+      TaSegs sg;
+      std::memset(&sg, 0, sizeof(sg));
+      const long long g1[8] = {a->off_f2w, a->off_f0w, a->off_lnffw, a->off_lnffb, a->off_f2b, a->off_f0b, a->off_lnw,
+                               a->off_lnb};
+      const int l1[8] = {4096, 4096, 64, 64, 64, 64, 64, 64};
+      int st = 0;
+      for (int k = 0; k < 8; ++k) { sg.s[k] = TaSeg{st, l1[k], g1[k]}; st += l1[k]; }
+      sg.n = 8; sg.total = st;
+      hipLaunchKernelGGL(ta_part_reduce_kernel, dim3((sg.total + 63) / 64), dim3(256), 0, s, a->part, grid, sg, a->grads);
+      F3_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), lds2, s, *a);
     F3_LAUNCH_CHECK();
+    if (a->part && !(a->dbg & 1)) {
+      TaSegs sg;
+      std::memset(&sg, 0, sizeof(sg));
+      const long long g2[6] = {a->off_vw, a->off_c1w, a->off_c2w, a->off_vb, a->off_c1b, a->off_c2b};
+      const int l2[6] = {4096, T * T * 3, T * T * 3, 64, T, T};
+      const int s2[6] = {0, 4096, 4096 + T * T * 3, 4096 + 2 * T * T * 3, 4096 + 2 * T * T * 3 + 64,
+                         4096 + 2 * T * T * 3 + 96};
+      for (int k = 0; k < 6; ++k) sg.s[k] = TaSeg{s2[k], l2[k], g2[k]};
+      sg.n = 6; sg.total = s2[5] + T;
+      hipLaunchKernelGGL(ta_part_reduce_kernel, dim3((sg.total + 63) / 64), dim3(256), 0, s, a->part, grid, sg, a->grads);
+      F3_LAUNCH_CHECK();
+    }
     return F3_OK;
   }
   static bool once = (allow_lds(ta_bwd_kernel, TA_BWD_LDS), true);

@@ -82,7 +82,7 @@ struct Plan {
   size_t S, cs, Wm, bm;
   size_t ops[2][2][5];  // Wf, Wb, Lf, Lb, bn
   size_t H[2], ZR[2], SG[2], HC[2], SU[2], XG[2], XI[2], UG[2], UI[2];
-  size_t ta_out0, ta_out1, ta_save[2], xm, pooled;
+  size_t ta_out0, ta_out1, ta_save[2], ta_part, xm, pooled;
   size_t hx, rhx, gsync, gx1, gx2;  // node-partitioned recurrences: exchange buffers, barrier counters
   // backward
   size_t dlog, dpooled, dY0, dH1, dH0, DP, DSG, DU, DSU, DXG, DUG;
@@ -133,6 +133,7 @@ Plan plan(const f3_targcn* net, int B) {
   p.ta_out0 = take(4 * R * C);
   p.ta_out1 = take(4 * R * C);
   for (int l = 0; l < 2; ++l) p.ta_save[l] = take(4 * (size_t)B * V * TA_SAVE);
+  p.ta_part = take(4 * (size_t)TA_MAX_WG * TA_PART);
   p.xm = take(4 * (size_t)B * 6 * H);
   p.pooled = take(4 * (size_t)B * C);
   p.dlog = take(4 * (size_t)B * net->C);
@@ -387,6 +388,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     a.dout = at<float>(ws, l == 1 ? p.dY1 : p.dY0);
     a.din = at<float>(ws, l == 1 ? p.dY0 : p.dH1);
     a.grads = grads;
+    a.part = at<float>(ws, p.ta_part);
     TG_TRY(f3_tg_ta_bwd(&a, s));
     mark(net, 7 - l, s);
   }
