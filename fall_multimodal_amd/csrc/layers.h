@@ -46,6 +46,24 @@ struct MixArgs {
 };
 constexpr int kMixParts = 1024;
 
+// the first block's graph convolution (Cin <= 4, C = 64) in the bf16 mode (layer0.hip)
+struct Gcn0Args {
+  int frames, K, V, Ci;
+  const float* A;               // A_eff [K][V][V]
+  const unsigned short* x;      // bf16 [frames][V][Ci] (data_bn output)
+  const unsigned short* w;      // bf16 packed gcn weight [64][K*Ci]
+  const float* beff;            // graph-mixed bias [V][64]
+  unsigned short* z;            // fwd out / bwd in: bf16 [frames][V][K][Ci]
+  unsigned short* g;            // fwd out: bf16 [frames*V][64]
+  double* st_sum;               // fwd: BN1 sums [64]
+  double* st_sq;
+  const unsigned short* dg;     // bwd in: bf16 [frames*V][64]
+  float* dx;                    // bwd out: fp32 [frames][V][Ci]
+  int accumulate;
+  float* part_dA;               // bwd: per-block partial rows [blocks][K*V*V]
+  float* part_dW;               // bwd: per-block partial rows [blocks][K*64*Ci] (gradient layout)
+};
+
 struct GcnBiasBwdArgs {
   int K, V, C;
   const float* Aeff;
@@ -186,6 +204,11 @@ int f3_mix_bwd(const f3::MixArgs* a, hipStream_t s);
 int f3_mix_bwd_parts(const f3::MixArgs* a);  // dA partial rows the LDS mix backward leaves (0: none)
 bool f3_mix_lds_ok(int K, int V, int Cin);  // the LDS/MFMA mix path (takes bf16 dZ)
 int f3_gcn_bias_bwd(const f3::GcnBiasBwdArgs* a, hipStream_t s);
+bool f3_gcn0_ok(int K, int V, int Ci, int C);
+int f3_gcn0_fwd(const f3::Gcn0Args* a, hipStream_t s);
+int f3_gcn0_bwd(const f3::Gcn0Args* a, hipStream_t s);
+int f3_gcn0_bwd_parts(const f3::Gcn0Args* a);  // partial rows f3_gcn0_bwd leaves (caller: f3_colsum)
+int f3_databn_bwd2(const f3::DataBnArgs* a, hipStream_t s);  // single-pass data_bn gamma/beta gradient
 int f3_block_out(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);

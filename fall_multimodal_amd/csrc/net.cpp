@@ -590,18 +590,27 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     std::memset(&bnr, 0, sizeof(bnr));
     if (L.res == RES_CONV) bnr = q.ref(L.bnr, X.bnr, (float)Mo, eval);
     // graph mix then 1x1 conv (stgcan.py:50-56)
-    MixArgs mx;
-    std::memset(&mx, 0, sizeof(mx));
-    mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
-    mx.zb = bfa(X.z, hb); mx.x16 = hb;
-    F3_TRY(f3_mix_fwd(&mx, s));
-    ConvGemmArgs ga;
-    std::memset(&ga, 0, sizeof(ga));
-    ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
-    ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
-    ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.outb = bfa(X.g, hb);
-    ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
-    F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
+    if (hb && f3_gcn0_ok(K, V, Ci, C)) {  // the 3-channel first block: one kernel (layer0.hip)
+      Gcn0Args g0;
+      std::memset(&g0, 0, sizeof(g0));
+      g0.frames = N * Ti; g0.K = K; g0.V = V; g0.Ci = Ci; g0.A = X.aeff;
+      g0.x = reinterpret_cast<const unsigned short*>(X.x); g0.w = bf(X.gw, 1); g0.beff = X.beff;
+      g0.z = bfa(X.z, 1); g0.g = bfa(X.g, 1); g0.st_sum = X.bn1.fsum; g0.st_sq = X.bn1.fsq;
+      F3_TRY(f3_gcn0_fwd(&g0, s));
+    } else {
+      MixArgs mx;
+      std::memset(&mx, 0, sizeof(mx));
+      mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
+      mx.zb = bfa(X.z, hb); mx.x16 = hb;
+      F3_TRY(f3_mix_fwd(&mx, s));
+      ConvGemmArgs ga;
+      std::memset(&ga, 0, sizeof(ga));
+      ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
+      ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
+      ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.outb = bfa(X.g, hb);
+      ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+      F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
+    }
     if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
       ConvGemmArgs ra;
       std::memset(&ra, 0, sizeof(ra));
@@ -742,6 +751,19 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     bb.Gpart = X.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb; bb.no_colsum = split;
     if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
+    const bool g0 = hb && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
+    Gcn0Args b0;
+    std::memset(&b0, 0, sizeof(b0));
+    int g0_parts = 0;
+    if (g0) {
+      b0.frames = N * Ti; b0.K = K; b0.V = V; b0.Ci = Ci; b0.A = X.aeff;
+      b0.x = reinterpret_cast<const unsigned short*>(X.x); b0.w = bf(X.gw, 1); b0.z = bfa(X.z, 1);
+      b0.dg = bfa(dg, 1); b0.dx = dx; b0.accumulate = L.res == RES_ID;
+      g0_parts = f3_gcn0_bwd_parts(&b0);
+      if ((size_t)g0_parts * (K * V * V + K * C * Ci) > (size_t)kMixParts * K * V * V) return F3_EINVAL;
+      b0.part_dA = X.mixpart;
+      b0.part_dW = X.mixpart + (size_t)g0_parts * K * V * V;
+    }
     ConvGemmArgs gd;
     std::memset(&gd, 0, sizeof(gd));
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
@@ -752,14 +774,14 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (!f3_igemm_ok(gd)) return F3_EINVAL;
       gd.outb = bfa(W.dZ, 1);
     }
-    if (part & 1) F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
+    if ((part & 1) && !g0) F3_TRY(f3_conv_gemm(&gd, 0, 0, s));
     MixArgs mx;
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
     mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = X.mixpart; mx.x16 = hb;
     mx.no_colsum = split;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
-    if (part & 1) F3_TRY(f3_mix_bwd(&mx, s));
+    if (part & 1) F3_TRY(g0 ? f3_gcn0_bwd(&b0, s) : f3_mix_bwd(&mx, s));
     if (L.res == RES_CONV) {
       ConvGemmArgs rd;
       std::memset(&rd, 0, sizeof(rd));
@@ -794,8 +816,12 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     if (split) {  // reductions whose results only feed weight gradients
       const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
       if (part & 2) F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
-      const int mparts = f3_mix_bwd_parts(&mx);
+      const int mparts = g0 ? 0 : f3_mix_bwd_parts(&mx);
       if (mparts && (part & 2)) F3_TRY(f3_colsum(X.mixpart, mparts, K * V * V, X.dAeff, ss));
+    }
+    if (g0 && (part & 2)) {  // the first block's dA_eff and gcn weight gradient partial rows
+      F3_TRY(f3_colsum(b0.part_dA, g0_parts, K * V * V, X.dAeff, ss));
+      F3_TRY(f3_colsum(b0.part_dW, g0_parts, K * C * Ci, q.g(L.gcn_w), ss));
     }
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
@@ -807,7 +833,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
-    if (part & 2) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
+    if ((part & 2) && !g0) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
     gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
@@ -834,7 +860,12 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
   d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), 0);
   d.dout = dout; d.dgamma = q.g(S.dbn.w); d.dbeta = q.g(S.dbn.b);
-  if (part & 1) F3_TRY(f3_databn_bwd(&d, s));
+  if (part & 1) {
+    static const int db2 = getenv("F3_DATABN_BWD2") ? atoi(getenv("F3_DATABN_BWD2")) : 1;
+    const int st = db2 ? f3_databn_bwd2(&d, s) : F3_EINVAL;
+    if (st == F3_EINVAL) F3_TRY(f3_databn_bwd(&d, s));
+    else if (st != F3_OK) return st;
+  }
   return F3_OK;
 }
 
