@@ -35,6 +35,7 @@ F3_DEV unsigned short g0_rne(float f) {
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
+template <int K, int Ci>
 __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
   __shared__ float As[3 * G0_MAXV * G0_MAXV];
   __shared__ float xs[G0_FB * G0_MAXV * 4];
@@ -42,12 +43,13 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
   __shared__ float bvs[G0_MAXV * 64];
   __shared__ float red[2][4][64];
   const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
-  const int K = a.K, V = a.V, Ci = a.Ci, KC = K * Ci, C = 64;
+  constexpr int KC = K * Ci, C = 64;
+  const int V = a.V;
   for (int i = tid; i < K * V * V; i += 256) As[i] = a.A[i];
   for (int i = tid; i < V * C; i += 256) bvs[i] = a.beff[i];
-  float wv[G0_MAXKC];
+  float wv[KC];
 #pragma unroll
-  for (int j = 0; j < G0_MAXKC; ++j) wv[j] = j < KC ? g0_bf(a.w[c * KC + j]) : 0.f;
+  for (int j = 0; j < KC; ++j) wv[j] = g0_bf(a.w[c * KC + j]);
   float ssum = 0.f, ssq = 0.f;
   for (int f0 = blockIdx.x * G0_FB; f0 < a.frames; f0 += gridDim.x * G0_FB) {
     const int nf = min(G0_FB, a.frames - f0);
@@ -65,13 +67,13 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
     }
     __syncthreads();
     // g[row][c] = sum_j Z[row][j] W[c][j] + bias_eff[v][c]
-    for (int r = rg; r < nf * V; r += 4) {
-      const int w = r % V;
+    for (int r = rg, w = rg; r < nf * V; r += 4) {
       float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < G0_MAXKC; ++j)
-        if (j < KC) acc += zs[r * KC + j] * wv[j];
+      for (int j = 0; j < KC; ++j) acc += zs[r * KC + j] * wv[j];
       acc += bvs[w * C + c];
+      w += 4;
+      if (w >= V) w -= V;  // (V >= 4)
       a.g[((size_t)f0 * V + r) * C + c] = g0_rne(acc);
       ssum += acc;
       ssq += acc * acc;
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
 // ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
+template <int K, int Ci>
 __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   __shared__ float As[3 * G0_MAXV * G0_MAXV];
   __shared__ float xs[G0_FB * G0_MAXV * 4];
@@ -97,7 +100,8 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   __shared__ float dzs[G0_FB * G0_MAXV * G0_MAXKC];  // dZ
   __shared__ float red[4][64 * G0_MAXKC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane, rg = wave;
-  const int K = a.K, V = a.V, Ci = a.Ci, KC = K * Ci, C = 64, KVV = K * V * V;
+  constexpr int KC = K * Ci, C = 64;
+  const int V = a.V, KVV = K * V * V;
   const int fr = lane & 15, fg = lane >> 4;
   for (int i = tid; i < KVV; i += 256) As[i] = a.A[i];
   // MFMA B operand (dZ = dg . W: k = c, n = j): lane (fg, fr) holds W[c = s*32 + fg*8 + e][j = fr]
@@ -111,9 +115,18 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
       wb[s][e] = __builtin_bit_cast(__bf16, u);
     }
   float dacc[4] = {0.f, 0.f, 0.f, 0.f};  // dA_eff entries tid + 256 q
-  float wacc[G0_MAXKC];                  // dW[.][c][.] over this thread's rows (j = k*Ci + ci)
+  float wacc[KC];                        // dW[.][c][.] over this thread's rows (j = k*Ci + ci)
 #pragma unroll
-  for (int j = 0; j < G0_MAXKC; ++j) wacc[j] = 0.f;
+  for (int j = 0; j < KC; ++j) wacc[j] = 0.f;
+  int dv[4], dw[4], dk[4];  // (k, v, w) of the thread's dA_eff entries
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = min(tid + q * 256, KVV - 1);
+    dk[q] = idx / (V * V);
+    const int r = idx - dk[q] * V * V;
+    dv[q] = r / V;
+    dw[q] = r - dv[q] * V;
+  }
   for (int f0 = blockIdx.x * G0_FB; f0 < a.frames; f0 += gridDim.x * G0_FB) {
     const int nf = min(G0_FB, a.frames - f0), nr = nf * V;
     __syncthreads();
@@ -148,11 +161,11 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
     // dA_eff[k][v][w] += sum_{f, ci} x[f][v][ci] dZ[f][w][k][ci]
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int idx = tid + q * 256;
-      if (idx < KVV) {
-        const int k = idx / (V * V), r = idx - k * V * V, v = r / V, w = r - v * V;
+      if (tid + q * 256 < KVV) {
+        const int k = dk[q], v = dv[q], w = dw[q];
         float acc = 0.f;
         for (int fl = 0; fl < nf; ++fl)
+#pragma unroll
           for (int ci = 0; ci < Ci; ++ci) acc += xs[(fl * V + v) * Ci + ci] * dzs[(fl * V + w) * KC + k * Ci + ci];
         dacc[q] += acc;
       }
@@ -161,8 +174,7 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
     for (int r = rg; r < nr; r += 4) {
       const float d = g0_bf(a.dg[((size_t)f0 * V + r) * C + c]);
 #pragma unroll
-      for (int j = 0; j < G0_MAXKC; ++j)
-        if (j < KC) wacc[j] += d * zs[r * KC + j];
+      for (int j = 0; j < KC; ++j) wacc[j] += d * zs[r * KC + j];
     }
   }
   // this block's partial rows: dA_eff [KVV] at part_dA[blockIdx], dW at part_dW[blockIdx] in the
@@ -175,8 +187,7 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < G0_MAXKC; ++j)
-    if (j < KC) red[rg][c * KC + j] = wacc[j];
+  for (int j = 0; j < KC; ++j) red[rg][c * KC + j] = wacc[j];
   __syncthreads();
   float* pw = a.part_dW + (size_t)blockIdx.x * C * KC;
   for (int e = tid; e < C * KC; e += 256) {
@@ -225,17 +236,21 @@ __global__ __launch_bounds__(256) void databn_bwd2_kernel(DataBnArgs a) {
 
 using namespace f3;
 
+// instantiated: K = 3 partitions (the 'spatial' strategy) with 3 (positions) or 2 input channels
 bool f3_gcn0_ok(int K, int V, int Ci, int C) {
   static const int on = getenv("F3_GCN0") ? atoi(getenv("F3_GCN0")) : 1;
-  return on && C == 64 && Ci >= 1 && Ci <= 4 && K >= 1 && K <= 3 && K * Ci <= G0_MAXKC && V <= G0_MAXV &&
+  return on && C == 64 && K == 3 && (Ci == 2 || Ci == 3) && V >= 4 && V <= G0_MAXV &&
          K * V * V <= 1024;  // dA_eff: 4 entries per thread
 }
 
-static int g0_grid(int frames) { return std::max(1, std::min(240, (frames + G0_FB - 1) / G0_FB)); }
+// ~2 blocks of 8 frames each per workgroup: 1-2 resident workgroups per SIMD hide the LDS and
+// integer latency the 1-per-CU form exposed (78 / 105 us alone -> see profiles/r03_layer0_ab.txt)
+static int g0_grid(int frames) { return std::max(1, std::min(480, (frames + G0_FB - 1) / G0_FB)); }
 
 int f3_gcn0_fwd(const Gcn0Args* a, hipStream_t s) {
   if (!f3_gcn0_ok(a->K, a->V, a->Ci, 64)) return F3_EINVAL;
-  hipLaunchKernelGGL(gcn0_fwd_kernel, dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  if (a->Ci == 3) hipLaunchKernelGGL((gcn0_fwd_kernel<3, 3>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((gcn0_fwd_kernel<3, 2>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -244,7 +259,8 @@ int f3_gcn0_bwd_parts(const Gcn0Args* a) { return g0_grid(a->frames); }
 
 int f3_gcn0_bwd(const Gcn0Args* a, hipStream_t s) {
   if (!f3_gcn0_ok(a->K, a->V, a->Ci, 64) || !a->part_dA || !a->part_dW) return F3_EINVAL;
-  hipLaunchKernelGGL(gcn0_bwd_kernel, dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  if (a->Ci == 3) hipLaunchKernelGGL((gcn0_bwd_kernel<3, 3>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((gcn0_bwd_kernel<3, 2>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
