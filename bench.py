@@ -21,6 +21,7 @@ host's cores on a bounded sample).
 """
 import argparse
 import json
+import subprocess
 import os
 import sys
 import time
@@ -689,6 +690,24 @@ def cpu_baseline(layout, V, S, seconds):
             "sample": f"{n} train steps (fwd+CE+bwd+RMSprop) of B={B}, V={V}, S={S}, fp32, torch CPU"}
 
 
+def model_leg(model, a):
+    """One of the other BASELINE configs (cfg 2 TARGCN, cfg 5 SkeletonTransformer, musa_model) timed
+    in a fresh child process (`bench.py --model M`, its own line embedded here): measured inside this
+    process after the 3-stream, fp32-mode and roofline legs, the TARGCN step read 8.4 ms against 6.7 ms
+    alone (profiles/r03_bench.json vs r03_bench_tg_alone.json)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--model", model, "--steps", "10", "--warmup", "3"]
+    if a.no_cpu_baseline:
+        cmd.append("--no-cpu-baseline")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        raise SystemExit(f"bench.py: the --model {model} leg failed (status {r.returncode}): {r.stderr[-2000:]}")
+    rec = json.loads(lines[-1])
+    rec["process"] = "fresh child process (bench.py --model %s)" % model
+    return rec
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -775,10 +794,10 @@ def main():
     ev = eval_throughput(model, sk, se) if rank == 0 else None
     agp = autograd_path_bench(model, sk, se, lb) if (rank == 0 and world == 1) else None
     roofs = roofline_kernels(dev, B, V, a.precision) if rank == 0 else None
-    tgrec = targcn_bench(dev, cpu_seconds=0.0 if a.no_cpu_baseline else 6.0) if (
-        rank == 0 and world == 1 and not a.no_targcn) else None
-    skrec = sktr_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
-    murec = musa_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    legs = rank == 0 and world == 1 and not a.no_targcn
+    tgrec = model_leg("targcn", a) if legs else None
+    skrec = model_leg("sktr", a) if legs else None
+    murec = model_leg("musa", a) if legs else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
     ldr = loader_bench(model, dev, B, V, S, C) if (rank == 0 and world == 1 and not a.no_targcn) else None

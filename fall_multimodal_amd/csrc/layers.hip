@@ -1824,8 +1824,17 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
+// F3_DBG_NO_CA (measurement only, results are wrong): bit 0 skips the channel-attention forward
+// launches, bit 1 the backward chain (ca_bwd1/2/3) - the step time without them bounds what a
+// faster channel attention can give
+static int dbg_no_ca() {
+  static const int v = getenv("F3_DBG_NO_CA") ? atoi(getenv("F3_DBG_NO_CA")) : 0;
+  return v;
+}
+
 int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256 * kCaMaxRowsPerThread) return F3_EINVAL;
+  if (dbg_no_ca() & 1) return F3_OK;
   hipLaunchKernelGGL(ca_fwd1_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_fwd2_kernel, dim3(a->N), dim3(256), 0, s, *a);
@@ -1835,6 +1844,7 @@ int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
 
 int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
+  if (dbg_no_ca() & 2) return F3_OK;
   hipLaunchKernelGGL(ca_bwd1_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);

@@ -33,17 +33,18 @@
 
 namespace f3 {
 
-constexpr int PW_BM = 64;        // rows per tile
 constexpr int PW_LDS_BUDGET = 156 * 1024;
-constexpr int PW_THREADS = 512;  // 8 waves: wm = wave & 1 (32 rows), wj = wave >> 1 (16*WN columns)
+constexpr int PW_THREADS = 512;  // 8 waves: wm = wave & 1 (BM/2 rows), wj = wave >> 1 (16*WN columns)
 constexpr int PW_VMAX = 18;      // joints of the BIASV table
 
-template <int EPI, int KS, int WN>
+// BM = rows per tile: 64, or 32 for K = 384 / 768 (a 64-row block of those is 48 / 96 KB)
+template <int EPI, int KS, int WN, int BM>
 struct PwLds {
   static constexpr bool ADD = (EPI & EPI_ADD) != 0;
+  static constexpr int PW_BM = BM;
   static constexpr int K = KS * 32;
   static constexpr int NT = 64 * WN;            // columns per workgroup
-  static constexpr int ABUF = PW_BM * K * 2;    // bytes per A buffer ([K/64][64 rows][128 B])
+  static constexpr int ABUF = PW_BM * K * 2;    // bytes per A buffer ([K/64][BM rows][128 B])
   static constexpr int OTS = ADD ? NT + 4 : NT + 8;  // output image row stride (elements)
   static constexpr int ES = ADD ? 4 : 2;             // image element size (fp32 / bf16)
   static constexpr int FIXED = PW_BM * OTS * ES + ((EPI & EPI_BIASV) ? PW_VMAX * NT * 4 : 0) +
@@ -57,7 +58,10 @@ struct PwLds {
   static constexpr int BV_OFF = OT_OFF + PW_BM * OTS * ES;
   static constexpr int RED_OFF = BV_OFF + ((EPI & EPI_BIASV) ? PW_VMAX * NT * 4 : 0);
   static constexpr int BYTES = RED_OFF + ((EPI & EPI_STATS) ? 2 * 2 * NT * 4 : 0);
-  static constexpr int PIECES = PW_BM * NT * ES / 16 / PW_THREADS;  // 16-B image pieces per thread
+  // 16-B image pieces per tile, and per thread: PIECES each, or (TP < 512) one for threads < TP
+  static constexpr int TP = PW_BM * NT * ES / 16;
+  static constexpr int PIECES = TP >= PW_THREADS ? TP / PW_THREADS : 1;
+  static constexpr int LPT = (KS / 2) * PW_BM / 64;  // DMA instructions per thread and tile
 };
 
 // s_waitcnt vmcnt(BASE + min(k, KMAX) * STEP) for a wave-uniform k (immediates only)
@@ -71,14 +75,16 @@ F3_DEV void pw_wait_vm(int k) {
   }
 }
 
-template <int EPI, int KS, int WN>
+template <int EPI, int KS, int WN, int BM>
 __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int ncg, int per_wg) {
-  using L = PwLds<EPI, KS, WN>;
-  constexpr int NT = L::NT, KC = KS / 2, OTS = L::OTS, NB = L::NB;
+  using L = PwLds<EPI, KS, WN, BM>;
+  constexpr int PW_BM = BM, MX = BM / 32;  // MX: 16-row MFMA tiles per wave
+  constexpr int NT = L::NT, KC = KS / 2, OTS = L::OTS, NB = L::NB, LPT = L::LPT;
   constexpr bool ADD = L::ADD;
   static_assert(KS % 2 == 0 && NB >= 3 && L::BYTES <= 160 * 1024, "pw_gemm LDS");
-  static_assert((NB - 2) * (KC + L::PIECES) < 64, "vmcnt immediate");
-  static_assert(PW_BM * NT * L::ES % (16 * PW_THREADS) == 0, "whole image pieces per thread");
+  static_assert((BM == 64 || (BM == 32 && !ADD && KC % 2 == 0)) && LPT * 64 == KC * BM, "tile rows");
+  static_assert((NB - 2) * (LPT + L::PIECES) < 64, "vmcnt immediate");
+  static_assert(L::TP % 64 == 0 && (L::TP < PW_THREADS || L::TP % PW_THREADS == 0), "image pieces");
   extern __shared__ __attribute__((aligned(16))) char pw_smem[];
   char* img = pw_smem + L::OT_OFF;
   float* bv = reinterpret_cast<float*>(pw_smem + L::BV_OFF);   // [V][NT] graph-mixed bias slice
@@ -131,19 +137,21 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     asm volatile("" ::"v"(bias[y]));
   }
 
-  // A staging: 1-KiB DMA pieces of 8 rows x 128 B; wave w stages row group w of every 64-channel
-  // chunk (KC instructions per thread and tile, always issued: past the range from the zero page)
-  const int sub = lane >> 3, pch = lane & 7, rr = wave * 8 + sub;
+  // A staging: 1-KiB DMA pieces of 8 rows x 128 B, piece q = (64-channel chunk, row group); wave w
+  // stages pieces w + 8i, i.e. row group w % (BM/8) of chunks (w + 8i) / (BM/8) (LPT instructions per
+  // thread and tile, always issued: past the range from the zero page)
+  constexpr int RGN = PW_BM / 8;
+  const int sub = lane >> 3, pch = lane & 7, rr = (wave % RGN) * 8 + sub;
   auto load_tile = [&](int tile, int buf) {
     char* dst = pw_smem + buf * L::ABUF;
     const int m = tile < tile1 ? phys(tile * PW_BM + rr) : -1;
     const int r = m >= 0 ? rowmap_src(rowmap(m, g), 0, g) : -1;
     const unsigned short* src = r >= 0 ? a.inb + (size_t)r * g.lda + swz(rr, pch) * 8 : nullptr;
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
+    for (int i = 0; i < LPT; ++i) {
+      const int q = wave + 8 * i, kc = q / RGN;
       const unsigned short* p = src ? src + kc * 64 : a.zero;
-      __builtin_amdgcn_global_load_lds((const void*)p, (lds_void_t*)(dst + (kc * (PW_BM / 8) + wave) * 1024), 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds((const void*)p, (lds_void_t*)(dst + q * 1024), 16, 0, 0);
     }
   };
   // the staged output of a tile -> HBM (16-B row pieces, L::PIECES per thread). FULL: every row of
@@ -152,7 +160,9 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
   // from one of the DMA destinations and waited vmcnt(0) before it, i.e. for the tile in flight.
   constexpr int CPR = NT * L::ES / 16;
   const unsigned img_lds = (unsigned)(size_t)(lds_void_t*)img;
+  const bool storer = L::TP >= PW_THREADS || tid < L::TP;  // wave-uniform (TP % 64 == 0)
   auto store_tile = [&](int tile, auto full) {
+    if (!storer) return;
 #pragma unroll
     for (int i = 0; i < L::PIECES; ++i) {
       const int q = tid + i * PW_THREADS, rl = q / CPR, c = q - rl * CPR;
@@ -187,7 +197,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
   for (int i = 0; i < NB - 1; ++i) load_tile(tile0 + i, i);
   // tile0's block has landed (the other NB - 2 stay in flight) and the bias table is written. A raw
   // barrier: __syncthreads() would wait vmcnt(0)
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NB - 2) * KC) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NB - 2) * LPT) : "memory");
   __builtin_amdgcn_s_barrier();
   if (ADD) preload(tile0);
   // One tile. Every vector-memory operation in it is unconditional (stores of full tiles, loads past
@@ -202,17 +212,17 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     if constexpr (!decltype(first)::value) store_tile(tile - 1, std::true_type{});
     load_tile(tile + NB - 1, (it + NB - 1) % NB);
     const char* A = pw_smem + buf * L::ABUF;
-    f32x4 acc[2][WN];
+    f32x4 acc[MX][WN];
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < MX; ++x)
 #pragma unroll
       for (int y = 0; y < WN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int kc = s >> 1, c = (s & 1) * 4 + fg;
 #pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const int r = wm * 32 + x * 16 + fr;
+      for (int x = 0; x < MX; ++x) {
+        const int r = wm * 16 * MX + x * 16 + fr;
         const bf16x8 fa = *reinterpret_cast<const bf16x8*>(A + (kc * PW_BM + r) * 128 + swz(r, c) * 16);
 #pragma unroll
         for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa, wf[y][s], acc[x][y]);
@@ -223,10 +233,10 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < MX; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int rl = wm * 32 + x * 16 + fg * 4 + r, m = phys(tile * PW_BM + rl);
+        const int rl = wm * 16 * MX + x * 16 + fg * 4 + r, m = phys(tile * PW_BM + rl);
         const bool ok = m >= 0;
         const int vj = (EPI & EPI_BIASV) && ok ? m % g.V : 0;
 #pragma unroll
@@ -245,7 +255,8 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
         }
       }
     // the next tile's block has landed (the NB - 2 after it stay in flight) and the image is written
-    pw_wait_vm<(NB - 2) * KC, L::PIECES, NB - 2>(it);
+    if (storer) pw_wait_vm<(NB - 2) * LPT, L::PIECES, NB - 2>(it);
+    else pw_wait_vm<(NB - 2) * LPT, 0, 0>(it);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (ADD) preload(min(tile + 1, tile1 - 1));
@@ -287,6 +298,7 @@ using namespace f3;
 // Instantiated (EPI, KS, WN) combinations: the step's shapes (and a plain conv for the unit test).
 #define F3_PW_TABLE(X)                                                                                \
   X(EPI_BIASV | EPI_STATS, 6, 1) X(EPI_BIASV | EPI_STATS, 6, 2)                                       \
+  X(EPI_BIASV | EPI_STATS, 12, 2) X(EPI_BIASV | EPI_STATS, 24, 1)                                     \
   X(EPI_BIAS | EPI_STATS, 2, 2) X(EPI_BIAS | EPI_STATS, 4, 4)                                         \
   X(EPI_BIAS, 2, 3)                                                                                   \
   X(0, 2, 3) X(0, 4, 3) X(0, 4, 6) X(0, 6, 1) X(0, 8, 3) X(0, 8, 4)                                   \
@@ -316,7 +328,8 @@ bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   static const int on = getenv("F3_PW") ? atoi(getenv("F3_PW")) : 1;
   const ConvGeom& g = a.g;
   if (!on || !a.inb || !a.wb || !a.zero) return false;
-  if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Kc > 256 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
+  if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
+  if (g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
   if (!pw_wn(g, epi)) return false;
   const bool add = epi == EPI_ADD;
   if (add ? !a.out : !a.outb) return false;
@@ -331,14 +344,17 @@ bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   return true;
 }
 
+constexpr int pw_bm(int ks) { return ks > 8 ? 32 : 64; }
+
 template <int EPI, int KS, int WN>
 static void pw_launch(const ConvGemmArgs& a, int grid, int ncg, int per_wg, hipStream_t s) {
-  constexpr int lds = PwLds<EPI, KS, WN>::BYTES;
-  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN>,
+  constexpr int BM = pw_bm(KS);
+  constexpr int lds = PwLds<EPI, KS, WN, BM>::BYTES;
+  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds),
                       true);
   (void)once;
-  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg, per_wg);
+  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg, per_wg);
 }
 
 int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
@@ -355,7 +371,8 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const int ncg = g.Nc / (64 * wn);
   const bool par = epi == EPI_ADD;
   const int Mp = par ? (g.M / (g.T_out * g.V)) * ((g.T_out + 1) >> 1) * g.V : g.M;
-  const int ntiles = (Mp + PW_BM - 1) / PW_BM;
+  const int bm = pw_bm(ks);
+  const int ntiles = (Mp + bm - 1) / bm;
   // one round over the CUs: contiguous ranges of tiles, one workgroup per (range, column group)
   const int nr0 = std::max(1, cus / ncg);
   const int per_wg = (ntiles + nr0 - 1) / nr0;

@@ -19,7 +19,10 @@ EPI_BIAS, EPI_BIASV, EPI_STATS, EPI_ADD = 1, 2, 4, 32
 CASES = [
     (5, 30, 30, 18, 192, 64, 1, 0, EPI_BIASV | EPI_STATS, 1),    # gcn forward, 64-channel layers
     (5, 30, 30, 18, 192, 128, 1, 0, EPI_BIASV | EPI_STATS, 1),   # layer 3
-    (3, 15, 15, 18, 384, 128, 1, 0, EPI_BIASV | EPI_STATS, 1),   # layer 4 (igemm_big path)
+    (3, 15, 15, 18, 384, 128, 1, 0, EPI_BIASV | EPI_STATS, 1),   # layer 4 (32-row tiles)
+    (3, 15, 15, 18, 384, 256, 1, 0, EPI_BIASV | EPI_STATS, 1),   # layer 5
+    (5, 8, 8, 18, 768, 256, 1, 0, EPI_BIASV | EPI_STATS, 1),     # layer 6 (half the waves store)
+    (4, 8, 8, 14, 768, 256, 1, 0, EPI_BIASV | EPI_STATS, 1),     # V = 14
     (5, 30, 30, 18, 64, 192, 1, 1, 0, 1),                        # gcn input gradient, 64-channel layers
     (5, 30, 30, 18, 128, 192, 1, 1, 0, 1),                       # layer 3
     (3, 15, 15, 18, 128, 384, 1, 1, 0, 1),                       # layer 4
