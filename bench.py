@@ -690,6 +690,44 @@ def cpu_baseline(layout, V, S, seconds):
             "sample": f"{n} train steps (fwd+CE+bwd+RMSprop) of B={B}, V={V}, S={S}, fp32, torch CPU"}
 
 
+def rgb_bench(dev, B=256, T=30, reps=10):
+    """The build-defined RGB spatial-conv branch (fall_multimodal_amd/rgb.py, csrc/rgb.hip; PARITY
+    UNPINNED: the reference has no RGB model arithmetic, SURVEY.md 8a R-RGB) on the north-star batch:
+    B=256 clips x T=30 channels-last bf16 224x224x3 frames (2.31 GB resident in HBM). Both kernels
+    stream the frames once (algorithmic bytes = the frame bytes; weights, bias and per-block partial
+    rows are < 0.1% of it), so each is priced against HBM."""
+    import fall_multimodal_amd.rgb as rgbm
+    frames = torch.empty(B, T, 224, 224, 3, dtype=torch.bfloat16, device=dev).uniform_()
+    conv = rgbm.RGBSpatialConv(device=dev)
+    w, b = conv.weight.detach(), conv.bias.detach()
+    dfeat = torch.randn(B, 64, device=dev)
+    s = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps / 1e3
+
+    t_f = timed(lambda: torch.ops.fall3.rgb_forward(frames, w, b))
+    t_b = timed(lambda: torch.ops.fall3.rgb_backward(frames, w, b, dfeat))
+    nbytes = frames.numel() * 2
+    out = {"workload": f"rgb_spatial_conv_B{B}_T{T}_224x224x3_bf16", "parity": "unpinned (build-defined branch)",
+           "clips_per_s_fwd_bwd": round(B / (t_f + t_b), 1), "fwd_ms": round(t_f * 1e3, 4), "bwd_ms": round(t_b * 1e3, 4),
+           "bytes_per_pass": nbytes}
+    for k, t in (("fwd", t_f), ("bwd", t_b)):
+        out["roofline_" + k] = {"bound": "hbm", "achieved": round(nbytes / t / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": round(nbytes / t / 1e9 / PEAK_HBM_GBS, 4), "traffic": None}
+    del frames
+    torch.cuda.empty_cache()
+    return out
+
+
 def model_leg(model, a):
     """One of the other BASELINE configs (cfg 2 TARGCN, cfg 5 SkeletonTransformer, musa_model) timed
     in a fresh child process (`bench.py --model M`, its own line embedded here): measured inside this
@@ -800,6 +838,7 @@ def main():
     murec = model_leg("musa", a) if legs else None
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
+    rgbr = rgb_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
     ldr = loader_bench(model, dev, B, V, S, C) if (rank == 0 and world == 1 and not a.no_targcn) else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)
@@ -818,7 +857,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"fall3_3stream_{a.layout}_V{V}_S{S}_B{B}_per_gpu",
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
-                       "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "absent in reference",
+                       "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "build-defined, timed on its own (rgb_branch key)",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
                        "ranks": world, "collective": "rccl all_reduce (2 buckets)" if world > 1 else None},
             "roofline": roofs.get("wgrad_l5", roofs["tcn_fwd"]),
@@ -839,6 +878,7 @@ def main():
             "cfg2_targcn": tgrec,
             "cfg5_sktr": skrec,
             "musa_model": murec,
+            "rgb_branch": rgbr,
             "fp32_mode": fp32m,
             "cpu_baseline": cpu,
             "reference_cpu_published": REFERENCE_CPU,

@@ -29,7 +29,7 @@ EXPORTS = (
     "f3_musa_create", "f3_musa_destroy", "f3_musa_num_entries", "f3_musa_entry", "f3_musa_param_count",
     "f3_musa_buffer_count", "f3_musa_counter_count", "f3_musa_workspace_bytes", "f3_musa_forward", "f3_musa_backward",
     "f3_musa_guards",
-    "f3_dwconv_t_forward", "f3_pointwise_conv",
+    "f3_dwconv_t_forward", "f3_pointwise_conv", "f3_rgb_scratch_floats", "f3_rgb_forward", "f3_rgb_backward",
 )
 
 F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE = 0, 1001, 1002, 1003, 1004
@@ -130,6 +130,9 @@ def lib():
         "f3_musa_backward": (I, [P, I, P, P, P, P, P, P]),
         "f3_dwconv_t_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, P]),
         "f3_pointwise_conv": (I, [P, P, P, P, I, P, P, I, I, I, I, I, I, I, I, I, P]),
+        "f3_rgb_scratch_floats": (ctypes.c_longlong, [I, I]),
+        "f3_rgb_forward": (I, [P, P, P, P, I, I, P]),
+        "f3_rgb_backward": (I, [P, P, P, P, P, P, P, ctypes.c_longlong, I, I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

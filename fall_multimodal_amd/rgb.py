@@ -1,0 +1,113 @@
+"""RGB spatial-conv branch — BUILD-DEFINED (the north star names an "RGB spatial-conv branch"; the
+reference has RGB frames only in preprocessing, 3_stream/har_create3.py:36-42,101-158, and no RGB
+model arithmetic, so this branch's parity is unpinned; SURVEY.md section 8a row R-RGB).
+
+    RGBSpatialConv   Conv2d(3, 64, 8, stride 8) over each 224x224 frame -> ReLU -> mean over the
+                     frames and the 28x28 patches -> feat [B, 64]   (HIP: csrc/rgb.hip)
+    RGBBranch        RGBSpatialConv + Linear(64, num_class): the branch's late-fusion logits
+    Fall3WithRGB     the reference 3-stream model plus the RGB branch, fused by adding logits
+
+Frames are channels-last bf16 [B, T, 224, 224, 3]. The conv runs as `fall3::rgb_forward` /
+`fall3::rgb_backward` custom ops (no input gradient: the frames are data)."""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+from torch import Tensor, nn
+
+from ._lib import check, lib, ptr, require_device, stream_handle
+
+
+def _pack(w: Tensor) -> Tensor:  # [64, 3, 8, 8] -> bf16 [64, 192], k = (dy*8 + dx)*3 + ch
+    return w.detach().permute(0, 2, 3, 1).reshape(w.shape[0], -1).to(torch.bfloat16).contiguous()
+
+
+@torch.library.custom_op("fall3::rgb_forward", mutates_args=())
+def rgb_forward(frames: Tensor, weight: Tensor, bias: Tensor) -> Tensor:
+    require_device(frames, "frames")
+    B, T = frames.shape[:2]
+    if frames.dtype != torch.bfloat16 or tuple(frames.shape[2:]) != (224, 224, 3) or not frames.is_contiguous():
+        raise ValueError("fall3 rgb: frames must be contiguous bf16 [B, T, 224, 224, 3]")
+    feat = torch.empty(B, 64, dtype=torch.float32, device=frames.device)
+    wp, b = _pack(weight), bias.detach().float().contiguous()
+    check(lib().f3_rgb_forward(ptr(frames), ptr(wp), ptr(b), ptr(feat), B, T, stream_handle()), "rgb forward")
+    return feat
+
+
+@rgb_forward.register_fake
+def _(frames, weight, bias):
+    return frames.new_empty(frames.shape[0], 64, dtype=torch.float32)
+
+
+@torch.library.custom_op("fall3::rgb_backward", mutates_args=())
+def rgb_backward(frames: Tensor, weight: Tensor, bias: Tensor, dfeat: Tensor) -> tuple[Tensor, Tensor]:
+    B, T = frames.shape[:2]
+    L = lib()
+    scratch = torch.empty(int(L.f3_rgb_scratch_floats(B, T)), dtype=torch.float32, device=frames.device)
+    dwp = torch.empty(64, 192, dtype=torch.float32, device=frames.device)
+    db = torch.empty(64, dtype=torch.float32, device=frames.device)
+    wp, b, d = _pack(weight), bias.detach().float().contiguous(), dfeat.float().contiguous()
+    check(L.f3_rgb_backward(ptr(frames), ptr(wp), ptr(b), ptr(d), ptr(dwp), ptr(db), ptr(scratch), scratch.numel(),
+                            B, T, stream_handle()), "rgb backward")
+    return dwp.reshape(64, 8, 8, 3).permute(0, 3, 1, 2).contiguous(), db
+
+
+@rgb_backward.register_fake
+def _(frames, weight, bias, dfeat):
+    return weight.new_empty(weight.shape, dtype=torch.float32), bias.new_empty(bias.shape, dtype=torch.float32)
+
+
+def _rgb_setup(ctx, inputs, output):
+    frames, weight, bias = inputs
+    ctx.save_for_backward(frames, weight, bias)
+
+
+def _rgb_bwd(ctx, dfeat):
+    frames, weight, bias = ctx.saved_tensors
+    dw, db = torch.ops.fall3.rgb_backward(frames, weight, bias, dfeat)
+    return None, dw.to(weight.dtype), db.to(bias.dtype)
+
+
+rgb_forward.register_autograd(_rgb_bwd, setup_context=_rgb_setup)
+
+
+class RGBSpatialConv(nn.Module):
+    """Conv2d(3, 64, 8, stride 8) -> ReLU -> mean over frames and patches (nn.Conv2d's default init)."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(64, 3, 8, 8, device=device))
+        self.bias = nn.Parameter(torch.empty(64, device=device))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(3 * 8 * 8)
+        nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, frames: Tensor) -> Tensor:
+        return torch.ops.fall3.rgb_forward(frames, self.weight, self.bias)
+
+
+class RGBBranch(nn.Module):
+    """The branch's late-fusion logits: RGBSpatialConv -> Linear(64, num_class)."""
+
+    def __init__(self, num_class: int, device=None):
+        super().__init__()
+        self.conv = RGBSpatialConv(device=device)
+        self.fc = nn.Linear(64, num_class, device=device)
+
+    def forward(self, frames: Tensor) -> Tensor:
+        return self.fc(self.conv(frames))
+
+
+class Fall3WithRGB(nn.Module):
+    """The reference's 3-stream model (unchanged, its own state_dict keys under `fall3.`) plus the
+    build-defined RGB branch; logits = fall3(skel, sensor) + rgb(frames)."""
+
+    def __init__(self, fall3: nn.Module, num_class: int, device=None):
+        super().__init__()
+        self.fall3 = fall3
+        self.rgb = RGBBranch(num_class, device=device)
+
+    def forward(self, skel: Tensor, sensor: Optional[Tensor], frames: Tensor) -> Tensor:
+        return self.fall3(skel, sensor) + self.rgb(frames)

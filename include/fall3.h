@@ -150,6 +150,17 @@ int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void*
                       double* st_sq, int N, int T_in, int T_out, int V, int Cin, int Cout, int stride, int transposed,
                       int epi, void* stream);
 
+/* RGB spatial-conv branch (BUILD-DEFINED: the reference has RGB frames only in preprocessing,
+ * 3_stream/har_create3.py:36-42,101-158, so its parity is unpinned; the north star names it).
+ * frames bf16 [B][T][224][224][3]; wpack bf16 [64][192] (the Conv2d(3, 64, 8, stride 8) weight
+ * [64][3][8][8] with k = (dy*8 + dx)*3 + ch); feat[B][64] = mean over frames and the 28 x 28 patch
+ * grid of relu(conv + bias) (overwritten). The backward gives dw [64][192] (packed order) and
+ * db [64] (overwritten) from dfeat [B][64]; scratch holds f3_rgb_scratch_floats(B, T) floats. */
+long long f3_rgb_scratch_floats(int B, int T);
+int f3_rgb_forward(const void* frames, const void* wpack, const float* bias, float* feat, int B, int T, void* stream);
+int f3_rgb_backward(const void* frames, const void* wpack, const float* bias, const float* dfeat, float* dw, float* db,
+                    float* scratch, long long scratch_floats, int B, int T, void* stream);
+
 /* Graph mix of one st_gcan block (stgcan.py:54, applied to the gcn input):
  * z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci]; backward gives dx and dA_eff (overwritten). */
 int f3_graph_mix_forward(const float* A_eff, const float* x, float* z, int frames, int K, int V, int Cin,
