@@ -948,6 +948,15 @@ void head_args(const f3_net& net, int N, const Ptrs& q, Ws& w, HeadArgs& h) {
   }
 }
 
+// flags of the events that fork / join the branch queues. They order work between queues of ONE
+// device, so a device-scope release is all they need; hipEventRecord's default is a system-scope
+// fence (L2 writeback + invalidate at every record). F3_EV_SCOPE: 0 = HIP's default release,
+// 1 = device-scope release (default), 2 = no fence at the record.
+static unsigned branch_event_flags() {
+  static const int v = getenv("F3_EV_SCOPE") ? atoi(getenv("F3_EV_SCOPE")) : 1;
+  return hipEventDisableTiming | (v == 1 ? hipEventReleaseToDevice : v == 2 ? hipEventDisableSystemFence : 0u);
+}
+
 // Private branch streams, created on the first eager call (never during a capture: there the
 // branches stay on the caller's stream). F3_SERIAL=1 keeps everything on one stream.
 bool ensure_parallel(f3_net& n, hipStream_t s) {
@@ -959,13 +968,14 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   }
   n.par_init = true;
   if (getenv("F3_SERIAL")) return n.par_ok = false;
+  const unsigned evf = branch_event_flags();
   bool ok = true;
   for (auto& a : n.aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
-  for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
+  for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (int i = 0; i < 2; ++i)
     for (int l = 0; l < 7; ++l) {
-      ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], evf) == hipSuccess;
     }
   (void)hipGetLastError();
   return n.par_ok = ok;
@@ -1018,7 +1028,7 @@ struct Branches {
     if (hipStreamIsCapturing(s, &cs) != hipSuccess) return F3_EHIP;
     if (cs != hipStreamCaptureStatusNone) return join();
     for (auto& e : n.ev_p1)  // (serial mode never created the branch events)
-      if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return F3_EHIP;
+      if (!e && hipEventCreateWithFlags(&e, branch_event_flags()) != hipSuccess) return F3_EHIP;
     for (int i = 0; i < 3 && par; ++i) {
       if (!(mask >> i & 1)) continue;
       if (hipEventRecord(n.ev_p1[i], n.aux[i]) != hipSuccess) return F3_EHIP;

@@ -37,6 +37,7 @@ constexpr int RG_PPT = (RG_STRIP16 + 255) / 256;                 // pieces per t
 constexpr int RG_K = RG_P * RG_P * 3;                            // 192
 constexpr int RG_KS = RG_K / 32;                                 // 6 MFMA k-steps
 constexpr int RG_STRIPS = RG_G;                                  // strips per frame
+constexpr int RG_BWD_MAXFPB = 15;                                // frames per backward workgroup (512 workgroups = 2 per CU at B=256, T=30)
 typedef unsigned rg_u32x4 __attribute__((ext_vector_type(4)));  // (HIP's rg_u32x4 struct arrays went to scratch)
 
 // patch p of a strip, k-group idx (8 consecutive k = one dy band's (dx, ch) 8-run): byte offset
@@ -64,7 +65,10 @@ F3_DEV void rg_load_strip(const char* src, rg_u32x4 (&r)[RG_PPT]) {
 }
 
 // the conv pre-activations of this wave's 16 channels for the strip in LDS: acc[t][i] =
-// conv[p = 16t + 4fg + i][c = 16w + fr] (without bias; rows 28..31 are clamped duplicates)
+// conv[p][c = 16w + fr] (without bias) for patch p = 16t + 4fg + i (PERM = false), or
+// p = 8fg + 4t + i (PERM = true: lane fg then holds patches 8fg .. 8fg + 7 of its channel, which is
+// the B-operand layout of a product that sums over patches). Rows p >= 28 are clamped duplicates.
+template <bool PERM>
 F3_DEV void rg_conv(const char* strip, const bf16x8 (&wf)[RG_KS], int fr, int fg, f32x4 (&acc)[2]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -73,7 +77,7 @@ F3_DEV void rg_conv(const char* strip, const bf16x8 (&wf)[RG_KS], int fr, int fg
     const int idx = s * 4 + fg;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int p = min(t * 16 + fr, RG_G - 1);
+      const int p = min(PERM ? 8 * (fr >> 2) + 4 * t + (fr & 3) : t * 16 + fr, RG_G - 1);
       const bf16x8 fa = *reinterpret_cast<const bf16x8*>(strip + rg_off(p, idx));
       acc[t] = mfma_bf16x(fa, wf[s], acc[t]);
     }
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256) void rgb_fwd_kernel(RgbArgs a) {
     rg_load_strip(strip_src(min(k + 2, nstrip - 1)), P);  // (unconditional: see rg_store_strip)
     __syncthreads();
     f32x4 acc[2];
-    rg_conv(buf, wf, fr, fg, acc);
+    rg_conv<false>(buf, wf, fr, fg, acc);
     const int clip = (f0 + k / RG_STRIPS) / a.T;
     if (clip != fcur) {
       flush(fcur);
@@ -143,10 +147,21 @@ __global__ __launch_bounds__(256) void rgb_fwd_kernel(RgbArgs a) {
   flush(fcur);
 }
 
+// dW^T[k][c] = sum_p X^T[k][p] mask[p][c] per strip, on bf16 MFMA 16x16x32 without any LDS copy
+// besides the staged strip: A = X^T comes straight from the strip image through the transposed LDS
+// read (ds_read_b64_tr_b16: a 16-lane group reads 4 patches x 16 consecutive k and each lane gets
+// one k's 4 patches), B = the exact 0/1 relu mask, built in registers by the permuted conv
+// (rg_conv<true>). The mask is constant-weighted within a clip (g = dfeat / (T*784) where the
+// pre-activation is > 0), so the MFMAs accumulate the clip's unscaled sums and its df scales them
+// in fp32 when the block moves to the next clip.
+typedef short rg_s16x4 __attribute__((ext_vector_type(4)));
+F3_DEV rg_s16x4 rg_tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) rg_s16x4*)(p));
+}
+
 __global__ __launch_bounds__(256) void rgb_bwd_kernel(RgbArgs a) {
   __shared__ __attribute__((aligned(16))) char sbuf[2][RG_STRIP];
-  __shared__ __attribute__((aligned(16))) __bf16 stt[RG_K][40];     // strip transposed [k][p] (p < 32)
-  __shared__ __attribute__((aligned(16))) __bf16 gt[4][16][40];     // per wave: g^T [c][p]
+  __shared__ float dfs[RG_BWD_MAXFPB][64];  // dfeat / (T*784) of this block's clips
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
@@ -161,12 +176,38 @@ __global__ __launch_bounds__(256) void rgb_bwd_kernel(RgbArgs a) {
     const int f = f0 + k / RG_STRIPS, sy = k % RG_STRIPS;
     return img + ((size_t)f * RG_IMG * RG_IMG * 3) * 2 + (size_t)sy * RG_STRIP;
   };
-  // the zero padding of the transposed strip (p = 28..31) and of g^T
-  for (int i = tid; i < RG_K * 40; i += 256) (&stt[0][0])[i] = (__bf16)0.f;
-  for (int i = tid; i < 4 * 16 * 40; i += 256) (&gt[0][0][0])[i] = (__bf16)0.f;
-  f32x4 dw[12];  // dW[c = 16w + 4fg + i][k = 16j + fr] (MFMA C layout: m = c, n = k)
+  // the upstream gradient of every clip this block touches (at most fpb clips), read once here so
+  // the strip loop has no global load besides the strip prefetch
+  const int clip0 = f0 / a.T;
+  for (int i = tid; i < RG_BWD_MAXFPB * 64; i += 256) {
+    const int cl = min(clip0 + i / 64, a.B - 1);
+    dfs[i / 64][i % 64] = a.dfeat[(size_t)cl * 64 + i % 64] * inv;
+  }
+  // transposed-read addresses: lane (q = fr >> 2, r = fr & 3) of group fg points at patch
+  // 8fg + 4h + q, k = 16j + 4r .. +3 (one dy band: 24 is a multiple of 4); patches past 27 clamp
+  int troff[2][12];
 #pragma unroll
-  for (int j = 0; j < 12; ++j) dw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int p = min(8 * fg + 4 * h + (fr >> 2), RG_G - 1), kc = 16 * j + 4 * (fr & 3);
+      const int dy = kc / 24;
+      troff[h][j] = dy * RG_ROWB + p * 48 + (kc - dy * 24) * 2;
+    }
+  f32x4 dw[12];   // dW^T[k = 16j + 4fg + i][c = 16w + fr]
+  f32x4 dwc[12];  // the current clip's unscaled mask^T x patch sums (scaled by its df at the clip's end)
+#pragma unroll
+  for (int j = 0; j < 12; ++j) dw[j] = dwc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int ccur = 0;  // clip of dwc (relative to clip0)
+  auto flush = [&]() __attribute__((always_inline)) {
+    const float dfc = dfs[ccur][wave * 16 + fr];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dw[j][i] = fmaf(dfc, dwc[j][i], dw[j][i]);
+      dwc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
   float dbs = 0.f;
   rg_u32x4 pa[RG_PPT], pb[RG_PPT];
   if (nstrip > 0) {
@@ -178,45 +219,42 @@ __global__ __launch_bounds__(256) void rgb_bwd_kernel(RgbArgs a) {
     rg_store_strip(buf, P);
     rg_load_strip(strip_src(min(k + 2, nstrip - 1)), P);  // (unconditional: see rg_store_strip)
     __syncthreads();
-    // transposed copy of the strip: stt[k][p] = patch[p][k] (k in (dy, dx, ch) order)
-    for (int e = tid; e < RG_G * RG_K; e += 256) {
-      const int p = e / RG_K, kk = e - p * RG_K, dy = kk / 24, r = kk - dy * 24;
-      stt[kk][p] = *reinterpret_cast<const __bf16*>(buf + dy * RG_ROWB + p * 48 + r * 2);
-    }
     f32x4 acc[2];
-    rg_conv(buf, wf, fr, fg, acc);
-    const int clip = (f0 + k / RG_STRIPS) / a.T;
-    const float df = a.dfeat[(size_t)clip * 64 + wave * 16 + fr] * inv;
-    // g[p][c] = df where conv + bias > 0; lane holds rows p = 16t + 4fg + i of column c = fr
+    rg_conv<true>(buf, wf, fr, fg, acc);
+    const int cl = (f0 + k / RG_STRIPS) / a.T - clip0;
+    if (cl != ccur) {
+      flush();
+      ccur = cl;
+    }
+    const float df = dfs[cl][wave * 16 + fr];
+    bf16x8 mk;  // B operand: mask[p = 8fg + e][c = fr]
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int p = t * 16 + fg * 4 + i;
-        const float g = (p < RG_G && acc[t][i] + bias > 0.f) ? df : 0.f;
-        dbs += g;
-        gt[wave][fr][p] = (__bf16)g;
+        const bool on = 8 * fg + 4 * t + i < RG_G && acc[t][i] + bias > 0.f;
+        dbs += on ? df : 0.f;
+        mk[4 * t + i] = (__bf16)(on ? 1.f : 0.f);
       }
-    __syncthreads();  // stt and every wave's gt written
-    // dW[c][k] += sum_p g^T[c][p] strip^T[k][p]: A = g^T (m = c, k = p), B^T = strip^T (n = k, k = p)
-    const bf16x8 ga = *reinterpret_cast<const bf16x8*>(&gt[wave][fr][fg * 8]);
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
-      const bf16x8 pb = *reinterpret_cast<const bf16x8*>(&stt[j * 16 + fr][fg * 8]);
-      dw[j] = mfma_bf16x(ga, pb, dw[j]);
+      const rg_s16x4 lo = rg_tr_read(buf + troff[0][j]), hi = rg_tr_read(buf + troff[1][j]);
+      // (whole-vector bit cast: element-wise short -> __bf16 casts were mis-assembled by hipcc)
+      const bf16x8 xa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      dwc[j] = mfma_bf16x(xa, mk, dwc[j]);
     }
-    __syncthreads();  // buf, stt, gt are rewritten by the next strip
+    __syncthreads();  // buf is restaged two strips later; every wave's reads of it are done
   };
   for (int k = 0; k < nstrip; k += 2) {
     step(k, sbuf[0], pa);
     if (k + 1 < nstrip) step(k + 1, sbuf[1], pb);
   }
+  flush();
   // this workgroup's partial row: dW [64][192] then db [64]
   float* row = a.part + (size_t)blockIdx.x * (64 * RG_K + 64);
 #pragma unroll
   for (int j = 0; j < 12; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) row[(size_t)(wave * 16 + fg * 4 + i) * RG_K + j * 16 + fr] = dw[j][i];
+    *reinterpret_cast<f32x4*>(row + (size_t)(wave * 16 + fr) * RG_K + j * 16 + fg * 4) = dw[j];
   dbs += __shfl_xor(dbs, 16, 64);
   dbs += __shfl_xor(dbs, 32, 64);
   if (fg == 0) row[64 * RG_K + wave * 16 + fr] = dbs;
@@ -285,7 +323,7 @@ static RgbArgs rgb_args(const void* frames, const void* wpack, const float* bias
   return a;
 }
 
-constexpr int kRgbFwdFpb = 6, kRgbBwdFpb = 12;
+constexpr int kRgbFwdFpb = 6, kRgbBwdFpb = RG_BWD_MAXFPB;
 
 extern "C" {
 

@@ -57,18 +57,28 @@ class RMSprop(torch.optim.Optimizer):
         return flat
 
     def _flat_cached(self, ps, cache):
+        """The remembered layout still holds when every gradient is contiguous and sits at its
+        parameter's relative offset from the first gradient, and that gradient's storage spans the
+        whole range: the gradients then ARE the range of one buffer. (Addresses, not `_base`: the
+        autograd engine hands parameters detached gradients, which share the buffer but are not
+        views of it, so a `_base` test failed on every step and sent it to the full ~7 us/parameter
+        check.)"""
         ids, rel, flat_p, flat_sq, sq0, p0 = cache
         if tuple(map(id, ps)) != ids or self.state[p0].get("square_avg") is not sq0:
             return None
         g0 = p0.grad
-        base = g0._base if g0._base is not None else g0
+        if g0.dtype != torch.float32 or g0.device != p0.device:
+            return None
+        n = flat_p.numel()
         gbase = g0.storage_offset()
+        if (gbase + n) * 4 > g0.untyped_storage().nbytes():
+            return None
+        a0 = g0.data_ptr()
         for p, r in zip(ps, rel):
             g = p.grad
-            if (g._base if g._base is not None else g) is not base or g.storage_offset() - gbase != r \
-                    or not g.is_contiguous():
+            if g is None or g.data_ptr() - a0 != 4 * r or not g.is_contiguous() or g.dtype != torch.float32:
                 return None
-        return flat_p, flat_sq, _flat_view(g0, gbase, flat_p.numel())
+        return flat_p, flat_sq, _flat_view(g0, gbase, n)
 
     def _flat_full(self, ps):
         ps = sorted(ps, key=lambda t: t.storage_offset())  # module order is not the flat order

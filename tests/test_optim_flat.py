@@ -81,3 +81,22 @@ def test_flat_per_tensor_update_matches_torch_cpu_layout():
     fa, fb = opt._flat(opt.param_groups[0]), opt._flat(opt.param_groups[1])
     assert fa[0].numel() == 4 and fb[0].numel() == 4
     assert fa[0].storage_offset() == 0 and fb[0].storage_offset() == 4
+
+
+def test_cached_layout_takes_detached_gradients():
+    """loss.backward() gives each parameter a DETACHED gradient that shares the flat gradient buffer
+    (no `_base`): the cached layout must still be recognised without the full per-tensor check, and
+    a gradient that moved must still be rejected."""
+    ps, flat, G = _setup()
+    opt = RMSprop(ps, lr=1e-3)
+    assert opt._flat(opt.param_groups[0]) is not None  # full check, layout cached
+    for p in ps:
+        p.grad = p.grad.detach()
+        assert p.grad._base is None
+    calls = []
+    full = opt._flat_full
+    opt._flat_full = lambda q: calls.append(1) or full(q)
+    r = opt._flat(opt.param_groups[0])
+    assert r is not None and not calls and r[2].data_ptr() == G.data_ptr() and r[2].numel() == 20
+    ps[2].grad = G[9:12].detach().clone()  # a gradient outside the buffer
+    assert opt._flat(opt.param_groups[0]) is None and calls

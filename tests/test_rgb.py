@@ -53,8 +53,9 @@ def test_rgb_kernels_vs_oracle(B, T):
     dfeat = torch.randn(B, 64, generator=torch.Generator().manual_seed(7))
     dw, db = torch.ops.fall3.rgb_backward(fd, wd, bd, dfeat.to(dev))
     (ref * dfeat.double()).sum().backward()
-    # dW is summed over T*784 patches of bf16 activations x the fp32 relu mask / count
-    tw = 2e-3 * wr.grad.abs().max().item()
+    # dW: exact 0/1 relu mask x bf16 patches on MFMA, scaled by dfeat/(T*784) in fp32 (a mask bit
+    # that flips between the fp32 and the fp64 pre-activation moves one patch term, ~1e-4 of max)
+    tw = 5e-4 * wr.grad.abs().max().item()
     assert (dw.cpu().double() - wr.grad).abs().max().item() < tw
     assert (db.cpu().double() - br.grad).abs().max().item() < 1e-4 * max(1.0, br.grad.abs().max().item())
 
