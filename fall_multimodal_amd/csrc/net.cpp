@@ -83,6 +83,7 @@ struct f3_net {
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_main[2][7] = {};  // per (skeleton stream, layer) main -> side hand-offs
+  hipEvent_t ev_early[2][7] = {}; // ... once the layer's dh / dres exist (tcn + residual wgrad)
   // end of backward phase 1 on each queue it used ([0..2] aux, [3] the caller's stream): the
   // gradient all-reduce of the phase-1 bucket waits on these instead of the caller's stream
   // joining every queue, so phase 2's critical path starts while phase 1's weight gradients drain
@@ -104,6 +105,7 @@ struct f3_net {
     for (int i = 0; i < 2; ++i)
       for (int l = 0; l < 7; ++l) {
         if (ev_main[i][l]) (void)hipEventDestroy(ev_main[i][l]);
+        if (ev_early[i][l]) (void)hipEventDestroy(ev_early[i][l]);
       }
   }
   f3_config cfg;
@@ -679,9 +681,9 @@ bool debug_stop(int si, int l) {
 // caller flushes it (one prep launch per stream) after the stream's last layer call.
 // Main stream s: the chain that carries the input gradient down the layers. Side stream ss
 // (== s when not parallel): the layer's weight gradients (tcn / gcn / residual wgrad, gcn
-// bias + edge importance), which nothing downstream waits for. Layer l's side work starts
-// after ev_main[si][l]; it reads only per-layer tensors, so the only side -> main edge is the
-// final join. (Main also waiting on the side stream per layer — double-buffered scratch —
+// bias + edge importance), which nothing downstream waits for. Layer l's side work starts after
+// ev_main[si][l] (F3_SIDE_EARLY: part of it after ev_early[si][l], see below). It reads only
+// per-layer tensors, so the only side -> main edge is the final join. (Main also waiting on the side stream per layer — double-buffered scratch —
 // made HIP's stream-capture end fault on ROCm 7.2.)
 int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
                     int l_hi, int l_lo, PrepTable& unpack, hipStream_t ss = nullptr, int call_hi = 6, int part = 3) {
@@ -734,6 +736,12 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
     if (part & 1) F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
     if (part & 1) F3_TRY(f3_block_bwd_apply(ba, s));
+    // F3_SIDE_EARLY=1 starts the tcn / residual / CA weight gradients at ev_early (right after
+    // block_bwd_apply) instead of after the layer's whole main chain: measured SLOWER (5.69 vs
+    // 5.54 ms/step, profiles/r03_side_early_ab.txt) - the side work then takes CUs from the main
+    // chain, which is the step's critical path - so it is off
+    static const bool early = getenv("F3_SIDE_EARLY") ? atoi(getenv("F3_SIDE_EARLY")) != 0 : false;
+    if (early && split && (part & 1) && hipEventRecord(net.ev_early[si][l], s) != hipSuccess) return F3_EHIP;
     // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
@@ -792,7 +800,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     }
     // ---- side stream: this layer's weight gradients ----
     if (split && (part & 1) && hipEventRecord(net.ev_main[si][l], s) != hipSuccess) return F3_EHIP;
-    if (split && (part & 2) && hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
+    if (split && (part & 2) && hipStreamWaitEvent(ss, early ? net.ev_early[si][l] : net.ev_main[si][l], 0) != hipSuccess)
+      return F3_EHIP;
     WgradArgs tw;
     std::memset(&tw, 0, sizeof(tw));
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
@@ -813,6 +822,20 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 1, ss));
     }
     if (part & 2) F3_TRY(f3_ca_bwd_weights(&ca, ss));
+    if (L.res == RES_CONV) {
+      WgradArgs rw;
+      std::memset(&rw, 0, sizeof(rw));
+      rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
+      rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
+      if (hb) {
+        rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+        if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
+      } else {
+        rw.dy = dres; rw.in = X.x;
+      }
+      if (part & 2) F3_TRY(f3_conv_wgrad(&rw, 0, ss));
+    }
+    if (early && split && (part & 2) && hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
     if (split) {  // reductions whose results only feed weight gradients
       const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
       if (part & 2) F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
@@ -838,19 +861,6 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
     gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
     if (part & 2) F3_TRY(f3_gcn_bias_bwd(&gb, ss));
-    if (L.res == RES_CONV) {
-      WgradArgs rw;
-      std::memset(&rw, 0, sizeof(rw));
-      rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
-      if (hb) {
-        rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
-        if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
-      } else {
-        rw.dy = dres; rw.in = X.x;
-      }
-      if (part & 2) F3_TRY(f3_conv_wgrad(&rw, 0, ss));
-    }
     dout = dx;
     pp ^= 1;
   }
@@ -970,12 +980,22 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   if (getenv("F3_SERIAL")) return n.par_ok = false;
   const unsigned evf = branch_event_flags();
   bool ok = true;
-  for (auto& a : n.aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+  // F3_SIDE_PRIO=1: the two queues that carry the weight gradients (aux[1], aux[2]) get the
+  // device's least priority, so the workgroup dispatcher favours the main chains (the step's
+  // critical path) when both have work
+  static const int prio = getenv("F3_SIDE_PRIO") ? atoi(getenv("F3_SIDE_PRIO")) : 0;
+  int least = 0, greatest = 0;
+  if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  for (int i = 0; i < 3; ++i)
+    ok = ok && (prio && i >= 1 && least != greatest
+                    ? hipStreamCreateWithPriority(&n.aux[i], hipStreamNonBlocking, least)
+                    : hipStreamCreateWithFlags(&n.aux[i], hipStreamNonBlocking)) == hipSuccess;
   for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (int i = 0; i < 2; ++i)
     for (int l = 0; l < 7; ++l) {
       ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], evf) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&n.ev_early[i][l], evf) == hipSuccess;
     }
   (void)hipGetLastError();
   return n.par_ok = ok;
