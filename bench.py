@@ -16,7 +16,7 @@ GPU, torch.distributed.run as a child process) and fails if the node has fewer t
 
 Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
 ranks), the roofline of the dominant kernel (the temporal-conv weight-gradient GEMM, measured
-live with HIP events on the stream it runs on; HBM traffic from profiles/r01_roofline_pmc.json) and the CPU baseline (the oracle timed on this
+live with HIP events on the stream it runs on; HBM traffic from profiles/r03_roofline_pmc.json) and the CPU baseline (the oracle timed on this
 host's cores on a bounded sample).
 """
 import argparse
@@ -99,7 +99,7 @@ def launch_check(world, rank):
     dist.destroy_process_group()
 
 
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 
 
 def _time_launch(fn, reps=20):

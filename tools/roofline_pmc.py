@@ -32,7 +32,8 @@ NAMES = {"wgrad": f"{_KN} + slab reduce (tcn 9x1 weight gradient incl. the split
          "wgrad_kernel": f"{_KN} alone (partials left in the slab, {_SHAPE})",
          "wgrad_l5": "wgrad_big<4,2,4,4,64> + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, "
                      "stride 2, C=256, T=15->8, N=256, V=18)",
-         "tcn_fwd": f"igemm_big (clip window unless F3_BIG_WIN=0) bf16-out (tcn 9x1 fwd, {_SHAPE})"}
+         "tcn_fwd": ("igemm_big<1,2,4,false,true> (clip window)" if os.environ.get("F3_BIG_WIN", "1") != "0"
+                     else "igemm_big<1,1,8>") + f" bf16-out (tcn 9x1 fwd, {_SHAPE})"}
 
 
 def run():
