@@ -1165,27 +1165,62 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   *reinterpret_cast<f32x4*>(row + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
-// u = relu(g * scale + shift) in bf16 (BN1 + ReLU of the tcn input, bf16 mode)
+// u = relu(g * scale + shift) in bf16 (BN1 + ReLU of the tcn input, bf16 mode). A thread owns
+// one 8-channel group for the whole launch: the grid stride (gridDim * 256 * 8 elements) is a
+// multiple of C, so its 8 scale / shift pairs are loaded once into registers; kBnReluU 16-B pieces
+// are loaded before any is converted (one memory round trip per kBnReluU pieces); 4 workgroups
+// per CU walk the rows so the per-workgroup coefficient prologue is paid ~4x per CU, not per piece.
+constexpr int kBnReluU = 4;
 template <bool G16>
 __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
-  __shared__ float sc[256], sh[256];
+  __shared__ float scs[256], shs[256];
   for (int c = threadIdx.x; c < a.C; c += 256) {
     float mu, rs;
-    bn_coeff(a.bn, c, sc[c], sh[c], mu, rs);
+    bn_coeff(a.bn, c, scs[c], shs[c], mu, rs);
   }
   __syncthreads();
-  const size_t total8 = (size_t)a.M * a.C / 8;
-  for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < total8; q += (size_t)gridDim.x * 256) {
-    const size_t e0 = q * 8;
-    const int c0 = (int)(e0 % a.C);
-    const f32x4 x0 = ld_act4<G16>(a.g, e0), x1 = ld_act4<G16>(a.g, e0 + 4);
+  const int c0 = (threadIdx.x * 8) % a.C;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scs[c0 + e];
+    sh[e] = shs[c0 + e];
+  }
+  const long long total8 = (long long)a.M * a.C / 8, step = (long long)gridDim.x * 256;
+  long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  auto piece = [&](long long qq, f32x4& x0, f32x4& x1) __attribute__((always_inline)) {
+    if constexpr (G16) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.g) + qq * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x0[e] = (float)v[e];
+        x1[e] = (float)v[4 + e];
+      }
+    } else {
+      x0 = *reinterpret_cast<const f32x4*>(a.g + qq * 8);
+      x1 = *reinterpret_cast<const f32x4*>(a.g + qq * 8 + 4);
+    }
+  };
+  auto put = [&](long long qq, const f32x4& x0, const f32x4& x1) __attribute__((always_inline)) {
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      o[e] = (__bf16)fmaxf(x0[e] * sc[c0 + e] + sh[c0 + e], 0.f);
-      o[4 + e] = (__bf16)fmaxf(x1[e] * sc[c0 + 4 + e] + sh[c0 + 4 + e], 0.f);
+      o[e] = (__bf16)fmaxf(x0[e] * sc[e] + sh[e], 0.f);
+      o[4 + e] = (__bf16)fmaxf(x1[e] * sc[4 + e] + sh[4 + e], 0.f);
     }
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + e0) = o;
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + qq * 8) = o;
+  };
+  for (; q + (kBnReluU - 1) * step < total8; q += kBnReluU * step) {
+    f32x4 x0[kBnReluU], x1[kBnReluU];
+#pragma unroll
+    for (int u = 0; u < kBnReluU; ++u) piece(q + u * step, x0[u], x1[u]);
+#pragma unroll
+    for (int u = 0; u < kBnReluU; ++u) put(q + u * step, x0[u], x1[u]);
+  }
+  for (; q < total8; q += step) {
+    f32x4 x0, x1;
+    piece(q, x0, x1);
+    put(q, x0, x1);
   }
 }
 
@@ -1729,7 +1764,12 @@ int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
+// rows per workgroup of the clip-chunk elementwise kernels (block_out, block_bwd_*):
+// F3_CHUNK_ROWS (default 96)
+static int chunks_for(int TV) {
+  static const int rows = getenv("F3_CHUNK_ROWS") ? std::max(16, atoi(getenv("F3_CHUNK_ROWS"))) : 96;
+  return max(1, (TV + rows - 1) / rows);
+}
 
 // backward block kernels: instantiate on (activation type, residual kind, pooled gradient)
 template <bool A16, int RES, bool DNC>
@@ -1817,7 +1857,9 @@ int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) 
 int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   if (a->C % 8 || a->C > 256) return F3_EINVAL;
   const size_t total8 = (size_t)a->M * a->C / 8;
-  const int grid = (int)std::min<size_t>((total8 + 255) / 256, 4096);
+  // (the kernel needs 2048 % C == 0: a thread's channel group is fixed over its grid stride)
+  if (2048 % a->C) return F3_EINVAL;
+  const int grid = (int)std::min<size_t>((total8 + 256 * kBnReluU - 1) / (256 * kBnReluU), 1024);
   if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
   else hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();

@@ -740,7 +740,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     // block_bwd_apply) instead of after the layer's whole main chain: measured SLOWER (5.69 vs
     // 5.54 ms/step, profiles/r03_side_early_ab.txt) - the side work then takes CUs from the main
     // chain, which is the step's critical path - so it is off
-    static const bool early = getenv("F3_SIDE_EARLY") ? atoi(getenv("F3_SIDE_EARLY")) != 0 : false;
+    // F3_SIDE_EARLY=2: only for the last layer (0), whose weight gradients are the step's tail
+    static const int early_mode = getenv("F3_SIDE_EARLY") ? atoi(getenv("F3_SIDE_EARLY")) : 0;
+    const bool early = early_mode == 1 || (early_mode == 2 && l == 0);
     if (early && split && (part & 1) && hipEventRecord(net.ev_early[si][l], s) != hipSuccess) return F3_EHIP;
     // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
     ConvGemmArgs td;
