@@ -1091,12 +1091,33 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
 
 // BN1 backward: dg = g1*rs1*(dv - S1/M - xhat1*S2/M), and the per-node column sums
 // G[v][c] = sum_{n,t} dg (gcn bias / edge-importance gradients). One workgroup per
-// (clip, kBnBwdFrames frames); thread (v, 8-channel group) walks the frames, so each
+// (clip, FR frames); thread (v, 8-channel group) walks the frames, so each
 // thread owns its G entries (no atomics) and a frame [V][C] is read contiguously. Each
 // workgroup writes one partial row [V][C]; f3_colsum adds the rows into G.
-constexpr int kBnBwdFrames = 4;
+// F3_BNBWD_FR: frames per workgroup (4 or 8; default 4), read in batches of 4 frames whose loads
+// are all issued before any use
+static int bn_bwd_frames() {
+  static const int v = getenv("F3_BNBWD_FR") && atoi(getenv("F3_BNBWD_FR")) == 8 ? 8 : 4;
+  return v;
+}
 
+// 8 activations at off: one 16-B load in the bf16 mode, two in fp32
 template <bool A16>
+F3_DEV void ld_act8(const void* p, size_t off, f32x4& x0, f32x4& x1) {
+  if constexpr (A16) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(p) + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x0[e] = (float)v[e];
+      x1[e] = (float)v[4 + e];
+    }
+  } else {
+    x0 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off);
+    x1 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + off + 4);
+  }
+}
+
+template <bool A16, int FR>
 __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __shared__ float mu[256], kk[256], m1[256], m2[256], rsv[256];
   const int C = a.C, CG = C / 8, V = a.V, T = a.TV / V, tid = threadIdx.x;
@@ -1118,46 +1139,47 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   }
   const int v = tid / CG, c0 = (tid - v * CG) * 8;
   if (v >= V) return;
-  const int n = blockIdx.y, t0 = blockIdx.x * kBnBwdFrames, t1 = min(T, t0 + kBnBwdFrames);
+  const int n = blockIdx.y, t0 = blockIdx.x * FR, t1 = min(T, t0 + FR);
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-  // all frames' loads first (clamped to the last frame, masked out of the sums; see kRowU)
-  f32x4 d0[kBnBwdFrames], d1[kBnBwdFrames], g0[kBnBwdFrames], g1[kBnBwdFrames];
-#pragma unroll
-  for (int u = 0; u < kBnBwdFrames; ++u) {
-    const size_t off = ((size_t)(n * T + min(t0 + u, t1 - 1)) * V + v) * C + c0;
-    d0[u] = ld_act4<A16>(a.dv, off);
-    d1[u] = ld_act4<A16>(a.dv, off + 4);
-    g0[u] = ld_act4<A16>(a.g, off);
-    g1[u] = ld_act4<A16>(a.g, off + 4);
-  }
   float ck[8], cm1[8], cm2[8], cmu[8], crs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     ck[e] = kk[c0 + e]; cm1[e] = m1[c0 + e]; cm2[e] = m2[c0 + e]; cmu[e] = mu[c0 + e]; crs[e] = rsv[c0 + e];
   }
 #pragma unroll
-  for (int u = 0; u < kBnBwdFrames; ++u) {
-    const int t = min(t0 + u, t1 - 1);
-    const size_t off = ((size_t)(n * T + t) * V + v) * C + c0;
-    const bool live = t0 + u < t1;
-    float o[8];
+  for (int b = 0; b < FR; b += 4) {
+    // the batch's loads first (clamped to the last frame, masked out of the sums; see kRowU)
+    f32x4 d0[4], d1[4], g0[4], g1[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float dv = e < 4 ? d0[u][e] : d1[u][e - 4];
-      const float gv = e < 4 ? g0[u][e] : g1[u][e - 4];
-      o[e] = ck[e] * (dv - cm1[e] - (gv - cmu[e]) * crs[e] * cm2[e]);
-      if (live) acc[e] += o[e];
+    for (int u = 0; u < 4; ++u) {
+      const size_t off = ((size_t)(n * T + min(t0 + b + u, t1 - 1)) * V + v) * C + c0;
+      ld_act8<A16>(a.dv, off, d0[u], d1[u]);
+      ld_act8<A16>(a.g, off, g0[u], g1[u]);
     }
-    if (a.dgb) {
-      bf16x8 ob;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ob[e] = (__bf16)o[e];
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
-    } else {
-      *reinterpret_cast<f32x4*>(a.dg + off) = f32x4{o[0], o[1], o[2], o[3]};
-      *reinterpret_cast<f32x4*>(a.dg + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    for (int u = 0; u < 4; ++u) {
+      const int t = min(t0 + b + u, t1 - 1);
+      const size_t off = ((size_t)(n * T + t) * V + v) * C + c0;
+      const bool live = t0 + b + u < t1;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dv = e < 4 ? d0[u][e] : d1[u][e - 4];
+        const float gv = e < 4 ? g0[u][e] : g1[u][e - 4];
+        o[e] = ck[e] * (dv - cm1[e] - (gv - cmu[e]) * crs[e] * cm2[e]);
+        if (live) acc[e] += o[e];
+      }
+      if (a.dgb) {
+        bf16x8 ob;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ob[e] = (__bf16)o[e];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
+      } else {
+        *reinterpret_cast<f32x4*>(a.dg + off) = f32x4{o[0], o[1], o[2], o[3]};
+        *reinterpret_cast<f32x4*>(a.dg + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      }
     }
   }
   float* row = a.Gpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * V * C + v * C + c0;
@@ -1834,14 +1856,23 @@ int f3_block_bwd_apply(BlockArgs a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_bn_bwd_parts(int N, int TV, int V) { return ((TV / V + kBnBwdFrames - 1) / kBnBwdFrames) * N; }
+int f3_bn_bwd_parts(int N, int TV, int V) {
+  const int fr = bn_bwd_frames();
+  return ((TV / V + fr - 1) / fr) * N;
+}
 
 int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
   if (a.C % 8 || a.C > 256 || a.TV % a.V || a.V * (a.C / 8) > 1024 || !a.Gpart) return F3_EINVAL;
-  const int T = a.TV / a.V, fch = (T + kBnBwdFrames - 1) / kBnBwdFrames;
+  const int fr = bn_bwd_frames();
+  const int T = a.TV / a.V, fch = (T + fr - 1) / fr;
   const int threads = ((a.V * (a.C / 8) + 63) / 64) * 64;
-  if (a.act16) hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(fch, a.N), dim3(threads), 0, s, a);
-  else hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(fch, a.N), dim3(threads), 0, s, a);
+  if (fr == 8) {
+    if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
+  } else {
+    if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
+  }
   F3_LAUNCH_CHECK();
   if (a.no_colsum) return F3_OK;
   return f3_colsum(a.Gpart, fch * a.N, a.V * a.C, a.G, s);
