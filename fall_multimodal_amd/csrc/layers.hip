@@ -1370,6 +1370,7 @@ __global__ __launch_bounds__(256) void ca_bwd1_kernel(CaArgs a) {
   if (j < H) {
     float acc0 = 0.f, acc1 = 0.f;
     int c = wv;
+#pragma unroll 8
     for (; c + 4 < C; c += 8) {
       acc0 += dq[c] * a.W2[(size_t)c * H + j];
       acc1 += dq[c + 4] * a.W2[(size_t)(c + 4) * H + j];
