@@ -23,7 +23,7 @@ EXPORTS = (
     "f3_graph_mix_backward", "f3_graph_mix_forward_ex", "f3_graph_mix_backward_ex", "f3_net_backward_phase",
     "f3_net_grad_split", "f3_net_wait_phase1",
     "f3_targcn_create", "f3_targcn_destroy", "f3_targcn_num_entries", "f3_targcn_entry", "f3_targcn_param_count",
-    "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_targcn_stage_times", "f3_net_sensor_times", "f3_soft_ce",
+    "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_targcn_stage_times", "f3_targcn_status", "f3_net_sensor_times", "f3_soft_ce",
     "f3_sktr_create", "f3_sktr_destroy", "f3_sktr_num_entries", "f3_sktr_entry", "f3_sktr_param_count",
     "f3_sktr_buffer_count", "f3_sktr_counter_count", "f3_sktr_workspace_bytes", "f3_sktr_forward", "f3_sktr_backward",
     "f3_musa_create", "f3_musa_destroy", "f3_musa_num_entries", "f3_musa_entry", "f3_musa_param_count",
@@ -32,7 +32,7 @@ EXPORTS = (
     "f3_dwconv_t_forward", "f3_pointwise_conv", "f3_rgb_scratch_floats", "f3_rgb_forward", "f3_rgb_backward",
 )
 
-F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE = 0, 1001, 1002, 1003, 1004
+F3_OK, F3_EINVAL, F3_EBATCH, F3_EHIP, F3_ESTATE, F3_EDEVICE = 0, 1001, 1002, 1003, 1004, 1005
 ENTRY_PARAM, ENTRY_BUFFER, ENTRY_COUNTER = 0, 1, 2
 
 
@@ -101,6 +101,7 @@ def lib():
         "f3_targcn_buffer_count": (I64, [P]),
         "f3_targcn_workspace_bytes": (I64, [P, I]),
         "f3_targcn_stage_times": (I, [P, I, P]),
+        "f3_targcn_status": (I, [P, I]),
         "f3_net_sensor_times": (I, [P, I, P]),
         "f3_targcn_forward": (I, [P, I, P, P, P, P, P, P]),
         "f3_targcn_backward": (I, [P, I, P, P, P, P, P, P]),

@@ -404,6 +404,7 @@ using namespace f3;
 
 int f3_conv_gemm(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
+  if (a.x3) return f3_conv_gemm_x3(args, pro, epi, s);
   if (a.wb) return f3_conv_gemm_bf16(args, pro, epi, s);
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (pro && a.g.Kc > 256) return F3_EINVAL;
@@ -427,6 +428,7 @@ int f3_conv_gemm(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
 }
 
 int f3_conv_wgrad(const WgradArgs* args, int pro, hipStream_t s) {
+  if (args->x3) return f3_conv_wgrad_x3(args, pro, s);
   if (args->bf16) {
     if (!pro && f3_wgrad_glds_ok(*args)) return f3_wgrad_glds_bf16(args, s);
     return f3_conv_wgrad_bf16(args, pro, s);

@@ -43,6 +43,7 @@ struct ConvGemmArgs {
   int ldaux;
   const unsigned short* auxb;  // RELUMASK source rows stored bf16 (instead of aux)
   BnRef epi_bn;
+  int x3;             // 1: split-bf16 kernel (fp32 in / out; wb = hi plane, wb + Nc*KT*Kc = lo plane)
 };
 
 enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };
@@ -76,6 +77,7 @@ struct WgradArgs {
   int groups;
   long long gs_dy, gs_in, gs_dw, gs_db;
   int dbg;                    // measurement knob of wgrad_taps (F3_TAPS_DBG): 1 no MFMA, 2 no restaging
+  int x3;                     // 1: split-bf16 kernel on fp32 dy / in (gemm_x3.hip)
 };
 
 // Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).
@@ -119,3 +121,6 @@ int f3_igemm_big(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_wgrad_glds_ok(const f3::WgradArgs& a);
 int f3_wgrad_glds_bf16(const f3::WgradArgs* a, hipStream_t s);
 int f3_conv_wgrad_bf16(const f3::WgradArgs* a, int pro, hipStream_t s);
+// split-bf16 (bf16x3) forms (gemm_x3.hip): fp32 activations, weights as pre-split bf16 hi / lo planes
+int f3_conv_gemm_x3(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
+int f3_conv_wgrad_x3(const f3::WgradArgs* a, int pro, hipStream_t s);

@@ -75,8 +75,15 @@ __global__ void prep_kernel(PrepTable t) {
         break;
       }
     }
-    if (j.bf16) reinterpret_cast<__bf16*>(j.dst)[e] = (__bf16)val;  // RNE (v_cvt_pk_bf16_f32)
-    else j.dst[e] = val;
+    if (j.bf16 == 2) {  // bf16x3 mode: hi = RNE bf16(val) at [e], lo = RNE bf16(val - hi) at [n + e]
+      const __bf16 hi = (__bf16)val;
+      reinterpret_cast<__bf16*>(j.dst)[e] = hi;
+      reinterpret_cast<__bf16*>(j.dst)[j.n + e] = (__bf16)(val - (float)hi);
+    } else if (j.bf16) {
+      reinterpret_cast<__bf16*>(j.dst)[e] = (__bf16)val;  // RNE (v_cvt_pk_bf16_f32)
+    } else {
+      j.dst[e] = val;
+    }
   }
 }
 
@@ -1246,6 +1253,39 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
   }
 }
 
+// widths whose 8-channel groups do not tile 2048 threads (C % 8 == 0, 2048 % C != 0, e.g. 96 / 192):
+// the piece's channel group is taken per piece (the pre-round-3 indexing)
+template <bool G16>
+__global__ __launch_bounds__(256) void bnrelu_bf16_any_kernel(BnReluArgs a) {
+  __shared__ float scs[256], shs[256];
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    float mu, rs;
+    bn_coeff(a.bn, c, scs[c], shs[c], mu, rs);
+  }
+  __syncthreads();
+  const long long total8 = (long long)a.M * a.C / 8, step = (long long)gridDim.x * 256;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total8; q += step) {
+    const int c0 = (int)((q * 8) % a.C);
+    float x[8];
+    if constexpr (G16) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.g) + q * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = (float)v[e];
+    } else {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(a.g + q * 8), x1 = *reinterpret_cast<const f32x4*>(a.g + q * 8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = x0[e];
+        x[4 + e] = x1[e];
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (__bf16)fmaxf(x[e] * scs[c0 + e] + shs[c0 + e], 0.f);
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + q * 8) = o;
+  }
+}
+
 // out[c] += sum_r part[r][c]: 64 columns x 64 rows per workgroup, one atomic per column
 __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int rows, int cols, float* out) {
   __shared__ float red[4][64];
@@ -1889,8 +1929,14 @@ int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) 
 int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   if (a->C % 8 || a->C > 256) return F3_EINVAL;
   const size_t total8 = (size_t)a->M * a->C / 8;
-  // (the kernel needs 2048 % C == 0: a thread's channel group is fixed over its grid stride)
-  if (2048 % a->C) return F3_EINVAL;
+  // (the main kernel needs 2048 % C == 0: a thread's channel group is fixed over its grid stride)
+  if (2048 % a->C) {
+    const int grid = (int)std::min<size_t>((total8 + 255) / 256, 4096);
+    if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_any_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL(bnrelu_bf16_any_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   const int grid = (int)std::min<size_t>((total8 + 256 * kBnReluU - 1) / (256 * kBnReluU), 1024);
   if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
   else hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, *a);

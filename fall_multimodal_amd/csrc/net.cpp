@@ -519,6 +519,11 @@ void add_job(PrepTable& t, int type, int n, float* dst, const float* s0, const f
 
 // bf16 view of a packed operand (the fp32-sized slot holds the bf16 copy in bf16 mode)
 inline const unsigned short* bf(const float* p, int on) { return on ? reinterpret_cast<const unsigned short*>(p) : nullptr; }
+// bf16x3 mode (F3_PRECISION_BF16X3): fp32 activations as in the fp32 mode, GEMMs on the split-bf16
+// kernels (gemm_x3.hip) with the packed weights as bf16 hi / lo planes (prep code 2)
+inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X3; }
+// prep code of the packed GEMM weights: 0 fp32, 1 bf16, 2 split hi / lo planes
+inline int wcode(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16 ? 1 : is_x3(n) ? 2 : 0; }
 // bf16 view of an activation slot (bf16 mode stores GEMM operand tensors as bf16)
 inline unsigned short* bfa(float* p, int on) { return on ? reinterpret_cast<unsigned short*>(p) : nullptr; }
 
@@ -541,6 +546,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V, eval = !train;
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
+  const int wc = wcode(net);
   // weights: A_eff, gcn bias through the graph, packed GEMM operands
   PrepTable pt;
   pt.n = 0;
@@ -551,15 +557,15 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     const int C = L.cout, Ci = L.cin;
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
-    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, hb);
-    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, hb);
+    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
+    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, wc);
     if (train) {
-      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, hb);
-      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, hb);
+      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
+      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, wc);
     }
     if (L.res == RES_CONV) {
-      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, hb);
-      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, hb);
+      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, wc);
+      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, wc);
     }
   }
   F3_TRY(f3_prep(pt, s));
@@ -581,6 +587,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V, eval = !train;
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
+  const int x3 = is_x3(net), wq = hb || x3;
   {
     const LayerIdx& L = S.L[l];
     LayerWs& X = W.L[l];
@@ -609,7 +616,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       std::memset(&ga, 0, sizeof(ga));
       ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
       ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
-      ga.w = X.gw; ga.wb = bf(X.gw, hb); ga.out = X.g; ga.outb = bfa(X.g, hb);
+      ga.w = X.gw; ga.wb = bf(X.gw, wq); ga.out = X.g; ga.outb = bfa(X.g, hb); ga.x3 = x3;
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
       F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     }
@@ -619,7 +626,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ra.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
       ra.in = hb ? nullptr : X.x; ra.inb = hb ? X.xb : nullptr; ra.zero = w.zero;
       if (hb && !X.xb) return F3_ESTATE;
-      ra.w = X.rw; ra.wb = bf(X.rw, hb); ra.out = X.r; ra.outb = bfa(X.r, hb);
+      ra.w = X.rw; ra.wb = bf(X.rw, wq); ra.out = X.r; ra.outb = bfa(X.r, hb); ra.x3 = x3;
       ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
@@ -627,7 +634,8 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     ConvGemmArgs ta;
     std::memset(&ta, 0, sizeof(ta));
     ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
-    ta.w = X.tw; ta.wb = bf(X.tw, hb); ta.out = X.h; ta.outb = bfa(X.h, hb); ta.bias = q.p(L.tcn_b);
+    ta.w = X.tw; ta.wb = bf(X.tw, wq); ta.out = X.h; ta.outb = bfa(X.h, hb); ta.bias = q.p(L.tcn_b);
+    ta.x3 = x3;
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
     if (hb) {  // materialise u = relu(bn1(g)) in bf16 (also the tcn wgrad operand)
       BnReluArgs br;
@@ -694,6 +702,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   StreamWs& W = w.st[si];
   const int K = net.K, V = net.V;
   const int hb = net.cfg.precision == F3_PRECISION_BF16;
+  const int x3 = is_x3(net), wq = hb || x3;
   const float* dout = l_hi == 6 ? nullptr : W.dx[(5 - l_hi) & 1];
   int pp = (6 - l_hi) & 1;
   for (int l = l_hi; l >= l_lo; --l) {
@@ -749,7 +758,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
     td.in = hb ? nullptr : dh; td.inb = bfa(dh, hb); td.zero = w.zero;
-    td.w = X.twT; td.wb = bf(X.twT, hb); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.w = X.twT; td.wb = bf(X.twT, wq); td.x3 = x3; td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     if (part & 1) F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
@@ -778,7 +787,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&gd, 0, sizeof(gd));
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
-    gd.w = X.gwT; gd.wb = bf(X.gwT, hb); gd.out = W.dZ;
+    gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
     const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
       if (!f3_igemm_ok(gd)) return F3_EINVAL;
@@ -797,7 +806,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       std::memset(&rd, 0, sizeof(rd));
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
       rd.in = hb ? nullptr : dres; rd.inb = bfa(dres, hb); rd.zero = w.zero;
-      rd.w = X.rwT; rd.wb = bf(X.rwT, hb); rd.out = dx;
+      rd.w = X.rwT; rd.wb = bf(X.rwT, wq); rd.x3 = x3; rd.out = dx;
       if (part & 1) F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
     }
     // ---- side stream: this layer's weight gradients ----
@@ -808,7 +817,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&tw, 0, sizeof(tw));
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
     tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
-    tw.outmap = WG_OUT_CONV; tw.bf16 = hb;
+    tw.outmap = WG_OUT_CONV; tw.bf16 = hb; tw.x3 = x3;
     if (hb) {  // bf16 operands dh, u; split partials in the stream's slab, summed into the grads
       tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
       if (wgrad_slab()) {
@@ -828,7 +837,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
       rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
-      rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb;
+      rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb; rw.x3 = x3;
       if (hb) {
         rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
@@ -857,7 +866,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     } else {
       gw.dy = dg; gw.in = X.z;
     }
-    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb;
+    gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
     if ((part & 2) && !g0) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
@@ -1082,7 +1091,9 @@ int f3_net_create(const f3_config* cfg, f3_net** out) {
   if (cfg->num_node < 2 || cfg->num_partition < 1 || cfg->num_class < 1 || cfg->num_class > 64) return F3_EINVAL;
   if (cfg->frames < 2 || cfg->model < 0 || cfg->model > 3) return F3_EINVAL;
   if (cfg->num_partition * cfg->num_node * cfg->num_node > 1024) return F3_EINVAL;
-  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16) return F3_EINVAL;  // not 2
+  if (cfg->precision != F3_PRECISION_FP32 && cfg->precision != F3_PRECISION_BF16 &&
+      cfg->precision != F3_PRECISION_BF16X3)
+    return F3_EINVAL;  // not 2 (kernel-level entries only)
   f3_net* n = new f3_net();
   n->cfg = *cfg;
   n->K = cfg->num_partition;
@@ -1390,14 +1401,15 @@ static float* test_scratch(size_t n) {
 int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
                     int V, int Cin, int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (precision < 0 || precision > F3_CONV_BF16_OUT) return F3_EINVAL;
+  if (precision < 0 || precision > F3_PRECISION_BF16X3) return F3_EINVAL;
   const bool bf_out = precision == F3_CONV_BF16_OUT;
   if (bf_out) precision = F3_PRECISION_BF16;
+  const int x3 = precision == F3_PRECISION_BF16X3;
   const int hb = precision != F3_PRECISION_FP32;
   if (w) {  // w == NULL: wpack already holds the packed operand (timing the GEMM alone)
     PrepTable t;
     t.n = 0;
-    add_job(t, PREP_PACK_CONV, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, hb);
+    add_job(t, PREP_PACK_CONV, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, x3 ? 2 : hb);
     F3_TRY(f3_prep(t, s));
   }
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
@@ -1410,7 +1422,7 @@ int f3_conv_forward(const void* x, const float* w, const float* bias, float* out
   } else {
     a.in = (const float*)x;
   }
-  a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias;
+  a.w = wpack; a.wb = bf(wpack, hb); a.out = out; a.bias = bias; a.x3 = x3;
   if (bf_out) a.outb = reinterpret_cast<unsigned short*>(out);
   return f3_conv_gemm(&a, 0, EPI_BIAS, s);
 }
@@ -1418,11 +1430,12 @@ int f3_conv_forward(const void* x, const float* w, const float* bias, float* out
 int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpack, int N, int T_in, int V, int Cin,
                           int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (precision < 0 || precision > 2) return F3_EINVAL;
+  if (precision < 0 || (precision > 2 && precision != F3_PRECISION_BF16X3)) return F3_EINVAL;
+  const int x3 = precision == F3_PRECISION_BF16X3;
   const int hb = precision != F3_PRECISION_FP32;
   PrepTable t;
   t.n = 0;
-  add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, hb);
+  add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin, wpack, w, nullptr, nullptr, Cout, Cin, KT, x3 ? 2 : hb);
   F3_TRY(f3_prep(t, s));
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
@@ -1434,7 +1447,7 @@ int f3_conv_backward_data(const void* dy, const float* w, float* dx, float* wpac
   } else {
     a.in = (const float*)dy;
   }
-  a.w = wpack; a.wb = bf(wpack, hb); a.out = dx;
+  a.w = wpack; a.wb = bf(wpack, hb); a.out = dx; a.x3 = x3;
   return f3_conv_gemm(&a, 0, 0, s);
 }
 
@@ -1464,7 +1477,7 @@ int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void*
 int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,
                             int Cout, int KT, int stride, int pad, int precision, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (precision < 0 || precision > 2) return F3_EINVAL;
+  if (precision < 0 || (precision > 2 && precision != F3_PRECISION_BF16X3)) return F3_EINVAL;
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
   if (db && hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
@@ -1472,7 +1485,8 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
   std::memset(&a, 0, sizeof(a));
   a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, Cin, Cout);
   a.ldy = Cout; a.dw = dw; a.db = db; a.outmap = WG_OUT_CONV;
-  a.bf16 = precision != F3_PRECISION_FP32;
+  a.x3 = precision == F3_PRECISION_BF16X3;
+  a.bf16 = precision != F3_PRECISION_FP32 && !a.x3;
   if (precision == F3_PRECISION_BF16) {
     a.dyb = (const unsigned short*)dy;
     a.inb = (const unsigned short*)x;
@@ -1614,6 +1628,7 @@ const char* f3_status_string(int st) {
     case F3_EBATCH: return "Expected more than 1 value per channel when training";
     case F3_EHIP: return "HIP launch error";
     case F3_ESTATE: return "backward without a training forward";
+    case F3_EDEVICE: return "device-side check failed (a GRU group barrier timed out; outputs are invalid)";
     default: return "unknown status";
   }
 }

@@ -53,6 +53,7 @@ struct GruFwdArgs {
   unsigned short* hx;   // [B][V][H] bf16 h_t of every node
   unsigned short* rhx;  // [B][V][H] bf16 r*h of every node
   int* gsync;           // [GN_MAXG] counters, then an error flag
+  int dbg_skip_arrive;  // test knob (F3_GN_SKIP_ARRIVE): workgroup 0 never arrives -> barrier timeout
 };
 
 constexpr int GN_BT = 32;     // clips per group of the node-partitioned recurrence
@@ -82,6 +83,7 @@ struct GruBwdArgs {
   unsigned short* gx1;  // [B][V][IP] bf16 (update part)
   unsigned short* gx2;  // [B][V][IP] bf16 (gate part)
   int* gsync;           // [GN_MAXG] counters, then an error flag
+  int dbg_skip_arrive;
 };
 
 struct TaArgs {

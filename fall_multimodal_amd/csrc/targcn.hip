@@ -447,24 +447,30 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
 // 6 x 4 bf16x8 fragments = 96 VGPRs). The node mixing S.[x, h] needs every node's h, so h and r*h
 // are exchanged through memory (hx, rhx) with two group barriers per step. The launch is
 // cooperative (all workgroups co-resident, or the launch fails and the clip-tile kernel runs);
-// a barrier that does not complete within ~2^22 polls sets the error flag and stops waiting, so a
-// fault shows as wrong results and a flag, never as a hang.
+// a barrier that does not complete within ~2^22 polls sets the error flag (gsync[GN_MAXG]) and
+// stops waiting, so a fault never hangs: the net copies the flag to a host status word after the
+// launch and the next f3_targcn_* call (or f3_targcn_status) returns F3_EDEVICE.
 // Numerics are those of gru_fwd_kernel: X = bf16([x, h]), Y = bf16(sum_m S[n][m] X_m) in fp32
 // in m order, fp32 MFMA accumulation, fp32 epilogue and saved tensors.
 // ---------------------------------------------------------------------------------------------
 constexpr int GN_THREADS = 256;
 constexpr int GN_XS = IP + 8;  // LDS row stride (bf16): 272-B rows
 
-F3_DEV void gn_barrier(int* cnt, int target, int* err) {
+// `arrive` false: this workgroup does not count itself (the F3_GN_SKIP_ARRIVE test knob, which
+// makes the group's barriers time out). Once any barrier has timed out (err set), every later
+// barrier returns after the first poll that sees the flag, so a faulted launch drains quickly.
+F3_DEV void gn_barrier(int* cnt, int target, int* err, bool arrive = true) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's exchange stores have reached L2
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();  // agent-scope release: the group's other XCDs see the stores
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrive) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int polls = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++polls > (1 << 22)) {
+      ++polls;
+      if ((polls & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (polls > (1 << 22)) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -487,6 +493,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_fwd_node_kernel(GruFwdArgs a) 
   const int col = lane & 15, rq = lane >> 4, cw = 16 * w + col, kofs = 8 * rq;
   int* cnt = a.gsync + g;
   int* err = a.gsync + GN_MAXG;
+  const bool arrive = !(a.dbg_skip_arrive && blockIdx.x == 0);
   for (int i = tid; i < GN_BT * GN_XS; i += GN_THREADS) {
     Ys[i] = (__bf16)0.f;
     Xs[i] = (__bf16)0.f;
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_fwd_node_kernel(GruFwdArgs a) 
         }
       }
     }
-    gn_barrier(cnt, V * ++nbar, err);  // every node's r*h (and every wave's reads of Xs / Ys) done
+    gn_barrier(cnt, V * ++nbar, err, arrive);  // every node's r*h (and every wave's reads of Xs / Ys) done
     // ---- update input: X = [x_t, r*h] of node n, Y = S.[x_t, r*h] (x parts unchanged) ----
     mix_h(a.rhx, false);
 #pragma unroll
@@ -675,7 +682,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_fwd_node_kernel(GruFwdArgs a) 
         }
       }
     }
-    gn_barrier(cnt, V * ++nbar, err);  // every node's h_t (and every wave's reads of Xs / Ys) done
+    gn_barrier(cnt, V * ++nbar, err, arrive);  // every node's h_t (and every wave's reads of Xs / Ys) done
   }
 }
 
@@ -1001,6 +1008,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_bwd_node_kernel(GruBwdArgs a) 
   const bool has_dx = a.dX != nullptr && Din == H;
   int* cnt = a.gsync + g;
   int* err = a.gsync + GN_MAXG;
+  const bool arrive = !(a.dbg_skip_arrive && blockIdx.x == 0);
   for (int i = tid; i < GN_BT * GN_XS; i += GN_THREADS) {
     AG[i] = (__bf16)0.f;
     AS[i] = (__bf16)0.f;
@@ -1138,7 +1146,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_bwd_node_kernel(GruBwdArgs a) 
     part_gemm(wu, lu, std::integral_constant<int, H / 32>{});
     __syncthreads();
     emit_gx(a.gx1, a.DUG, t);
-    gn_barrier(cnt, V * ++nbar, err);  // every node's update-part GX rows
+    gn_barrier(cnt, V * ++nbar, err, arrive);  // every node's update-part GX rows
     mix_t(a.gx1);
     __syncthreads();
     // ---- gate part ----
@@ -1172,7 +1180,7 @@ __global__ __launch_bounds__(GN_THREADS) void gru_bwd_node_kernel(GruBwdArgs a) 
     part_gemm(wg, lg, std::integral_constant<int, 2 * H / 32>{});
     __syncthreads();
     emit_gx(a.gx2, a.DXG, t);
-    gn_barrier(cnt, V * ++nbar, err);  // every node's gate-part GX rows
+    gn_barrier(cnt, V * ++nbar, err, arrive);  // every node's gate-part GX rows
     mix_t(a.gx2);
     __syncthreads();
 #pragma unroll

@@ -58,6 +58,15 @@ struct f3_targcn {
   // f3_targcn_stage_times: timing events around the recurrences and the TA layers (0 = off)
   int timing = 0;
   hipEvent_t tev[11] = {};
+  // GRU group-barrier error flag, copied to a pinned host word after the recurrences
+  int* status_host = nullptr;
+  hipEvent_t status_ev = nullptr;
+  bool status_pending = false;
+  ~f3_targcn() {
+    for (auto& e : tev) if (e) (void)hipEventDestroy(e);
+    if (status_ev) (void)hipEventDestroy(status_ev);
+    if (status_host) (void)hipHostFree(status_host);
+  }
 
   int64_t add(const std::string& name, std::vector<int64_t> shape, int kind = F3_ENTRY_PARAM) {
     int64_t n = 1;
@@ -208,6 +217,54 @@ inline void mark(f3_targcn* n, int i, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// F3_GN_SKIP_ARRIVE=1: test knob, workgroup 0 of the node-partitioned recurrences never arrives at
+// the group barriers (they time out and raise the flag)
+int gn_skip_arrive() {
+  const char* e = getenv("F3_GN_SKIP_ARRIVE");
+  return e && atoi(e) != 0;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;
+  }
+  return cs != hipStreamCaptureStatusNone;
+}
+
+// a completed, flagged copy from an earlier call -> F3_EDEVICE (the word is cleared)
+int take_status(f3_targcn* net, bool wait) {
+  if (!net->status_pending || !net->status_ev) return F3_OK;
+  if (wait) {
+    if (hipEventSynchronize(net->status_ev) != hipSuccess) return F3_EHIP;
+  } else if (hipEventQuery(net->status_ev) != hipSuccess) {
+    (void)hipGetLastError();
+    return F3_OK;
+  }
+  net->status_pending = false;
+  const int flag = *net->status_host;
+  *net->status_host = 0;
+  return flag ? F3_EDEVICE : F3_OK;
+}
+
+// enqueue the copy of the flag (gsync[GN_MAXG]) to the host word
+int post_status(f3_targcn* net, const int* gsync, hipStream_t s) {
+  if (capturing(s)) return F3_OK;  // the node-partitioned path is off under capture
+  if (!net->status_host && hipHostMalloc(&net->status_host, sizeof(int), hipHostMallocDefault) != hipSuccess)
+    return F3_EHIP;
+  if (!net->status_ev && hipEventCreateWithFlags(&net->status_ev, hipEventDisableTiming) != hipSuccess) return F3_EHIP;
+  if (hipMemcpyAsync(net->status_host, gsync + GN_MAXG, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
+    return F3_EHIP;
+  if (hipEventRecord(net->status_ev, s) != hipSuccess) return F3_EHIP;
+  net->status_pending = true;
+  return F3_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int f3_targcn_create(const f3_targcn_config* cfg, f3_targcn** out) {
@@ -293,6 +350,10 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
   const Plan p = plan(net, B);
   void* ws = workspace;
   const int V = net->V, b16 = net->prec == F3_PRECISION_BF16;
+  TG_TRY(take_status(net, false));
+  // clear the barrier counters and the error flag once per forward (each recurrence launch
+  // re-zeroes only its counters, so a flag raised by layer 0 survives to the status copy)
+  if (hipMemsetAsync(at<char>(ws, p.gsync), 0, sizeof(int) * (GN_MAXG + 1), s) != hipSuccess) return F3_EHIP;
   const float* E = params + net->E;
   float* S = at<float>(ws, p.S);
   float* cs = at<float>(ws, p.cs);
@@ -320,6 +381,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     g.HC = at<float>(ws, p.HC[l]); g.SU = at<float>(ws, p.SU[l]);
     g.XG = at<void>(ws, p.XG[l]); g.XI = at<void>(ws, p.XI[l]); g.UG = at<void>(ws, p.UG[l]); g.UI = at<void>(ws, p.UI[l]);
     g.hx = at<unsigned short>(ws, p.hx); g.rhx = at<unsigned short>(ws, p.rhx); g.gsync = at<int>(ws, p.gsync);
+    g.dbg_skip_arrive = gn_skip_arrive();
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
@@ -339,6 +401,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
       fprintf(stderr, "\n");
     }
   }
+  if (b16) TG_TRY(post_status(net, at<int>(ws, p.gsync), s));
   for (int l = 0; l < 2; ++l) {  // transformer_layer (TA.py:101-108)
     TaArgs a = ta_args(net, l, B, params);
     a.in = l == 0 ? at<float>(ws, p.H[1]) : at<float>(ws, p.ta_out0);
@@ -365,6 +428,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
   const Plan p = plan(net, B);
   void* ws = workspace;
   const int V = net->V, b16 = net->prec == F3_PRECISION_BF16;
+  TG_TRY(take_status(net, false));
   if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
   if (hipMemsetAsync(at<char>(ws, p.zero_begin), 0, p.zero_end - p.zero_begin, s) != hipSuccess) return F3_EHIP;
   // Linear(64 -> C)
@@ -411,6 +475,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     g.DP = at<void>(ws, p.DP); g.DSG = at<void>(ws, p.DSG); g.DU = at<void>(ws, p.DU); g.DSU = at<void>(ws, p.DSU);
     g.DXG = at<void>(ws, p.DXG); g.DUG = at<void>(ws, p.DUG);
     g.gx1 = at<unsigned short>(ws, p.gx1); g.gx2 = at<unsigned short>(ws, p.gx2); g.gsync = at<int>(ws, p.gsync);
+    g.dbg_skip_arrive = gn_skip_arrive();
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
@@ -464,6 +529,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     sg.dS = dS;
     TG_TRY(f3_tg_supp_grad(&sg, b16, s));
   }
+  if (b16) TG_TRY(post_status(net, at<int>(ws, p.gsync), s));
   for (int l = 0; l < 2; ++l)
     for (int q = 0; q < 2; ++q) {
       const EmbOff& e = net->emb[l][q];
@@ -496,6 +562,11 @@ int f3_targcn_stage_times(f3_targcn* net, int enable, float* ms) {
   }
   net->timing = enable;
   return F3_OK;
+}
+
+int f3_targcn_status(f3_targcn* net, int wait) {
+  if (!net) return F3_EINVAL;
+  return take_status(net, wait != 0);
 }
 
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream) {

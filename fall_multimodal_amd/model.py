@@ -34,7 +34,7 @@ from .graph import STRATEGY_PARTITIONS, Graph
 
 MODEL_IDS = {"two_stgcan_bilstm": 0, "two_stgcan": 1, "stgcn": 2, "bilstm": 3}
 SENSOR_IDS = {"none": 0, "bilstm": 1, "cnn_bilstm": 2}
-PRECISION_IDS = {"fp32": 0, "bf16": 1}
+PRECISION_IDS = {"fp32": 0, "bf16": 1, "bf16x3": 4}
 
 
 @dataclass
@@ -51,7 +51,8 @@ class NetSpec:
     naming: str = "package"
     frames: int = 30
     sensor_frames: int = 30
-    precision: str = "fp32"   # "fp32": exact fp32 MFMA (parity mode); "bf16": bf16 operands, fp32 accumulate
+    precision: str = "fp32"   # "fp32": exact fp32 MFMA; "bf16": bf16 operands, fp32 accumulate;
+    #                           "bf16x3": fp32 activations, split-bf16 GEMMs (parity at bf16-MFMA rates)
     extra: dict = field(default_factory=dict)
 
 
@@ -377,7 +378,7 @@ class TwoStreamSpatialTemporalGraph(Fall3Net):
 
 def build_model(config, device=None, precision="fp32"):
     """build_model.py:5-19: MODEL.NAME in {stgcn, bilstm, two_stgcan, two_stgcan_bilstm}.
-    `precision` ("fp32" | "bf16") selects the GEMM operand type of the skeleton streams."""
+    `precision` ("fp32" | "bf16" | "bf16x3") selects the GEMM arithmetic of the skeleton streams."""
     name = config.MODEL.NAME
     graph_args = {"layout": config.GRAPH.LAYOUT, "strategy": config.GRAPH.STRATEGY}
     if name == "stgcn":

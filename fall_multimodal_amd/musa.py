@@ -230,15 +230,24 @@ class Model(nn.Module):
         return out
 
 
-_NONE_GRAD = re.compile(r"(^|\.)A$|^stream_(pos|mot)\.[12]\.edge$")
+_FROZEN = re.compile(r"(^|\.)A$")
+_SEP_EDGE = re.compile(r"^stream_(pos|mot)\.[12]\.edge$")
 
 
-def grad_is_none(name):
-    """True for the parameters whose .grad the reference leaves None after backward: the frozen
-    graphs `A` and the SepTemporal blocks' `edge`, which only shape the DropBlock masks
-    (musa_model.py:148-199; f3_musa_backward zero-fills their slots). Adam/AdamW with weight
-    decay would otherwise move them on a zero gradient."""
-    return bool(_NONE_GRAD.search(name))
+def grad_is_none(name, dropblock_active):
+    """True for the parameters whose .grad the reference leaves None after backward.
+    * The graphs `A` (requires_grad False): always.
+    * The SepTemporal blocks' `edge` (musa_model.py:184-198): it enters the graph only through
+      Randomized_DropBlock_Ske's M = matmul(M_seed, A * edge), whose every element the masked writes
+      `M[M > 0.001] = 1.0; M[M < 0.5] = 0.0` (musa_model.py:66-69) then overwrite with a constant.
+      With DropBlock active (training, keep_prob < 1: the driver's 0.9, musa_model.py:510) autograd
+      therefore gives edge an all-ZERO gradient tensor - so weight-decaying optimizers (the
+      reference's SGD / Adam / AdamW builders) still move it and keep state for it. Without DropBlock
+      (keep_prob 1, eval) edge is unused and its gradient stays None. f3_musa_backward zero-fills
+      these slots either way."""
+    if _FROZEN.search(name):
+        return True
+    return bool(_SEP_EDGE.search(name)) and not dropblock_active
 
 
 class MusaStep:
@@ -257,10 +266,11 @@ class MusaStep:
         self.dout = torch.empty_like(self.out)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.last_seed = None
-        # A (frozen) and the SepTemporal blocks' edge get zero gradients, which RMSprop maps to a
-        # zero update (square_avg stays 0): they stay put, as torch.optim skips their None grads
+        # A (frozen) has no gradient; the SepTemporal blocks' edges get the zero gradient the
+        # reference's DropBlock gives them (None without DropBlock). RMSprop maps a zero gradient
+        # to a zero update (square_avg stays 0), as torch.optim.RMSprop (no weight decay) does
         for (name, shape, off), p in zip(model.param_views(), model.parameters()):
-            if not grad_is_none(name):
+            if not grad_is_none(name, model.dropblock):
                 p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
 
     def forward_backward(self, x, label, seed=None):

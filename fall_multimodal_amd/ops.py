@@ -291,8 +291,9 @@ def _mu_backward(ctx, dout, dws, dbuf, dcnt):
     m = _module(ctx.net)
     grads = torch.ops.fall3.musa_backward(ctx.net, list(m.parameters()), dout.float(), ws)
     from .musa import grad_is_none
-    # A (frozen) and the SepTemporal edges get None, as the reference's autograd leaves them
-    gl = [None if grad_is_none(name) else g for g, (name, _, _) in zip(_split_grads(m, grads), m.param_views())]
+    # None where the reference's autograd leaves None: A (frozen) always, the SepTemporal edges
+    # unless DropBlock ran (then the reference gives them a zero tensor; musa.grad_is_none)
+    gl = [None if grad_is_none(name, m.dropblock) else g for g, (name, _, _) in zip(_split_grads(m, grads), m.param_views())]
     return None, gl, None, None, None, None, None
 
 

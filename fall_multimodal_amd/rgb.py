@@ -24,12 +24,25 @@ def _pack(w: Tensor) -> Tensor:  # [64, 3, 8, 8] -> bf16 [64, 192], k = (dy*8 + 
     return w.detach().permute(0, 2, 3, 1).reshape(w.shape[0], -1).to(torch.bfloat16).contiguous()
 
 
+def _check_frames(frames: Tensor, weight: Tensor, bias: Tensor, dfeat: Optional[Tensor] = None):
+    """Validation shared by both custom ops (they hand raw pointers to the kernels)."""
+    require_device(frames, "frames")
+    if frames.dim() != 5 or frames.dtype != torch.bfloat16 or tuple(frames.shape[2:]) != (224, 224, 3) \
+            or not frames.is_contiguous():
+        raise ValueError("fall3 rgb: frames must be contiguous bf16 [B, T, 224, 224, 3]")
+    if tuple(weight.shape) != (64, 3, 8, 8) or tuple(bias.shape) != (64,):
+        raise ValueError("fall3 rgb: weight must be [64, 3, 8, 8] and bias [64]")
+    tensors = [weight, bias] + ([] if dfeat is None else [dfeat])
+    if any(t.device != frames.device for t in tensors):
+        raise ValueError("fall3 rgb: frames, weight, bias (and dfeat) must be on one device")
+    if dfeat is not None and tuple(dfeat.shape) != (frames.shape[0], 64):
+        raise ValueError(f"fall3 rgb: dfeat must be [{frames.shape[0]}, 64], got {tuple(dfeat.shape)}")
+
+
 @torch.library.custom_op("fall3::rgb_forward", mutates_args=())
 def rgb_forward(frames: Tensor, weight: Tensor, bias: Tensor) -> Tensor:
-    require_device(frames, "frames")
+    _check_frames(frames, weight, bias)
     B, T = frames.shape[:2]
-    if frames.dtype != torch.bfloat16 or tuple(frames.shape[2:]) != (224, 224, 3) or not frames.is_contiguous():
-        raise ValueError("fall3 rgb: frames must be contiguous bf16 [B, T, 224, 224, 3]")
     feat = torch.empty(B, 64, dtype=torch.float32, device=frames.device)
     wp, b = _pack(weight), bias.detach().float().contiguous()
     check(lib().f3_rgb_forward(ptr(frames), ptr(wp), ptr(b), ptr(feat), B, T, stream_handle()), "rgb forward")
@@ -43,6 +56,7 @@ def _(frames, weight, bias):
 
 @torch.library.custom_op("fall3::rgb_backward", mutates_args=())
 def rgb_backward(frames: Tensor, weight: Tensor, bias: Tensor, dfeat: Tensor) -> tuple[Tensor, Tensor]:
+    _check_frames(frames, weight, bias, dfeat)
     B, T = frames.shape[:2]
     L = lib()
     scratch = torch.empty(int(L.f3_rgb_scratch_floats(B, T)), dtype=torch.float32, device=frames.device)

@@ -184,6 +184,11 @@ class TARGCN(nn.Module):
         check(lib().f3_targcn_backward(self._native.h, B, ptr(self._flat_params), ptr(self._flat_buffers),
                                        ptr(dout), ptr(grads), ptr(workspace), st), "targcn backward")
 
+    def device_status(self, wait=True):
+        """Raise if a GRU group barrier of the last forward / backward timed out (F3_EDEVICE: the
+        node-partitioned recurrences' outputs are then wrong); wait=False checks only a completed copy."""
+        check(lib().f3_targcn_status(self._native.h, 1 if wait else 0), "targcn device status")
+
     def forward(self, source):
         """One fall3::targcn_forward custom op (its autograd calls fall3::targcn_backward)."""
         source = source.detach().contiguous().float()
@@ -229,6 +234,8 @@ class TargcnStep:
         m.native_backward(self.N, self.dout, self.grads, self.ws, st)
 
     def __call__(self, source, label):
+        # a flagged barrier of an earlier step surfaces here (or from the native calls themselves)
+        self.model.device_status(wait=False)
         self.forward_backward(source, label)
         check(lib().f3_rmsprop_step(ptr(self.model.flat_parameters()), ptr(self.square_avg), ptr(self.grads),
                                     self.grads.numel(), self.lr, self.alpha, self.eps, 1.0, stream_handle()),

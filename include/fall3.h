@@ -30,13 +30,17 @@ extern "C" {
 #define F3_EBATCH 1002 /* train-mode batch of 1: BatchNorm needs >1 value per channel */
 #define F3_EHIP 1003   /* HIP launch error */
 #define F3_ESTATE 1004 /* backward without a training forward on this workspace */
+#define F3_EDEVICE 1005 /* a device-side check failed (TARGCN: a GRU group barrier timed out) */
 
 enum { F3_MODEL_TWO_STGCAN_BILSTM = 0, F3_MODEL_TWO_STGCAN = 1, F3_MODEL_STGCN = 2, F3_MODEL_BILSTM = 3 };
 enum { F3_SENSOR_NONE = 0, F3_SENSOR_BILSTM = 1, F3_SENSOR_CNN_BILSTM = 2 };
 enum { F3_NAMING_PACKAGE = 0, F3_NAMING_NOTEBOOK = 1 };
 enum { F3_PRECISION_FP32 = 0, /* exact fp32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
        F3_PRECISION_BF16 = 1, /* bf16 GEMM operands in HBM, fp32 accumulate (v_mfma_f32_16x16x32_bf16) */
-       F3_PRECISION_BF16_FP32IN = 2 /* kernel-level entries only: bf16 arithmetic on fp32 activations */ };
+       F3_PRECISION_BF16_FP32IN = 2, /* kernel-level entries only: bf16 arithmetic on fp32 activations */
+       F3_PRECISION_BF16X3 = 4 /* split-bf16 parity mode: fp32 activations, every GEMM operand split into
+                                  bf16 hi + lo, products hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_bf16
+                                  with fp32 accumulate (~2^-16 per product; gemm_x3.hip) */ };
 enum { F3_ENTRY_PARAM = 0, F3_ENTRY_BUFFER = 1, F3_ENTRY_COUNTER = 2 };
 
 typedef struct f3_config {
@@ -120,7 +124,8 @@ int f3_rmsprop_step(float* params, float* square_avg, const float* grads, int64_
  * (stgcan.py:24-31 tcn Conv2d). wpack is scratch of Cout*KT*Cin floats for the packed
  * operand; w == NULL reuses what a previous call packed there. precision = F3_PRECISION_*:
  * FP32 -> x/dy are fp32; BF16 -> x/dy are bf16 (the network's bf16 operand tensors);
- * BF16_FP32IN -> fp32 x/dy rounded to bf16 while staging. f3_conv_forward also takes
+ * BF16_FP32IN -> fp32 x/dy rounded to bf16 while staging; BF16X3 -> fp32 x/dy, split-bf16 products (wpack
+ * then holds the bf16 hi and lo planes of the packed weight). f3_conv_forward also takes
  * F3_CONV_BF16_OUT (bf16 x, out written as bf16 [N,T_out,V,Cout]: the step's tcn output type). */
 enum { F3_CONV_BF16_OUT = 3 };
 int f3_conv_forward(const void* x, const float* w, const float* bias, float* out, float* wpack, int N, int T_in,
@@ -216,6 +221,14 @@ int f3_targcn_backward(f3_targcn* net, int batch, const float* params, const flo
  * their stream; ms != NULL (after such a pair) waits for them and writes 8 durations in ms:
  * gru_fwd l0, gru_fwd l1, ta_fwd l0, ta_fwd l1, ta_bwd l1, ta_bwd l0, gru_bwd l1, gru_bwd l0. */
 int f3_targcn_stage_times(f3_targcn* net, int enable, float* ms);
+/* Device-side status of the node-partitioned GRU recurrences (no reference counterpart: the
+ * reference's GRU.py:17-27 loop has no inter-workgroup barrier). Each forward clears the barrier
+ * error flag; after its recurrences the forward and the backward copy it to a host status word.
+ * Returns F3_EDEVICE if a group barrier of the last forward / backward timed out (its outputs are
+ * then wrong), F3_OK otherwise. wait = 1 first waits for that copy; wait = 0 reports only a copy
+ * that has completed. Every f3_targcn_forward / _backward also returns F3_EDEVICE (and clears
+ * the word) when it finds a completed copy flagged by an earlier call. */
+int f3_targcn_status(f3_targcn* net, int wait);
 /* loss = -(1/N) sum_i sum_c y_ic log_softmax(out_i)_c (soft targets, not renormalised);
  * dout = dloss/dout. loss is overwritten. */
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream);

@@ -150,3 +150,31 @@ def test_targcn_training_tracks_oracle():
     err = float(np.abs(out - out_ref).max())
     print(f"TARGCN after {steps} steps: held-out max|dlogit| {err:.2e}")
     assert err < 1e-3 and (out.argmax(1) == out_ref.argmax(1)).all()
+
+
+def test_targcn_gru_barrier_timeout_is_reported(monkeypatch):
+    """The node-partitioned GRU recurrences (bf16) synchronise a clip group's V workgroups with a
+    bounded-spin barrier. A barrier that times out must surface as F3_EDEVICE, not as F3_OK with
+    wrong logits: F3_GN_SKIP_ARRIVE=1 makes workgroup 0 skip its arrivals, and the step must then
+    raise (from the native calls or from device_status). A clean step before and after reports OK
+    (the flag is cleared per forward)."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    V, B = 17, 64
+    st = tg.init_state(V, 11)
+    src, label = (torch.from_numpy(x).to(d) for x in tg.synthetic_source(B, V, 11, 5))
+    model = f3.TARGCN(num_nodes=V, device=d, precision="bf16")
+    model.load_state_dict(st)
+    step = f3.TargcnStep(model, B, lr=1e-5)
+    step.forward_backward(src, label)
+    model.device_status(wait=True)
+    monkeypatch.setenv("F3_GN_SKIP_ARRIVE", "1")
+    with pytest.raises(RuntimeError, match="barrier"):
+        step.forward_backward(src, label)
+        model.device_status(wait=True)
+    monkeypatch.delenv("F3_GN_SKIP_ARRIVE")
+    torch.cuda.synchronize()
+    model.device_status(wait=True)  # the flagged word was consumed by the raise
+    step.forward_backward(src, label)
+    model.device_status(wait=True)
+    assert np.isfinite(step.out.cpu().numpy()).all()

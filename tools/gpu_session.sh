@@ -4,7 +4,8 @@
 # step that faults, aborts or hits its limit (exit >= 124, 134, 139) ends it at once.
 #   tools/gpu_session.sh tests step_prof bench [pytest args for "tests" via PYTEST_ARGS]
 # Steps:
-#   tests       pytest -m gpu over ${TESTS:-tests} (+ PYTEST_ARGS)         -> gpurun_out/gpu_tests.log
+#   tests       pytest -m gpu over ${TESTS:-tests} (+ PYTEST_ARGS; PYTEST_K: a -k expression) -> gpurun_out/gpu_tests.log
+#   step_time   tools/step_only.py 10 for each precision in ${PRECS:-bf16}   -> gpurun_out/step_time.log
 #   step_prof   rocprofv3 kernel trace + stats of the bench step alone  -> gpurun_out/step_kernels.txt
 #   step_prof_ag  the same for the reference loop body through the custom ops -> gpurun_out/step_ag_*.txt
 #   step_prof_serial  the bench step with every queue joined (F3_SERIAL=1): per-kernel alone times
@@ -40,8 +41,13 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case $step in
     tests)
-      run tests 900 python -u -m pytest ${TESTS:-tests} -m gpu -q --timeout 300 --timeout-method thread \
-        ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+      if [ -n "${PYTEST_K:-}" ]; then
+        run tests 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -s --timeout 300 --timeout-method thread \
+          -k "$PYTEST_K" ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+      else
+        run tests 900 python -u -m pytest ${TESTS:-tests} -m gpu -q --timeout 300 --timeout-method thread \
+          ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+      fi
       tail -5 gpurun_out/gpu_tests.log ;;
     step_prof)
       run step_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step -o run -- \
@@ -50,6 +56,12 @@ for step in "$@"; do
         > gpurun_out/step_kernels.txt 2>&1
       python tools/timeline.py gpurun_out/step/run_results.db --list > gpurun_out/step_timeline.txt 2>&1
       head -25 gpurun_out/step_kernels.txt ;;
+    step_time)
+      for pr in ${PRECS:-bf16}; do
+        echo "precision $pr" >> gpurun_out/step_time.log
+        run "step_time[$pr]" 300 env F3_STEP_PREC=$pr python tools/step_only.py 10 >> gpurun_out/step_time.log 2>&1
+      done
+      cat gpurun_out/step_time.log ;;
     step_prof_ag)
       run step_prof_ag 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step_ag -o run -- \
         python tools/step_only.py 8 autograd > gpurun_out/step_prof_ag.log 2>&1
