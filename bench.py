@@ -486,12 +486,34 @@ def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0, precision="bf16"
     accumulate; "fp32": fp32 MFMA (the parity mode, also reported). The 10-fold CV shards folds over
     GPUs as independent replicas (no collective), so per-GPU throughput is the whole story."""
     import fall_multimodal_amd as f3
+    from fall_multimodal_amd.cv import folds_of_rank, kfold_indices
     from oracle import sktr_cpu as sk
-    x, lab = sk.synthetic_clips(B, 14, 11, 3)
+    # the rank's CV fold (cv.py: rank r runs folds r, r + world, ...; no collective): synthetic HAR-30
+    # windows in videos of 30, 10-fold split by video (cv_dataloader.py:155-167); the timed steps cycle
+    # through the fold's training windows, pre-gathered into resident B-clip batches
+    on = dist.is_available() and dist.is_initialized()
+    rank_, world_ = (dist.get_rank(), dist.get_world_size()) if on else (0, 1)
+    nwin = B * 12
+    x_all, lab_all = sk.synthetic_clips(nwin, 14, 11, 3)
+    folds = kfold_indices([f"v{i // 30:03d}" for i in range(nwin)], seed=42)
+    mine = folds_of_rank(len(folds), rank_ % len(folds), min(world_, len(folds)))
+    tr = folds[mine[0]][0]
+    perm = np.random.default_rng(mine[0]).permutation(tr)
+    nb = len(perm) // B
+    xb = [torch.from_numpy(x_all[perm[i * B:(i + 1) * B]]).to(dev) for i in range(nb)]
+    yb = [torch.from_numpy(lab_all[perm[i * B:(i + 1) * B]]).to(dev) for i in range(nb)]
+    x, lab = x_all[perm[:B]], lab_all[perm[:B]]
     model = f3.SkeletonTransformer(device=dev, precision=precision)
     step = f3.SktrStep(model, B)
-    xd, yd = torch.from_numpy(x).to(dev), torch.from_numpy(lab).to(dev)
-    dt, world = replica_seconds(lambda: step(xd, yd), steps, warmup)
+    xd, yd = xb[0], yb[0]
+    it = [0]
+
+    def fold_step():
+        i = it[0] % nb
+        it[0] += 1
+        step(xb[i], yb[i])
+
+    dt, world = replica_seconds(fold_step, steps, warmup)
     fp32_ms = None
     if precision != "fp32":  # the parity mode's step time beside it
         m32 = f3.SkeletonTransformer(device=dev)
@@ -503,7 +525,8 @@ def sktr_bench(dev, B=256, steps=10, warmup=3, cpu_seconds=0.0, precision="bf16"
            "ms_per_step": round(dt * 1e3, 3), "dtype": precision, "steps": steps,
            "config": {"workload": f"sktr_V14_T30_M1_B{B}", "global_batch": world * B, "joints": 14, "frames": 30,
                       "blocks": 6, "heads": 8,
-                      "parallelism": f"replicas{world} (10-fold CV, one fold per GPU)"},
+                      "parallelism": f"folds over ranks (world {world}, 10-fold CV by video, no collective)",
+                      "folds_rank0": mine, "fold_train_windows": int(len(tr)), "fold_batches": nb},
            "final_loss": round(float(step.loss.item()), 5), "fp32_mode_ms_per_step": fp32_ms}
     if cpu_seconds > 0:  # the oracle (pinned to the reference) on this host's cores
         threads = cpu_threads()
@@ -729,6 +752,36 @@ def rgb_bench(dev, B=256, T=30, reps=10):
     return out
 
 
+def rgb_step_bench(dev, a, V, S, C, sk, se, lb, steps=10, warmup=3):
+    """The north-star workload as ONE training step WITH the RGB branch (rgb.Fall3RGBStep): the
+    3-stream model (skeleton x2 + IMU, the headline's precision) plus the build-defined RGB
+    spatial-conv branch (B x 30 channels-last bf16 224x224x3 frames, resident in HBM), fused by adding
+    logits, one CE, both backwards, RMSprop over both parameter sets. The RGB branch runs on its own
+    HIP stream beside the skeleton / sensor queues. RGB parity is unpinned (no reference arithmetic)."""
+    import fall_multimodal_amd as f3
+    from fall_multimodal_amd.rgb import Fall3RGBStep, Fall3WithRGB
+    B = sk.shape[0]
+    frames = torch.empty(B, 30, 224, 224, 3, dtype=torch.bfloat16, device=dev).uniform_()
+    base = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": a.layout, "strategy": "spatial"}, C, S, device=dev,
+                                     precision=a.precision)
+    step = Fall3RGBStep(Fall3WithRGB(base, C, device=dev), B, lr=1e-3)
+    for _ in range(warmup):
+        step(sk, se, frames, lb)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(sk, se, frames, lb)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    res = {"workload": f"fall3_3stream_plus_rgb_{a.layout}_V{V}_S{S}_B{B}_T30_224x224x3", "dtype": a.precision,
+           "ms_per_step": round(dt * 1e3, 3), "clips_per_s": round(B / dt, 1), "steps": steps,
+           "final_loss": round(float(step.loss.item()), 5), "rgb_parity": "unpinned (build-defined branch)",
+           "note": "skeleton (2 ST-GCAN streams) + IMU BiLSTM + RGB conv branch as ONE step; RGB on its own stream"}
+    del step, base, frames
+    torch.cuda.empty_cache()
+    return res
+
+
 def model_leg(model, a):
     """One of the other BASELINE configs (cfg 2 TARGCN, cfg 5 SkeletonTransformer, musa_model) timed
     in a fresh child process (`bench.py --model M`, its own line embedded here): measured inside this
@@ -840,6 +893,8 @@ def main():
     mix = mix_roofline(dev, B, V, a.precision) if rank == 0 else None
     sens = sensor_bench(dev) if (rank == 0 and world == 1) else None
     rgbr = rgb_bench(dev) if (rank == 0 and world == 1 and not a.no_targcn) else None
+    if rgbr is not None:
+        rgbr["north_star_step_with_rgb"] = rgb_step_bench(dev, a, V, S, C, sk, se, lb)
     ldr = loader_bench(model, dev, B, V, S, C) if (rank == 0 and world == 1 and not a.no_targcn) else None
     if rank == 0:
         cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(a.layout, V, S, a.cpu_seconds)

@@ -43,6 +43,7 @@ struct MixArgs {
   unsigned short* zb;    // fwd: write z as bf16 (bf16 mode GEMM operand) instead of fp32
   const unsigned short* dzb;  // bwd: dZ in bf16 (instead of z) — LDS mix path only
   int no_colsum;         // bwd: leave the dA partial rows in `part` (caller reduces: f3_mix_bwd_parts)
+  int x3;                // bf16x3 mode: fp32 x / z / dz on the split-bf16 MFMA kernels (mix_*_x3)
 };
 constexpr int kMixParts = 1024;
 

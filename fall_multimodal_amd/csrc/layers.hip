@@ -823,6 +823,225 @@ __global__ __launch_bounds__(256) void mix_fwd_bf16_kernel(MixArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// Graph mix of the bf16x3 parity mode (F3_PRECISION_BF16X3: fp32 x / Z / dZ, gemm_x3.hip's split):
+// the bf16 kernels' structure with BOTH operands split, x = x_hi + x_lo (hi = RNE bf16, lo = RNE
+// bf16 of the rest) and A~ = hi + lo (a_split), each product as lo*hi + hi*lo + hi*hi on bf16
+// MFMA into one fp32 accumulator (~2^-16 per product). The frame's fp32 rows are prefetched into
+// registers one frame ahead and split while they are staged into two bf16 LDS planes (hi, lo) of
+// rows of 2C + 16 bytes. The forward writes fp32 Z straight from the accumulators (a lane's 4
+// consecutive channels: 16-B pieces); the backward as mix_bwd_bf16 (dX: A~ fragments in registers,
+// dZ by transposed LDS reads; dA: x and dZ by 16-B LDS reads; per-workgroup dA partial rows).
+// ----------------------------------------------------------------------------
+F3_DEV void split4_store(const f32x4 v, char* hi, char* lo) {
+  bf16x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  *reinterpret_cast<bf16x4*>(hi) = h;
+  *reinterpret_cast<bf16x4*>(lo) = l;
+}
+
+F3_DEV f32x4 mfma_x3m(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = mfma_bf16x(al, bh, c);
+  c = mfma_bf16x(ah, bl, c);
+  return mfma_bf16x(ah, bh, c);
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
+  constexpr int RB = 2 * CIN + 16, XR = 32, C4 = CIN / 4;
+  constexpr int PX = (18 * C4 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smb[];
+  char* xh = smb;             // [32][RB] hi plane
+  char* xl = smb + XR * RB;   // [32][RB] lo plane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  const int nx = V * C4;
+  bf16x8 bhi[4], blo[4];  // B operand: lane holds k = v = 8 fg + e, n = wk = 16 nt + fr
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 h, l;
+      a_split(atil(a.A, K, V, 16 * nt + fr, 8 * fg + e), h, l);
+      bhi[nt][e] = h;
+      blo[nt][e] = l;
+    }
+  for (int o = V * RB + tid * 16; o < XR * RB; o += 256 * 16) {
+    *reinterpret_cast<f32x4*>(xh + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(xl + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 rx[PX];
+  auto prefetch = [&](int f) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * CIN);
+#pragma unroll
+    for (int q = 0; q < PX; ++q) rx[q] = xg[min(tid + q * 256, nx - 1)];
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame's reads of the planes are done
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = tid + q * 256;
+      if (i < nx) {
+        const int o = (i / C4) * RB + (i % C4) * 8;
+        split4_store(rx[q], xh + o, xl + o);
+      }
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
+    float* zf = a.z + (size_t)f * KV * CIN;
+    for (int mt = wave; mt < CIN / 16; mt += 4) {
+      const int o = (8 * fg + (fr >> 2)) * RB + 32 * mt + 8 * (fr & 3);
+      const unsigned ph = (unsigned)(size_t)(mx_lds_t*)(xh + o), pl = (unsigned)(size_t)(mx_lds_t*)(xl + o);
+      mx_s16x4 h0, h1, l0, l1;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(h0) : "v"(ph));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(h1) : "v"(ph), "n"(4 * RB));
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l0) : "v"(pl));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(l1) : "v"(pl), "n"(4 * RB));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h0), "+v"(h1), "+v"(l0), "+v"(l1)::"memory");
+      const bf16x8 xah = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+      const bf16x8 xal = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int wk = 16 * nt + fr;
+        const f32x4 acc = mfma_x3m(xah, xal, bhi[nt], blo[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+        // lane holds Z[wk][c = 16 mt + 4 fg + r], r = 0..3: one 16-B piece of row wk
+        if (wk < KV) *reinterpret_cast<f32x4*>(zf + (size_t)wk * CIN + 16 * mt + 4 * fg) = acc;
+      }
+    }
+  }
+}
+
+template <int CIN, bool ACC>
+__global__ __launch_bounds__(256) void mix_bwd_x3_kernel(MixArgs a) {
+  constexpr int RB = 2 * CIN + 16, XR = 32, ZR = 64, C4 = CIN / 4;
+  constexpr int PX = (18 * C4 + 255) / 256, PZ = (54 * C4 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smb[];
+  char* xh = smb;                    // [32][RB]
+  char* xl = xh + XR * RB;           // [32][RB]
+  char* zh = xl + XR * RB;           // [64][RB]
+  char* zl = zh + ZR * RB;           // [64][RB]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int K = a.K, V = a.V, KV = K * V;
+  const int nx = V * C4, nz = KV * C4;
+  bf16x8 ahi[2][2], alo[2][2];  // A~ as the dX A operand: rows v = 16 mt + fr, k = wk = 32 ks + 8 fg + e
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 h, l;
+        a_split(atil(a.A, K, V, 32 * ks + 8 * fg + e, 16 * mt + fr), h, l);
+        ahi[mt][ks][e] = h;
+        alo[mt][ks][e] = l;
+      }
+  for (int o = KV * RB + tid * 16; o < ZR * RB; o += 256 * 16) {
+    *reinterpret_cast<f32x4*>(zh + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(zl + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  f32x4 rx[PX], rz[PZ];
+  auto prefetch = [&](int f) {
+    const f32x4* xg = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * CIN);
+    const f32x4* zg = reinterpret_cast<const f32x4*>(a.z + (size_t)f * KV * CIN);
+#pragma unroll
+    for (int q = 0; q < PX; ++q) rx[q] = xg[min(tid + q * 256, nx - 1)];
+#pragma unroll
+    for (int q = 0; q < PZ; ++q) rz[q] = zg[min(tid + q * 256, nz - 1)];
+  };
+  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
+  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
+    __syncthreads();  // the previous frame's reads of the planes are done
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+      const int i = tid + q * 256;
+      if (i < nx) {
+        const int o = (i / C4) * RB + (i % C4) * 8;
+        split4_store(rx[q], xh + o, xl + o);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PZ; ++q) {
+      const int i = tid + q * 256;
+      if (i < nz) {
+        const int o = (i / C4) * RB + (i % C4) * 8;
+        split4_store(rz[q], zh + o, zl + o);
+      }
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
+    // dX_f[v][c] = sum_wk A~[v][wk] dZ_f[wk][c]
+    float* dxf = a.dx + (size_t)f * V * CIN;
+    for (int nt = wave; nt < CIN / 16; nt += 4) {
+      bf16x8 bh[2], bl[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int o = (32 * ks + 8 * fg + (fr >> 2)) * RB + 32 * nt + 8 * (fr & 3);
+        const unsigned ph = (unsigned)(size_t)(mx_lds_t*)(zh + o), pl = (unsigned)(size_t)(mx_lds_t*)(zl + o);
+        mx_s16x4 h0, h1, l0, l1;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(h0) : "v"(ph));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(h1) : "v"(ph), "n"(4 * RB));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l0) : "v"(pl));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(l1) : "v"(pl), "n"(4 * RB));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h0), "+v"(h1), "+v"(l0), "+v"(l1)::"memory");
+        bh[ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+        bl[ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[mt] = mfma_x3m(ahi[mt][ks], alo[mt][ks], bh[ks], bl[ks], acc[mt]);
+      float old[2][4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = min(16 * mt + 4 * fg + r, V - 1);
+          old[mt][r] = ACC ? dxf[(size_t)v * CIN + 16 * nt + fr] : 0.f;
+        }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = 16 * mt + 4 * fg + r;
+          if (v < V) dxf[(size_t)v * CIN + 16 * nt + fr] = acc[mt][r] + old[mt][r];
+        }
+    }
+    // dA[v][wk] += sum_c X_f[v][c] dZ_f[wk][c]: this wave's wk tile, both v tiles
+#pragma unroll 2
+    for (int ks = 0; ks < CIN / 32; ++ks) {
+      const int cb = (32 * ks + 8 * fg) * 2;
+      const bf16x8 z_h = *reinterpret_cast<const bf16x8*>(zh + (16 * wave + fr) * RB + cb);
+      const bf16x8 z_l = *reinterpret_cast<const bf16x8*>(zl + (16 * wave + fr) * RB + cb);
+      const bf16x8 x0h = *reinterpret_cast<const bf16x8*>(xh + fr * RB + cb);
+      const bf16x8 x0l = *reinterpret_cast<const bf16x8*>(xl + fr * RB + cb);
+      const bf16x8 x1h = *reinterpret_cast<const bf16x8*>(xh + (16 + fr) * RB + cb);
+      const bf16x8 x1l = *reinterpret_cast<const bf16x8*>(xl + (16 + fr) * RB + cb);
+      dacc[0] = mfma_x3m(x0h, x0l, z_h, z_l, dacc[0]);
+      dacc[1] = mfma_x3m(x1h, x1l, z_h, z_l, dacc[1]);
+    }
+  }
+  float* row = a.part + (size_t)blockIdx.x * K * V * V;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = 16 * mt + 4 * fg + r, wk = 16 * wave + fr;
+      if (v < V && wk < KV) {
+        const int w = wk / K, k = wk - w * K;
+        row[(k * V + v) * V + w] = dacc[mt][r];
+      }
+    }
+}
+
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
 // dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
 __global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
@@ -1698,7 +1917,59 @@ static int launch_mix_fwd_bf16(const MixArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
+// bf16x3 mode: grid = one round of resident workgroups (occupancy at the kernel's LDS)
+template <class KERN>
+static int resident_slots(KERN k, size_t lds) {
+  int per_cu = 0, dev = 0, cus = 256;
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetLastError();
+  return per_cu * cus;
+}
+template <int CIN>
+static size_t mix_x3_lds_fwd() { return (size_t)64 * (2 * CIN + 16); }
+template <int CIN>
+static size_t mix_x3_lds_bwd() { return (size_t)192 * (2 * CIN + 16); }
+template <int CIN>
+static int launch_mix_fwd_x3(const MixArgs* a, hipStream_t s) {
+  static const int slots = resident_slots(mix_fwd_x3_kernel<CIN>, mix_x3_lds_fwd<CIN>());
+  const int grid = std::max(1, std::min(a->frames, slots));
+  hipLaunchKernelGGL(mix_fwd_x3_kernel<CIN>, dim3(grid), dim3(256), mix_x3_lds_fwd<CIN>(), s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+template <int CIN>
+static int mix_bwd_x3_grid(const MixArgs* a) {
+  static const int slots = [] {
+    (void)resident_slots(mix_bwd_x3_kernel<CIN, false>, mix_x3_lds_bwd<CIN>());
+    return resident_slots(mix_bwd_x3_kernel<CIN, true>, mix_x3_lds_bwd<CIN>());
+  }();
+  return std::max(1, std::min(std::min(a->frames, 768), slots));
+}
+template <int CIN>
+static int launch_mix_bwd_x3(const MixArgs* a, hipStream_t s) {
+  const int grid = mix_bwd_x3_grid<CIN>(a);
+  if (a->accumulate)
+    hipLaunchKernelGGL((mix_bwd_x3_kernel<CIN, true>), dim3(grid), dim3(256), mix_x3_lds_bwd<CIN>(), s, *a);
+  else
+    hipLaunchKernelGGL((mix_bwd_x3_kernel<CIN, false>), dim3(grid), dim3(256), mix_x3_lds_bwd<CIN>(), s, *a);
+  F3_LAUNCH_CHECK();
+  if (a->no_colsum) return F3_OK;
+  return f3_colsum(a->part, grid, a->K * a->V * a->V, a->dA, s);
+}
+static bool mix_x3_ok(const MixArgs& a) {
+  return a.x3 && !a.x16 && !a.zb && !a.dzb && (a.Cin == 64 || a.Cin == 128 || a.Cin == 256) && a.K * a.V <= 64 &&
+         a.V <= 32;
+}
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
+  if (a->x3 && mix_x3_ok(*a)) {  // (the first block's Cin = 2 / 3 mix stays on the fp32 kernels)
+    if (a->frames <= 0) return F3_OK;
+    return a->Cin == 64 ? launch_mix_fwd_x3<64>(a, s) : a->Cin == 128 ? launch_mix_fwd_x3<128>(a, s)
+                                                         : launch_mix_fwd_x3<256>(a, s);
+  }
   static const bool fwd_bf16 = !getenv("F3_MIX_FWD_BF16") || atoi(getenv("F3_MIX_FWD_BF16")) != 0;
   if (fwd_bf16 && mix_lds_ok(*a) && a->x16 && a->zb && a->K * a->V <= 64 && a->V <= 32) {
     if (a->frames <= 0) return F3_OK;
@@ -1796,6 +2067,8 @@ static int mix_bwd_cin(const MixArgs* a, hipStream_t s) {
 }
 
 int f3_mix_bwd_parts(const MixArgs* a) {  // rows of `part` the launch leaves (no_colsum callers sum them)
+  if (a->x3 && mix_x3_ok(*a))
+    return a->Cin == 64 ? mix_bwd_x3_grid<64>(a) : a->Cin == 128 ? mix_bwd_x3_grid<128>(a) : mix_bwd_x3_grid<256>(a);
   if (!mix_lds_ok(*a)) return 0;
   if (a->dzb && mix_bwd_bf16_on() && a->K * a->V <= 64 && a->V <= 32)
     return a->Cin == 64 ? mix_bwd_bf16_grid<64>(a) : a->Cin == 128 ? mix_bwd_bf16_grid<128>(a) : mix_bwd_bf16_grid<256>(a);
@@ -1803,6 +2076,12 @@ int f3_mix_bwd_parts(const MixArgs* a) {  // rows of `part` the launch leaves (n
 }
 
 int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
+  if (a->x3 && mix_x3_ok(*a)) {
+    if (!a->part) return F3_EINVAL;
+    if (a->frames <= 0) return F3_OK;
+    return a->Cin == 64 ? launch_mix_bwd_x3<64>(a, s) : a->Cin == 128 ? launch_mix_bwd_x3<128>(a, s)
+                                                         : launch_mix_bwd_x3<256>(a, s);
+  }
   if (mix_lds_ok(*a)) {
     if (!a->part) return F3_EINVAL;
     const int r = a->Cin == 64 ? mix_bwd_cin<64>(a, s) : a->Cin == 128 ? mix_bwd_cin<128>(a, s) : mix_bwd_cin<256>(a, s);

@@ -66,6 +66,9 @@ struct QuadLayout {
 // block size) from a kernel argument: a loop, a __syncthreads fence or a blockDim read (a vector
 // load from the dispatch packet) ahead of the lane adds made hipcc wait vmcnt(0) for the
 // workgroup's row stores first (7 us of a 27 us conv launch). Needs C <= 256 and nb >= C.
+// STORE: the workgroup owns lane row blockIdx.x (grid <= kLanes) and writes its partial row with
+// plain stores instead of memory-side adds (the depthwise conv's F3_DW_STORE form)
+template <bool STORE = false>
 F3_DEV void channel_flush(int C, int q, bool act, const float (&s1)[4], const float (&s2)[4], float* lanes, int nb) {
   __shared__ float r[512];
   const int t = threadIdx.x, n2 = 2 * C;
@@ -89,7 +92,10 @@ F3_DEV void channel_flush(int C, int q, bool act, const float (&s1)[4], const fl
   for (int i = 0; i < 8; ++i) v[i] = t + 64 * i < n2 ? r[t + 64 * i] : 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
-    if (t + 64 * i < n2) atomicAdd(l + t + 64 * i, v[i]);
+    if (t + 64 * i < n2) {
+      if constexpr (STORE) l[t + 64 * i] = v[i];
+      else atomicAdd(l + t + 64 * i, v[i]);
+    }
 }
 F3_DEV void channel_flush(int C, const QuadLayout& L, const float (&s1)[4], const float (&s2)[4], float* lanes) {
   channel_flush(C, L.q, L.act, s1, s2, lanes, 256);  // QuadLayout kernels run 256 threads
@@ -141,7 +147,7 @@ F3_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 // that is a multiple of the quad count, so a thread's BN partial sums stay per channel quad.
 constexpr int kDwChunk = 8;
 
-template <int K, int S>
+template <int K, int S, bool STORE>
 __global__ __launch_bounds__(512) void mu_dwconv_fwd_kernel(DwConvArgs a) {
   const int nq = a.C >> 2;
   const int nchunk = (a.T_out + kDwChunk - 1) / kDwChunk;
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(512) void mu_dwconv_fwd_kernel(DwConvArgs a) {
     }
   }
   if (a.sum) {
-    channel_flush(a.C, q, g0 < total, s1, s2, a.lanes, a.block);
+    channel_flush<STORE>(a.C, q, g0 < total, s1, s2, a.lanes, a.block);
   }
 }
 
@@ -866,18 +872,23 @@ int f3_mu_dwconv_fwd(const DwConvArgs* a, hipStream_t s) {
   // costs ~2.3 ns per wave of the grid at the launch's end (1024 x 256 threads: 28.3 vs 18.8 us
   // without sums; 512 x 256: 24.9 vs 19.9; 512-thread blocks or one wave issuing the lane adds:
   // the same), so 512 workgroups of 256 threads
+  // F3_DW_STORE=1: at most kLanes workgroups, each storing its BN partial row into its own lane
+  // row (plain stores; the finalize adds the rows) instead of memory-side adds (A/B, round 4)
+  static const int store = getenv("F3_DW_STORE") ? atoi(getenv("F3_DW_STORE")) : 0;
   static const int cap = getenv("F3_DW_GRID") ? std::max(64, atoi(getenv("F3_DW_GRID"))) : 512;
-  const int grid = (int)std::min<long long>(want, cap);
+  const bool st_rows = store && a->sum;
+  const int grid = (int)std::min<long long>(want, st_rows ? std::min(cap, kLanes) : cap);
   DwConvArgs b = *a;
   b.grid = grid;
   b.block = block;
   a = &b;
-  if (a->K == 1 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<1, 1>), dim3(grid), dim3(block), 0, s, *a);
-  else if (a->K == 3 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<3, 1>), dim3(grid), dim3(block), 0, s, *a);
-  else if (a->K == 5 && a->S == 1) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<5, 1>), dim3(grid), dim3(block), 0, s, *a);
-  else if (a->K == 3 && a->S == 2) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<3, 2>), dim3(grid), dim3(block), 0, s, *a);
-  else if (a->K == 5 && a->S == 2) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<5, 2>), dim3(grid), dim3(block), 0, s, *a);
-  else return F3_EINVAL;
+#define MU_DWF(K_, S_)                                                                                   \
+  if (a->K == K_ && a->S == S_) {                                                                        \
+    if (st_rows) hipLaunchKernelGGL((mu_dwconv_fwd_kernel<K_, S_, true>), dim3(grid), dim3(block), 0, s, *a); \
+    else hipLaunchKernelGGL((mu_dwconv_fwd_kernel<K_, S_, false>), dim3(grid), dim3(block), 0, s, *a);      \
+  } else
+  MU_DWF(1, 1) MU_DWF(3, 1) MU_DWF(5, 1) MU_DWF(3, 2) MU_DWF(5, 2) return F3_EINVAL;
+#undef MU_DWF
   F3_LAUNCH_CHECK();
   if (a->sum) return lane_finalize(a->lanes, a->C, a->sum, a->sumsq, s);
   return F3_OK;

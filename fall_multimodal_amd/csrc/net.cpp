@@ -610,7 +610,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       MixArgs mx;
       std::memset(&mx, 0, sizeof(mx));
       mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
-      mx.zb = bfa(X.z, hb); mx.x16 = hb;
+      mx.zb = bfa(X.z, hb); mx.x16 = hb; mx.x3 = x3;
       F3_TRY(f3_mix_fwd(&mx, s));
       ConvGemmArgs ga;
       std::memset(&ga, 0, sizeof(ga));
@@ -798,7 +798,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&mx, 0, sizeof(mx));
     mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = W.dZ;
     mx.dx = dx; mx.dA = X.dAeff; mx.accumulate = L.res == RES_ID; mx.part = X.mixpart; mx.x16 = hb;
-    mx.no_colsum = split;
+    mx.no_colsum = split; mx.x3 = x3;
     mx.dzb = dzb ? bfa(W.dZ, 1) : nullptr;
     if (part & 1) F3_TRY(g0 ? f3_gcn0_bwd(&b0, s) : f3_mix_bwd(&mx, s));
     if (L.res == RES_CONV) {
@@ -1543,11 +1543,11 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
 
 int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int frames, int K, int V, int Cin, int flags,
                             void* stream) {
-  if (!A_eff || !x || !z || frames < 0 || (flags & ~3)) return F3_EINVAL;
+  if (!A_eff || !x || !z || frames < 0 || (flags & ~7) || ((flags & F3_MIX_X3) && (flags & 3))) return F3_EINVAL;
   MixArgs m;
   std::memset(&m, 0, sizeof(m));
   m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff;
-  m.x = static_cast<const float*>(x); m.x16 = flags & F3_MIX_X_BF16;
+  m.x = static_cast<const float*>(x); m.x16 = flags & F3_MIX_X_BF16; m.x3 = (flags & F3_MIX_X3) != 0;
   m.z = static_cast<float*>(z);
   if (flags & F3_MIX_Z_BF16) m.zb = static_cast<unsigned short*>(z);
   return f3_mix_fwd(&m, (hipStream_t)stream);
@@ -1555,13 +1555,14 @@ int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int fram
 
 int f3_graph_mix_backward_ex(const float* A_eff, const void* x, const void* dz, float* dx, float* dA, int frames, int K,
                              int V, int Cin, int flags, void* stream) {
-  if (!A_eff || !x || !dz || !dx || !dA || frames < 0 || (flags & ~1)) return F3_EINVAL;
+  if (!A_eff || !x || !dz || !dx || !dA || frames < 0 || (flags & ~5) || ((flags & F3_MIX_X3) && (flags & 1)))
+    return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(dA, 0, sizeof(float) * K * V * V, s) != hipSuccess) return F3_EHIP;
   MixArgs m;
   std::memset(&m, 0, sizeof(m));
   m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff; m.x = static_cast<const float*>(x);
-  m.dx = dx; m.dA = dA; m.accumulate = 0;
+  m.dx = dx; m.dA = dA; m.accumulate = 0; m.x3 = (flags & F3_MIX_X3) != 0;
   if (flags & F3_MIX_X_BF16) {
     m.x16 = 1;
     m.dzb = static_cast<const unsigned short*>(dz);

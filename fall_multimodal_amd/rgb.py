@@ -6,6 +6,8 @@ model arithmetic, so this branch's parity is unpinned; SURVEY.md section 8a row 
                      frames and the 28x28 patches -> feat [B, 64]   (HIP: csrc/rgb.hip)
     RGBBranch        RGBSpatialConv + Linear(64, num_class): the branch's late-fusion logits
     Fall3WithRGB     the reference 3-stream model plus the RGB branch, fused by adding logits
+    Fall3RGBStep     the north-star workload as ONE fused training step (skeleton + IMU + RGB): the
+                     RGB branch on its own HIP stream, concurrent with the skeleton / sensor queues
 
 Frames are channels-last bf16 [B, T, 224, 224, 3]. The conv runs as `fall3::rgb_forward` /
 `fall3::rgb_backward` custom ops (no input gradient: the frames are data)."""
@@ -125,3 +127,87 @@ class Fall3WithRGB(nn.Module):
 
     def forward(self, skel: Tensor, sensor: Optional[Tensor], frames: Tensor) -> Tensor:
         return self.fall3(skel, sensor) + self.rgb(frames)
+
+
+class Fall3RGBStep:
+    """North-star training step with the RGB branch (BASELINE.json: "B=256, T=30, J=17 skeleton +
+    6-axis IMU + 224^2 RGB" as ONE step): logits = fall3(skel, sensor) + fc(rgb_conv(frames)), soft-target
+    CE, backward of both branches, RMSprop over both parameter sets (torch.optim.RMSprop semantics).
+
+    Queues: the fall3 model runs exactly as TrainStep runs it (the caller's stream plus its private
+    branch queues); the RGB forward (conv, fc), and after the loss its backward (fc gradients, dfeat,
+    conv backward), run on one extra HIP stream, so the frames' two HBM passes overlap the skeleton
+    streams. The RGB parameters are views into one flat buffer (16-B aligned entries) so the update is
+    one f3_rmsprop_step launch, like the fall3 flat range. The reference has no RGB model arithmetic:
+    this branch's parity is unpinned (oracle/rgb_cpu.py restates the build's definition)."""
+
+    def __init__(self, model: Fall3WithRGB, batch, lr=1e-3, alpha=0.99, eps=1e-8, optimizer=None):
+        from .train import TrainStep
+        self.model, self.N = model, batch
+        self.inner = TrainStep(model.fall3, batch, lr=lr, alpha=alpha, eps=eps, optimizer=optimizer)
+        dev = model.fall3.flat_parameters().device
+        params = [model.rgb.conv.weight, model.rgb.conv.bias, model.rgb.fc.weight, model.rgb.fc.bias]
+        offs, off = [], 0
+        for p in params:
+            offs.append(off)
+            off += (p.numel() + 3) // 4 * 4
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros_like(self.flat)
+        self.square_avg = torch.zeros_like(self.flat)
+        with torch.no_grad():
+            for p, o in zip(params, offs):
+                v = self.flat[o:o + p.numel()].view(p.shape)
+                v.copy_(p.detach())
+                p.data = v
+                p.grad = self.grads[o:o + p.numel()].view(p.shape)
+        self.params = params
+        C = model.fall3.spec.num_class
+        self.feat = torch.empty(batch, 64, dtype=torch.float32, device=dev)
+        self.rlog = torch.empty(batch, C, dtype=torch.float32, device=dev)
+        self.total = torch.empty(batch, C, dtype=torch.float32, device=dev)
+        self.stream = torch.cuda.Stream(device=dev)
+
+    @property
+    def loss(self):
+        return self.inner.loss
+
+    @property
+    def out(self):
+        return self.total
+
+    def __call__(self, skel, sensor, frames, label):
+        inner, m = self.inner, self.model.fall3
+        label = inner.prepare(skel, sensor, label)
+        _check_frames(frames, self.params[0], self.params[1])
+        if frames.shape[0] != self.N:
+            raise ValueError(f"Fall3RGBStep was built for batch {self.N}, got frames with batch {frames.shape[0]}")
+        cw, cb, fw, fb = self.params
+        cur = torch.cuda.current_stream()
+        s = self.stream
+        s.wait_stream(cur)  # frames and the previous step's parameter update
+        with torch.cuda.stream(s):
+            self.feat.copy_(torch.ops.fall3.rgb_forward(frames, cw.detach(), cb.detach()))
+            torch.addmm(fb.detach(), self.feat, fw.detach().t(), out=self.rlog)
+        st = stream_handle()
+        m.native_forward(skel, sensor, inner.out, inner.ws, True, st)
+        cur.wait_stream(s)
+        torch.add(inner.out, self.rlog, out=self.total)
+        check(lib().f3_net_loss(m._native.h, self.N, ptr(self.total), ptr(label), ptr(inner.loss), ptr(inner.dout),
+                                st), "fall3 loss")
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            dout = inner.dout
+            torch.mm(dout.t(), self.feat, out=fw.grad)
+            torch.sum(dout, 0, out=fb.grad)
+            dfeat = dout @ fw.detach()
+            dw, db = torch.ops.fall3.rgb_backward(frames, cw.detach(), cb.detach(), dfeat)
+            cw.grad.copy_(dw)
+            cb.grad.copy_(db)
+        inner.backward_phase(0)
+        cur.wait_stream(s)
+        inner.optimizer_step()
+        check(lib().f3_rmsprop_step(ptr(self.flat), ptr(self.square_avg), ptr(self.grads), self.grads.numel(),
+                                    inner.lr, inner.alpha, inner.eps, 1.0, stream_handle()), "rgb rmsprop")
+        for t in (frames, dout, dfeat):
+            t.record_stream(s)
+        return inner.loss

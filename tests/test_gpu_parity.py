@@ -240,6 +240,35 @@ def _mix_bwd_bf16_check(V, K, Cin, F, d=None):
         np.testing.assert_allclose(got.cpu().double().numpy(), r, rtol=0, atol=rel * np.abs(r).max())
 
 
+@pytest.mark.parametrize("V,K,Cin,F", [(18, 3, 64, 300), (14, 3, 128, 77), (18, 3, 256, 41), (17, 1, 64, 5),
+                                        (18, 3, 64, 7680)])
+def test_graph_mix_bf16x3_kernels(V, K, Cin, F):
+    """The bf16x3 mode's mix forward and backward (fp32 x / z / dz; both operands split into bf16 hi +
+    lo, three MFMA products each) against fp64 on the fp32 operands: z, dx, dA within X3_TOL of
+    their max (each product carries ~2^-16)."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    torch.manual_seed(V * 11 + Cin + F)
+    A = (torch.rand(K, V, V, dtype=torch.float64) / V).float().double().requires_grad_(True)
+    x = torch.randn(F, V, Cin, dtype=torch.float64).float().double().requires_grad_(True)
+    z = torch.einsum("kvw,fvc->fwkc", A, x)
+    dz = torch.randn_like(z).float().double()
+    z.backward(dz)
+    Ag, xg, dzg = (t.detach().float().contiguous().to(d) for t in (A, x, dz))
+    zo = torch.empty(F, V, K, Cin, device=d)
+    dx = torch.empty(F, V, Cin, device=d)
+    dA = torch.empty(K, V, V, device=d)
+    L.check(L.lib().f3_graph_mix_forward_ex(L.ptr(Ag), L.ptr(xg), L.ptr(zo), F, K, V, Cin, 4, L.stream_handle()), "mix")
+    L.check(L.lib().f3_graph_mix_backward_ex(L.ptr(Ag), L.ptr(xg), L.ptr(dzg), L.ptr(dx), L.ptr(dA), F, K, V, Cin, 4,
+                                             L.stream_handle()), "mixbwd")
+    errs = {}
+    for name, got, ref in (("z", zo, z.detach()), ("dx", dx, x.grad), ("dA", dA, A.grad)):
+        r = ref.numpy()
+        errs[name] = float(np.abs(got.cpu().double().numpy() - r).max() / np.abs(r).max())
+        np.testing.assert_allclose(got.cpu().double().numpy(), r, rtol=0, atol=X3_TOL * np.abs(r).max())
+    print(f"bf16x3 mix V={V} K={K} Cin={Cin} F={F}: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+
+
 @pytest.mark.parametrize("tag", TAGS)
 def test_train_step_matches_reference_golden(tag):
     """fp32 path vs the reference's own outputs (golden, B=4):

@@ -185,3 +185,17 @@ def test_sktr_training_tracks_oracle():
     err = float(np.abs(out - out_ref).max())
     print(f"sktr after {steps} steps: held-out max|dlogit| {err:.2e}")
     assert err < 1e-3 and (out.argmax(1) == out_ref.argmax(1)).all()
+
+
+def test_cv_fold_fn_trains_and_evaluates_a_fold():
+    """cv.sktr_fold_fn (BASELINE cfg 5's fold body, main_cross_validation.py:256-361): a fresh model per
+    fold trains on the fold's windows and reports held-out metrics; two folds of a small synthetic set."""
+    d = dev()
+    from fall_multimodal_amd.cv import kfold_indices, sktr_fold_fn
+    x, lab = sk.synthetic_clips(200, 14, 11, 5)
+    folds = kfold_indices([f"v{i // 10:02d}" for i in range(200)], seed=42)
+    fn = sktr_fold_fn(torch.from_numpy(x).to(d), torch.from_numpy(lab).to(d), epochs=2, batch=16, precision="bf16")
+    for k in (0, 1):
+        r = fn(k, *folds[k])
+        assert r["held_out"] == len(folds[k][1]) and r["train_steps"] == 2 * (len(folds[k][0]) // 16)
+        assert 0.0 <= r["accuracy"] <= 1.0 and 0.0 <= r["f1"] <= 1.0
