@@ -5,8 +5,10 @@ RMSprop, + gradient all-reduce for N > 1) on MI355X, one process per GPU.
 Workload (BASELINE.json north star / configs[3] per GPU): synthetic clips with B=256 per
 GPU, T=30 frames, J=17 COCO joints + centre node (coco_mmpose, V=18), 3-channel skeleton
 + 6-axis IMU at the frame rate (Ts=30), 11 classes; random-init weights of the reference
-architecture (TwoStreamSTGCAN_BiLSTM, combination.py:27-46). The reference has no RGB
-branch, so none is built or timed.
+architecture (TwoStreamSTGCAN_BiLSTM, combination.py:27-46). The reference has no RGB model
+arithmetic; the build-defined RGB spatial-conv branch is timed beside the headline
+(`rgb_branch`: its kernels alone, and the whole north-star step WITH it, skeleton + IMU + RGB as
+one step), its parity unpinned.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N

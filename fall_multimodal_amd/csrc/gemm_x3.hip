@@ -80,7 +80,13 @@ F3_DEV s16x4 tr_read(const __bf16* p) {
 
 }  // namespace
 
-template <int PRO, int EPI, int WM, int WN>
+// rows of the input tensor of a conv geometry (N * T_in * V); the lo plane of a pre-split operand
+// starts this many rows (x lda) after the hi plane
+F3_DEV size_t in_rows(const ConvGeom& g) { return (size_t)(g.M / (g.T_out * g.V)) * g.T_in * g.V; }
+
+// AS: the activation operand arrives pre-split (a.inb = hi plane, lo plane in_rows * lda later;
+// e.g. u = relu(bn1(g)) split once by bnrelu_x3 instead of once per tap here); no prologue
+template <int PRO, int EPI, int WM, int WN, bool AS>
 __global__ __launch_bounds__(256) void conv_gemm_x3(ConvGemmArgs a) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int AIT = BM * 4 / 256;  // (row, k octet) items of the A tile per thread
@@ -137,12 +143,23 @@ __global__ __launch_bounds__(256) void conv_gemm_x3(ConvGemmArgs a) {
     }
   }
   float ra[AIT][8];
+  uint4 rah[AIT], ral[AIT];
   uint4 rbh[BIT], rbl[BIT];
+  const unsigned short* ah_plane = a.inb;
+  const unsigned short* al_plane = AS ? a.inb + in_rows(g) * g.lda : nullptr;
   auto load_chunk = [&](int c) {
 #pragma unroll
     for (int q = 0; q < AIT; ++q) {
       const int k0 = c * XBK + aoct[q] * 8;
-      if (fastA) {
+      if constexpr (AS) {  // launcher guarantees Kc % 8 == 0 and lda % 8 == 0
+        const int dt = k0 / g.Kc, i = k0 - dt * g.Kc;
+        const int r = (aok[q] && k0 < Ktot) ? src_row_x(an[q], at[q], av[q], dt, g) : -1;
+        const size_t o = (size_t)max(r, 0) * g.lda + i;
+        const uint4 h = *reinterpret_cast<const uint4*>(ah_plane + o), l = *reinterpret_cast<const uint4*>(al_plane + o);
+        const uint4 z = {0u, 0u, 0u, 0u};
+        rah[q] = r >= 0 ? h : z;
+        ral[q] = r >= 0 ? l : z;
+      } else if (fastA) {
         const int dt = k0 / g.Kc, i = k0 - dt * g.Kc;
         const int r = (aok[q] && k0 < Ktot) ? src_row_x(an[q], at[q], av[q], dt, g) : -1;
         if (r >= 0) {
@@ -202,10 +219,15 @@ __global__ __launch_bounds__(256) void conv_gemm_x3(ConvGemmArgs a) {
   auto store_chunk = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < AIT; ++q) {
-      bf16x8 hi, lo;
-      split8(ra[q], hi, lo);
-      *reinterpret_cast<bf16x8*>(&As[buf][xoff(arow[q], aoct[q])]) = hi;
-      *reinterpret_cast<bf16x8*>(&As[buf][xoff(arow[q], 4 + aoct[q])]) = lo;
+      if constexpr (AS) {
+        *reinterpret_cast<uint4*>(&As[buf][xoff(arow[q], aoct[q])]) = rah[q];
+        *reinterpret_cast<uint4*>(&As[buf][xoff(arow[q], 4 + aoct[q])]) = ral[q];
+      } else {
+        bf16x8 hi, lo;
+        split8(ra[q], hi, lo);
+        *reinterpret_cast<bf16x8*>(&As[buf][xoff(arow[q], aoct[q])]) = hi;
+        *reinterpret_cast<bf16x8*>(&As[buf][xoff(arow[q], 4 + aoct[q])]) = lo;
+      }
     }
 #pragma unroll
     for (int q = 0; q < BIT; ++q) {
@@ -334,7 +356,9 @@ __global__ __launch_bounds__(256) void conv_gemm_x3(ConvGemmArgs a) {
 }
 
 // dW[j][i'] = sum_m dY[m][j] * pro(In[src(m,dt)][i]); split over rows, f32 atomics.
-template <int PRO, int WM, int WN>
+// XS: the input rows arrive pre-split (a.inb hi plane, lo plane in_rows * lda later); no prologue
+// YS: dY arrives pre-split (a.dyb hi plane, lo plane M * ldy later)
+template <int PRO, int WM, int WN, bool XS, bool YS>
 __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
   WgradArgs a = a_;
   const int nsplit = (a.g.M + a.rows_per_split - 1) / a.rows_per_split;
@@ -368,6 +392,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
   const bool fastY = (a.ldy % 4) == 0 && (g.Nc % 4) == 0;
   const bool fastX = (g.lda % 4) == 0 && (g.Kc % 4) == 0;
   float ry[VPY], rx[VPX], dbp[VPY];
+  uint4 rxh[VPX / 8], rxl[VPX / 8], ryh[VPY / 8], ryl[VPY / 8];
+  const unsigned short* yh_plane = a.dyb;
+  const unsigned short* yl_plane = YS ? a.dyb + (size_t)g.M * a.ldy : nullptr;
+  const unsigned short* xh_plane = a.inb;
+  const unsigned short* xl_plane = XS ? a.inb + in_rows(g) * g.lda : nullptr;
 #pragma unroll
   for (int e = 0; e < VPY; ++e) dbp[e] = 0.f;
   const bool do_db = a.db && blockIdx.y == 0;
@@ -375,7 +404,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
     const int m = r0 + lrow;
     const bool ok = m < r_end;
     const int j = j0 + cy;
-    if (ok && fastY && j + VPY <= g.Nc) {
+    if constexpr (YS) {  // launcher guarantees Nc % BJ == 0 and ldy % 8 == 0
+      const size_t o = (size_t)(ok ? m : r_begin) * a.ldy + j;
+      const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int q = 0; q < VPY / 8; ++q) {
+        const uint4 h = *reinterpret_cast<const uint4*>(yh_plane + o + 8 * q);
+        const uint4 l = *reinterpret_cast<const uint4*>(yl_plane + o + 8 * q);
+        ryh[q] = ok ? h : z;
+        ryl[q] = ok ? l : z;
+        if (do_db) {  // the bias gradient from hi + lo in fp32
+          const bf16x8 hv = __builtin_bit_cast(bf16x8, ryh[q]), lv = __builtin_bit_cast(bf16x8, ryl[q]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ry[8 * q + e] = (float)hv[e] + (float)lv[e];
+        }
+      }
+    } else if (ok && fastY && j + VPY <= g.Nc) {
 #pragma unroll
       for (int q = 0; q < VPY / 4; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(a.dy + (size_t)m * a.ldy + j + 4 * q);
@@ -396,7 +440,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
       r = src_row_x(n, t, v, dt, g);
     }
     const int i = i0 + cx;
-    if (r >= 0 && fastX && i + VPX <= g.Kc) {
+    if constexpr (XS) {  // launcher guarantees Kc % BI == 0 and lda % 8 == 0
+      const size_t o = (size_t)max(r, 0) * g.lda + i;
+      const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int q = 0; q < VPX / 8; ++q) {
+        const uint4 h = *reinterpret_cast<const uint4*>(xh_plane + o + 8 * q);
+        const uint4 l = *reinterpret_cast<const uint4*>(xl_plane + o + 8 * q);
+        rxh[q] = r >= 0 ? h : z;
+        rxl[q] = r >= 0 ? l : z;
+      }
+    } else if (r >= 0 && fastX && i + VPX <= g.Kc) {
 #pragma unroll
       for (int q = 0; q < VPX / 4; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(a.in + (size_t)r * g.lda + i + 4 * q);
@@ -422,17 +476,27 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
   auto store_chunk = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < VPY / 8; ++q) {
-      bf16x8 hi, lo;
-      split8(&ry[8 * q], hi, lo);
-      *reinterpret_cast<bf16x8*>(&Ys[buf][0][lrow * YLD + cy + 8 * q]) = hi;
-      *reinterpret_cast<bf16x8*>(&Ys[buf][1][lrow * YLD + cy + 8 * q]) = lo;
+      if constexpr (YS) {
+        *reinterpret_cast<uint4*>(&Ys[buf][0][lrow * YLD + cy + 8 * q]) = ryh[q];
+        *reinterpret_cast<uint4*>(&Ys[buf][1][lrow * YLD + cy + 8 * q]) = ryl[q];
+      } else {
+        bf16x8 hi, lo;
+        split8(&ry[8 * q], hi, lo);
+        *reinterpret_cast<bf16x8*>(&Ys[buf][0][lrow * YLD + cy + 8 * q]) = hi;
+        *reinterpret_cast<bf16x8*>(&Ys[buf][1][lrow * YLD + cy + 8 * q]) = lo;
+      }
     }
 #pragma unroll
     for (int q = 0; q < VPX / 8; ++q) {
-      bf16x8 hi, lo;
-      split8(&rx[8 * q], hi, lo);
-      *reinterpret_cast<bf16x8*>(&Xs[buf][0][lrow * XLD + cx + 8 * q]) = hi;
-      *reinterpret_cast<bf16x8*>(&Xs[buf][1][lrow * XLD + cx + 8 * q]) = lo;
+      if constexpr (XS) {
+        *reinterpret_cast<uint4*>(&Xs[buf][0][lrow * XLD + cx + 8 * q]) = rxh[q];
+        *reinterpret_cast<uint4*>(&Xs[buf][1][lrow * XLD + cx + 8 * q]) = rxl[q];
+      } else {
+        bf16x8 hi, lo;
+        split8(&rx[8 * q], hi, lo);
+        *reinterpret_cast<bf16x8*>(&Xs[buf][0][lrow * XLD + cx + 8 * q]) = hi;
+        *reinterpret_cast<bf16x8*>(&Xs[buf][1][lrow * XLD + cx + 8 * q]) = lo;
+      }
     }
   };
   const int wm = wave >> 1, wj = wave & 1;
@@ -534,14 +598,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
 
 using namespace f3;
 
-template <int WM, int WN>
+template <int WM, int WN, bool AS>
 static int launch_gemm_x3(const ConvGemmArgs& a, int pro, int epi, hipStream_t s) {
   dim3 grid((a.g.M + 32 * WM - 1) / (32 * WM), (a.g.Nc + 32 * WN - 1) / (32 * WN));
-#define F3_XCASE(P, E)                                                               \
-  if (pro == P && epi == (E)) {                                                     \
-    hipLaunchKernelGGL((conv_gemm_x3<P, (E), WM, WN>), grid, dim3(256), 0, s, a);   \
-    F3_LAUNCH_CHECK();                                                               \
-    return F3_OK;                                                                    \
+#define F3_XCASE(P, E)                                                                 \
+  if (pro == P && epi == (E)) {                                                       \
+    hipLaunchKernelGGL((conv_gemm_x3<P, (E), WM, WN, AS>), grid, dim3(256), 0, s, a); \
+    F3_LAUNCH_CHECK();                                                                 \
+    return F3_OK;                                                                      \
   }
   F3_XCASE(0, EPI_BIASV | EPI_STATS)           // gcn forward
   F3_XCASE(1, EPI_BIAS | EPI_STATS | EPI_GAP)  // tcn forward
@@ -558,18 +622,25 @@ static int launch_gemm_x3(const ConvGemmArgs& a, int pro, int epi, hipStream_t s
 int f3_conv_gemm_x3(const ConvGemmArgs* args, int pro, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
-  if (!a.wb || !a.in || a.inb || a.outb) return F3_EINVAL;  // fp32 activations, split weight planes
+  // fp32 activations (in) or pre-split bf16 planes (inb: no prologue, Kc and lda multiples of 8);
+  // split weight planes; fp32 output
+  if (!a.wb || a.outb || (a.in != nullptr) == (a.inb != nullptr)) return F3_EINVAL;
+  if (a.inb && (pro || a.g.Kc % 8 || a.g.lda % 8)) return F3_EINVAL;
   if (pro && a.g.Kc > 256) return F3_EINVAL;
-  if (a.g.Nc >= 128 && a.g.M >= 4096) return launch_gemm_x3<4, 4>(a, pro, epi, s);
-  return launch_gemm_x3<4, 2>(a, pro, epi, s);
+  const bool wide = a.g.Nc >= 128 && a.g.M >= 4096;
+  if (a.inb) return wide ? launch_gemm_x3<4, 4, true>(a, pro, epi, s) : launch_gemm_x3<4, 2, true>(a, pro, epi, s);
+  return wide ? launch_gemm_x3<4, 4, false>(a, pro, epi, s) : launch_gemm_x3<4, 2, false>(a, pro, epi, s);
 }
 
 int f3_conv_wgrad_x3(const WgradArgs* args, int pro, hipStream_t s) {
   WgradArgs a = *args;
   if (a.g.M <= 0) return F3_OK;
-  if (!a.dy || !a.in || a.dyb || a.inb || a.slab) return F3_EINVAL;
+  if (a.slab || (a.dy != nullptr) == (a.dyb != nullptr) || (a.in != nullptr) == (a.inb != nullptr)) return F3_EINVAL;
   if (pro && a.g.Kc > 256) return F3_EINVAL;
   const bool big = a.g.Nc >= 128 && a.g.Kc >= 128;
+  const bool xs = a.inb != nullptr, ys = a.dyb != nullptr;
+  if (xs && (pro || a.g.Kc % (big ? 128 : 64) || a.g.lda % 8)) return F3_EINVAL;
+  if (ys && (a.g.Nc % (big ? 128 : 64) || a.ldy % 8 || (pro && !xs))) return F3_EINVAL;
   const int BJ = big ? 128 : 64, BI = big ? 128 : 64;
   const int gx = (a.g.Nc + BJ - 1) / BJ;
   const int gy = a.g.KT * ((a.g.Kc + BI - 1) / BI);
@@ -580,13 +651,18 @@ int f3_conv_wgrad_x3(const WgradArgs* args, int pro, hipStream_t s) {
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
   dim3 grid(gx, gy, splits * std::max(1, a.groups));
+#define F3_XW(WM_, WN_)                                                                                      \
+  if (xs && ys) hipLaunchKernelGGL((conv_wgrad_x3<0, WM_, WN_, true, true>), grid, dim3(256), 0, s, a);       \
+  else if (xs) hipLaunchKernelGGL((conv_wgrad_x3<0, WM_, WN_, true, false>), grid, dim3(256), 0, s, a);       \
+  else if (ys) hipLaunchKernelGGL((conv_wgrad_x3<0, WM_, WN_, false, true>), grid, dim3(256), 0, s, a);       \
+  else if (pro) hipLaunchKernelGGL((conv_wgrad_x3<1, WM_, WN_, false, false>), grid, dim3(256), 0, s, a);     \
+  else hipLaunchKernelGGL((conv_wgrad_x3<0, WM_, WN_, false, false>), grid, dim3(256), 0, s, a);
   if (big) {
-    if (pro) hipLaunchKernelGGL((conv_wgrad_x3<1, 4, 4>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_x3<0, 4, 4>), grid, dim3(256), 0, s, a);
+    F3_XW(4, 4)
   } else {
-    if (pro) hipLaunchKernelGGL((conv_wgrad_x3<1, 2, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_x3<0, 2, 2>), grid, dim3(256), 0, s, a);
+    F3_XW(2, 2)
   }
+#undef F3_XW
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -107,6 +107,7 @@ struct BlockArgs {
   float* dres;           // dr (conv) or dx (identity)
   unsigned short* dhb;   // bf16 mode: dh written as bf16 (GEMM operand) instead of fp32
   unsigned short* dresb; // bf16 mode, conv residual: dr as bf16 instead of fp32
+  int x3;                // bf16x3 mode: dhb receives dh as bf16 hi plane [M][C] then lo plane [M][C]
   float* dgamma2;
   float* dbeta2;
   float* dgammar;
@@ -136,6 +137,7 @@ struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the
   BnRef bn;
   const float* g;
   unsigned short* u;
+  int x3;                // bf16x3 mode: u as bf16 hi plane [M][C] then lo plane [M][C] (fp32 g)
 };
 
 struct CaArgs {

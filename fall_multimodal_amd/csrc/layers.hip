@@ -1296,10 +1296,15 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
         }
       }
       if (a.dhb) {
-        bf16x4 hb;
+        bf16x4 hb, lb;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) hb[e] = (__bf16)dh[e];
+        for (int e = 0; e < 4; ++e) {
+          hb[e] = (__bf16)dh[e];
+          lb[e] = (__bf16)(dh[e] - (float)hb[e]);
+        }
         *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off[u]) = hb;
+        if (a.x3)  // split planes (gemm_x3.hip): lo = RNE bf16(dh - hi) one plane further
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + (size_t)a.N * a.TV * C + off[u]) = lb;
       } else {
         *reinterpret_cast<f32x4*>(a.dh + off[u]) = dh;
       }
@@ -1419,7 +1424,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
 // are loaded before any is converted (one memory round trip per kBnReluU pieces); 4 workgroups
 // per CU walk the rows so the per-workgroup coefficient prologue is paid ~4x per CU, not per piece.
 constexpr int kBnReluU = 4;
-template <bool G16>
+template <bool G16, bool X3 = false>
 __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
   __shared__ float scs[256], shs[256];
   for (int c = threadIdx.x; c < a.C; c += 256) {
@@ -1450,13 +1455,19 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
     }
   };
   auto put = [&](long long qq, const f32x4& x0, const f32x4& x1) __attribute__((always_inline)) {
-    bf16x8 o;
+    bf16x8 o, l;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      o[e] = (__bf16)fmaxf(x0[e] * sc[e] + sh[e], 0.f);
-      o[4 + e] = (__bf16)fmaxf(x1[e] * sc[4 + e] + sh[4 + e], 0.f);
+      const float u0 = fmaxf(x0[e] * sc[e] + sh[e], 0.f), u1 = fmaxf(x1[e] * sc[4 + e] + sh[4 + e], 0.f);
+      o[e] = (__bf16)u0;
+      o[4 + e] = (__bf16)u1;
+      if constexpr (X3) {  // lo = RNE bf16(u - hi), exact difference (the split of gemm_x3.hip)
+        l[e] = (__bf16)(u0 - (float)o[e]);
+        l[4 + e] = (__bf16)(u1 - (float)o[4 + e]);
+      }
     }
     *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + qq * 8) = o;
+    if constexpr (X3) *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + total8 * 8 + qq * 8) = l;
   };
   for (; q + (kBnReluU - 1) * step < total8; q += kBnReluU * step) {
     f32x4 x0[kBnReluU], x1[kBnReluU];
@@ -2210,6 +2221,7 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   const size_t total8 = (size_t)a->M * a->C / 8;
   // (the main kernel needs 2048 % C == 0: a thread's channel group is fixed over its grid stride)
   if (2048 % a->C) {
+    if (a->x3) return F3_EINVAL;
     const int grid = (int)std::min<size_t>((total8 + 255) / 256, 4096);
     if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_any_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
     else hipLaunchKernelGGL(bnrelu_bf16_any_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
@@ -2217,8 +2229,14 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
     return F3_OK;
   }
   const int grid = (int)std::min<size_t>((total8 + 256 * kBnReluU - 1) / (256 * kBnReluU), 1024);
-  if (a->g16) hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
+  if (a->x3) {
+    if (a->g16) return F3_EINVAL;
+    hipLaunchKernelGGL((bnrelu_bf16_kernel<false, true>), dim3(grid), dim3(256), 0, s, *a);
+  } else if (a->g16) {
+    hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
+  } else {
+    hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

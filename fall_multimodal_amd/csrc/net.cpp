@@ -330,6 +330,7 @@ Ws plan(const f3_net& net, int N, char* base) {
   const int Ts = net.cfg.sensor_frames;
   const int Tl = cnn ? (Ts / 2) / 2 : Ts;
   const bool hb = net.cfg.precision == F3_PRECISION_BF16;
+  const bool x3 = net.cfg.precision == F3_PRECISION_BF16X3;
   // ---- zero-at-forward region ----
   w.zf0 = A.take<char>(0);
   w.zero = reinterpret_cast<const unsigned short*>(A.take<char>(256));
@@ -399,7 +400,8 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.xb = xinb;
       X.z = A.take<float>(Mi * K * Ci);
       X.g = A.take<float>(Mi * C);
-      if (hb) X.u = A.take<unsigned short>(Mi * C);
+      // u = relu(bn1(g)): bf16 (bf16 mode) or bf16 hi + lo planes (bf16x3 mode)
+      if (hb || x3) X.u = A.take<unsigned short>((x3 ? 2 : 1) * Mi * C);
       X.h = A.take<float>(Mo * C);
       if (L.res == RES_CONV) X.r = A.take<float>(Mo * C);
       X.out = A.take<float>(Mo * C);
@@ -637,9 +639,11 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     ta.w = X.tw; ta.wb = bf(X.tw, wq); ta.out = X.h; ta.outb = bfa(X.h, hb); ta.bias = q.p(L.tcn_b);
     ta.x3 = x3;
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
-    if (hb) {  // materialise u = relu(bn1(g)) in bf16 (also the tcn wgrad operand)
+    if (hb || x3) {  // materialise u = relu(bn1(g)) once (also the tcn wgrad operand): bf16, or
+      // (bf16x3) split into bf16 hi / lo planes, instead of BN + ReLU + split at every tap's staging
       BnReluArgs br;
-      br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = 1;
+      std::memset(&br, 0, sizeof(br));
+      br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = hb; br.x3 = x3;
       F3_TRY(f3_bnrelu_bf16(&br, s));
       ta.inb = X.u; ta.zero = w.zero;
       F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
@@ -727,7 +731,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.P1 = X.P1; ba.P2 = X.P2; ba.Q2 = X.Q2; ba.bnr_bsum = X.bnr.bsum; ba.bnr_bsq = X.bnr.bsq;
     ba.bn2_bsum = X.bn2.bsum; ba.bn2_bsq = X.bn2.bsq; ba.e = X.e; ba.dh = dh;
     ba.dres = L.res == RES_CONV ? dres : (L.res == RES_ID ? dx : nullptr);
-    ba.dhb = bfa(dh, hb);
+    ba.dhb = bfa(dh, hb || x3);  // bf16x3: dh as split hi / lo planes (the tcn dgrad / wgrad operand)
+    ba.x3 = x3;
     ba.dresb = L.res == RES_CONV ? bfa(dres, hb) : nullptr;
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
@@ -757,7 +762,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
-    td.in = hb ? nullptr : dh; td.inb = bfa(dh, hb); td.zero = w.zero;
+    td.in = (hb || x3) ? nullptr : dh; td.inb = bfa(dh, hb || x3); td.zero = w.zero;
     td.w = X.twT; td.wb = bf(X.twT, wq); td.x3 = x3; td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
@@ -827,6 +832,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
         if (part & 2) add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
+      if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
+    } else if (x3) {  // dh and u as split planes (block_bwd_apply / bnrelu wrote them)
+      tw.dyb = bfa(dh, 1); tw.inb = X.u;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
