@@ -295,16 +295,17 @@ def sensor_bench(dev, precision="fp32"):
 def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
     """GB/s of the sensor CNN1D launches (GSTCAN_UR_conv.ipynb:493-514: Conv1d(S->16,k5) BN ReLU
     MaxPool, Conv1d(16->32,k5) BN ReLU MaxPool), from HIP events around each launch on the sensor
-    queue (f3_net_sensor_times), mean over `reps` steps. Algorithmic bytes (fp32, each tensor once):
-    conv fwd x + w + y; pool fwd y + p; conv bwd y + dp + x (+ dx for conv2) + dW. The tensors are
-    0.02-0.5 MB, so these launches are latency-bound (a few us each): the GB/s says how close to
-    launch latency they run, not to the 8 TB/s roofline."""
+    queue (f3_net_sensor_times), mean over `reps` steps. Since round 4 the two layers run as six
+    fused launches (sensor.hip cnn_f*/cnn_b*: BN1 + ReLU + pool1 in conv2's load, pool1's backward
+    behind conv2's, BatchNorm sums as per-workgroup partial rows added by the next launch). Algorithmic
+    bytes (fp32, each tensor once): conv1 fwd x + w1 + y1; pool1+conv2 fwd y1 + p1 + w2 + y2; pool2 fwd
+    y2 + p2; pool2 bwd y2 + dp2 + dy2; conv2+pool1 bwd y2 + dy2 + p1 + w2 + dW2 + y1 + dy1; conv1 bwd
+    y1 + dy1 + x + dW1. The tensors are 0.02-1 MB, so these launches are latency-bound (a few us each)."""
     import ctypes
     import fall_multimodal_amd._lib as FL
     L, check = FL.lib(), FL.check
     h = model._native.h
     f32 = 4
-    shapes = [(T, S, 16), (T // 2, 16, 32)]  # (T_in, Ci, Co) per conv layer
     acc = [0.0] * 6
     check(L.f3_net_sensor_times(h, 1, None), "sensor times on")
     for _ in range(3):
@@ -317,23 +318,21 @@ def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
         for i in range(6):
             acc[i] += ms[i] / reps
     check(L.f3_net_sensor_times(h, 0, None), "sensor times off")
+    T2, T3 = T // 2, (T // 2) // 2
+    xb, y1, p1, y2, p2 = (B * T * S * f32, B * T * 16 * f32, B * T2 * 16 * f32, B * T2 * 32 * f32,
+                          B * T3 * 32 * f32)
+    w1, w2 = 16 * S * 5 * f32, 32 * 16 * 5 * f32
+    nbytes = {"conv1_fwd": xb + w1 + y1, "pool1_conv2_fwd": y1 + p1 + w2 + y2, "pool2_fwd": y2 + p2,
+              "pool2_bwd": y2 + p2 + y2, "conv2_pool1_bwd": 2 * y2 + p1 + 2 * w2 + 2 * y1,
+              "conv1_bwd": 2 * y1 + xb + w1}
     out = {}
-    names = ["conv1_fwd", "pool1_fwd", "conv2_fwd", "pool2_fwd", "conv2_bwd", "conv1_bwd"]
-    for i, nm in enumerate(names):
-        layer = 0 if nm.startswith(("conv1", "pool1")) else 1
-        Tl, Ci, Co = shapes[layer]
-        x_b, y_b, p_b, w_b = B * Tl * Ci * f32, B * Tl * Co * f32, B * (Tl // 2) * Co * f32, Co * Ci * 5 * f32
-        if nm.startswith("conv") and nm.endswith("fwd"):
-            nb = x_b + w_b + y_b
-        elif nm.startswith("pool"):
-            nb = y_b + p_b
-        else:
-            nb = y_b + p_b + x_b + 2 * w_b + (x_b if layer == 1 else 0)
+    for i, nm in enumerate(nbytes):
         us = acc[i] * 1e3
-        out[nm] = {"us": round(us, 2), "bytes": nb, "GBps": round(nb / (us * 1e-6) / 1e9, 1)}
+        out[nm] = {"us": round(us, 2), "bytes": nbytes[nm], "GBps": round(nbytes[nm] / (us * 1e-6) / 1e9, 1)}
+    out["total_us"] = round(sum(acc) * 1e3, 2)
     out["batch"] = B
-    out["note"] = ("HIP events around each launch on the sensor queue; latency-bound (tensors of "
-                   "0.02-0.5 MB): GB/s against 8 TB/s is not a meaningful fraction at this size")
+    out["note"] = ("HIP events around each launch on the sensor queue; six fused launches per step (round 4); "
+                   "latency-bound (tensors of 0.02-1 MB): GB/s against 8 TB/s is not a meaningful fraction here")
     return out
 
 

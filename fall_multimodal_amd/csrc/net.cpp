@@ -91,7 +91,7 @@ struct f3_net {
   int p1_mask = 0;  // bit i: ev_p1[i] recorded by the last phase-1 backward
   bool par_init = false, par_ok = false;
   // f3_net_sensor_times: events around the sensor CNN1D launches (0 = off). Forward
-  // 0 | conv1 | 1 | pool1 | 2 | conv2 | 3 | pool2 | 4, backward 5 | conv2' | 6 | conv1' | 7
+  // 0 | conv1 | 1 | pool1 + conv2 | 2 | pool2 | 3, backward 4 | pool2' | 5 | conv2' + pool1' | 6 | conv1' | 7
   int stiming = 0;
   hipEvent_t sev[8] = {};
   void smark(int i, hipStream_t s) {
@@ -270,6 +270,12 @@ struct BnWs {
   double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
 };
 
+// F3_CNN_FUSED=0: the round-3 CNN1D launches (8 per step, same-address fp64 atomics) for A/B
+inline bool cnn_fused() {
+  static const bool on = !getenv("F3_CNN_FUSED") || atoi(getenv("F3_CNN_FUSED")) != 0;
+  return on;
+}
+
 struct LayerWs {
   const float* x = nullptr;  // block input (previous block output or data_bn output)
   float *z, *g, *h, *r = nullptr, *out, *q1, *hid, *att, *gap;
@@ -302,6 +308,7 @@ struct Ws {
   StreamWs st[2];
   // sensor
   float *y1, *p1, *y2, *p2, *dy1, *dp1, *dy2, *dp2;
+  float* cpart;  // fused CNN1D: per-workgroup BatchNorm partial rows (f3_cnn1d_part_floats)
   BnWs cbn1, cbn2, sbn;
   float *seq, *gates, *cell, *hmean, *ybn, *a1, *satt, *sout, *sdy, *sdpre2, *sdpre1, *dhmean;
   // head
@@ -452,6 +459,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       w.dy1 = A.take<float>((size_t)N * Ts * 16);
       w.dp1 = A.take<float>((size_t)N * (Ts / 2) * 16);
       w.dy2 = A.take<float>((size_t)N * (Ts / 2) * 32);
+      w.cpart = A.take<float>((size_t)f3_cnn1d_part_floats());
     }
     w.seq = A.take<float>((size_t)N * Tl * 128);
     w.gates = A.take<float>((size_t)2 * N * Tl * 256);
@@ -1213,16 +1221,25 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     SHeadArgs sa;
     Conv1dArgs c1, c2;
     sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
-    if (net->has_cnn) {
+    if (net->has_cnn && cnn_fused()) {  // conv1 | pool1 + conv2 | pool2 (sensor.hip cnn_f*_kernel)
+      for (int st = 0; st < 3; ++st) {
+        net->smark(st, ss);
+        F3_TRY(f3_cnn1d_fwd(&c1, &c2, w.cpart, st, ss));
+      }
+      net->smark(3, ss);
+      if (training) {
+        add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
+        add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
+      }
+    } else if (net->has_cnn) {
       net->smark(0, ss);
       F3_TRY(f3_conv1d_fwd(&c1, ss));
-      net->smark(1, ss);
       F3_TRY(f3_bnrelupool_fwd(&c1, ss));
-      net->smark(2, ss);
+      net->smark(1, ss);
       F3_TRY(f3_conv1d_fwd(&c2, ss));
-      net->smark(3, ss);
+      net->smark(2, ss);
       F3_TRY(f3_bnrelupool_fwd(&c2, ss));
-      net->smark(4, ss);
+      net->smark(3, ss);
       if (training) {
         add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
         add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
@@ -1343,7 +1360,14 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
     const hipStream_t ss = br.at(2);
     F3_TRY(f3_shead_bwd(&sa, ss));
     F3_TRY(f3_lstm_bwd(&la, ss));
-    if (net->has_cnn) {
+    if (net->has_cnn && cnn_fused()) {  // pool2' | conv2' + pool1' | conv1'
+      for (int st = 0; st < 3; ++st) {
+        net->smark(4 + st, ss);
+        F3_TRY(f3_cnn1d_bwd(&c1, &c2, w.cpart, st, ss));
+      }
+      net->smark(7, ss);
+    } else if (net->has_cnn) {
+      net->smark(4, ss);
       net->smark(5, ss);
       F3_TRY(f3_conv1d_bwd(&c2, ss));
       net->smark(6, ss);
@@ -1364,9 +1388,9 @@ int f3_net_sensor_times(f3_net* net, int enable, float* ms) {
     for (auto& e : net->sev)
       if (!e && hipEventCreate(&e) != hipSuccess) return F3_EHIP;
   }
-  if (ms) {  // conv1 fwd, pool1 fwd, conv2 fwd, pool2 fwd, conv2 bwd, conv1 bwd (ms)
+  if (ms) {  // fwd: conv1 | pool1 + conv2 | pool2; bwd: pool2' | conv2' + pool1' | conv1' (ms)
     if (!net->stiming) return F3_ESTATE;
-    const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {5, 6}, {6, 7}};
+    const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}};
     for (int i = 0; i < 6; ++i) {
       if (hipEventSynchronize(net->sev[pairs[i][1]]) != hipSuccess ||
           hipEventElapsedTime(&ms[i], net->sev[pairs[i][0]], net->sev[pairs[i][1]]) != hipSuccess)

@@ -694,6 +694,322 @@ __global__ __launch_bounds__(C1D_THREADS) void conv1d_bwd_kernel(Conv1dArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// Fused CNN1D (round 4): six launches instead of eight, and no same-address atomics. Each launch
+// walks the clips with a grid of <= kCnnGrid workgroups; its BatchNorm sums leave as one fp32
+// partial row per workgroup (plain stores, part[blk][2 Co]), and the NEXT launch's prologue adds the
+// rows in fp64 (every workgroup; <= 128 x 64 floats) before it needs the coefficients. Workgroup 0 of
+// that launch also stores the totals where the running-stat update / backward BnRef read them.
+//   fwd: F1 conv1 + BN1 rows | F2 BN1 + ReLU + pool1 (-> p1) + conv2 + BN2 rows | F3 BN2 + ReLU + pool2
+//   bwd: B1 pool2 / ReLU backward (-> dy2) + BN2-bwd rows | B2 BN2 apply backward, conv2 dW / db, dp1
+//        in LDS, pool1 / ReLU backward (-> dy1) + BN1-bwd rows | B3 BN1 apply backward, conv1 dW / db
+// (GSTCAN_UR_conv.ipynb:493-514: Conv1d(k5, p2) -> BatchNorm1d -> ReLU -> MaxPool1d(2), twice.)
+// ----------------------------------------------------------------------------
+constexpr int kCnnGrid = 128;
+
+// fp64 totals of a launch's partial rows: out[j] = sum_g part[g][j], j < n (every thread of the
+// workgroup takes part; result in LDS)
+F3_DEV void cnn_rows_total(const float* part, int rows, int n, double* out) {
+  const int tid = threadIdx.x;
+  if (tid < n) {
+    double s = 0.0;
+    for (int g = 0; g < rows; ++g) s += (double)part[(size_t)g * n + tid];
+    out[tid] = s;
+  }
+  __syncthreads();
+}
+
+// per-channel block sums of two register partials (channel = tid % Co) -> part row [2 Co]
+F3_DEV void cnn_rows_store(float v1, float v2, int Co, float* red, float* row) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  red[tid] = v1;
+  red[C1D_THREADS + tid] = v2;
+  __syncthreads();
+  if (tid < 2 * Co) {
+    const int c = tid % Co, h = tid / Co;
+    float s = 0.f;
+    for (int i = c; i < C1D_THREADS; i += Co) s += red[h * C1D_THREADS + i];
+    row[tid] = s;
+  }
+}
+
+// train-mode coefficients from fp64 totals (count values per channel) or eval-mode running stats
+F3_DEV void cnn_coeff(const BnRef& b, const double* tot, int Co, int c, float& sc, float& sh, float& mu, float& rs) {
+  if (b.eval) {
+    bn_coeff(b, c, sc, sh, mu, rs);
+    return;
+  }
+  const double m = tot[c] / (double)b.count;
+  double v = tot[Co + c] / (double)b.count - m * m;
+  if (v < 0) v = 0;
+  mu = (float)m;
+  rs = (float)(1.0 / sqrt(v + (double)kBnEps));
+  sc = b.gamma[c] * rs;
+  sh = b.beta[c] - mu * sc;
+}
+
+__global__ __launch_bounds__(C1D_THREADS) void cnn_f1_kernel(Conv1dArgs a, float* part) {
+  extern __shared__ float c1d_sm[];
+  float* ws = c1d_sm;                  // [Co][Ci][5]
+  float* xs = ws + a.Co * a.Ci * 5;    // [T][Ci]
+  float* red = xs + a.T * a.Ci;        // [2][256]
+  const int tid = threadIdx.x, o = tid % a.Co, TCo = a.T * a.Co, TCi = a.T * a.Ci;
+  for (int i = tid; i < a.Co * a.Ci * 5; i += C1D_THREADS) ws[i] = a.w[i];
+  float s1 = 0.f, s2 = 0.f;
+  const float bo = a.b[o];
+  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
+    __syncthreads();
+    for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
+    __syncthreads();
+    for (int i = tid; i < TCo; i += C1D_THREADS) {
+      const int t = i / a.Co;
+      float acc = bo;
+      for (int k = 0; k < 5; ++k) {
+        const int ti = t + k - 2;
+        if (ti < 0 || ti >= a.T) continue;
+        const float* xr = xs + ti * a.Ci;
+        const float* wr = ws + o * a.Ci * 5 + k;
+        for (int c = 0; c < a.Ci; ++c) acc += wr[c * 5] * xr[c];
+      }
+      a.y[(size_t)n * TCo + i] = acc;
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+  cnn_rows_store(s1, s2, a.Co, red, part + (size_t)blockIdx.x * 2 * a.Co);
+}
+
+// a1: conv1 (its y, BN1, pooled output p); a2: conv2 (input a2.x == a1.p)
+__global__ __launch_bounds__(C1D_THREADS) void cnn_f2_kernel(Conv1dArgs a1, Conv1dArgs a2, const float* part1,
+                                                            int rows1, float* part2) {
+  extern __shared__ float c1d_sm[];
+  __shared__ double tot[64];
+  __shared__ float sc1[32], sh1[32];
+  float* ws = c1d_sm;                     // [Co2][Ci2][5]
+  float* ys = ws + a2.Co * a2.Ci * 5;     // [T1][Co1] the clip's conv1 output
+  float* ps = ys + a1.T * a1.Co;          // [T2][Ci2] pooled (conv2 input)
+  float* red = ps + a2.T * a2.Ci;         // [2][256]
+  const int tid = threadIdx.x, Co1 = a1.Co;
+  cnn_rows_total(part1, rows1, 2 * Co1, tot);
+  if (tid < Co1) {
+    float mu, rs;
+    cnn_coeff(a1.bn, tot, Co1, tid, sc1[tid], sh1[tid], mu, rs);
+  }
+  if (blockIdx.x == 0 && !a1.bn.eval && tid < 2 * Co1) (tid < Co1 ? a1.st_sum[tid] : a1.st_sq[tid - Co1]) = tot[tid];
+  for (int i = tid; i < a2.Co * a2.Ci * 5; i += C1D_THREADS) ws[i] = a2.w[i];
+  const int o = tid % a2.Co, TCo2 = a2.T * a2.Co, TC1 = a1.T * Co1, TP = a2.T * Co1;
+  float s1 = 0.f, s2 = 0.f;
+  const float bo = a2.b[o];
+  for (int n = blockIdx.x; n < a2.N; n += gridDim.x) {
+    __syncthreads();
+    for (int i = tid; i < TC1; i += C1D_THREADS) ys[i] = a1.y[(size_t)n * TC1 + i];
+    __syncthreads();
+    for (int i = tid; i < TP; i += C1D_THREADS) {  // MaxPool1d(2) of ReLU(BN1), T1 / 2 frames
+      const int tp = i / Co1, c = i - tp * Co1;
+      const float v = fmaxf(fmaxf(ys[(2 * tp) * Co1 + c] * sc1[c] + sh1[c], 0.f),
+                            fmaxf(ys[(2 * tp + 1) * Co1 + c] * sc1[c] + sh1[c], 0.f));
+      ps[i] = v;
+      a1.p[(size_t)n * TP + i] = v;
+    }
+    __syncthreads();
+    for (int i = tid; i < TCo2; i += C1D_THREADS) {
+      const int t = i / a2.Co;
+      float acc = bo;
+      for (int k = 0; k < 5; ++k) {
+        const int ti = t + k - 2;
+        if (ti < 0 || ti >= a2.T) continue;
+        const float* xr = ps + ti * a2.Ci;
+        const float* wr = ws + o * a2.Ci * 5 + k;
+        for (int c = 0; c < a2.Ci; ++c) acc += wr[c * 5] * xr[c];
+      }
+      a2.y[(size_t)n * TCo2 + i] = acc;
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+  cnn_rows_store(s1, s2, a2.Co, red, part2 + (size_t)blockIdx.x * 2 * a2.Co);
+}
+
+// BN2 + ReLU + MaxPool1d(2) -> p (the LSTM input)
+__global__ __launch_bounds__(C1D_THREADS) void cnn_f3_kernel(Conv1dArgs a, const float* part, int rows) {
+  __shared__ double tot[64];
+  __shared__ float sc[32], sh[32];
+  const int tid = threadIdx.x;
+  cnn_rows_total(part, rows, 2 * a.Co, tot);
+  if (tid < a.Co) {
+    float mu, rs;
+    cnn_coeff(a.bn, tot, a.Co, tid, sc[tid], sh[tid], mu, rs);
+  }
+  if (blockIdx.x == 0 && !a.bn.eval && tid < 2 * a.Co) (tid < a.Co ? a.st_sum[tid] : a.st_sq[tid - a.Co]) = tot[tid];
+  __syncthreads();
+  const int Tp = a.T / 2, tot_n = a.N * Tp * a.Co;
+  for (int i = blockIdx.x * C1D_THREADS + tid; i < tot_n; i += gridDim.x * C1D_THREADS) {
+    const int o = i % a.Co, r = i / a.Co, n = r / Tp, tp = r - n * Tp;
+    const float* y = a.y + ((size_t)n * a.T + 2 * tp) * a.Co + o;
+    a.p[i] = fmaxf(fmaxf(y[0] * sc[o] + sh[o], 0.f), fmaxf(y[a.Co] * sc[o] + sh[o], 0.f));
+  }
+}
+
+// gradient through MaxPool1d(2) + ReLU of one clip's channel-o rows; returns d for frame t
+F3_DEV float cnn_pool_bwd(const float* yc, int Co, int t, int o, float sc, float sh, int Tp, const float* dpc) {
+  const int tp = t >> 1;
+  if (tp >= Tp) return 0.f;
+  const float v0 = fmaxf(yc[(2 * tp) * Co + o] * sc + sh, 0.f);
+  const float v1 = fmaxf(yc[(2 * tp + 1) * Co + o] * sc + sh, 0.f);
+  const int win = (v1 > v0) ? 1 : 0;  // first max wins ties (max_pool1d)
+  const float me = fmaxf(yc[t * Co + o] * sc + sh, 0.f);
+  return ((t & 1) == win && me > 0.f) ? dpc[tp * Co + o] : 0.f;
+}
+
+// B1: dy2 and the BN2-backward partial rows (sum dy, sum dy * xhat)
+__global__ __launch_bounds__(C1D_THREADS) void cnn_b1_kernel(Conv1dArgs a, float* part) {
+  __shared__ float red[2 * C1D_THREADS];
+  const int tid = threadIdx.x, o = tid % a.Co, Tp = a.T / 2, TCo = a.T * a.Co;
+  float sc, sh, mu, rs;
+  bn_coeff(a.bn, o, sc, sh, mu, rs);
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
+    const float* yc = a.y + (size_t)n * TCo;
+    const float* dpc = a.dp + (size_t)n * Tp * a.Co;
+    for (int i = tid; i < TCo; i += C1D_THREADS) {
+      const int t = i / a.Co;
+      const float d = cnn_pool_bwd(yc, a.Co, t, o, sc, sh, Tp, dpc);
+      a.dy[(size_t)n * TCo + i] = d;
+      s1 += d;
+      s2 += d * ((yc[i] - mu) * rs);
+    }
+  }
+  cnn_rows_store(s1, s2, a.Co, red, part + (size_t)blockIdx.x * 2 * a.Co);
+}
+
+// B2: BN2 apply backward, conv2 dW / db (register partials), dp1 = conv2^T(dc2) in LDS, then the
+// pool1 / ReLU backward of conv1's output (dy1) and the BN1-backward partial rows
+__global__ __launch_bounds__(C1D_THREADS) void cnn_b2_kernel(Conv1dArgs a1, Conv1dArgs a2, const float* part2,
+                                                            int rows2, float* part1) {
+  extern __shared__ float c1d_sm[];
+  __shared__ double tot[64];
+  float* dcs = c1d_sm;                    // [T2][Co2]
+  float* xs = dcs + a2.T * a2.Co;         // [T2][Ci2] conv2 input (p1)
+  float* ws = xs + a2.T * a2.Ci;          // [Co2][Ci2][5]
+  float* dps = ws + a2.Co * a2.Ci * 5;    // [T2][Ci2] dp1
+  float* red = dps + a2.T * a2.Ci;        // [2][256]
+  const int tid = threadIdx.x, Co2 = a2.Co, Ci2 = a2.Ci, T2 = a2.T, NW = Co2 * Ci2 * 5;
+  const float M2 = a2.bn.count;
+  cnn_rows_total(part2, rows2, 2 * Co2, tot);
+  if (blockIdx.x == 0 && tid < Co2) {
+    a2.g_gamma[tid] += (float)tot[Co2 + tid];
+    a2.g_beta[tid] += (float)tot[tid];
+  }
+  for (int i = tid; i < NW; i += C1D_THREADS) ws[i] = a2.w[i];
+  float gw[C1D_WMAX], gb = 0.f;
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) gw[e] = 0.f;
+  // conv1's BN1 coefficients for the pool1 backward (channel of this thread: tid % Co1)
+  const int Co1 = a1.Co, o1 = tid % Co1, Tp1 = a1.T / 2, TC1 = a1.T * Co1;
+  float sc1, sh1, mu1, rs1;
+  bn_coeff(a1.bn, o1, sc1, sh1, mu1, rs1);
+  float q1 = 0.f, q2 = 0.f;
+  for (int n = blockIdx.x; n < a2.N; n += gridDim.x) {
+    __syncthreads();
+    for (int i = tid; i < T2 * Co2; i += C1D_THREADS) {
+      const int o = i % Co2;
+      float sc, sh, mu, rs;
+      bn_coeff(a2.bn, o, sc, sh, mu, rs);
+      const float xh = (a2.y[(size_t)n * T2 * Co2 + i] - mu) * rs;
+      const float d = a2.dy[(size_t)n * T2 * Co2 + i];
+      dcs[i] = a2.bn.gamma[o] * rs * (d - (float)tot[o] / M2 - xh * (float)tot[Co2 + o] / M2);
+    }
+    for (int i = tid; i < T2 * Ci2; i += C1D_THREADS) xs[i] = a2.x[(size_t)n * T2 * Ci2 + i];
+    __syncthreads();
+    if (tid < Co2)
+      for (int t = 0; t < T2; ++t) gb += dcs[t * Co2 + tid];
+#pragma unroll
+    for (int e = 0; e < C1D_WMAX; ++e) {
+      const int i = tid + e * C1D_THREADS;
+      if (i >= NW) break;
+      const int o = i / (Ci2 * 5), r = i - o * Ci2 * 5, c = r / 5, k = r - c * 5;
+      float acc = 0.f;
+      for (int t = max(0, 2 - k); t < min(T2, T2 + 2 - k); ++t) acc += dcs[t * Co2 + o] * xs[(t + k - 2) * Ci2 + c];
+      gw[e] += acc;
+    }
+    for (int i = tid; i < T2 * Ci2; i += C1D_THREADS) {
+      const int ti = i / Ci2, c = i - ti * Ci2;
+      float acc = 0.f;
+      for (int k = 0; k < 5; ++k) {
+        const int t = ti - k + 2;
+        if (t < 0 || t >= T2) continue;
+        for (int o = 0; o < Co2; ++o) acc += dcs[t * Co2 + o] * ws[(o * Ci2 + c) * 5 + k];
+      }
+      dps[i] = acc;
+    }
+    __syncthreads();
+    const float* yc = a1.y + (size_t)n * TC1;
+    for (int i = tid; i < TC1; i += C1D_THREADS) {  // channel of i is o1 (256 % Co1 == 0)
+      const int t = i / Co1;
+      const float d = cnn_pool_bwd(yc, Co1, t, o1, sc1, sh1, Tp1, dps);
+      a1.dy[(size_t)n * TC1 + i] = d;
+      q1 += d;
+      q2 += d * ((yc[i] - mu1) * rs1);
+    }
+  }
+  if (tid < Co2) atomic_add_f(a2.g_b + tid, gb);
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) {
+    const int i = tid + e * C1D_THREADS;
+    if (i < NW) atomic_add_f(a2.g_w + i, gw[e]);
+  }
+  cnn_rows_store(q1, q2, Co1, red, part1 + (size_t)blockIdx.x * 2 * Co1);
+}
+
+// B3: BN1 apply backward and the conv1 weight / bias gradients (no input gradient: the sensor data)
+__global__ __launch_bounds__(C1D_THREADS) void cnn_b3_kernel(Conv1dArgs a, const float* part, int rows) {
+  extern __shared__ float c1d_sm[];
+  __shared__ double tot[64];
+  float* dcs = c1d_sm;                 // [T][Co]
+  float* xs = dcs + a.T * a.Co;        // [T][Ci]
+  const int tid = threadIdx.x, TCo = a.T * a.Co, TCi = a.T * a.Ci, NW = a.Co * a.Ci * 5;
+  const float M = a.bn.count;
+  cnn_rows_total(part, rows, 2 * a.Co, tot);
+  if (blockIdx.x == 0 && tid < a.Co) {
+    a.g_gamma[tid] += (float)tot[a.Co + tid];
+    a.g_beta[tid] += (float)tot[tid];
+  }
+  float gw[C1D_WMAX], gb = 0.f;
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) gw[e] = 0.f;
+  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
+    __syncthreads();
+    for (int i = tid; i < TCo; i += C1D_THREADS) {
+      const int o = i % a.Co;
+      float sc, sh, mu, rs;
+      bn_coeff(a.bn, o, sc, sh, mu, rs);
+      const float xh = (a.y[(size_t)n * TCo + i] - mu) * rs;
+      const float d = a.dy[(size_t)n * TCo + i];
+      dcs[i] = a.bn.gamma[o] * rs * (d - (float)tot[o] / M - xh * (float)tot[a.Co + o] / M);
+    }
+    for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
+    __syncthreads();
+    if (tid < a.Co)
+      for (int t = 0; t < a.T; ++t) gb += dcs[t * a.Co + tid];
+#pragma unroll
+    for (int e = 0; e < C1D_WMAX; ++e) {
+      const int i = tid + e * C1D_THREADS;
+      if (i >= NW) break;
+      const int o = i / (a.Ci * 5), r = i - o * a.Ci * 5, c = r / 5, k = r - c * 5;
+      float acc = 0.f;
+      for (int t = max(0, 2 - k); t < min(a.T, a.T + 2 - k); ++t) acc += dcs[t * a.Co + o] * xs[(t + k - 2) * a.Ci + c];
+      gw[e] += acc;
+    }
+  }
+  if (tid < a.Co) atomic_add_f(a.g_b + tid, gb);
+#pragma unroll
+  for (int e = 0; e < C1D_WMAX; ++e) {
+    const int i = tid + e * C1D_THREADS;
+    if (i < NW) atomic_add_f(a.g_w + i, gw[e]);
+  }
+}
+
 }  // namespace f3
 
 using namespace f3;
@@ -799,6 +1115,56 @@ int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(conv1d_bwd_kernel, dim3(c1d_grid(*a)), dim3(C1D_THREADS),
                      ((size_t)a->T * (a->Co + a->Ci) + (size_t)a->Co * a->Ci * 5) * 4, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+// ---- fused CNN1D entry points (six launches per step; see cnn_f1_kernel) ----
+static int cnn_grid(int N) { return std::max(1, std::min(N, kCnnGrid)); }
+
+long long f3_cnn1d_part_floats() { return 4LL * kCnnGrid * 64; }
+
+static bool cnn_ok(const Conv1dArgs& c1, const Conv1dArgs& c2) {
+  return c1d_ok(c1) && c1d_ok(c2) && c2.Ci == c1.Co && c2.T == c1.T / 2 && 2 * c1.Co <= 64 && 2 * c2.Co <= 64 &&
+         c1.N == c2.N && c1.Co <= 32 && c2.Co <= 32;
+}
+
+int f3_cnn1d_fwd(const Conv1dArgs* c1, const Conv1dArgs* c2, float* part, int stage, hipStream_t s) {
+  if (!cnn_ok(*c1, *c2) || !part) return F3_EINVAL;
+  const int G = cnn_grid(c1->N);
+  float* p1 = part;                 // BN1 rows [G][2 Co1]
+  float* p2 = part + kCnnGrid * 64; // BN2 rows [G][2 Co2]
+  if (stage == 0) {
+    const size_t lds = ((size_t)c1->Co * c1->Ci * 5 + (size_t)c1->T * c1->Ci + 2 * C1D_THREADS) * 4;
+    hipLaunchKernelGGL(cnn_f1_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, p1);
+  } else if (stage == 1) {
+    const size_t lds = ((size_t)c2->Co * c2->Ci * 5 + (size_t)c1->T * c1->Co + (size_t)c2->T * c2->Ci +
+                        2 * C1D_THREADS) * 4;
+    hipLaunchKernelGGL(cnn_f2_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, *c2, (const float*)p1, G, p2);
+  } else {
+    const int tot = c2->N * (c2->T / 2) * c2->Co;
+    const int g3 = std::max(1, std::min((tot + C1D_THREADS - 1) / C1D_THREADS, 64));
+    hipLaunchKernelGGL(cnn_f3_kernel, dim3(g3), dim3(C1D_THREADS), 0, s, *c2, (const float*)p2, G);
+  }
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_cnn1d_bwd(const Conv1dArgs* c1, const Conv1dArgs* c2, float* part, int stage, hipStream_t s) {
+  if (!cnn_ok(*c1, *c2) || !part) return F3_EINVAL;
+  const int G = cnn_grid(c1->N);
+  float* q2 = part + 2 * kCnnGrid * 64;  // BN2-backward rows
+  float* q1 = part + 3 * kCnnGrid * 64;  // BN1-backward rows
+  if (stage == 0) {
+    hipLaunchKernelGGL(cnn_b1_kernel, dim3(G), dim3(C1D_THREADS), 0, s, *c2, q2);
+  } else if (stage == 1) {
+    const size_t lds = ((size_t)c2->T * c2->Co + 2 * (size_t)c2->T * c2->Ci + (size_t)c2->Co * c2->Ci * 5 +
+                        2 * C1D_THREADS) * 4;
+    hipLaunchKernelGGL(cnn_b2_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, *c2, (const float*)q2, G, q1);
+  } else {
+    const size_t lds = ((size_t)c1->T * (c1->Co + c1->Ci)) * 4;
+    hipLaunchKernelGGL(cnn_b3_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, (const float*)q1, G);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
