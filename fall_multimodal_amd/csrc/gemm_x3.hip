@@ -608,7 +608,8 @@ static int launch_gemm_x3(const ConvGemmArgs& a, int pro, int epi, hipStream_t s
     return F3_OK;                                                                      \
   }
   F3_XCASE(0, EPI_BIASV | EPI_STATS)           // gcn forward
-  F3_XCASE(1, EPI_BIAS | EPI_STATS | EPI_GAP)  // tcn forward
+  F3_XCASE(1, EPI_BIAS | EPI_STATS | EPI_GAP)  // tcn forward, BN1 + ReLU in the staging
+  F3_XCASE(0, EPI_BIAS | EPI_STATS | EPI_GAP)  // tcn forward on the pre-split u
   F3_XCASE(0, EPI_BIAS | EPI_STATS)            // residual forward
   F3_XCASE(0, EPI_RELUMASK)                    // tcn dgrad (+BN1 bwd sums)
   F3_XCASE(0, 0)                               // gcn dgrad
