@@ -1412,6 +1412,39 @@ static int launch_wgrad_seg(WgradArgs a, int nks, hipStream_t s) {
   return F3_OK;
 }
 
+// bf16x3 (K-concatenated) weight gradient: dw_ref[j][i][dt] += sum_s (slab[s][j][dt*Kc2 + i] +
+// slab[s][j][dt*Kc2 + Ci + i] + slab[s][C + j][dt*Kc2 + i]), i.e. the hi*hi + hi*lo + lo*hi quadrants
+// of the [2C][KT][2Ci] partials (the lo*lo quadrant is dropped, as the split-bf16 product drops it);
+// workgroup 0 also folds the [2C] bias-gradient scratch. One thread per (j, dt, i): slab reads are
+// contiguous in i.
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_x3_kernel(const float* __restrict__ slab, int splits, int Nc2,
+                                                                   int Kc2, int KT, float* __restrict__ dw_ref,
+                                                                   const float* __restrict__ dbs, float* db) {
+  const int C = Nc2 / 2, Ci = Kc2 / 2;
+  const long long per = (long long)Nc2 * KT * Kc2;
+  const long long n = (long long)C * KT * Ci;
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (long long)gridDim.x * 256) {
+    const int j = (int)(idx / ((long long)KT * Ci));
+    const int r = (int)(idx - (long long)j * KT * Ci), dt = r / Ci, i = r - dt * Ci;
+    const float* p0 = slab + (size_t)j * KT * Kc2 + (size_t)dt * Kc2 + i;
+    const float* p1 = slab + (size_t)(C + j) * KT * Kc2 + (size_t)dt * Kc2 + i;
+    float v = 0.f;
+    for (int sp = 0; sp < splits; ++sp) v += p0[sp * per] + p0[sp * per + Ci] + p1[sp * per];
+    dw_ref[((size_t)j * Ci + i) * KT + dt] += v;
+  }
+  if (blockIdx.x == 0 && db && dbs)
+    for (int c = threadIdx.x; c < C; c += 256) db[c] += dbs[c] + dbs[C + c];
+}
+
+static int launch_fold_x3(const WgradArgs& a, int splits, hipStream_t s) {
+  const long long n = (long long)(a.g.Nc / 2) * a.g.KT * (a.g.Kc / 2);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(wgrad_slab_reduce_x3_kernel, dim3(grid), dim3(256), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
+                     a.g.KT, a.dw_ref, a.db, a.db_fold);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
 bool f3_wgrad_glds_ok(const WgradArgs& a) {
   return a.dyb && a.inb && a.zero && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && a.ldy % 8 == 0 && a.g.lda % 8 == 0;
 }
@@ -1443,7 +1476,8 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   if (to_slab) {
     if (a.slab_cap < per_split) return F3_EINVAL;
     // (the slab grew for wgrad_taps; these tiles keep their measured split count)
-    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, 512LL * 128 * 128) / per_split);
+    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, a.x3fold ? a.slab_cap : 512LL * 128 * 128) /
+                                                  per_split);
   }
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + 63) / 64) * 64;
@@ -1459,6 +1493,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), 0, s, a);
   F3_LAUNCH_CHECK();
   if (to_slab && a.dw_ref) {
+    if (a.x3fold) return launch_fold_x3(a, splits, s);
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
                        a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref);
     F3_LAUNCH_CHECK();
@@ -1470,6 +1505,8 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const WgradArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  if (a.x3fold && (!a.slab || !a.dw_ref || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.Nc % 2 || a.g.Kc % 2))
+    return F3_EINVAL;
   // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
   static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
   const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
@@ -1477,7 +1514,7 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const int bigv = a.groups > 1 ? 1 : big;
   // F3_WGRAD_TAPS=0: the per-tap wgrad_big tiles for the stride-1 clip-sized layers too
   static const int taps_env = getenv("F3_WGRAD_TAPS") ? atoi(getenv("F3_WGRAD_TAPS")) : 1;
-  if (taps_env && bigv) {
+  if (taps_env && bigv && !a.x3fold) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
     const int nks = wgrad_taps_nks(a);
     if (nks) return launch_wgrad_taps(a, nks, s);
     const int nseg = wgrad_seg_nks(a);  // every other (9,1) layer: clip segments, stride 2 by parity

@@ -34,13 +34,6 @@ constexpr int XBK = 32;  // k (or m) per chunk
 
 F3_DEV f32x4 mfma_x(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
-// the three products of a split pair, small terms first
-F3_DEV f32x4 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
-  c = mfma_x(al, bh, c);
-  c = mfma_x(ah, bl, c);
-  return mfma_x(ah, bh, c);
-}
-
 F3_DEV void split8(const float* x, bf16x8& hi, bf16x8& lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -266,10 +259,19 @@ __global__ __launch_bounds__(256) void conv_gemm_x3(ConvGemmArgs a) {
       bh[y] = *reinterpret_cast<const bf16x8*>(&Bs[buf][xoff(r, fg)]);
       bl[y] = *reinterpret_cast<const bf16x8*>(&Bs[buf][xoff(r, 4 + fg)]);
     }
+    // the three products as three passes over the tile: consecutive MFMAs never share an accumulator
 #pragma unroll
     for (int x = 0; x < WM; ++x)
 #pragma unroll
-      for (int y = 0; y < WN; ++y) acc[x][y] = mfma_x3(ah[x], al[x], bh[y], bl[y], acc[x][y]);
+      for (int y = 0; y < WN; ++y) acc[x][y] = mfma_x(al[x], bh[y], acc[x][y]);
+#pragma unroll
+    for (int x = 0; x < WM; ++x)
+#pragma unroll
+      for (int y = 0; y < WN; ++y) acc[x][y] = mfma_x(ah[x], bl[y], acc[x][y]);
+#pragma unroll
+    for (int x = 0; x < WM; ++x)
+#pragma unroll
+      for (int y = 0; y < WN; ++y) acc[x][y] = mfma_x(ah[x], bh[y], acc[x][y]);
     if (c + 1 < nchunk) store_chunk(buf ^ 1);
     __syncthreads();
   }
@@ -542,10 +544,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(WgradArgs a_) {
         f[k] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo4[k], hi4[k], 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int x = 0; x < WM; ++x)
+      for (int p = 0; p < 3; ++p)  // lo*hi, hi*lo, hi*hi passes (no back-to-back accumulator reuse)
 #pragma unroll
-        for (int y = 0; y < WN; ++y)
-          acc[x][y] = mfma_x3(f[2 * x], f[2 * x + 1], f[2 * WM + 2 * y], f[2 * WM + 2 * y + 1], acc[x][y]);
+        for (int x = 0; x < WM; ++x)
+#pragma unroll
+          for (int y = 0; y < WN; ++y)
+            acc[x][y] = mfma_x(f[2 * x + (p == 0)], f[2 * WM + 2 * y + (p == 1)], acc[x][y]);
       if (more) store_chunk(buf ^ 1);
       __syncthreads();
       buf ^= 1;

@@ -14,7 +14,7 @@ struct PrepJob {
   const float* s1;
   const float* s2;
   int d0, d1, d2;
-  int bf16;  // store dst as bf16 (packed GEMM operands of the bf16 mode)
+  int bf16;  // dst type: 0 fp32, 1 bf16, 2 bf16 hi / lo planes, 3 K-concatenated [hi | hi | lo] (bf16x3)
 };
 
 struct DataBnArgs {
@@ -107,7 +107,7 @@ struct BlockArgs {
   float* dres;           // dr (conv) or dx (identity)
   unsigned short* dhb;   // bf16 mode: dh written as bf16 (GEMM operand) instead of fp32
   unsigned short* dresb; // bf16 mode, conv residual: dr as bf16 instead of fp32
-  int x3;                // bf16x3 mode: dhb receives dh as bf16 hi plane [M][C] then lo plane [M][C]
+  int x3;                // bf16x3 mode: dhb receives dh as rows [hi | lo | hi] of 3C bf16
   float* dgamma2;
   float* dbeta2;
   float* dgammar;
@@ -137,7 +137,7 @@ struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the
   BnRef bn;
   const float* g;
   unsigned short* u;
-  int x3;                // bf16x3 mode: u as bf16 hi plane [M][C] then lo plane [M][C] (fp32 g)
+  int x3;                // bf16x3 mode: u as rows [hi | lo | hi] of 3C bf16 (fp32 g)
 };
 
 struct CaArgs {

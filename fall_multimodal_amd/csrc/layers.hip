@@ -20,9 +20,28 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // ----------------------------------------------------------------------------
 // prep: A_eff = A * E, gcn bias through the graph, weight packing  (one launch)
 // ----------------------------------------------------------------------------
+// bf16x3 on the bf16 kernels (prep code 3, PACK_CONV / PACK_CONV_T): every tap's k range is
+// tripled to [W_hi | W_hi | W_lo] (dst [J][KT][3I]; the activation operand is [x_hi | x_lo | x_hi]),
+// so one bf16 GEMM over 3I computes x_hi W_hi + x_lo W_hi + x_hi W_lo. j.n counts the dst elements.
+F3_DEV void prep_x3cat(const PrepJob& j, int e) {
+  const bool tr = j.type == PREP_PACK_CONV_T;
+  const int J = j.d0, I = j.d1, KT = j.d2;
+  const int inner = tr ? J : I;            // channels per tap of the packed operand
+  const int row = e / (KT * 3 * inner), r = e - row * KT * 3 * inner;
+  const int dt = r / (3 * inner), q = r - dt * 3 * inner, seg = q / inner, c = q - seg * inner;
+  // source weight [J][I][KT]: PACK_CONV row = output channel jj, c = input channel i
+  const float val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
+  const __bf16 hi = (__bf16)val;
+  reinterpret_cast<__bf16*>(j.dst)[e] = seg < 2 ? hi : (__bf16)(val - (float)hi);
+}
+
 __global__ void prep_kernel(PrepTable t) {
   const PrepJob j = t.jobs[blockIdx.y];
   const int stride = gridDim.x * blockDim.x;
+  if (j.bf16 == 3) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) prep_x3cat(j, e);
+    return;
+  }
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) {
     float val = 0.f;
     switch (j.type) {
@@ -1302,9 +1321,14 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
           hb[e] = (__bf16)dh[e];
           lb[e] = (__bf16)(dh[e] - (float)hb[e]);
         }
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off[u]) = hb;
-        if (a.x3)  // split planes (gemm_x3.hip): lo = RNE bf16(dh - hi) one plane further
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + (size_t)a.N * a.TV * C + off[u]) = lb;
+        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated tcn operand), lo = RNE bf16(dh - hi)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dhb) + 3 * (off[u] - c0) + c0;
+          *reinterpret_cast<bf16x4*>(row) = hb;
+          *reinterpret_cast<bf16x4*>(row + C) = lb;
+          *reinterpret_cast<bf16x4*>(row + 2 * C) = hb;
+        } else {
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off[u]) = hb;
+        }
       } else {
         *reinterpret_cast<f32x4*>(a.dh + off[u]) = dh;
       }
@@ -1466,8 +1490,15 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
         l[4 + e] = (__bf16)(u1 - (float)o[4 + e]);
       }
     }
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + qq * 8) = o;
-    if constexpr (X3) *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + total8 * 8 + qq * 8) = l;
+    if constexpr (X3) {  // row [hi | lo | hi] of 3C (the K-concatenated tcn operand)
+      const long long e0 = qq * 8, m = e0 / a.C, c = e0 - m * a.C;
+      __bf16* row = reinterpret_cast<__bf16*>(a.u) + m * 3 * a.C + c;
+      *reinterpret_cast<bf16x8*>(row) = o;
+      *reinterpret_cast<bf16x8*>(row + a.C) = l;
+      *reinterpret_cast<bf16x8*>(row + 2 * a.C) = o;
+    } else {
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + qq * 8) = o;
+    }
   };
   for (; q + (kBnReluU - 1) * step < total8; q += kBnReluU * step) {
     f32x4 x0[kBnReluU], x1[kBnReluU];

@@ -287,6 +287,7 @@ struct LayerWs {
   unsigned short *u = nullptr, *outb = nullptr;
   const unsigned short* xb = nullptr;  // bf16 copy of the block input (RES_CONV blocks)
   float* dWp = nullptr;
+  float* dbx3 = nullptr;  // bf16x3: [2C] tcn bias-gradient scratch of the K-concatenated weight gradient
   // per-layer backward tensors the side stream's weight gradients read (dh: tcn output
   // gradient, dg: gcn output gradient, dres: residual-conv output gradient): never re-used
   // by another layer, so the main stream needs no wait on the side stream before the join
@@ -381,6 +382,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
       if (hb && !wgrad_slab()) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);  // atomic accumulator
+      if (x3) X.dbx3 = A.take<float>((size_t)2 * L.cout);
     }
   }
   if (net.has_sensor && cnn) {
@@ -407,8 +409,8 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.xb = xinb;
       X.z = A.take<float>(Mi * K * Ci);
       X.g = A.take<float>(Mi * C);
-      // u = relu(bn1(g)): bf16 (bf16 mode) or bf16 hi + lo planes (bf16x3 mode)
-      if (hb || x3) X.u = A.take<unsigned short>((x3 ? 2 : 1) * Mi * C);
+      // u = relu(bn1(g)): bf16 (bf16 mode) or rows [hi | lo | hi] of 3C bf16 (bf16x3 mode)
+      if (hb || x3) X.u = A.take<unsigned short>((x3 ? 3 : 1) * Mi * C);
       X.h = A.take<float>(Mo * C);
       if (L.res == RES_CONV) X.r = A.take<float>(Mo * C);
       X.out = A.take<float>(Mo * C);
@@ -417,8 +419,9 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.att = A.take<float>((size_t)N * C);
       X.gw = A.take<float>((size_t)C * K * Ci);
       X.gwT = A.take<float>((size_t)C * K * Ci);
-      X.tw = A.take<float>((size_t)C * 9 * C);
-      X.twT = A.take<float>((size_t)C * 9 * C);
+      // bf16x3: the tcn weights K-concatenated [hi | hi | lo] per tap (3 C 9 C bf16 = 1.5x the fp32 slot)
+      X.tw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
+      X.twT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
       if (L.res == RES_CONV) {
         X.rw = A.take<float>((size_t)C * Ci);
         X.rwT = A.take<float>((size_t)C * Ci);
@@ -429,7 +432,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dbn = A.take<float>((size_t)N * C / 4);
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
-      X.dh = A.take<float>(Mo * C);
+      X.dh = reinterpret_cast<float*>(A.take<unsigned short>(Mo * C * (x3 ? 3 : 2)));  // x3: [hi | lo | hi] rows
       X.dg = A.take<float>(Mi * C);
       X.gpart = A.take<float>((size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       X.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
@@ -443,7 +446,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     }
 
     W.dv = A.take<float>(maxMC);
-    W.slab = A.take<float>(kWgradSlabFloats);
+    W.slab = A.take<float>(kWgradSlabFloats * (x3 ? 4 : 1));  // x3: [2C][9][2C] partials
 
     W.dZ = A.take<float>(maxZ);
     W.dx[0] = A.take<float>(maxMC);
@@ -568,10 +571,12 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
     add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
-    add_job(pt, PREP_PACK_CONV, C * 9 * C, X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, wc);
+    add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
+            wc == 2 ? 3 : wc);  // bf16x3: K-concatenated for the bf16 implicit-GEMM kernels
     if (train) {
       add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
-      add_job(pt, PREP_PACK_CONV_T, C * 9 * C, X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, wc);
+      add_job(pt, PREP_PACK_CONV_T, C * 9 * C * (wc == 2 ? 3 : 1), X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
+              wc == 2 ? 3 : wc);
     }
     if (L.res == RES_CONV) {
       add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, wc);
@@ -645,14 +650,15 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     std::memset(&ta, 0, sizeof(ta));
     ta.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
     ta.w = X.tw; ta.wb = bf(X.tw, wq); ta.out = X.h; ta.outb = bfa(X.h, hb); ta.bias = q.p(L.tcn_b);
-    ta.x3 = x3;
     ta.st_sum = X.bn2.fsum; ta.st_sq = X.bn2.fsq; ta.gap = X.gap;
     if (hb || x3) {  // materialise u = relu(bn1(g)) once (also the tcn wgrad operand): bf16, or
-      // (bf16x3) split into bf16 hi / lo planes, instead of BN + ReLU + split at every tap's staging
+      // (bf16x3) rows [u_hi | u_lo | u_hi] against the packed [W_hi | W_hi | W_lo]: the bf16 LDS-DMA
+      // implicit-GEMM kernels then compute u_hi W_hi + u_lo W_hi + u_hi W_lo over K = 9 x 3C
       BnReluArgs br;
       std::memset(&br, 0, sizeof(br));
       br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = hb; br.x3 = x3;
       F3_TRY(f3_bnrelu_bf16(&br, s));
+      if (x3) ta.g = geom(Mo, C, 3 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, C);
       ta.inb = X.u; ta.zero = w.zero;
       F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
     } else {
@@ -771,7 +777,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     std::memset(&td, 0, sizeof(td));
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
     td.in = (hb || x3) ? nullptr : dh; td.inb = bfa(dh, hb || x3); td.zero = w.zero;
-    td.w = X.twT; td.wb = bf(X.twT, wq); td.x3 = x3; td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    td.w = X.twT; td.wb = bf(X.twT, wq); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
+    if (x3) td.g = geom(Mi, C, 3 * C, 9, L.stride, 4, 1, Ti, To, V, 3 * C, C);  // K-concatenated dh rows
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     if (part & 1) F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
@@ -841,8 +848,14 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
-    } else if (x3) {  // dh and u as split planes (block_bwd_apply / bnrelu wrote them)
-      tw.dyb = bfa(dh, 1); tw.inb = X.u;
+    } else if (x3) {  // [dh_hi | dh_lo] x [u_hi | u_lo] (the first 2C of the 3C rows) on the bf16 kernels;
+      // the slab reduce keeps the hi*hi + hi*lo + lo*hi quadrants (and folds the bias scratch)
+      tw.x3 = 0; tw.bf16 = 1;
+      tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, 2 * C);
+      tw.ldy = 3 * C; tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
+      tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats * 4; tw.dw_ref = q.g(L.tcn_w);
+      tw.x3fold = 1; tw.db = X.dbx3; tw.db_fold = q.g(L.tcn_b);
+      if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;

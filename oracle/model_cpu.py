@@ -560,7 +560,7 @@ def train_step(st, spec, skel, sensor, label, lr=1e-3, sq=None, storage="fp32"):
     return out.detach(), loss.detach(), grads
 
 
-def gradient_sensitivity(st, spec, skel, sensor, label, eps=1e-6, trials=3, per_param=False):
+def gradient_sensitivity(st, spec, skel, sensor, label, eps=1e-6, trials=3, per_param=False, base=None):
     """Conditioning probe (test infrastructure): max normalised change of any gradient
     when every BatchNorm / pooling output is perturbed by relative noise `eps` (fp64).
 
@@ -569,6 +569,7 @@ def gradient_sensitivity(st, spec, skel, sensor, label, eps=1e-6, trials=3, per_
     perturbation can flip one and move whole gradients by 1e-2..1e-1. Gradient parity is
     only meaningful on cases where this probe is small; golden seeds are chosen so.
     Biases that feed a train-mode BN have a zero true gradient and are skipped.
+    base: the unperturbed fp64 gradients if the caller already has them (saves one run).
     """
     st64 = {k: (v.double() if v.dtype == torch.float32 else v.clone()) for k, v in st.items()}
     args = [None if x is None else x.double() for x in (skel, sensor, label)]
@@ -588,7 +589,7 @@ def gradient_sensitivity(st, spec, skel, sensor, label, eps=1e-6, trials=3, per_
         finally:
             F.batch_norm, F.adaptive_avg_pool2d = orig_bn, orig_pool
 
-    base = run(-1)
+    base = run(-1) if base is None else base
     env = {}
     for t in range(trials):
         g = run(1000 + t)
