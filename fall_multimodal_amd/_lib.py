@@ -19,9 +19,10 @@ EXPORTS = (
     "f3_net_create", "f3_net_destroy", "f3_net_num_entries", "f3_net_entry", "f3_net_param_count",
     "f3_net_buffer_count", "f3_net_counter_count", "f3_net_workspace_bytes", "f3_net_forward",
     "f3_net_loss", "f3_net_backward", "f3_rmsprop_step", "f3_conv_forward", "f3_status_string",
-    "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_graph_mix_forward",
+    "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_split_x3cat",
+    "f3_conv_forward_x3cat", "f3_conv_backward_data_x3cat", "f3_conv_backward_weight_x3cat", "f3_graph_mix_forward",
     "f3_graph_mix_backward", "f3_graph_mix_forward_ex", "f3_graph_mix_backward_ex", "f3_net_backward_phase",
-    "f3_net_grad_split", "f3_net_wait_phase1",
+    "f3_net_grad_split", "f3_net_wait_phase1", "f3_net_backward_rmsprop",
     "f3_targcn_create", "f3_targcn_destroy", "f3_targcn_num_entries", "f3_targcn_entry", "f3_targcn_param_count",
     "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_targcn_stage_times", "f3_targcn_status", "f3_net_sensor_times", "f3_soft_ce",
     "f3_sktr_create", "f3_sktr_destroy", "f3_sktr_num_entries", "f3_sktr_entry", "f3_sktr_param_count",
@@ -81,6 +82,7 @@ def lib():
         "f3_net_backward_phase": (I, [P, I, P, P, P, P, I, P]),
         "f3_net_grad_split": (I64, [P]),
         "f3_net_wait_phase1": (I, [P, P]),
+        "f3_net_backward_rmsprop": (I, [P, I, P, P, P, P, P, F, F, F, P]),
         "f3_rmsprop_step": (I, [P, P, P, I64, F, F, F, F, P]),
         "f3_conv_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_status_string": (ctypes.c_char_p, [I]),
@@ -88,6 +90,10 @@ def lib():
         "f3_conv_backward_data": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_conv_backward_weight": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_conv_wgrad_packed": (I, [P, P, P, ctypes.c_longlong, I, I, I, I, I, I, I, I, P]),
+        "f3_split_x3cat": (I, [P, P, ctypes.c_int64, I, P]),
+        "f3_conv_forward_x3cat": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_backward_data_x3cat": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_backward_weight_x3cat": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
         "f3_graph_mix_forward_ex": (I, [P, P, P, I, I, I, I, I, P]),

@@ -1418,7 +1418,7 @@ static int launch_wgrad_seg(WgradArgs a, int nks, hipStream_t s) {
 // workgroup 0 also folds the [2C] bias-gradient scratch. One thread per (j, dt, i): slab reads are
 // contiguous in i.
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_x3_kernel(const float* __restrict__ slab, int splits, int Nc2,
-                                                                   int Kc2, int KT, float* __restrict__ dw_ref,
+                                                                   int Kc2, int KT, int gcn_cin, float* __restrict__ dw_ref,
                                                                    const float* __restrict__ dbs, float* db) {
   const int C = Nc2 / 2, Ci = Kc2 / 2;
   const long long per = (long long)Nc2 * KT * Kc2;
@@ -1430,7 +1430,12 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_x3_kernel(const float* 
     const float* p1 = slab + (size_t)(C + j) * KT * Kc2 + (size_t)dt * Kc2 + i;
     float v = 0.f;
     for (int sp = 0; sp < splits; ++sp) v += p0[sp * per] + p0[sp * per + Ci] + p1[sp * per];
-    dw_ref[((size_t)j * Ci + i) * KT + dt] += v;
+    if (gcn_cin > 0) {  // gcn reference layout [K*C][gcn_cin]
+      const int k = i / gcn_cin, ci = i - k * gcn_cin;
+      dw_ref[((size_t)k * C + j) * gcn_cin + ci] += v;
+    } else {
+      dw_ref[((size_t)j * Ci + i) * KT + dt] += v;
+    }
   }
   if (blockIdx.x == 0 && db && dbs)
     for (int c = threadIdx.x; c < C; c += 256) db[c] += dbs[c] + dbs[C + c];
@@ -1440,7 +1445,7 @@ static int launch_fold_x3(const WgradArgs& a, int splits, hipStream_t s) {
   const long long n = (long long)(a.g.Nc / 2) * a.g.KT * (a.g.Kc / 2);
   const int grid = (int)std::min<long long>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(wgrad_slab_reduce_x3_kernel, dim3(grid), dim3(256), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
-                     a.g.KT, a.dw_ref, a.db, a.db_fold);
+                     a.g.KT, a.gcn_cin, a.dw_ref, a.db, a.db_fold);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -1505,8 +1510,10 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const WgradArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
-  if (a.x3fold && (!a.slab || !a.dw_ref || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.Nc % 2 || a.g.Kc % 2))
+  // (x3fold with dw_ref == null: the GEMM alone at the step's split count, partials left in the slab)
+  if (a.x3fold && (!a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.Nc % 2 || a.g.Kc % 2))
     return F3_EINVAL;
+  if (a.x3fold && a.gcn_cin > 0 && (a.g.KT != 1 || (a.g.Kc / 2) % a.gcn_cin)) return F3_EINVAL;
   // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
   static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
   const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only

@@ -150,9 +150,46 @@ __global__ void rmsprop_kernel(float* __restrict__ p, float* __restrict__ sq, co
   }
 }
 
+__global__ void rmsprop_ranges_kernel(float* __restrict__ p, float* __restrict__ sq, const float* __restrict__ g,
+                                      RmsRanges r, long long n4, float lr, float alpha, float eps, float scale) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    long long k = i, base = 0;
+    int j = 0;
+    for (; j < r.n - 1 && k >= r.len[j] / 4; ++j) k -= r.len[j] / 4;
+    base = r.lo[j] / 4 + k;
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[base] * scale;
+    f32x4 sv = reinterpret_cast<f32x4*>(sq)[base];
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[base];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sv[e] = alpha * sv[e] + (1.f - alpha) * gv[e] * gv[e];
+      pv[e] -= lr * gv[e] / (sqrtf(sv[e]) + eps);
+    }
+    reinterpret_cast<f32x4*>(sq)[base] = sv;
+    reinterpret_cast<f32x4*>(p)[base] = pv;
+  }
+}
+
 }  // namespace f3
 
 using namespace f3;
+
+int f3_rmsprop_ranges(float* p, float* sq, const float* g, const RmsRanges& r, float lr, float alpha, float eps,
+                      float scale, hipStream_t s) {
+  if (r.n < 0 || r.n > kRmsRanges) return F3_EINVAL;
+  long long n4 = 0;
+  for (int j = 0; j < r.n; ++j) {
+    if (r.lo[j] % 4 || r.len[j] % 4 || r.len[j] < 0) return F3_EINVAL;
+    n4 += r.len[j] / 4;
+  }
+  if (n4 == 0) return F3_OK;
+  const long long blocks = (n4 + 255) / 256;
+  const int grid = (int)(blocks < 4096 ? blocks : 4096);
+  hipLaunchKernelGGL(rmsprop_ranges_kernel, dim3(grid), dim3(256), 0, s, p, sq, g, r, n4, lr, alpha, eps, scale);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
 
 int f3_head_fwd(const HeadArgs* a, hipStream_t s) {
   if (a->C > 64) return F3_EINVAL;

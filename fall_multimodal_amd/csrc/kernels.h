@@ -80,7 +80,9 @@ struct WgradArgs {
   int x3;                     // 1: split-bf16 kernel on fp32 dy / in (gemm_x3.hip)
   // bf16x3 mode on the bf16 kernels (K-concatenated operands): the GEMM ran on dY' = [dY_hi | dY_lo]
   // (Nc = 2C) and X' = [X_hi | X_lo] (Kc = 2Ci); the slab reduce adds the hh + hl + lh quadrants
-  // into dw_ref [C][Ci][KT], and db (a [2C] scratch here) is folded into db_fold[c] += db[c] + db[C+c]
+  // into dw_ref [C][Ci][KT], and db (a [2C] scratch here) is folded into db_fold[c] += db[c] + db[C+c].
+  // With gcn_cin > 0 (KT = 1, Ci = K gcn_cin) dw_ref is the gcn weight's reference layout
+  // [K*C][gcn_cin] instead (column k gcn_cin + ci of the packed operand -> row k C + c).
   int x3fold;
   float* db_fold;
 };

@@ -10,6 +10,7 @@
 #include "layers.h"
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 namespace f3 {
@@ -20,17 +21,27 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // ----------------------------------------------------------------------------
 // prep: A_eff = A * E, gcn bias through the graph, weight packing  (one launch)
 // ----------------------------------------------------------------------------
-// bf16x3 on the bf16 kernels (prep code 3, PACK_CONV / PACK_CONV_T): every tap's k range is
-// tripled to [W_hi | W_hi | W_lo] (dst [J][KT][3I]; the activation operand is [x_hi | x_lo | x_hi]),
-// so one bf16 GEMM over 3I computes x_hi W_hi + x_lo W_hi + x_hi W_lo. j.n counts the dst elements.
+// bf16x3 on the bf16 kernels (prep code 3): every tap's k range is tripled to [W_hi | W_hi | W_lo]
+// (dst [rows][KT][3 inner]; the activation operand is [x_hi | x_lo | x_hi]), so one bf16 GEMM over
+// 3 inner computes x_hi W_hi + x_lo W_hi + x_hi W_lo. j.n counts the dst elements.
+//   PACK_CONV    src [J][I][KT]   -> dst [J][KT][3I]        (d0 J, d1 I, d2 KT)
+//   PACK_CONV_T  src [J][I][KT]   -> dst [I][KT][3J]
+//   PACK_GCN     src [K*C][Cin]   -> dst [C][3 K Cin]       (d0 C, d1 Cin, d2 K; one "tap")
+//   PACK_GCN_T   src [K*C][Cin]   -> dst [K Cin][3C]
 F3_DEV void prep_x3cat(const PrepJob& j, int e) {
-  const bool tr = j.type == PREP_PACK_CONV_T;
-  const int J = j.d0, I = j.d1, KT = j.d2;
-  const int inner = tr ? J : I;            // channels per tap of the packed operand
+  const bool gcn = j.type == PREP_PACK_GCN || j.type == PREP_PACK_GCN_T;
+  const bool tr = j.type == PREP_PACK_CONV_T || j.type == PREP_PACK_GCN_T;
+  const int J = j.d0, I = j.d1, KT = gcn ? 1 : j.d2;
+  const int inner = gcn ? (tr ? J : j.d2 * I) : (tr ? J : I);  // channels per tap of the packed operand
   const int row = e / (KT * 3 * inner), r = e - row * KT * 3 * inner;
   const int dt = r / (3 * inner), q = r - dt * 3 * inner, seg = q / inner, c = q - seg * inner;
-  // source weight [J][I][KT]: PACK_CONV row = output channel jj, c = input channel i
-  const float val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
+  float val;
+  if (gcn) {  // W[k*C + c][ci]: (k, ci) from the packed row (transposed) or column
+    const int kc = tr ? row : c, cc = tr ? c : row, k = kc / I, ci = kc - k * I;
+    val = j.s0[((size_t)k * J + cc) * I + ci];
+  } else {  // source weight [J][I][KT]: PACK_CONV row = output channel jj, c = input channel i
+    val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
+  }
   const __bf16 hi = (__bf16)val;
   reinterpret_cast<__bf16*>(j.dst)[e] = seg < 2 ? hi : (__bf16)(val - (float)hi);
 }
@@ -930,7 +941,24 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
         const int wk = 16 * nt + fr;
         const f32x4 acc = mfma_x3m(xah, xal, bhi[nt], blo[nt], f32x4{0.f, 0.f, 0.f, 0.f});
         // lane holds Z[wk][c = 16 mt + 4 fg + r], r = 0..3: one 16-B piece of row wk
-        if (wk < KV) *reinterpret_cast<f32x4*>(zf + (size_t)wk * CIN + 16 * mt + 4 * fg) = acc;
+        if (wk < KV) {
+          if (a.z3) {  // GEMM row (f, w = wk / K) of [hi | lo | hi] over 3 K Cin, column k Cin + c
+            const int w = wk / K, k = wk - w * K;
+            char* row = reinterpret_cast<char*>(a.z3) +
+                        2 * (((size_t)f * V + w) * 3 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg);
+            bf16x4 h, l;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              h[e] = (__bf16)acc[e];
+              l[e] = (__bf16)(acc[e] - (float)h[e]);
+            }
+            *reinterpret_cast<bf16x4*>(row) = h;
+            *reinterpret_cast<bf16x4*>(row + 2 * K * CIN) = l;
+            *reinterpret_cast<bf16x4*>(row + 4 * K * CIN) = h;
+          } else {
+            *reinterpret_cast<f32x4*>(zf + (size_t)wk * CIN + 16 * mt + 4 * fg) = acc;
+          }
+        }
       }
     }
   }
@@ -1167,10 +1195,20 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
       }
       st_act4<A16>(a.out, off[u], o);
       if (a.outb) {
-        bf16x4 ob;
+        bf16x4 ob, lb;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off[u]) = ob;
+        for (int e = 0; e < 4; ++e) {
+          ob[e] = (__bf16)o[e];
+          lb[e] = (__bf16)(o[e] - (float)ob[e]);
+        }
+        if (a.x3) {  // row [hi | lo | hi] of 3C: the next block's K-concatenated residual-conv operand
+          __bf16* row = reinterpret_cast<__bf16*>(a.outb) + 3 * (off[u] - c0) + c0;
+          *reinterpret_cast<bf16x4*>(row) = ob;
+          *reinterpret_cast<bf16x4*>(row + C) = lb;
+          *reinterpret_cast<bf16x4*>(row + 2 * C) = ob;
+        } else {
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off[u]) = ob;
+        }
       }
       if (mb + u * RP < r1) pool += o;
     }
@@ -1333,10 +1371,20 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
         *reinterpret_cast<f32x4*>(a.dh + off[u]) = dh;
       }
       if (RES == RES_CONV && a.dresb) {
-        bf16x4 rb;
+        bf16x4 rb, rl;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) rb[e] = (__bf16)dr[e];
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off[u]) = rb;
+        for (int e = 0; e < 4; ++e) {
+          rb[e] = (__bf16)dr[e];
+          rl[e] = (__bf16)(dr[e] - (float)rb[e]);
+        }
+        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated residual dgrad / wgrad operand)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dresb) + 3 * (off[u] - c0) + c0;
+          *reinterpret_cast<bf16x4*>(row) = rb;
+          *reinterpret_cast<bf16x4*>(row + C) = rl;
+          *reinterpret_cast<bf16x4*>(row + 2 * C) = rb;
+        } else {
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off[u]) = rb;
+        }
       } else if (RES != RES_NONE) {
         *reinterpret_cast<f32x4*>(a.dres + off[u]) = dr;
       }
@@ -1427,10 +1475,20 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
         if (live) acc[e] += o[e];
       }
       if (a.dgb) {
-        bf16x8 ob;
+        bf16x8 ob, lb;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ob[e] = (__bf16)o[e];
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
+        for (int e = 0; e < 8; ++e) {
+          ob[e] = (__bf16)o[e];
+          lb[e] = (__bf16)(o[e] - (float)ob[e]);
+        }
+        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated gcn dgrad / wgrad operand)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dgb) + 3 * (off - c0) + c0;
+          *reinterpret_cast<bf16x8*>(row) = ob;
+          *reinterpret_cast<bf16x8*>(row + C) = lb;
+          *reinterpret_cast<bf16x8*>(row + 2 * C) = ob;
+        } else {
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
+        }
       } else {
         *reinterpret_cast<f32x4*>(a.dg + off) = f32x4{o[0], o[1], o[2], o[3]};
         *reinterpret_cast<f32x4*>(a.dg + off + 4) = f32x4{o[4], o[5], o[6], o[7]};
@@ -2006,7 +2064,46 @@ static bool mix_x3_ok(const MixArgs& a) {
          a.V <= 32;
 }
 
+// bf16x3 K-concatenated operand rows: out[r] = [hi | lo | hi] of x[r] (3C bf16), hi = RNE bf16(x),
+// lo = RNE bf16(x - hi). One thread per 4 channels: a 16-B read, three 8-B writes.
+__global__ __launch_bounds__(256) void split_x3cat_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
+                                                          long long n4, int C4) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const long long r = i / C4;
+    const int c = (int)(i - r * C4) * 4, C = C4 * 4;
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    bf16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h[e] = (__bf16)v[e];
+      l[e] = (__bf16)(v[e] - (float)h[e]);
+    }
+    __bf16* row = out + r * 3 * C + c;
+    *reinterpret_cast<bf16x4*>(row) = h;
+    *reinterpret_cast<bf16x4*>(row + C) = l;
+    *reinterpret_cast<bf16x4*>(row + 2 * C) = h;
+  }
+}
+
+int f3_split_x3(const float* x, unsigned short* out, long long rows, int C, hipStream_t s) {
+  if (C % 4 || rows < 0) return F3_EINVAL;
+  const long long n4 = rows * (C / 4);
+  if (n4 == 0) return F3_OK;
+  const int grid = (int)std::min<long long>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(split_x3cat_kernel, dim3(grid), dim3(256), 0, s, x, reinterpret_cast<__bf16*>(out), n4, C / 4);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+bool f3_mix_x3_ok(int K, int V, int Cin) {
+  MixArgs m;
+  std::memset(&m, 0, sizeof(m));
+  m.K = K; m.V = V; m.Cin = Cin; m.x3 = 1;
+  return mix_x3_ok(m);
+}
+
 int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
+  if (a->z3 && !(a->x3 && mix_x3_ok(*a))) return F3_EINVAL;  // (only the split-bf16 kernel writes z3)
   if (a->x3 && mix_x3_ok(*a)) {  // (the first block's Cin = 2 / 3 mix stays on the fp32 kernels)
     if (a->frames <= 0) return F3_OK;
     return a->Cin == 64 ? launch_mix_fwd_x3<64>(a, s) : a->Cin == 128 ? launch_mix_fwd_x3<128>(a, s)

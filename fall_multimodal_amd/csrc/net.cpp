@@ -9,6 +9,7 @@
 // pure function of the batch size.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -287,7 +288,8 @@ struct LayerWs {
   unsigned short *u = nullptr, *outb = nullptr;
   const unsigned short* xb = nullptr;  // bf16 copy of the block input (RES_CONV blocks)
   float* dWp = nullptr;
-  float* dbx3 = nullptr;  // bf16x3: [2C] tcn bias-gradient scratch of the K-concatenated weight gradient
+  float* dbx3 = nullptr;   // bf16x3: [2C] tcn bias-gradient scratch of the K-concatenated weight gradient
+  float* dbx3r = nullptr;  // bf16x3: the same for the residual conv
   // per-layer backward tensors the side stream's weight gradients read (dh: tcn output
   // gradient, dg: gcn output gradient, dres: residual-conv output gradient): never re-used
   // by another layer, so the main stream needs no wait on the side stream before the join
@@ -383,6 +385,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dAeff = A.take<float>((size_t)K * V * V);
       if (hb && !wgrad_slab()) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);  // atomic accumulator
       if (x3) X.dbx3 = A.take<float>((size_t)2 * L.cout);
+      if (x3 && L.res == RES_CONV) X.dbx3r = A.take<float>((size_t)2 * L.cout);
     }
   }
   if (net.has_sensor && cnn) {
@@ -405,9 +408,12 @@ Ws plan(const f3_net& net, int N, char* base) {
       LayerWs& X = W.L[l];
       const size_t Mi = (size_t)N * L.T_in * V, Mo = (size_t)N * L.T_out * V;
       const int C = L.cout, Ci = L.cin;
+      // bf16x3 with the split-bf16 graph mix (Ci = 64 / 128 / 256): the gcn GEMM operands Z and dg
+      // as rows [hi | lo | hi] of 3 K Ci / 3C bf16 (1.5x the fp32 slot), the packed weights K-concatenated
+      const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);
       X.x = xin;
       X.xb = xinb;
-      X.z = A.take<float>(Mi * K * Ci);
+      X.z = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mi * K * Ci)) : A.take<float>(Mi * K * Ci);
       X.g = A.take<float>(Mi * C);
       // u = relu(bn1(g)): bf16 (bf16 mode) or rows [hi | lo | hi] of 3C bf16 (bf16x3 mode)
       if (hb || x3) X.u = A.take<unsigned short>((x3 ? 3 : 1) * Mi * C);
@@ -417,14 +423,14 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.q1 = A.take<float>((size_t)N * C / 4);
       X.hid = A.take<float>((size_t)N * C / 4);
       X.att = A.take<float>((size_t)N * C);
-      X.gw = A.take<float>((size_t)C * K * Ci);
-      X.gwT = A.take<float>((size_t)C * K * Ci);
+      X.gw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * (gcat ? 3 : 2)));
+      X.gwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * (gcat ? 3 : 2)));
       // bf16x3: the tcn weights K-concatenated [hi | hi | lo] per tap (3 C 9 C bf16 = 1.5x the fp32 slot)
       X.tw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
       X.twT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
-      if (L.res == RES_CONV) {
-        X.rw = A.take<float>((size_t)C * Ci);
-        X.rwT = A.take<float>((size_t)C * Ci);
+      if (L.res == RES_CONV) {  // (bf16x3: K-concatenated, 3 C Ci bf16)
+        X.rw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * (x3 ? 3 : 2)));
+        X.rwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * (x3 ? 3 : 2)));
       }
       X.aeff = A.take<float>((size_t)K * V * V);
       X.beff = A.take<float>((size_t)V * C);
@@ -433,13 +439,16 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
       X.dh = reinterpret_cast<float*>(A.take<unsigned short>(Mo * C * (x3 ? 3 : 2)));  // x3: [hi | lo | hi] rows
-      X.dg = A.take<float>(Mi * C);
+      X.dg = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mi * C)) : A.take<float>(Mi * C);
       X.gpart = A.take<float>((size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       X.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
-      if (L.res == RES_CONV) X.dres = A.take<float>(Mo * C);
+      // (bf16x3: dres as rows [hi | lo | hi] of 3C bf16)
+      if (L.res == RES_CONV) X.dres = x3 ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mo * C)) : A.take<float>(Mo * C);
       xin = X.out;
-      // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand)
+      // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand);
+      // bf16x3: a [hi | lo | hi] copy of it when the next block has a residual conv
       xinb = hb ? reinterpret_cast<const unsigned short*>(X.out) : nullptr;
+      if (x3 && l < 6 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(3 * Mo * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
@@ -492,6 +501,11 @@ struct Ptrs {
   float* B;
   int64_t* C;
   float* G;
+  // f3_net_backward_rmsprop: RMSprop(lr, alpha, eps) on params / square_avg, each skeleton layer's
+  // range issued on the queue that finishes its gradients (opt_p == null: no fused update)
+  float* opt_p = nullptr;
+  float* opt_sq = nullptr;
+  float lr = 0.f, alpha = 0.f, eps = 0.f;
   const float* p(int i) const { return P + net.entries[i].offset; }
   float* g(int i) const { return G + net.entries[i].offset; }
   float* b(int i) const { return B + net.entries[i].offset; }
@@ -570,17 +584,21 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     const int C = L.cout, Ci = L.cin;
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
-    add_job(pt, PREP_PACK_GCN, C * K * Ci, X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
+    // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
+    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : wc;
+    add_job(pt, PREP_PACK_GCN, C * K * Ci * (gc == 3 ? 3 : 1), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
     add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
             wc == 2 ? 3 : wc);  // bf16x3: K-concatenated for the bf16 implicit-GEMM kernels
     if (train) {
-      add_job(pt, PREP_PACK_GCN_T, C * K * Ci, X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, wc);
+      add_job(pt, PREP_PACK_GCN_T, C * K * Ci * (gc == 3 ? 3 : 1), X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
       add_job(pt, PREP_PACK_CONV_T, C * 9 * C * (wc == 2 ? 3 : 1), X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
               wc == 2 ? 3 : wc);
     }
     if (L.res == RES_CONV) {
-      add_job(pt, PREP_PACK_CONV, C * Ci, X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, wc);
-      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci, X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, wc);
+      const int rc = wc == 2 ? 3 : wc;  // bf16x3: K-concatenated
+      add_job(pt, PREP_PACK_CONV, C * Ci * (rc == 3 ? 3 : 1), X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, rc);
+      if (train)
+        add_job(pt, PREP_PACK_CONV_T, C * Ci * (rc == 3 ? 3 : 1), X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, rc);
     }
   }
   F3_TRY(f3_prep(pt, s));
@@ -626,6 +644,8 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       std::memset(&mx, 0, sizeof(mx));
       mx.K = K; mx.V = V; mx.Cin = Ci; mx.frames = N * Ti; mx.A = X.aeff; mx.x = X.x; mx.z = X.z;
       mx.zb = bfa(X.z, hb); mx.x16 = hb; mx.x3 = x3;
+      const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);
+      mx.z3 = bfa(X.z, gcat);
       F3_TRY(f3_mix_fwd(&mx, s));
       ConvGemmArgs ga;
       std::memset(&ga, 0, sizeof(ga));
@@ -633,6 +653,10 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
       ga.w = X.gw; ga.wb = bf(X.gw, wq); ga.out = X.g; ga.outb = bfa(X.g, hb); ga.x3 = x3;
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
+      if (gcat) {  // [Z_hi | Z_lo | Z_hi] x [W_hi | W_hi | W_lo] over 3 K Ci on the bf16 kernels
+        ga.x3 = 0; ga.in = nullptr; ga.inb = bfa(X.z, 1);
+        ga.g = geom(Mi, C, 3 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, C);
+      }
       F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     }
     if (L.res == RES_CONV) {  // residual conv (stgcan.py:128-131)
@@ -643,6 +667,11 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       if (hb && !X.xb) return F3_ESTATE;
       ra.w = X.rw; ra.wb = bf(X.rw, wq); ra.out = X.r; ra.outb = bfa(X.r, hb); ra.x3 = x3;
       ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
+      if (x3) {  // the previous block's [x_hi | x_lo | x_hi] copy against [W_hi | W_hi | W_lo]
+        if (!X.xb) return F3_ESTATE;
+        ra.x3 = 0; ra.in = nullptr; ra.inb = X.xb;
+        ra.g = geom(Mo, C, 3 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, C);
+      }
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
     // tcn: BN1 + ReLU prologue, (9,1) conv, bias, BN2 stats + channel-attention pool epilogue
@@ -680,6 +709,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.pool = l == 6 ? W.pool : nullptr;
     ba.act16 = hb;
+    if (x3 && X.outb) { ba.outb = X.outb; ba.x3 = 1; }
     F3_TRY(f3_block_out(ba, s));
     if (train) {
       add_bnrun(run, q, L.bn1, X.bn1.fsum, X.bn1.fsq, Mi);
@@ -689,6 +719,20 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     }
   }
   return F3_OK;
+}
+
+// The flat-parameter ranges of one skeleton layer: [gcn.conv.weight .. channel_attention ... 4.bias]
+// (contiguous: entries are laid out in creation order within a phase group, 16-B aligned) and its
+// edge_importance entry (created after the stream's layers).
+RmsRanges layer_ranges(const f3_net& n, const LayerIdx& L) {
+  RmsRanges r;
+  r.n = 2;
+  const Entry &a = n.entries[L.gcn_w], &b = n.entries[L.ca_b2], &e = n.entries[L.edge];
+  r.lo[0] = a.offset;
+  r.len[0] = b.offset + (b.numel + 3) / 4 * 4 - a.offset;
+  r.lo[1] = e.offset;
+  r.len[1] = (e.numel + 3) / 4 * 4;
+  return r;
 }
 
 // debugging aid: F3_DEBUG_BWD_STOP="stream,layer" ends the backward right after that
@@ -747,7 +791,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.dres = L.res == RES_CONV ? dres : (L.res == RES_ID ? dx : nullptr);
     ba.dhb = bfa(dh, hb || x3);  // bf16x3: dh as split hi / lo planes (the tcn dgrad / wgrad operand)
     ba.x3 = x3;
-    ba.dresb = L.res == RES_CONV ? bfa(dres, hb) : nullptr;
+    ba.dresb = L.res == RES_CONV ? bfa(dres, hb || x3) : nullptr;  // bf16x3: [hi | lo | hi] rows
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
@@ -788,6 +832,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = dg; bb.G = X.G;
     bb.Gpart = X.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb; bb.no_colsum = split;
+    const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);  // dg as [hi | lo | hi] rows (see plan)
+    if (gcat) { bb.dgb = bfa(dg, 1); bb.x3 = 1; }
     if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
     const bool g0 = hb && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
@@ -808,6 +854,10 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
+    if (gcat) {  // [dg_hi | dg_lo | dg_hi] x [W^T_hi | W^T_hi | W^T_lo] over 3C
+      gd.x3 = 0; gd.in = nullptr; gd.inb = bfa(dg, 1);
+      gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 3 * C, K * Ci);
+    }
     const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
       if (!f3_igemm_ok(gd)) return F3_EINVAL;
@@ -827,6 +877,10 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
       rd.in = hb ? nullptr : dres; rd.inb = bfa(dres, hb); rd.zero = w.zero;
       rd.w = X.rwT; rd.wb = bf(X.rwT, wq); rd.x3 = x3; rd.out = dx;
+      if (x3) {  // K-concatenated over 3C
+        rd.x3 = 0; rd.in = nullptr; rd.inb = bfa(dres, 1);
+        rd.g = geom(Mi, Ci, 3 * C, 1, L.stride, 0, 1, Ti, To, V, 3 * C, Ci);
+      }
       if (part & 1) F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
     }
     // ---- side stream: this layer's weight gradients ----
@@ -870,6 +924,13 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (hb) {
         rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
+      } else if (x3) {  // [dr_hi | dr_lo] x [x_hi | x_lo] quadrants, folded like the tcn's
+        rw.x3 = 0; rw.bf16 = 1;
+        rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, 2 * C);
+        rw.ldy = 3 * C; rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+        rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats * 4; rw.dw_ref = q.g(L.res_w);
+        rw.x3fold = 1; rw.db = X.dbx3r; rw.db_fold = q.g(L.res_b);
+        if (!f3_wgrad_glds_ok(rw)) return F3_EINVAL;
       } else {
         rw.dy = dres; rw.in = X.x;
       }
@@ -896,11 +957,23 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
+    if (gcat) {  // [dg_hi | dg_lo] x [Z_hi | Z_lo] quadrants into the slab, folded to the gcn layout
+      gw.x3 = 0; gw.bf16 = 1; gw.outmap = WG_OUT_CONV;
+      gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, 2 * C);
+      gw.ldy = 3 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
+      gw.slab = W.slab; gw.slab_cap = kWgradSlabFloats * 4; gw.dw_ref = q.g(L.gcn_w); gw.dw = nullptr;
+      gw.x3fold = 1;
+      if (!f3_wgrad_glds_ok(gw)) return F3_EINVAL;
+    }
     if ((part & 2) && !g0) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
     GcnBiasBwdArgs gb;
     gb.K = K; gb.V = V; gb.C = C; gb.Aeff = X.aeff; gb.A = W.A; gb.G = X.G; gb.bias = q.p(L.gcn_b);
     gb.db = q.g(L.gcn_b); gb.dAeff = X.dAeff; gb.dE = q.g(L.edge);
     if (part & 2) F3_TRY(f3_gcn_bias_bwd(&gb, ss));
+    // fused optimizer: every gradient of this layer is final here on ss (its main-chain parts were
+    // waited for through ev_main), and nothing later in the backward reads these parameters
+    if (q.opt_p && (part & 2))
+      F3_TRY(f3_rmsprop_ranges(q.opt_p, q.opt_sq, q.G, layer_ranges(net, L), q.lr, q.alpha, q.eps, 1.f, ss));
     dout = dx;
     pp ^= 1;
   }
@@ -1297,13 +1370,100 @@ int f3_net_backward(f3_net* net, int N, const float* params, const float* dout, 
 
 int64_t f3_net_grad_split(const f3_net* net) { return net ? net->nparam_phase1 : 0; }
 
+}  // extern "C"
+
+namespace {
+struct FusedOpt {
+  float *p, *sq;
+  float lr, alpha, eps;
+};
+
+int net_backward(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace, int phase,
+                 void* stream, const FusedOpt* opt);
+
+// the skeleton layers' ranges cover exactly their own parameter entries (the fused optimizer's
+// per-layer launches rely on it; checked once per call, ~300 entries)
+bool layer_ranges_ok(const f3_net& n) {
+  for (int si = 0; si < n.nstreams; ++si)
+    for (int l = 0; l < 7; ++l) {
+      const LayerIdx& L = n.st[si].L[l];
+      const RmsRanges r = layer_ranges(n, L);
+      long long sum = 0;
+      for (int i = L.gcn_w; i <= L.ca_b2; ++i) {
+        const Entry& e = n.entries[i];
+        if (e.kind != F3_ENTRY_PARAM) continue;
+        if (e.offset < r.lo[0] || e.offset >= r.lo[0] + r.len[0]) return false;
+        sum += (e.numel + 3) / 4 * 4;
+      }
+      if (sum != r.len[0]) return false;
+    }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int f3_net_backward_rmsprop(f3_net* net, int N, float* params, const float* dout, float* grads, float* square_avg,
+                            void* workspace, float lr, float alpha, float eps, void* stream) {
+  if (!net || !params || !square_avg) return F3_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  // bf16 mode with F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers: no per-layer
+  // update then (one launch after the backward, as f3_net_backward + f3_rmsprop_step)
+  const bool fused = !(net->cfg.precision == F3_PRECISION_BF16 && !wgrad_slab()) && layer_ranges_ok(*net);
+  if (!fused) {
+    F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, nullptr));
+    return f3_rmsprop(params, square_avg, grads, net->nparam, lr, alpha, eps, 1.f, s);
+  }
+  const FusedOpt o{params, square_avg, lr, alpha, eps};
+  F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, &o));
+  // every parameter outside the layers' ranges (data_bn, sensor branch, head), after the join
+  std::vector<std::pair<long long, long long>> done, rest;
+  for (int si = 0; si < net->nstreams; ++si)
+    for (int l = 0; l < 7; ++l) {
+      const RmsRanges r = layer_ranges(*net, net->st[si].L[l]);
+      for (int j = 0; j < r.n; ++j) done.push_back({r.lo[j], r.lo[j] + r.len[j]});
+    }
+  for (const Entry& e : net->entries) {
+    if (e.kind != F3_ENTRY_PARAM) continue;
+    bool in = false;
+    for (auto& d : done) in = in || (e.offset >= d.first && e.offset < d.second);
+    if (in) continue;
+    const long long lo = e.offset, hi = e.offset + (e.numel + 3) / 4 * 4;
+    if (!rest.empty() && rest.back().second == lo) rest.back().second = hi;
+    else rest.push_back({lo, hi});
+  }
+  RmsRanges r;
+  r.n = 0;
+  for (size_t i = 0; i < rest.size(); ++i) {
+    r.lo[r.n] = rest[i].first;
+    r.len[r.n] = rest[i].second - rest[i].first;
+    if (++r.n == kRmsRanges || i + 1 == rest.size()) {
+      F3_TRY(f3_rmsprop_ranges(params, square_avg, grads, r, lr, alpha, eps, 1.f, s));
+      r.n = 0;
+    }
+  }
+  return F3_OK;
+}
+
 int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
                           int phase, void* stream) {
+  return net_backward(net, N, params, dout, grads, workspace, phase, stream, nullptr);
+}
+
+}  // extern "C"
+
+namespace {
+int net_backward(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace, int phase,
+                 void* stream, const FusedOpt* opt) {
   if (!net || !params || !grads || !workspace || N < 2 || phase < 0 || phase > 2) return F3_EINVAL;
   if (phase != 2 && !dout) return F3_EINVAL;
+  if (opt && phase != 0) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   Ws w = plan(*net, N, (char*)workspace);
   Ptrs q{*net, params, nullptr, nullptr, grads};
+  if (opt) {
+    q.opt_p = opt->p; q.opt_sq = opt->sq; q.lr = opt->lr; q.alpha = opt->alpha; q.eps = opt->eps;
+  }
   // skeleton streams layer by layer, interleaved (see stream_forward), then each stream's
   // packed weight-gradient unpack
   auto skeleton = [&](Branches& br, int l_hi, int l_lo) -> int {
@@ -1393,6 +1553,9 @@ int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* 
   F3_TRY(br.join());
   return F3_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int f3_net_sensor_times(f3_net* net, int enable, float* ms) {
   if (!net) return F3_EINVAL;
@@ -1517,6 +1680,84 @@ int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void*
   a.bias = bias; a.st_sum = st_sum; a.st_sq = st_sq;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
   return f3_igemm_bf16(&a, epi, (hipStream_t)stream);
+}
+
+// ---- bf16x3 on the bf16 kernels, as the step launches them (K-concatenated operands) ----
+int f3_split_x3cat(const float* x, void* out, int64_t rows, int C, void* stream) {
+  if (!x || !out || rows < 0 || C <= 0 || C % 4) return F3_EINVAL;
+  return f3_split_x3(x, static_cast<unsigned short*>(out), rows, C, (hipStream_t)stream);
+}
+
+static bool x3cat_shape_ok(int N, int T_in, int V, int Cin, int Cout, int KT, int stride, int pad) {
+  return N > 0 && T_in > 0 && V > 0 && Cin > 0 && Cout > 0 && KT > 0 && (stride == 1 || stride == 2) && pad >= 0 &&
+         (T_in + 2 * pad - KT) / stride + 1 > 0 && Cin % 8 == 0 && Cout % 8 == 0;
+}
+
+int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, float* out, void* wpack, int N, int T_in,
+                          int V, int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!x3 || !bias || !out || !wpack || !x3cat_shape_ok(N, T_in, V, Cin, Cout, KT, stride, pad)) return F3_EINVAL;
+  if (w) {  // [Cout][KT][W_hi | W_hi | W_lo] (w == NULL: wpack already packed)
+    PrepTable t;
+    t.n = 0;
+    add_job(t, PREP_PACK_CONV, Cout * KT * Cin * 3, static_cast<float*>(wpack), w, nullptr, nullptr, Cout, Cin, KT, 3);
+    F3_TRY(f3_prep(t, s));
+  }
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, Cout, 3 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, Cout);
+  a.inb = static_cast<const unsigned short*>(x3); a.zero = test_zero_page();
+  a.wb = static_cast<const unsigned short*>(wpack); a.out = out; a.bias = bias;
+  if (!f3_igemm_ok(a)) return F3_EINVAL;
+  return f3_conv_gemm(&a, 0, EPI_BIAS, s);
+}
+
+int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void* wpack, int N, int T_in, int V,
+                                int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!dy3 || !dx || !wpack || !x3cat_shape_ok(N, T_in, V, Cin, Cout, KT, stride, pad)) return F3_EINVAL;
+  if (w) {  // [Cin][KT][W^T_hi | W^T_hi | W^T_lo]
+    PrepTable t;
+    t.n = 0;
+    add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin * 3, static_cast<float*>(wpack), w, nullptr, nullptr, Cout, Cin, KT, 3);
+    F3_TRY(f3_prep(t, s));
+  }
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_in * V, Cin, 3 * Cout, KT, stride, pad, 1, T_in, T_out, V, 3 * Cout, Cin);
+  a.inb = static_cast<const unsigned short*>(dy3); a.zero = test_zero_page();
+  a.wb = static_cast<const unsigned short*>(wpack); a.out = dx;
+  if (!f3_igemm_ok(a)) return F3_EINVAL;
+  return f3_conv_gemm(&a, 0, 0, s);
+}
+
+int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, float* db, int N, int T_in, int V,
+                                  int Cin, int Cout, int KT, int stride, int pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!dy3 || !x3 || !x3cat_shape_ok(N, T_in, V, Cin, Cout, KT, stride, pad)) return F3_EINVAL;
+  const int T_out = (T_in + 2 * pad - KT) / stride + 1;
+  const long long cap = kWgradSlabFloats * 4;  // the step's x3 slab (plan: W.slab)
+  float* slab = test_scratch((size_t)cap + 2 * Cout);
+  if (!slab) return F3_EHIP;
+  WgradArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, 2 * Cout);
+  a.ldy = 3 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1; a.x3fold = 1;
+  a.dyb = static_cast<const unsigned short*>(dy3); a.inb = static_cast<const unsigned short*>(x3);
+  a.zero = test_zero_page(); a.slab = slab; a.slab_cap = cap;
+  if (dw) {  // dw == NULL: the GEMM alone (partials left in the slab)
+    if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
+    a.dw_ref = dw;
+    if (db) {
+      if (hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
+      if (hipMemsetAsync(slab + cap, 0, sizeof(float) * 2 * Cout, s) != hipSuccess) return F3_EHIP;
+      a.db = slab + cap; a.db_fold = db;
+    }
+  }
+  if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
+  return f3_conv_wgrad(&a, 0, s);
 }
 
 int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db, int N, int T_in, int V, int Cin,

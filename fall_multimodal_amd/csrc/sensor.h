@@ -110,5 +110,14 @@ long long f3_cnn1d_part_floats();
 int f3_head_fwd(const f3::HeadArgs* a, hipStream_t s);
 int f3_ce(const f3::HeadArgs* a, hipStream_t s);
 int f3_head_bwd(const f3::HeadArgs* a, hipStream_t s);
+// RMSprop over up to kRmsRanges ranges of one flat buffer in one launch (offsets and lengths in
+// floats, multiples of 4: the entries of the flat parameter layout are 16-B aligned)
+constexpr int kRmsRanges = 8;
+struct RmsRanges {
+  int n;
+  long long lo[kRmsRanges], len[kRmsRanges];
+};
+int f3_rmsprop_ranges(float* p, float* sq, const float* g, const RmsRanges& r, float lr, float alpha, float eps,
+                      float scale, hipStream_t s);
 int f3_rmsprop(float* p, float* sq, const float* g, long long n, float lr, float alpha, float eps, float scale,
                hipStream_t s);

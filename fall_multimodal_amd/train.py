@@ -16,6 +16,7 @@ per-rank (the reference's per-device batch semantics).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -105,6 +106,8 @@ class TrainStep:
             p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
         self.graph = None
         self._static = None
+        # world 1: the RMSprop update per layer inside the backward (F3_FUSED_OPT=0: one launch after it)
+        self.fused_optimizer = self.world == 1 and os.environ.get("F3_FUSED_OPT", "1") != "0"
 
     # -- the pieces ------------------------------------------------------------
     def prepare(self, skel, sensor, label):
@@ -156,6 +159,18 @@ class TrainStep:
                                     self.grads.numel(), self.lr, self.alpha, self.eps, scale, stream_handle()),
               "rmsprop")
 
+    def backward_optimizer_step(self):
+        """loss.backward() + optimizer.step() in one native call (world 1): each skeleton layer's
+        RMSprop update starts on the queue that finishes its gradients (f3_net_backward_rmsprop);
+        self.grads holds the gradients afterwards as with backward_phase(0)."""
+        if self.optimizer is not None:
+            g = self.optimizer.param_groups[0]
+            self.lr, self.alpha, self.eps = g["lr"], g.get("alpha", self.alpha), g.get("eps", self.eps)
+        m = self.model
+        check(lib().f3_net_backward_rmsprop(m._native.h, self.N, ptr(m.flat_parameters()), ptr(self.dout),
+                                            ptr(self.grads), ptr(self.square_avg), ptr(self.ws), self.lr, self.alpha,
+                                            self.eps, stream_handle()), "fall3 backward + rmsprop")
+
     def allreduce(self):
         self.sync.all()
 
@@ -168,6 +183,9 @@ class TrainStep:
             self.backward_phase(2)
             self.sync.start_tail()
             self.sync.finish()
+        elif self.fused_optimizer:
+            self.backward_optimizer_step()
+            return
         else:
             self.backward_phase(0)
         self.optimizer_step()

@@ -10,6 +10,8 @@
  *   f3_net_loss        <- loss_fn(pred, label_onehot)     model/main.py:113,280 (CE, soft targets)
  *   f3_net_backward    <- loss.backward()                 model/main.py:115
  *   f3_rmsprop_step    <- optimizer.step()                model/main.py:127, optimizer.py:21
+ *   f3_net_backward_rmsprop <- loss.backward(); optimizer.step()  (one GPU: the update per layer
+ *                              as soon as its gradients are final)
  *
  * Conventions: plain pointers to device memory (HIP), sizes in elements, a HIP stream
  * passed as void*. No call allocates, frees or synchronises: every buffer (flat
@@ -114,6 +116,16 @@ int f3_net_backward_phase(f3_net* net, int batch, const float* params, const flo
 int64_t f3_net_grad_split(const f3_net* net);
 int f3_net_wait_phase1(f3_net* net, void* stream);
 
+/* The single-GPU step's backward and optimizer in one call: f3_net_backward followed by
+ * f3_rmsprop_step(params, square_avg, grads, nparam, lr, alpha, eps, 1.0) (loss.backward() +
+ * optimizer.step(), model/main.py:115-127), except that each skeleton layer's RMSprop update is
+ * issued on the queue that finishes that layer's gradients, as soon as they are final, instead of
+ * after the whole backward; the rest (data_bn, sensor branch, head) follows the join. grads holds
+ * the step's gradients afterwards as with f3_net_backward. Identical updates; not for data
+ * parallelism (the all-reduce must come between the two). */
+int f3_net_backward_rmsprop(f3_net* net, int batch, float* params, const float* dout, float* grads, float* square_avg,
+                            void* workspace, float lr, float alpha, float eps, void* stream);
+
 /* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
  * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):
  * sq = alpha*sq + (1-alpha)*g^2 ; p -= lr*g/(sqrt(sq)+eps). */
@@ -143,6 +155,25 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
  * requires Cout % 64 == 0, Cin % 64 == 0, slab_floats >= Cout*KT*Cin. Used to time the kernel. */
 int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long slab_floats, int N, int T_in, int V,
                          int Cin, int Cout, int KT, int stride, int pad, void* stream);
+
+/* F3_PRECISION_BF16X3 as the training step runs it (K-concatenation on the bf16 LDS-DMA kernels):
+ * f3_split_x3cat writes each fp32 row x[r][0..C) as the bf16 row [hi | lo | hi] of 3C (hi = RNE
+ * bf16(x), lo = RNE bf16(x - hi)); the packed weight of a tap is [W_hi | W_hi | W_lo], so ONE bf16 GEMM
+ * over 3C computes x_hi W_hi + x_lo W_hi + x_hi W_lo (the split product, ~2^-16 relative).
+ * f3_conv_forward_x3cat / f3_conv_backward_data_x3cat: x3 / dy3 are such rows ([N,T,V,3Cin] /
+ * [N,T_out,V,3Cout]); wpack is scratch of 1.5 * Cout*KT*Cin floats (w == NULL reuses it); out / dx
+ * fp32 as f3_conv_forward / f3_conv_backward_data (bias required, epilogue + bias).
+ * f3_conv_backward_weight_x3cat: one bf16 GEMM on [dy_hi | dy_lo] x [x_hi | x_lo] (the first 2C of
+ * each 3C row) whose hi*hi + hi*lo + lo*hi quadrants a fold launch adds into dw [Cout][Cin][KT] and db
+ * (both overwritten; db may be NULL). dw == NULL: the GEMM alone at the step's split count, partials
+ * left in an internal slab (timing). Requires Cin, Cout multiples of 64 for the weight gradient. */
+int f3_split_x3cat(const float* x, void* out, int64_t rows, int C, void* stream);
+int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, float* out, void* wpack, int N, int T_in,
+                          int V, int Cin, int Cout, int KT, int stride, int pad, void* stream);
+int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void* wpack, int N, int T_in, int V,
+                                int Cin, int Cout, int KT, int stride, int pad, void* stream);
+int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, float* db, int N, int T_in, int V,
+                                  int Cin, int Cout, int KT, int stride, int pad, void* stream);
 
 /* The 1x1 conv GEMM of the bf16 step with the step's epilogues (stgcan.py:50-56 gcn conv, its
  * input gradient; stgcan.py:123-144 stride-2 residual conv and its input gradient), through the

@@ -146,6 +146,68 @@ def test_conv_backward_kernels_match_torch(shape, precision):
     np.testing.assert_allclose(db.cpu().numpy(), b.grad.numpy(), rtol=0, atol=2e-5 * np.abs(b.grad.numpy()).max())
 
 
+X3CAT_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
+                (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4), (2, 30, 18, 64, 192, 1, 1, 0),
+                (3, 30, 18, 192, 64, 1, 1, 0), (3, 15, 18, 256, 256, 9, 2, 4), (2, 29, 18, 128, 128, 9, 1, 4)]
+
+
+@pytest.mark.parametrize("shape", X3CAT_SHAPES)
+def test_conv_x3cat_kernels_match_torch(shape):
+    """bf16x3 as the step runs it: fp32 operands split by f3_split_x3cat into [hi | lo | hi] rows and
+    K-concatenated weights [W_hi | W_hi | W_lo] on the bf16 LDS-DMA kernels (forward, input gradient);
+    the weight gradient as one bf16 GEMM on [hi | lo] x [hi | lo] with the quadrant fold. Each against
+    fp64 on the fp32 operands within X3_TOL of the max (the split-bf16 product, ~2^-16 per term)."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    lib, st = L.lib(), L.stream_handle()
+    N, T, V, Ci, Co, KT, s, p = shape
+    torch.manual_seed(5)
+    x = torch.randn(N, Ci, T, V, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(Co, Ci, KT, 1, dtype=torch.float64) / np.sqrt(Ci * KT)).requires_grad_(True)
+    b = torch.randn(Co, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, b, stride=(s, 1), padding=(p, 0))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    To = y.shape[2]
+
+    def split(t_cl):
+        t = t_cl.float().contiguous().to(d)
+        rows, C = t.numel() // t.shape[-1], t.shape[-1]
+        out = torch.empty(rows, 3 * C, device=d, dtype=torch.bfloat16)
+        L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), rows, C, st), "split")
+        torch.cuda.synchronize()
+        hi = t.to(torch.bfloat16)
+        lo = (t - hi.float()).to(torch.bfloat16)
+        ref = torch.cat([hi.reshape(rows, C), lo.reshape(rows, C), hi.reshape(rows, C)], 1)
+        assert torch.equal(out.view(torch.int16), ref.view(torch.int16))  # bit-exact RNE split
+        return out
+
+    x3 = split(x.detach().permute(0, 2, 3, 1))
+    dy3 = split(dy.permute(0, 2, 3, 1))
+    wg, bg = w.detach().float().contiguous().to(d), b.detach().float().to(d)
+    wp = torch.empty(3 * Co * KT * Ci // 2 + 64, device=d)
+    out = torch.empty(N, To, V, Co, device=d)
+    L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(wg), L.ptr(bg), L.ptr(out), L.ptr(wp), N, T, V, Ci, Co, KT, s, p,
+                                      st), "fwd")
+    dx = torch.empty(N, T, V, Ci, device=d)
+    wpt = torch.empty(3 * Co * KT * Ci // 2 + 64, device=d)
+    L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(wg), L.ptr(dx), L.ptr(wpt), N, T, V, Ci, Co, KT, s, p,
+                                            st), "dgrad")
+    dw = torch.empty(Co, Ci, KT, device=d)
+    db = torch.empty(Co, device=d)
+    L.check(lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, Ci, Co, KT, s, p,
+                                              st), "wgrad")
+    torch.cuda.synchronize()
+    errs = {}
+    for name, got, ref in (("y", out.cpu().double(), y.detach().permute(0, 2, 3, 1)),
+                           ("dx", dx.cpu().double(), x.grad.permute(0, 2, 3, 1)),
+                           ("dw", dw.cpu().double(), w.grad.reshape(Co, Ci, KT)),
+                           ("db", db.cpu().double(), b.grad)):
+        errs[name] = float((got - ref).abs().max() / ref.abs().max())
+    print(f"bf16x3 cat {shape}: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert max(errs.values()) <= X3_TOL, errs
+
+
 @pytest.mark.parametrize("V,K,Cin,F", [(14, 3, 64, 40), (18, 3, 64, 37), (18, 3, 256, 20), (14, 3, 3, 30),
                                         (18, 3, 2, 29), (18, 1, 128, 9), (14, 2, 128, 11)])
 def test_graph_mix_kernels_match_torch(V, K, Cin, F):
@@ -401,6 +463,38 @@ def test_rmsprop_flat_path_matches_torch():
             sq = [opt.state[p]["square_avg"] for p in params]
             assert len({s.untyped_storage().data_ptr() for s in sq}) == 1
             assert int(opt.state[params[0]]["step"]) == 3
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32", "bf16"])
+def test_backward_rmsprop_per_layer_updates(precision):
+    """TrainStep at world 1 runs f3_net_backward_rmsprop: each skeleton layer's RMSprop update is
+    issued on the queue that finishes its gradients, the rest after the join. Over two steps the
+    parameters and square_avg must equal torch's RMSprop arithmetic applied to the step's own
+    gradients (step.grads) from the previous state - every parameter updated exactly once."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    spec = oc.Spec(model="two_stgcan_bilstm", layout="coco_mmpose", num_class=11, sensor_dim=6)
+    st = oc.init_state(spec, 9)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d,
+                                      precision=precision)
+    model.load_state_dict(st)
+    B, lr, alpha, eps = 32, 1e-3, 0.99, 1e-8
+    step = f3.TrainStep(model, B, lr=lr)
+    assert step.fused_optimizer
+    for k in range(2):
+        sk, se, lb = (torch.from_numpy(x).to(d) for x in synthetic_batch(B, 18, 11, 6, 40 + k))
+        p0 = model.flat_parameters().detach().clone()
+        sq0 = step.square_avg.clone()
+        step(sk, se, lb)
+        torch.cuda.synchronize()
+        g = step.grads
+        sq = alpha * sq0 + (1 - alpha) * g * g
+        p = p0 - lr * g / (sq.sqrt() + eps)
+        torch.testing.assert_close(step.square_avg, sq, rtol=1e-6, atol=1e-12)
+        torch.testing.assert_close(model.flat_parameters().detach(), p, rtol=1e-6, atol=1e-7)
+        if k == 0:  # from square_avg = 0 every update is ~lr in size: nothing may be skipped
+            moved = (model.flat_parameters().detach() != p0) | (g == 0)
+            assert bool(moved.all()), int((~moved).sum())
 
 
 @pytest.mark.parametrize("layout,S,B", [("coco_mmpose", 6, 32), ("coco_cut", 15, 24), ("coco_mmpose", 6, 13)])

@@ -11,8 +11,9 @@
 #   step_prof_serial  the bench step with every queue joined (F3_SERIAL=1): per-kernel alone times
 #                     -> gpurun_out/step_serial_kernels.txt
 #   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
-#   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches  -> gpurun_out/roof_kernels.txt
-#   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the roofline launches -> gpurun_out/roofline_pmc.json
+#   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches, one process per key in
+#               ${ROOF_KEYS:-wgrad_l5 wgrad wgrad_kernel tcn_fwd}          -> gpurun_out/roof_kernels_KEY.txt
+#   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the same, per key     -> gpurun_out/roofline_pmc.json
 #   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
 #   bench_fp32  bench.py --precision fp32 --no-targcn                   -> gpurun_out/bench_fp32.json
 #   ab          tools/ab.sh env $AB_CFGS (eager bench A/B, optional serial profiles) -> gpurun_out/ab.log
@@ -88,17 +89,21 @@ for step in "$@"; do
       python tools/pmc_summary.py gpurun_out --top 60 > gpurun_out/step_hbm_traffic.txt 2>&1
       head -30 gpurun_out/step_hbm_traffic.txt ;;
     roof_prof)
-      run roof_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof -o run -- \
-        python tools/roofline_pmc.py run > gpurun_out/roof_prof.log 2>&1
-      python tools/prof_summary.py gpurun_out/roof/run_results.db --top 30 > gpurun_out/roof_kernels.txt 2>&1
-      head -20 gpurun_out/roof_kernels.txt ;;
+      for K in ${ROOF_KEYS:-wgrad_l5 wgrad wgrad_kernel tcn_fwd}; do
+        run roof_prof_$K 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof_$K -o run -- \
+          python tools/roofline_pmc.py run $K > gpurun_out/roof_prof_$K.log 2>&1
+        python tools/prof_summary.py gpurun_out/roof_$K/run_results.db --top 30 > gpurun_out/roof_kernels_$K.txt 2>&1
+        head -8 gpurun_out/roof_kernels_$K.txt
+      done ;;
     roof_pmc)
-      for C in FETCH_SIZE WRITE_SIZE; do
-        rm -rf gpurun_out/rpmc_$C
-        run rpmc_$C 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/rpmc_$C -o run -- python tools/roofline_pmc.py run \
-          > gpurun_out/roof_pmc_$C.log 2>&1
-        db=$(find gpurun_out/rpmc_$C -name "*.db" | head -1)
-        [ -n "$db" ] && [ "$db" != "gpurun_out/rpmc_$C/run_results.db" ] && mv "$db" gpurun_out/rpmc_$C/run_results.db
+      for K in ${ROOF_KEYS:-wgrad_l5 wgrad wgrad_kernel tcn_fwd}; do
+        for C in FETCH_SIZE WRITE_SIZE; do
+          rm -rf gpurun_out/rpmc_${K}_$C
+          run rpmc_${K}_$C 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/rpmc_${K}_$C -o run -- \
+            python tools/roofline_pmc.py run $K > gpurun_out/roof_pmc_${K}_$C.log 2>&1
+          db=$(find gpurun_out/rpmc_${K}_$C -name "*.db" | head -1)
+          [ -n "$db" ] && [ "$db" != "gpurun_out/rpmc_${K}_$C/run_results.db" ] && mv "$db" gpurun_out/rpmc_${K}_$C/run_results.db
+        done
       done
       python tools/roofline_pmc.py summarize gpurun_out > gpurun_out/roofline_pmc.json 2>&1
       cat gpurun_out/roofline_pmc.json | head -40 ;;

@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch of bench.py's roofline kernels, from rocprofv3 PMC counters.
+"""HBM traffic per launch of bench.py's roofline kernels (the bf16x3 headline mode), from rocprofv3
+PMC counters. One profiled process per roofline key, so launches of the same kernel name in
+different keys (layer 6 / layer 5 / the GEMM alone) never mix.
 
-    run:        python tools/roofline_pmc.py run          (the kernels bench.py times, 20 launches each)
-    on the box: timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/rpmc_FETCH_SIZE -o run -- python tools/roofline_pmc.py run
-                timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/rpmc_WRITE_SIZE -o run -- python tools/roofline_pmc.py run
-    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r01_roofline_pmc.json
+    run:        python tools/roofline_pmc.py run KEY   (bench.roofline_kernels(..., "bf16x3", only=KEY):
+                                                       3 warm-up + 20 timed launches; writes the record
+                                                       to gpurun_out/roof_names/KEY.json)
+    on the box: per KEY and counter C: timeout -s KILL 60 rocprofv3 --pmc C --kernel-trace
+                    -d gpurun_out/rpmc_KEY_C -o run -- python tools/roofline_pmc.py run KEY
+                (tools/gpu_session.sh roof_pmc)
+    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r04_roofline_pmc.json
 
 FETCH_SIZE on gfx950 counts 1/2 of the bytes of wide streaming reads (MI355X_MICROARCH.md,
 HBM section; calibrated here on rmsprop_kernel: 51.6 MB read = 2 x FETCH_SIZE), so fetch is
@@ -19,27 +24,20 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-_TAPS = os.environ.get("F3_WGRAD_TAPS", "1") != "0"
-_WG = "wgrad_taps<5>" if _TAPS else "wgrad_big<4, 2, 4, 4, 64>"
-_RED = "wgrad_taps_reduce_kernel" if _TAPS else "wgrad_slab_reduce_kernel"
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
-KERNELS = {"wgrad": [_WG, _RED], "wgrad_kernel": [_WG],
-           "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_kernel"],
-           "tcn_fwd": ["igemm_big<1, 2, 4, false, true," if os.environ.get("F3_BIG_WIN", "1") != "0" else "igemm_big<1, 1, 8,"]}
-_SHAPE = "C=256, T=8, N=256, V=18"
-_KN = _WG.replace(", ", ",")
-NAMES = {"wgrad": f"{_KN} + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, {_SHAPE})",
-         "wgrad_kernel": f"{_KN} alone (partials left in the slab, {_SHAPE})",
-         "wgrad_l5": "wgrad_big<4,2,4,4,64> + slab reduce (tcn 9x1 weight gradient incl. the split-K reduce, "
-                     "stride 2, C=256, T=15->8, N=256, V=18)",
-         "tcn_fwd": ("igemm_big<1,2,4,false,true> (clip window)" if os.environ.get("F3_BIG_WIN", "1") != "0"
-                     else "igemm_big<1,1,8>") + f" bf16-out (tcn 9x1 fwd, {_SHAPE})"}
+KERNELS = {"wgrad_l5": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_x3_kernel"],
+           "wgrad": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_x3_kernel"],
+           "wgrad_kernel": ["wgrad_big<4, 2, 4, 4, 64>"],
+           "tcn_fwd": ["igemm_big<"]}
 
 
-def run():
+def run(key):
     import torch
     import bench
-    r = bench.roofline_kernels(torch.device("cuda"), 256, 18, "bf16")
+    r = bench.roofline_kernels(torch.device("cuda"), 256, 18, "bf16x3", only=key)
+    os.makedirs(os.path.join(ROOT, "gpurun_out", "roof_names"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "roof_names", key + ".json"), "w") as f:
+        json.dump(r[key], f)
     print(json.dumps({k: [v["kernel"], v["ms_per_launch"], v["frac"]] for k, v in r.items()}))
 
 
@@ -53,26 +51,32 @@ def per_launch(db, counter, pattern):
 def summarize(d):
     out = {}
     for key, pats in KERNELS.items():
+        names = os.path.join(d, "roof_names", key + ".json")
+        if not os.path.exists(names):
+            continue
+        with open(names) as f:
+            rec = json.load(f)
         fetch = write = 0.0
         launches = []
         for pat in pats:
-            f, nf = per_launch(os.path.join(d, "rpmc_FETCH_SIZE", "run_results.db"), "FETCH_SIZE", pat)
-            w, nw = per_launch(os.path.join(d, "rpmc_WRITE_SIZE", "run_results.db"), "WRITE_SIZE", pat)
+            f, nf = per_launch(os.path.join(d, f"rpmc_{key}_FETCH_SIZE", "run_results.db"), "FETCH_SIZE", pat)
+            w, nw = per_launch(os.path.join(d, f"rpmc_{key}_WRITE_SIZE", "run_results.db"), "WRITE_SIZE", pat)
             if f is None or w is None:
                 break
             fetch += 2.0 * f
             write += w
             launches.append([pat, nf, nw])
         else:
-            out[key] = {"kernel": NAMES[key], "fetch_bytes": fetch, "write_bytes": write,
+            out[key] = {"kernel": rec["kernel"], "fetch_bytes": fetch, "write_bytes": write,
                         "bytes_per_launch": round(fetch + write), "launches": launches,
+                        "ms_per_launch_in_profiled_run": rec["ms_per_launch"],
                         "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, mean over launches, "
-                                "summed over the kernels of one launch"}
+                                "summed over the kernels of one launch; one profiled process per key"}
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run()
+        run(sys.argv[2])
     else:
         summarize(sys.argv[2])
