@@ -205,15 +205,14 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     T=8 output frames, B clips), launched alone through the C ABI exactly as the step launches them:
     K-concatenated operand rows [hi | lo | hi] (f3_split_x3cat, done once outside the timing, as the
     step's producers write them) on the bf16 LDS-DMA kernels:
-    * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): ONE bf16 GEMM on [dy_hi | dy_lo] x
-      [x_hi | x_lo] (512 x 9 x 512, wgrad_big<4,2,4,4,64>, split-K partials in the slab) + the quadrant
-      fold into dW[Cout][Cin][KT] (f3_conv_backward_weight_x3cat) - the headline: the step's largest
-      kernel share in this mode;
+    * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,64> over three
+      row segments of the [hi | lo | hi] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
+      three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
+      (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
     * "wgrad": the same on layer 6 (stride 1, T 8); "wgrad_kernel": its GEMM alone (dw = NULL);
     * "tcn_fwd": the layer-6 forward over K = 9 x 3C (f3_conv_forward_x3cat, fp32 out + bias).
     Algorithmic FLOP per launch = the split product's three bf16 products, 3 * 2*M*N*K with
-    M = B*8*V, N = 256, K = 9*256; priced against the dense bf16 MFMA peak. (The weight-gradient GEMM
-    also computes the unused lo*lo quadrant, so its MFMA work is 4/3 of this.) `only`: one key (the
+    M = B*8*V, N = 256, K = 9*256; priced against the dense bf16 MFMA peak. `only`: one key (the
     per-key PMC passes of tools/roofline_pmc.py)."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
@@ -247,16 +246,16 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     db = torch.empty(C, device=dev)
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, C,
                                                                 C, KT, 1, 4, st)) if want("wgrad") else 0.0
-    out["wgrad"] = {"kernel": f"wgrad_big<4,2,4,4,64> 512x9x512 + x3 quadrant fold (tcn 9x1 weight gradient, bf16x3 "
-                              f"K-concatenated, C=256, T=8, N={N}, V={V})", "ms": ms}
+    out["wgrad"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
+                              f"bf16x3, C=256, T=8, N={N}, V={V})", "ms": ms}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), None, None, N, T, V, C, C, KT, 1,
                                                                 4, st)) if want("wgrad_kernel") else 0.0
-    out["wgrad_kernel"] = {"kernel": f"wgrad_big<4,2,4,4,64> alone (bf16x3 K-concatenated, partials left in the slab, "
-                                     f"C=256, T=8, N={N}, V={V})", "ms": ms}
+    out["wgrad_kernel"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments alone (bf16x3, partials left in the "
+                                     f"slab, C=256, T=8, N={N}, V={V})", "ms": ms}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15, V, C,
                                                                 C, KT, 2, 4, st)) if want("wgrad_l5") else 0.0
-    out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,64> 512x9x512 + x3 quadrant fold (tcn 9x1 weight gradient, "
-                                 f"bf16x3 K-concatenated, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms}
+    out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
+                                 f"bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms}
     return _roofline_records({k: v for k, v in out.items() if want(k)}, flop, peak)
 
 

@@ -668,7 +668,8 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
 // elements (one (j, dt) row piece, Kc % 64 == 0); its 4 waves sum interleaved split subsets
 // (coalesced 256-B reads, independent loads) and combine through LDS.
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
-                                                                int Kc, int KT, float* __restrict__ dw_ref) {
+                                                                int Kc, int KT, float* __restrict__ dw_ref,
+                                                                int gcn_cin = 0) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t e = (size_t)blockIdx.x * 64 + lane;  // slab element (j, dt, i)
@@ -685,7 +686,12 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
   if (wave == 0) {
     const float v = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
     const int j = (int)(e / ((size_t)KT * Kc)), r = (int)(e - (size_t)j * KT * Kc), dt = r / Kc, i = r - dt * Kc;
-    dw_ref[((size_t)j * Kc + i) * KT + dt] += v;
+    if (gcn_cin > 0) {  // gcn reference layout [K*Nc][gcn_cin] (KT = 1, i = k gcn_cin + ci)
+      const int k = i / gcn_cin, ci = i - k * gcn_cin;
+      dw_ref[((size_t)k * Nc + j) * gcn_cin + ci] += v;
+    } else {
+      dw_ref[((size_t)j * Kc + i) * KT + dt] += v;
+    }
   }
 }
 
@@ -740,11 +746,14 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int j0 = bx * TJ;
   const int dt = by / itiles;
   const int i0 = (by - dt * itiles) * TI;
-  const int r_begin = bz * a.rows_per_split;
+  // bf16x3 row segments (x3seg): split bz covers rows of segment seg = bz / seg_splits, whose
+  // operands sit at column offsets (0, 0) hi x hi, (Nc, 0) lo x hi, (0, Kc) hi x lo of the rows
+  const int seg = a.x3seg ? bz / a.seg_splits : 0;
+  const int r_begin = (a.x3seg ? bz - seg * a.seg_splits : bz) * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
-  const bool do_db = a.db && by == 0;
-  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
-  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const bool do_db = a.db && by == 0 && seg < 2;
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb) + (seg == 2 ? g.Kc : 0);
   const __bf16* zero = reinterpret_cast<const __bf16*>(a.zero);
   const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
 
@@ -1475,20 +1484,25 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   static const int slots = resident_wgs((const void*)KERNEL, THREADS);
   const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
   const int groups = std::max(1, a.groups);  // grouped launches: wgrad_big, atomics (checked by the caller)
-  int splits = std::max(1, target / (gx * gy * groups));
+  // x3seg: three row segments, `splits` row splits each (one round of resident workgroups in all)
+  const int nseg = a.x3seg ? 3 : 1;
+  int splits = std::max(1, target / (gx * gy * groups * nseg));
   const bool to_slab = a.slab && a.outmap == WG_OUT_CONV;
   const long long per_split = (long long)a.g.Nc * a.g.KT * a.g.Kc;
   if (to_slab) {
-    if (a.slab_cap < per_split) return F3_EINVAL;
+    if (a.slab_cap < per_split * nseg) return F3_EINVAL;
     // (the slab grew for wgrad_taps; these tiles keep their measured split count)
-    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, a.x3fold ? a.slab_cap : 512LL * 128 * 128) /
-                                                  per_split);
+    const bool x3 = a.x3fold || a.x3seg;
+    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, x3 ? a.slab_cap : 512LL * 128 * 128) /
+                                                  (per_split * nseg));
   }
   int rps = (a.g.M + splits - 1) / splits;
   rps = ((rps + 63) / 64) * 64;
   if (rps < 256) rps = 256;
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
+  a.seg_splits = splits;
+  splits *= nseg;  // slab partials (all segments)
   // XCD-aware grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
   // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the
   // round-robin 3-D grid
@@ -1500,7 +1514,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   if (to_slab && a.dw_ref) {
     if (a.x3fold) return launch_fold_x3(a, splits, s);
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
-                       a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref);
+                       a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref, a.gcn_cin);
     F3_LAUNCH_CHECK();
   }
   return F3_OK;
@@ -1514,6 +1528,10 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   if (a.x3fold && (!a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.Nc % 2 || a.g.Kc % 2))
     return F3_EINVAL;
   if (a.x3fold && a.gcn_cin > 0 && (a.g.KT != 1 || (a.g.Kc / 2) % a.gcn_cin)) return F3_EINVAL;
+  if (a.x3seg && (a.x3fold || !a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.transposed ||
+                  a.ldy < 3 * a.g.Nc || a.g.lda < 3 * a.g.Kc))
+    return F3_EINVAL;
+  if (a.x3seg && a.gcn_cin > 0 && (a.g.KT != 1 || a.g.Kc % a.gcn_cin)) return F3_EINVAL;
   // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
   static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
   const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
@@ -1521,12 +1539,13 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const int bigv = a.groups > 1 ? 1 : big;
   // F3_WGRAD_TAPS=0: the per-tap wgrad_big tiles for the stride-1 clip-sized layers too
   static const int taps_env = getenv("F3_WGRAD_TAPS") ? atoi(getenv("F3_WGRAD_TAPS")) : 1;
-  if (taps_env && bigv && !a.x3fold) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
+  if (taps_env && bigv && !a.x3fold && !a.x3seg) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
     const int nks = wgrad_taps_nks(a);
     if (nks) return launch_wgrad_taps(a, nks, s);
     const int nseg = wgrad_seg_nks(a);  // every other (9,1) layer: clip segments, stride 2 by parity
     if (nseg) return launch_wgrad_seg(a, nseg, s);
   }
+  if (a.x3seg && !bigv) return F3_EINVAL;  // (row segments: wgrad_big only)
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once

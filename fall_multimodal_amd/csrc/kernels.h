@@ -85,6 +85,13 @@ struct WgradArgs {
   // [K*C][gcn_cin] instead (column k gcn_cin + ci of the packed operand -> row k C + c).
   int x3fold;
   float* db_fold;
+  // bf16x3 on the bf16 kernels by row segments (wgrad_big): dy / in are [hi | lo | hi] rows (ldy = 3 Nc,
+  // lda = 3 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi), (dY_lo, X_hi),
+  // (dY_hi, X_lo) - the split product's three terms, no unused quadrant - with seg_splits row splits
+  // per segment (set by the launcher); the bias sums the first two segments (dY_hi + dY_lo).
+  // With gcn_cin > 0 the slab reduce writes the gcn layout (as x3fold).
+  int x3seg;
+  int seg_splits;
 };
 
 // Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).

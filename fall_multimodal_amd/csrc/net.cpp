@@ -266,6 +266,12 @@ inline bool wgrad_slab() {
   static const bool on = !getenv("F3_WGRAD_SLAB") || atoi(getenv("F3_WGRAD_SLAB")) != 0;
   return on;
 }
+// bf16x3 weight gradients: row segments (the three split products, WgradArgs::x3seg; default) or
+// F3_X3_FOLD=1: one GEMM on [hi | lo] x [hi | lo] whose quadrants a fold launch adds (x3fold)
+inline bool x3_fold() {
+  static const bool on = getenv("F3_X3_FOLD") && atoi(getenv("F3_X3_FOLD")) != 0;
+  return on;
+}
 
 struct BnWs {
   double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
@@ -902,13 +908,19 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
-    } else if (x3) {  // [dh_hi | dh_lo] x [u_hi | u_lo] (the first 2C of the 3C rows) on the bf16 kernels;
-      // the slab reduce keeps the hi*hi + hi*lo + lo*hi quadrants (and folds the bias scratch)
+    } else if (x3) {  // on the bf16 kernels over the [hi | lo | hi] rows of dh and u: three row
+      // segments (dh_hi u_hi, dh_lo u_hi, dh_hi u_lo), or (F3_X3_FOLD=1) [dh_hi | dh_lo] x [u_hi | u_lo]
+      // whose slab reduce keeps the hi*hi + hi*lo + lo*hi quadrants (and folds the bias scratch)
       tw.x3 = 0; tw.bf16 = 1;
-      tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, 2 * C);
       tw.ldy = 3 * C; tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
       tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats * 4; tw.dw_ref = q.g(L.tcn_w);
-      tw.x3fold = 1; tw.db = X.dbx3; tw.db_fold = q.g(L.tcn_b);
+      if (x3_fold()) {
+        tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, 2 * C);
+        tw.x3fold = 1; tw.db = X.dbx3; tw.db_fold = q.g(L.tcn_b);
+      } else {
+        tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, C);
+        tw.x3seg = 1;
+      }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
     } else {
@@ -924,12 +936,17 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (hb) {
         rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
-      } else if (x3) {  // [dr_hi | dr_lo] x [x_hi | x_lo] quadrants, folded like the tcn's
+      } else if (x3) {  // row segments / quadrant fold as the tcn's
         rw.x3 = 0; rw.bf16 = 1;
-        rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, 2 * C);
         rw.ldy = 3 * C; rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats * 4; rw.dw_ref = q.g(L.res_w);
-        rw.x3fold = 1; rw.db = X.dbx3r; rw.db_fold = q.g(L.res_b);
+        if (x3_fold()) {
+          rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, 2 * C);
+          rw.x3fold = 1; rw.db = X.dbx3r; rw.db_fold = q.g(L.res_b);
+        } else {
+          rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, C);
+          rw.x3seg = 1;
+        }
         if (!f3_wgrad_glds_ok(rw)) return F3_EINVAL;
       } else {
         rw.dy = dres; rw.in = X.x;
@@ -957,12 +974,17 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
-    if (gcat) {  // [dg_hi | dg_lo] x [Z_hi | Z_lo] quadrants into the slab, folded to the gcn layout
+    if (gcat) {  // row segments (or quadrants) into the slab, reduced into the gcn layout
       gw.x3 = 0; gw.bf16 = 1; gw.outmap = WG_OUT_CONV;
-      gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, 2 * C);
       gw.ldy = 3 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
       gw.slab = W.slab; gw.slab_cap = kWgradSlabFloats * 4; gw.dw_ref = q.g(L.gcn_w); gw.dw = nullptr;
-      gw.x3fold = 1;
+      if (x3_fold()) {
+        gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, 2 * C);
+        gw.x3fold = 1;
+      } else {
+        gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, C);
+        gw.x3seg = 1;
+      }
       if (!f3_wgrad_glds_ok(gw)) return F3_EINVAL;
     }
     if ((part & 2) && !g0) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
@@ -1743,17 +1765,28 @@ int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, fl
   if (!slab) return F3_EHIP;
   WgradArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, 2 * Cout);
-  a.ldy = 3 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1; a.x3fold = 1;
+  a.ldy = 3 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1;
   a.dyb = static_cast<const unsigned short*>(dy3); a.inb = static_cast<const unsigned short*>(x3);
   a.zero = test_zero_page(); a.slab = slab; a.slab_cap = cap;
+  const bool fold = x3_fold();  // as the step (F3_X3_FOLD)
+  if (fold) {
+    a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, 2 * Cout);
+    a.x3fold = 1;
+  } else {
+    a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, Cout);
+    a.x3seg = 1;
+  }
   if (dw) {  // dw == NULL: the GEMM alone (partials left in the slab)
     if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
     a.dw_ref = dw;
     if (db) {
       if (hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
-      if (hipMemsetAsync(slab + cap, 0, sizeof(float) * 2 * Cout, s) != hipSuccess) return F3_EHIP;
-      a.db = slab + cap; a.db_fold = db;
+      if (fold) {
+        if (hipMemsetAsync(slab + cap, 0, sizeof(float) * 2 * Cout, s) != hipSuccess) return F3_EHIP;
+        a.db = slab + cap; a.db_fold = db;
+      } else {
+        a.db = db;
+      }
     }
   }
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;

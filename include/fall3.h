@@ -163,10 +163,10 @@ int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long s
  * f3_conv_forward_x3cat / f3_conv_backward_data_x3cat: x3 / dy3 are such rows ([N,T,V,3Cin] /
  * [N,T_out,V,3Cout]); wpack is scratch of 1.5 * Cout*KT*Cin floats (w == NULL reuses it); out / dx
  * fp32 as f3_conv_forward / f3_conv_backward_data (bias required, epilogue + bias).
- * f3_conv_backward_weight_x3cat: one bf16 GEMM on [dy_hi | dy_lo] x [x_hi | x_lo] (the first 2C of
- * each 3C row) whose hi*hi + hi*lo + lo*hi quadrants a fold launch adds into dw [Cout][Cin][KT] and db
- * (both overwritten; db may be NULL). dw == NULL: the GEMM alone at the step's split count, partials
- * left in an internal slab (timing). Requires Cin, Cout multiples of 64 for the weight gradient. */
+ * f3_conv_backward_weight_x3cat: the bf16 weight-gradient GEMM over three row segments of the rows,
+ * dy_hi x_hi + dy_lo x_hi + dy_hi x_lo (split-K partials summed into dw [Cout][Cin][KT]; db from
+ * dy_hi + dy_lo; both overwritten, db may be NULL). dw == NULL: the GEMM alone at the step's split
+ * count, partials left in an internal slab (timing). Requires Cin, Cout multiples of 64. */
 int f3_split_x3cat(const float* x, void* out, int64_t rows, int C, void* stream);
 int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, float* out, void* wpack, int N, int T_in,
                           int V, int Cin, int Cout, int KT, int stride, int pad, void* stream);

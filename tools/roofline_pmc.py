@@ -25,8 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
-KERNELS = {"wgrad_l5": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_x3_kernel"],
-           "wgrad": ["wgrad_big<4, 2, 4, 4, 64>", "wgrad_slab_reduce_x3_kernel"],
+_RED = "wgrad_slab_reduce_x3_kernel" if os.environ.get("F3_X3_FOLD", "0") != "0" else "wgrad_slab_reduce_kernel"
+KERNELS = {"wgrad_l5": ["wgrad_big<4, 2, 4, 4, 64>", _RED],
+           "wgrad": ["wgrad_big<4, 2, 4, 4, 64>", _RED],
            "wgrad_kernel": ["wgrad_big<4, 2, 4, 4, 64>"],
            "tcn_fwd": ["igemm_big<"]}
 
