@@ -69,7 +69,7 @@ def parse():
                    help="fall3: the headline 3-stream step (default). targcn / sktr: BASELINE config 2 / 5 alone; "
                         "musa: the root main.py's musa_model")
     p.add_argument("--no-targcn", action="store_true", help="skip the config-2 TARGCN and config-5 lines in the default run")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=24.0)
     p.add_argument("--launch-check", action="store_true",
                    help="start the --gpus N ranks exactly as a bench run does, all-reduce each rank's id over gloo and "
                         "print the ranks seen; touches no GPU (tests/test_bench_launch.py)")
@@ -209,7 +209,9 @@ def roofline_kernels_x3(dev, batch, V, only=None):
       row segments of the [hi | lo | hi] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
       three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
       (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
-    * "wgrad": the same on layer 6 (stride 1, T 8); "wgrad_kernel": its GEMM alone (dw = NULL);
+    * "wgrad": the same on layer 6 (stride 1, T 8), where the step runs wgrad_taps<5> (all 9 taps from
+      one staged copy of each clip) over the three segments + its reduce; "wgrad_kernel": that GEMM
+      alone (dw = NULL);
     * "tcn_fwd": the layer-6 forward over K = 9 x 3C (f3_conv_forward_x3cat, fp32 out + bias).
     Algorithmic FLOP per launch = the split product's three bf16 products, 3 * 2*M*N*K with
     M = B*8*V, N = 256, K = 9*256; priced against the dense bf16 MFMA peak. `only`: one key (the
@@ -246,12 +248,12 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     db = torch.empty(C, device=dev)
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, C,
                                                                 C, KT, 1, 4, st)) if want("wgrad") else 0.0
-    out["wgrad"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
-                              f"bf16x3, C=256, T=8, N={N}, V={V})", "ms": ms}
+    out["wgrad"] = {"kernel": f"wgrad_taps<5> x 3 row segments + reduce (tcn 9x1 weight gradient, bf16x3, C=256, "
+                              f"T=8, N={N}, V={V})", "ms": ms}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), None, None, N, T, V, C, C, KT, 1,
                                                                 4, st)) if want("wgrad_kernel") else 0.0
-    out["wgrad_kernel"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments alone (bf16x3, partials left in the "
-                                     f"slab, C=256, T=8, N={N}, V={V})", "ms": ms}
+    out["wgrad_kernel"] = {"kernel": f"wgrad_taps<5> x 3 row segments alone (bf16x3, partials left in the slab, "
+                                     f"C=256, T=8, N={N}, V={V})", "ms": ms}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15, V, C,
                                                                 C, KT, 2, 4, st)) if want("wgrad_l5") else 0.0
     out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "

@@ -961,10 +961,12 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a split's tiles stay on one XCD
   const int bz = lin / tiles, tile = lin - bz * tiles;
   const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
-  const int n_begin = bz * a.rows_per_split;          // rows_per_split holds clips per split here
+  // bf16x3 row segments (x3seg, as wgrad_big): (dY_hi, X_hi), (dY_lo, X_hi), (dY_hi, X_lo)
+  const int seg = a.x3seg ? bz / a.seg_splits : 0;
+  const int n_begin = (a.x3seg ? bz - seg * a.seg_splits : bz) * a.rows_per_split;  // clips per split here
   const int n_end = min(g.M / TV, n_begin + a.rows_per_split);
-  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
-  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
+  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb) + (seg == 2 ? g.Kc : 0);
   const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
 
   // ---- staging: 1-KiB pieces (8 rows), dY pieces then input pieces; a lane's slots are fixed ----
@@ -1097,8 +1099,8 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
     __syncthreads();
   }
   // bias gradient: the ones column of wave (kh 1, wi 0) in the i0 == 0 tiles; lane (fg, fr = 0)
-  // holds co = x*16 + fg*4 + r (all 16 columns carry the same sum)
-  if (a.db && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
+  // holds co = x*16 + fg*4 + r (all 16 columns carry the same sum); x3seg: dY_hi + dY_lo only
+  if (a.db && seg < 2 && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -1353,12 +1355,15 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
   const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
   static const int target = getenv("F3_TAPS_WGS") ? atoi(getenv("F3_TAPS_WGS")) : 256;  // one per CU
-  int splits = std::max(1, std::min(clips, target / tiles));
-  splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
+  const int nseg = a.x3seg ? 3 : 1;  // bf16x3 row segments: `splits` clip splits per segment
+  int splits = std::max(1, std::min(clips, target / (tiles * nseg)));
+  splits = (int)std::min<long long>(splits, a.slab_cap / (per_split * nseg));
   if (splits < 1) return F3_EINVAL;
   const int cps = (clips + splits - 1) / splits;
   splits = (clips + cps - 1) / cps;
   a.rows_per_split = cps;  // clips per split
+  a.seg_splits = splits;
+  splits *= nseg;
   static const int dbg = getenv("F3_TAPS_DBG") ? atoi(getenv("F3_TAPS_DBG")) : 0;
   a.dbg = dbg;
   const dim3 grid(tiles * splits);
@@ -1539,13 +1544,15 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const int bigv = a.groups > 1 ? 1 : big;
   // F3_WGRAD_TAPS=0: the per-tap wgrad_big tiles for the stride-1 clip-sized layers too
   static const int taps_env = getenv("F3_WGRAD_TAPS") ? atoi(getenv("F3_WGRAD_TAPS")) : 1;
-  if (taps_env && bigv && !a.x3fold && !a.x3seg) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
+  if (taps_env && bigv && !a.x3fold) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
     const int nks = wgrad_taps_nks(a);
     if (nks) return launch_wgrad_taps(a, nks, s);
+    if (a.x3seg) goto big;  // (wgrad_seg has no row segments)
     const int nseg = wgrad_seg_nks(a);  // every other (9,1) layer: clip segments, stride 2 by parity
     if (nseg) return launch_wgrad_seg(a, nseg, s);
   }
-  if (a.x3seg && !bigv) return F3_EINVAL;  // (row segments: wgrad_big only)
+big:
+  if (a.x3seg && !bigv) return F3_EINVAL;  // (row segments: wgrad_taps / wgrad_big only)
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once
