@@ -28,13 +28,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //   PACK_CONV_T  src [J][I][KT]   -> dst [I][KT][3J]
 //   PACK_GCN     src [K*C][Cin]   -> dst [C][3 K Cin]       (d0 C, d1 Cin, d2 K; one "tap")
 //   PACK_GCN_T   src [K*C][Cin]   -> dst [K Cin][3C]
+// One item e = one source value (j.n / 3 items), written to its three places.
 F3_DEV void prep_x3cat(const PrepJob& j, int e) {
   const bool gcn = j.type == PREP_PACK_GCN || j.type == PREP_PACK_GCN_T;
   const bool tr = j.type == PREP_PACK_CONV_T || j.type == PREP_PACK_GCN_T;
   const int J = j.d0, I = j.d1, KT = gcn ? 1 : j.d2;
   const int inner = gcn ? (tr ? J : j.d2 * I) : (tr ? J : I);  // channels per tap of the packed operand
-  const int row = e / (KT * 3 * inner), r = e - row * KT * 3 * inner;
-  const int dt = r / (3 * inner), q = r - dt * 3 * inner, seg = q / inner, c = q - seg * inner;
+  const int row = e / (KT * inner), r = e - row * KT * inner, dt = r / inner, c = r - dt * inner;
   float val;
   if (gcn) {  // W[k*C + c][ci]: (k, ci) from the packed row (transposed) or column
     const int kc = tr ? row : c, cc = tr ? c : row, k = kc / I, ci = kc - k * I;
@@ -43,17 +43,32 @@ F3_DEV void prep_x3cat(const PrepJob& j, int e) {
     val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
   }
   const __bf16 hi = (__bf16)val;
-  reinterpret_cast<__bf16*>(j.dst)[e] = seg < 2 ? hi : (__bf16)(val - (float)hi);
+  __bf16* d = reinterpret_cast<__bf16*>(j.dst) + ((size_t)row * KT + dt) * 3 * inner + c;
+  d[0] = hi;
+  d[inner] = hi;
+  d[2 * inner] = (__bf16)(val - (float)hi);
 }
 
-__global__ void prep_kernel(PrepTable t) {
-  const PrepJob j = t.jobs[blockIdx.y];
-  const int stride = gridDim.x * blockDim.x;
+// The job table plus each job's first block: a 1-D grid whose blocks are shared out in proportion
+// to the jobs' sizes (a fixed 64 blocks per job left the 256-channel packs to a few blocks looping
+// ~100 times while the small jobs' blocks idled: 83 us per launch in the bf16x3 step)
+struct PrepLaunch {
+  PrepTable t;
+  int boff[kMaxPrepJobs + 1];
+};
+static_assert(sizeof(PrepLaunch) <= 4096, "kernel argument block");
+
+__global__ void prep_kernel(PrepLaunch L) {
+  int jb = 0;
+  while (jb + 1 < L.t.n && (int)blockIdx.x >= L.boff[jb + 1]) ++jb;
+  const PrepJob j = L.t.jobs[jb];
+  const int nb = L.boff[jb + 1] - L.boff[jb], lb = blockIdx.x - L.boff[jb];
+  const int stride = nb * blockDim.x;
   if (j.bf16 == 3) {
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) prep_x3cat(j, e);
+    for (int e = lb * blockDim.x + threadIdx.x; e < j.n / 3; e += stride) prep_x3cat(j, e);
     return;
   }
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < j.n; e += stride) {
+  for (int e = lb * blockDim.x + threadIdx.x; e < j.n; e += stride) {
     float val = 0.f;
     switch (j.type) {
       case PREP_MUL:
@@ -1912,7 +1927,14 @@ using namespace f3;
 int f3_prep(const PrepTable& t, hipStream_t s) {
   if (t.n <= 0) return F3_OK;
   if (t.n > kMaxPrepJobs) return F3_EINVAL;
-  hipLaunchKernelGGL(prep_kernel, dim3(64, t.n), dim3(256), 0, s, t);
+  PrepLaunch L;
+  L.t = t;
+  L.boff[0] = 0;
+  for (int j = 0; j < t.n; ++j) {  // ~4 items per thread, 1..2048 blocks per job
+    const long long items = t.jobs[j].bf16 == 3 ? t.jobs[j].n / 3 : t.jobs[j].n;
+    L.boff[j + 1] = L.boff[j] + (int)std::min<long long>(2048, std::max<long long>(1, (items + 1023) / 1024));
+  }
+  hipLaunchKernelGGL(prep_kernel, dim3(L.boff[t.n]), dim3(256), 0, s, L);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Per-step timeline of a rocprofv3 --kernel-trace database: the window between two
-consecutive RMSprop dispatches (one training step), per HW queue: busy time, idle gaps,
-and the kernels in order. Shows which branch stream is the critical path.
+"""Per-step timeline of a rocprofv3 --kernel-trace database: the window between the ends of two
+consecutive steps (one training step), per HW queue: busy time, idle gaps, and the kernels in
+order. Shows which branch stream is the critical path. A step ends with its last RMSprop launch
+before the next step's loss kernel (the fused backward + RMSprop issues one launch per layer, the
+last after the join).
 
     python tools/timeline.py gpurun_out/prof/run_results.db [--step -2] [--list]
 """
@@ -17,7 +19,15 @@ def main():
     a = p.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, queue_id, grid_x, grid_y, grid_z from kernels order by start").fetchall()
-    ends = [r[2] for r in rows if "rmsprop" in r[0]]
+    ends, last = [], None
+    for r in rows:
+        if "rmsprop" in r[0]:
+            last = r[2] if last is None else max(last, r[2])
+        elif "::ce_kernel" in r[0] and last is not None:
+            ends.append(last)
+            last = None
+    if last is not None:
+        ends.append(last)
     t0, t1 = ends[a.step - 1], ends[a.step]
     win = [r for r in rows if r[1] >= t0 and r[2] <= t1]
     print(f"step window {(t1 - t0) / 1e3:.1f} us, {len(win)} kernels")
