@@ -203,10 +203,10 @@ def roofline_kernels(dev, batch, V, precision, only=None):
 def roofline_kernels_x3(dev, batch, V, only=None):
     """bf16x3 (the headline mode): the step's tcn GEMMs on the layer-6 / layer-5 shapes (C=256, 9 taps,
     T=8 output frames, B clips), launched alone through the C ABI exactly as the step launches them:
-    K-concatenated operand rows [hi | lo | hi] (f3_split_x3cat, done once outside the timing, as the
+    K-concatenated operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
     step's producers write them) on the bf16 LDS-DMA kernels:
     * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,64> over three
-      row segments of the [hi | lo | hi] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
+      row segments of the [hi | lo] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
       three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
       (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
     * "wgrad": the same on layer 6 (stride 1, T 8), where the step runs wgrad_taps<5> (all 9 taps from
@@ -225,7 +225,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
 
     def split(t):
         rows, c = t.numel() // t.shape[-1], t.shape[-1]
-        out = torch.empty(rows, 3 * c, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(rows, 2 * c, device=dev, dtype=torch.bfloat16)
         L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), rows, c, st), "split")
         return out
 

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       char* dst;
       if (q < AP) {
         const int r = rowmap_src(amap[i], dt, g);
-        src = r >= 0 ? (const void*)(in + (size_t)r * g.lda + i0 + swz(q * 8 + sub, pch) * 8) : (const void*)a.zero;
+        src = r >= 0 ? (const void*)(in + (size_t)r * g.lda + acol(a, i0) + swz(q * 8 + sub, pch) * 8) : (const void*)a.zero;
         dst = sbase + q * 1024;
       } else {
         src = wb + boff[i] + k0;
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         } else if (q < NP && dt >= 2 && c + 1 < kpt) {
           const int pa = (dt - 2) * WIN_APS + (q - Cfg::BP);  // A piece of chunk c + 1
           if (pa < BM / 8) {
-            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + (c + 1) * G_BK + swz(pa * 8 + sub, pch) * 8;
+            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acol(a, (c + 1) * G_BK) + swz(pa * 8 + sub, pch) * 8;
             dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
           }
         }

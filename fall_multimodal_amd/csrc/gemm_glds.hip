@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
       const int r = rowmap_src(a_map[i], dt, g);
-      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + i0 + a_c[i] : a.zero;
+      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + acol(a, i0) + a_c[i] : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sa + (wave * A_INSTR + i) * 1024), 16, 0, 0);
     }
     char* sb = sa + A_BYTES;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     for (int q = wave; q < nwp; q += 4) {
       const int rr = q * 8 + sub, gm = m0 - PV + rr;
       const bool ok = rr < WR && gm >= 0 && gm < g.M;
-      const unsigned short* src = ok ? in + (size_t)gm * g.lda + i0 + swz(rr, pch) * 8 : a.zero;
+      const unsigned short* src = ok ? in + (size_t)gm * g.lda + acol(a, i0) + swz(rr, pch) * 8 : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(smem + WIN_OFF + q * 1024), 16, 0, 0);
     }
   };
@@ -375,7 +375,8 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 using namespace f3;
 
 bool f3_igemm_ok(const ConvGemmArgs& a) {
-  return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0;
+  return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0 &&
+         (a.kwrap == 0 || (a.kwrap % G_BK == 0 && a.g.Kc == 3 * a.kwrap && a.g.lda >= 2 * a.kwrap));
 }
 
 // Window mode (see igemm_bf16): stride-1 temporal convs with "same" padding whose output
@@ -1534,7 +1535,7 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
     return F3_EINVAL;
   if (a.x3fold && a.gcn_cin > 0 && (a.g.KT != 1 || (a.g.Kc / 2) % a.gcn_cin)) return F3_EINVAL;
   if (a.x3seg && (a.x3fold || !a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.transposed ||
-                  a.ldy < 3 * a.g.Nc || a.g.lda < 3 * a.g.Kc))
+                  a.ldy < 2 * a.g.Nc || a.g.lda < 2 * a.g.Kc))
     return F3_EINVAL;
   if (a.x3seg && a.gcn_cin > 0 && (a.g.KT != 1 || a.g.Kc % a.gcn_cin)) return F3_EINVAL;
   // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)

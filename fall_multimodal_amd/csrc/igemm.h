@@ -29,6 +29,10 @@ F3_DEV int g_src_row(int n, int t, int v, int dt, const ConvGeom& g) {
 
 F3_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
+// A operand column of K index k (ConvGemmArgs::kwrap: the third segment of a bf16x3 row re-reads the
+// hi segment; 64-column chunks never straddle the boundary since kwrap % 64 == 0)
+F3_DEV int acol(const ConvGemmArgs& a, int k) { return (a.kwrap > 0 && k >= 2 * a.kwrap) ? k - 2 * a.kwrap : k; }
+
 // Parity-split rows for a stride-2 input gradient (see igemm_bf16). Measured on MI355X (B=256,
 // V=18): tcn layer 5 (Kc=256) 162 -> 144 us, but layer 3 (Kc=128, 2 k-chunks per tap) 85 ->
 // 94 us — with short per-tap k loops the halved MFMA work does not pay for the wider row

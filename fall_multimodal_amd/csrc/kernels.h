@@ -44,6 +44,10 @@ struct ConvGemmArgs {
   const unsigned short* auxb;  // RELUMASK source rows stored bf16 (instead of aux)
   BnRef epi_bn;
   int x3;             // 1: split-bf16 kernel (fp32 in / out; wb = hi plane, wb + Nc*KT*Kc = lo plane)
+  // bf16x3 on the bf16 kernels (K-concatenated, Kc = 3 kwrap): the activation rows hold [x_hi | x_lo]
+  // (2 kwrap columns, lda >= 2 kwrap) and the third K segment re-reads x_hi: A column k >= 2 kwrap
+  // is read at k - 2 kwrap (igemm_bf16 / igemm_big; 0 = off)
+  int kwrap;
 };
 
 enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };
@@ -85,8 +89,8 @@ struct WgradArgs {
   // [K*C][gcn_cin] instead (column k gcn_cin + ci of the packed operand -> row k C + c).
   int x3fold;
   float* db_fold;
-  // bf16x3 on the bf16 kernels by row segments (wgrad_big): dy / in are [hi | lo | hi] rows (ldy = 3 Nc,
-  // lda = 3 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi), (dY_lo, X_hi),
+  // bf16x3 on the bf16 kernels by row segments (wgrad_big): dy / in are [hi | lo] rows (ldy = 2 Nc,
+  // lda = 2 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi), (dY_lo, X_hi),
   // (dY_hi, X_lo) - the split product's three terms, no unused quadrant - with seg_splits row splits
   // per segment (set by the launcher); the bias sums the first two segments (dY_hi + dY_lo).
   // With gcn_cin > 0 the slab reduce writes the gcn layout (as x3fold).

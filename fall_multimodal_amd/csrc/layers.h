@@ -44,7 +44,7 @@ struct MixArgs {
   const unsigned short* dzb;  // bwd: dZ in bf16 (instead of z) — LDS mix path only
   int no_colsum;         // bwd: leave the dA partial rows in `part` (caller reduces: f3_mix_bwd_parts)
   int x3;                // bf16x3 mode: fp32 x / z / dz on the split-bf16 MFMA kernels (mix_*_x3)
-  unsigned short* z3;    // bf16x3 fwd: Z as rows [hi | lo | hi] of 3 K Cin bf16 (the K-concatenated gcn
+  unsigned short* z3;    // bf16x3 fwd: Z as rows [hi | lo] of 2 K Cin bf16 (the K-concatenated gcn
                          // GEMM / weight-gradient operand) instead of fp32 z
 };
 constexpr int kMixParts = 1024;
@@ -110,7 +110,7 @@ struct BlockArgs {
   unsigned short* dhb;   // bf16 mode: dh written as bf16 (GEMM operand) instead of fp32
   unsigned short* dresb; // bf16 mode, conv residual: dr as bf16 instead of fp32
   int x3;                // bf16x3 mode: dhb, dresb (backward) and outb (forward) receive rows
-                         // [hi | lo | hi] of 3C bf16 (the K-concatenated GEMM operands)
+                         // [hi | lo] of 2C bf16 (the K-concatenated GEMM operands)
   float* dgamma2;
   float* dbeta2;
   float* dgammar;
@@ -132,7 +132,7 @@ struct BnBwdArgs {
   float* Gpart;          // [gridDim][V*C] per-workgroup partial rows
   unsigned short* dgb;   // bf16 mode: dg as bf16 (GEMM operand) instead of fp32
   int no_colsum;         // leave the G partial rows in Gpart (caller reduces with f3_colsum)
-  int x3;                // bf16x3 mode: dgb receives dg as rows [hi | lo | hi] of 3C bf16
+  int x3;                // bf16x3 mode: dgb receives dg as rows [hi | lo] of 2C bf16
 };
 
 struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the bf16 mode
@@ -141,7 +141,7 @@ struct BnReluArgs {      // u = relu(bn(g)) as bf16: the tcn GEMM operand of the
   BnRef bn;
   const float* g;
   unsigned short* u;
-  int x3;                // bf16x3 mode: u as rows [hi | lo | hi] of 3C bf16 (fp32 g)
+  int x3;                // bf16x3 mode: u as rows [hi | lo] of 2C bf16 (fp32 g)
 };
 
 struct CaArgs {
@@ -211,7 +211,7 @@ int f3_mix_bwd(const f3::MixArgs* a, hipStream_t s);
 int f3_mix_bwd_parts(const f3::MixArgs* a);  // dA partial rows the LDS mix backward leaves (0: none)
 bool f3_mix_lds_ok(int K, int V, int Cin);  // the LDS/MFMA mix path (takes bf16 dZ)
 bool f3_mix_x3_ok(int K, int V, int Cin);   // the split-bf16 mix kernels (bf16x3 mode; MixArgs::z3)
-int f3_split_x3(const float* x, unsigned short* out, long long rows, int C, hipStream_t s);  // [hi | lo | hi] rows
+int f3_split_x3(const float* x, unsigned short* out, long long rows, int C, hipStream_t s);  // [hi | lo] rows
 int f3_gcn_bias_bwd(const f3::GcnBiasBwdArgs* a, hipStream_t s);
 bool f3_gcn0_ok(int K, int V, int Ci, int C);
 int f3_gcn0_fwd(const f3::Gcn0Args* a, hipStream_t s);

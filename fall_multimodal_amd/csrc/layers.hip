@@ -957,10 +957,10 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
         const f32x4 acc = mfma_x3m(xah, xal, bhi[nt], blo[nt], f32x4{0.f, 0.f, 0.f, 0.f});
         // lane holds Z[wk][c = 16 mt + 4 fg + r], r = 0..3: one 16-B piece of row wk
         if (wk < KV) {
-          if (a.z3) {  // GEMM row (f, w = wk / K) of [hi | lo | hi] over 3 K Cin, column k Cin + c
+          if (a.z3) {  // GEMM row (f, w = wk / K) of [hi | lo] over 2 K Cin, column k Cin + c
             const int w = wk / K, k = wk - w * K;
             char* row = reinterpret_cast<char*>(a.z3) +
-                        2 * (((size_t)f * V + w) * 3 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg);
+                        2 * (((size_t)f * V + w) * 2 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg);
             bf16x4 h, l;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -969,7 +969,6 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
             }
             *reinterpret_cast<bf16x4*>(row) = h;
             *reinterpret_cast<bf16x4*>(row + 2 * K * CIN) = l;
-            *reinterpret_cast<bf16x4*>(row + 4 * K * CIN) = h;
           } else {
             *reinterpret_cast<f32x4*>(zf + (size_t)wk * CIN + 16 * mt + 4 * fg) = acc;
           }
@@ -1216,11 +1215,10 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
           ob[e] = (__bf16)o[e];
           lb[e] = (__bf16)(o[e] - (float)ob[e]);
         }
-        if (a.x3) {  // row [hi | lo | hi] of 3C: the next block's K-concatenated residual-conv operand
-          __bf16* row = reinterpret_cast<__bf16*>(a.outb) + 3 * (off[u] - c0) + c0;
+        if (a.x3) {  // row [hi | lo] of 2C: the next block's K-concatenated residual-conv operand
+          __bf16* row = reinterpret_cast<__bf16*>(a.outb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = ob;
           *reinterpret_cast<bf16x4*>(row + C) = lb;
-          *reinterpret_cast<bf16x4*>(row + 2 * C) = ob;
         } else {
           *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.outb) + off[u]) = ob;
         }
@@ -1374,11 +1372,10 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
           hb[e] = (__bf16)dh[e];
           lb[e] = (__bf16)(dh[e] - (float)hb[e]);
         }
-        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated tcn operand), lo = RNE bf16(dh - hi)
-          __bf16* row = reinterpret_cast<__bf16*>(a.dhb) + 3 * (off[u] - c0) + c0;
+        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated tcn operand), lo = RNE bf16(dh - hi)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dhb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = hb;
           *reinterpret_cast<bf16x4*>(row + C) = lb;
-          *reinterpret_cast<bf16x4*>(row + 2 * C) = hb;
         } else {
           *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dhb) + off[u]) = hb;
         }
@@ -1392,11 +1389,10 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
           rb[e] = (__bf16)dr[e];
           rl[e] = (__bf16)(dr[e] - (float)rb[e]);
         }
-        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated residual dgrad / wgrad operand)
-          __bf16* row = reinterpret_cast<__bf16*>(a.dresb) + 3 * (off[u] - c0) + c0;
+        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated residual dgrad / wgrad operand)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dresb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = rb;
           *reinterpret_cast<bf16x4*>(row + C) = rl;
-          *reinterpret_cast<bf16x4*>(row + 2 * C) = rb;
         } else {
           *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dresb) + off[u]) = rb;
         }
@@ -1496,11 +1492,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
           ob[e] = (__bf16)o[e];
           lb[e] = (__bf16)(o[e] - (float)ob[e]);
         }
-        if (a.x3) {  // row [hi | lo | hi] of 3C (the K-concatenated gcn dgrad / wgrad operand)
-          __bf16* row = reinterpret_cast<__bf16*>(a.dgb) + 3 * (off - c0) + c0;
+        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated gcn dgrad / wgrad operand)
+          __bf16* row = reinterpret_cast<__bf16*>(a.dgb) + 2 * (off - c0) + c0;
           *reinterpret_cast<bf16x8*>(row) = ob;
           *reinterpret_cast<bf16x8*>(row + C) = lb;
-          *reinterpret_cast<bf16x8*>(row + 2 * C) = ob;
         } else {
           *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.dgb) + off) = ob;
         }
@@ -1563,12 +1558,11 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
         l[4 + e] = (__bf16)(u1 - (float)o[4 + e]);
       }
     }
-    if constexpr (X3) {  // row [hi | lo | hi] of 3C (the K-concatenated tcn operand)
+    if constexpr (X3) {  // row [hi | lo] of 2C (the K-concatenated tcn operand; kwrap re-reads hi)
       const long long e0 = qq * 8, m = e0 / a.C, c = e0 - m * a.C;
-      __bf16* row = reinterpret_cast<__bf16*>(a.u) + m * 3 * a.C + c;
+      __bf16* row = reinterpret_cast<__bf16*>(a.u) + m * 2 * a.C + c;
       *reinterpret_cast<bf16x8*>(row) = o;
       *reinterpret_cast<bf16x8*>(row + a.C) = l;
-      *reinterpret_cast<bf16x8*>(row + 2 * a.C) = o;
     } else {
       *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.u) + qq * 8) = o;
     }
@@ -2086,8 +2080,8 @@ static bool mix_x3_ok(const MixArgs& a) {
          a.V <= 32;
 }
 
-// bf16x3 K-concatenated operand rows: out[r] = [hi | lo | hi] of x[r] (3C bf16), hi = RNE bf16(x),
-// lo = RNE bf16(x - hi). One thread per 4 channels: a 16-B read, three 8-B writes.
+// bf16x3 K-concatenated operand rows: out[r] = [hi | lo] of x[r] (2C bf16), hi = RNE bf16(x),
+// lo = RNE bf16(x - hi). One thread per 4 channels: a 16-B read, two 8-B writes.
 __global__ __launch_bounds__(256) void split_x3cat_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                           long long n4, int C4) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
@@ -2100,10 +2094,9 @@ __global__ __launch_bounds__(256) void split_x3cat_kernel(const float* __restric
       h[e] = (__bf16)v[e];
       l[e] = (__bf16)(v[e] - (float)h[e]);
     }
-    __bf16* row = out + r * 3 * C + c;
+    __bf16* row = out + r * 2 * C + c;
     *reinterpret_cast<bf16x4*>(row) = h;
     *reinterpret_cast<bf16x4*>(row + C) = l;
-    *reinterpret_cast<bf16x4*>(row + 2 * C) = h;
   }
 }
 

@@ -415,14 +415,14 @@ Ws plan(const f3_net& net, int N, char* base) {
       const size_t Mi = (size_t)N * L.T_in * V, Mo = (size_t)N * L.T_out * V;
       const int C = L.cout, Ci = L.cin;
       // bf16x3 with the split-bf16 graph mix (Ci = 64 / 128 / 256): the gcn GEMM operands Z and dg
-      // as rows [hi | lo | hi] of 3 K Ci / 3C bf16 (1.5x the fp32 slot), the packed weights K-concatenated
+      // as rows [hi | lo] of 2 K Ci / 2C bf16 (the fp32 slot), the packed weights K-concatenated
       const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);
       X.x = xin;
       X.xb = xinb;
-      X.z = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mi * K * Ci)) : A.take<float>(Mi * K * Ci);
+      X.z = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(2 * Mi * K * Ci)) : A.take<float>(Mi * K * Ci);
       X.g = A.take<float>(Mi * C);
-      // u = relu(bn1(g)): bf16 (bf16 mode) or rows [hi | lo | hi] of 3C bf16 (bf16x3 mode)
-      if (hb || x3) X.u = A.take<unsigned short>((x3 ? 3 : 1) * Mi * C);
+      // u = relu(bn1(g)): bf16 (bf16 mode) or rows [hi | lo] of 2C bf16 (bf16x3 mode)
+      if (hb || x3) X.u = A.take<unsigned short>((x3 ? 2 : 1) * Mi * C);
       X.h = A.take<float>(Mo * C);
       if (L.res == RES_CONV) X.r = A.take<float>(Mo * C);
       X.out = A.take<float>(Mo * C);
@@ -444,17 +444,17 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dbn = A.take<float>((size_t)N * C / 4);
       X.dq1 = A.take<float>((size_t)N * C / 4);
       X.e = A.take<float>((size_t)N * C);
-      X.dh = reinterpret_cast<float*>(A.take<unsigned short>(Mo * C * (x3 ? 3 : 2)));  // x3: [hi | lo | hi] rows
-      X.dg = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mi * C)) : A.take<float>(Mi * C);
+      X.dh = reinterpret_cast<float*>(A.take<unsigned short>(Mo * C * 2));  // x3: [hi | lo] rows
+      X.dg = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(2 * Mi * C)) : A.take<float>(Mi * C);
       X.gpart = A.take<float>((size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
       X.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
-      // (bf16x3: dres as rows [hi | lo | hi] of 3C bf16)
-      if (L.res == RES_CONV) X.dres = x3 ? reinterpret_cast<float*>(A.take<unsigned short>(3 * Mo * C)) : A.take<float>(Mo * C);
+      // (bf16x3: dres as rows [hi | lo] of 2C bf16)
+      if (L.res == RES_CONV) X.dres = x3 ? reinterpret_cast<float*>(A.take<unsigned short>(2 * Mo * C)) : A.take<float>(Mo * C);
       xin = X.out;
       // bf16 mode: the block output itself is stored bf16 (the next block's residual-conv operand);
-      // bf16x3: a [hi | lo | hi] copy of it when the next block has a residual conv
+      // bf16x3: a [hi | lo] copy of it when the next block has a residual conv
       xinb = hb ? reinterpret_cast<const unsigned short*>(X.out) : nullptr;
-      if (x3 && l < 6 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(3 * Mo * C);
+      if (x3 && l < 6 && S.L[l + 1].res == RES_CONV) xinb = X.outb = A.take<unsigned short>(2 * Mo * C);
       maxMC = std::max(maxMC, std::max(Mi * C, Mi * Ci));
       maxMC = std::max(maxMC, Mo * C);
       maxZ = std::max(maxZ, Mi * K * Ci);
@@ -661,7 +661,8 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
       if (gcat) {  // [Z_hi | Z_lo | Z_hi] x [W_hi | W_hi | W_lo] over 3 K Ci on the bf16 kernels
         ga.x3 = 0; ga.in = nullptr; ga.inb = bfa(X.z, 1);
-        ga.g = geom(Mi, C, 3 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, C);
+        ga.g = geom(Mi, C, 3 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, C);
+        ga.kwrap = K * Ci;
       }
       F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     }
@@ -676,7 +677,8 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       if (x3) {  // the previous block's [x_hi | x_lo | x_hi] copy against [W_hi | W_hi | W_lo]
         if (!X.xb) return F3_ESTATE;
         ra.x3 = 0; ra.in = nullptr; ra.inb = X.xb;
-        ra.g = geom(Mo, C, 3 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, C);
+        ra.g = geom(Mo, C, 3 * Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
+        ra.kwrap = Ci;
       }
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
@@ -693,7 +695,10 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       std::memset(&br, 0, sizeof(br));
       br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = hb; br.x3 = x3;
       F3_TRY(f3_bnrelu_bf16(&br, s));
-      if (x3) ta.g = geom(Mo, C, 3 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, C);
+      if (x3) {
+        ta.g = geom(Mo, C, 3 * C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
+        ta.kwrap = C;
+      }
       ta.inb = X.u; ta.zero = w.zero;
       F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
     } else {
@@ -797,7 +802,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.dres = L.res == RES_CONV ? dres : (L.res == RES_ID ? dx : nullptr);
     ba.dhb = bfa(dh, hb || x3);  // bf16x3: dh as split hi / lo planes (the tcn dgrad / wgrad operand)
     ba.x3 = x3;
-    ba.dresb = L.res == RES_CONV ? bfa(dres, hb || x3) : nullptr;  // bf16x3: [hi | lo | hi] rows
+    ba.dresb = L.res == RES_CONV ? bfa(dres, hb || x3) : nullptr;  // bf16x3: [hi | lo] rows
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
@@ -828,7 +833,10 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
     td.in = (hb || x3) ? nullptr : dh; td.inb = bfa(dh, hb || x3); td.zero = w.zero;
     td.w = X.twT; td.wb = bf(X.twT, wq); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
-    if (x3) td.g = geom(Mi, C, 3 * C, 9, L.stride, 4, 1, Ti, To, V, 3 * C, C);  // K-concatenated dh rows
+    if (x3) {  // K-concatenated dh rows
+      td.g = geom(Mi, C, 3 * C, 9, L.stride, 4, 1, Ti, To, V, 2 * C, C);
+      td.kwrap = C;
+    }
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     if (part & 1) F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
@@ -838,7 +846,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     bb.N = N; bb.TV = Ti * V; bb.C = C; bb.V = V; bb.bn = bn1; bb.bsum = X.bn1.bsum; bb.bsq = X.bn1.bsq;
     bb.dgamma = q.g(L.bn1.w); bb.dbeta = q.g(L.bn1.b); bb.dv = W.dv; bb.g = X.g; bb.dg = dg; bb.G = X.G;
     bb.Gpart = X.gpart; bb.dgb = bfa(dg, hb); bb.act16 = hb; bb.no_colsum = split;
-    const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);  // dg as [hi | lo | hi] rows (see plan)
+    const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);  // dg as [hi | lo] rows (see plan)
     if (gcat) { bb.dgb = bfa(dg, 1); bb.x3 = 1; }
     if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
@@ -862,7 +870,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
     if (gcat) {  // [dg_hi | dg_lo | dg_hi] x [W^T_hi | W^T_hi | W^T_lo] over 3C
       gd.x3 = 0; gd.in = nullptr; gd.inb = bfa(dg, 1);
-      gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 3 * C, K * Ci);
+      gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 2 * C, K * Ci);
+      gd.kwrap = C;
     }
     const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
@@ -885,7 +894,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       rd.w = X.rwT; rd.wb = bf(X.rwT, wq); rd.x3 = x3; rd.out = dx;
       if (x3) {  // K-concatenated over 3C
         rd.x3 = 0; rd.in = nullptr; rd.inb = bfa(dres, 1);
-        rd.g = geom(Mi, Ci, 3 * C, 1, L.stride, 0, 1, Ti, To, V, 3 * C, Ci);
+        rd.g = geom(Mi, Ci, 3 * C, 1, L.stride, 0, 1, Ti, To, V, 2 * C, Ci);
+        rd.kwrap = C;
       }
       if (part & 1) F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
     }
@@ -908,17 +918,17 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
-    } else if (x3) {  // on the bf16 kernels over the [hi | lo | hi] rows of dh and u: three row
+    } else if (x3) {  // on the bf16 kernels over the [hi | lo] rows of dh and u: three row
       // segments (dh_hi u_hi, dh_lo u_hi, dh_hi u_lo), or (F3_X3_FOLD=1) [dh_hi | dh_lo] x [u_hi | u_lo]
       // whose slab reduce keeps the hi*hi + hi*lo + lo*hi quadrants (and folds the bias scratch)
       tw.x3 = 0; tw.bf16 = 1;
-      tw.ldy = 3 * C; tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
+      tw.ldy = 2 * C; tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
       tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats * 4; tw.dw_ref = q.g(L.tcn_w);
       if (x3_fold()) {
-        tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, 2 * C);
+        tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, 2 * C);
         tw.x3fold = 1; tw.db = X.dbx3; tw.db_fold = q.g(L.tcn_b);
       } else {
-        tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 3 * C, C);
+        tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
         tw.x3seg = 1;
       }
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
@@ -938,13 +948,13 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
         if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
       } else if (x3) {  // row segments / quadrant fold as the tcn's
         rw.x3 = 0; rw.bf16 = 1;
-        rw.ldy = 3 * C; rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
+        rw.ldy = 2 * C; rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats * 4; rw.dw_ref = q.g(L.res_w);
         if (x3_fold()) {
-          rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, 2 * C);
+          rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, 2 * C);
           rw.x3fold = 1; rw.db = X.dbx3r; rw.db_fold = q.g(L.res_b);
         } else {
-          rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 3 * Ci, C);
+          rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
           rw.x3seg = 1;
         }
         if (!f3_wgrad_glds_ok(rw)) return F3_EINVAL;
@@ -976,13 +986,13 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
     if (gcat) {  // row segments (or quadrants) into the slab, reduced into the gcn layout
       gw.x3 = 0; gw.bf16 = 1; gw.outmap = WG_OUT_CONV;
-      gw.ldy = 3 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
+      gw.ldy = 2 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
       gw.slab = W.slab; gw.slab_cap = kWgradSlabFloats * 4; gw.dw_ref = q.g(L.gcn_w); gw.dw = nullptr;
       if (x3_fold()) {
-        gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, 2 * C);
+        gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, 2 * C);
         gw.x3fold = 1;
       } else {
-        gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, 3 * K * Ci, C);
+        gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, C);
         gw.x3seg = 1;
       }
       if (!f3_wgrad_glds_ok(gw)) return F3_EINVAL;
@@ -1728,7 +1738,8 @@ int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, flo
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.g = geom(N * T_out * V, Cout, 3 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, Cout);
+  a.g = geom(N * T_out * V, Cout, 3 * Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
+  a.kwrap = Cin;
   a.inb = static_cast<const unsigned short*>(x3); a.zero = test_zero_page();
   a.wb = static_cast<const unsigned short*>(wpack); a.out = out; a.bias = bias;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
@@ -1748,7 +1759,8 @@ int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.g = geom(N * T_in * V, Cin, 3 * Cout, KT, stride, pad, 1, T_in, T_out, V, 3 * Cout, Cin);
+  a.g = geom(N * T_in * V, Cin, 3 * Cout, KT, stride, pad, 1, T_in, T_out, V, 2 * Cout, Cin);
+  a.kwrap = Cout;
   a.inb = static_cast<const unsigned short*>(dy3); a.zero = test_zero_page();
   a.wb = static_cast<const unsigned short*>(wpack); a.out = dx;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
@@ -1765,15 +1777,15 @@ int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, fl
   if (!slab) return F3_EHIP;
   WgradArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.ldy = 3 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1;
+  a.ldy = 2 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1;
   a.dyb = static_cast<const unsigned short*>(dy3); a.inb = static_cast<const unsigned short*>(x3);
   a.zero = test_zero_page(); a.slab = slab; a.slab_cap = cap;
   const bool fold = x3_fold();  // as the step (F3_X3_FOLD)
   if (fold) {
-    a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, 2 * Cout);
+    a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, 2 * Cout);
     a.x3fold = 1;
   } else {
-    a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 3 * Cin, Cout);
+    a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
     a.x3seg = 1;
   }
   if (dw) {  // dw == NULL: the GEMM alone (partials left in the slab)

@@ -327,7 +327,7 @@ static int pw_wn(const ConvGeom& g, int epi) {
 bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   static const int on = getenv("F3_PW") ? atoi(getenv("F3_PW")) : 1;
   const ConvGeom& g = a.g;
-  if (!on || !a.inb || !a.wb || !a.zero) return false;
+  if (!on || !a.inb || !a.wb || !a.zero || a.kwrap) return false;
   if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
   if (g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
   if (!pw_wn(g, epi)) return false;

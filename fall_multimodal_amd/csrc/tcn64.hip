@@ -235,7 +235,7 @@ using namespace f3;
 bool f3_tcn64_ok(const ConvGemmArgs& a, int epi) {
   static const int on = getenv("F3_TCN64") ? atoi(getenv("F3_TCN64")) : 1;
   const ConvGeom& g = a.g;
-  if (!on || !a.inb || !a.wb || !a.zero || !a.outb) return false;
+  if (!on || !a.inb || !a.wb || !a.zero || !a.outb || a.kwrap) return false;
   if (g.Kc != 64 || g.Nc != 64 || g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out) return false;
   if (g.V > 18 || g.lda % 8 != 0 || g.ldo % 8 != 0 || g.T_out * g.V < T64_BM || g.M % (g.T_out * g.V) != 0) return false;
   if (epi == (EPI_BIAS | EPI_STATS | EPI_GAP)) return a.gap && a.st_sum && a.st_sq && a.bias;

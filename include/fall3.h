@@ -157,11 +157,12 @@ int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long s
                          int Cin, int Cout, int KT, int stride, int pad, void* stream);
 
 /* F3_PRECISION_BF16X3 as the training step runs it (K-concatenation on the bf16 LDS-DMA kernels):
- * f3_split_x3cat writes each fp32 row x[r][0..C) as the bf16 row [hi | lo | hi] of 3C (hi = RNE
- * bf16(x), lo = RNE bf16(x - hi)); the packed weight of a tap is [W_hi | W_hi | W_lo], so ONE bf16 GEMM
- * over 3C computes x_hi W_hi + x_lo W_hi + x_hi W_lo (the split product, ~2^-16 relative).
- * f3_conv_forward_x3cat / f3_conv_backward_data_x3cat: x3 / dy3 are such rows ([N,T,V,3Cin] /
- * [N,T_out,V,3Cout]); wpack is scratch of 1.5 * Cout*KT*Cin floats (w == NULL reuses it); out / dx
+ * f3_split_x3cat writes each fp32 row x[r][0..C) as the bf16 row [hi | lo] of 2C (hi = RNE bf16(x),
+ * lo = RNE bf16(x - hi)); the packed weight of a tap is [W_hi | W_hi | W_lo] and the GEMM's third K
+ * segment re-reads x_hi, so ONE bf16 GEMM over K = 3C computes x_hi W_hi + x_lo W_hi + x_hi W_lo (the
+ * split product, ~2^-16 relative).
+ * f3_conv_forward_x3cat / f3_conv_backward_data_x3cat: x3 / dy3 are such rows ([N,T,V,2Cin] /
+ * [N,T_out,V,2Cout]); wpack is scratch of 1.5 * Cout*KT*Cin floats (w == NULL reuses it); out / dx
  * fp32 as f3_conv_forward / f3_conv_backward_data (bias required, epilogue + bias).
  * f3_conv_backward_weight_x3cat: the bf16 weight-gradient GEMM over three row segments of the rows,
  * dy_hi x_hi + dy_lo x_hi + dy_hi x_lo (split-K partials summed into dw [Cout][Cin][KT]; db from
