@@ -95,6 +95,18 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const int kpt = g.Kc / G_BK;
   const int dt0 = par ? ((p + g.P) & 1) : 0;
   const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
+  const int ntap = par ? (g.KT - dt0 + 1) / 2 : g.KT;
+  // k step t -> (tap, channel chunk): tap-major, or chunk-major (ConvGemmArgs::kmajor)
+  auto tapchunk = [&](int t, int& tap, int& i0) {
+    if (a.kmajor) {
+      const int c = t / ntap;
+      tap = t - c * ntap;
+      i0 = c * G_BK;
+    } else {
+      tap = t / kpt;
+      i0 = (t - tap * kpt) * G_BK;
+    }
+  };
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
 
@@ -127,7 +139,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     }
   }
   auto stage = [&](int t, int buf) {
-    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    int tap, i0;
+    tapchunk(t, tap, i0);
     const int dt = par ? dt0 + 2 * tap : tap;
     const int k0 = dt * g.Kc + i0;
     char* sbase = smem + buf * STAGE;
@@ -158,7 +171,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   // BD: this lane's B fragments of chunk t, [ks][y] = W[wn*32 + y*16 + fr][k0 + (ks*4 + fg)*8 ..+8]
   bf16x8 fbr[2][BG_NT];
   auto load_b = [&](int t, bf16x8 (&f)[2][BG_NT]) {
-    const int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
+    int tap, i0;
+    tapchunk(t, tap, i0);
     const int dt = par ? dt0 + 2 * tap : tap;
     const int k0 = dt * g.Kc + i0;
 #pragma unroll
@@ -560,7 +574,12 @@ static bool big_win_ok(const ConvGemmArgs& a) {
 }
 
 int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
-  const ConvGemmArgs& a = *args;
+  // F3_BIG_KMAJOR=1: chunk-major k order in the tiled (non-window) kernel (ConvGemmArgs::kmajor)
+  static const int kmaj = getenv("F3_BIG_KMAJOR") ? atoi(getenv("F3_BIG_KMAJOR")) : 0;
+  ConvGemmArgs ak = *args;
+  ak.kmajor = kmaj;
+  const ConvGemmArgs& a = ak;
+  args = &ak;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   if (big_win_ok(a)) {

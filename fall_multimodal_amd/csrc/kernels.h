@@ -48,6 +48,10 @@ struct ConvGemmArgs {
   // (2 kwrap columns, lda >= 2 kwrap) and the third K segment re-reads x_hi: A column k >= 2 kwrap
   // is read at k - 2 kwrap (igemm_bf16 / igemm_big; 0 = off)
   int kwrap;
+  // igemm_big k order: 0 tap-major (all channel chunks of a tap, then the next tap), 1 chunk-major
+  // (the 9 taps of one 64-channel chunk back to back: a tile's rows +- 4 frames of that chunk stay
+  // in L2 across the taps instead of being re-fetched once per tap). Set by the launcher.
+  int kmajor;
 };
 
 enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };

@@ -698,14 +698,14 @@ __global__ __launch_bounds__(C1D_THREADS) void conv1d_bwd_kernel(Conv1dArgs a) {
 // Fused CNN1D (round 4): six launches instead of eight, and no same-address atomics. Each launch
 // walks the clips with a grid of <= kCnnGrid workgroups; its BatchNorm sums leave as one fp32
 // partial row per workgroup (plain stores, part[blk][2 Co]), and the NEXT launch's prologue adds the
-// rows in fp64 (every workgroup; <= 128 x 64 floats) before it needs the coefficients. Workgroup 0 of
+// rows in fp64 (every workgroup; <= kCnnGrid x 64 floats) before it needs the coefficients. Workgroup 0 of
 // that launch also stores the totals where the running-stat update / backward BnRef read them.
 //   fwd: F1 conv1 + BN1 rows | F2 BN1 + ReLU + pool1 (-> p1) + conv2 + BN2 rows | F3 BN2 + ReLU + pool2
 //   bwd: B1 pool2 / ReLU backward (-> dy2) + BN2-bwd rows | B2 BN2 apply backward, conv2 dW / db, dp1
 //        in LDS, pool1 / ReLU backward (-> dy1) + BN1-bwd rows | B3 BN1 apply backward, conv1 dW / db
 // (GSTCAN_UR_conv.ipynb:493-514: Conv1d(k5, p2) -> BatchNorm1d -> ReLU -> MaxPool1d(2), twice.)
 // ----------------------------------------------------------------------------
-constexpr int kCnnGrid = 128;
+constexpr int kCnnGrid = 1024;  // capacity of the partial-row buffers (workgroups per launch)
 
 // fp64 totals of a launch's partial rows: out[j] = sum_g part[g][j], j < n (every thread of the
 // workgroup takes part; result in LDS)
@@ -1120,7 +1120,12 @@ int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {
 }
 
 // ---- fused CNN1D entry points (six launches per step; see cnn_f1_kernel) ----
-static int cnn_grid(int N) { return std::max(1, std::min(N, kCnnGrid)); }
+// workgroups per fused launch: one per clip up to F3_CNN_GRID (default 1024; round 4's first
+// version used 128, i.e. two clips per workgroup at B = 256 on half the CUs)
+static int cnn_grid(int N) {
+  static const int cap = getenv("F3_CNN_GRID") ? std::max(1, std::min(kCnnGrid, atoi(getenv("F3_CNN_GRID")))) : kCnnGrid;
+  return std::max(1, std::min(N, cap));
+}
 
 long long f3_cnn1d_part_floats() { return 4LL * kCnnGrid * 64; }
 

@@ -3,7 +3,8 @@
 (tests/fr8_grads.py): the B=32 step's gradients and logits with FR=8 against FR=4 on the same
 weights and batch. T = 30 (position stream) and 29 (motion stream) are not multiples of 8, so the
 ragged last frame group of every clip is exercised. FR only changes how the per-node column sums
-are partitioned into partial rows, so the results agree to float-summation noise."""
+are partitioned into partial rows, so FR=8 must sit within the step's own run-to-run spread (float
+atomics order the reductions differently every run): measured against two FR=4 runs."""
 import os
 import subprocess
 import sys
@@ -14,6 +15,14 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _cmp(a, b):
+    ga, gb = a["grads"].astype(np.float64), b["grads"].astype(np.float64)
+    cos = float(ga @ gb / (np.linalg.norm(ga) * np.linalg.norm(gb)))
+    rel = float(np.abs(gb - ga).max() / np.abs(ga).max())
+    dl = float(np.abs(a["logits"] - b["logits"]).max())
+    return cos, rel, dl
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 def test_bn_bwd_apply_fr8_matches_fr4(precision, tmp_path):
@@ -21,16 +30,17 @@ def test_bn_bwd_apply_fr8_matches_fr4(precision, tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     res = {}
-    for fr in ("4", "8"):
-        out = tmp_path / f"fr{fr}.npz"
+    for tag, fr in (("4a", "4"), ("4b", "4"), ("8", "8")):
+        out = tmp_path / f"fr{tag}.npz"
         env = dict(os.environ, F3_BNBWD_FR=fr)
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "fr8_grads.py"), precision, str(out)],
                            capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        res[fr] = np.load(out)
-    g4, g8 = res["4"]["grads"].astype(np.float64), res["8"]["grads"].astype(np.float64)
-    np.testing.assert_allclose(res["8"]["logits"], res["4"]["logits"], rtol=0, atol=1e-5)
-    cos = float(g4 @ g8 / (np.linalg.norm(g4) * np.linalg.norm(g8)))
-    rel = float(np.abs(g8 - g4).max() / np.abs(g4).max())
-    print(f"{precision}: FR=8 vs FR=4 gradient cosine {cos:.9f}, max rel {rel:.2e}")
-    assert cos > 0.99999 and rel < 1e-3, (cos, rel)
+        res[tag] = np.load(out)
+    cos0, rel0, dl0 = _cmp(res["4a"], res["4b"])   # run-to-run floor
+    cos8, rel8, dl8 = _cmp(res["4a"], res["8"])
+    print(f"{precision}: FR=4 vs FR=4 cosine {cos0:.9f} rel {rel0:.2e} dlogit {dl0:.1e}; "
+          f"FR=8 vs FR=4 cosine {cos8:.9f} rel {rel8:.2e} dlogit {dl8:.1e}")
+    assert dl8 <= 4 * dl0 + 1e-5, (dl8, dl0)
+    assert rel8 <= 4 * rel0 + 2e-4, (rel8, rel0)
+    assert 1 - cos8 <= 4 * (1 - cos0) + 1e-7, (cos8, cos0)
