@@ -411,7 +411,9 @@ def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
         out[nm] = {"us": round(us, 2), "bytes": nbytes[nm], "GBps": round(nbytes[nm] / (us * 1e-6) / 1e9, 1)}
     out["total_us"] = round(sum(acc) * 1e3, 2)
     out["batch"] = B
-    out["note"] = ("HIP events around each launch on the sensor queue; six fused launches per step (round 4); "
+    fused = os.environ.get("F3_CNN_FUSED", "0") != "0"
+    out["form"] = "fused (6 launches, F3_CNN_FUSED=1)" if fused else "round-3 launches (the default; F3_CNN_FUSED=1 measured slower)"
+    out["note"] = ("HIP events around each stage on the sensor queue (a stage may hold several launches); "
                    "latency-bound (tensors of 0.02-1 MB): GB/s against 8 TB/s is not a meaningful fraction here")
     return out
 

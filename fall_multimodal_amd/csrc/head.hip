@@ -42,22 +42,38 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
 }
 
 // loss += -(1/N) sum_c y log_softmax(out);  dout = (softmax(out) * sum_c y - y) / N
+constexpr int kCeOneBlock = 4096;  // batches up to this size: the single-workgroup form
+
+// ONE: a single 256-thread workgroup walks every row and stores the mean loss (no zeroed loss word
+// beforehand, no atomics: deterministic); otherwise one row per thread, atomics into a zeroed loss
+template <bool ONE>
 __global__ void ce_kernel(HeadArgs a) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= a.N) return;
-  const float* o = a.out + (size_t)n * a.C;
-  const float* y = a.label + (size_t)n * a.C;
-  float mx = -INFINITY;
-  for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, o[c]);
-  float s = 0.f, ys = 0.f;
-  for (int c = 0; c < a.C; ++c) { s += expf(o[c] - mx); ys += y[c]; }
-  const float lse = mx + logf(s);
-  float l = 0.f;
-  for (int c = 0; c < a.C; ++c) {
-    l -= y[c] * (o[c] - lse);
-    a.dout[(size_t)n * a.C + c] = (expf(o[c] - lse) * ys - y[c]) / (float)a.N;
+  float lsum = 0.f;
+  const int n0 = ONE ? threadIdx.x : blockIdx.x * blockDim.x + threadIdx.x;
+  for (int n = n0; n < a.N; n += ONE ? blockDim.x : a.N) {
+    const float* o = a.out + (size_t)n * a.C;
+    const float* y = a.label + (size_t)n * a.C;
+    float mx = -INFINITY;
+    for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, o[c]);
+    float s = 0.f, ys = 0.f;
+    for (int c = 0; c < a.C; ++c) { s += expf(o[c] - mx); ys += y[c]; }
+    const float lse = mx + logf(s);
+    float l = 0.f;
+    for (int c = 0; c < a.C; ++c) {
+      l -= y[c] * (o[c] - lse);
+      a.dout[(size_t)n * a.C + c] = (expf(o[c] - lse) * ys - y[c]) / (float)a.N;
+    }
+    lsum += l;
   }
-  atomic_add_f(a.loss, l / (float)a.N);
+  if constexpr (ONE) {
+    __shared__ float red[4];
+    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) *a.loss = (red[0] + red[1] + red[2] + red[3]) / (float)a.N;
+  } else {
+    if (n0 < a.N) atomic_add_f(a.loss, lsum / (float)a.N);
+  }
 }
 
 // dlogits from the gradient of the module output (softmax Jacobian for the notebook form)
@@ -200,7 +216,12 @@ int f3_head_fwd(const HeadArgs* a, hipStream_t s) {
 }
 
 int f3_ce(const HeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(ce_kernel, dim3((a->N + 255) / 256), dim3(256), 0, s, *a);
+  if (a->N <= kCeOneBlock) {
+    hipLaunchKernelGGL(ce_kernel<true>, dim3(1), dim3(256), 0, s, *a);
+  } else {
+    if (hipMemsetAsync(a->loss, 0, sizeof(float), s) != hipSuccess) return F3_EHIP;
+    hipLaunchKernelGGL(ce_kernel<false>, dim3((a->N + 255) / 256), dim3(256), 0, s, *a);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

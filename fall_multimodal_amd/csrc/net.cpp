@@ -277,9 +277,13 @@ struct BnWs {
   double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
 };
 
-// F3_CNN_FUSED=0: the round-3 CNN1D launches (8 per step, same-address fp64 atomics) for A/B
+// F3_CNN_FUSED=1: the fused CNN1D launches (6 per step, per-workgroup BN partial rows reduced by the
+// next launch; sensor.hip cnn_f*/cnn_b*). Off by default: measured SLOWER than the round-3 launches
+// at B = 256 (224 / 303 us with 128 / 256 workgroups vs 127 us; profiles/r04_cnn1d_ab.txt) - every
+// workgroup re-reads all partial rows in its prologue, and a clip per workgroup leaves each stage a
+// short dependent chain
 inline bool cnn_fused() {
-  static const bool on = !getenv("F3_CNN_FUSED") || atoi(getenv("F3_CNN_FUSED")) != 0;
+  static const bool on = getenv("F3_CNN_FUSED") && atoi(getenv("F3_CNN_FUSED")) != 0;
   return on;
 }
 
@@ -1388,7 +1392,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
 int f3_net_loss(f3_net* net, int N, const float* out, const float* label, float* loss, float* dout, void* stream) {
   if (!net || !out || !label || !loss || !dout) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(loss, 0, sizeof(float), s) != hipSuccess) return F3_EHIP;
+  // (f3_ce stores the loss; larger batches zero it and accumulate)
   HeadArgs h;
   std::memset(&h, 0, sizeof(h));
   h.N = N; h.C = net->cfg.num_class; h.out = const_cast<float*>(out); h.label = label; h.loss = loss; h.dout = dout;

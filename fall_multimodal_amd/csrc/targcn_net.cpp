@@ -572,7 +572,7 @@ int f3_targcn_status(f3_targcn* net, int wait) {
 int f3_soft_ce(const float* out, const float* label, int N, int C, float* loss, float* dout, void* stream) {
   if (!out || !label || !loss || !dout || N < 1 || C < 1) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(loss, 0, sizeof(float), s) != hipSuccess) return F3_EHIP;
+  // (f3_ce stores the loss; larger batches zero it and accumulate)
   HeadArgs h;
   std::memset(&h, 0, sizeof(h));
   h.N = N; h.C = C; h.out = const_cast<float*>(out); h.label = label; h.loss = loss; h.dout = dout;
