@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -1335,8 +1336,11 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
   Branches br{*net, s, ensure_parallel(*net, s)};
   br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0);
   F3_TRY(br.fork());
-  // sensor branch first (small, latency-bound), then the two skeleton streams stage by stage,
-  // interleaved, so every branch queue is fed from the start
+  // the skeleton streams' weight prep + data_bn first (the motion stream's queue waited ~130 us for
+  // the host to submit the sensor branch ahead of it), then the sensor branch (small, latency-bound),
+  // then the skeleton streams stage by stage, interleaved, so every branch queue is fed early
+  for (int si = 0; si < net->nstreams; ++si)
+    F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, br.at(si), -1));
   if (net->has_sensor) {
     const hipStream_t ss = br.at(2);
     LstmArgs la;
@@ -1371,7 +1375,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     F3_TRY(f3_shead_fwd(&sa, ss));
     if (training) add_bnrun(run, q, net->lstm.bn, w.sbn.fsum, w.sbn.fsq, N);
   }
-  for (int stage = -1; stage < 7; ++stage)
+  for (int stage = 0; stage < 7; ++stage)
     for (int si = 0; si < net->nstreams; ++si)
       F3_TRY(stream_forward(*net, si, N, training, q, w, w.skel, run, br.at(si), stage));
   F3_TRY(br.join());
@@ -1502,7 +1506,9 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
   }
   // skeleton streams layer by layer, interleaved (see stream_forward), then each stream's
   // packed weight-gradient unpack
-  auto skeleton = [&](Branches& br, int l_hi, int l_lo) -> int {
+  // after_first: called once the first layer's main chains are submitted (the sensor backward, so its
+  // host submission does not hold back the skeleton streams' first layer)
+  auto skeleton = [&](Branches& br, int l_hi, int l_lo, const std::function<int()>& after_first) -> int {
     PrepTable unpack[2];
     unpack[0].n = unpack[1].n = 0;
     // Each layer's main chains are submitted before the previous layer's side-stream work (the
@@ -1520,6 +1526,7 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
                                defer ? 1 : 3));
         if (debug_stop(si, l)) return F3_OK;  // leave the scratch as is for f3_net_debug_tensor
       }
+      if (l == l_hi && after_first) F3_TRY(after_first());
       if (defer && l < l_hi)
         for (int si = 0; si < net->nstreams; ++si)
           F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, unpack[si], side_of(si, l + 1),
@@ -1540,7 +1547,7 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) |
               (net->nstreams > 0 ? BR_SIDE : 0);
     F3_TRY(br.fork());
-    F3_TRY(skeleton(br, kSplitLayer - 1, 0));
+    F3_TRY(skeleton(br, kSplitLayer - 1, 0, nullptr));
     F3_TRY(br.join());
     F3_TRY(wait_phase1(*net, s));  // phase 1's queues (e.g. the sensor queue) are done too
     net->p1_mask = 0;
@@ -1565,7 +1572,8 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
   static const bool no_side = getenv("F3_NO_SIDE") != nullptr;
   br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) | (net->nstreams > 0 && !no_side ? BR_SIDE : 0);
   F3_TRY(br.fork());
-  if (net->has_sensor) {
+  auto sensor_bwd = [&]() -> int {
+    if (!net->has_sensor) return F3_OK;
     const hipStream_t ss = br.at(2);
     F3_TRY(f3_shead_bwd(&sa, ss));
     F3_TRY(f3_lstm_bwd(&la, ss));
@@ -1583,8 +1591,14 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
       F3_TRY(f3_conv1d_bwd(&c1, ss));
       net->smark(7, ss);
     }
-  }
-  F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0));
+    return F3_OK;
+  };
+  // the skeleton streams' first layer is submitted before the sensor backward (F3_SENSOR_FIRST=1:
+  // the round-3 order); a sensor-only model has no skeleton layer to wait for
+  static const bool sensor_first = getenv("F3_SENSOR_FIRST") && atoi(getenv("F3_SENSOR_FIRST")) != 0;
+  if (sensor_first || net->nstreams == 0) F3_TRY(sensor_bwd());
+  F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0, sensor_first || net->nstreams == 0 ? std::function<int()>()
+                                                                                              : std::function<int()>(sensor_bwd)));
   if (phase == 1) return br.mark_phase1();  // the caller orders its all-reduce after f3_net_wait_phase1
   F3_TRY(br.join());
   return F3_OK;
