@@ -42,7 +42,6 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   constexpr int WIN_OFF = NST * STAGE, WIN_BYTES = WIN ? G_WIN_ROWS * 128 : 0;
   constexpr int SMEM_MAIN = WIN_OFF + WIN_BYTES > 16 * 1024 + BM * (BN + 8) * 2 ? WIN_OFF + WIN_BYTES
                                                                                  : 16 * 1024 + BM * (BN + 8) * 2;
-  static_assert(!WIN || NST == 2, "window mode uses the 2-stage loop");
   // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code): NST
   // stages (and the window), then the epilogue coefficient tables; the reductions reuse stage 0.
   __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN + 4 * BN * 4];
@@ -169,6 +168,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else {  // NST == 3: two stages in flight; raw barriers keep the newest one in flight
+    if (WIN) load_win(0);  // (older than both stages: the counted wait below covers it)
     stage(0, 0);
     if (nchunk > 1) {
       stage(1, 1);
@@ -435,12 +435,18 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (f3_tcn64_ok(a, epi)) return f3_tcn64(args, epi, s);
   if (f3_pw_ok(a, epi)) return f3_pw_gemm(args, epi, s);
   if (igemm_win_ok(a, epi)) {
+    // F3_WIN_STAGES=3: three weight stages (two in flight across the raw end-of-step barrier)
+    static const int wst = getenv("F3_WIN_STAGES") && atoi(getenv("F3_WIN_STAGES")) == 3 ? 3 : 2;
+    if (wst == 3) {
+      if (a.g.Nc == 128) return launch_igemm<4, 3, true>(a, epi, s);
+      return launch_igemm<2, 3, true>(a, epi, s);
+    }
     if (a.g.Nc == 128) return launch_igemm<4, 2, true>(a, epi, s);
     return launch_igemm<2, 2, true>(a, epi, s);
   }
   if (f3_igemm_big_ok(a)) return f3_igemm_big(args, epi, s);
   if (igemm_stages() == 3) {
-    if (a.g.Nc > 64) return launch_igemm<4, 3>(a, epi, s);
+    if (a.g.Nc > 64 && a.g.Nc % 128 == 0) return launch_igemm<4, 3>(a, epi, s);
     return launch_igemm<2, 3>(a, epi, s);
   }
   // 128-wide column tiles unless they would leave a partial tile (Nc = 192: the gcn input
