@@ -114,6 +114,7 @@ def launch_check(world, rank):
 
 
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r04_roofline_pmc.json")
+RGB_PMC = os.path.join(ROOT, "profiles", "r04_rgb_pmc.json")
 
 
 def _time_launch(fn, reps=20):
@@ -834,9 +835,14 @@ def rgb_bench(dev, B=256, T=30, reps=10):
     out = {"workload": f"rgb_spatial_conv_B{B}_T{T}_224x224x3_bf16", "parity": "unpinned (build-defined branch)",
            "clips_per_s_fwd_bwd": round(B / (t_f + t_b), 1), "fwd_ms": round(t_f * 1e3, 4), "bwd_ms": round(t_b * 1e3, 4),
            "bytes_per_pass": nbytes}
+    pmc = {}
+    if os.path.exists(RGB_PMC):  # HBM bytes per launch from rocprofv3 PMC (tools/rgb_pmc.py)
+        with open(RGB_PMC) as f:
+            pmc = json.load(f)
     for k, t in (("fwd", t_f), ("bwd", t_b)):
         out["roofline_" + k] = {"bound": "hbm", "achieved": round(nbytes / t / 1e9, 1), "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": round(nbytes / t / 1e9 / PEAK_HBM_GBS, 4), "traffic": None}
+                                "unit": "GB/s", "frac": round(nbytes / t / 1e9 / PEAK_HBM_GBS, 4),
+                                "traffic": (pmc.get(k) or {}).get("bytes_per_launch")}
     del frames
     torch.cuda.empty_cache()
     return out

@@ -895,7 +895,9 @@ F3_DEV f32x4 mfma_x3m(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
   return mfma_bf16x(ah, bh, c);
 }
 
-template <int CIN>
+// ZI (z3 output): the frame's Z rows [hi | lo] are assembled in an LDS image and leave as one
+// contiguous V x 4 K CIN-byte block of 16-B pieces (the per-fragment stores wrote 32-B runs per row)
+template <int CIN, bool ZI = false>
 __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
   constexpr int RB = 2 * CIN + 16, XR = 32, C4 = CIN / 4;
   constexpr int PX = (18 * C4 + 255) / 256;
@@ -940,6 +942,7 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
     __syncthreads();
     if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
     float* zf = a.z + (size_t)f * KV * CIN;
+    char* zimg = smb + 2 * XR * RB;  // ZI: [V][2 K CIN] bf16
     for (int mt = wave; mt < CIN / 16; mt += 4) {
       const int o = (8 * fg + (fr >> 2)) * RB + 32 * mt + 8 * (fr & 3);
       const unsigned ph = (unsigned)(size_t)(mx_lds_t*)(xh + o), pl = (unsigned)(size_t)(mx_lds_t*)(xl + o);
@@ -959,8 +962,9 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
         if (wk < KV) {
           if (a.z3) {  // GEMM row (f, w = wk / K) of [hi | lo] over 2 K Cin, column k Cin + c
             const int w = wk / K, k = wk - w * K;
-            char* row = reinterpret_cast<char*>(a.z3) +
-                        2 * (((size_t)f * V + w) * 2 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg);
+            char* row = ZI ? zimg + 2 * ((size_t)w * 2 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg)
+                           : reinterpret_cast<char*>(a.z3) +
+                                 2 * (((size_t)f * V + w) * 2 * K * CIN + (size_t)k * CIN + 16 * mt + 4 * fg);
             bf16x4 h, l;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -974,6 +978,13 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
           }
         }
       }
+    }
+    if constexpr (ZI) {  // the frame's image -> its contiguous Z rows
+      __syncthreads();
+      const int n16 = V * K * CIN / 2;  // V rows x 4 K CIN bytes / 16
+      uint4* dst = reinterpret_cast<uint4*>(a.z3 + (size_t)f * V * 2 * K * CIN);
+      const uint4* srcv = reinterpret_cast<const uint4*>(zimg);
+      for (int i = tid; i < n16; i += 256) dst[i] = srcv[i];
     }
   }
 }
@@ -2050,6 +2061,19 @@ template <int CIN>
 static size_t mix_x3_lds_bwd() { return (size_t)192 * (2 * CIN + 16); }
 template <int CIN>
 static int launch_mix_fwd_x3(const MixArgs* a, hipStream_t s) {
+  // z3 output through the frame image (F3_MIX_ZIMG=1; default: per-fragment stores)
+  static const bool zimg_on = getenv("F3_MIX_ZIMG") && atoi(getenv("F3_MIX_ZIMG")) != 0;
+  if (a->z3 && zimg_on) {
+    const size_t lds = mix_x3_lds_fwd<CIN>() + (size_t)a->V * 4 * a->K * CIN;
+    if (lds > 160 * 1024) return F3_EINVAL;
+    static size_t lds0 = lds;
+    static const int slots = (allow_big_lds((const void*)mix_fwd_x3_kernel<CIN, true>),
+                              resident_slots(mix_fwd_x3_kernel<CIN, true>, lds0));
+    const int grid = std::max(1, std::min(a->frames, lds == lds0 ? slots : 256));
+    hipLaunchKernelGGL((mix_fwd_x3_kernel<CIN, true>), dim3(grid), dim3(256), lds, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   static const int slots = resident_slots(mix_fwd_x3_kernel<CIN>, mix_x3_lds_fwd<CIN>());
   const int grid = std::max(1, std::min(a->frames, slots));
   hipLaunchKernelGGL(mix_fwd_x3_kernel<CIN>, dim3(grid), dim3(256), mix_x3_lds_fwd<CIN>(), s, *a);

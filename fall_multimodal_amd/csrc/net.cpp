@@ -1892,13 +1892,15 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
 
 int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int frames, int K, int V, int Cin, int flags,
                             void* stream) {
-  if (!A_eff || !x || !z || frames < 0 || (flags & ~7) || ((flags & F3_MIX_X3) && (flags & 3))) return F3_EINVAL;
+  if (!A_eff || !x || !z || frames < 0 || (flags & ~15) || ((flags & F3_MIX_X3) && (flags & 3))) return F3_EINVAL;
+  if ((flags & F3_MIX_Z3) && !(flags & F3_MIX_X3)) return F3_EINVAL;
   MixArgs m;
   std::memset(&m, 0, sizeof(m));
   m.K = K; m.V = V; m.Cin = Cin; m.frames = frames; m.A = A_eff;
   m.x = static_cast<const float*>(x); m.x16 = flags & F3_MIX_X_BF16; m.x3 = (flags & F3_MIX_X3) != 0;
   m.z = static_cast<float*>(z);
   if (flags & F3_MIX_Z_BF16) m.zb = static_cast<unsigned short*>(z);
+  if (flags & F3_MIX_Z3) m.z3 = static_cast<unsigned short*>(z);
   return f3_mix_fwd(&m, (hipStream_t)stream);
 }
 

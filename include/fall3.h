@@ -207,8 +207,10 @@ int f3_graph_mix_backward(const float* A_eff, const float* x, const float* dz, f
                           int V, int Cin, void* stream);
 /* The same with the bf16 mode's operand types: F3_MIX_X_BF16 -> x (and, backward, dz) bf16;
  * F3_MIX_Z_BF16 -> forward z written bf16 (the gcn GEMM's operand, as the step stores it);
- * F3_MIX_X3 -> fp32 operands on the bf16x3 (split-bf16) MFMA kernels of F3_PRECISION_BF16X3. */
-enum { F3_MIX_X_BF16 = 1, F3_MIX_Z_BF16 = 2, F3_MIX_X3 = 4 };
+ * F3_MIX_X3 -> fp32 operands on the bf16x3 (split-bf16) MFMA kernels of F3_PRECISION_BF16X3;
+ * F3_MIX_Z3 (with F3_MIX_X3) -> forward z written as the step stores it for the gcn GEMM: per (frame,
+ * node) one bf16 row [z_hi | z_lo] of 2 K Cin (z_hi = RNE bf16(z), z_lo = RNE bf16(z - z_hi)). */
+enum { F3_MIX_X_BF16 = 1, F3_MIX_Z_BF16 = 2, F3_MIX_X3 = 4, F3_MIX_Z3 = 8 };
 int f3_graph_mix_forward_ex(const float* A_eff, const void* x, void* z, int frames, int K, int V, int Cin, int flags,
                             void* stream);
 int f3_graph_mix_backward_ex(const float* A_eff, const void* x, const void* dz, float* dx, float* dA, int frames, int K,

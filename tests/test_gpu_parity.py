@@ -232,6 +232,33 @@ def test_graph_mix_kernels_match_torch(V, K, Cin, F):
         np.testing.assert_allclose(got.cpu().numpy(), r, rtol=0, atol=1e-5 * np.abs(r).max())
 
 
+@pytest.mark.parametrize("V,K,Cin,F", [(18, 3, 64, 300), (14, 3, 128, 77), (18, 3, 256, 41), (18, 1, 64, 9)])
+def test_graph_mix_x3_z3_rows(V, K, Cin, F):
+    """The bf16x3 mix forward writing Z as the step stores it for the gcn GEMM (F3_MIX_Z3): per
+    (frame, node) the bf16 row [z_hi | z_lo] of 2 K Cin. z_hi + z_lo against fp64 within X3_TOL of
+    the max, and z_hi / z_lo bit-exactly the RNE split of the kernel's own fp32 z (F3_MIX_X3 alone)."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    torch.manual_seed(V + K + Cin)
+    A = torch.rand(K, V, V, dtype=torch.float64) / V
+    x = torch.randn(F, V, Cin, dtype=torch.float64)
+    ref = torch.einsum("kvw,fvc->fwkc", A, x)  # [F][V][K][Cin]
+    Ad, xd = A.float().contiguous().to(d), x.float().contiguous().to(d)
+    zf = torch.empty(F, V, K, Cin, device=d)
+    z3 = torch.empty(F, V, 2 * K * Cin, device=d, dtype=torch.bfloat16)
+    st = L.stream_handle()
+    L.check(L.lib().f3_graph_mix_forward_ex(L.ptr(Ad), L.ptr(xd), L.ptr(zf), F, K, V, Cin, 4, st), "mix x3")
+    L.check(L.lib().f3_graph_mix_forward_ex(L.ptr(Ad), L.ptr(xd), L.ptr(z3), F, K, V, Cin, 4 | 8, st), "mix z3")
+    torch.cuda.synchronize()
+    hi, lo = z3[..., :K * Cin].reshape(F, V, K, Cin), z3[..., K * Cin:].reshape(F, V, K, Cin)
+    assert torch.equal(hi, zf.to(torch.bfloat16))
+    assert torch.equal(lo, (zf - zf.to(torch.bfloat16).float()).to(torch.bfloat16))
+    got = (hi.double() + lo.double()).cpu()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    print(f"mix z3 V={V} K={K} Cin={Cin} F={F}: {err:.2e}")
+    assert err <= X3_TOL, err
+
+
 @pytest.mark.parametrize("V,Cin,F", [(18, 64, 300), (14, 128, 77), (18, 256, 41), (17, 64, 5), (18, 64, 7680)])
 @pytest.mark.parametrize("a_bf16", [True, False], ids=["A_bf16", "A_fp32"])
 def test_graph_mix_bf16_forward(V, Cin, F, a_bf16):

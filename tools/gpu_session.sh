@@ -14,6 +14,7 @@
 #   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches, one process per key in
 #               ${ROOF_KEYS:-wgrad_l5 wgrad wgrad_kernel tcn_fwd}          -> gpurun_out/roof_kernels_KEY.txt
 #   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the same, per key     -> gpurun_out/roofline_pmc.json
+#   rgb_pmc     FETCH_SIZE / WRITE_SIZE passes of the RGB branch kernels -> gpurun_out/rgb_pmc.json
 #   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
 #   bench_fp32  bench.py --precision fp32 --no-targcn                   -> gpurun_out/bench_fp32.json
 #   ab          tools/ab.sh env $AB_CFGS (eager bench A/B, optional serial profiles) -> gpurun_out/ab.log
@@ -107,6 +108,16 @@ for step in "$@"; do
       done
       python tools/roofline_pmc.py summarize gpurun_out > gpurun_out/roofline_pmc.json 2>&1
       cat gpurun_out/roofline_pmc.json | head -40 ;;
+    rgb_pmc)   # HBM traffic of the RGB branch kernels (bench.py rgb_branch) -> gpurun_out/rgb_pmc.json
+      for C in FETCH_SIZE WRITE_SIZE; do
+        rm -rf gpurun_out/pmc_$C
+        run rgbpmc_$C 180 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run -- python tools/rgb_bench.py \
+          > gpurun_out/rgb_pmc_$C.log 2>&1
+        db=$(find gpurun_out/pmc_$C -name "*.db" | head -1)
+        [ -n "$db" ] && [ "$db" != "gpurun_out/pmc_$C/run_results.db" ] && mv "$db" gpurun_out/pmc_$C/run_results.db
+      done
+      python tools/rgb_pmc.py gpurun_out > gpurun_out/rgb_pmc.json 2>&1
+      cat gpurun_out/rgb_pmc.json ;;
     bench)
       run bench 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
       cut -c1-600 gpurun_out/bench.json ;;
