@@ -755,8 +755,8 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int i0 = (by - dt * itiles) * TI;
   // bf16x3 row segments (x3seg): split bz covers rows of segment seg = bz / seg_splits, whose
   // operands sit at column offsets (0, 0) hi x hi, (Nc, 0) lo x hi, (0, Kc) hi x lo of the rows
-  const int seg = a.x3seg ? bz / a.seg_splits : 0;
-  const int r_begin = (a.x3seg ? bz - seg * a.seg_splits : bz) * a.rows_per_split;
+  const int seg = a.x3seg ? (a.seg_minor ? bz % 3 : bz / a.seg_splits) : 0;
+  const int r_begin = (a.x3seg ? (a.seg_minor ? bz / 3 : bz - seg * a.seg_splits) : bz) * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
   const bool do_db = a.db && by == 0 && seg < 2;
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
@@ -969,8 +969,8 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const int bz = lin / tiles, tile = lin - bz * tiles;
   const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
   // bf16x3 row segments (x3seg, as wgrad_big): (dY_hi, X_hi), (dY_lo, X_hi), (dY_hi, X_lo)
-  const int seg = a.x3seg ? bz / a.seg_splits : 0;
-  const int n_begin = (a.x3seg ? bz - seg * a.seg_splits : bz) * a.rows_per_split;  // clips per split here
+  const int seg = a.x3seg ? (a.seg_minor ? bz % 3 : bz / a.seg_splits) : 0;
+  const int n_begin = (a.x3seg ? (a.seg_minor ? bz / 3 : bz - seg * a.seg_splits) : bz) * a.rows_per_split;  // clips per split
   const int n_end = min(g.M / TV, n_begin + a.rows_per_split);
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
   const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb) + (seg == 2 ? g.Kc : 0);
@@ -1345,6 +1345,12 @@ __global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __r
   *o += *reinterpret_cast<const f32x4*>(img + row * 144 + c4 * 4);
 }
 
+// F3_SEG_MINOR=1: bf16x3 row segments ordered segment-minor (WgradArgs::seg_minor)
+static int seg_minor_env() {
+  static const int v = getenv("F3_SEG_MINOR") ? atoi(getenv("F3_SEG_MINOR")) != 0 : 0;
+  return v;
+}
+
 // wgrad_taps applies (see its comment); nks = padded clip rows / 32
 static int wgrad_taps_nks(const WgradArgs& a) {
   const ConvGeom& g = a.g;
@@ -1370,6 +1376,7 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   splits = (clips + cps - 1) / cps;
   a.rows_per_split = cps;  // clips per split
   a.seg_splits = splits;
+  a.seg_minor = seg_minor_env();
   splits *= nseg;
   static const int dbg = getenv("F3_TAPS_DBG") ? atoi(getenv("F3_TAPS_DBG")) : 0;
   a.dbg = dbg;
@@ -1514,6 +1521,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
   a.seg_splits = splits;
+  a.seg_minor = seg_minor_env();
   splits *= nseg;  // slab partials (all segments)
   // XCD-aware grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
   // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the

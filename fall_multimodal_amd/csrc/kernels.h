@@ -100,6 +100,8 @@ struct WgradArgs {
   // With gcn_cin > 0 the slab reduce writes the gcn layout (as x3fold).
   int x3seg;
   int seg_splits;
+  int seg_minor;  // 1: split index bz = row split * 3 + segment (the three segments of one row range on
+                  // adjacent workgroups, i.e. mostly one XCD: X_hi / dY_hi re-reads hit its L2)
 };
 
 // Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).
