@@ -981,7 +981,7 @@ __global__ __launch_bounds__(256) void mix_fwd_x3_kernel(MixArgs a) {
     }
     if constexpr (ZI) {  // the frame's image -> its contiguous Z rows
       __syncthreads();
-      const int n16 = V * K * CIN / 2;  // V rows x 4 K CIN bytes / 16
+      const int n16 = V * K * CIN / 4;  // V rows x 4 K CIN bytes / 16
       uint4* dst = reinterpret_cast<uint4*>(a.z3 + (size_t)f * V * 2 * K * CIN);
       const uint4* srcv = reinterpret_cast<const uint4*>(zimg);
       for (int i = tid; i < n16; i += 256) dst[i] = srcv[i];
