@@ -1345,9 +1345,11 @@ __global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __r
   *o += *reinterpret_cast<const f32x4*>(img + row * 144 + c4 * 4);
 }
 
-// F3_SEG_MINOR=1: bf16x3 row segments ordered segment-minor (WgradArgs::seg_minor)
+// bf16x3 row segments ordered segment-minor (WgradArgs::seg_minor; F3_SEG_MINOR=0: segment-major).
+// Measured 10.39 -> 10.25-10.32 ms/step alone, 10.18 with the mix frame image
+// (profiles/r04_zimg_segminor_ab.txt)
 static int seg_minor_env() {
-  static const int v = getenv("F3_SEG_MINOR") ? atoi(getenv("F3_SEG_MINOR")) != 0 : 0;
+  static const int v = getenv("F3_SEG_MINOR") ? atoi(getenv("F3_SEG_MINOR")) != 0 : 1;
   return v;
 }
 

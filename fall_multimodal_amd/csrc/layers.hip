@@ -2061,8 +2061,9 @@ template <int CIN>
 static size_t mix_x3_lds_bwd() { return (size_t)192 * (2 * CIN + 16); }
 template <int CIN>
 static int launch_mix_fwd_x3(const MixArgs* a, hipStream_t s) {
-  // z3 output through the frame image (F3_MIX_ZIMG=1; default: per-fragment stores)
-  static const bool zimg_on = getenv("F3_MIX_ZIMG") && atoi(getenv("F3_MIX_ZIMG")) != 0;
+  // z3 output through the frame image (F3_MIX_ZIMG=0: per-fragment stores; measured 10.39 -> 10.22
+  // ms/step, profiles/r04_zimg_segminor_ab.txt)
+  static const bool zimg_on = !getenv("F3_MIX_ZIMG") || atoi(getenv("F3_MIX_ZIMG")) != 0;
   if (a->z3 && zimg_on) {
     const size_t lds = mix_x3_lds_fwd<CIN>() + (size_t)a->V * 4 * a->K * CIN;
     if (lds > 160 * 1024) return F3_EINVAL;
