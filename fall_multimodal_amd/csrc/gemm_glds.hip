@@ -388,7 +388,9 @@ static bool igemm_win_ok(const ConvGemmArgs& a, int epi) {
   if (!on || g.S != 1 || g.KT < 2 || 2 * g.P != g.KT - 1 || g.T_in != g.T_out) return false;
   // 128 channels: only the input gradient (77 vs 87-111 us for igemm_big at layer 4; the
   // forward measured 77 vs 58 us)
-  if (g.Nc != 64 && !(g.Nc == 128 && epi == EPI_RELUMASK)) return false;
+  // (F3_WIN128_FWD=1: the 128-channel forward too - A/B for the bf16x3 operands, K = 9 x 3C)
+  static const int fwd128 = getenv("F3_WIN128_FWD") ? atoi(getenv("F3_WIN128_FWD")) : 0;
+  if (g.Nc != 64 && !(g.Nc == 128 && (epi == EPI_RELUMASK || fwd128))) return false;
   if (G_BM + 2 * g.P * g.V > G_WIN_ROWS || g.M % (g.T_out * g.V) != 0) return false;
   return epi == (EPI_BIAS | EPI_STATS | EPI_GAP) || epi == EPI_RELUMASK || epi == EPI_BIAS;
 }

@@ -872,9 +872,10 @@ int f3_mu_dwconv_fwd(const DwConvArgs* a, hipStream_t s) {
   // costs ~2.3 ns per wave of the grid at the launch's end (1024 x 256 threads: 28.3 vs 18.8 us
   // without sums; 512 x 256: 24.9 vs 19.9; 512-thread blocks or one wave issuing the lane adds:
   // the same), so 512 workgroups of 256 threads
-  // F3_DW_STORE=1: at most kLanes workgroups, each storing its BN partial row into its own lane
-  // row (plain stores; the finalize adds the rows) instead of memory-side adds (A/B, round 4)
-  static const int store = getenv("F3_DW_STORE") ? atoi(getenv("F3_DW_STORE")) : 0;
+  // at most kLanes workgroups, each storing its BN partial row into its own lane row (plain stores;
+  // the finalize adds the rows) instead of memory-side adds: k3/s1 48.8 -> 51.3 % of HBM, k5/s2
+  // 46.4 -> 45.7 %, step unchanged (profiles/r04_musa_dwstore_ab.txt). F3_DW_STORE=0: the adds
+  static const int store = getenv("F3_DW_STORE") ? atoi(getenv("F3_DW_STORE")) : 1;
   static const int cap = getenv("F3_DW_GRID") ? std::max(64, atoi(getenv("F3_DW_GRID"))) : 512;
   const bool st_rows = store && a->sum;
   const int grid = (int)std::min<long long>(want, st_rows ? std::min(cap, kLanes) : cap);

@@ -560,6 +560,13 @@ inline const unsigned short* bf(const float* p, int on) { return on ? reinterpre
 // bf16x3 mode (F3_PRECISION_BF16X3): fp32 activations as in the fp32 mode, GEMMs on the split-bf16
 // kernels (gemm_x3.hip) with the packed weights as bf16 hi / lo planes (prep code 2)
 inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X3; }
+// bf16x3: the first block's gcn GEMMs (K Cin = 9 / 6, too narrow for the K-concatenated kernels)
+// on the fp32 kernels (exact fp32 products) instead of the register-staged split kernels
+// (F3_X3_L0_FP32=1; A/B)
+inline bool x3_l0_fp32() {
+  static const bool on = getenv("F3_X3_L0_FP32") && atoi(getenv("F3_X3_L0_FP32")) != 0;
+  return on;
+}
 // prep code of the packed GEMM weights: 0 fp32, 1 bf16, 2 split hi / lo planes
 inline int wcode(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16 ? 1 : is_x3(n) ? 2 : 0; }
 // bf16 view of an activation slot (bf16 mode stores GEMM operand tensors as bf16)
@@ -596,7 +603,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
     // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
-    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : wc;
+    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : (wc == 2 && x3_l0_fp32() ? 0 : wc);
     add_job(pt, PREP_PACK_GCN, C * K * Ci * (gc == 3 ? 3 : 1), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
     add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
             wc == 2 ? 3 : wc);  // bf16x3: K-concatenated for the bf16 implicit-GEMM kernels
@@ -663,6 +670,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
       ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
       ga.w = X.gw; ga.wb = bf(X.gw, wq); ga.out = X.g; ga.outb = bfa(X.g, hb); ga.x3 = x3;
+      if (x3 && !gcat && x3_l0_fp32()) { ga.x3 = 0; ga.wb = nullptr; }  // fp32 packed weights (prep code 0)
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
       if (gcat) {  // [Z_hi | Z_lo | Z_hi] x [W_hi | W_hi | W_lo] over 3 K Ci on the bf16 kernels
         ga.x3 = 0; ga.in = nullptr; ga.inb = bfa(X.z, 1);
@@ -873,6 +881,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
+    if (x3 && !gcat && x3_l0_fp32()) { gd.x3 = 0; gd.wb = nullptr; }
     if (gcat) {  // [dg_hi | dg_lo | dg_hi] x [W^T_hi | W^T_hi | W^T_lo] over 3C
       gd.x3 = 0; gd.in = nullptr; gd.inb = bfa(dg, 1);
       gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 2 * C, K * Ci);
@@ -989,6 +998,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
+    if (x3 && !gcat && x3_l0_fp32()) gw.x3 = 0;  // conv_wgrad_f32 on the fp32 dg / Z
     if (gcat) {  // row segments (or quadrants) into the slab, reduced into the gcn layout
       gw.x3 = 0; gw.bf16 = 1; gw.outmap = WG_OUT_CONV;
       gw.ldy = 2 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
