@@ -719,19 +719,27 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
 // whole loop (the tr reads of a fragment differ only by immediates: +4 rows, +32 rows), and
 // each staging lane walks its (clip, frame, joint) row coordinates incrementally instead of
 // dividing by V and T per stage. Forward-geometry rows only (g.transposed == 0).
+//
+// NTW > 1 (tap groups): a workgroup computes NTW consecutive taps dt0 .. dt0 + NTW - 1 of its
+// (j, i) tile from ONE staged copy of the dY rows — the input rows of each tap are staged into
+// their own region — so the dY bytes staged per MFMA and the A-fragment LDS reads per MFMA
+// drop by NTW (each wave holds NTW x MJ x MI accumulators). Taps past KT (the last group when
+// NTW does not divide KT) are staged from the zero page and their MFMAs skipped.
 // ----------------------------------------------------------------------------
-template <int WJW, int WIW, int MJ, int MI, int BK = 64>
+template <int WJW, int WIW, int MJ, int MI, int BK = 64, int NTW = 1>
 __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   constexpr int NW = WJW * WIW;  // waves: 8 (one workgroup per CU) or 4 (the 64-wide tiles)
   constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;
   constexpr int UJ = TJ / 16, UI = TI / 16;
   constexpr int RJ = TJ * 2, RI = TI * 2;  // row bytes of the dY / input tiles
   constexpr int NKS = BK / 32;             // 32-deep MFMA k steps per stage
-  constexpr int Y_BYTES = BK * RJ, X_BYTES = BK * RI, STAGE = Y_BYTES + X_BYTES;
-  constexpr int YPW = Y_BYTES / 1024 / NW, XPW = X_BYTES / 1024 / NW, PPW = YPW + XPW;  // pieces per wave
+  constexpr int Y_BYTES = BK * RJ, X_BYTES = BK * RI, STAGE = Y_BYTES + NTW * X_BYTES;
+  constexpr int YPW = Y_BYTES / 1024 / NW, XPW = X_BYTES / 1024 / NW, PPW = YPW + NTW * XPW;  // pieces per wave
   constexpr int YRPI = 1024 / RJ, XRPI = 1024 / RI;  // rows per piece
   constexpr int NST = 3;
+  constexpr int NB = NTW * MI;  // B fragments per k step (all taps)
   static_assert(BK == 32 || BK == 64, "stage depth");
+  static_assert(NTW >= 1 && NTW <= 3 && PPW < 64, "tap group");
   static_assert((NW == 8 || NW == 4) && YPW * NW * 1024 == Y_BYTES && XPW * NW * 1024 == X_BYTES, "whole pieces");
   static_assert(UJ >= 4 && UI >= 4, "64-column tiles at least");
   static_assert(NST * STAGE + TJ * 4 <= 160 * 1024, "LDS");
@@ -741,7 +749,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const ConvGeom& g = a_.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int itiles = (g.Kc + TI - 1) / TI;
-  const int gx = (g.Nc + TJ - 1) / TJ, gy = g.KT * itiles;
+  const int gx = (g.Nc + TJ - 1) / TJ, gy = ((g.KT + NTW - 1) / NTW) * itiles;
   int lin = xcd_remap(blockIdx.x, gridDim.x);  // a row split's tiles stay on one XCD
   WgradArgs a = a_;
   if (a_.groups > 1) {  // grouped launch: problem-major over the 1-D grid
@@ -753,8 +761,8 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int rem = lin - bz * gx * gy;
   const int by = rem / gx, bx = rem - by * gx;
   const int j0 = bx * TJ;
-  const int dt = by / itiles;
-  const int i0 = (by - dt * itiles) * TI;
+  const int grp = by / itiles, dt0 = grp * NTW;  // taps dt0 .. dt0 + NTW - 1
+  const int i0 = (by - grp * itiles) * TI;
   // bf16x3 row segments (x3seg): split bz covers rows of segment seg = bz / seg_splits, whose
   // operands sit at column offsets (0, 0) hi x hi, (Nc, 0) lo x hi, (0, Kc) hi x lo of the rows
   const int seg = a.x3seg ? (a.seg_minor ? bz % 3 : bz / a.seg_splits) : 0;
@@ -790,7 +798,8 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     xt[i] = nt - xn[i] * g.T_out;
     xcol[i] = i0 + ((xph >> 1) ^ wswz<UI>(rr)) * 16 + (xph & 1) * 8;
   }
-  const int tshift = dt - g.P;
+  const int tshift = dt0 - g.P;
+  const int ntap = min(NTW, g.KT - dt0);  // valid taps of this group
   auto stage = [&](int buf) {  // issue the next BK rows of every staging lane, then advance them
     const unsigned sy = lds0 + buf * STAGE;
 #pragma unroll
@@ -803,11 +812,17 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     const unsigned sx = sy + Y_BYTES;
 #pragma unroll
     for (int i = 0; i < XPW; ++i) {
-      const int ti = xt[i] * g.S + tshift;
-      const bool ok = xm[i] < r_end && xcol[i] < g.Kc && ti >= 0 && ti < g.T_in;
-      const __bf16* src = ok ? xb + (size_t)((xn[i] * g.T_in + ti) * g.V + xv[i]) * g.lda + xcol[i] : zero;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (lds_void_t*)(size_t)(sx + (i * NW + wave) * 1024), 16, 0, 0);
+      const int tb = xt[i] * g.S + tshift;
+      const bool okr = xm[i] < r_end && xcol[i] < g.Kc;
+      const long long rb = (long long)(xn[i] * g.T_in + tb) * g.V + xv[i];
+#pragma unroll
+      for (int tt = 0; tt < NTW; ++tt) {  // tap dt0 + tt: input frame tb + tt (rows V apart)
+        const int ti = tb + tt;
+        const bool ok = okr && tt < ntap && ti >= 0 && ti < g.T_in;
+        const __bf16* src = ok ? xb + (size_t)(rb + (long long)tt * g.V) * g.lda + xcol[i] : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (lds_void_t*)(size_t)(sx + tt * X_BYTES + (i * NW + wave) * 1024), 16, 0, 0);
+      }
       xm[i] += BK;
       xv[i] += dv;
       xt[i] += dnt;
@@ -821,17 +836,20 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
   const int r0 = 8 * fg + tq;                 // rows r0, r0+4 (lo/hi), +32 for the second k half
   const int fj = wswz<UJ>(r0), fi = wswz<UI>(r0);  // unchanged at r0 + 4, r0 + 32, r0 + 36
-  unsigned offa[MJ], offb[MI];
+  unsigned offa[MJ], offb[NB];
 #pragma unroll
   for (int x = 0; x < MJ; ++x) offa[x] = r0 * RJ + (((wj * MJ + x) ^ fj) * 32) + tp * 8;
 #pragma unroll
-  for (int y = 0; y < MI; ++y) offb[y] = Y_BYTES + r0 * RI + (((wi * MI + y) ^ fi) * 32) + tp * 8;
+  for (int tt = 0; tt < NTW; ++tt)
+#pragma unroll
+    for (int y = 0; y < MI; ++y)
+      offb[tt * MI + y] = Y_BYTES + tt * X_BYTES + r0 * RI + (((wi * MI + y) ^ fi) * 32) + tp * 8;
 
-  f32x4 acc[MJ][MI];
+  f32x4 acc[MJ][NB];
 #pragma unroll
   for (int x = 0; x < MJ; ++x)
 #pragma unroll
-    for (int y = 0; y < MI; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < NB; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   float dbp[MJ];
 #pragma unroll
   for (int x = 0; x < MJ; ++x) dbp[x] = 0.f;
@@ -853,7 +871,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     const unsigned base = lds0 + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      s16x4_t lo[MJ + MI], hi[MJ + MI];
+      s16x4_t lo[MJ + NB], hi[MJ + NB];
 #pragma unroll
       for (int x = 0; x < MJ; ++x) {
         const unsigned p = base + offa[x];
@@ -866,7 +884,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
         }
       }
 #pragma unroll
-      for (int y = 0; y < MI; ++y) {
+      for (int y = 0; y < NB; ++y) {
         const unsigned p = base + offb[y];
         if (ks == 0) {
           asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[MJ + y]) : "v"(p));
@@ -877,11 +895,11 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
         }
       }
       tr_wait(lo, hi);
-      bf16x8 fa[MJ], fb[MI];
+      bf16x8 fa[MJ], fb[NB];
 #pragma unroll
       for (int x = 0; x < MJ; ++x) fa[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[x], hi[x], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-      for (int y = 0; y < MI; ++y)
+      for (int y = 0; y < NB; ++y)
         fb[y] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[MJ + y], hi[MJ + y], 0, 1, 2, 3, 4, 5, 6, 7));
       if (do_db && wi == 0) {
 #pragma unroll
@@ -890,9 +908,13 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
           for (int e = 0; e < 8; ++e) dbp[x] += (float)fa[x][e];
       }
 #pragma unroll
-      for (int x = 0; x < MJ; ++x)
+      for (int tt = 0; tt < NTW; ++tt) {
+        if (NTW > 1 && tt >= ntap) continue;  // (uniform) a tap past KT: zeros, skipped
 #pragma unroll
-        for (int y = 0; y < MI; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+        for (int x = 0; x < MJ; ++x)
+#pragma unroll
+          for (int y = 0; y < MI; ++y) acc[x][tt * MI + y] = mfma_bf16x(fa[x], fb[tt * MI + y], acc[x][tt * MI + y]);
+      }
     }
     if (t + 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -916,24 +938,30 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   if (nst == 0 && !to_slab) return;
   float* slab = to_slab ? a.slab + (size_t)bz * g.Nc * g.KT * g.Kc : nullptr;
 #pragma unroll
-  for (int x = 0; x < MJ; ++x) {
+  for (int tt = 0; tt < NTW; ++tt) {
+    if (tt >= ntap) continue;
+    const int dt = dt0 + tt;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = j0 + wj * 16 * MJ + x * 16 + fg * 4 + r;
-      if (j >= g.Nc) continue;
+    for (int x = 0; x < MJ; ++x) {
 #pragma unroll
-      for (int y = 0; y < MI; ++y) {
-        const int i = i0 + wi * 16 * MI + y * 16 + fr;
-        if (i >= g.Kc) continue;
-        size_t idx;
-        if (a.outmap == WG_OUT_GCN) {
-          const int k = i / a.gcn_cin, ci = i - k * a.gcn_cin;
-          idx = ((size_t)k * g.Nc + j) * a.gcn_cin + ci;
-        } else {
-          idx = (size_t)j * g.KT * g.Kc + (size_t)dt * g.Kc + i;
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + wj * 16 * MJ + x * 16 + fg * 4 + r;
+        if (j >= g.Nc) continue;
+#pragma unroll
+        for (int y = 0; y < MI; ++y) {
+          const int i = i0 + wi * 16 * MI + y * 16 + fr;
+          if (i >= g.Kc) continue;
+          size_t idx;
+          if (a.outmap == WG_OUT_GCN) {
+            const int k = i / a.gcn_cin, ci = i - k * a.gcn_cin;
+            idx = ((size_t)k * g.Nc + j) * a.gcn_cin + ci;
+          } else {
+            idx = (size_t)j * g.KT * g.Kc + (size_t)dt * g.Kc + i;
+          }
+          const float v = acc[x][tt * MI + y][r];
+          if (to_slab) slab[idx] = v;
+          else atomic_add_f(a.dw + idx, v);
         }
-        if (to_slab) slab[idx] = acc[x][y][r];
-        else atomic_add_f(a.dw + idx, acc[x][y][r]);
       }
     }
   }
@@ -1497,10 +1525,10 @@ static int resident_wgs(const void* fn, int threads) {
   return per_cu * cus;
 }
 
-template <int TJ, int TI, int THREADS, void (*KERNEL)(WgradArgs)>
+template <int TJ, int TI, int THREADS, void (*KERNEL)(WgradArgs), int NTW = 1>
 static int launch_wgrad(WgradArgs a, hipStream_t s) {
   const int gx = (a.g.Nc + TJ - 1) / TJ;
-  const int gy = a.g.KT * ((a.g.Kc + TI - 1) / TI);
+  const int gy = ((a.g.KT + NTW - 1) / NTW) * ((a.g.Kc + TI - 1) / TI);  // (tap groups of NTW)
   // Split-K over rows sized to ONE round of resident workgroups: rounding the split count up
   // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
   // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
@@ -1576,15 +1604,25 @@ big:
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once
   // per 256 output channels) wins. F3_WGRAD_BIG=0 restores the first 4-wave kernel (wgrad_glds_bf16).
-  if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0)
+  // Tap groups (wgrad_big NTW > 1, the (9,1) tcn layers): F3_WG_NTW bit 0 the 256 x 128 tiles
+  // (2 taps, BK 32), bit 1 the 128 x 128 tiles (3 taps, BK 32), bit 2 the 64 x 64 tiles (3 taps,
+  // BK 32)
+  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 0;
+  const bool taps9 = a.g.KT == 9;
+  if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
+    if (taps9 && (ntw & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
+  }
   if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 256 == 0)
     return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4>>(a, s);
-  if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0)
+  if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
+    if (taps9 && (ntw & 2)) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
+  }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);
     if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4>>(a, s);
+    if (taps9 && (ntw & 4)) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2>>(a, s);
   }
   const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;

@@ -1147,8 +1147,8 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   int least = 0, greatest = 0;
   if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
   for (int i = 0; i < 3; ++i)
-    ok = ok && (prio && i >= 1 && least != greatest
-                    ? hipStreamCreateWithPriority(&n.aux[i], hipStreamNonBlocking, least)
+    ok = ok && (prio && i >= 1 && least != greatest  // (F3_SIDE_PRIO=2: the greatest priority instead)
+                    ? hipStreamCreateWithPriority(&n.aux[i], hipStreamNonBlocking, prio == 2 ? greatest : least)
                     : hipStreamCreateWithFlags(&n.aux[i], hipStreamNonBlocking)) == hipSuccess;
   for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
