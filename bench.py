@@ -206,7 +206,8 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     T=8 output frames, B clips), launched alone through the C ABI exactly as the step launches them:
     K-concatenated operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
     step's producers write them) on the bf16 LDS-DMA kernels:
-    * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,64> over three
+    * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,32,2> (taps in groups
+      of two from one staged dY copy; F3_WG_NTW=0: the per-tap wgrad_big<4,2,4,4,64>) over three
       row segments of the [hi | lo] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
       three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
       (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
@@ -257,7 +258,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
                                      f"C=256, T=8, N={N}, V={V})", "ms": ms}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15, V, C,
                                                                 C, KT, 2, 4, st)) if want("wgrad_l5") else 0.0
-    out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
+    out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,2> (2-tap groups) x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
                                  f"bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms}
     return _roofline_records({k: v for k, v in out.items() if want(k)}, flop, peak)
 

@@ -1395,11 +1395,18 @@ static int wgrad_taps_nks(const WgradArgs& a) {
   return nks == 4 || nks == 5 ? nks : 0;
 }
 
+static int wgrad_frac() {
+  static const int f = getenv("F3_WGRAD_FRAC") ? std::max(1, std::min(100, atoi(getenv("F3_WGRAD_FRAC")))) : 100;
+  return f;
+}
+
 static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const int TV = a.g.T_out * a.g.V, clips = a.g.M / TV;
   const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
   const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
-  static const int target = getenv("F3_TAPS_WGS") ? atoi(getenv("F3_TAPS_WGS")) : 256;  // one per CU
+  static const int taps_wgs = getenv("F3_TAPS_WGS") ? atoi(getenv("F3_TAPS_WGS")) : 0;
+  const int target = taps_wgs > 0 ? taps_wgs  // one per CU, or the share wg_pct / F3_WGRAD_FRAC of them
+                                  : std::max(1, 256 * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : wgrad_frac()) / 100);
   const int nseg = a.x3seg ? 3 : 1;  // bf16x3 row segments: `splits` clip splits per segment
   int splits = std::max(1, std::min(clips, target / (tiles * nseg)));
   splits = (int)std::min<long long>(splits, a.slab_cap / (per_split * nseg));
@@ -1533,7 +1540,9 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
   // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
   static const int slots = resident_wgs((const void*)KERNEL, THREADS);
-  const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : slots;
+  // F3_WGRAD_FRAC (percent): size the splits to that share of the resident slots, leaving CUs to
+  // the main chains the weight gradients run beside (side queues)
+  const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : std::max(1, slots * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : wgrad_frac()) / 100);
   const int groups = std::max(1, a.groups);  // grouped launches: wgrad_big, atomics (checked by the caller)
   // x3seg: three row segments, `splits` row splits each (one round of resident workgroups in all)
   const int nseg = a.x3seg ? 3 : 1;
@@ -1606,8 +1615,9 @@ big:
   // per 256 output channels) wins. F3_WGRAD_BIG=0 restores the first 4-wave kernel (wgrad_glds_bf16).
   // Tap groups (wgrad_big NTW > 1, the (9,1) tcn layers): F3_WG_NTW bit 0 the 256 x 128 tiles
   // (2 taps, BK 32), bit 1 the 128 x 128 tiles (3 taps, BK 32), bit 2 the 64 x 64 tiles (3 taps,
-  // BK 32)
-  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 0;
+  // BK 32). Measured on MI355X (bf16x3, B = 256): the layer-5 weight gradient 0.260 -> 0.222 ms
+  // per launch pair with bit 0; bits 1 and 2 step-neutral (profiles/r04_ntw_ab.txt). Default 1.
+  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 1;
   const bool taps9 = a.g.KT == 9;
   if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
     if (taps9 && (ntw & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);

@@ -85,6 +85,7 @@ struct WgradArgs {
   int groups;
   long long gs_dy, gs_in, gs_dw, gs_db;
   int dbg;                    // measurement knob of wgrad_taps (F3_TAPS_DBG): 1 no MFMA, 2 no restaging
+  int wg_pct;                 // split sizing, percent of the resident workgroup slots (0: F3_WGRAD_FRAC / all)
   int x3;                     // 1: split-bf16 kernel on fp32 dy / in (gemm_x3.hip)
   // bf16x3 mode on the bf16 kernels (K-concatenated operands): the GEMM ran on dY' = [dY_hi | dY_lo]
   // (Nc = 2C) and X' = [X_hi | X_lo] (Kc = 2Ci); the slab reduce adds the hh + hl + lh quadrants

@@ -563,6 +563,17 @@ inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X
 // bf16x3: the first block's gcn GEMMs (K Cin = 9 / 6, too narrow for the K-concatenated kernels)
 // on the fp32 kernels (exact fp32 products) instead of the register-staged split kernels
 // (F3_X3_L0_FP32=1; A/B)
+// F3_SIDE_FRAC=p (percent): the side-queue weight gradients of layers >= F3_SIDE_FRAC_FROM
+// (default 2) are split for p % of the chip's workgroup slots, so the main chains running beside
+// them keep CUs (a whole-chip wgrad_big grid holds every CU's LDS until it drains: the main
+// queues sat idle 190-335 us behind the layer-5 weight gradient, profiles/r04_x3_step_timeline.txt);
+// the last layers' (the step's tail, main chains done) keep the whole chip. Measured (bf16x3
+// step): 10.17 -> 10.07 ms at 50 or 75 (profiles/r04_ntw_ab.txt); default 75, 0 = whole chip
+inline int side_pct(bool split, int l) {
+  static const int pct = getenv("F3_SIDE_FRAC") ? atoi(getenv("F3_SIDE_FRAC")) : 75;
+  static const int from = getenv("F3_SIDE_FRAC_FROM") ? atoi(getenv("F3_SIDE_FRAC_FROM")) : 2;
+  return split && pct > 0 && l >= from ? pct : 0;
+}
 inline bool x3_l0_fp32() {
   static const bool on = getenv("F3_X3_L0_FP32") && atoi(getenv("F3_X3_L0_FP32")) != 0;
   return on;
@@ -919,6 +930,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       return F3_EHIP;
     WgradArgs tw;
     std::memset(&tw, 0, sizeof(tw));
+    tw.wg_pct = side_pct(split, l);
     tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, C, C);
     tw.ldy = C; tw.dw = q.g(L.tcn_w); tw.db = q.g(L.tcn_b);
     tw.outmap = WG_OUT_CONV; tw.bf16 = hb; tw.x3 = x3;
@@ -955,6 +967,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     if (L.res == RES_CONV) {
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
+      rw.wg_pct = side_pct(split, l);
       rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, Ci, C);
       rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb; rw.x3 = x3;
       if (hb) {
@@ -990,6 +1003,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     }
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
+    gw.wg_pct = side_pct(split, l);
     gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
     gw.ldy = C; gw.dw = q.g(L.gcn_w); gw.db = nullptr;
     if (hb) {
