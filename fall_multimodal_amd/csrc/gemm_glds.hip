@@ -726,7 +726,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
 // drop by NTW (each wave holds NTW x MJ x MI accumulators). Taps past KT (the last group when
 // NTW does not divide KT) are staged from the zero page and their MFMAs skipped.
 // ----------------------------------------------------------------------------
-template <int WJW, int WIW, int MJ, int MI, int BK = 64, int NTW = 1>
+template <int WJW, int WIW, int MJ, int MI, int BK = 64, int NTW = 1, int NSTG = 3>
 __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   constexpr int NW = WJW * WIW;  // waves: 8 (one workgroup per CU) or 4 (the 64-wide tiles)
   constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;
@@ -736,10 +736,11 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   constexpr int Y_BYTES = BK * RJ, X_BYTES = BK * RI, STAGE = Y_BYTES + NTW * X_BYTES;
   constexpr int YPW = Y_BYTES / 1024 / NW, XPW = X_BYTES / 1024 / NW, PPW = YPW + NTW * XPW;  // pieces per wave
   constexpr int YRPI = 1024 / RJ, XRPI = 1024 / RI;  // rows per piece
-  constexpr int NST = 3;
+  constexpr int NST = NSTG;  // LDS stages in the ring (NST - 1 in flight)
   constexpr int NB = NTW * MI;  // B fragments per k step (all taps)
   static_assert(BK == 32 || BK == 64, "stage depth");
-  static_assert(NTW >= 1 && NTW <= 3 && PPW < 64, "tap group");
+  static_assert(NTW >= 1 && NTW <= 3 && (NST - 1) * PPW < 64, "tap group");
+  static_assert(NST == 3 || NST == 4, "ring depth");
   static_assert((NW == 8 || NW == 4) && YPW * NW * 1024 == Y_BYTES && XPW * NW * 1024 == X_BYTES, "whole pieces");
   static_assert(UJ >= 4 && UI >= 4, "64-column tiles at least");
   static_assert(NST * STAGE + TJ * 4 <= 160 * 1024, "LDS");
@@ -857,7 +858,11 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int nst = r_end > r_begin ? (r_end - r_begin + BK - 1) / BK : 0;
   if (nst > 0) {
     stage(0);
-    if (nst > 1) {
+    if (NST == 4 && nst > 2) {
+      stage(1);
+      stage(2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+    } else if (nst > 1) {
       stage(1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
     } else {
@@ -867,7 +872,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   }
   for (int t = 0; t < nst; ++t) {
     const int buf = t % NST;
-    if (t + 2 < nst) stage((t + 2) % NST);
+    if (t + NST - 1 < nst) stage((t + NST - 1) % NST);
     const unsigned base = lds0 + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -916,7 +921,8 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
           for (int y = 0; y < MI; ++y) acc[x][tt * MI + y] = mfma_bf16x(fa[x], fb[tt * MI + y], acc[x][tt * MI + y]);
       }
     }
-    if (t + 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    // stage t + 1 must have landed: at most NST - 2 later stages still in flight
+    if (t + NST - 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -1618,8 +1624,12 @@ big:
   // BK 32). Measured on MI355X (bf16x3, B = 256): the layer-5 weight gradient 0.260 -> 0.222 ms
   // per launch pair with bit 0; bits 1 and 2 step-neutral (profiles/r04_ntw_ab.txt). Default 1.
   static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 1;
+  // F3_WG_NST4 (A/B): 4-stage rings (three stages in flight) - bit 0 the 256 x 128 tap groups (129 KiB
+  // of LDS), bit 1 the 128 x 128 tiles (BK 64, 129 KiB)
+  static const int nst4 = getenv("F3_WG_NST4") ? atoi(getenv("F3_WG_NST4")) : 0;
   const bool taps9 = a.g.KT == 9;
   if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
+    if (taps9 && (ntw & 1) && (nst4 & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2, 4>, 2>(a, s);
     if (taps9 && (ntw & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
   }
@@ -1627,6 +1637,7 @@ big:
     return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4>>(a, s);
   if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
     if (taps9 && (ntw & 2)) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
+    if (nst4 & 2) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 64, 1, 4>>(a, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
   }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)

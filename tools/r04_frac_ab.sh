@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 A/B: share of the chip the side-queue weight gradients are split for (F3_WGRAD_FRAC),
-# with and without the tap groups (F3_WG_NTW)
+# Round-4 A/B: which layers' side-queue weight gradients get split for part of the chip, and how
+# large a part (F3_SIDE_FRAC / F3_SIDE_FRAC_FROM; default 75 from layer 2), + side priority
 set -o pipefail
 mkdir -p gpurun_out
-ROUNDS=3 tools/step_ab.sh bf16x3 - F3_WGRAD_FRAC=50 F3_WGRAD_FRAC=75 "${NTW_BEST:-F3_WG_NTW=7}" \
-  "${NTW_BEST:-F3_WG_NTW=7},F3_WGRAD_FRAC=50" "${NTW_BEST:-F3_WG_NTW=7},F3_WGRAD_FRAC=75" 2>&1 | tee gpurun_out/frac_ab.txt
+ROUNDS=3 tools/step_ab.sh bf16x3 - F3_SIDE_FRAC_FROM=1 F3_SIDE_FRAC_FROM=0 F3_SIDE_FRAC=60 F3_SIDE_FRAC=90 \
+  F3_SIDE_PRIO=1 F3_SIDE_FRAC=0 2>&1 | tee gpurun_out/frac_ab.txt
