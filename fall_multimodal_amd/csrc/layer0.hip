@@ -15,6 +15,9 @@
 //              slab that f3_colsum adds into the gradients (no dZ in HBM, no weight-gradient GEMM);
 //   databn_bwd2  one pass over the channels-last gradient rows (coalesced), per-(v, c) sums in
 //              registers and LDS, one atomic per channel and block.
+// F32 (Gcn0Args::f32, the bf16x3 mode): the same kernels on fp32 x / w / Z / g / dg, every product
+// in fp32 (dZ on v_mfma_f32_16x16x4_f32): the generic path's mix + 9-column split GEMM + mix
+// backward + weight-gradient GEMM took ~200 us per stream and step for this layer.
 #include "layers.h"
 #include "igemm.h"
 
@@ -35,7 +38,7 @@ F3_DEV unsigned short g0_rne(float f) {
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-template <int K, int Ci>
+template <int K, int Ci, bool F32>
 __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
   __shared__ float As[3 * G0_MAXV * G0_MAXV];
   __shared__ float xs[G0_FB * G0_MAXV * 4];
@@ -47,23 +50,32 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
   const int V = a.V;
   for (int i = tid; i < K * V * V; i += 256) As[i] = a.A[i];
   for (int i = tid; i < V * C; i += 256) bvs[i] = a.beff[i];
+  const float* xf = reinterpret_cast<const float*>(a.x);
+  const float* wf = reinterpret_cast<const float*>(a.w);
+  float* zf = reinterpret_cast<float*>(a.z);
+  float* gf = reinterpret_cast<float*>(a.g);
   float wv[KC];
 #pragma unroll
-  for (int j = 0; j < KC; ++j) wv[j] = g0_bf(a.w[c * KC + j]);
+  for (int j = 0; j < KC; ++j) wv[j] = F32 ? wf[c * KC + j] : g0_bf(a.w[c * KC + j]);
   float ssum = 0.f, ssq = 0.f;
   for (int f0 = blockIdx.x * G0_FB; f0 < a.frames; f0 += gridDim.x * G0_FB) {
     const int nf = min(G0_FB, a.frames - f0);
     __syncthreads();
-    for (int i = tid; i < nf * V * Ci; i += 256) xs[i] = g0_bf(a.x[(size_t)f0 * V * Ci + i]);
+    for (int i = tid; i < nf * V * Ci; i += 256) xs[i] = F32 ? xf[(size_t)f0 * V * Ci + i] : g0_bf(a.x[(size_t)f0 * V * Ci + i]);
     __syncthreads();
     // Z[f][w][k][ci] = sum_v A_eff[k][v][w] x[f][v][ci] (v ascending, as mix_fwd_kernel), bf16
     for (int o = tid; o < nf * V * KC; o += 256) {
       const int ci = o % Ci, t = o / Ci, k = t % K, t2 = t / K, w = t2 % V, fl = t2 / V;
       float acc = 0.f;
       for (int v = 0; v < V; ++v) acc += As[(k * V + v) * V + w] * xs[(fl * V + v) * Ci + ci];
-      const unsigned short zb = g0_rne(acc);
-      a.z[(size_t)f0 * V * KC + o] = zb;
-      zs[o] = g0_bf(zb);
+      if (F32) {
+        zf[(size_t)f0 * V * KC + o] = acc;
+        zs[o] = acc;
+      } else {
+        const unsigned short zb = g0_rne(acc);
+        a.z[(size_t)f0 * V * KC + o] = zb;
+        zs[o] = g0_bf(zb);
+      }
     }
     __syncthreads();
     // g[row][c] = sum_j Z[row][j] W[c][j] + bias_eff[v][c]
@@ -74,7 +86,8 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
       acc += bvs[w * C + c];
       w += 4;
       if (w >= V) w -= V;  // (V >= 4)
-      a.g[((size_t)f0 * V + r) * C + c] = g0_rne(acc);
+      if (F32) gf[((size_t)f0 * V + r) * C + c] = acc;
+      else a.g[((size_t)f0 * V + r) * C + c] = g0_rne(acc);
       ssum += acc;
       ssq += acc * acc;
     }
@@ -92,7 +105,7 @@ __global__ __launch_bounds__(256) void gcn0_fwd_kernel(Gcn0Args a) {
 // ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
-template <int K, int Ci>
+template <int K, int Ci, bool F32>
 __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   __shared__ float As[3 * G0_MAXV * G0_MAXV];
   __shared__ float xs[G0_FB * G0_MAXV * 4];
@@ -106,14 +119,26 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   for (int i = tid; i < KVV; i += 256) As[i] = a.A[i];
   // MFMA B operand (dZ = dg . W: k = c, n = j): lane (fg, fr) holds W[c = s*32 + fg*8 + e][j = fr]
   bf16x8 wb[2];
+  // F32: v_mfma_f32_16x16x4_f32 steps s = 0..15, k slot fg of step s = channel c = fg*16 + s: lane
+  // (fg, fr) holds W[fg*16 + s][fr] (A: dg[row fr][fg*16 + s], 16 consecutive floats per lane)
+  float wf32[F32 ? 16 : 1];
+  const float* wf = reinterpret_cast<const float*>(a.w);
+  const float* xf = reinterpret_cast<const float*>(a.x);
+  const float* zf = reinterpret_cast<const float*>(a.z);
+  const float* dgf = reinterpret_cast<const float*>(a.dg);
+  if (F32) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 16; ++s) wf32[s] = fr < KC ? wf[(fg * 16 + s) * KC + fr] : 0.f;
+  } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int cc = s * 32 + fg * 8 + e;
-      const unsigned short u = fr < KC ? a.w[cc * KC + fr] : (unsigned short)0;
-      wb[s][e] = __builtin_bit_cast(__bf16, u);
-    }
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int cc = s * 32 + fg * 8 + e;
+        const unsigned short u = fr < KC ? a.w[cc * KC + fr] : (unsigned short)0;
+        wb[s][e] = __builtin_bit_cast(__bf16, u);
+      }
+  }
   float dacc[4] = {0.f, 0.f, 0.f, 0.f};  // dA_eff entries tid + 256 q
   float wacc[KC];                        // dW[.][c][.] over this thread's rows (j = k*Ci + ci)
 #pragma unroll
@@ -130,15 +155,24 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
   for (int f0 = blockIdx.x * G0_FB; f0 < a.frames; f0 += gridDim.x * G0_FB) {
     const int nf = min(G0_FB, a.frames - f0), nr = nf * V;
     __syncthreads();
-    for (int i = tid; i < nf * V * Ci; i += 256) xs[i] = g0_bf(a.x[(size_t)f0 * V * Ci + i]);
-    for (int i = tid; i < nr * KC; i += 256) zs[i] = g0_bf(a.z[(size_t)f0 * V * KC + i]);
+    for (int i = tid; i < nf * V * Ci; i += 256) xs[i] = F32 ? xf[(size_t)f0 * V * Ci + i] : g0_bf(a.x[(size_t)f0 * V * Ci + i]);
+    for (int i = tid; i < nr * KC; i += 256) zs[i] = F32 ? zf[(size_t)f0 * V * KC + i] : g0_bf(a.z[(size_t)f0 * V * KC + i]);
     // dZ tiles of 16 rows: A fragment = 8 consecutive dg channels of row r0 + fr (16-B loads)
     for (int t = wave; t * 16 < nr; t += 4) {
       const int r = min(t * 16 + fr, nr - 1);
-      const unsigned short* dgr = a.dg + ((size_t)f0 * V + r) * C + fg * 8;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (F32) {
+        const f32x4* dgr = reinterpret_cast<const f32x4*>(dgf + ((size_t)f0 * V + r) * C + fg * 16);
+        f32x4 d[4];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) acc = mfma_bf16x(*reinterpret_cast<const bf16x8*>(dgr + s * 32), wb[s], acc);
+        for (int q = 0; q < 4; ++q) d[q] = dgr[q];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(d[s >> 2][s & 3], wf32[s], acc, 0, 0, 0);
+      } else {
+        const unsigned short* dgr = a.dg + ((size_t)f0 * V + r) * C + fg * 8;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = mfma_bf16x(*reinterpret_cast<const bf16x8*>(dgr + s * 32), wb[s], acc);
+      }
       // lane holds dZ[rows t*16 + 4fg + i][col fr]
       if (fr < KC)
 #pragma unroll
@@ -172,7 +206,7 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
     }
     // dW[k][c][ci] += sum_rows dg[row][c] Z[row][k*Ci + ci]
     for (int r = rg; r < nr; r += 4) {
-      const float d = g0_bf(a.dg[((size_t)f0 * V + r) * C + c]);
+      const float d = F32 ? dgf[((size_t)f0 * V + r) * C + c] : g0_bf(a.dg[((size_t)f0 * V + r) * C + c]);
 #pragma unroll
       for (int j = 0; j < KC; ++j) wacc[j] += d * zs[r * KC + j];
     }
@@ -249,8 +283,14 @@ static int g0_grid(int frames) { return std::max(1, std::min(480, (frames + G0_F
 
 int f3_gcn0_fwd(const Gcn0Args* a, hipStream_t s) {
   if (!f3_gcn0_ok(a->K, a->V, a->Ci, 64)) return F3_EINVAL;
-  if (a->Ci == 3) hipLaunchKernelGGL((gcn0_fwd_kernel<3, 3>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL((gcn0_fwd_kernel<3, 2>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  const dim3 grid(g0_grid(a->frames));
+  if (a->f32) {
+    if (a->Ci == 3) hipLaunchKernelGGL((gcn0_fwd_kernel<3, 3, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((gcn0_fwd_kernel<3, 2, true>), grid, dim3(256), 0, s, *a);
+  } else {
+    if (a->Ci == 3) hipLaunchKernelGGL((gcn0_fwd_kernel<3, 3, false>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((gcn0_fwd_kernel<3, 2, false>), grid, dim3(256), 0, s, *a);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -259,8 +299,14 @@ int f3_gcn0_bwd_parts(const Gcn0Args* a) { return g0_grid(a->frames); }
 
 int f3_gcn0_bwd(const Gcn0Args* a, hipStream_t s) {
   if (!f3_gcn0_ok(a->K, a->V, a->Ci, 64) || !a->part_dA || !a->part_dW) return F3_EINVAL;
-  if (a->Ci == 3) hipLaunchKernelGGL((gcn0_bwd_kernel<3, 3>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL((gcn0_bwd_kernel<3, 2>), dim3(g0_grid(a->frames)), dim3(256), 0, s, *a);
+  const dim3 grid(g0_grid(a->frames));
+  if (a->f32) {
+    if (a->Ci == 3) hipLaunchKernelGGL((gcn0_bwd_kernel<3, 3, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((gcn0_bwd_kernel<3, 2, true>), grid, dim3(256), 0, s, *a);
+  } else {
+    if (a->Ci == 3) hipLaunchKernelGGL((gcn0_bwd_kernel<3, 3, false>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((gcn0_bwd_kernel<3, 2, false>), grid, dim3(256), 0, s, *a);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -65,6 +65,9 @@ struct Gcn0Args {
   int accumulate;
   float* part_dA;               // bwd: per-block partial rows [blocks][K*V*V]
   float* part_dW;               // bwd: per-block partial rows [blocks][K*64*Ci] (gradient layout)
+  // 1: fp32 operands and results (the bf16x3 mode: x, w, z, g, dg are float* behind these
+  // pointers; products in fp32 on the VALU / fp32 MFMA instead of bf16)
+  int f32;
 };
 
 struct GcnBiasBwdArgs {

@@ -574,6 +574,13 @@ inline int side_pct(bool split, int l) {
   static const int from = getenv("F3_SIDE_FRAC_FROM") ? atoi(getenv("F3_SIDE_FRAC_FROM")) : 2;
   return split && pct > 0 && l >= from ? pct : 0;
 }
+// bf16x3: the first block's gcn (Cin = 3: a 9-column GEMM) on layer0.hip's fused kernels in their
+// fp32 form (mix + GEMM + bias + BN1 sums in one pass; backward dZ, dx, dA and dW partials in one
+// pass). F3_GCN0_X3=0: the generic mix + split GEMMs + weight-gradient GEMM
+inline bool gcn0_x3() {
+  static const bool on = !getenv("F3_GCN0_X3") || atoi(getenv("F3_GCN0_X3")) != 0;
+  return on;
+}
 inline bool x3_l0_fp32() {
   static const bool on = getenv("F3_X3_L0_FP32") && atoi(getenv("F3_X3_L0_FP32")) != 0;
   return on;
@@ -614,7 +621,8 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
     // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
-    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : (wc == 2 && x3_l0_fp32() ? 0 : wc);
+    const bool l0f = wc == 2 && (x3_l0_fp32() || (gcn0_x3() && f3_gcn0_ok(K, V, Ci, C)));  // fp32 weights
+    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : (l0f ? 0 : wc);
     add_job(pt, PREP_PACK_GCN, C * K * Ci * (gc == 3 ? 3 : 1), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
     add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
             wc == 2 ? 3 : wc);  // bf16x3: K-concatenated for the bf16 implicit-GEMM kernels
@@ -661,12 +669,13 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     std::memset(&bnr, 0, sizeof(bnr));
     if (L.res == RES_CONV) bnr = q.ref(L.bnr, X.bnr, (float)Mo, eval);
     // graph mix then 1x1 conv (stgcan.py:50-56)
-    if (hb && f3_gcn0_ok(K, V, Ci, C)) {  // the 3-channel first block: one kernel (layer0.hip)
+    if ((hb || (x3 && gcn0_x3())) && f3_gcn0_ok(K, V, Ci, C)) {  // the 3-channel first block: one kernel (layer0.hip)
       Gcn0Args g0;
       std::memset(&g0, 0, sizeof(g0));
       g0.frames = N * Ti; g0.K = K; g0.V = V; g0.Ci = Ci; g0.A = X.aeff;
       g0.x = reinterpret_cast<const unsigned short*>(X.x); g0.w = bf(X.gw, 1); g0.beff = X.beff;
       g0.z = bfa(X.z, 1); g0.g = bfa(X.g, 1); g0.st_sum = X.bn1.fsum; g0.st_sq = X.bn1.fsq;
+      g0.f32 = x3;  // bf16x3: fp32 x / w / Z / g behind the same pointers
       F3_TRY(f3_gcn0_fwd(&g0, s));
     } else {
       MixArgs mx;
@@ -874,7 +883,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     if (gcat) { bb.dgb = bfa(dg, 1); bb.x3 = 1; }
     if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
-    const bool g0 = hb && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
+    const bool g0 = (hb || (x3 && gcn0_x3())) && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
     Gcn0Args b0;
     std::memset(&b0, 0, sizeof(b0));
     int g0_parts = 0;
@@ -882,6 +891,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       b0.frames = N * Ti; b0.K = K; b0.V = V; b0.Ci = Ci; b0.A = X.aeff;
       b0.x = reinterpret_cast<const unsigned short*>(X.x); b0.w = bf(X.gw, 1); b0.z = bfa(X.z, 1);
       b0.dg = bfa(dg, 1); b0.dx = dx; b0.accumulate = L.res == RES_ID;
+      b0.f32 = x3;  // bf16x3: fp32 x / w / Z / dg
       g0_parts = f3_gcn0_bwd_parts(&b0);
       if ((size_t)g0_parts * (K * V * V + K * C * Ci) > (size_t)kMixParts * K * V * V) return F3_EINVAL;
       b0.part_dA = X.mixpart;
