@@ -1442,11 +1442,25 @@ F3_DEV void ld_act8(const void* p, size_t off, f32x4& x0, f32x4& x1) {
   }
 }
 
-template <bool A16, int FR>
+template <bool A16, int FR, bool HOIST = true>
 __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __shared__ float mu[256], kk[256], m1[256], m2[256], rsv[256];
   const int C = a.C, CG = C / 8, V = a.V, T = a.TV / V, tid = threadIdx.x;
   const float invM = 1.f / (float)a.bn.count;
+  const int v = tid / CG, c0 = (tid - v * CG) * 8;
+  const int n = blockIdx.y, t0 = blockIdx.x * FR, t1 = min(T, t0 + FR);
+  // the first batch's loads go out before the coefficient prologue (they do not depend on it), so
+  // the prologue's parameter loads and barrier overlap them instead of preceding them
+  f32x4 d0[4], d1[4], g0[4], g1[4];
+  const int vl = min(v, V - 1);  // (threads past V load a valid row and return after the barrier)
+  if (HOIST) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t off = ((size_t)(n * T + min(t0 + u, t1 - 1)) * V + vl) * C + c0;
+      ld_act8<A16>(a.dv, off, d0[u], d1[u]);
+      ld_act8<A16>(a.g, off, g0[u], g1[u]);
+    }
+  }
   for (int c = tid; c < C; c += blockDim.x) {
     float sc, sh, rs;
     bn_coeff(a.bn, c, sc, sh, mu[c], rs);
@@ -1462,9 +1476,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
       a.dbeta[c] += (float)a.bsum[c];
     }
   }
-  const int v = tid / CG, c0 = (tid - v * CG) * 8;
   if (v >= V) return;
-  const int n = blockIdx.y, t0 = blockIdx.x * FR, t1 = min(T, t0 + FR);
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
@@ -1475,13 +1487,15 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
   }
 #pragma unroll
   for (int b = 0; b < FR; b += 4) {
-    // the batch's loads first (clamped to the last frame, masked out of the sums; see kRowU)
-    f32x4 d0[4], d1[4], g0[4], g1[4];
+    // the batch's loads first (clamped to the last frame, masked out of the sums; see kRowU);
+    // batch 0's went out before the prologue
+    if (b > 0 || !HOIST) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const size_t off = ((size_t)(n * T + min(t0 + b + u, t1 - 1)) * V + v) * C + c0;
-      ld_act8<A16>(a.dv, off, d0[u], d1[u]);
-      ld_act8<A16>(a.g, off, g0[u], g1[u]);
+      for (int u = 0; u < 4; ++u) {
+        const size_t off = ((size_t)(n * T + min(t0 + b + u, t1 - 1)) * V + v) * C + c0;
+        ld_act8<A16>(a.dv, off, d0[u], d1[u]);
+        ld_act8<A16>(a.g, off, g0[u], g1[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1681,6 +1695,8 @@ __global__ __launch_bounds__(256) void ca_fwd1_kernel(CaArgs a) {
     if (n < a.N) {
       float q = a.b1[j];
       const float* gp = a.gapsum + (size_t)n * C;
+      // (unrolled: the row's loads are independent of the sum; one load round trip per 8 channels)
+#pragma unroll 8
       for (int c = 0; c < C; ++c) q += w1[c] * (gp[c] * a.inv_tv * sc2[c] + sh2[c]);
       a.q1[(size_t)n * H + j] = q;
       qv[r] = q;
@@ -1861,15 +1877,19 @@ __global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
 // workgroup, their channel sums combined in registers before the (double) atomics, so each
 // channel slot takes N/kCaB3Clips atomics instead of N.
 constexpr int kCaB3Clips = 4;
+// NCL = 1 (F3_CA_B3=1, A/B): one clip per workgroup of min(C, 256) threads - N workgroups instead
+// of N / 4 with 3/4 of the threads idle at C = 64 (the kernel is a latency chain per thread)
+template <int NCL>
 __global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
+  constexpr int kCaB3Clips = NCL;
   __shared__ float dq[kCaB3Clips][64];
   const int n0 = blockIdx.x * kCaB3Clips, C = a.C, H = C / 4, N = a.N;
-  for (int i = threadIdx.x; i < kCaB3Clips * H; i += 256) {
+  for (int i = threadIdx.x; i < kCaB3Clips * H; i += blockDim.x) {
     const int nn = i / H, k = i - nn * H;
     dq[nn][k] = n0 + nn < N ? a.dq1[(size_t)(n0 + nn) * H + k] : 0.f;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float sc, sh, mu, rs;
     bn_coeff(a.bn2, c, sc, sh, mu, rs);
     // W1's column c read once for all the workgroup's clips (the clip loop outside re-read it
@@ -2369,8 +2389,16 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
     if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
     else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
   } else {
-    if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    // F3_BNBWD_HOIST=0 (A/B): the first batch's loads after the coefficient prologue
+    static const int hoist = getenv("F3_BNBWD_HOIST") ? atoi(getenv("F3_BNBWD_HOIST")) : 1;
+    if (!hoist) {
+      if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4, false>), dim3(fch, a.N), dim3(threads), 0, s, a);
+      else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4, false>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    } else if (a.act16) {
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
+    }
   }
   F3_LAUNCH_CHECK();
   if (a.no_colsum) return F3_OK;
@@ -2434,7 +2462,13 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ca_bwd3_kernel, dim3((a->N + kCaB3Clips - 1) / kCaB3Clips), dim3(256), 0, s, *a);
+  static const int b3 = getenv("F3_CA_B3") ? atoi(getenv("F3_CA_B3")) : 0;
+  if (b3 == 1) {
+    const int thr = std::min(256, (a->C + 63) / 64 * 64);
+    hipLaunchKernelGGL(ca_bwd3_kernel<1>, dim3(a->N), dim3(thr), 0, s, *a);
+  } else {
+    hipLaunchKernelGGL(ca_bwd3_kernel<kCaB3Clips>, dim3((a->N + kCaB3Clips - 1) / kCaB3Clips), dim3(256), 0, s, *a);
+  }
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
