@@ -38,15 +38,16 @@ constexpr int PW_THREADS = 512;  // 8 waves: wm = wave & 1 (BM/2 rows), wj = wav
 constexpr int PW_VMAX = 18;      // joints of the BIASV table
 
 // BM = rows per tile: 64, or 32 for K = 384 / 768 (a 64-row block of those is 48 / 96 KB)
-template <int EPI, int KS, int WN, int BM>
+template <int EPI, int KS, int WN, int BM, bool F32O = false>
 struct PwLds {
   static constexpr bool ADD = (EPI & EPI_ADD) != 0;
+  static constexpr bool WIDE = ADD || F32O;  // fp32 output image (accumulated, or plain fp32 rows)
   static constexpr int PW_BM = BM;
   static constexpr int K = KS * 32;
   static constexpr int NT = 64 * WN;            // columns per workgroup
   static constexpr int ABUF = PW_BM * K * 2;    // bytes per A buffer ([K/64][BM rows][128 B])
-  static constexpr int OTS = ADD ? NT + 4 : NT + 8;  // output image row stride (elements)
-  static constexpr int ES = ADD ? 4 : 2;             // image element size (fp32 / bf16)
+  static constexpr int OTS = WIDE ? NT + 4 : NT + 8;  // output image row stride (elements)
+  static constexpr int ES = WIDE ? 4 : 2;             // image element size (fp32 / bf16)
   static constexpr int FIXED = PW_BM * OTS * ES + ((EPI & EPI_BIASV) ? PW_VMAX * NT * 4 : 0) +
                                ((EPI & EPI_STATS) ? 2 * 2 * NT * 4 : 0);
   // A ring depth: as many buffers as the LDS holds (NB - 2 tiles stay in flight across the end-of-
@@ -75,9 +76,11 @@ F3_DEV void pw_wait_vm(int k) {
   }
 }
 
-template <int EPI, int KS, int WN, int BM>
+// F32O: fp32 output rows (a.out) instead of bf16 (the bf16x3 mode's fp32 activations), with the
+// A operand's K-concatenated [hi | lo | hi] columns through ConvGemmArgs::kwrap
+template <int EPI, int KS, int WN, int BM, bool F32O = false>
 __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int ncg, int per_wg) {
-  using L = PwLds<EPI, KS, WN, BM>;
+  using L = PwLds<EPI, KS, WN, BM, F32O>;
   constexpr int PW_BM = BM, MX = BM / 32;  // MX: 16-row MFMA tiles per wave
   constexpr int NT = L::NT, KC = KS / 2, OTS = L::OTS, NB = L::NB, LPT = L::LPT;
   constexpr bool ADD = L::ADD;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int q = wave + 8 * i, kc = q / RGN;
-      const unsigned short* p = src ? src + kc * 64 : a.zero;
+      const unsigned short* p = src ? src + acol(a, kc * 64) : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)p, (lds_void_t*)(dst + q * 1024), 16, 0, 0);
     }
   };
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
                    : "=v"(v)
                    : "v"(img_lds + (unsigned)((rl * OTS) * L::ES + c * 16))
                    : "memory");
-      char* dst = ADD ? reinterpret_cast<char*>(a.out + (size_t)m * g.ldo + j0)
+      char* dst = L::WIDE ? reinterpret_cast<char*>(a.out + (size_t)m * g.ldo + j0)
                       : reinterpret_cast<char*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j0);
       *reinterpret_cast<uint4*>(dst + c * 16) = v;
     }
@@ -251,6 +254,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
             ssq[y] += v * v;
           }
           if (ADD) reinterpret_cast<float*>(img)[rl * OTS + jl] = pre[x][r][y] + v;
+          else if (F32O) reinterpret_cast<float*>(img)[rl * OTS + jl] = v;
           else reinterpret_cast<__bf16*>(img)[rl * OTS + jl] = (__bf16)v;
         }
       }
@@ -303,22 +307,37 @@ using namespace f3;
   X(EPI_BIAS, 2, 3)                                                                                   \
   X(0, 2, 3) X(0, 4, 3) X(0, 4, 6) X(0, 6, 1) X(0, 8, 3) X(0, 8, 4)                                   \
   X(EPI_ADD, 4, 1) X(EPI_ADD, 8, 2)
+// the bf16x3 mode's K-concatenated 1x1 GEMMs (K = 3 C) with fp32 output rows (F32O): the gcn input
+// gradients (K 192 / 384 / 768) and the residual forwards (the residual input gradients' 64-row A
+// blocks at K = 384 / 768 do not fit the EPI_ADD ring)
+#define F3_PW_TABLE_X3(X)                                                                             \
+  X(0, 6, 1) X(0, 12, 2) X(0, 24, 1) X(EPI_BIAS | EPI_STATS, 6, 2) X(EPI_BIAS | EPI_STATS, 12, 2)
 
-static bool pw_has(int epi, int ks, int wn) {
+static bool pw_has(int epi, int ks, int wn, bool x3) {
 #define F3_PW_HAS(E, KSV, WNV) \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) return true;
-  F3_PW_TABLE(F3_PW_HAS)
+  if (x3) {
+    F3_PW_TABLE_X3(F3_PW_HAS)
+  } else {
+    F3_PW_TABLE(F3_PW_HAS)
+  }
 #undef F3_PW_HAS
   return false;
 }
 
 // column-group width: the widest 64*WN that divides Nc, keeps the weight slice within 128 VGPRs
 // per lane and is instantiated (0 = none)
-static int pw_wn(const ConvGeom& g, int epi) {
+static int pw_wn(const ConvGeom& g, int epi, bool x3) {
   const int ks = g.Kc / 32;
   for (int wn : {6, 4, 3, 2, 1})
-    if (g.Nc % (64 * wn) == 0 && wn * ks * 4 <= 128 && pw_has(epi, ks, wn)) return wn;
+    if (g.Nc % (64 * wn) == 0 && wn * ks * 4 <= 128 && pw_has(epi, ks, wn, x3)) return wn;
   return 0;
+}
+
+// F3_PW_X3=1 (A/B): the bf16x3 mode's K-concatenated 1x1 GEMMs on this kernel too
+static bool pw_x3_on() {
+  static const bool on = getenv("F3_PW_X3") && atoi(getenv("F3_PW_X3")) != 0;
+  return on;
 }
 
 // Shapes this kernel takes: 1x1 (KT = 1, P = 0) convs over bf16 rows with Kc in {64, 128, 192, 256}
@@ -327,13 +346,15 @@ static int pw_wn(const ConvGeom& g, int epi) {
 bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   static const int on = getenv("F3_PW") ? atoi(getenv("F3_PW")) : 1;
   const ConvGeom& g = a.g;
-  if (!on || !a.inb || !a.wb || !a.zero || a.kwrap) return false;
+  const bool x3 = a.kwrap > 0;  // bf16x3: [hi | lo | hi] x [W_hi | W_hi | W_lo] over K = 3 kwrap, fp32 out
+  if (!on || !a.inb || !a.wb || !a.zero || (x3 && !pw_x3_on())) return false;
+  if (x3 && (a.kwrap % 64 || g.Kc != 3 * a.kwrap || g.lda < 2 * a.kwrap)) return false;
   if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
   if (g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
-  if (!pw_wn(g, epi)) return false;
+  if (!pw_wn(g, epi, x3)) return false;
   const bool add = epi == EPI_ADD;
-  if (add ? !a.out : !a.outb) return false;
-  if (g.ldo % (add ? 4 : 8) != 0) return false;
+  if ((add || x3) ? (!a.out || (!add && a.outb)) : !a.outb) return false;
+  if (g.ldo % ((add || x3) ? 4 : 8) != 0) return false;
   // EPI_ADD is the stride-2 input gradient (accumulating into the even frames only); the others
   // are forwards or stride-1 input gradients
   if (add != (g.transposed && g.S == 2)) return false;
@@ -346,15 +367,16 @@ bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
 
 constexpr int pw_bm(int ks) { return ks > 8 ? 32 : 64; }
 
-template <int EPI, int KS, int WN>
+template <int EPI, int KS, int WN, bool F32O = false>
 static void pw_launch(const ConvGemmArgs& a, int grid, int ncg, int per_wg, hipStream_t s) {
   constexpr int BM = pw_bm(KS);
-  constexpr int lds = PwLds<EPI, KS, WN, BM>::BYTES;
-  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM>,
+  constexpr int lds = PwLds<EPI, KS, WN, BM, F32O>::BYTES;
+  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM, F32O>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds),
                       true);
   (void)once;
-  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg, per_wg);
+  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM, F32O>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg,
+                     per_wg);
 }
 
 int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
@@ -366,7 +388,8 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
     (void)hipGetLastError();
     return n;
   }();
-  const int wn = pw_wn(g, epi), ks = g.Kc / 32;
+  const bool x3 = a.kwrap > 0;
+  const int wn = pw_wn(g, epi, x3), ks = g.Kc / 32;
   if (!wn) return F3_EINVAL;
   const int ncg = g.Nc / (64 * wn);
   const bool par = epi == EPI_ADD;
@@ -384,7 +407,18 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
     F3_LAUNCH_CHECK();                                            \
     return F3_OK;                                                 \
   }
-  F3_PW_TABLE(F3_PW_LAUNCH)
+#define F3_PW_LAUNCH_X3(E, KSV, WNV)                                       \
+  if (epi == (E) && ks == (KSV) && wn == (WNV)) {                          \
+    pw_launch<(E), KSV, WNV, (E) != EPI_ADD>(a, grid, ncg, per_wg, s);     \
+    F3_LAUNCH_CHECK();                                                     \
+    return F3_OK;                                                          \
+  }
+  if (x3) {
+    F3_PW_TABLE_X3(F3_PW_LAUNCH_X3)
+  } else {
+    F3_PW_TABLE(F3_PW_LAUNCH)
+  }
+#undef F3_PW_LAUNCH_X3
 #undef F3_PW_LAUNCH
   return F3_EINVAL;
 }
