@@ -334,9 +334,10 @@ static int pw_wn(const ConvGeom& g, int epi, bool x3) {
   return 0;
 }
 
-// F3_PW_X3=1 (A/B): the bf16x3 mode's K-concatenated 1x1 GEMMs on this kernel too
+// the bf16x3 mode's K-concatenated 1x1 GEMMs on this kernel too: 9.89 -> 9.84 ms/step in three of
+// three interleaved rounds (profiles/r04_pw_x3_ab.txt); F3_PW_X3=0: the tiled igemm_bf16 / igemm_big
 static bool pw_x3_on() {
-  static const bool on = getenv("F3_PW_X3") && atoi(getenv("F3_PW_X3")) != 0;
+  static const bool on = !getenv("F3_PW_X3") || atoi(getenv("F3_PW_X3")) != 0;
   return on;
 }
 
