@@ -1622,8 +1622,9 @@ big:
   // Tap groups (wgrad_big NTW > 1, the (9,1) tcn layers): F3_WG_NTW bit 0 the 256 x 128 tiles
   // (2 taps, BK 32), bit 1 the 128 x 128 tiles (3 taps, BK 32), bit 2 the 64 x 64 tiles (3 taps,
   // BK 32). Measured on MI355X (bf16x3, B = 256): the layer-5 weight gradient 0.260 -> 0.222 ms
-  // per launch pair with bit 0; bits 1 and 2 step-neutral (profiles/r04_ntw_ab.txt). Default 1.
-  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 1;
+  // per launch pair with bit 0; bits 0 + 1 9.90 -> 9.81 ms/step in four of four rounds at the final
+  // defaults, bit 2 no further gain (profiles/r04_ntw_ab.txt, r04_last_ab.txt). Default 3.
+  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 3;
   // F3_WG_NST4 (A/B): 4-stage rings (three stages in flight) - bit 0 the 256 x 128 tap groups (129 KiB
   // of LDS), bit 1 the 128 x 128 tiles (BK 64, 129 KiB)
   static const int nst4 = getenv("F3_WG_NST4") ? atoi(getenv("F3_WG_NST4")) : 0;
