@@ -123,6 +123,9 @@ struct f3_net {
 
   int cur_phase = 1;
   int64_t nparam_phase1 = 0;
+  // f3_net_backward_rmsprop's plan, fixed by the parameter layout: computed once (first call)
+  int fused_opt = -1;                  // -1 unknown, 0 one update after the backward, 1 per layer
+  std::vector<RmsRanges> rest_ranges;  // parameters outside the skeleton layers' ranges
   int add(const std::string& name, int kind, std::vector<int64_t> shape) {
     Entry e;
     e.name = name;
@@ -1473,31 +1476,21 @@ bool layer_ranges_ok(const f3_net& n) {
     }
   return true;
 }
-}  // namespace
 
-extern "C" {
-
-int f3_net_backward_rmsprop(f3_net* net, int N, float* params, const float* dout, float* grads, float* square_avg,
-                            void* workspace, float lr, float alpha, float eps, void* stream) {
-  if (!net || !params || !square_avg) return F3_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
-  // bf16 mode with F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers: no per-layer
-  // update then (one launch after the backward, as f3_net_backward + f3_rmsprop_step)
-  const bool fused = !(net->cfg.precision == F3_PRECISION_BF16 && !wgrad_slab()) && layer_ranges_ok(*net);
-  if (!fused) {
-    F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, nullptr));
-    return f3_rmsprop(params, square_avg, grads, net->nparam, lr, alpha, eps, 1.f, s);
-  }
-  const FusedOpt o{params, square_avg, lr, alpha, eps};
-  F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, &o));
-  // every parameter outside the layers' ranges (data_bn, sensor branch, head), after the join
+// f3_net_backward_rmsprop's plan: whether the per-layer updates apply (bf16 mode with
+// F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers; a layout whose layer entries are
+// not contiguous cannot be updated per layer) and the leftover ranges updated after the join
+void fused_opt_plan(f3_net& n) {
+  n.fused_opt = !(n.cfg.precision == F3_PRECISION_BF16 && !wgrad_slab()) && layer_ranges_ok(n);
+  n.rest_ranges.clear();
+  if (!n.fused_opt) return;
   std::vector<std::pair<long long, long long>> done, rest;
-  for (int si = 0; si < net->nstreams; ++si)
+  for (int si = 0; si < n.nstreams; ++si)
     for (int l = 0; l < 7; ++l) {
-      const RmsRanges r = layer_ranges(*net, net->st[si].L[l]);
+      const RmsRanges r = layer_ranges(n, n.st[si].L[l]);
       for (int j = 0; j < r.n; ++j) done.push_back({r.lo[j], r.lo[j] + r.len[j]});
     }
-  for (const Entry& e : net->entries) {
+  for (const Entry& e : n.entries) {
     if (e.kind != F3_ENTRY_PARAM) continue;
     bool in = false;
     for (auto& d : done) in = in || (e.offset >= d.first && e.offset < d.second);
@@ -1512,12 +1505,41 @@ int f3_net_backward_rmsprop(f3_net* net, int N, float* params, const float* dout
     r.lo[r.n] = rest[i].first;
     r.len[r.n] = rest[i].second - rest[i].first;
     if (++r.n == kRmsRanges || i + 1 == rest.size()) {
-      F3_TRY(f3_rmsprop_ranges(params, square_avg, grads, r, lr, alpha, eps, 1.f, s));
+      n.rest_ranges.push_back(r);
       r.n = 0;
     }
   }
+}
+}  // namespace
+
+extern "C" {
+
+int f3_net_backward_rmsprop(f3_net* net, int N, float* params, const float* dout, float* grads, float* square_avg,
+                            void* workspace, float lr, float alpha, float eps, void* stream) {
+  if (!net || !params || !square_avg) return F3_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  // bf16 mode with F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers: no per-layer
+  // update then (one launch after the backward, as f3_net_backward + f3_rmsprop_step)
+  if (net->fused_opt < 0) fused_opt_plan(*net);
+  if (!net->fused_opt) {
+    F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, nullptr));
+    return f3_rmsprop(params, square_avg, grads, net->nparam, lr, alpha, eps, 1.f, s);
+  }
+  const FusedOpt o{params, square_avg, lr, alpha, eps};
+  F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, &o));
+  // every parameter outside the layers' ranges (data_bn, sensor branch, head), after the join
+  for (const RmsRanges& r : net->rest_ranges)
+    F3_TRY(f3_rmsprop_ranges(params, square_avg, grads, r, lr, alpha, eps, 1.f, s));
   return F3_OK;
 }
+
+int f3_net_fused_rmsprop(f3_net* net) {
+  if (!net) return -1;
+  if (net->fused_opt < 0) fused_opt_plan(*net);
+  return net->fused_opt;
+}
+
+int f3_net_precision(const f3_net* net) { return net ? net->cfg.precision : -1; }
 
 int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
                           int phase, void* stream) {

@@ -58,13 +58,17 @@ struct f3_targcn {
   // f3_targcn_stage_times: timing events around the recurrences and the TA layers (0 = off)
   int timing = 0;
   hipEvent_t tev[11] = {};
-  // GRU group-barrier error flag, copied to a pinned host word after the recurrences
-  int* status_host = nullptr;
-  hipEvent_t status_ev = nullptr;
-  bool status_pending = false;
+  // GRU group-barrier error flag, copied after the recurrences of every call into the next slot of a
+  // ring of pinned host words (one event each), so a flag is never overwritten by a later call's copy
+  // before the host has read it; `sticky` keeps a read flag until a status query reports it
+  static constexpr int kStatusRing = 16;
+  int* status_host = nullptr;              // [kStatusRing]
+  hipEvent_t status_ev[kStatusRing] = {};
+  int status_head = 0, status_count = 0;   // oldest pending slot, number of pending copies
+  bool sticky = false;
   ~f3_targcn() {
     for (auto& e : tev) if (e) (void)hipEventDestroy(e);
-    if (status_ev) (void)hipEventDestroy(status_ev);
+    for (auto& e : status_ev) if (e) (void)hipEventDestroy(e);
     if (status_host) (void)hipHostFree(status_host);
   }
 
@@ -219,11 +223,13 @@ inline void mark(f3_targcn* n, int i, hipStream_t s) {
 
 namespace {
 
-// F3_GN_SKIP_ARRIVE=1: test knob, workgroup 0 of the node-partitioned recurrences never arrives at
-// the group barriers (they time out and raise the flag)
-int gn_skip_arrive() {
+// F3_GN_SKIP_ARRIVE: test knob, workgroup 0 of the node-partitioned recurrences never arrives at
+// the group barriers (they time out and raise the flag): 1 in the forward and backward recurrences,
+// 2 in the backward ones only
+int gn_skip_arrive(bool backward) {
   const char* e = getenv("F3_GN_SKIP_ARRIVE");
-  return e && atoi(e) != 0;
+  const int v = e ? atoi(e) : 0;
+  return v == 1 || (v == 2 && backward);
 }
 
 bool capturing(hipStream_t s) {
@@ -235,31 +241,51 @@ bool capturing(hipStream_t s) {
   return cs != hipStreamCaptureStatusNone;
 }
 
-// a completed, flagged copy from an earlier call -> F3_EDEVICE (the word is cleared)
+// fold the completed copies (oldest first; wait: all of them) into `sticky`; a flag raised by any
+// earlier call -> F3_EDEVICE once (then cleared)
 int take_status(f3_targcn* net, bool wait) {
-  if (!net->status_pending || !net->status_ev) return F3_OK;
-  if (wait) {
-    if (hipEventSynchronize(net->status_ev) != hipSuccess) return F3_EHIP;
-  } else if (hipEventQuery(net->status_ev) != hipSuccess) {
-    (void)hipGetLastError();
-    return F3_OK;
+  while (net->status_count > 0) {
+    const int i = net->status_head;
+    if (wait) {
+      if (hipEventSynchronize(net->status_ev[i]) != hipSuccess) return F3_EHIP;
+    } else if (hipEventQuery(net->status_ev[i]) != hipSuccess) {
+      (void)hipGetLastError();
+      break;  // later copies are behind this one on the same stream order
+    }
+    net->sticky = net->sticky || net->status_host[i] != 0;
+    net->status_host[i] = 0;
+    net->status_head = (i + 1) % f3_targcn::kStatusRing;
+    --net->status_count;
   }
-  net->status_pending = false;
-  const int flag = *net->status_host;
-  *net->status_host = 0;
-  return flag ? F3_EDEVICE : F3_OK;
+  if (!net->sticky) return F3_OK;
+  net->sticky = false;
+  return F3_EDEVICE;
 }
 
-// enqueue the copy of the flag (gsync[GN_MAXG]) to the host word
+// enqueue the copy of the flag (gsync[GN_MAXG]) into the next free slot of the ring (a full ring
+// first waits for its oldest copy and folds it into `sticky`)
 int post_status(f3_targcn* net, const int* gsync, hipStream_t s) {
+  constexpr int R = f3_targcn::kStatusRing;
   if (capturing(s)) return F3_OK;  // the node-partitioned path is off under capture
-  if (!net->status_host && hipHostMalloc(&net->status_host, sizeof(int), hipHostMallocDefault) != hipSuccess)
+  if (!net->status_host) {
+    if (hipHostMalloc(&net->status_host, sizeof(int) * R, hipHostMallocDefault) != hipSuccess) return F3_EHIP;
+    for (int i = 0; i < R; ++i) net->status_host[i] = 0;
+  }
+  if (net->status_count == R) {
+    const int i = net->status_head;
+    if (hipEventSynchronize(net->status_ev[i]) != hipSuccess) return F3_EHIP;
+    net->sticky = net->sticky || net->status_host[i] != 0;
+    net->status_host[i] = 0;
+    net->status_head = (i + 1) % R;
+    --net->status_count;
+  }
+  const int slot = (net->status_head + net->status_count) % R;
+  if (!net->status_ev[slot] && hipEventCreateWithFlags(&net->status_ev[slot], hipEventDisableTiming) != hipSuccess)
     return F3_EHIP;
-  if (!net->status_ev && hipEventCreateWithFlags(&net->status_ev, hipEventDisableTiming) != hipSuccess) return F3_EHIP;
-  if (hipMemcpyAsync(net->status_host, gsync + GN_MAXG, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
+  if (hipMemcpyAsync(net->status_host + slot, gsync + GN_MAXG, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
     return F3_EHIP;
-  if (hipEventRecord(net->status_ev, s) != hipSuccess) return F3_EHIP;
-  net->status_pending = true;
+  if (hipEventRecord(net->status_ev[slot], s) != hipSuccess) return F3_EHIP;
+  ++net->status_count;
   return F3_OK;
 }
 
@@ -381,7 +407,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     g.HC = at<float>(ws, p.HC[l]); g.SU = at<float>(ws, p.SU[l]);
     g.XG = at<void>(ws, p.XG[l]); g.XI = at<void>(ws, p.XI[l]); g.UG = at<void>(ws, p.UG[l]); g.UI = at<void>(ws, p.UI[l]);
     g.hx = at<unsigned short>(ws, p.hx); g.rhx = at<unsigned short>(ws, p.rhx); g.gsync = at<int>(ws, p.gsync);
-    g.dbg_skip_arrive = gn_skip_arrive();
+    g.dbg_skip_arrive = gn_skip_arrive(false);
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
@@ -475,7 +501,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     g.DP = at<void>(ws, p.DP); g.DSG = at<void>(ws, p.DSG); g.DU = at<void>(ws, p.DU); g.DSU = at<void>(ws, p.DSU);
     g.DXG = at<void>(ws, p.DXG); g.DUG = at<void>(ws, p.DUG);
     g.gx1 = at<unsigned short>(ws, p.gx1); g.gx2 = at<unsigned short>(ws, p.gx2); g.gsync = at<int>(ws, p.gsync);
-    g.dbg_skip_arrive = gn_skip_arrive();
+    g.dbg_skip_arrive = gn_skip_arrive(true);
     static long long* prof = nullptr;
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;

@@ -145,6 +145,10 @@ class Fall3RGBStep:
         from .train import TrainStep
         self.model, self.N = model, batch
         self.inner = TrainStep(model.fall3, batch, lr=lr, alpha=alpha, eps=eps, optimizer=optimizer)
+        if self.inner.world > 1:
+            # this step has no gradient all-reduce (neither the skeleton's phased buckets nor the RGB
+            # range): under torchrun it would update each rank from its own shard only
+            raise NotImplementedError("Fall3RGBStep is single-GPU (world 1); use TrainStep for data parallelism")
         dev = model.fall3.flat_parameters().device
         params = [model.rgb.conv.weight, model.rgb.conv.bias, model.rgb.fc.weight, model.rgb.fc.bias]
         offs, off = [], 0

@@ -125,6 +125,12 @@ int f3_net_wait_phase1(f3_net* net, void* stream);
  * parallelism (the all-reduce must come between the two). */
 int f3_net_backward_rmsprop(f3_net* net, int batch, float* params, const float* dout, float* grads, float* square_avg,
                             void* workspace, float lr, float alpha, float eps, void* stream);
+/* 1 if f3_net_backward_rmsprop issues the per-layer updates, 0 if it falls back to the backward
+ * followed by one update (fixed by the parameter layout and precision; planned once per net). */
+int f3_net_fused_rmsprop(f3_net* net);
+
+/* The F3_PRECISION_* the net was created with (reads back f3_config.precision; -1 for NULL). */
+int f3_net_precision(const f3_net* net);
 
 /* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
  * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):
@@ -263,7 +269,8 @@ int f3_targcn_stage_times(f3_targcn* net, int enable, float* ms);
  * Returns F3_EDEVICE if a group barrier of the last forward / backward timed out (its outputs are
  * then wrong), F3_OK otherwise. wait = 1 first waits for that copy; wait = 0 reports only a copy
  * that has completed. Every f3_targcn_forward / _backward also returns F3_EDEVICE (and clears
- * the word) when it finds a completed copy flagged by an earlier call. */
+ * the word) when it finds a completed copy flagged by an earlier call. Each call's copy has its own
+ * host word (a ring), so a flag is reported once even when later calls run before the host asks. */
 int f3_targcn_status(f3_targcn* net, int wait);
 /* loss = -(1/N) sum_i sum_c y_ic log_softmax(out_i)_c (soft targets, not renormalised);
  * dout = dloss/dout. loss is overwritten. */

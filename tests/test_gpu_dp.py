@@ -26,18 +26,19 @@ def _free_port():
 
 
 @pytest.mark.gpu
-def test_two_rank_replicas_stay_identical():
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_two_rank_replicas_stay_identical(precision):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tools", "dp_check.py"), "--backend",
-           "gloo", "--same-device", "--steps", "3"]
+           "gloo", "--same-device", "--steps", "3", "--precision", precision]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(lines[-1])
     assert res["world"] == 2 and res["replicas_identical"] and res["max_param_change"] > 0
     s1 = res["first_step_vs_mean_of_shard_grads"]
-    print(s1)
+    print(precision, s1)
     assert s1["ok"], s1

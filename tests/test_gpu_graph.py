@@ -20,8 +20,9 @@ def _grads(model):
     return {n: p.grad.detach().double().cpu().clone() for n, p in model.named_parameters()}
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("phased", [False, True], ids=["one_pass", "phased"])
-def test_captured_step_matches_eager(phased):
+def test_captured_step_matches_eager(phased, precision):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import fall_multimodal_amd as f3
@@ -30,7 +31,8 @@ def test_captured_step_matches_eager(phased):
     st = oc.init_state(spec, 61)
     B = 32
     sk, se, lb = (torch.from_numpy(x).to(d) for x in synthetic_batch(B, 18, 11, 6, 62))
-    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d)
+    model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d,
+                                      precision=precision)
     model.load_state_dict(st)
     step = f3.TrainStep(model, B, lr=1e-3, phased=phased)
     buf0 = model._flat_buffers.clone()
@@ -70,7 +72,8 @@ def test_captured_step_matches_eager(phased):
     # the whole captured step (incl. RMSprop) replays repeatedly; its loss trajectory is the eager one's
     model._flat_buffers.copy_(buf0)
     losses = [float(step(sk, se, lbl).item()) for _ in range(3)]
-    twin = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d)
+    twin = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, 6, device=d,
+                                     precision=precision)
     twin.load_state_dict(st)
     tstep = f3.TrainStep(twin, B, lr=1e-3, phased=phased)
     ref = [float(tstep(sk, se, lbl).item()) for _ in range(3)]

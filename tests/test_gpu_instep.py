@@ -33,10 +33,13 @@ def _view(ws, ptr, n, dtype):
     return ws[off:off + n * es].view(dtype)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
 @pytest.mark.parametrize("layer,C,T", [(6, 256, 8), (1, 64, 30)])  # T: the position stream's frames
-def test_asm_wait_kernels_inside_the_step(layer, C, T):
+def test_asm_wait_kernels_inside_the_step(layer, C, T, precision):
     """layer 6: igemm_big clip window + wgrad_taps; layer 1 (64 channels, T=30): the
-    weight-stationary tcn64 forward / input gradient (tcn64.hip) and wgrad_big."""
+    weight-stationary tcn64 forward / input gradient (tcn64.hip) and wgrad_big. bf16x3: the same
+    kernels over the K-concatenated [hi | lo] rows (u, dh, dg stored as bf16 rows [x_hi | x_lo] of 2C,
+    h / g fp32, weights fp32), checked against torch fp64 on hi + lo at the split's 1e-4 of max."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import fall_multimodal_amd as f3
@@ -44,7 +47,8 @@ def test_asm_wait_kernels_inside_the_step(layer, C, T):
     d = torch.device("cuda")
     B, V, S = 256, 18, 6
     model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, S, device=d,
-                                      precision="bf16")
+                                      precision=precision)
+    x3 = precision == "bf16x3"
     step = f3.TrainStep(model, B, lr=0.0)
     batch = [torch.from_numpy(x).to(d) for x in synthetic_batch(B, V, 11, S, 257)]
     for _ in range(3):   # several steps: the check reads the last one's tensors
@@ -61,21 +65,26 @@ def test_asm_wait_kernels_inside_the_step(layer, C, T):
             assert p, what
             return _view(step.ws, p, n, dtype)
 
-        u = t("u").float().view(B, T, V, C).permute(0, 3, 1, 2)          # NCHW views of the rows
-        hh = t("h").float().view(B, T, V, C).permute(0, 3, 1, 2)
-        dh = t("dh").float().view(B, T, V, C).permute(0, 3, 1, 2)
-        g = t("g").float().view(B, T, V, C).permute(0, 3, 1, 2)
-        dg = t("dg").float().view(B, T, V, C).permute(0, 3, 1, 2)
+        def rows(what):   # NCHW view of a [B, T, V, C] row tensor as the precision stores it
+            if x3 and what in ("u", "dh", "dg"):   # bf16 rows [hi | lo] of 2C: the value is hi + lo
+                r = t(what, 2 * M * C).double().view(B, T, V, 2, C).sum(3)
+            elif x3:
+                r = t(what, M * C, torch.float32).double().view(B, T, V, C)
+            else:
+                r = t(what).float().view(B, T, V, C)
+            return r.permute(0, 3, 1, 2)
+        u, hh, dh, g, dg = rows("u"), rows("h"), rows("dh"), rows("g"), rows("dg")
         p = f"{pre}.st_gcan_networks.{layer}."
-        W = params[p + "tcn.2.weight"].detach().to(torch.bfloat16).float()
-        bias = params[p + "tcn.2.bias"].detach()
-        # forward (igemm_big clip window), bf16 output
+        W = params[p + "tcn.2.weight"].detach()
+        W = W.double() if x3 else W.to(torch.bfloat16).float()
+        bias = params[p + "tcn.2.bias"].detach().to(W.dtype)
+        # forward (igemm_big clip window), bf16 output (bf16x3: fp32 output of the split products)
         ref = F.conv2d(u, W, bias, padding=(4, 0))
         err = float((hh - ref).abs().max() / ref.abs().max())
-        assert err < 2 ** -7, (pre, "forward", err)
+        assert err < (1e-4 if x3 else 2 ** -7), (pre, "forward", err)
         # weight gradient (wgrad_taps + reduce)
         dw_ref = torch.nn.grad.conv2d_weight(u, W.shape, dh, padding=(4, 0))
-        dw = params[p + "tcn.2.weight"].grad.detach()
+        dw = params[p + "tcn.2.weight"].grad.detach().to(W.dtype)
         err = float((dw - dw_ref).abs().max() / dw_ref.abs().max())
         assert err < 1e-4, (pre, "wgrad", err)
         for dt in range(9):   # per tap, so a garbage tap is named
@@ -88,16 +97,18 @@ def test_asm_wait_kernels_inside_the_step(layer, C, T):
         fq = t("bn1_fsq", C, torch.float64)
         mean = fs / M
         var = (fq / M - mean * mean).clamp_min(0)
-        rs = (1.0 / torch.sqrt(var + 1e-5)).float()
-        gamma = params[p + "tcn.0.weight"].detach()
-        xhat = (g - mean.float().view(1, C, 1, 1)) * rs.view(1, C, 1, 1)
+        rs = (1.0 / torch.sqrt(var + 1e-5)).to(W.dtype)
+        gamma = params[p + "tcn.0.weight"].detach().to(W.dtype)
+        xhat = (g - mean.to(W.dtype).view(1, C, 1, 1)) * rs.view(1, C, 1, 1)
         s1 = dv.sum((0, 2, 3))
         s2 = (dv * xhat).sum((0, 2, 3))
-        bs = t("bn1_bsum", C, torch.float64).float()
+        bs = t("bn1_bsum", C, torch.float64).to(W.dtype)
         err = float((bs - s1).abs().max() / s1.abs().max())
-        assert err < 1e-2, (pre, "bn1 backward sums", err)
+        assert err < (1e-3 if x3 else 1e-2), (pre, "bn1 backward sums", err)
         dg_ref = (gamma * rs).view(1, C, 1, 1) * (dv - (s1 / M).view(1, C, 1, 1) - xhat * (s2 / M).view(1, C, 1, 1))
         err = float((dg - dg_ref).abs().max() / dg_ref.abs().max())
-        assert err < 2 ** -6, (pre, "dgrad", err)
-        frac = float(((dg - dg_ref).abs() > 2 ** -7 * dg_ref.abs().max()).double().mean())
-        assert frac < 1e-4, (pre, "dgrad outliers", frac)
+        assert err < (1e-3 if x3 else 2 ** -6), (pre, "dgrad", err)
+        if not x3:
+            frac = float(((dg - dg_ref).abs() > 2 ** -7 * dg_ref.abs().max()).double().mean())
+            assert frac < 1e-4, (pre, "dgrad outliers", frac)
+        print(f"{precision} layer {layer} {pre}: in-step forward / wgrad / dgrad ok")

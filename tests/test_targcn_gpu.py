@@ -178,3 +178,38 @@ def test_targcn_gru_barrier_timeout_is_reported(monkeypatch):
     step.forward_backward(src, label)
     model.device_status(wait=True)
     assert np.isfinite(step.out.cpu().numpy()).all()
+
+
+def test_targcn_backward_barrier_flag_survives_later_forward(monkeypatch):
+    """a barrier timeout raised only in step k's BACKWARD must still be reported when the
+    host runs ahead and submits step k+1's clean forward before asking (no sync in between): each
+    call's flag copy lands in its own host word, so the later clean copy cannot overwrite it.
+    F3_GN_SKIP_ARRIVE=2 skips the arrivals in the backward recurrences only."""
+    d = dev()
+    import fall_multimodal_amd as f3
+    V, B = 17, 64
+    st = tg.init_state(V, 11)
+    src, label = (torch.from_numpy(x).to(d) for x in tg.synthetic_source(B, V, 11, 5))
+    model = f3.TARGCN(num_nodes=V, device=d, precision="bf16")
+    model.load_state_dict(st)
+    step = f3.TargcnStep(model, B, lr=1e-5)
+    step.forward_backward(src, label)
+    model.device_status(wait=True)
+    monkeypatch.setenv("F3_GN_SKIP_ARRIVE", "2")
+    step.forward_backward(src, label)           # clean forward, faulting backward
+    monkeypatch.delenv("F3_GN_SKIP_ARRIVE")
+    raised = False
+    try:
+        m = step.model
+        m.native_forward(src, step.out, step.ws, f3._lib.stream_handle())   # clean forward, no sync
+        torch.cuda.synchronize()
+    except RuntimeError:                        # the native call may already report it
+        raised = True
+    if not raised:
+        with pytest.raises(RuntimeError):
+            model.device_status(wait=True)
+    torch.cuda.synchronize()
+    model.device_status(wait=True)              # reported once, then clear
+    step.forward_backward(src, label)
+    model.device_status(wait=True)
+

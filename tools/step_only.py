@@ -1,5 +1,5 @@
 """The bench's 3-stream training step alone (B=256, V=18, S=6, eager; precision from F3_STEP_PREC,
-default bf16), for kernel traces:
+default bf16x3, the headline mode), for kernel traces:
     rocprofv3 --kernel-trace -d gpurun_out/step -o run -- python tools/step_only.py [steps] [autograd]
     python tools/timeline.py gpurun_out/step/run_results.db --list
 With `autograd` the step is the reference loop body through the custom ops instead of TrainStep
@@ -20,7 +20,7 @@ def main():
     dev = torch.device("cuda")
     B, V, S, C = 256, 18, 6, 11
     model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, C, S, device=dev,
-                                      precision=os.environ.get("F3_STEP_PREC", "bf16"))
+                                      precision=os.environ.get("F3_STEP_PREC", "bf16x3"))
     sk, se, lb = (torch.from_numpy(x).to(dev) for x in synthetic_batch(B, V, C, S, 100))
     if len(sys.argv) > 2 and sys.argv[2] == "autograd":
         opt = f3.RMSprop(model.parameters(), lr=1e-3)
