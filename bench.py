@@ -136,15 +136,14 @@ def roofline_kernels(dev, batch, V, precision, only=None):
     """The step's GEMM kernels on the layer-6 tcn shape (C=256, T=8, 9 taps, B clips), each
     launched alone through the C ABI exactly as the step launches it:
     * "wgrad": the tcn weight gradient as the step computes it: wgrad_taps<5> (all 9 taps of a
-      64x64 tile from one staged copy of each clip; split-K partials into the slab; F3_WGRAD_TAPS=0:
-      the per-tap wgrad_big<4,2,4,4,64>) + wgrad_slab_reduce (partials summed into dW[Cout][Cin][KT]);
+      64x64 tile from one staged copy of each clip; split-K partials into the slab) + wgrad_slab_reduce (partials summed into dW[Cout][Cin][KT]);
       f3_conv_backward_weight(bf16). The headline roofline (the step's largest kernel share,
       profiles/r01_bf16_kernel_summary.txt);
     * "wgrad_kernel": the GEMM kernel alone (partials left in the slab), for the kernel's own fraction;
     * "tcn_fwd": the forward implicit GEMM with bf16 output (the step writes the tcn output bf16;
       its launch adds the BN-statistics/pool epilogue, EPI 13): igemm_big<1,2,4,false,true>, the
       clip-window form (two clips x 128 channels per workgroup, each channel chunk's rows staged
-      once for all 9 taps); F3_BIG_WIN=0: the 144 x 256 tile igemm_big<1,1,8>.
+      once for all 9 taps).
     Algorithmic FLOP per launch = 2*M*N*K = 2 * (B*8*V) * 256 * (9*256) for all three."""
     if precision == "bf16x3":
         return roofline_kernels_x3(dev, batch, V, only)
@@ -169,20 +168,20 @@ def roofline_kernels(dev, batch, V, precision, only=None):
             "conv")  # packs w into wp; the timed launches reuse it (the GEMM alone)
     ms = _time_launch(lambda: lib.f3_conv_forward(L.ptr(x), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1,
                                                   4, prec, st))
-    win = os.environ.get("F3_BIG_WIN", "1") != "0" and (N * T * V) % 288 == 0 and T * V == 144
-    fname = "igemm_big<1,2,4,false,true> (clip window)" if win else "igemm_big<1,1,8>"
+    win = (N * T * V) % 288 == 0 and T * V == 144
+    fname = "igemm_big<1,2,4,true> (clip window)" if win else "igemm_big<1,1,8>"
     out["tcn_fwd"] = {"kernel": f"{fname + ' bf16-out' if bf else 'conv_gemm_f32'} (tcn 9x1 fwd, C=256, T=8, "
                                 f"N={N}, V={V})", "ms": ms}
     if bf:
         dw = torch.empty(C, C, KT, device=dev)
         ms = _time_launch(lambda: lib.f3_conv_backward_weight(L.ptr(dy), L.ptr(x), L.ptr(dw), None, N, T, V, C, C, KT,
                                                               1, 4, 1, st))
-        taps = os.environ.get("F3_WGRAD_TAPS", "1") != "0" and V % 2 == 0
+        taps = V % 2 == 0
         kname = "wgrad_taps<5>" if taps else "wgrad_big<4,2,4,4,64>"
         out["wgrad"] = {"kernel": f"{kname} + slab reduce (tcn 9x1 weight gradient incl. the "
                                   f"split-K reduce, C=256, T=8, N={N}, V={V})", "ms": ms}
         # the step's slab (net.cpp wgrad_slab_floats)
-        cap = max(512 * 128 * 128, 16 * 256 * 256 * 9) * max(1, int(os.environ.get("F3_SLAB_X", "1")))
+        cap = max(512 * 128 * 128, 16 * 256 * 256 * 9)
         slab = torch.empty(cap, device=dev)
         L.check(lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4, st), "wgrad")
         ms = _time_launch(lambda: lib.f3_conv_wgrad_packed(L.ptr(dy), L.ptr(x), L.ptr(slab), cap, N, T, V, C, C, KT, 1, 4,
@@ -207,7 +206,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     K-concatenated operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
     step's producers write them) on the bf16 LDS-DMA kernels:
     * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,32,2> (taps in groups
-      of two from one staged dY copy; F3_WG_NTW=0: the per-tap wgrad_big<4,2,4,4,64>) over three
+      of two from one staged dY copy) over three
       row segments of the [hi | lo] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
       three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
       (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
@@ -215,13 +214,15 @@ def roofline_kernels_x3(dev, batch, V, only=None):
       one staged copy of each clip) over the three segments + its reduce; "wgrad_kernel": that GEMM
       alone (dw = NULL);
     * "tcn_fwd": the layer-6 forward over K = 9 x 3C (f3_conv_forward_x3cat, fp32 out + bias).
-    Algorithmic FLOP per launch = the split product's three bf16 products, 3 * 2*M*N*K with
-    M = B*8*V, N = 256, K = 9*256; priced against the dense bf16 MFMA peak. `only`: one key (the
-    per-key PMC passes of tools/roofline_pmc.py)."""
+    Algorithmic FLOP per launch = 2*M*N*K with M = B*8*V, N = 256, K = 9*256 (43.5 GFLOP at B=256,
+    V=18), priced against the dense bf16 MFMA peak; the split product issues 3 bf16 products per FLOP
+    (mfma_issue_frac). Algorithmic bytes (the stored formats: [hi | lo] rows = 4 B per element, fp32
+    outputs and weights): wgrad = dY + X + dW, tcn_fwd = X + W + Y. `only`: one key (the per-key PMC
+    passes of tools/roofline_pmc.py)."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
     N, T, C, KT = batch, 8, 256, 9
-    flop = 3 * 2.0 * (N * T * V) * C * (KT * C)
+    flop = 2.0 * (N * T * V) * C * (KT * C)   # algorithmic (the split's 3 products: products_per_flop)
     peak = PEAK_MFMA_TFLOPS["bf16x3"]
     st = L.stream_handle()
 
@@ -242,28 +243,35 @@ def roofline_kernels_x3(dev, batch, V, only=None):
             "conv")  # packs w; the timed launches reuse it (the GEMM alone)
     out = {}
     want = (lambda k: only is None or k == only)
+    row8, row15, wbytes = N * T * V * C * 4, N * 15 * V * C * 4, C * C * KT * 4   # [hi | lo] rows: 4 B / element
     ms = _time_launch(lambda: lib.f3_conv_forward_x3cat(L.ptr(x3), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C,
                                                         KT, 1, 4, st)) if want("tcn_fwd") else 0.0
     out["tcn_fwd"] = {"kernel": f"igemm_big (clip window) over K = 9 x 3C, bf16x3 K-concatenated (tcn 9x1 fwd, C=256, "
-                                f"T=8, N={N}, V={V})", "ms": ms}
+                                f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes * 3 // 2}
     dw = torch.empty(C, C, KT, device=dev)
     db = torch.empty(C, device=dev)
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, C,
                                                                 C, KT, 1, 4, st)) if want("wgrad") else 0.0
     out["wgrad"] = {"kernel": f"wgrad_taps<5> x 3 row segments + reduce (tcn 9x1 weight gradient, bf16x3, C=256, "
-                              f"T=8, N={N}, V={V})", "ms": ms}
+                              f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), None, None, N, T, V, C, C, KT, 1,
                                                                 4, st)) if want("wgrad_kernel") else 0.0
     out["wgrad_kernel"] = {"kernel": f"wgrad_taps<5> x 3 row segments alone (bf16x3, partials left in the slab, "
-                                     f"C=256, T=8, N={N}, V={V})", "ms": ms}
+                                     f"C=256, T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes}
     ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15, V, C,
                                                                 C, KT, 2, 4, st)) if want("wgrad_l5") else 0.0
     out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,2> (2-tap groups) x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
-                                 f"bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms}
-    return _roofline_records({k: v for k, v in out.items() if want(k)}, flop, peak)
+                                 f"bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms,
+                       "bytes": row8 + row15 + wbytes}
+    return _roofline_records({k: v for k, v in out.items() if want(k)}, flop, peak, products=3)
 
 
-def _roofline_records(out, flop, peak):
+def _roofline_records(out, flop, peak, products=1):
+    """flop: ALGORITHMIC FLOPs per launch (2*M*N*K of the reference's conv). `achieved` / `frac` are
+    algorithmic: flop / time / the dense bf16 (or fp32) MFMA peak. bf16x3 issues `products` = 3 bf16
+    MFMA products per algorithmic FLOP; `mfma_issue_frac` = products x frac is the matrix cores' issue
+    utilisation (what rounds <= 4 reported as frac). `algorithmic_bytes`: each operand read once and
+    the result written once, in the stored formats (r["bytes"]); `traffic` the PMC bytes per launch."""
     pmc = {}
     if os.path.exists(ROOFLINE_PMC):
         with open(ROOFLINE_PMC) as f:
@@ -275,7 +283,11 @@ def _roofline_records(out, flop, peak):
         traffic = t.get("bytes_per_launch") if t.get("kernel") == r["kernel"] else None
         res[key] = {"kernel": r["kernel"], "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "flop_per_launch": flop, "ms_per_launch": round(r["ms"], 4)}
+                    "flop_per_launch": flop, "ms_per_launch": round(r["ms"], 4),
+                    "products_per_flop": products, "mfma_issue_frac": round(products * achieved / peak, 4),
+                    "algorithmic_bytes": r.get("bytes"),
+                    "traffic_over_algorithmic": None if (traffic is None or not r.get("bytes")) else
+                    round(traffic / r["bytes"], 3)}
     return res
 
 
@@ -307,7 +319,7 @@ def mix_roofline(dev, batch, V, precision):
     bwd_kern = ("mix_bwd_bf16 (bf16 MFMA) + colsum" if bf and os.environ.get("F3_MIX_BWD_BF16", "1") != "0"
                 else "mix_bwd_x3 (split-bf16 MFMA) + colsum" if x3f else "mix_bwd_lds (fp32 MFMA) + colsum")
     res = {}
-    fwd_kern = ("mix_fwd_bf16 (bf16 MFMA)" if bf and os.environ.get("F3_MIX_FWD_BF16", "1") != "0"
+    fwd_kern = ("mix_fwd_bf16 (bf16 MFMA)" if bf
                 else "mix_fwd_x3 (split-bf16 MFMA, fp32 z)" if x3f else "mix_fwd_wave (fp32 MFMA)")
     for key, byt, ms, kern in (("fwd", bytes_f, ms_f, fwd_kern), ("bwd", bytes_b, ms_b, bwd_kern)):
         gbs = byt / (ms * 1e-3) / 1e9
@@ -413,8 +425,7 @@ def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
         out[nm] = {"us": round(us, 2), "bytes": nbytes[nm], "GBps": round(nbytes[nm] / (us * 1e-6) / 1e9, 1)}
     out["total_us"] = round(sum(acc) * 1e3, 2)
     out["batch"] = B
-    fused = os.environ.get("F3_CNN_FUSED", "0") != "0"
-    out["form"] = "fused (6 launches, F3_CNN_FUSED=1)" if fused else "round-3 launches (the default; F3_CNN_FUSED=1 measured slower)"
+    out["form"] = "six launches (conv1 | BN1+ReLU+pool1 | conv2 | BN2+ReLU+pool2, and their backward)"
     out["note"] = ("HIP events around each stage on the sensor queue (a stage may hold several launches); "
                    "latency-bound (tensors of 0.02-1 MB): GB/s against 8 TB/s is not a meaningful fraction here")
     return out
@@ -911,8 +922,9 @@ def main():
         launch_check(world, rank)
         return
     if world > 1:
+        from fall_multimodal_amd.train import rccl_options
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", pg_options=rccl_options())   # RCCL on a high-priority queue
     dev = torch.device("cuda", local)
     torch.manual_seed(1234 + rank)
 
@@ -1019,7 +1031,7 @@ def main():
                        "global_batch": world * B, "seq_len": 30, "parallelism": f"dp{world}",
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "build-defined, timed on its own (rgb_branch key)",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
-                       "ranks": world, "collective": "rccl all_reduce (2 buckets)" if world > 1 else None},
+                       "ranks": world, "collective": "rccl all_reduce (2 buckets, high-priority streams)" if world > 1 else None},
             "roofline": roofs.get("wgrad_l5", roofs["tcn_fwd"]),
             "roofline_wgrad_l6": roofs.get("wgrad"),
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
@@ -1029,10 +1041,12 @@ def main():
                 (V, S)) is None else round(B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12, 2),
                 "products_per_flop": PRODUCTS[a.precision],
                 "peak": PEAK_MFMA_TFLOPS[a.precision], "frac": None if FLOP_PER_CLIP.get((V, S)) is None else round(
+                    B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12 / PEAK_MFMA_TFLOPS[a.precision], 4),
+                "mfma_issue_frac": None if FLOP_PER_CLIP.get((V, S)) is None else round(
                     PRODUCTS[a.precision] * B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12 /
                     PEAK_MFMA_TFLOPS[a.precision], 4),
-                "note": "whole step (fwd+bwd conv/einsum/addmm FLOPs, SURVEY 8d) x bf16 products per FLOP of the mode "
-                        "/ ms_per_step / dense peak"},
+                "note": "whole step's algorithmic FLOPs (fwd+bwd conv/einsum/addmm, SURVEY 8d) / ms_per_step / dense "
+                        "peak; mfma_issue_frac counts the mode's bf16 products per FLOP (3 for bf16x3)"},
             "sensor": sens,
             "loader": ldr,
             "eval_forward": ev,

@@ -25,9 +25,8 @@ namespace f3 {
 constexpr int BG_MT = 9, BG_NT = 2, BG_NST = 3;  // per-wave MFMA tiles (rows x cols), LDS stages
 constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 
-// BD (B direct): the weight fragments are loaded from global memory straight into registers one
-// k chunk ahead instead of through the LDS stages, which then carry the A rows only (the stages
-// are bound by the L2 -> LDS fill rate, ~12 B/cycle/CU: 50 KB per chunk with B, 18 KB without).
+// (Loading the weight fragments straight from global memory into registers, so the LDS stages carry
+// the A rows only, measured slower: 67 -> 87 us on the layer-6 forward)
 // WIN (clip window): for stride-1 temporal convs whose clips are exactly 144 rows (T*V = 144,
 // the 256-channel layers at T = 8) a workgroup owns two whole clips x BN = 128 output channels.
 // Each channel chunk's 288 input rows are staged ONCE (two 36-KiB A buffers) and all KT taps
@@ -36,10 +35,10 @@ constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 // 720 KiB of L2 -> LDS fill instead of 36 x 50 KiB = 1.8 MiB for the 144 x 256 tile.
 typedef __attribute__((address_space(3))) const char lds_cchar_t;
 constexpr int WIN_APS = 6;  // A pieces of the next chunk carried by one step (steps 2..7 of 9)
-template <int WM, int WN, bool BD = false, bool WIN = false>
+template <int WM, int WN, bool WIN = false>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
-  static constexpr int AP = WIN ? WIN_APS : BM / 8, BP = BD ? 0 : BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
+  static constexpr int AP = WIN ? WIN_APS : BM / 8, BP = BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
   static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;              // pieces per wave
   static constexpr int STAGE = WIN ? BN * 128 : NP * 1024;
   static constexpr int AWIN = WIN ? BM * 128 : 0;    // one A window buffer (WIN: two of them)
@@ -51,10 +50,10 @@ struct BigCfg {
   static constexpr int SMEM = ZOFF + (WIN ? 128 : 0);
 };
 
-template <int EPI, int WM, int WN, bool BD = false, bool WIN = false, bool ARD = false>
+template <int EPI, int WM, int WN, bool WIN = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
-  using Cfg = BigCfg<WM, WN, BD, WIN>;
-  static_assert(!(WIN && (BD || WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips, weights through LDS");
+  using Cfg = BigCfg<WM, WN, WIN>;
+  static_assert(!(WIN && (WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips");
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
   static_assert(WM * WN == BG_WAVES, "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
@@ -96,16 +95,11 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const int dt0 = par ? ((p + g.P) & 1) : 0;
   const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
   const int ntap = par ? (g.KT - dt0 + 1) / 2 : g.KT;
-  // k step t -> (tap, channel chunk): tap-major, or chunk-major (ConvGemmArgs::kmajor)
+  // k step t -> (tap, channel chunk), tap-major (chunk-major order, all taps of a chunk back to back,
+  // measured within 1 %: DESIGN.md §4.11)
   auto tapchunk = [&](int t, int& tap, int& i0) {
-    if (a.kmajor) {
-      const int c = t / ntap;
-      tap = t - c * ntap;
-      i0 = c * G_BK;
-    } else {
-      tap = t / kpt;
-      i0 = (t - tap * kpt) * G_BK;
-    }
+    tap = t / kpt;
+    i0 = (t - tap * kpt) * G_BK;
   };
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
@@ -168,20 +162,6 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // BD: this lane's B fragments of chunk t, [ks][y] = W[wn*32 + y*16 + fr][k0 + (ks*4 + fg)*8 ..+8]
-  bf16x8 fbr[2][BG_NT];
-  auto load_b = [&](int t, bf16x8 (&f)[2][BG_NT]) {
-    int tap, i0;
-    tapchunk(t, tap, i0);
-    const int dt = par ? dt0 + 2 * tap : tap;
-    const int k0 = dt * g.Kc + i0;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int y = 0; y < BG_NT; ++y)
-        f[ks][y] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(wn * 32 + y * 16 + fr) * Ktot + k0 + (ks * 4 + fg) * 8);
-  };
-
   if constexpr (WIN) {
     // step u = (chunk c, tap dt), chunk-major: c = u / KT, dt = u % KT. Per step every wave
     // issues PPW DMAs: its B pieces of step u's weight stage, the 6 A pieces of chunk c + 1 that
@@ -285,7 +265,6 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       if (EPI & EPI_ADD) return;
       __syncthreads();
     } else {
-      if (BD) load_b(0, fbr);
       stage(0, 0);
       if (nchunk > 1) {
         stage(1, 1);
@@ -297,51 +276,10 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     }
     for (int t = 0; t < nchunk; ++t) {
       const int buf = t % 3;
-      bf16x8 fbn[2][BG_NT];
-      if (BD && t + 1 < nchunk) load_b(t + 1, fbn);  // issued before the stage: one vmcnt serves both
       if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
       const char* sa = smem + buf * STAGE;
       const char* sb = sa + AP * 1024;
-      if constexpr (!BD && ARD) {
-        // ARD (F3_BIG_ASM=1): as the WIN loop: both k halves' 22 fragment reads issued at once (inline asm), each half
-        // released by a counted wait; hipcc's own schedule waits lgkmcnt(0) before every MFMA pair
-        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        const unsigned la = (unsigned)(size_t)(lds_cchar_t*)sa, lb = (unsigned)(size_t)(lds_cchar_t*)sb;
-        u32x4_t f[2][BG_NT + BG_MT];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int c = ks * 4 + fg;
-#pragma unroll
-          for (int y = 0; y < BG_NT; ++y) {
-            const int r = wn * 32 + y * 16 + fr;
-            asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(lb + r * 128 + swz(r, c) * 16));
-          }
-#pragma unroll
-          for (int x = 0; x < BG_MT; ++x) {
-            const int r = wm * 144 + x * 16 + fr;
-            asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][BG_NT + x]) : "v"(la + r * 128 + swz(r, c) * 16));
-          }
-        }
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
-          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int q = 0; q < BG_NT + BG_MT; ++q) asm volatile("" : "+v"(f[ks][q]));
-#pragma unroll
-          for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-            for (int y = 0; y < BG_NT; ++y)
-              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[ks][y]),
-                                     acc[x][y]);
-          if (ks == 0) {
-#pragma unroll
-            for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-              for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
-          }
-        }
-      } else
+      // (batched inline-asm fragment reads as in the WIN loop measured neutral here: DESIGN.md §4.6)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 fa[BG_MT], fb[BG_NT];
@@ -349,7 +287,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
         for (int y = 0; y < BG_NT; ++y) {
           const int r = wn * 32 + y * 16 + fr;
-          fb[y] = BD ? fbr[ks][y] : *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+          fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
         }
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x) {
@@ -365,12 +303,6 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (BD && t + 1 < nchunk) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int y = 0; y < BG_NT; ++y) fbr[ks][y] = fbn[ks][y];
-      }
     }
   }
   __syncthreads();
@@ -522,10 +454,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 using namespace f3;
 
 // Large tiles pay when the k loop is long enough to amortise the 3-stage prologue.
-// F3_IGEMM_BIG=0 turns the kernel off (A/B against igemm_bf16).
 bool f3_igemm_big_ok(const ConvGemmArgs& a) {
-  static const int on = getenv("F3_IGEMM_BIG") ? atoi(getenv("F3_IGEMM_BIG")) : 1;
-  if (!on || !f3_igemm_ok(a)) return false;
+  if (!f3_igemm_ok(a)) return false;
   if (a.g.Nc != 128 && a.g.Nc != 256) return false;
   return a.g.KT * a.g.Kc / G_BK >= 6;
 }
@@ -540,15 +470,9 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
     const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
     tiles = (M0 + BM - 1) / BM + (M1 + BM - 1) / BM;
   }
-  // F3_BIG_BDIRECT=1: weight fragments straight to registers (BD), A rows only through LDS
-  static const int bd = getenv("F3_BIG_BDIRECT") ? atoi(getenv("F3_BIG_BDIRECT")) : 0;
-  // F3_BIG_ASM=1: the batched inline-asm fragment reads of the WIN loop in the regular loop too
-  static const int ard = getenv("F3_BIG_ASM") ? atoi(getenv("F3_BIG_ASM")) : 0;
 #define F3_BCASE(E)                                                                        \
   if (epi == (E)) {                                                                       \
-    if (bd) hipLaunchKernelGGL((igemm_big<(E), WM, WN, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    else if (ard) hipLaunchKernelGGL((igemm_big<(E), WM, WN, false, false, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);   \
+    hipLaunchKernelGGL((igemm_big<(E), WM, WN>), dim3(tiles), dim3(BG_THREADS), 0, s, a);  \
     F3_LAUNCH_CHECK();                                                                     \
     return F3_OK;                                                                          \
   }
@@ -564,29 +488,22 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
 }
 
 // Clip-window form (WIN): stride-1 9-tap temporal convs (forward or input gradient) of the
-// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows. F3_BIG_WIN=0 turns it
-// off (A/B against the 144 x 256 tile).
+// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows.
 static bool big_win_ok(const ConvGemmArgs& a) {
-  static const int on = getenv("F3_BIG_WIN") ? atoi(getenv("F3_BIG_WIN")) : 1;
   const ConvGeom& g = a.g;
-  return on && g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
+  return g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
          g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % G_BK == 0 && g.Kc / G_BK >= 2 && !igemm_parity(g);
 }
 
 int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
-  // F3_BIG_KMAJOR=1: chunk-major k order in the tiled (non-window) kernel (ConvGemmArgs::kmajor)
-  static const int kmaj = getenv("F3_BIG_KMAJOR") ? atoi(getenv("F3_BIG_KMAJOR")) : 0;
-  ConvGemmArgs ak = *args;
-  ak.kmajor = kmaj;
-  const ConvGemmArgs& a = ak;
-  args = &ak;
+  const ConvGemmArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   if (big_win_ok(a)) {
     const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
 #define F3_WCASE(E)                                                                        \
     if (epi == (E)) {                                                                     \
-      hipLaunchKernelGGL((igemm_big<(E), 2, 4, false, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+      hipLaunchKernelGGL((igemm_big<(E), 2, 4, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
       F3_LAUNCH_CHECK();                                                                   \
       return F3_OK;                                                                        \
     }

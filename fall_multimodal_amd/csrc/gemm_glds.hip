@@ -381,26 +381,14 @@ bool f3_igemm_ok(const ConvGemmArgs& a) {
 
 // Window mode (see igemm_bf16): stride-1 temporal convs with "same" padding whose output
 // channels fit one column tile (64 or 128) and whose window fits the LDS reserve.
-// F3_IGEMM_WIN=0 turns it off.
 static bool igemm_win_ok(const ConvGemmArgs& a, int epi) {
-  static const int on = getenv("F3_IGEMM_WIN") ? atoi(getenv("F3_IGEMM_WIN")) : 1;
   const ConvGeom& g = a.g;
-  if (!on || g.S != 1 || g.KT < 2 || 2 * g.P != g.KT - 1 || g.T_in != g.T_out) return false;
+  if (g.S != 1 || g.KT < 2 || 2 * g.P != g.KT - 1 || g.T_in != g.T_out) return false;
   // 128 channels: only the input gradient (77 vs 87-111 us for igemm_big at layer 4; the
-  // forward measured 77 vs 58 us)
-  // (F3_WIN128_FWD=1: the 128-channel forward too - A/B for the bf16x3 operands, K = 9 x 3C)
-  static const int fwd128 = getenv("F3_WIN128_FWD") ? atoi(getenv("F3_WIN128_FWD")) : 0;
-  if (g.Nc != 64 && !(g.Nc == 128 && (epi == EPI_RELUMASK || fwd128))) return false;
+  // forward measured 77 vs 58 us, and within noise on the bf16x3 operands)
+  if (g.Nc != 64 && !(g.Nc == 128 && epi == EPI_RELUMASK)) return false;
   if (G_BM + 2 * g.P * g.V > G_WIN_ROWS || g.M % (g.T_out * g.V) != 0) return false;
   return epi == (EPI_BIAS | EPI_STATS | EPI_GAP) || epi == EPI_RELUMASK || epi == EPI_BIAS;
-}
-
-static int igemm_stages() {
-  static const int v = [] {
-    const char* e = getenv("F3_IGEMM_STAGES");
-    return e && atoi(e) == 3 ? 3 : 2;
-  }();
-  return v;
 }
 
 template <int WN, int NST, bool WIN = false>
@@ -436,21 +424,12 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (!f3_igemm_ok(a)) return F3_EINVAL;
   if (f3_tcn64_ok(a, epi)) return f3_tcn64(args, epi, s);
   if (f3_pw_ok(a, epi)) return f3_pw_gemm(args, epi, s);
+  // two LDS stages (three measured slower for both the windows and the tiles)
   if (igemm_win_ok(a, epi)) {
-    // F3_WIN_STAGES=3: three weight stages (two in flight across the raw end-of-step barrier)
-    static const int wst = getenv("F3_WIN_STAGES") && atoi(getenv("F3_WIN_STAGES")) == 3 ? 3 : 2;
-    if (wst == 3) {
-      if (a.g.Nc == 128) return launch_igemm<4, 3, true>(a, epi, s);
-      return launch_igemm<2, 3, true>(a, epi, s);
-    }
     if (a.g.Nc == 128) return launch_igemm<4, 2, true>(a, epi, s);
     return launch_igemm<2, 2, true>(a, epi, s);
   }
   if (f3_igemm_big_ok(a)) return f3_igemm_big(args, epi, s);
-  if (igemm_stages() == 3) {
-    if (a.g.Nc > 64 && a.g.Nc % 128 == 0) return launch_igemm<4, 3>(a, epi, s);
-    return launch_igemm<2, 3>(a, epi, s);
-  }
   // 128-wide column tiles unless they would leave a partial tile (Nc = 192: the gcn input
   // gradient of the 64-channel layers, where a second 128-wide tile is half empty)
   if (a.g.Nc > 64 && a.g.Nc % 128 == 0) return launch_igemm<4, 2>(a, epi, s);
@@ -764,10 +743,10 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int j0 = bx * TJ;
   const int grp = by / itiles, dt0 = grp * NTW;  // taps dt0 .. dt0 + NTW - 1
   const int i0 = (by - grp * itiles) * TI;
-  // bf16x3 row segments (x3seg): split bz covers rows of segment seg = bz / seg_splits, whose
+  // bf16x3 row segments (x3seg): split bz = row range bz / 3, segment seg = bz % 3, whose
   // operands sit at column offsets (0, 0) hi x hi, (Nc, 0) lo x hi, (0, Kc) hi x lo of the rows
-  const int seg = a.x3seg ? (a.seg_minor ? bz % 3 : bz / a.seg_splits) : 0;
-  const int r_begin = (a.x3seg ? (a.seg_minor ? bz / 3 : bz - seg * a.seg_splits) : bz) * a.rows_per_split;
+  const int seg = a.x3seg ? bz % 3 : 0;
+  const int r_begin = (a.x3seg ? bz / 3 : bz) * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
   const bool do_db = a.db && by == 0 && seg < 2;
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
@@ -1005,8 +984,8 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const int bz = lin / tiles, tile = lin - bz * tiles;
   const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
   // bf16x3 row segments (x3seg, as wgrad_big): (dY_hi, X_hi), (dY_lo, X_hi), (dY_hi, X_lo)
-  const int seg = a.x3seg ? (a.seg_minor ? bz % 3 : bz / a.seg_splits) : 0;
-  const int n_begin = (a.x3seg ? (a.seg_minor ? bz / 3 : bz - seg * a.seg_splits) : bz) * a.rows_per_split;  // clips per split
+  const int seg = a.x3seg ? bz % 3 : 0;
+  const int n_begin = (a.x3seg ? bz / 3 : bz) * a.rows_per_split;  // clips per split
   const int n_end = min(g.M / TV, n_begin + a.rows_per_split);
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
   const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb) + (seg == 2 ? g.Kc : 0);
@@ -1096,7 +1075,7 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   __syncthreads();
   for (int t = 0; t < nst; ++t) {
     const int buf = t & 1;
-    if (t + 1 < nst && a.dbg != 2) stage(n_begin + t + 1, buf ^ 1);
+    if (t + 1 < nst) stage(n_begin + t + 1, buf ^ 1);
     const unsigned base = lds0 + buf * STAGE;
     // k step ks + 1's 26 fragment reads are issued before k step ks's MFMAs (two register sets);
     // the loop is branch-free between every read and its wait, so no read destination can be
@@ -1131,12 +1110,10 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
       // second half: the 5th column is the ones fragment (bit select, no branch)
       fbs[4] = __builtin_bit_cast(bf16x8, (__builtin_bit_cast(u32x4_t, fbs[4]) & keep_v) | ones_v);
       if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
-      if (a.dbg != 1) {
 #pragma unroll
-        for (int tt = 0; tt < 5; ++tt)
+      for (int tt = 0; tt < 5; ++tt)
 #pragma unroll
-          for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fbs[tt], acc[tt][x]);
-      }
+        for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fbs[tt], acc[tt][x]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1152,192 +1129,6 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   // partials in fragment order, slab[split][tile][wi][dt][x][lane] as 16-B pieces: each store is
   // one contiguous KiB per wave (the reference-layout scatter took 80 4-B stores per lane at
   // the kernel's end, when every CU stores at once); wgrad_taps_reduce_kernel reorders
-  f32x4* slab = reinterpret_cast<f32x4*>(a.slab) + ((size_t)(bz * tiles + tile) * 4 + wi) * 9 * 4 * 64 + lane;
-#pragma unroll
-  for (int tt = 0; tt < 5; ++tt) {
-    if (tt < ntap) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x) slab[((dt0 + tt) * 4 + x) * 64] = acc[tt][x];
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
-// wgrad_seg<NKS, S>: wgrad_taps' tap reuse for every (9,1) tcn layer, not only the clips that fit
-// one staged window. A work unit is (clip, segment of kSegFrames = 8 output frames); output frame
-// t, tap dt reads input frame S*t + dt - 4, so a unit stages
-//   dY rows of output frames [t0, t0 + 8)                      -> Y rows [0, 8V)
-//   S = 1: input frames t0-4 .. t0+11 (real halo frames of the same clip)  -> X rows [0, 16V);
-//          tap dt reads X row m + dt*V (m = dY row within the unit)
-//   S = 2: the input frames de-interleaved by parity: even frames 2t0-4, 2t0-2, ... -> E rows,
-//          odd frames 2t0-3, 2t0-1, ... -> O rows (12 frames each); tap dt reads E row
-//          m + (dt/2)*V (dt even) or O row m + ((dt-1)/2)*V (dt odd): a uniform row shift again.
-// Rows outside the clip (frame < 0 or >= T) and the dY rows past a short last segment are DMA'd
-// from the zero page, so no unit sees another unit's rows and no masking is needed. Fragments,
-// waves, the MFMA schedule (all reads unconditional, nothing but address arithmetic and MFMAs
-// between a read and its wait), the bias column and the slab format are wgrad_taps'.
-// Needs: bf16 operands, forward geometry, KT = 9, P = 4, S in {1, 2}, V even, V <= 18,
-// 8V % 8 == 0, roundup(8V, 32) == 32*NKS, Nc % 64 == 0, Kc % 64 == 0.
-// ----------------------------------------------------------------------------
-constexpr int kSegFrames = 8;
-
-template <int NKS, int S>
-__global__ __launch_bounds__(512) void wgrad_seg(WgradArgs a) {
-  constexpr int R = 128;                                      // row bytes of every region (64 bf16)
-  constexpr int TVP = 32 * NKS;                               // padded dY rows of a unit
-  constexpr int VMAX = 18;
-  constexpr int NREG = S == 1 ? 1 : 2;                        // input regions (X, or E and O)
-  constexpr int RR = S == 1 ? TVP + 8 * VMAX : TVP + 4 * VMAX;  // rows of one input region
-  constexpr int Y_BYTES = TVP * R, STAGE = Y_BYTES + NREG * RR * R;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const ConvGeom& g = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int V = g.V, SV = kSegFrames * V;
-  const int nseg = (g.T_out + kSegFrames - 1) / kSegFrames;
-  const int jt = g.Nc / 64, tiles = jt * (g.Kc / 64);
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // a split's tiles stay on one XCD
-  const int bz = lin / tiles, tile = lin - bz * tiles;
-  const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
-  const int nunits = g.M / (g.T_out * V) * nseg;
-  const int u_begin = bz * a.rows_per_split;                // rows_per_split holds units per split
-  const int u_end = min(nunits, u_begin + a.rows_per_split);
-  const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb);
-  const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb);
-  const __bf16* zp = reinterpret_cast<const __bf16*>(a.zero);
-  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
-
-  // ---- staging: 1-KiB pieces (8 rows); a lane's rows are fixed, their source frame per unit ----
-  const int xrows = (S == 1 ? kSegFrames + 8 : kSegFrames + 4) * V;
-  const int npy = SV / 8, npx = xrows / 8, np = npy + NREG * npx, ppw = (np + 7) / 8;
-  const int sub = lane >> 3, ph = lane & 7;
-  constexpr int PPW_MAX = (TVP / 8 + NREG * (RR / 8) + 7) / 8;
-  unsigned ldso[PPW_MAX];
-  long long rowoff[PPW_MAX];  // source offset from the unit's first dY row / first input frame
-  int rfr[PPW_MAX];           // the row's frame offset within the unit's window
-  bool isy[PPW_MAX];
-#pragma unroll
-  for (int k = 0; k < PPW_MAX; ++k) {
-    int piece = k * 8 + wave;
-    if (piece >= np) piece %= np;  // the last round re-issues earlier pieces: same bytes, same place
-    const bool y = piece < npy;
-    const int q = piece - npy, kd = y ? 0 : 1 + (q >= npx);   // 0 dY, 1 X / E, 2 O
-    const int pr = y ? piece : q - (kd - 1) * npx;
-    const int crow = pr * 8 + sub;                            // row within its region
-    const int qf = crow / V, vv = crow - qf * V;
-    const int u = (ph >> 1) ^ wswz<4>(crow);
-    const int col = (u * 2 + (ph & 1)) * 8;
-    isy[k] = y;
-    ldso[k] = (unsigned)((y ? 0 : Y_BYTES + (kd - 1) * RR * R) + crow * R + ph * 16);
-    rfr[k] = y ? qf : S * qf + (kd - 1);
-    rowoff[k] = y ? (long long)crow * a.ldy + j0 + col : (long long)(rfr[k] * V + vv) * g.lda + i0 + col;
-  }
-  auto stage = [&](int unit, int buf) {
-    const int n = unit / nseg, t0 = (unit - n * nseg) * kSegFrames, fb = S * t0 - 4;
-    const __bf16* yb = dyb + ((long long)n * g.T_out + t0) * V * a.ldy;
-    const __bf16* xbase = xb + ((long long)n * g.T_in + fb) * V * g.lda;  // dereferenced only in range
-#pragma unroll
-    for (int k = 0; k < PPW_MAX; ++k) {
-      if (k < ppw) {
-        const int f = isy[k] ? t0 + rfr[k] : fb + rfr[k];
-        const bool ok = isy[k] ? f < g.T_out : (f >= 0 && f < g.T_in);
-        const __bf16* src = ok ? (isy[k] ? yb : xbase) + rowoff[k] : zp;
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (lds_void_t*)(size_t)(lds0 + buf * STAGE + ldso[k] - lane * 16), 16, 0, 0);
-      }
-    }
-  };
-
-  // ---- fragment lanes (wgrad_taps') ----
-  const int wi = wave & 3, kh = wave >> 2;
-  const int ntap = kh == 0 ? 5 : 4, dt0 = kh * 5;
-  const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
-  const int r0 = 8 * fg + tq;
-  const int fa = wswz<4>(r0);
-  unsigned offa[4];
-#pragma unroll
-  for (int x = 0; x < 4; ++x) offa[x] = r0 * R + ((x ^ fa) * 32) + tp * 8;
-  unsigned offl[5], offh[5];
-#pragma unroll
-  for (int tt = 0; tt < 5; ++tt) {
-    const int dt = dt0 + min(tt, ntap - 1);
-    const int reg = S == 1 ? 0 : (dt & 1), sh = S == 1 ? dt : (dt >> 1);
-    const int rl = r0 + sh * V, rh = rl + 4;
-    const unsigned rb = Y_BYTES + reg * RR * R;
-    offl[tt] = rb + rl * R + ((wi ^ wswz<4>(rl)) * 32) + tp * 8;
-    offh[tt] = rb + rh * R + ((wi ^ wswz<4>(rh)) * 32) + tp * 8;
-  }
-
-  f32x4 acc[5][4];
-#pragma unroll
-  for (int tt = 0; tt < 5; ++tt)
-#pragma unroll
-    for (int x = 0; x < 4; ++x) acc[tt][x] = f32x4{0.f, 0.f, 0.f, 0.f};
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  const unsigned ones_m = kh ? 0xffffffffu : 0u;
-  const u32x4_t ones_v = {0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m, 0x3f803f80u & ones_m};
-  const u32x4_t keep_v = {~ones_m, ~ones_m, ~ones_m, ~ones_m};
-
-  const int nst = u_end - u_begin;
-  if (nst > 0) stage(u_begin, 0);
-  // zero the rows no unit ever stages (dY padding past 8V; each input region past its staged
-  // rows), in both buffers, while the first unit's DMA is in flight (disjoint bytes)
-  for (int b = 0; b < 2; ++b) {
-    for (int o = SV * R + tid * 16; o < Y_BYTES; o += 512 * 16)
-      *reinterpret_cast<f32x4*>(smem + b * STAGE + o) = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < NREG; ++r)
-      for (int o = xrows * R + tid * 16; o < RR * R; o += 512 * 16)
-        *reinterpret_cast<f32x4*>(smem + b * STAGE + Y_BYTES + r * RR * R + o) = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nst; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nst) stage(u_begin + t + 1, buf ^ 1);
-    const unsigned base = lds0 + buf * STAGE;
-    s16x4_t lo[2][9], hi[2][9];
-    auto issue = [&](int ks, s16x4_t (&l)[9], s16x4_t (&h)[9]) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const unsigned p = base + offa[x] + ks * 32 * R;
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[x]) : "v"(p));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(h[x]) : "v"(p), "n"(4 * R));
-      }
-#pragma unroll
-      for (int tt = 0; tt < 5; ++tt) {
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(l[4 + tt]) : "v"(base + offl[tt] + ks * 32 * R));
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(h[4 + tt]) : "v"(base + offh[tt] + ks * 32 * R));
-      }
-    };
-    issue(0, lo[0], hi[0]);
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int c = ks & 1;
-      tr_wait(lo[c], hi[c]);
-      bf16x8 fa_[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        fa_[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][x], hi[c][x], 0, 1, 2, 3, 4, 5, 6, 7));
-      bf16x8 fbs[5];
-#pragma unroll
-      for (int tt = 0; tt < 5; ++tt)
-        fbs[tt] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[c][4 + tt], hi[c][4 + tt], 0, 1, 2, 3, 4, 5, 6, 7));
-      fbs[4] = __builtin_bit_cast(bf16x8, (__builtin_bit_cast(u32x4_t, fbs[4]) & keep_v) | ones_v);
-      if (ks + 1 < NKS) issue(ks + 1, lo[c ^ 1], hi[c ^ 1]);
-#pragma unroll
-      for (int tt = 0; tt < 5; ++tt)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) acc[tt][x] = mfma_bf16x(fa_[x], fbs[tt], acc[tt][x]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (a.db && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) atomic_add_f(a.db + j0 + x * 16 + fg * 4 + r, acc[4][x][r]);
-  }
   f32x4* slab = reinterpret_cast<f32x4*>(a.slab) + ((size_t)(bz * tiles + tile) * 4 + wi) * 9 * 4 * 64 + lane;
 #pragma unroll
   for (int tt = 0; tt < 5; ++tt) {
@@ -1381,13 +1172,9 @@ __global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __r
   *o += *reinterpret_cast<const f32x4*>(img + row * 144 + c4 * 4);
 }
 
-// bf16x3 row segments ordered segment-minor (WgradArgs::seg_minor; F3_SEG_MINOR=0: segment-major).
-// Measured 10.39 -> 10.25-10.32 ms/step alone, 10.18 with the mix frame image
-// (profiles/r04_zimg_segminor_ab.txt)
-static int seg_minor_env() {
-  static const int v = getenv("F3_SEG_MINOR") ? atoi(getenv("F3_SEG_MINOR")) != 0 : 1;
-  return v;
-}
+// bf16x3 row segments are ordered segment-minor (split index = row range * 3 + segment: the three
+// products of one row range on adjacent workgroups; 10.39 -> 10.25-10.32 ms/step against
+// segment-major, profiles/r04_zimg_segminor_ab.txt)
 
 // wgrad_taps applies (see its comment); nks = padded clip rows / 32
 static int wgrad_taps_nks(const WgradArgs& a) {
@@ -1401,18 +1188,12 @@ static int wgrad_taps_nks(const WgradArgs& a) {
   return nks == 4 || nks == 5 ? nks : 0;
 }
 
-static int wgrad_frac() {
-  static const int f = getenv("F3_WGRAD_FRAC") ? std::max(1, std::min(100, atoi(getenv("F3_WGRAD_FRAC")))) : 100;
-  return f;
-}
-
 static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const int TV = a.g.T_out * a.g.V, clips = a.g.M / TV;
   const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
   const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
-  static const int taps_wgs = getenv("F3_TAPS_WGS") ? atoi(getenv("F3_TAPS_WGS")) : 0;
-  const int target = taps_wgs > 0 ? taps_wgs  // one per CU, or the share wg_pct / F3_WGRAD_FRAC of them
-                                  : std::max(1, 256 * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : wgrad_frac()) / 100);
+  // one workgroup per CU, or the share wg_pct of them (side-queue launches beside the main chains)
+  const int target = std::max(1, 256 * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : 100) / 100);
   const int nseg = a.x3seg ? 3 : 1;  // bf16x3 row segments: `splits` clip splits per segment
   int splits = std::max(1, std::min(clips, target / (tiles * nseg)));
   splits = (int)std::min<long long>(splits, a.slab_cap / (per_split * nseg));
@@ -1420,11 +1201,7 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   const int cps = (clips + splits - 1) / splits;
   splits = (clips + cps - 1) / cps;
   a.rows_per_split = cps;  // clips per split
-  a.seg_splits = splits;
-  a.seg_minor = seg_minor_env();
   splits *= nseg;
-  static const int dbg = getenv("F3_TAPS_DBG") ? atoi(getenv("F3_TAPS_DBG")) : 0;
-  a.dbg = dbg;
   const dim3 grid(tiles * splits);
   if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
@@ -1434,92 +1211,6 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
                        a.dw_ref);
     F3_LAUNCH_CHECK();
   }
-  return F3_OK;
-}
-
-// wgrad_seg applies (see its comment): its NKS (4 or 5), 0 if not. F3_WGRAD_SEG: bit 0 stride-1
-// layers, bit 1 stride-2 layers. Off by default: measured on MI355X (B=256 step, serial launches)
-// it is SLOWER than the per-tap wgrad_big tiles it replaces - 61 us vs 35 us for the 64-channel
-// T=30 layers (one 64x64 tile: 256 splits of 4 units, whose 37.7 MB of partials and their
-// reduce, 15.7 us, outweigh the 9x smaller staging) and 83 us vs 53-62 us for the stride-2 layers -
-// and the step 5.94-6.01 -> 6.42 ms (profiles/r03_wgrad_seg_ab.txt).
-static int wgrad_seg_nks(const WgradArgs& a) {
-  static const int on = getenv("F3_WGRAD_SEG") ? atoi(getenv("F3_WGRAD_SEG")) : 0;
-  const ConvGeom& g = a.g;
-  if (!a.dyb || !a.inb || !a.slab || !a.zero || a.outmap != WG_OUT_CONV || a.groups > 1 || g.transposed) return 0;
-  if (g.KT != 9 || g.P != 4 || (g.S != 1 && g.S != 2) || !((on >> (g.S - 1)) & 1)) return 0;
-  if (g.T_out != (g.T_in + 2 * g.P - g.KT) / g.S + 1) return 0;
-  if (g.V % 2 || g.V > 18 || g.Nc % 64 || g.Kc % 64 || a.ldy % 8 || g.lda % 8) return 0;
-  const int SV = kSegFrames * g.V;
-  if (SV % 8 || g.M % (g.T_out * g.V)) return 0;
-  const int nks = (SV + 31) / 32;
-  return nks == 4 || nks == 5 ? nks : 0;
-}
-
-static int launch_wgrad_seg(WgradArgs a, int nks, hipStream_t s) {
-  const int nseg = (a.g.T_out + kSegFrames - 1) / kSegFrames;
-  const int units = a.g.M / (a.g.T_out * a.g.V) * nseg;
-  const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
-  const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
-  static const int target = getenv("F3_SEG_WGS") ? atoi(getenv("F3_SEG_WGS")) : 256;  // one per CU
-  int splits = std::max(1, std::min(units, target / tiles));
-  splits = (int)std::min<long long>(splits, a.slab_cap / per_split);
-  if (splits < 1) return F3_EINVAL;
-  const int ups = (units + splits - 1) / splits;
-  splits = (units + ups - 1) / ups;
-  a.rows_per_split = ups;  // units per split
-  const dim3 grid(tiles * splits);
-  if (a.g.S == 1) {
-    if (nks == 5) hipLaunchKernelGGL((wgrad_seg<5, 1>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_seg<4, 1>), grid, dim3(512), 0, s, a);
-  } else {
-    if (nks == 5) hipLaunchKernelGGL((wgrad_seg<5, 2>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_seg<4, 2>), grid, dim3(512), 0, s, a);
-  }
-  F3_LAUNCH_CHECK();
-  if (a.dw_ref) {
-    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
-                       a.dw_ref);
-    F3_LAUNCH_CHECK();
-  }
-  return F3_OK;
-}
-
-// bf16x3 (K-concatenated) weight gradient: dw_ref[j][i][dt] += sum_s (slab[s][j][dt*Kc2 + i] +
-// slab[s][j][dt*Kc2 + Ci + i] + slab[s][C + j][dt*Kc2 + i]), i.e. the hi*hi + hi*lo + lo*hi quadrants
-// of the [2C][KT][2Ci] partials (the lo*lo quadrant is dropped, as the split-bf16 product drops it);
-// workgroup 0 also folds the [2C] bias-gradient scratch. One thread per (j, dt, i): slab reads are
-// contiguous in i.
-__global__ __launch_bounds__(256) void wgrad_slab_reduce_x3_kernel(const float* __restrict__ slab, int splits, int Nc2,
-                                                                   int Kc2, int KT, int gcn_cin, float* __restrict__ dw_ref,
-                                                                   const float* __restrict__ dbs, float* db) {
-  const int C = Nc2 / 2, Ci = Kc2 / 2;
-  const long long per = (long long)Nc2 * KT * Kc2;
-  const long long n = (long long)C * KT * Ci;
-  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (long long)gridDim.x * 256) {
-    const int j = (int)(idx / ((long long)KT * Ci));
-    const int r = (int)(idx - (long long)j * KT * Ci), dt = r / Ci, i = r - dt * Ci;
-    const float* p0 = slab + (size_t)j * KT * Kc2 + (size_t)dt * Kc2 + i;
-    const float* p1 = slab + (size_t)(C + j) * KT * Kc2 + (size_t)dt * Kc2 + i;
-    float v = 0.f;
-    for (int sp = 0; sp < splits; ++sp) v += p0[sp * per] + p0[sp * per + Ci] + p1[sp * per];
-    if (gcn_cin > 0) {  // gcn reference layout [K*C][gcn_cin]
-      const int k = i / gcn_cin, ci = i - k * gcn_cin;
-      dw_ref[((size_t)k * C + j) * gcn_cin + ci] += v;
-    } else {
-      dw_ref[((size_t)j * Ci + i) * KT + dt] += v;
-    }
-  }
-  if (blockIdx.x == 0 && db && dbs)
-    for (int c = threadIdx.x; c < C; c += 256) db[c] += dbs[c] + dbs[C + c];
-}
-
-static int launch_fold_x3(const WgradArgs& a, int splits, hipStream_t s) {
-  const long long n = (long long)(a.g.Nc / 2) * a.g.KT * (a.g.Kc / 2);
-  const int grid = (int)std::min<long long>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(wgrad_slab_reduce_x3_kernel, dim3(grid), dim3(256), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
-                     a.g.KT, a.gcn_cin, a.dw_ref, a.db, a.db_fold);
-  F3_LAUNCH_CHECK();
   return F3_OK;
 }
 
@@ -1546,9 +1237,9 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
   // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
   static const int slots = resident_wgs((const void*)KERNEL, THREADS);
-  // F3_WGRAD_FRAC (percent): size the splits to that share of the resident slots, leaving CUs to
-  // the main chains the weight gradients run beside (side queues)
-  const int target = getenv("F3_WGRAD_WGS") ? f3_wgrad_target_wgs() : std::max(1, slots * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : wgrad_frac()) / 100);
+  // wg_pct (percent): size the splits to that share of the resident slots, leaving CUs to the main
+  // chains the side-queue weight gradients run beside
+  const int target = std::max(1, slots * (a.wg_pct > 0 ? std::min(100, a.wg_pct) : 100) / 100);
   const int groups = std::max(1, a.groups);  // grouped launches: wgrad_big, atomics (checked by the caller)
   // x3seg: three row segments, `splits` row splits each (one round of resident workgroups in all)
   const int nseg = a.x3seg ? 3 : 1;
@@ -1558,8 +1249,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   if (to_slab) {
     if (a.slab_cap < per_split * nseg) return F3_EINVAL;
     // (the slab grew for wgrad_taps; these tiles keep their measured split count)
-    const bool x3 = a.x3fold || a.x3seg;
-    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, x3 ? a.slab_cap : 512LL * 128 * 128) /
+    splits = (int)std::min<long long>(splits, std::min<long long>(a.slab_cap, a.x3seg ? a.slab_cap : 512LL * 128 * 128) /
                                                   (per_split * nseg));
   }
   int rps = (a.g.M + splits - 1) / splits;
@@ -1567,19 +1257,14 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   if (rps < 256) rps = 256;
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
-  a.seg_splits = splits;
-  a.seg_minor = seg_minor_env();
   splits *= nseg;  // slab partials (all segments)
-  // XCD-aware grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
-  // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time; F3_WGRAD_XCD=0 restores the
-  // round-robin 3-D grid
-  static const int xcd = getenv("F3_WGRAD_XCD") ? atoi(getenv("F3_WGRAD_XCD")) : 1;
-  a.xcd = xcd || THREADS == 512 || groups > 1;  // wgrad_big always maps its 1-D grid by XCD
-  dim3 grid = a.xcd ? dim3(gx * gy * splits * groups) : dim3(gx, gy, splits);
+  // XCD-aware 1-D grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
+  // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time against a round-robin 3-D grid
+  a.xcd = 1;
+  const dim3 grid(gx * gy * splits * groups);
   hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), 0, s, a);
   F3_LAUNCH_CHECK();
   if (to_slab && a.dw_ref) {
-    if (a.x3fold) return launch_fold_x3(a, splits, s);
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
                        a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref, a.gcn_cin);
     F3_LAUNCH_CHECK();
@@ -1591,60 +1276,45 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   const WgradArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;
-  // (x3fold with dw_ref == null: the GEMM alone at the step's split count, partials left in the slab)
-  if (a.x3fold && (!a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.Nc % 2 || a.g.Kc % 2))
-    return F3_EINVAL;
-  if (a.x3fold && a.gcn_cin > 0 && (a.g.KT != 1 || (a.g.Kc / 2) % a.gcn_cin)) return F3_EINVAL;
-  if (a.x3seg && (a.x3fold || !a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.transposed ||
-                  a.ldy < 2 * a.g.Nc || a.g.lda < 2 * a.g.Kc))
+  // (dw_ref == null: the GEMM alone at the step's split count, partials left in the slab)
+  if (a.x3seg && (!a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || a.g.transposed || a.ldy < 2 * a.g.Nc ||
+                  a.g.lda < 2 * a.g.Kc))
     return F3_EINVAL;
   if (a.x3seg && a.gcn_cin > 0 && (a.g.KT != 1 || a.g.Kc % a.gcn_cin)) return F3_EINVAL;
-  // 8-wave wide tiles for the 128/256-channel layers (F3_WGRAD_BIG=0: the 4-wave kernel)
-  static const int big_env = getenv("F3_WGRAD_BIG") ? atoi(getenv("F3_WGRAD_BIG")) : 1;
-  const int big = a.g.transposed ? 0 : big_env;  // wgrad_big walks forward-geometry rows only
+  // 8-wave wide tiles for the 128/256-channel layers; the first 4-wave kernel (wgrad_glds_bf16) only
+  // for transposed-geometry rows, which wgrad_big does not walk
   if (a.groups > 1 && (a.g.transposed || a.slab)) return F3_EINVAL;  // grouped: wgrad_big + atomics only
-  const int bigv = a.groups > 1 ? 1 : big;
-  // F3_WGRAD_TAPS=0: the per-tap wgrad_big tiles for the stride-1 clip-sized layers too
-  static const int taps_env = getenv("F3_WGRAD_TAPS") ? atoi(getenv("F3_WGRAD_TAPS")) : 1;
-  if (taps_env && bigv && !a.x3fold) {  // (the tap-reuse kernels' fragment-order slabs have no x3 fold)
+  const bool bigv = !a.g.transposed;
+  if (bigv) {
+    // all 9 taps of a clip-sized stride-1 layer from one staged copy of each clip (wgrad_taps); clip
+    // segments with halo rows for the other (9,1) layers measured slower (61 vs 35 us)
     const int nks = wgrad_taps_nks(a);
     if (nks) return launch_wgrad_taps(a, nks, s);
-    if (a.x3seg) goto big;  // (wgrad_seg has no row segments)
-    const int nseg = wgrad_seg_nks(a);  // every other (9,1) layer: clip segments, stride 2 by parity
-    if (nseg) return launch_wgrad_seg(a, nseg, s);
   }
-big:
   if (a.x3seg && !bigv) return F3_EINVAL;  // (row segments: wgrad_taps / wgrad_big only)
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,
   // 128 x 256 71 us, 256 x 256 (BK 32) 63 us, the 4-wave 128 x 128 kernel 99 us. The loop is
   // bound by the L2 -> LDS fill rate per CU, so the wider dY tile (each input row staged once
-  // per 256 output channels) wins. F3_WGRAD_BIG=0 restores the first 4-wave kernel (wgrad_glds_bf16).
-  // Tap groups (wgrad_big NTW > 1, the (9,1) tcn layers): F3_WG_NTW bit 0 the 256 x 128 tiles
-  // (2 taps, BK 32), bit 1 the 128 x 128 tiles (3 taps, BK 32), bit 2 the 64 x 64 tiles (3 taps,
-  // BK 32). Measured on MI355X (bf16x3, B = 256): the layer-5 weight gradient 0.260 -> 0.222 ms
-  // per launch pair with bit 0; bits 0 + 1 9.90 -> 9.81 ms/step in four of four rounds at the final
-  // defaults, bit 2 no further gain (profiles/r04_ntw_ab.txt, r04_last_ab.txt). Default 3.
-  static const int ntw = getenv("F3_WG_NTW") ? atoi(getenv("F3_WG_NTW")) : 3;
-  // F3_WG_NST4 (A/B): 4-stage rings (three stages in flight) - bit 0 the 256 x 128 tap groups (129 KiB
-  // of LDS), bit 1 the 128 x 128 tiles (BK 64, 129 KiB)
-  static const int nst4 = getenv("F3_WG_NST4") ? atoi(getenv("F3_WG_NST4")) : 0;
+  // per 256 output channels) wins.
+  // Tap groups (wgrad_big NTW > 1, the (9,1) tcn layers): the 256 x 128 tiles 2 taps (BK 32), the
+  // 128 x 128 tiles 3 taps (BK 32). Measured on MI355X (bf16x3, B = 256): the layer-5 weight gradient
+  // 0.260 -> 0.222 ms per launch pair with the 2-tap groups; both 9.90 -> 9.81 ms/step in four of four
+  // rounds; 3-tap groups for the 64 x 64 tiles and 4-stage rings gave nothing (profiles/r04_ntw_ab.txt,
+  // r04_last_ab.txt, r04_nst4_ab.txt)
   const bool taps9 = a.g.KT == 9;
   if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
-    if (taps9 && (ntw & 1) && (nst4 & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2, 4>, 2>(a, s);
-    if (taps9 && (ntw & 1)) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
+    if (taps9) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
   }
   if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 256 == 0)
     return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4>>(a, s);
   if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
-    if (taps9 && (ntw & 2)) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
-    if (nst4 & 2) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 64, 1, 4>>(a, s);
+    if (taps9) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
   }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);
     if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4>>(a, s);
-    if (taps9 && (ntw & 4)) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2>>(a, s);
   }
   const int TJ = a.g.Nc >= 128 ? 128 : 64, TI = a.g.Kc >= 128 ? 128 : 64;

@@ -48,10 +48,6 @@ struct ConvGemmArgs {
   // (2 kwrap columns, lda >= 2 kwrap) and the third K segment re-reads x_hi: A column k >= 2 kwrap
   // is read at k - 2 kwrap (igemm_bf16 / igemm_big; 0 = off)
   int kwrap;
-  // igemm_big k order: 0 tap-major (all channel chunks of a tap, then the next tap), 1 chunk-major
-  // (the 9 taps of one 64-channel chunk back to back: a tile's rows +- 4 frames of that chunk stay
-  // in L2 across the taps instead of being re-fetched once per tap). Set by the launcher.
-  int kmajor;
 };
 
 enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };
@@ -84,25 +80,16 @@ struct WgradArgs {
   // dw + q*gs_dw, db + q*gs_db. groups <= 1: one problem. Atomics path only (slab == null).
   int groups;
   long long gs_dy, gs_in, gs_dw, gs_db;
-  int dbg;                    // measurement knob of wgrad_taps (F3_TAPS_DBG): 1 no MFMA, 2 no restaging
-  int wg_pct;                 // split sizing, percent of the resident workgroup slots (0: F3_WGRAD_FRAC / all)
+  int wg_pct;                 // split sizing, percent of the resident workgroup slots (0: all)
   int x3;                     // 1: split-bf16 kernel on fp32 dy / in (gemm_x3.hip)
-  // bf16x3 mode on the bf16 kernels (K-concatenated operands): the GEMM ran on dY' = [dY_hi | dY_lo]
-  // (Nc = 2C) and X' = [X_hi | X_lo] (Kc = 2Ci); the slab reduce adds the hh + hl + lh quadrants
-  // into dw_ref [C][Ci][KT], and db (a [2C] scratch here) is folded into db_fold[c] += db[c] + db[C+c].
-  // With gcn_cin > 0 (KT = 1, Ci = K gcn_cin) dw_ref is the gcn weight's reference layout
-  // [K*C][gcn_cin] instead (column k gcn_cin + ci of the packed operand -> row k C + c).
-  int x3fold;
-  float* db_fold;
-  // bf16x3 on the bf16 kernels by row segments (wgrad_big): dy / in are [hi | lo] rows (ldy = 2 Nc,
-  // lda = 2 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi), (dY_lo, X_hi),
-  // (dY_hi, X_lo) - the split product's three terms, no unused quadrant - with seg_splits row splits
-  // per segment (set by the launcher); the bias sums the first two segments (dY_hi + dY_lo).
-  // With gcn_cin > 0 the slab reduce writes the gcn layout (as x3fold).
+  // bf16x3 on the bf16 kernels by row segments (wgrad_big / wgrad_taps): dy / in are [hi | lo] rows
+  // (ldy = 2 Nc, lda = 2 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi),
+  // (dY_lo, X_hi), (dY_hi, X_lo) - the split product's three terms - with the split index
+  // bz = row split * 3 + segment (the three segments of one row range on adjacent workgroups, i.e.
+  // mostly one XCD: X_hi / dY_hi re-reads hit its L2); the bias sums the first two segments
+  // (dY_hi + dY_lo). With gcn_cin > 0 (KT = 1, Ci = K gcn_cin) the slab reduce writes the gcn
+  // weight's reference layout [K*C][gcn_cin] (column k gcn_cin + ci of the packed operand -> row k C + c).
   int x3seg;
-  int seg_splits;
-  int seg_minor;  // 1: split index bz = row split * 3 + segment (the three segments of one row range on
-                  // adjacent workgroups, i.e. mostly one XCD: X_hi / dY_hi re-reads hit its L2)
 };
 
 // Apply a grouped launch's per-problem pointer offsets (no-op for groups <= 1).
@@ -118,17 +105,10 @@ F3_DEV void wgrad_group(WgradArgs& a, int grp) {
 
 }  // namespace f3
 
-// Weight-gradient split-K sizing: target number of workgroups per launch. Each workgroup
-// adds its whole output tile with float atomics (executed at the memory side, ~1.3 TB/s
-// chip-wide), so more splits = more atomic traffic; F3_WGRAD_WGS overrides (tuning).
-inline int f3_wgrad_target_wgs() {
-  static const int v = [] {
-    const char* e = getenv("F3_WGRAD_WGS");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : 512;
-  }();
-  return v;
-}
+// Weight-gradient split-K sizing of the atomics-path kernels (gemm.hip, gemm_bf16.hip, gemm_x3.hip):
+// target number of workgroups per launch. Each workgroup adds its whole output tile with float
+// atomics (executed at the memory side, ~1.3 TB/s chip-wide), so more splits = more atomic traffic.
+inline int f3_wgrad_target_wgs() { return 512; }
 
 int f3_conv_gemm(const f3::ConvGemmArgs* a, int pro, int epi, hipStream_t s);
 int f3_conv_wgrad(const f3::WgradArgs* a, int pro, hipStream_t s);

@@ -272,8 +272,7 @@ using namespace f3;
 
 // instantiated: K = 3 partitions (the 'spatial' strategy) with 3 (positions) or 2 input channels
 bool f3_gcn0_ok(int K, int V, int Ci, int C) {
-  static const int on = getenv("F3_GCN0") ? atoi(getenv("F3_GCN0")) : 1;
-  return on && C == 64 && K == 3 && (Ci == 2 || Ci == 3) && V >= 4 && V <= G0_MAXV &&
+  return C == 64 && K == 3 && (Ci == 2 || Ci == 3) && V >= 4 && V <= G0_MAXV &&
          K * V * V <= 1024;  // dA_eff: 4 entries per thread
 }
 

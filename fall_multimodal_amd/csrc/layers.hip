@@ -318,92 +318,8 @@ F3_DEV f32x4 bf4_to_f4(u32x2 r) {
                __uint_as_float(r.y & 0xffff0000u)};
 }
 
-template <int KS, int CIN, bool XB>  // k steps over v: ceil(V/4), compile-time so the A~ fragments stay in
-__global__ __launch_bounds__(256) void mix_fwd_lds_kernel(MixArgs a) {  // registers; XB: x stored bf16
-  constexpr int kMixPX = MixCap<CIN>::PX;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int K = a.K, V = a.V, KV = K * V;
-  constexpr int Cin = CIN, S = CIN + 20, SZ = CIN + 4;
-  float* xs = sm;                 // [V][S]
-  float* zs = sm + V * S;         // [KV][SZ]
-  float af[4][KS];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) af[mt][ks] = atil(a.A, K, V, 16 * mt + fr, 4 * ks + fg);
-  const int tiles = Cin / 16, n4 = V * Cin / 4, n8 = KV * Cin / 8, C4 = Cin / 4, C8 = Cin / 8;
-  f32x4 rx[XB ? 1 : kMixPX];
-  u32x2 rxb[XB ? kMixPX : 1];  // raw bf16 pieces (converted when written to LDS)
-  // prefetch: unconditional loads from clamped indices (a conditional load is waited for on
-  // the spot — vmcnt(0) per element — which serialised the prefetch meant to overlap the frame)
-  auto prefetch = [&](int f) {
-#pragma unroll
-    for (int q = 0; q < kMixPX; ++q) {
-      const int i = min(tid + q * 256, n4 - 1);
-      if constexpr (XB) rxb[q] = reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.x) + (size_t)f * V * Cin)[i];
-      else rx[q] = reinterpret_cast<const f32x4*>(a.x + (size_t)f * V * Cin)[i];
-    }
-  };
-  if (blockIdx.x < a.frames) prefetch(blockIdx.x);
-  for (int f = blockIdx.x; f < a.frames; f += gridDim.x) {
-    __syncthreads();  // the previous frame is done with xs / zs
-#pragma unroll
-    for (int q = 0; q < kMixPX; ++q) {
-      const int i = tid + q * 256;
-      if (i < n4) {
-        const int v = i / C4, c = (i - v * C4) * 4;
-        if constexpr (XB) *reinterpret_cast<f32x4*>(xs + v * S + c) = bf4_to_f4(rxb[q]);
-        else *reinterpret_cast<f32x4*>(xs + v * S + c) = rx[q];
-      }
-    }
-    __syncthreads();
-    if (f + (int)gridDim.x < a.frames) prefetch(f + gridDim.x);
-    for (int t = wave; t < tiles; t += 4) {
-      const int ci0 = t * 16;
-      f32x4 acc[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      float b[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int v = 4 * ks + fg;
-        b[ks] = xs[min(v, V - 1) * S + ci0 + fr] * (v < V ? 1.f : 0.f);
-      }
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x4(af[mt][ks], b[ks], acc[mt]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int wk = 16 * mt + 4 * fg + r;
-          if (wk < KV) zs[wk * SZ + ci0 + fr] = acc[mt][r];
-        }
-    }
-    __syncthreads();
-    const size_t zoff = (size_t)f * KV * Cin;
-    for (int i = tid; i < n8; i += 256) {
-      const int wk = i / C8, c = (i - wk * C8) * 8;
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(zs + wk * SZ + c);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(zs + wk * SZ + c + 4);
-      if (a.zb) {
-        bf16x8 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { o[e] = (__bf16)u0[e]; o[4 + e] = (__bf16)u1[e]; }
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.zb) + zoff + (size_t)i * 8) = o;
-      } else {
-        *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8) = u0;
-        *reinterpret_cast<f32x4*>(a.z + zoff + (size_t)i * 8 + 4) = u1;
-      }
-    }
-  }
-}
-
-// Wave-per-frame graph mix forward: each wave owns whole frames (no workgroup barrier, so the 3
-// barriers per frame of mix_fwd_lds_kernel are gone), keeps its frame's [V][Cin] input in a
+// Wave-per-frame graph mix forward: each wave owns whole frames (no workgroup barrier: a
+// workgroup-per-frame form paid 3 barriers per frame), keeps its frame's [V][Cin] input in a
 // wave-private LDS slab (bf16 when x is bf16), prefetches the next frame's input into registers
 // during the MFMAs, and writes Z one 16-channel tile at a time through a [64][20] fp32 LDS tile
 // as 16-B row pieces (L2 merges a wave's consecutive tiles into whole lines).
@@ -1993,37 +1909,21 @@ static void allow_big_lds(const void* fn) {
   (void)hipGetLastError();  // a refused attribute must not surface as the next launch's error
 }
 
-static size_t mix_lds_fwd2(const MixArgs& a) {
-  return sizeof(float) * ((size_t)a.V * (a.Cin + 20) + (size_t)a.K * a.V * (a.Cin + 4));
-}
 static size_t mix_lds_bwd2(const MixArgs& a) {
   return sizeof(float) * std::max((size_t)(2 * a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
 }
 
 template <int KS, int CIN, bool XB>
 static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_fwd_lds_kernel<KS, CIN, XB>),
-                      allow_big_lds((const void*)mix_fwd_wave_kernel<KS, CIN, XB>), true);
+  static bool once = (allow_big_lds((const void*)mix_fwd_wave_kernel<KS, CIN, XB>), true);
   (void)once;
-  // F3_MIX_WAVE=0: the workgroup-per-frame kernel. (A bf16-MFMA form with 64-channel groups
-  // assembled in LDS and written as whole 128-B row segments measured slower: 31 / 34 / 29 us vs
-  // 25 / 25 / 25 at the three layer shapes; the fp32 MFMA work is not what bounds these kernels.)
-  static const int wave_env = getenv("F3_MIX_WAVE") ? atoi(getenv("F3_MIX_WAVE")) : 1;
-  if (wave_env) {
-    const size_t per_wave = 18 * (CIN + (XB ? 8 : 4)) * (XB ? 2 : 4) + 64 * 20 * 4;
-    static const int wcap = getenv("F3_MIX_WGRID") ? atoi(getenv("F3_MIX_WGRID")) : 1024;
-    const int grid = std::max(1, std::min((a->frames + 3) / 4, wcap));
-    const size_t lds = 4 * per_wave + sizeof(float) * a->K * a->V * a->V;
-    hipLaunchKernelGGL((mix_fwd_wave_kernel<KS, CIN, XB>), dim3(grid), dim3(256), lds, s, *a);
-    F3_LAUNCH_CHECK();
-    return F3_OK;
-  }
-  // resident workgroups loop over frames; measured (serial step, 256-1024-4096 swept with
-  // F3_MIX_GRID): 1024 best for 64/128 channels, 512 for 256 (30.4 vs 32.7 us)
-  static const int env = getenv("F3_MIX_GRID") ? atoi(getenv("F3_MIX_GRID")) : 0;
-  const int cap = env > 0 ? env : (CIN >= 256 ? 512 : 1024);
-  const int grid = std::min(a->frames, cap);
-  hipLaunchKernelGGL((mix_fwd_lds_kernel<KS, CIN, XB>), dim3(grid), dim3(256), mix_lds_fwd2(*a), s, *a);
+  // a wave per frame (the workgroup-per-frame mix_fwd_lds_kernel measured slower; a bf16-MFMA form
+  // with 64-channel groups assembled in LDS measured slower too: 31 / 34 / 29 us vs 25 / 25 / 25 at
+  // the three layer shapes: the fp32 MFMA work is not what bounds these kernels)
+  const size_t per_wave = 18 * (CIN + (XB ? 8 : 4)) * (XB ? 2 : 4) + 64 * 20 * 4;
+  const int grid = std::max(1, std::min((a->frames + 3) / 4, 1024));
+  const size_t lds = 4 * per_wave + sizeof(float) * a->K * a->V * a->V;
+  hipLaunchKernelGGL((mix_fwd_wave_kernel<KS, CIN, XB>), dim3(grid), dim3(256), lds, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -2081,10 +1981,9 @@ template <int CIN>
 static size_t mix_x3_lds_bwd() { return (size_t)192 * (2 * CIN + 16); }
 template <int CIN>
 static int launch_mix_fwd_x3(const MixArgs* a, hipStream_t s) {
-  // z3 output through the frame image (F3_MIX_ZIMG=0: per-fragment stores; measured 10.39 -> 10.22
-  // ms/step, profiles/r04_zimg_segminor_ab.txt)
-  static const bool zimg_on = !getenv("F3_MIX_ZIMG") || atoi(getenv("F3_MIX_ZIMG")) != 0;
-  if (a->z3 && zimg_on) {
+  // z3 output through the frame image (per-fragment stores measured 10.39 vs 10.22 ms/step,
+  // profiles/r04_zimg_segminor_ab.txt)
+  if (a->z3) {
     const size_t lds = mix_x3_lds_fwd<CIN>() + (size_t)a->V * 4 * a->K * CIN;
     if (lds > 160 * 1024) return F3_EINVAL;
     static size_t lds0 = lds;
@@ -2169,8 +2068,7 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
     return a->Cin == 64 ? launch_mix_fwd_x3<64>(a, s) : a->Cin == 128 ? launch_mix_fwd_x3<128>(a, s)
                                                          : launch_mix_fwd_x3<256>(a, s);
   }
-  static const bool fwd_bf16 = !getenv("F3_MIX_FWD_BF16") || atoi(getenv("F3_MIX_FWD_BF16")) != 0;
-  if (fwd_bf16 && mix_lds_ok(*a) && a->x16 && a->zb && a->K * a->V <= 64 && a->V <= 32) {
+  if (mix_lds_ok(*a) && a->x16 && a->zb && a->K * a->V <= 64 && a->V <= 32) {
     if (a->frames <= 0) return F3_OK;
     return a->Cin == 64 ? launch_mix_fwd_bf16<64>(a, s) : a->Cin == 128 ? launch_mix_fwd_bf16<128>(a, s)
                                                            : launch_mix_fwd_bf16<256>(a, s);
@@ -2305,12 +2203,9 @@ int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-// rows per workgroup of the clip-chunk elementwise kernels (block_out, block_bwd_*):
-// F3_CHUNK_ROWS (default 96)
-static int chunks_for(int TV) {
-  static const int rows = getenv("F3_CHUNK_ROWS") ? std::max(16, atoi(getenv("F3_CHUNK_ROWS"))) : 96;
-  return max(1, (TV + rows - 1) / rows);
-}
+// rows per workgroup of the clip-chunk elementwise kernels (block_out, block_bwd_*): 96 (192 or 270
+// measured no faster, profiles/r03_chunk_ab.txt)
+static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
 
 // backward block kernels: instantiate on (activation type, residual kind, pooled gradient)
 template <bool A16, int RES, bool DNC>
@@ -2389,12 +2284,7 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
     if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
     else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 8>), dim3(fch, a.N), dim3(threads), 0, s, a);
   } else {
-    // F3_BNBWD_HOIST=0 (A/B): the first batch's loads after the coefficient prologue
-    static const int hoist = getenv("F3_BNBWD_HOIST") ? atoi(getenv("F3_BNBWD_HOIST")) : 1;
-    if (!hoist) {
-      if (a.act16) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4, false>), dim3(fch, a.N), dim3(threads), 0, s, a);
-      else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4, false>), dim3(fch, a.N), dim3(threads), 0, s, a);
-    } else if (a.act16) {
+    if (a.act16) {
       hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
     } else {
       hipLaunchKernelGGL((bn_bwd_apply_kernel<false, 4>), dim3(fch, a.N), dim3(threads), 0, s, a);
@@ -2437,17 +2327,8 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-// F3_DBG_NO_CA (measurement only, results are wrong): bit 0 skips the channel-attention forward
-// launches, bit 1 the backward chain (ca_bwd1/2/3) - the step time without them bounds what a
-// faster channel attention can give
-static int dbg_no_ca() {
-  static const int v = getenv("F3_DBG_NO_CA") ? atoi(getenv("F3_DBG_NO_CA")) : 0;
-  return v;
-}
-
 int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256 * kCaMaxRowsPerThread) return F3_EINVAL;
-  if (dbg_no_ca() & 1) return F3_OK;
   hipLaunchKernelGGL(ca_fwd1_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_fwd2_kernel, dim3(a->N), dim3(256), 0, s, *a);
@@ -2457,18 +2338,12 @@ int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
 
 int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
-  if (dbg_no_ca() & 2) return F3_OK;
   hipLaunchKernelGGL(ca_bwd1_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  static const int b3 = getenv("F3_CA_B3") ? atoi(getenv("F3_CA_B3")) : 0;
-  if (b3 == 1) {
-    const int thr = std::min(256, (a->C + 63) / 64 * 64);
-    hipLaunchKernelGGL(ca_bwd3_kernel<1>, dim3(a->N), dim3(thr), 0, s, *a);
-  } else {
-    hipLaunchKernelGGL(ca_bwd3_kernel<kCaB3Clips>, dim3((a->N + kCaB3Clips - 1) / kCaB3Clips), dim3(256), 0, s, *a);
-  }
+  // (one clip per workgroup measured no faster, profiles/r04_ca_b3_ab.txt)
+  hipLaunchKernelGGL(ca_bwd3_kernel<kCaB3Clips>, dim3((a->N + kCaB3Clips - 1) / kCaB3Clips), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }

@@ -863,21 +863,18 @@ int f3_mu_dwconv_fwd(const DwConvArgs* a, hipStream_t s) {
   if (!c_ok(a->C)) return F3_EINVAL;
   const long long total = (long long)a->N * a->V * (a->C / 4) * ((a->T_out + kDwChunk - 1) / kDwChunk);
   if (total >= (1LL << 31)) return F3_EINVAL;
-  // F3_DW_BLOCK: threads per workgroup (rounded down to a multiple of the quad count, so a
-  // thread's channel quad stays fixed over its grid-stride walk)
-  static const int bt = getenv("F3_DW_BLOCK") ? std::min(512, std::max(256, atoi(getenv("F3_DW_BLOCK")))) : 256;
-  const int nq = a->C / 4, block = bt / nq * nq;
+  // 256 threads per workgroup (rounded down to a multiple of the quad count, so a thread's channel
+  // quad stays fixed over its grid-stride walk)
+  const int nq = a->C / 4, block = 256 / nq * nq;
   const long long want = (total + block - 1) / block;
-  // F3_DW_GRID: the workgroup cap. Measured (C=128, V=14, T=30, B=256, k3): the BN-sum epilogue
-  // costs ~2.3 ns per wave of the grid at the launch's end (1024 x 256 threads: 28.3 vs 18.8 us
-  // without sums; 512 x 256: 24.9 vs 19.9; 512-thread blocks or one wave issuing the lane adds:
-  // the same), so 512 workgroups of 256 threads
-  // at most kLanes workgroups, each storing its BN partial row into its own lane row (plain stores;
-  // the finalize adds the rows) instead of memory-side adds: k3/s1 48.8 -> 51.3 % of HBM, k5/s2
-  // 46.4 -> 45.7 %, step unchanged (profiles/r04_musa_dwstore_ab.txt). F3_DW_STORE=0: the adds
-  static const int store = getenv("F3_DW_STORE") ? atoi(getenv("F3_DW_STORE")) : 1;
-  static const int cap = getenv("F3_DW_GRID") ? std::max(64, atoi(getenv("F3_DW_GRID"))) : 512;
-  const bool st_rows = store && a->sum;
+  // The workgroup cap. Measured (C=128, V=14, T=30, B=256, k3): the BN-sum epilogue costs ~2.3 ns per
+  // wave of the grid at the launch's end (1024 x 256 threads: 28.3 vs 18.8 us without sums; 512 x
+  // 256: 24.9 vs 19.9; 512-thread blocks or one wave issuing the lane adds: the same), so 512
+  // workgroups of 256 threads, at most kLanes of them, each storing its BN partial row into its own
+  // lane row (plain stores; the finalize adds the rows) instead of memory-side adds: k3/s1 48.8 ->
+  // 51.3 % of HBM, k5/s2 46.4 -> 45.7 %, step unchanged (profiles/r04_musa_dwstore_ab.txt)
+  constexpr int cap = 512;
+  const bool st_rows = a->sum != nullptr;
   const int grid = (int)std::min<long long>(want, st_rows ? std::min(cap, kLanes) : cap);
   DwConvArgs b = *a;
   b.grid = grid;

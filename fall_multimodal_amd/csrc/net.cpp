@@ -85,7 +85,6 @@ struct f3_net {
   hipStream_t aux[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_main[2][7] = {};  // per (skeleton stream, layer) main -> side hand-offs
-  hipEvent_t ev_early[2][7] = {}; // ... once the layer's dh / dres exist (tcn + residual wgrad)
   // end of backward phase 1 on each queue it used ([0..2] aux, [3] the caller's stream): the
   // gradient all-reduce of the phase-1 bucket waits on these instead of the caller's stream
   // joining every queue, so phase 2's critical path starts while phase 1's weight gradients drain
@@ -107,7 +106,6 @@ struct f3_net {
     for (int i = 0; i < 2; ++i)
       for (int l = 0; l < 7; ++l) {
         if (ev_main[i][l]) (void)hipEventDestroy(ev_main[i][l]);
-        if (ev_early[i][l]) (void)hipEventDestroy(ev_early[i][l]);
       }
   }
   f3_config cfg;
@@ -259,37 +257,12 @@ struct Arena {
 // slab capacity: one round of resident 128x128 weight-gradient tiles (2 per CU x 256 CUs), or 16
 // splits of the 256 x 256 x 9 tcn weight (wgrad_taps: 16 tiles x 16 splits = one workgroup per
 // CU); the launchers cap the split count to it
-long long wgrad_slab_floats() {  // F3_SLAB_X: capacity multiplier (A/B of split count vs slab traffic)
-  static const long long v = std::max(512LL * 128 * 128, 16LL * 256 * 256 * 9) *
-                             (getenv("F3_SLAB_X") ? std::max(1, atoi(getenv("F3_SLAB_X"))) : 1);
-  return v;
-}
-#define kWgradSlabFloats wgrad_slab_floats()
-// F3_WGRAD_SLAB=0: fp32 atomics into a packed accumulator instead of slab partials (A/B)
-inline bool wgrad_slab() {
-  static const bool on = !getenv("F3_WGRAD_SLAB") || atoi(getenv("F3_WGRAD_SLAB")) != 0;
-  return on;
-}
-// bf16x3 weight gradients: row segments (the three split products, WgradArgs::x3seg; default) or
-// F3_X3_FOLD=1: one GEMM on [hi | lo] x [hi | lo] whose quadrants a fold launch adds (x3fold)
-inline bool x3_fold() {
-  static const bool on = getenv("F3_X3_FOLD") && atoi(getenv("F3_X3_FOLD")) != 0;
-  return on;
-}
+// capacity of a stream's weight-gradient split-K slab (floats; the bf16x3 launches use 4x this)
+constexpr long long kWgradSlabFloats = std::max(512LL * 128 * 128, 16LL * 256 * 256 * 9);
 
 struct BnWs {
   double *fsum = nullptr, *fsq = nullptr, *bsum = nullptr, *bsq = nullptr;
 };
-
-// F3_CNN_FUSED=1: the fused CNN1D launches (6 per step, per-workgroup BN partial rows reduced by the
-// next launch; sensor.hip cnn_f*/cnn_b*). Off by default: measured SLOWER than the round-3 launches
-// at B = 256 (224 / 303 us with 128 / 256 workgroups vs 127 us; profiles/r04_cnn1d_ab.txt) - every
-// workgroup re-reads all partial rows in its prologue, and a clip per workgroup leaves each stage a
-// short dependent chain
-inline bool cnn_fused() {
-  static const bool on = getenv("F3_CNN_FUSED") && atoi(getenv("F3_CNN_FUSED")) != 0;
-  return on;
-}
 
 struct LayerWs {
   const float* x = nullptr;  // block input (previous block output or data_bn output)
@@ -301,9 +274,6 @@ struct LayerWs {
   // block output when the next block has a residual conv, the packed tcn weight gradient
   unsigned short *u = nullptr, *outb = nullptr;
   const unsigned short* xb = nullptr;  // bf16 copy of the block input (RES_CONV blocks)
-  float* dWp = nullptr;
-  float* dbx3 = nullptr;   // bf16x3: [2C] tcn bias-gradient scratch of the K-concatenated weight gradient
-  float* dbx3r = nullptr;  // bf16x3: the same for the residual conv
   // per-layer backward tensors the side stream's weight gradients read (dh: tcn output
   // gradient, dg: gcn output gradient, dres: residual-conv output gradient): never re-used
   // by another layer, so the main stream needs no wait on the side stream before the join
@@ -325,7 +295,6 @@ struct Ws {
   StreamWs st[2];
   // sensor
   float *y1, *p1, *y2, *p2, *dy1, *dp1, *dy2, *dp2;
-  float* cpart;  // fused CNN1D: per-workgroup BatchNorm partial rows (f3_cnn1d_part_floats)
   BnWs cbn1, cbn2, sbn;
   float *seq, *gates, *cell, *hmean, *ybn, *a1, *satt, *sout, *sdy, *sdpre2, *sdpre1, *dhmean;
   // head
@@ -397,9 +366,6 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.Q2 = L.res == RES_CONV ? A.take<float>((size_t)N * L.cout) : nullptr;
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
-      if (hb && !wgrad_slab()) X.dWp = A.take<float>((size_t)L.cout * 9 * L.cout);  // atomic accumulator
-      if (x3) X.dbx3 = A.take<float>((size_t)2 * L.cout);
-      if (x3 && L.res == RES_CONV) X.dbx3r = A.take<float>((size_t)2 * L.cout);
     }
   }
   if (net.has_sensor && cnn) {
@@ -485,7 +451,6 @@ Ws plan(const f3_net& net, int N, char* base) {
       w.dy1 = A.take<float>((size_t)N * Ts * 16);
       w.dp1 = A.take<float>((size_t)N * (Ts / 2) * 16);
       w.dy2 = A.take<float>((size_t)N * (Ts / 2) * 32);
-      w.cpart = A.take<float>((size_t)f3_cnn1d_part_floats());
     }
     w.seq = A.take<float>((size_t)N * Tl * 128);
     w.gates = A.take<float>((size_t)2 * N * Tl * 256);
@@ -563,31 +528,17 @@ inline const unsigned short* bf(const float* p, int on) { return on ? reinterpre
 // bf16x3 mode (F3_PRECISION_BF16X3): fp32 activations as in the fp32 mode, GEMMs on the split-bf16
 // kernels (gemm_x3.hip) with the packed weights as bf16 hi / lo planes (prep code 2)
 inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X3; }
-// bf16x3: the first block's gcn GEMMs (K Cin = 9 / 6, too narrow for the K-concatenated kernels)
-// on the fp32 kernels (exact fp32 products) instead of the register-staged split kernels
-// (F3_X3_L0_FP32=1; A/B)
-// F3_SIDE_FRAC=p (percent): the side-queue weight gradients of layers >= F3_SIDE_FRAC_FROM
-// (default 2) are split for p % of the chip's workgroup slots, so the main chains running beside
-// them keep CUs (a whole-chip wgrad_big grid holds every CU's LDS until it drains: the main
-// queues sat idle 190-335 us behind the layer-5 weight gradient, profiles/r04_x3_step_timeline.txt);
-// the last layers' (the step's tail, main chains done) keep the whole chip. Measured (bf16x3
-// step): 10.17 -> 10.07 ms at 50 or 75 (profiles/r04_ntw_ab.txt); default 75, 0 = whole chip
-inline int side_pct(bool split, int l) {
-  static const int pct = getenv("F3_SIDE_FRAC") ? atoi(getenv("F3_SIDE_FRAC")) : 75;
-  static const int from = getenv("F3_SIDE_FRAC_FROM") ? atoi(getenv("F3_SIDE_FRAC_FROM")) : 2;
-  return split && pct > 0 && l >= from ? pct : 0;
-}
-// bf16x3: the first block's gcn (Cin = 3: a 9-column GEMM) on layer0.hip's fused kernels in their
-// fp32 form (mix + GEMM + bias + BN1 sums in one pass; backward dZ, dx, dA and dW partials in one
-// pass). F3_GCN0_X3=0: the generic mix + split GEMMs + weight-gradient GEMM
-inline bool gcn0_x3() {
-  static const bool on = !getenv("F3_GCN0_X3") || atoi(getenv("F3_GCN0_X3")) != 0;
-  return on;
-}
-inline bool x3_l0_fp32() {
-  static const bool on = getenv("F3_X3_L0_FP32") && atoi(getenv("F3_X3_L0_FP32")) != 0;
-  return on;
-}
+// Side-queue weight gradients of layers >= 2 are split for 75 % of the chip's workgroup slots, so the
+// main chains running beside them keep CUs (a whole-chip wgrad_big grid holds every CU's LDS until it
+// drains: the main queues sat idle 190-335 us behind the layer-5 weight gradient,
+// profiles/r04_x3_step_timeline.txt); layers 0-1 (the step's tail, main chains done) keep the whole
+// chip. Measured (bf16x3 step): 10.17 -> 10.07 ms at 50 or 75 %, flat over 50-90 % and the first split
+// layer 0-2 (profiles/r04_ntw_ab.txt, r04_frac_ab.txt)
+inline int side_pct(bool split, int l) { return split && l >= 2 ? 75 : 0; }
+// bf16x3: the first block's gcn (Cin = 3: a 9-column GEMM, too narrow for the K-concatenated kernels)
+// runs on layer0.hip's fused kernels in their fp32 form (mix + GEMM + bias + BN1 sums in one pass;
+// backward dZ, dx, dA and dW partials in one pass): 10.14 -> 9.92 ms/step against the generic mix +
+// split GEMMs (profiles/r04_gcn0_x3_ab.txt)
 // prep code of the packed GEMM weights: 0 fp32, 1 bf16, 2 split hi / lo planes
 inline int wcode(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16 ? 1 : is_x3(n) ? 2 : 0; }
 // bf16 view of an activation slot (bf16 mode stores GEMM operand tensors as bf16)
@@ -624,7 +575,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
     // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
-    const bool l0f = wc == 2 && (x3_l0_fp32() || (gcn0_x3() && f3_gcn0_ok(K, V, Ci, C)));  // fp32 weights
+    const bool l0f = wc == 2 && f3_gcn0_ok(K, V, Ci, C);  // fp32 weights (layer0.hip)
     const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : (l0f ? 0 : wc);
     add_job(pt, PREP_PACK_GCN, C * K * Ci * (gc == 3 ? 3 : 1), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
     add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
@@ -672,7 +623,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     std::memset(&bnr, 0, sizeof(bnr));
     if (L.res == RES_CONV) bnr = q.ref(L.bnr, X.bnr, (float)Mo, eval);
     // graph mix then 1x1 conv (stgcan.py:50-56)
-    if ((hb || (x3 && gcn0_x3())) && f3_gcn0_ok(K, V, Ci, C)) {  // the 3-channel first block: one kernel (layer0.hip)
+    if ((hb || x3) && f3_gcn0_ok(K, V, Ci, C)) {  // the 3-channel first block: one kernel (layer0.hip)
       Gcn0Args g0;
       std::memset(&g0, 0, sizeof(g0));
       g0.frames = N * Ti; g0.K = K; g0.V = V; g0.Ci = Ci; g0.A = X.aeff;
@@ -693,7 +644,6 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ga.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, K * Ci, C);
       ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
       ga.w = X.gw; ga.wb = bf(X.gw, wq); ga.out = X.g; ga.outb = bfa(X.g, hb); ga.x3 = x3;
-      if (x3 && !gcat && x3_l0_fp32()) { ga.x3 = 0; ga.wb = nullptr; }  // fp32 packed weights (prep code 0)
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
       if (gcat) {  // [Z_hi | Z_lo | Z_hi] x [W_hi | W_hi | W_lo] over 3 K Ci on the bf16 kernels
         ga.x3 = 0; ga.in = nullptr; ga.inb = bfa(X.z, 1);
@@ -794,16 +744,14 @@ bool debug_stop(int si, int l) {
 
 // Backward of layers l_hi..l_lo (descending); data_bn after layer 0. Layer l writes its
 // input gradient to W.dx[(6-l)&1] and reads layer l+1's from W.dx[(5-l)&1].
-// `unpack` collects the bf16 mode's packed tcn weight-gradient -> reference-layout jobs; the
-// caller flushes it (one prep launch per stream) after the stream's last layer call.
 // Main stream s: the chain that carries the input gradient down the layers. Side stream ss
 // (== s when not parallel): the layer's weight gradients (tcn / gcn / residual wgrad, gcn
 // bias + edge importance), which nothing downstream waits for. Layer l's side work starts after
-// ev_main[si][l] (F3_SIDE_EARLY: part of it after ev_early[si][l], see below). It reads only
+// ev_main[si][l]. It reads only
 // per-layer tensors, so the only side -> main edge is the final join. (Main also waiting on the side stream per layer — double-buffered scratch —
 // made HIP's stream-capture end fault on ROCm 7.2.)
 int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, const float* skel, hipStream_t s,
-                    int l_hi, int l_lo, PrepTable& unpack, hipStream_t ss = nullptr, int call_hi = 6, int part = 3) {
+                    int l_hi, int l_lo, hipStream_t ss = nullptr, int call_hi = 6, int part = 3) {
   if (!ss) ss = s;
   (void)call_hi;
   const bool split = ss != s;
@@ -855,14 +803,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
     if (part & 1) F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
     if (part & 1) F3_TRY(f3_block_bwd_apply(ba, s));
-    // F3_SIDE_EARLY=1 starts the tcn / residual / CA weight gradients at ev_early (right after
-    // block_bwd_apply) instead of after the layer's whole main chain: measured SLOWER (5.69 vs
-    // 5.54 ms/step, profiles/r03_side_early_ab.txt) - the side work then takes CUs from the main
-    // chain, which is the step's critical path - so it is off
-    // F3_SIDE_EARLY=2: only for the last layer (0), whose weight gradients are the step's tail
-    static const int early_mode = getenv("F3_SIDE_EARLY") ? atoi(getenv("F3_SIDE_EARLY")) : 0;
-    const bool early = early_mode == 1 || (early_mode == 2 && l == 0);
-    if (early && split && (part & 1) && hipEventRecord(net.ev_early[si][l], s) != hipSuccess) return F3_EHIP;
+    // (Starting the tcn / residual / CA weight gradients right after block_bwd_apply instead of after
+    // the layer's whole main chain measured slower, 5.69 vs 5.54 ms/step, profiles/r03_side_early_ab.txt:
+    // the side work then takes CUs from the main chain, the step's critical path.)
     // tcn input gradient (transposed conv) with ReLU mask + BN1-backward sums
     ConvGemmArgs td;
     std::memset(&td, 0, sizeof(td));
@@ -886,7 +829,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     if (gcat) { bb.dgb = bfa(dg, 1); bb.x3 = 1; }
     if (part & 1) F3_TRY(f3_bn_bwd_apply(bb, s));
     // gcn: dZ = dg W^T ; dW ; mix^T ; bias/edge grads
-    const bool g0 = (hb || (x3 && gcn0_x3())) && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
+    const bool g0 = (hb || x3) && f3_gcn0_ok(K, V, Ci, C);  // the 3-channel first block (layer0.hip)
     Gcn0Args b0;
     std::memset(&b0, 0, sizeof(b0));
     int g0_parts = 0;
@@ -905,7 +848,6 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
-    if (x3 && !gcat && x3_l0_fp32()) { gd.x3 = 0; gd.wb = nullptr; }
     if (gcat) {  // [dg_hi | dg_lo | dg_hi] x [W^T_hi | W^T_hi | W^T_lo] over 3C
       gd.x3 = 0; gd.in = nullptr; gd.inb = bfa(dg, 1);
       gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 2 * C, K * Ci);
@@ -939,8 +881,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     }
     // ---- side stream: this layer's weight gradients ----
     if (split && (part & 1) && hipEventRecord(net.ev_main[si][l], s) != hipSuccess) return F3_EHIP;
-    if (split && (part & 2) && hipStreamWaitEvent(ss, early ? net.ev_early[si][l] : net.ev_main[si][l], 0) != hipSuccess)
-      return F3_EHIP;
+    if (split && (part & 2) && hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
     WgradArgs tw;
     std::memset(&tw, 0, sizeof(tw));
     tw.wg_pct = side_pct(split, l);
@@ -949,27 +890,17 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     tw.outmap = WG_OUT_CONV; tw.bf16 = hb; tw.x3 = x3;
     if (hb) {  // bf16 operands dh, u; split partials in the stream's slab, summed into the grads
       tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
-      if (wgrad_slab()) {
-        tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats; tw.dw_ref = q.g(L.tcn_w);
-      } else {  // fp32 atomics into a packed accumulator, unpacked below
-        tw.dw = X.dWp;
-        if (part & 2) add_job(unpack, PREP_UNPACK_CONV, C * C * 9, q.g(L.tcn_w), X.dWp, nullptr, nullptr, C, C, 9);
-      }
+      tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats; tw.dw_ref = q.g(L.tcn_w);
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
-    } else if (x3) {  // on the bf16 kernels over the [hi | lo] rows of dh and u: three row
-      // segments (dh_hi u_hi, dh_lo u_hi, dh_hi u_lo), or (F3_X3_FOLD=1) [dh_hi | dh_lo] x [u_hi | u_lo]
-      // whose slab reduce keeps the hi*hi + hi*lo + lo*hi quadrants (and folds the bias scratch)
+    } else if (x3) {  // on the bf16 kernels over the [hi | lo] rows of dh and u: three row segments
+      // (dh_hi u_hi, dh_lo u_hi, dh_hi u_lo). (One GEMM on [dh_hi | dh_lo] x [u_hi | u_lo] whose
+      // quadrants a fold adds computes the unused lo*lo quadrant too: 11.31 vs 10.78 ms/step.)
       tw.x3 = 0; tw.bf16 = 1;
       tw.ldy = 2 * C; tw.dyb = bfa(dh, 1); tw.inb = X.u; tw.zero = w.zero;
       tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats * 4; tw.dw_ref = q.g(L.tcn_w);
-      if (x3_fold()) {
-        tw.g = geom(Mo, 2 * C, 2 * C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, 2 * C);
-        tw.x3fold = 1; tw.db = X.dbx3; tw.db_fold = q.g(L.tcn_b);
-      } else {
-        tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
-        tw.x3seg = 1;
-      }
+      tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
+      tw.x3seg = 1;
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
     } else {
@@ -985,25 +916,19 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       rw.ldy = C; rw.dw = q.g(L.res_w); rw.db = q.g(L.res_b); rw.outmap = WG_OUT_CONV; rw.bf16 = hb; rw.x3 = x3;
       if (hb) {
         rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
-        if (wgrad_slab()) { rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w); }
-      } else if (x3) {  // row segments / quadrant fold as the tcn's
+        rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats; rw.dw_ref = q.g(L.res_w);
+      } else if (x3) {  // row segments as the tcn's
         rw.x3 = 0; rw.bf16 = 1;
         rw.ldy = 2 * C; rw.dyb = bfa(dres, 1); rw.inb = X.xb; rw.zero = w.zero;
         rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats * 4; rw.dw_ref = q.g(L.res_w);
-        if (x3_fold()) {
-          rw.g = geom(Mo, 2 * C, 2 * Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, 2 * C);
-          rw.x3fold = 1; rw.db = X.dbx3r; rw.db_fold = q.g(L.res_b);
-        } else {
-          rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
-          rw.x3seg = 1;
-        }
+        rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
+        rw.x3seg = 1;
         if (!f3_wgrad_glds_ok(rw)) return F3_EINVAL;
       } else {
         rw.dy = dres; rw.in = X.x;
       }
       if (part & 2) F3_TRY(f3_conv_wgrad(&rw, 0, ss));
     }
-    if (early && split && (part & 2) && hipStreamWaitEvent(ss, net.ev_main[si][l], 0) != hipSuccess) return F3_EHIP;
     if (split) {  // reductions whose results only feed weight gradients
       const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
       if (part & 2) F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
@@ -1025,18 +950,12 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       gw.dy = dg; gw.in = X.z;
     }
     gw.outmap = WG_OUT_GCN; gw.gcn_cin = Ci; gw.bf16 = hb; gw.x3 = x3;
-    if (x3 && !gcat && x3_l0_fp32()) gw.x3 = 0;  // conv_wgrad_f32 on the fp32 dg / Z
-    if (gcat) {  // row segments (or quadrants) into the slab, reduced into the gcn layout
+    if (gcat) {  // row segments into the slab, reduced into the gcn layout
       gw.x3 = 0; gw.bf16 = 1; gw.outmap = WG_OUT_CONV;
       gw.ldy = 2 * C; gw.dyb = bfa(dg, 1); gw.inb = bfa(X.z, 1); gw.zero = w.zero; gw.dy = nullptr; gw.in = nullptr;
       gw.slab = W.slab; gw.slab_cap = kWgradSlabFloats * 4; gw.dw_ref = q.g(L.gcn_w); gw.dw = nullptr;
-      if (x3_fold()) {
-        gw.g = geom(Mi, 2 * C, 2 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, 2 * C);
-        gw.x3fold = 1;
-      } else {
-        gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, C);
-        gw.x3seg = 1;
-      }
+      gw.g = geom(Mi, C, K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, C);
+      gw.x3seg = 1;
       if (!f3_wgrad_glds_ok(gw)) return F3_EINVAL;
     }
     if ((part & 2) && !g0) F3_TRY(f3_conv_wgrad(&gw, 0, ss));
@@ -1057,9 +976,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
   d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), 0);
   d.dout = dout; d.dgamma = q.g(S.dbn.w); d.dbeta = q.g(S.dbn.b);
-  if (part & 1) {
-    static const int db2 = getenv("F3_DATABN_BWD2") ? atoi(getenv("F3_DATABN_BWD2")) : 1;
-    const int st = db2 ? f3_databn_bwd2(&d, s) : F3_EINVAL;
+  if (part & 1) {  // the coalesced single-pass data_bn gradient where its shape fits, else the per-channel one
+    const int st = f3_databn_bwd2(&d, s);
     if (st == F3_EINVAL) F3_TRY(f3_databn_bwd(&d, s));
     else if (st != F3_OK) return st;
   }
@@ -1146,13 +1064,10 @@ void head_args(const f3_net& net, int N, const Ptrs& q, Ws& w, HeadArgs& h) {
 }
 
 // flags of the events that fork / join the branch queues. They order work between queues of ONE
-// device, so a device-scope release is all they need; hipEventRecord's default is a system-scope
-// fence (L2 writeback + invalidate at every record). F3_EV_SCOPE: 0 = HIP's default release,
-// 1 = device-scope release (default), 2 = no fence at the record.
-static unsigned branch_event_flags() {
-  static const int v = getenv("F3_EV_SCOPE") ? atoi(getenv("F3_EV_SCOPE")) : 1;
-  return hipEventDisableTiming | (v == 1 ? hipEventReleaseToDevice : v == 2 ? hipEventDisableSystemFence : 0u);
-}
+// device, so a device-scope release is all they need (hipEventRecord's default is a system-scope
+// fence: L2 writeback + invalidate at every record; 5.56-5.57 -> 5.55-5.56 ms/step,
+// profiles/r03_event_scope_ab.txt).
+static unsigned branch_event_flags() { return hipEventDisableTiming | hipEventReleaseToDevice; }
 
 // Private branch streams, created on the first eager call (never during a capture: there the
 // branches stay on the caller's stream). F3_SERIAL=1 keeps everything on one stream.
@@ -1167,22 +1082,13 @@ bool ensure_parallel(f3_net& n, hipStream_t s) {
   if (getenv("F3_SERIAL")) return n.par_ok = false;
   const unsigned evf = branch_event_flags();
   bool ok = true;
-  // F3_SIDE_PRIO=1: the two queues that carry the weight gradients (aux[1], aux[2]) get the
-  // device's least priority, so the workgroup dispatcher favours the main chains (the step's
-  // critical path) when both have work
-  static const int prio = getenv("F3_SIDE_PRIO") ? atoi(getenv("F3_SIDE_PRIO")) : 0;
-  int least = 0, greatest = 0;
-  if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-  for (int i = 0; i < 3; ++i)
-    ok = ok && (prio && i >= 1 && least != greatest  // (F3_SIDE_PRIO=2: the greatest priority instead)
-                    ? hipStreamCreateWithPriority(&n.aux[i], hipStreamNonBlocking, prio == 2 ? greatest : least)
-                    : hipStreamCreateWithFlags(&n.aux[i], hipStreamNonBlocking)) == hipSuccess;
+  // (the side queues at the lowest or highest stream priority measured within noise, r04_queue_ab.txt)
+  for (int i = 0; i < 3; ++i) ok = ok && hipStreamCreateWithFlags(&n.aux[i], hipStreamNonBlocking) == hipSuccess;
   for (auto& e : n.ev) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (auto& e : n.ev_p1) ok = ok && hipEventCreateWithFlags(&e, evf) == hipSuccess;
   for (int i = 0; i < 2; ++i)
     for (int l = 0; l < 7; ++l) {
       ok = ok && hipEventCreateWithFlags(&n.ev_main[i][l], evf) == hipSuccess;
-      ok = ok && hipEventCreateWithFlags(&n.ev_early[i][l], evf) == hipSuccess;
     }
   (void)hipGetLastError();
   return n.par_ok = ok;
@@ -1203,11 +1109,7 @@ struct Branches {
   // idle once the (short) sensor backward is done, so the two streams' weight gradients drain
   // in parallel at the end of the backward instead of one after the other on aux[2]
   hipStream_t side(int si) const {
-    return si == 1 && par && (mask & BR_SIDE) && (mask & BR_SENSOR) && side_split() ? n.aux[1] : side();
-  }
-  static bool side_split() {
-    static const bool v = getenv("F3_SIDE_SPLIT") ? atoi(getenv("F3_SIDE_SPLIT")) != 0 : true;
-    return v;
+    return si == 1 && par && (mask & BR_SIDE) && (mask & BR_SENSOR) ? n.aux[1] : side();
   }
   int fork() {
     if (!par || !mask) return F3_OK;
@@ -1384,17 +1286,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     SHeadArgs sa;
     Conv1dArgs c1, c2;
     sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
-    if (net->has_cnn && cnn_fused()) {  // conv1 | pool1 + conv2 | pool2 (sensor.hip cnn_f*_kernel)
-      for (int st = 0; st < 3; ++st) {
-        net->smark(st, ss);
-        F3_TRY(f3_cnn1d_fwd(&c1, &c2, w.cpart, st, ss));
-      }
-      net->smark(3, ss);
-      if (training) {
-        add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
-        add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
-      }
-    } else if (net->has_cnn) {
+    if (net->has_cnn) {
       net->smark(0, ss);
       F3_TRY(f3_conv1d_fwd(&c1, ss));
       F3_TRY(f3_bnrelupool_fwd(&c1, ss));
@@ -1477,11 +1369,10 @@ bool layer_ranges_ok(const f3_net& n) {
   return true;
 }
 
-// f3_net_backward_rmsprop's plan: whether the per-layer updates apply (bf16 mode with
-// F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers; a layout whose layer entries are
+// f3_net_backward_rmsprop's plan: whether the per-layer updates apply (a layout whose layer entries are
 // not contiguous cannot be updated per layer) and the leftover ranges updated after the join
 void fused_opt_plan(f3_net& n) {
-  n.fused_opt = !(n.cfg.precision == F3_PRECISION_BF16 && !wgrad_slab()) && layer_ranges_ok(n);
+  n.fused_opt = layer_ranges_ok(n);
   n.rest_ranges.clear();
   if (!n.fused_opt) return;
   std::vector<std::pair<long long, long long>> done, rest;
@@ -1518,8 +1409,8 @@ int f3_net_backward_rmsprop(f3_net* net, int N, float* params, const float* dout
                             void* workspace, float lr, float alpha, float eps, void* stream) {
   if (!net || !params || !square_avg) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  // bf16 mode with F3_WGRAD_SLAB=0 unpacks the tcn weight gradients after all layers: no per-layer
-  // update then (one launch after the backward, as f3_net_backward + f3_rmsprop_step)
+  // (a layout without contiguous per-layer ranges: one update after the backward, as f3_net_backward +
+  // f3_rmsprop_step)
   if (net->fused_opt < 0) fused_opt_plan(*net);
   if (!net->fused_opt) {
     F3_TRY(net_backward(net, N, params, dout, grads, workspace, 0, stream, nullptr));
@@ -1560,39 +1451,34 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
   if (opt) {
     q.opt_p = opt->p; q.opt_sq = opt->sq; q.lr = opt->lr; q.alpha = opt->alpha; q.eps = opt->eps;
   }
-  // skeleton streams layer by layer, interleaved (see stream_forward), then each stream's
-  // packed weight-gradient unpack
+  // skeleton streams layer by layer, interleaved (see stream_forward)
   // after_first: called once the first layer's main chains are submitted (the sensor backward, so its
   // host submission does not hold back the skeleton streams' first layer)
   auto skeleton = [&](Branches& br, int l_hi, int l_lo, const std::function<int()>& after_first) -> int {
-    PrepTable unpack[2];
-    unpack[0].n = unpack[1].n = 0;
     // Each layer's main chains are submitted before the previous layer's side-stream work (the
     // weight gradients): the host can be held up submitting to the long side queue, and the
-    // main queues should already hold their next layer by then. F3_SIDE_LAG=0: same layer.
-    static const int lag = getenv("F3_SIDE_LAG") ? atoi(getenv("F3_SIDE_LAG")) : 1;
-    const bool defer = lag && br.side() != br.s;
+    // main queues should already hold their next layer by then (neutral in time since the side
+    // split, kept: it removed 150-490 us idle stretches of the main queues before it)
+    const bool defer = br.side() != br.s;
     // Every layer's weight gradients run on the side queues. (A former F3_TAIL_SIDE=0 option ran
     // layer 0's on the stream's own queue: measured neutral to 1 % slower, and it raced with the
     // side queue's layer-1 launch on the stream's shared split-K slab, so it is gone.)
     auto side_of = [&](int si, int) { return br.side(si); };
     for (int l = l_hi; l >= l_lo; --l) {
       for (int si = 0; si < net->nstreams; ++si) {
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, unpack[si], side_of(si, l), l_hi,
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l, l, side_of(si, l), l_hi,
                                defer ? 1 : 3));
         if (debug_stop(si, l)) return F3_OK;  // leave the scratch as is for f3_net_debug_tensor
       }
       if (l == l_hi && after_first) F3_TRY(after_first());
       if (defer && l < l_hi)
         for (int si = 0; si < net->nstreams; ++si)
-          F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, unpack[si], side_of(si, l + 1),
+          F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l + 1, l + 1, side_of(si, l + 1),
                                  l_hi, 2));
     }
     if (defer)
       for (int si = 0; si < net->nstreams; ++si)
-        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l_lo, l_lo, unpack[si], side_of(si, l_lo), l_hi, 2));
-    for (int si = 0; si < net->nstreams; ++si)
-      F3_TRY(f3_prep(unpack[si], br.side(si)));  // the packed tcn weight gradients come from the side stream
+        F3_TRY(stream_backward(*net, si, N, q, w, w.skel, br.at(si), l_lo, l_lo, side_of(si, l_lo), l_hi, 2));
     return F3_OK;
   };
   if (phase == 2) {
@@ -1625,21 +1511,14 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     F3_TRY(f3_head_bwd(&h, s));
   }
   Branches br{*net, s, ensure_parallel(*net, s)};
-  static const bool no_side = getenv("F3_NO_SIDE") != nullptr;
-  br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) | (net->nstreams > 0 && !no_side ? BR_SIDE : 0);
+  br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) | (net->nstreams > 0 ? BR_SIDE : 0);
   F3_TRY(br.fork());
   auto sensor_bwd = [&]() -> int {
     if (!net->has_sensor) return F3_OK;
     const hipStream_t ss = br.at(2);
     F3_TRY(f3_shead_bwd(&sa, ss));
     F3_TRY(f3_lstm_bwd(&la, ss));
-    if (net->has_cnn && cnn_fused()) {  // pool2' | conv2' + pool1' | conv1'
-      for (int st = 0; st < 3; ++st) {
-        net->smark(4 + st, ss);
-        F3_TRY(f3_cnn1d_bwd(&c1, &c2, w.cpart, st, ss));
-      }
-      net->smark(7, ss);
-    } else if (net->has_cnn) {
+    if (net->has_cnn) {
       net->smark(4, ss);
       net->smark(5, ss);
       F3_TRY(f3_conv1d_bwd(&c2, ss));
@@ -1649,12 +1528,11 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     }
     return F3_OK;
   };
-  // the skeleton streams' first layer is submitted before the sensor backward (F3_SENSOR_FIRST=1:
-  // the round-3 order); a sensor-only model has no skeleton layer to wait for
-  static const bool sensor_first = getenv("F3_SENSOR_FIRST") && atoi(getenv("F3_SENSOR_FIRST")) != 0;
-  if (sensor_first || net->nstreams == 0) F3_TRY(sensor_bwd());
-  F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0, sensor_first || net->nstreams == 0 ? std::function<int()>()
-                                                                                              : std::function<int()>(sensor_bwd)));
+  // the skeleton streams' first layer is submitted before the sensor backward; a sensor-only model has
+  // no skeleton layer to wait for
+  if (net->nstreams == 0) F3_TRY(sensor_bwd());
+  F3_TRY(skeleton(br, 6, phase == 1 ? kSplitLayer : 0,
+                  net->nstreams == 0 ? std::function<int()>() : std::function<int()>(sensor_bwd)));
   if (phase == 1) return br.mark_phase1();  // the caller orders its all-reduce after f3_net_wait_phase1
   F3_TRY(br.join());
   return F3_OK;
@@ -1854,25 +1732,14 @@ int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, fl
   a.ldy = 2 * Cout; a.outmap = WG_OUT_CONV; a.bf16 = 1;
   a.dyb = static_cast<const unsigned short*>(dy3); a.inb = static_cast<const unsigned short*>(x3);
   a.zero = test_zero_page(); a.slab = slab; a.slab_cap = cap;
-  const bool fold = x3_fold();  // as the step (F3_X3_FOLD)
-  if (fold) {
-    a.g = geom(N * T_out * V, 2 * Cout, 2 * Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, 2 * Cout);
-    a.x3fold = 1;
-  } else {
-    a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
-    a.x3seg = 1;
-  }
+  a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
+  a.x3seg = 1;
   if (dw) {  // dw == NULL: the GEMM alone (partials left in the slab)
     if (hipMemsetAsync(dw, 0, sizeof(float) * Cout * Cin * KT, s) != hipSuccess) return F3_EHIP;
     a.dw_ref = dw;
     if (db) {
       if (hipMemsetAsync(db, 0, sizeof(float) * Cout, s) != hipSuccess) return F3_EHIP;
-      if (fold) {
-        if (hipMemsetAsync(slab + cap, 0, sizeof(float) * 2 * Cout, s) != hipSuccess) return F3_EHIP;
-        a.db = slab + cap; a.db_fold = db;
-      } else {
-        a.db = db;
-      }
+      a.db = db;
     }
   }
   if (!f3_wgrad_glds_ok(a)) return F3_EINVAL;

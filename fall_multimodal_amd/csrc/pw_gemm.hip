@@ -334,21 +334,16 @@ static int pw_wn(const ConvGeom& g, int epi, bool x3) {
   return 0;
 }
 
-// the bf16x3 mode's K-concatenated 1x1 GEMMs on this kernel too: 9.89 -> 9.84 ms/step in three of
-// three interleaved rounds (profiles/r04_pw_x3_ab.txt); F3_PW_X3=0: the tiled igemm_bf16 / igemm_big
-static bool pw_x3_on() {
-  static const bool on = !getenv("F3_PW_X3") || atoi(getenv("F3_PW_X3")) != 0;
-  return on;
-}
+// (the bf16x3 mode's K-concatenated 1x1 GEMMs run on this kernel too: 9.89 -> 9.84 ms/step in three
+// of three interleaved rounds against the tiled kernels, profiles/r04_pw_x3_ab.txt)
 
 // Shapes this kernel takes: 1x1 (KT = 1, P = 0) convs over bf16 rows with Kc in {64, 128, 192, 256}
 // and an instantiated column group; the forward at stride 1 or 2, the input gradient (transposed)
-// at stride 1 or, accumulating (EPI_ADD), stride 2. F3_PW=0 turns it off.
+// at stride 1 or, accumulating (EPI_ADD), stride 2.
 bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
-  static const int on = getenv("F3_PW") ? atoi(getenv("F3_PW")) : 1;
   const ConvGeom& g = a.g;
   const bool x3 = a.kwrap > 0;  // bf16x3: [hi | lo | hi] x [W_hi | W_hi | W_lo] over K = 3 kwrap, fp32 out
-  if (!on || !a.inb || !a.wb || !a.zero || (x3 && !pw_x3_on())) return false;
+  if (!a.inb || !a.wb || !a.zero) return false;
   if (x3 && (a.kwrap % 64 || g.Kc != 3 * a.kwrap || g.lda < 2 * a.kwrap)) return false;
   if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
   if (g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;

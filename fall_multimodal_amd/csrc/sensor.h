@@ -102,11 +102,6 @@ int f3_shead_bwd(const f3::SHeadArgs* a, hipStream_t s);
 int f3_conv1d_fwd(const f3::Conv1dArgs* a, hipStream_t s);
 int f3_bnrelupool_fwd(const f3::Conv1dArgs* a, hipStream_t s);
 int f3_conv1d_bwd(const f3::Conv1dArgs* a, hipStream_t s);
-// fused two-layer CNN1D (round 4): stage 0..2 of the forward (conv1 | pool1 + conv2 | pool2) and of
-// the backward (pool2' | conv2' + pool1' | conv1'); part: f3_cnn1d_part_floats() scratch floats
-int f3_cnn1d_fwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, float* part, int stage, hipStream_t s);
-int f3_cnn1d_bwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, float* part, int stage, hipStream_t s);
-long long f3_cnn1d_part_floats();
 int f3_head_fwd(const f3::HeadArgs* a, hipStream_t s);
 int f3_ce(const f3::HeadArgs* a, hipStream_t s);
 int f3_head_bwd(const f3::HeadArgs* a, hipStream_t s);

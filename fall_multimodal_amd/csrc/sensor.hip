@@ -208,76 +208,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
 
 // ----------------------------------------------------------------------------
 // sensor head: hmean -> BN1d(2H, batch stats) -> CA (2H->2H/8->2H) -> Linear(2H->Cs)
-// single workgroup (N <= 1024): every stage is a [N x 128] pass
 // ----------------------------------------------------------------------------
 constexpr int HC = 2 * H, HR = HC / 8;
 
-__global__ __launch_bounds__(1024) void shead_fwd_kernel(SHeadArgs a) {
-  __shared__ float sc[HC], sh[HC], w1[HR * HC], w2[HC * HR], b1[HR], b2[HC];
-  const int tid = threadIdx.x, N = a.N;
-  for (int i = tid; i < HR * HC; i += 1024) { w1[i] = a.W1[i]; w2[i] = a.W2[i]; }
-  if (tid < HR) b1[tid] = a.b1[tid];
-  if (tid < HC) b2[tid] = a.b2[tid];
-  if (tid < HC) {
-    const int c = tid;
-    float mean, rstd;
-    if (a.bn.eval) {
-      mean = a.bn.rmean[c];
-      rstd = rsqrtf(a.bn.rvar[c] + kBnEps);
-    } else {
-      double s = 0, q = 0;
-      for (int n = 0; n < N; ++n) {
-        const double v = a.hmean[(size_t)n * HC + c];
-        s += v;
-        q += v * v;
-      }
-      a.bn_sum[c] = s;
-      a.bn_sq[c] = q;
-      const double m = s / N;
-      double var = q / N - m * m;
-      if (var < 0) var = 0;
-      mean = (float)m;
-      rstd = (float)(1.0 / sqrt(var + kBnEps));
-    }
-    sc[c] = a.bn.gamma[c] * rstd;
-    sh[c] = a.bn.beta[c] - mean * sc[c];
-  }
-  __syncthreads();
-  for (int i = tid; i < N * HC; i += 1024) {
-    const int c = i % HC;
-    a.ybn[i] = a.hmean[i] * sc[c] + sh[c];
-  }
-  __syncthreads();
-  for (int i = tid; i < N * HR; i += 1024) {
-    const int n = i / HR, j = i - n * HR;
-    float q = b1[j];
-    const float* y = a.ybn + (size_t)n * HC;
-    for (int c = 0; c < HC; ++c) q += w1[j * HC + c] * y[c];
-    a.a1[i] = fmaxf(q, 0.f);
-  }
-  __syncthreads();
-  for (int i = tid; i < N * HC; i += 1024) {
-    const int n = i / HC, c = i - n * HC;
-    float q = b2[c];
-    const float* h1 = a.a1 + (size_t)n * HR;
-    for (int j = 0; j < HR; ++j) q += w2[c * HR + j] * h1[j];
-    a.att[i] = sigmoidf_(q);
-  }
-  __syncthreads();
-  for (int i = tid; i < N * a.Cs; i += 1024) {
-    const int n = i / a.Cs, k = i - n * a.Cs;
-    float q = a.b3[k];
-    const float* y = a.ybn + (size_t)n * HC;
-    const float* at = a.att + (size_t)n * HC;
-    const float* w = a.W3 + (size_t)k * HC;
-    for (int c = 0; c < HC; ++c) q += w[c] * y[c] * at[c];
-    a.out[(size_t)n * a.out_ld + k] = q;
-  }
-}
-
-// The same head as two launches: the BatchNorm1d batch statistics (one workgroup, 8 row slices
-// per channel, fp64) and one workgroup of 128 threads per clip for BN -> CA -> Linear (the single
-// workgroup above walked every [N x 128] stage alone: 127 us at N = 256).
+// Two launches: the BatchNorm1d batch statistics (one workgroup, 8 row slices per channel, fp64) and
+// one workgroup of 128 threads per clip for BN -> CA -> Linear (a single workgroup walking every
+// [N x 128] stage alone took 127 us at N = 256).
 __global__ __launch_bounds__(1024) void shead_stats_kernel(SHeadArgs a) {
   __shared__ double rs[8][HC], rq[8][HC];
   const int c = threadIdx.x % HC, part = threadIdx.x / HC;
@@ -342,104 +278,9 @@ __global__ __launch_bounds__(128) void shead_clip_kernel(SHeadArgs a) {
   }
 }
 
-__global__ __launch_bounds__(1024) void shead_bwd_kernel(SHeadArgs a) {
-  __shared__ float w1[HR * HC], w2[HC * HR];
-  __shared__ float red1[HC], red2[HC], mean_s[HC], rstd_s[HC];
-  const int tid = threadIdx.x, N = a.N, Cs = a.Cs;
-  for (int i = tid; i < HR * HC; i += 1024) { w1[i] = a.W1[i]; w2[i] = a.W2[i]; }
-  __syncthreads();
-  // out = W3 (y*att) + b3
-  for (int i = tid; i < Cs * HC; i += 1024) {
-    const int k = i / HC, c = i - k * HC;
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n)
-      acc += a.dout[(size_t)n * a.dout_ld + k] * a.ybn[(size_t)n * HC + c] * a.att[(size_t)n * HC + c];
-    a.g_W3[i] += acc;
-  }
-  for (int k = tid; k < Cs; k += 1024) {
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += a.dout[(size_t)n * a.dout_ld + k];
-    a.g_b3[k] += acc;
-  }
-  // d(y*att): dy2 ; dyn_a = dy2*att ; dpre2 = dy2*y*att*(1-att)
-  for (int i = tid; i < N * HC; i += 1024) {
-    const int n = i / HC, c = i - n * HC;
-    float d = 0.f;
-    for (int k = 0; k < Cs; ++k) d += a.dout[(size_t)n * a.dout_ld + k] * a.W3[(size_t)k * HC + c];
-    const float at = a.att[i];
-    a.dy[i] = d * at;                                   // dyn partial
-    a.dpre2[i] = d * a.ybn[i] * at * (1.f - at);
-  }
-  __syncthreads();
-  for (int i = tid; i < HC * HR; i += 1024) {          // dW2[c][j], db2 by j==0 threads
-    const int c = i / HR, j = i - c * HR;
-    float acc = 0.f, accb = 0.f;
-    for (int n = 0; n < N; ++n) {
-      const float d = a.dpre2[(size_t)n * HC + c];
-      acc += d * a.a1[(size_t)n * HR + j];
-      accb += d;
-    }
-    a.g_W2[i] += acc;
-    if (j == 0) a.g_b2[c] += accb;
-  }
-  for (int i = tid; i < N * HR; i += 1024) {           // dpre1 = (W2^T dpre2) * (a1 > 0)
-    const int n = i / HR, j = i - n * HR;
-    float acc = 0.f;
-    for (int c = 0; c < HC; ++c) acc += a.dpre2[(size_t)n * HC + c] * w2[c * HR + j];
-    a.dpre1[i] = a.a1[i] > 0.f ? acc : 0.f;
-  }
-  __syncthreads();
-  for (int i = tid; i < HR * HC; i += 1024) {          // dW1[j][c], db1
-    const int j = i / HC, c = i - j * HC;
-    float acc = 0.f, accb = 0.f;
-    for (int n = 0; n < N; ++n) {
-      const float d = a.dpre1[(size_t)n * HR + j];
-      acc += d * a.ybn[(size_t)n * HC + c];
-      accb += d;
-    }
-    a.g_W1[i] += acc;
-    if (c == 0) a.g_b1[j] += accb;
-  }
-  for (int i = tid; i < N * HC; i += 1024) {           // dyn += W1^T dpre1
-    const int n = i / HC, c = i - n * HC;
-    float acc = 0.f;
-    for (int j = 0; j < HR; ++j) acc += a.dpre1[(size_t)n * HR + j] * w1[j * HC + c];
-    a.dy[i] += acc;
-  }
-  __syncthreads();
-  // BatchNorm1d backward over the batch
-  if (tid < HC) {
-    const int c = tid;
-    const double m = a.bn_sum[c] / N;
-    double var = a.bn_sq[c] / N - m * m;
-    if (var < 0) var = 0;
-    const float rstd = (float)(1.0 / sqrt(var + kBnEps));
-    float s1 = 0.f, s2 = 0.f;
-    for (int n = 0; n < N; ++n) {
-      const float d = a.dy[(size_t)n * HC + c];
-      const float xh = (a.hmean[(size_t)n * HC + c] - (float)m) * rstd;
-      s1 += d;
-      s2 += d * xh;
-    }
-    a.g_gamma[c] += s2;
-    a.g_beta[c] += s1;
-    red1[c] = s1 / N;
-    red2[c] = s2 / N;
-    mean_s[c] = (float)m;
-    rstd_s[c] = rstd;
-  }
-  __syncthreads();
-  for (int i = tid; i < N * HC; i += 1024) {
-    const int c = i % HC;
-    const float mean = mean_s[c], rstd = rstd_s[c];
-    const float xh = (a.hmean[i] - mean) * rstd;
-    a.dhmean[i] = a.bn.gamma[c] * rstd * (a.dy[i] - red1[c] - xh * red2[c]);
-  }
-}
-
-// The same backward as four launches whose outputs are spread over the whole chip (one
-// thread per output, the batch reduction in a loop): the single-workgroup form took 640 us on
-// one CU and delayed the motion stream's weight gradients queued behind it.
+// The backward as four launches whose outputs are spread over the whole chip (one thread per
+// output, the batch reduction in a loop): a single-workgroup form took 640 us on one CU and
+// delayed the motion stream's weight gradients queued behind it.
 //
 // Batch sums use 4 independent partial sums (n = u mod 4), so the loads of 4 clips are in
 // flight together instead of one dependent add chain of N loads.
@@ -694,321 +535,6 @@ __global__ __launch_bounds__(C1D_THREADS) void conv1d_bwd_kernel(Conv1dArgs a) {
   }
 }
 
-// ----------------------------------------------------------------------------
-// Fused CNN1D (round 4): six launches instead of eight, and no same-address atomics. Each launch
-// walks the clips with a grid of <= kCnnGrid workgroups; its BatchNorm sums leave as one fp32
-// partial row per workgroup (plain stores, part[blk][2 Co]), and the NEXT launch's prologue adds the
-// rows in fp64 (every workgroup; <= kCnnGrid x 64 floats) before it needs the coefficients. Workgroup 0 of
-// that launch also stores the totals where the running-stat update / backward BnRef read them.
-//   fwd: F1 conv1 + BN1 rows | F2 BN1 + ReLU + pool1 (-> p1) + conv2 + BN2 rows | F3 BN2 + ReLU + pool2
-//   bwd: B1 pool2 / ReLU backward (-> dy2) + BN2-bwd rows | B2 BN2 apply backward, conv2 dW / db, dp1
-//        in LDS, pool1 / ReLU backward (-> dy1) + BN1-bwd rows | B3 BN1 apply backward, conv1 dW / db
-// (GSTCAN_UR_conv.ipynb:493-514: Conv1d(k5, p2) -> BatchNorm1d -> ReLU -> MaxPool1d(2), twice.)
-// ----------------------------------------------------------------------------
-constexpr int kCnnGrid = 1024;  // capacity of the partial-row buffers (workgroups per launch)
-
-// fp64 totals of a launch's partial rows: out[j] = sum_g part[g][j], j < n (every thread of the
-// workgroup takes part; result in LDS)
-F3_DEV void cnn_rows_total(const float* part, int rows, int n, double* out) {
-  const int tid = threadIdx.x;
-  if (tid < n) {
-    double s = 0.0;
-    for (int g = 0; g < rows; ++g) s += (double)part[(size_t)g * n + tid];
-    out[tid] = s;
-  }
-  __syncthreads();
-}
-
-// per-channel block sums of two register partials (channel = tid % Co) -> part row [2 Co]
-F3_DEV void cnn_rows_store(float v1, float v2, int Co, float* red, float* row) {
-  const int tid = threadIdx.x;
-  __syncthreads();
-  red[tid] = v1;
-  red[C1D_THREADS + tid] = v2;
-  __syncthreads();
-  if (tid < 2 * Co) {
-    const int c = tid % Co, h = tid / Co;
-    float s = 0.f;
-    for (int i = c; i < C1D_THREADS; i += Co) s += red[h * C1D_THREADS + i];
-    row[tid] = s;
-  }
-}
-
-// train-mode coefficients from fp64 totals (count values per channel) or eval-mode running stats
-F3_DEV void cnn_coeff(const BnRef& b, const double* tot, int Co, int c, float& sc, float& sh, float& mu, float& rs) {
-  if (b.eval) {
-    bn_coeff(b, c, sc, sh, mu, rs);
-    return;
-  }
-  const double m = tot[c] / (double)b.count;
-  double v = tot[Co + c] / (double)b.count - m * m;
-  if (v < 0) v = 0;
-  mu = (float)m;
-  rs = (float)(1.0 / sqrt(v + (double)kBnEps));
-  sc = b.gamma[c] * rs;
-  sh = b.beta[c] - mu * sc;
-}
-
-__global__ __launch_bounds__(C1D_THREADS) void cnn_f1_kernel(Conv1dArgs a, float* part) {
-  extern __shared__ float c1d_sm[];
-  float* ws = c1d_sm;                  // [Co][Ci][5]
-  float* xs = ws + a.Co * a.Ci * 5;    // [T][Ci]
-  float* red = xs + a.T * a.Ci;        // [2][256]
-  const int tid = threadIdx.x, o = tid % a.Co, TCo = a.T * a.Co, TCi = a.T * a.Ci;
-  for (int i = tid; i < a.Co * a.Ci * 5; i += C1D_THREADS) ws[i] = a.w[i];
-  float s1 = 0.f, s2 = 0.f;
-  const float bo = a.b[o];
-  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
-    __syncthreads();
-    for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
-    __syncthreads();
-    for (int i = tid; i < TCo; i += C1D_THREADS) {
-      const int t = i / a.Co;
-      float acc = bo;
-      for (int k = 0; k < 5; ++k) {
-        const int ti = t + k - 2;
-        if (ti < 0 || ti >= a.T) continue;
-        const float* xr = xs + ti * a.Ci;
-        const float* wr = ws + o * a.Ci * 5 + k;
-        for (int c = 0; c < a.Ci; ++c) acc += wr[c * 5] * xr[c];
-      }
-      a.y[(size_t)n * TCo + i] = acc;
-      s1 += acc;
-      s2 += acc * acc;
-    }
-  }
-  cnn_rows_store(s1, s2, a.Co, red, part + (size_t)blockIdx.x * 2 * a.Co);
-}
-
-// a1: conv1 (its y, BN1, pooled output p); a2: conv2 (input a2.x == a1.p)
-__global__ __launch_bounds__(C1D_THREADS) void cnn_f2_kernel(Conv1dArgs a1, Conv1dArgs a2, const float* part1,
-                                                            int rows1, float* part2) {
-  extern __shared__ float c1d_sm[];
-  __shared__ double tot[64];
-  __shared__ float sc1[32], sh1[32];
-  float* ws = c1d_sm;                     // [Co2][Ci2][5]
-  float* ys = ws + a2.Co * a2.Ci * 5;     // [T1][Co1] the clip's conv1 output
-  float* ps = ys + a1.T * a1.Co;          // [T2][Ci2] pooled (conv2 input)
-  float* red = ps + a2.T * a2.Ci;         // [2][256]
-  const int tid = threadIdx.x, Co1 = a1.Co;
-  cnn_rows_total(part1, rows1, 2 * Co1, tot);
-  if (tid < Co1) {
-    float mu, rs;
-    cnn_coeff(a1.bn, tot, Co1, tid, sc1[tid], sh1[tid], mu, rs);
-  }
-  if (blockIdx.x == 0 && !a1.bn.eval && tid < 2 * Co1) (tid < Co1 ? a1.st_sum[tid] : a1.st_sq[tid - Co1]) = tot[tid];
-  for (int i = tid; i < a2.Co * a2.Ci * 5; i += C1D_THREADS) ws[i] = a2.w[i];
-  const int o = tid % a2.Co, TCo2 = a2.T * a2.Co, TC1 = a1.T * Co1, TP = a2.T * Co1;
-  float s1 = 0.f, s2 = 0.f;
-  const float bo = a2.b[o];
-  for (int n = blockIdx.x; n < a2.N; n += gridDim.x) {
-    __syncthreads();
-    for (int i = tid; i < TC1; i += C1D_THREADS) ys[i] = a1.y[(size_t)n * TC1 + i];
-    __syncthreads();
-    for (int i = tid; i < TP; i += C1D_THREADS) {  // MaxPool1d(2) of ReLU(BN1), T1 / 2 frames
-      const int tp = i / Co1, c = i - tp * Co1;
-      const float v = fmaxf(fmaxf(ys[(2 * tp) * Co1 + c] * sc1[c] + sh1[c], 0.f),
-                            fmaxf(ys[(2 * tp + 1) * Co1 + c] * sc1[c] + sh1[c], 0.f));
-      ps[i] = v;
-      a1.p[(size_t)n * TP + i] = v;
-    }
-    __syncthreads();
-    for (int i = tid; i < TCo2; i += C1D_THREADS) {
-      const int t = i / a2.Co;
-      float acc = bo;
-      for (int k = 0; k < 5; ++k) {
-        const int ti = t + k - 2;
-        if (ti < 0 || ti >= a2.T) continue;
-        const float* xr = ps + ti * a2.Ci;
-        const float* wr = ws + o * a2.Ci * 5 + k;
-        for (int c = 0; c < a2.Ci; ++c) acc += wr[c * 5] * xr[c];
-      }
-      a2.y[(size_t)n * TCo2 + i] = acc;
-      s1 += acc;
-      s2 += acc * acc;
-    }
-  }
-  cnn_rows_store(s1, s2, a2.Co, red, part2 + (size_t)blockIdx.x * 2 * a2.Co);
-}
-
-// BN2 + ReLU + MaxPool1d(2) -> p (the LSTM input)
-__global__ __launch_bounds__(C1D_THREADS) void cnn_f3_kernel(Conv1dArgs a, const float* part, int rows) {
-  __shared__ double tot[64];
-  __shared__ float sc[32], sh[32];
-  const int tid = threadIdx.x;
-  cnn_rows_total(part, rows, 2 * a.Co, tot);
-  if (tid < a.Co) {
-    float mu, rs;
-    cnn_coeff(a.bn, tot, a.Co, tid, sc[tid], sh[tid], mu, rs);
-  }
-  if (blockIdx.x == 0 && !a.bn.eval && tid < 2 * a.Co) (tid < a.Co ? a.st_sum[tid] : a.st_sq[tid - a.Co]) = tot[tid];
-  __syncthreads();
-  const int Tp = a.T / 2, tot_n = a.N * Tp * a.Co;
-  for (int i = blockIdx.x * C1D_THREADS + tid; i < tot_n; i += gridDim.x * C1D_THREADS) {
-    const int o = i % a.Co, r = i / a.Co, n = r / Tp, tp = r - n * Tp;
-    const float* y = a.y + ((size_t)n * a.T + 2 * tp) * a.Co + o;
-    a.p[i] = fmaxf(fmaxf(y[0] * sc[o] + sh[o], 0.f), fmaxf(y[a.Co] * sc[o] + sh[o], 0.f));
-  }
-}
-
-// gradient through MaxPool1d(2) + ReLU of one clip's channel-o rows; returns d for frame t
-F3_DEV float cnn_pool_bwd(const float* yc, int Co, int t, int o, float sc, float sh, int Tp, const float* dpc) {
-  const int tp = t >> 1;
-  if (tp >= Tp) return 0.f;
-  const float v0 = fmaxf(yc[(2 * tp) * Co + o] * sc + sh, 0.f);
-  const float v1 = fmaxf(yc[(2 * tp + 1) * Co + o] * sc + sh, 0.f);
-  const int win = (v1 > v0) ? 1 : 0;  // first max wins ties (max_pool1d)
-  const float me = fmaxf(yc[t * Co + o] * sc + sh, 0.f);
-  return ((t & 1) == win && me > 0.f) ? dpc[tp * Co + o] : 0.f;
-}
-
-// B1: dy2 and the BN2-backward partial rows (sum dy, sum dy * xhat)
-__global__ __launch_bounds__(C1D_THREADS) void cnn_b1_kernel(Conv1dArgs a, float* part) {
-  __shared__ float red[2 * C1D_THREADS];
-  const int tid = threadIdx.x, o = tid % a.Co, Tp = a.T / 2, TCo = a.T * a.Co;
-  float sc, sh, mu, rs;
-  bn_coeff(a.bn, o, sc, sh, mu, rs);
-  float s1 = 0.f, s2 = 0.f;
-  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
-    const float* yc = a.y + (size_t)n * TCo;
-    const float* dpc = a.dp + (size_t)n * Tp * a.Co;
-    for (int i = tid; i < TCo; i += C1D_THREADS) {
-      const int t = i / a.Co;
-      const float d = cnn_pool_bwd(yc, a.Co, t, o, sc, sh, Tp, dpc);
-      a.dy[(size_t)n * TCo + i] = d;
-      s1 += d;
-      s2 += d * ((yc[i] - mu) * rs);
-    }
-  }
-  cnn_rows_store(s1, s2, a.Co, red, part + (size_t)blockIdx.x * 2 * a.Co);
-}
-
-// B2: BN2 apply backward, conv2 dW / db (register partials), dp1 = conv2^T(dc2) in LDS, then the
-// pool1 / ReLU backward of conv1's output (dy1) and the BN1-backward partial rows
-__global__ __launch_bounds__(C1D_THREADS) void cnn_b2_kernel(Conv1dArgs a1, Conv1dArgs a2, const float* part2,
-                                                            int rows2, float* part1) {
-  extern __shared__ float c1d_sm[];
-  __shared__ double tot[64];
-  float* dcs = c1d_sm;                    // [T2][Co2]
-  float* xs = dcs + a2.T * a2.Co;         // [T2][Ci2] conv2 input (p1)
-  float* ws = xs + a2.T * a2.Ci;          // [Co2][Ci2][5]
-  float* dps = ws + a2.Co * a2.Ci * 5;    // [T2][Ci2] dp1
-  float* red = dps + a2.T * a2.Ci;        // [2][256]
-  const int tid = threadIdx.x, Co2 = a2.Co, Ci2 = a2.Ci, T2 = a2.T, NW = Co2 * Ci2 * 5;
-  const float M2 = a2.bn.count;
-  cnn_rows_total(part2, rows2, 2 * Co2, tot);
-  if (blockIdx.x == 0 && tid < Co2) {
-    a2.g_gamma[tid] += (float)tot[Co2 + tid];
-    a2.g_beta[tid] += (float)tot[tid];
-  }
-  for (int i = tid; i < NW; i += C1D_THREADS) ws[i] = a2.w[i];
-  float gw[C1D_WMAX], gb = 0.f;
-#pragma unroll
-  for (int e = 0; e < C1D_WMAX; ++e) gw[e] = 0.f;
-  // conv1's BN1 coefficients for the pool1 backward (channel of this thread: tid % Co1)
-  const int Co1 = a1.Co, o1 = tid % Co1, Tp1 = a1.T / 2, TC1 = a1.T * Co1;
-  float sc1, sh1, mu1, rs1;
-  bn_coeff(a1.bn, o1, sc1, sh1, mu1, rs1);
-  float q1 = 0.f, q2 = 0.f;
-  for (int n = blockIdx.x; n < a2.N; n += gridDim.x) {
-    __syncthreads();
-    for (int i = tid; i < T2 * Co2; i += C1D_THREADS) {
-      const int o = i % Co2;
-      float sc, sh, mu, rs;
-      bn_coeff(a2.bn, o, sc, sh, mu, rs);
-      const float xh = (a2.y[(size_t)n * T2 * Co2 + i] - mu) * rs;
-      const float d = a2.dy[(size_t)n * T2 * Co2 + i];
-      dcs[i] = a2.bn.gamma[o] * rs * (d - (float)tot[o] / M2 - xh * (float)tot[Co2 + o] / M2);
-    }
-    for (int i = tid; i < T2 * Ci2; i += C1D_THREADS) xs[i] = a2.x[(size_t)n * T2 * Ci2 + i];
-    __syncthreads();
-    if (tid < Co2)
-      for (int t = 0; t < T2; ++t) gb += dcs[t * Co2 + tid];
-#pragma unroll
-    for (int e = 0; e < C1D_WMAX; ++e) {
-      const int i = tid + e * C1D_THREADS;
-      if (i >= NW) break;
-      const int o = i / (Ci2 * 5), r = i - o * Ci2 * 5, c = r / 5, k = r - c * 5;
-      float acc = 0.f;
-      for (int t = max(0, 2 - k); t < min(T2, T2 + 2 - k); ++t) acc += dcs[t * Co2 + o] * xs[(t + k - 2) * Ci2 + c];
-      gw[e] += acc;
-    }
-    for (int i = tid; i < T2 * Ci2; i += C1D_THREADS) {
-      const int ti = i / Ci2, c = i - ti * Ci2;
-      float acc = 0.f;
-      for (int k = 0; k < 5; ++k) {
-        const int t = ti - k + 2;
-        if (t < 0 || t >= T2) continue;
-        for (int o = 0; o < Co2; ++o) acc += dcs[t * Co2 + o] * ws[(o * Ci2 + c) * 5 + k];
-      }
-      dps[i] = acc;
-    }
-    __syncthreads();
-    const float* yc = a1.y + (size_t)n * TC1;
-    for (int i = tid; i < TC1; i += C1D_THREADS) {  // channel of i is o1 (256 % Co1 == 0)
-      const int t = i / Co1;
-      const float d = cnn_pool_bwd(yc, Co1, t, o1, sc1, sh1, Tp1, dps);
-      a1.dy[(size_t)n * TC1 + i] = d;
-      q1 += d;
-      q2 += d * ((yc[i] - mu1) * rs1);
-    }
-  }
-  if (tid < Co2) atomic_add_f(a2.g_b + tid, gb);
-#pragma unroll
-  for (int e = 0; e < C1D_WMAX; ++e) {
-    const int i = tid + e * C1D_THREADS;
-    if (i < NW) atomic_add_f(a2.g_w + i, gw[e]);
-  }
-  cnn_rows_store(q1, q2, Co1, red, part1 + (size_t)blockIdx.x * 2 * Co1);
-}
-
-// B3: BN1 apply backward and the conv1 weight / bias gradients (no input gradient: the sensor data)
-__global__ __launch_bounds__(C1D_THREADS) void cnn_b3_kernel(Conv1dArgs a, const float* part, int rows) {
-  extern __shared__ float c1d_sm[];
-  __shared__ double tot[64];
-  float* dcs = c1d_sm;                 // [T][Co]
-  float* xs = dcs + a.T * a.Co;        // [T][Ci]
-  const int tid = threadIdx.x, TCo = a.T * a.Co, TCi = a.T * a.Ci, NW = a.Co * a.Ci * 5;
-  const float M = a.bn.count;
-  cnn_rows_total(part, rows, 2 * a.Co, tot);
-  if (blockIdx.x == 0 && tid < a.Co) {
-    a.g_gamma[tid] += (float)tot[a.Co + tid];
-    a.g_beta[tid] += (float)tot[tid];
-  }
-  float gw[C1D_WMAX], gb = 0.f;
-#pragma unroll
-  for (int e = 0; e < C1D_WMAX; ++e) gw[e] = 0.f;
-  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
-    __syncthreads();
-    for (int i = tid; i < TCo; i += C1D_THREADS) {
-      const int o = i % a.Co;
-      float sc, sh, mu, rs;
-      bn_coeff(a.bn, o, sc, sh, mu, rs);
-      const float xh = (a.y[(size_t)n * TCo + i] - mu) * rs;
-      const float d = a.dy[(size_t)n * TCo + i];
-      dcs[i] = a.bn.gamma[o] * rs * (d - (float)tot[o] / M - xh * (float)tot[a.Co + o] / M);
-    }
-    for (int i = tid; i < TCi; i += C1D_THREADS) xs[i] = a.x[(size_t)n * TCi + i];
-    __syncthreads();
-    if (tid < a.Co)
-      for (int t = 0; t < a.T; ++t) gb += dcs[t * a.Co + tid];
-#pragma unroll
-    for (int e = 0; e < C1D_WMAX; ++e) {
-      const int i = tid + e * C1D_THREADS;
-      if (i >= NW) break;
-      const int o = i / (a.Ci * 5), r = i - o * a.Ci * 5, c = r / 5, k = r - c * 5;
-      float acc = 0.f;
-      for (int t = max(0, 2 - k); t < min(a.T, a.T + 2 - k); ++t) acc += dcs[t * a.Co + o] * xs[(t + k - 2) * a.Ci + c];
-      gw[e] += acc;
-    }
-  }
-  if (tid < a.Co) atomic_add_f(a.g_b + tid, gb);
-#pragma unroll
-  for (int e = 0; e < C1D_WMAX; ++e) {
-    const int i = tid + e * C1D_THREADS;
-    if (i < NW) atomic_add_f(a.g_w + i, gw[e]);
-  }
-}
 
 }  // namespace f3
 
@@ -1021,16 +547,8 @@ static size_t lstm_bwd_lds(const LstmArgs& a) {
   return ((size_t)G4 * (H + 1) + G4 * a.S + LSTM_NB * a.T * a.S + LSTM_NB * H + LSTM_NB * G4 + LSTM_NB * H) * 4;
 }
 
-// F3_DBG_NO_LSTM=1 (timing experiments only; results are wrong): skip both LSTM launches, to
-// measure what the recurrences' CU and LDS occupancy costs the concurrent skeleton streams
-static bool dbg_no_lstm() {
-  static const bool v = getenv("F3_DBG_NO_LSTM") && atoi(getenv("F3_DBG_NO_LSTM")) != 0;
-  return v;
-}
-
 int f3_lstm_fwd(const LstmArgs* a, hipStream_t s) {
   if (a->S > 32 || a->S < 1) return F3_EINVAL;
-  if (dbg_no_lstm()) return F3_OK;
   dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
   hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), lstm_fwd_lds(*a), s, *a);
   F3_LAUNCH_CHECK();
@@ -1039,7 +557,6 @@ int f3_lstm_fwd(const LstmArgs* a, hipStream_t s) {
 
 int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
   if (a->S > 32 || a->S < 1) return F3_EINVAL;
-  if (dbg_no_lstm()) return F3_OK;
   dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
   const size_t lds = lstm_bwd_lds(*a);
   if (lds > 160 * 1024) return F3_EINVAL;
@@ -1052,12 +569,6 @@ int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
 }
 
 int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
-  static const bool one_wg = getenv("F3_SHEAD_1WG") != nullptr;  // the single-workgroup form (A/B)
-  if (one_wg) {
-    hipLaunchKernelGGL(shead_fwd_kernel, dim3(1), dim3(1024), 0, s, *a);
-    F3_LAUNCH_CHECK();
-    return F3_OK;
-  }
   if (!a->bn.eval) {
     hipLaunchKernelGGL(shead_stats_kernel, dim3(1), dim3(1024), 0, s, *a);
     F3_LAUNCH_CHECK();
@@ -1068,12 +579,6 @@ int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
 }
 
 int f3_shead_bwd(const SHeadArgs* a, hipStream_t s) {
-  static const bool one_wg = getenv("F3_SHEAD_1WG") != nullptr;  // the single-workgroup form (A/B)
-  if (one_wg) {
-    hipLaunchKernelGGL(shead_bwd_kernel, dim3(1), dim3(1024), 0, s, *a);
-    F3_LAUNCH_CHECK();
-    return F3_OK;
-  }
   const int N = a->N, Cs = a->Cs;
   auto blocks = [](int n) { return dim3((n + 255) / 256); };
   hipLaunchKernelGGL(shead_bwd_p1, blocks(Cs * HC + Cs + N * HC), dim3(256), 0, s, *a);
@@ -1119,57 +624,3 @@ int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-// ---- fused CNN1D entry points (six launches per step; see cnn_f1_kernel) ----
-// workgroups per fused launch: one per clip up to F3_CNN_GRID (default 1024; round 4's first
-// version used 128, i.e. two clips per workgroup at B = 256 on half the CUs)
-static int cnn_grid(int N) {
-  static const int cap = getenv("F3_CNN_GRID") ? std::max(1, std::min(kCnnGrid, atoi(getenv("F3_CNN_GRID")))) : kCnnGrid;
-  return std::max(1, std::min(N, cap));
-}
-
-long long f3_cnn1d_part_floats() { return 4LL * kCnnGrid * 64; }
-
-static bool cnn_ok(const Conv1dArgs& c1, const Conv1dArgs& c2) {
-  return c1d_ok(c1) && c1d_ok(c2) && c2.Ci == c1.Co && c2.T == c1.T / 2 && 2 * c1.Co <= 64 && 2 * c2.Co <= 64 &&
-         c1.N == c2.N && c1.Co <= 32 && c2.Co <= 32;
-}
-
-int f3_cnn1d_fwd(const Conv1dArgs* c1, const Conv1dArgs* c2, float* part, int stage, hipStream_t s) {
-  if (!cnn_ok(*c1, *c2) || !part) return F3_EINVAL;
-  const int G = cnn_grid(c1->N);
-  float* p1 = part;                 // BN1 rows [G][2 Co1]
-  float* p2 = part + kCnnGrid * 64; // BN2 rows [G][2 Co2]
-  if (stage == 0) {
-    const size_t lds = ((size_t)c1->Co * c1->Ci * 5 + (size_t)c1->T * c1->Ci + 2 * C1D_THREADS) * 4;
-    hipLaunchKernelGGL(cnn_f1_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, p1);
-  } else if (stage == 1) {
-    const size_t lds = ((size_t)c2->Co * c2->Ci * 5 + (size_t)c1->T * c1->Co + (size_t)c2->T * c2->Ci +
-                        2 * C1D_THREADS) * 4;
-    hipLaunchKernelGGL(cnn_f2_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, *c2, (const float*)p1, G, p2);
-  } else {
-    const int tot = c2->N * (c2->T / 2) * c2->Co;
-    const int g3 = std::max(1, std::min((tot + C1D_THREADS - 1) / C1D_THREADS, 64));
-    hipLaunchKernelGGL(cnn_f3_kernel, dim3(g3), dim3(C1D_THREADS), 0, s, *c2, (const float*)p2, G);
-  }
-  F3_LAUNCH_CHECK();
-  return F3_OK;
-}
-
-int f3_cnn1d_bwd(const Conv1dArgs* c1, const Conv1dArgs* c2, float* part, int stage, hipStream_t s) {
-  if (!cnn_ok(*c1, *c2) || !part) return F3_EINVAL;
-  const int G = cnn_grid(c1->N);
-  float* q2 = part + 2 * kCnnGrid * 64;  // BN2-backward rows
-  float* q1 = part + 3 * kCnnGrid * 64;  // BN1-backward rows
-  if (stage == 0) {
-    hipLaunchKernelGGL(cnn_b1_kernel, dim3(G), dim3(C1D_THREADS), 0, s, *c2, q2);
-  } else if (stage == 1) {
-    const size_t lds = ((size_t)c2->T * c2->Co + 2 * (size_t)c2->T * c2->Ci + (size_t)c2->Co * c2->Ci * 5 +
-                        2 * C1D_THREADS) * 4;
-    hipLaunchKernelGGL(cnn_b2_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, *c2, (const float*)q2, G, q1);
-  } else {
-    const size_t lds = ((size_t)c1->T * (c1->Co + c1->Ci)) * 4;
-    hipLaunchKernelGGL(cnn_b3_kernel, dim3(G), dim3(C1D_THREADS), lds, s, *c1, (const float*)q1, G);
-  }
-  F3_LAUNCH_CHECK();
-  return F3_OK;
-}

@@ -100,7 +100,7 @@ struct TaArgs {
   const float* dout;     // [B][T][V][C]
   float* din;            // [B][T][V][C]
   float* grads;          // flat grads (same offsets as p), accumulated
-  int dbg;               // measurement knob (F3_TA_DBG): 1 = skip the backward's weight-gradient flush
+  int dbg;               // (unused: kept for the argument layout)
   // backward weight gradients: each workgroup adds its waves' sums through LDS and stores them to
   // part[blockIdx][TA_PART] (plain stores); ta_part_reduce then adds the workgroups' rows into grads.
   // (Every wave's atomics into the same 64x64 matrices serialised at the end of the kernel.)

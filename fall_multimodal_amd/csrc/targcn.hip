@@ -2665,7 +2665,6 @@ __global__ __launch_bounds__(64 * TAB_WAVES) void ta_bwd_mfma_kernel(TaArgs a) {
     tam_wsync();
   }
   // ---------------- flush this wave's weight gradients ----------------
-  if (a.dbg & 1) return;  // measurement only (F3_TA_DBG=1): results are wrong
   if (a.part) {  // workgroup sums through LDS -> this workgroup's row of the partial slab
     float* red = reinterpret_cast<float*>(tab_smem);  // [4 waves][4096] (the sequence slots are done)
     float* row = a.part + (size_t)blockIdx.x * TA_PART;
@@ -2870,11 +2869,10 @@ static int gru_bwd_launch(const GruBwdArgs& a, hipStream_t s) {
 
 // node-partitioned forward (see gru_fwd_node_kernel): bf16 mode, exchange buffers present, a
 // cooperative launch of V x ceil(B / GN_BT) workgroups. Returns false (caller falls back to the
-// clip-tile kernel) when off (F3_GRU_NODE=0) or when the cooperative launch is refused.
+// clip-tile kernel) when the cooperative launch is refused.
 static bool gru_fwd_node(const GruFwdArgs& a, hipStream_t s) {
-  static const int on = getenv("F3_GRU_NODE") ? atoi(getenv("F3_GRU_NODE")) : 3;
   const int NG = (a.B + GN_BT - 1) / GN_BT;
-  if (!(on & 1) || !a.hx || !a.rhx || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
+  if (!a.hx || !a.rhx || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -2899,9 +2897,8 @@ int f3_tg_gru_fwd(const GruFwdArgs* a, int b16, hipStream_t s) {
 }
 
 static bool gru_bwd_node(const GruBwdArgs& a, hipStream_t s) {
-  static const int on = getenv("F3_GRU_NODE") ? atoi(getenv("F3_GRU_NODE")) : 3;
   const int NG = (a.B + GN_BT - 1) / GN_BT;
-  if (!(on & 2) || !a.gx1 || !a.gx2 || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
+  if (!a.gx1 || !a.gx2 || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -3011,9 +3008,7 @@ static int ta_grid(const TaArgs& a) {
 }
 
 int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
-  // F3_TA_MFMA (bf16 mode): bit 0 the MFMA forward, bit 1 the MFMA backward (default both)
-  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
-  if (a->b16 && (mfma_env & 1)) {  // bf16 mode: one wave per sequence on bf16 MFMA
+  if (a->b16) {  // bf16 mode: one wave per sequence on bf16 MFMA
     static bool once_m = (allow_lds(ta_fwd_mfma_kernel, TAM_LDS), true);
     (void)once_m;
     const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAM_WAVES - 1) / TAM_WAVES));
@@ -3029,12 +3024,8 @@ int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
 }
 
 int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
-  static const int mfma_env = getenv("F3_TA_MFMA") ? atoi(getenv("F3_TA_MFMA")) : 3;
-  static const int dbg_env = getenv("F3_TA_DBG") ? atoi(getenv("F3_TA_DBG")) : 0;
-  TaArgs ad = *a_;
-  ad.dbg = dbg_env;
-  const TaArgs* a = &ad;
-  if (a->b16 && (mfma_env & 2)) {  // bf16 mode: one wave per sequence on bf16 MFMA
+  const TaArgs* a = a_;
+  if (a->b16) {  // bf16 mode: one wave per sequence on bf16 MFMA
     static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, std::max(TAB_LDS1, TAB_RED_LDS)),
                           allow_lds(ta_bwd_mfma_kernel<2>, std::max(TAB_LDS2, TAB_RED_LDS)), true);
     (void)once_m;
@@ -3044,7 +3035,7 @@ int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
     const int lds2 = a->part ? std::max(TAB_LDS2, TAB_RED_LDS) : TAB_LDS2;
     hipLaunchKernelGGL(ta_bwd_mfma_kernel<1>, dim3(grid), dim3(64 * TAB_WAVES), lds1, s, *a);
     F3_LAUNCH_CHECK();
-    if (a->part && !(a->dbg & 1)) {
+    if (a->part) {
       TaSegs sg;
       std::memset(&sg, 0, sizeof(sg));
       const long long g1[8] = {a->off_f2w, a->off_f0w, a->off_lnffw, a->off_lnffb, a->off_f2b, a->off_f0b, a->off_lnw,
@@ -3058,7 +3049,7 @@ int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
     }
     hipLaunchKernelGGL(ta_bwd_mfma_kernel<2>, dim3(grid), dim3(64 * TAB_WAVES), lds2, s, *a);
     F3_LAUNCH_CHECK();
-    if (a->part && !(a->dbg & 1)) {
+    if (a->part) {
       TaSegs sg;
       std::memset(&sg, 0, sizeof(sg));
       const long long g2[6] = {a->off_vw, a->off_c1w, a->off_c2w, a->off_vb, a->off_c1b, a->off_c2b};

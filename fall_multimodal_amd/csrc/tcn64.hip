@@ -231,11 +231,10 @@ using namespace f3;
 
 // Shapes this kernel takes: 64 -> 64 channels, 9 taps, stride 1, "same" padding, T_in == T_out,
 // bf16 in / out, a clip at least one tile long (a tile spans at most two clips), and the two
-// epilogues of the bf16 step (tcn forward, tcn input gradient). F3_TCN64=0 turns it off.
+// epilogues of the bf16 step (tcn forward, tcn input gradient).
 bool f3_tcn64_ok(const ConvGemmArgs& a, int epi) {
-  static const int on = getenv("F3_TCN64") ? atoi(getenv("F3_TCN64")) : 1;
   const ConvGeom& g = a.g;
-  if (!on || !a.inb || !a.wb || !a.zero || !a.outb || a.kwrap) return false;
+  if (!a.inb || !a.wb || !a.zero || !a.outb || a.kwrap) return false;
   if (g.Kc != 64 || g.Nc != 64 || g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out) return false;
   if (g.V > 18 || g.lda % 8 != 0 || g.ldo % 8 != 0 || g.T_out * g.V < T64_BM || g.M % (g.T_out * g.V) != 0) return false;
   if (epi == (EPI_BIAS | EPI_STATS | EPI_GAP)) return a.gap && a.st_sum && a.st_sq && a.bias;
@@ -252,10 +251,8 @@ int f3_tcn64(const ConvGemmArgs* args, int epi, hipStream_t s) {
     (void)hipGetLastError();
     return n;
   }();
-  // tiles per workgroup: one round over the CUs by default; F3_TCN64_TPW=n for n tiles each (more,
-  // shorter workgroups fill in around the other queues' kernels in the concurrent step)
-  static const int tpw = getenv("F3_TCN64_TPW") ? atoi(getenv("F3_TCN64_TPW")) : 0;
-  const int per_wg = tpw > 0 ? tpw : (ntiles + cus - 1) / cus;
+  // tiles per workgroup: one round over the CUs
+  const int per_wg = (ntiles + cus - 1) / cus;
   const int grid = (ntiles + per_wg - 1) / per_wg;
   if (epi == (EPI_BIAS | EPI_STATS | EPI_GAP)) {
     static bool once = (hipFuncSetAttribute((const void*)tcn64_kernel<EPI_BIAS | EPI_STATS | EPI_GAP>,

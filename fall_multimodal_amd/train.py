@@ -36,7 +36,11 @@ class GradSync:
         self.grads, self.split, self.group = grads, int(split), group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.wait_phase1 = wait_phase1
-        self._side = torch.cuda.Stream(device=grads.device) if (self.world > 1 and grads.is_cuda) else None
+        # high priority: ROCm draws high-priority streams from their own hardware-queue pool, so the head
+        # bucket's wait + all-reduce never queue behind main-chain kernels on a shared normal-priority
+        # queue (the step's four native queues already fill GPU_MAX_HW_QUEUES = 4)
+        self._side = (torch.cuda.Stream(device=grads.device, priority=-1) if (self.world > 1 and grads.is_cuda)
+                      else None)
         self._work = []
 
     def _reduce(self, t):
@@ -73,6 +77,14 @@ class GradSync:
         self.start_head()
         self.start_tail()
         self.finish()
+
+
+def rccl_options():
+    """ProcessGroupNCCL options for the gradient all-reduce: RCCL's internal stream high priority, for
+    the same reason as GradSync's side stream (pass as init_process_group("nccl", pg_options=...))."""
+    o = dist.ProcessGroupNCCL.Options()
+    o.is_high_priority_stream = True
+    return o
 
 
 class TrainStep:

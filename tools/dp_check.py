@@ -37,7 +37,11 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    dist.init_process_group(a.backend)
+    if a.backend == "nccl":
+        from fall_multimodal_amd.train import rccl_options
+        dist.init_process_group(a.backend, pg_options=rccl_options())
+    else:
+        dist.init_process_group(a.backend)
     dev = torch.device("cuda", local)
     import fall_multimodal_amd as f3
     from oracle.prng import synthetic_batch

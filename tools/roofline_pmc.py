@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
-_RED = "wgrad_slab_reduce_x3_kernel" if os.environ.get("F3_X3_FOLD", "0") != "0" else "wgrad_slab_reduce_kernel"
+_RED = "wgrad_slab_reduce_kernel"
 KERNELS = {"wgrad_l5": ["wgrad_big<4, 2, 4, 4, ", _RED],
            "wgrad": ["wgrad_taps<5>", "wgrad_taps_reduce_kernel"],
            "wgrad_kernel": ["wgrad_taps<5>"],
