@@ -50,7 +50,9 @@ struct BigCfg {
   static constexpr int SMEM = ZOFF + (WIN ? 128 : 0);
 };
 
-template <int EPI, int WM, int WN, bool WIN = false>
+// X3N: the bf16x3 native form (ConvGemmArgs::x3n): a k step is one 32-channel block, its staged row
+// piece [x_hi 32 | x_lo 32] / [W_hi 32 | W_lo 32], and the wave issues x_hi W_hi + x_lo W_hi + x_hi W_lo
+template <int EPI, int WM, int WN, bool WIN = false, bool X3N = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
   static_assert(!(WIN && (WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips");
@@ -90,17 +92,21 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     return (n * g.T_out + 2 * tt + p) * g.V + v;
   };
   const int m0 = tile * BM;
-  const int Ktot = g.KT * g.Kc;
-  const int kpt = g.Kc / G_BK;
+  constexpr int CB = X3N ? 32 : G_BK;                 // channels per k step
+  const int Ktot = g.KT * g.Kc * (X3N ? 2 : 1);       // packed weight row length
+  const int kpt = g.Kc / CB;
   const int dt0 = par ? ((p + g.P) & 1) : 0;
-  const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
   const int ntap = par ? (g.KT - dt0 + 1) / 2 : g.KT;
+  const int nchunk = ntap * kpt;
   // k step t -> (tap, channel chunk), tap-major (chunk-major order, all taps of a chunk back to back,
   // measured within 1 %: DESIGN.md §4.11)
   auto tapchunk = [&](int t, int& tap, int& i0) {
     tap = t / kpt;
-    i0 = (t - tap * kpt) * G_BK;
+    i0 = (t - tap * kpt) * CB;
   };
+  // weight column of (tap dt, channel offset i0), A column of the lane's 16-B chunk cg
+  auto wcol = [&](int dt, int i0) { return X3N ? dt * 2 * g.Kc + 2 * i0 : dt * g.Kc + i0; };
+  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : acol(a, i0) + cg * 8; };
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
 
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     int tap, i0;
     tapchunk(t, tap, i0);
     const int dt = par ? dt0 + 2 * tap : tap;
-    const int k0 = dt * g.Kc + i0;
+    const int k0 = wcol(dt, i0);
     char* sbase = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       char* dst;
       if (q < AP) {
         const int r = rowmap_src(amap[i], dt, g);
-        src = r >= 0 ? (const void*)(in + (size_t)r * g.lda + acol(a, i0) + swz(q * 8 + sub, pch) * 8) : (const void*)a.zero;
+        src = r >= 0 ? (const void*)(in + (size_t)r * g.lda + acolx(i0, swz(q * 8 + sub, pch))) : (const void*)a.zero;
         dst = sbase + q * 1024;
       } else {
         src = wb + boff[i] + k0;
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     const int sgn = g.transposed ? -1 : 1;
     auto stage_w = [&](int u, int buf) {
       const int c = u / KTW, dt = u - c * KTW;
-      const int k0 = dt * g.Kc + c * G_BK;
+      const int k0 = wcol(dt, c * CB);
       char* sbase = smem + Cfg::SOFF + buf * STAGE;
       const void* src0 = wb + (size_t)(n0 + wave * 8 + sub) * Ktot + k0 + swz(wave * 8 + sub, pch) * 8;
 #pragma unroll
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         } else if (q < NP && dt >= 2 && c + 1 < kpt) {
           const int pa = (dt - 2) * WIN_APS + (q - Cfg::BP);  // A piece of chunk c + 1
           if (pa < BM / 8) {
-            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acol(a, (c + 1) * G_BK) + swz(pa * 8 + sub, pch) * 8;
+            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx((c + 1) * CB, swz(pa * 8 + sub, pch));
             dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
           }
         }
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A0W; ++i) {
       const int pa = (wave + BG_WAVES * i) % (BM / 8);
-      __builtin_amdgcn_global_load_lds(in + (size_t)(m0 + pa * 8 + sub) * g.lda + swz(pa * 8 + sub, pch) * 8,
+      __builtin_amdgcn_global_load_lds(in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx(0, swz(pa * 8 + sub, pch)),
                                        (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
     stage_w(0, 0);
@@ -246,9 +252,14 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y)
-            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[ks][y]),
-                                   acc[x][y]);
+          for (int y = 0; y < BG_NT; ++y) {
+            // X3N: half 0 = the hi fragments (x_hi W_hi), half 1 = the lo ones (x_lo W_hi + x_hi W_lo)
+            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]),
+                                   __builtin_bit_cast(bf16x8, f[X3N ? 0 : ks][y]), acc[x][y]);
+            if (X3N && ks == 1)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
+                                     acc[x][y]);
+          }
         if (ks == 0) {  // pin the first half's MFMAs above the second wait (hipcc sinks them below it)
 #pragma unroll
           for (int x = 0; x < BG_MT; ++x)
@@ -280,24 +291,49 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       const char* sa = smem + buf * STAGE;
       const char* sb = sa + AP * 1024;
       // (batched inline-asm fragment reads as in the WIN loop measured neutral here: DESIGN.md §4.6)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[BG_MT], fb[BG_NT];
-        const int c = ks * 4 + fg;
+      if constexpr (X3N) {
+        // the hi and lo fragments of the block (chunks fg and 4 + fg), three products
+        bf16x8 fah[BG_MT], fal[BG_MT], fbh[BG_NT], fbl[BG_NT];
 #pragma unroll
         for (int y = 0; y < BG_NT; ++y) {
           const int r = wn * 32 + y * 16 + fr;
-          fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+          fbh[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, fg) * 16);
+          fbl[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, 4 + fg) * 16);
         }
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x) {
           const int r = wm * 144 + x * 16 + fr;
-          fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+          fah[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, fg) * 16);
+          fal[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, 4 + fg) * 16);
         }
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+          for (int y = 0; y < BG_NT; ++y) {
+            acc[x][y] = mfma_bf16x(fah[x], fbh[y], acc[x][y]);
+            acc[x][y] = mfma_bf16x(fal[x], fbh[y], acc[x][y]);
+            acc[x][y] = mfma_bf16x(fah[x], fbl[y], acc[x][y]);
+          }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 fa[BG_MT], fb[BG_NT];
+          const int c = ks * 4 + fg;
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) {
+            const int r = wn * 32 + y * 16 + fr;
+            fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+          }
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x) {
+            const int r = wm * 144 + x * 16 + fr;
+            fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+          }
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+        }
       }
       if (t + 2 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -457,10 +493,10 @@ using namespace f3;
 bool f3_igemm_big_ok(const ConvGemmArgs& a) {
   if (!f3_igemm_ok(a)) return false;
   if (a.g.Nc != 128 && a.g.Nc != 256) return false;
-  return a.g.KT * a.g.Kc / G_BK >= 6;
+  return a.g.KT * a.g.Kc / (a.x3n ? 32 : G_BK) >= 6;
 }
 
-template <int WM, int WN>
+template <int WM, int WN, bool X3N>
 static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int BM = BigCfg<WM, WN>::BM;
   int tiles = (a.g.M + BM - 1) / BM;
@@ -470,11 +506,11 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
     const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
     tiles = (M0 + BM - 1) / BM + (M1 + BM - 1) / BM;
   }
-#define F3_BCASE(E)                                                                        \
-  if (epi == (E)) {                                                                       \
-    hipLaunchKernelGGL((igemm_big<(E), WM, WN>), dim3(tiles), dim3(BG_THREADS), 0, s, a);  \
-    F3_LAUNCH_CHECK();                                                                     \
-    return F3_OK;                                                                          \
+#define F3_BCASE(E)                                                                              \
+  if (epi == (E)) {                                                                             \
+    hipLaunchKernelGGL((igemm_big<(E), WM, WN, false, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    F3_LAUNCH_CHECK();                                                                           \
+    return F3_OK;                                                                                \
   }
   F3_BCASE(EPI_BIASV | EPI_STATS)            // gcn forward
   F3_BCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
@@ -491,8 +527,26 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
 // 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows.
 static bool big_win_ok(const ConvGemmArgs& a) {
   const ConvGeom& g = a.g;
+  const int cb = a.x3n ? 32 : G_BK;
   return g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
-         g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % G_BK == 0 && g.Kc / G_BK >= 2 && !igemm_parity(g);
+         g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % cb == 0 && g.Kc / cb >= 2 && !igemm_parity(g);
+}
+
+template <bool X3N>
+static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
+  const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
+#define F3_WCASE(E)                                                                                 \
+  if (epi == (E)) {                                                                                \
+    hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a);  \
+    F3_LAUNCH_CHECK();                                                                              \
+    return F3_OK;                                                                                   \
+  }
+  F3_WCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
+  F3_WCASE(EPI_RELUMASK)                     // tcn dgrad
+  F3_WCASE(EPI_BIAS)                         // plain conv (tests)
+  F3_WCASE(0)                                // plain input gradient (tests)
+#undef F3_WCASE
+  return F3_EINVAL;
 }
 
 int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
@@ -500,19 +554,9 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   if (big_win_ok(a)) {
-    const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
-#define F3_WCASE(E)                                                                        \
-    if (epi == (E)) {                                                                     \
-      hipLaunchKernelGGL((igemm_big<(E), 2, 4, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-      F3_LAUNCH_CHECK();                                                                   \
-      return F3_OK;                                                                        \
-    }
-    F3_WCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
-    F3_WCASE(EPI_RELUMASK)                     // tcn dgrad
-    F3_WCASE(EPI_BIAS)                         // plain conv (tests)
-    F3_WCASE(0)                                // plain input gradient (tests)
-#undef F3_WCASE
+    const int r = a.x3n ? launch_win<true>(a, epi, s) : launch_win<false>(a, epi, s);
+    if (r != F3_EINVAL) return r;
   }
-  if (a.g.Nc == 256) return launch_big<1, 8>(a, epi, s);
-  return launch_big<2, 4>(a, epi, s);
+  if (a.g.Nc == 256) return a.x3n ? launch_big<1, 8, true>(a, epi, s) : launch_big<1, 8, false>(a, epi, s);
+  return a.x3n ? launch_big<2, 4, true>(a, epi, s) : launch_big<2, 4, false>(a, epi, s);
 }

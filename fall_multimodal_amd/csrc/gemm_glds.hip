@@ -33,7 +33,8 @@ constexpr int G_BM = 128;
 // staged 2x more A than B bytes).
 constexpr int G_WIN_ROWS = 128 + 2 * 4 * 18;  // window capacity: P <= 4, V <= 18 (3 workgroups per CU)
 
-template <int EPI, int WN, int NST, bool WIN = false>
+// X3N: the bf16x3 native form (ConvGemmArgs::x3n; see igemm_big)
+template <int EPI, int WN, int NST, bool WIN = false, bool X3N = false>
 __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   constexpr int BM = G_BM, BN = 32 * WN;
   constexpr int A_BYTES = WIN ? 0 : BM * G_BK * 2, B_BYTES = BN * G_BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -74,10 +75,13 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     return (n * g.T_out + 2 * tt + p) * g.V + v;
   };
   const int m0 = (tile / ntn) * BM, j0 = (tile % ntn) * BN;
-  const int Ktot = g.KT * g.Kc;
-  const int kpt = g.Kc / G_BK;                    // k chunks per tap
+  constexpr int CB = X3N ? 32 : G_BK;             // channels per k step
+  const int Ktot = g.KT * g.Kc * (X3N ? 2 : 1);   // packed weight row length
+  const int kpt = g.Kc / CB;                      // k chunks per tap
   const int dt0 = par ? ((p + g.P) & 1) : 0;      // first tap of this parity
-  const int nchunk = par ? ((g.KT - dt0 + 1) / 2) * kpt : Ktot / G_BK;
+  const int nchunk = (par ? (g.KT - dt0 + 1) / 2 : g.KT) * kpt;
+  auto wcol = [&](int dt, int i0) { return X3N ? dt * 2 * g.Kc + 2 * i0 : dt * g.Kc + i0; };
+  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : acol(a, i0) + cg * 8; };
   // window mode: stage t = (chunk t / KT, tap t % KT); window row of tile row r for tap dt:
   // r + wofs(dt) with wofs = dt*V (forward) or (2P - dt)*V (input gradient)
   const int PV = g.P * g.V, WR = BM + 2 * PV;
@@ -98,11 +102,11 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   // per-lane staging rows (fixed for the whole k loop)
   const int sub = lane >> 3, pch = lane & 7;
   RowMap a_map[A_INSTR > 0 ? A_INSTR : 1];
-  int a_c[A_INSTR > 0 ? A_INSTR : 1];
+  int a_c[A_INSTR > 0 ? A_INSTR : 1];  // the lane's 16-B chunk of its staging row (swizzled)
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int rr = (wave * A_INSTR + i) * 8 + sub;
-    a_c[i] = swz(rr, pch) * 8;
+    a_c[i] = swz(rr, pch);
     a_map[i] = rowmap(phys(m0 + rr), g);
   }
   const unsigned short* b_row[B_INSTR];
@@ -116,15 +120,15 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   (void)b_step;
 
   auto stage = [&](int t, int buf) {
-    int tap = t / kpt, i0 = (t - tap * kpt) * G_BK;
-    if (WIN) { tap = t % g.KT; i0 = (t / g.KT) * G_BK; }
+    int tap = t / kpt, i0 = (t - tap * kpt) * CB;
+    if (WIN) { tap = t % g.KT; i0 = (t / g.KT) * CB; }
     const int dt = par ? dt0 + 2 * tap : tap;
-    const int k0 = dt * g.Kc + i0;
+    const int k0 = wcol(dt, i0);
     char* sa = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
       const int r = rowmap_src(a_map[i], dt, g);
-      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + acol(a, i0) + a_c[i] : a.zero;
+      const unsigned short* src = r >= 0 ? in + (size_t)r * g.lda + acolx(i0, a_c[i]) : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(sa + (wave * A_INSTR + i) * 1024), 16, 0, 0);
     }
     char* sb = sa + A_BYTES;
@@ -137,11 +141,11 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 
   // window staging: 1-KiB pieces of 8 rows, dealt round-robin to the 4 waves (waited with vmcnt(0))
   auto load_win = [&](int chunk) {
-    const int i0 = chunk * G_BK, nwp = (WR + 7) >> 3;
+    const int i0 = chunk * CB, nwp = (WR + 7) >> 3;
     for (int q = wave; q < nwp; q += 4) {
       const int rr = q * 8 + sub, gm = m0 - PV + rr;
       const bool ok = rr < WR && gm >= 0 && gm < g.M;
-      const unsigned short* src = ok ? in + (size_t)gm * g.lda + acol(a, i0) + swz(rr, pch) * 8 : a.zero;
+      const unsigned short* src = ok ? in + (size_t)gm * g.lda + acolx(i0, swz(rr, pch)) : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(smem + WIN_OFF + q * 1024), 16, 0, 0);
     }
   };
@@ -195,31 +199,55 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
     }
     const char* sa = smem + buf * STAGE;
     const char* sb = sa + A_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[4], fb[WN];
-      const int c = ks * 4 + fg;
+    // the A / B fragments of chunk c (16-B chunk index within the staged 128-B row)
+    auto frag_a = [&](int x, int c) -> bf16x8 {
+      if (WIN) {
+        const int r = wm * 64 + x * 16 + fr + wo;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + WIN_OFF + r * 128 + swz(r, c) * 16);
+        const bool ok = (unsigned)(tfr[x] + wsh) < (unsigned)g.T_out;
+        return ok ? v : bf16x8{};
+      }
+      const int r = wm * 64 + x * 16 + fr;
+      return *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
+    };
+    auto frag_b = [&](int y, int c) -> bf16x8 {
+      const int r = wj * 16 * WN + y * 16 + fr;
+      return *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+    };
+    if constexpr (X3N) {  // hi fragments (chunk fg), lo fragments (chunk 4 + fg), three products
+      bf16x8 fah[4], fal[4], fbh[WN], fbl[WN];
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        if (WIN) {
-          const int r = wm * 64 + x * 16 + fr + wo;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + WIN_OFF + r * 128 + swz(r, c) * 16);
-          const bool ok = (unsigned)(tfr[x] + wsh) < (unsigned)g.T_out;
-          fa[x] = ok ? v : bf16x8{};
-        } else {
-          const int r = wm * 64 + x * 16 + fr;
-          fa[x] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, c) * 16);
-        }
+        fah[x] = frag_a(x, fg);
+        fal[x] = frag_a(x, 4 + fg);
       }
 #pragma unroll
       for (int y = 0; y < WN; ++y) {
-        const int r = wj * 16 * WN + y * 16 + fr;
-        fb[y] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, c) * 16);
+        fbh[y] = frag_b(y, fg);
+        fbl[y] = frag_b(y, 4 + fg);
       }
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+        for (int y = 0; y < WN; ++y) {
+          acc[x][y] = mfma_bf16x(fah[x], fbh[y], acc[x][y]);
+          acc[x][y] = mfma_bf16x(fal[x], fbh[y], acc[x][y]);
+          acc[x][y] = mfma_bf16x(fah[x], fbl[y], acc[x][y]);
+        }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[4], fb[WN];
+        const int c = ks * 4 + fg;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) fa[x] = frag_a(x, c);
+#pragma unroll
+        for (int y = 0; y < WN; ++y) fb[y] = frag_b(y, c);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa[x], fb[y], acc[x][y]);
+      }
     }
     if (NST == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -375,7 +403,9 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
 using namespace f3;
 
 bool f3_igemm_ok(const ConvGemmArgs& a) {
-  return a.inb && a.wb && a.zero && a.g.Kc % G_BK == 0 && a.g.lda % 8 == 0 &&
+  if (!a.inb || !a.wb || !a.zero || a.g.lda % 8 != 0) return false;
+  if (a.x3n) return a.kwrap == 0 && a.g.Kc % 32 == 0 && a.g.lda >= 2 * a.g.Kc;
+  return a.g.Kc % G_BK == 0 &&
          (a.kwrap == 0 || (a.kwrap % G_BK == 0 && a.g.Kc == 3 * a.kwrap && a.g.lda >= 2 * a.kwrap));
 }
 
@@ -391,7 +421,7 @@ static bool igemm_win_ok(const ConvGemmArgs& a, int epi) {
   return epi == (EPI_BIAS | EPI_STATS | EPI_GAP) || epi == EPI_RELUMASK || epi == EPI_BIAS;
 }
 
-template <int WN, int NST, bool WIN = false>
+template <int WN, int NST, bool WIN = false, bool X3N = false>
 static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
   const int ntn = (a.g.Nc + 32 * WN - 1) / (32 * WN);
   int tiles = ((a.g.M + G_BM - 1) / G_BM) * ntn;
@@ -403,7 +433,7 @@ static int launch_igemm(const ConvGemmArgs& a, int epi, hipStream_t s) {
   }
 #define F3_ICASE(E)                                                                   \
   if (epi == (E)) {                                                                  \
-    hipLaunchKernelGGL((igemm_bf16<(E), WN, NST, WIN>), dim3(tiles), dim3(256), 0, s, a); \
+    hipLaunchKernelGGL((igemm_bf16<(E), WN, NST, WIN, X3N>), dim3(tiles), dim3(256), 0, s, a); \
     F3_LAUNCH_CHECK();                                                                \
     return F3_OK;                                                                     \
   }
@@ -426,14 +456,15 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (f3_pw_ok(a, epi)) return f3_pw_gemm(args, epi, s);
   // two LDS stages (three measured slower for both the windows and the tiles)
   if (igemm_win_ok(a, epi)) {
-    if (a.g.Nc == 128) return launch_igemm<4, 2, true>(a, epi, s);
-    return launch_igemm<2, 2, true>(a, epi, s);
+    if (a.x3n) return a.g.Nc == 128 ? launch_igemm<4, 2, true, true>(a, epi, s) : launch_igemm<2, 2, true, true>(a, epi, s);
+    return a.g.Nc == 128 ? launch_igemm<4, 2, true>(a, epi, s) : launch_igemm<2, 2, true>(a, epi, s);
   }
   if (f3_igemm_big_ok(a)) return f3_igemm_big(args, epi, s);
   // 128-wide column tiles unless they would leave a partial tile (Nc = 192: the gcn input
   // gradient of the 64-channel layers, where a second 128-wide tile is half empty)
-  if (a.g.Nc > 64 && a.g.Nc % 128 == 0) return launch_igemm<4, 2>(a, epi, s);
-  return launch_igemm<2, 2>(a, epi, s);
+  const bool wide = a.g.Nc > 64 && a.g.Nc % 128 == 0;
+  if (a.x3n) return wide ? launch_igemm<4, 2, false, true>(a, epi, s) : launch_igemm<2, 2, false, true>(a, epi, s);
+  return wide ? launch_igemm<4, 2>(a, epi, s) : launch_igemm<2, 2>(a, epi, s);
 }
 
 // ============================================================================

@@ -33,6 +33,11 @@ F3_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // hi segment; 64-column chunks never straddle the boundary since kwrap % 64 == 0)
 F3_DEV int acol(const ConvGemmArgs& a, int k) { return (a.kwrap > 0 && k >= 2 * a.kwrap) ? k - 2 * a.kwrap : k; }
 
+// bf16x3 native form (ConvGemmArgs::x3n): the 16-B chunk cg (0..7) of the staged 128-B row piece of
+// channel block i0 (32 channels) comes from the hi half (cg < 4: column i0 + 8 cg) or the lo half
+// (cg >= 4: column C + i0 + 8 (cg - 4)) of a row [x_hi (C) | x_lo (C)]
+F3_DEV int x3n_col(int C, int i0, int cg) { return i0 + 8 * cg + (cg >= 4 ? C - 32 : 0); }
+
 // Parity-split rows for a stride-2 input gradient (see igemm_bf16). Measured on MI355X (B=256,
 // V=18): tcn layer 5 (Kc=256) 162 -> 144 us, but layer 3 (Kc=128, 2 k-chunks per tap) 85 ->
 // 94 us — with short per-tap k loops the halved MFMA work does not pay for the wider row

@@ -48,6 +48,14 @@ struct ConvGemmArgs {
   // (2 kwrap columns, lda >= 2 kwrap) and the third K segment re-reads x_hi: A column k >= 2 kwrap
   // is read at k - 2 kwrap (igemm_bf16 / igemm_big; 0 = off)
   int kwrap;
+  // bf16x3 native form (x3n = 1, igemm_bf16 / igemm_big / pw_gemm): the activation rows hold
+  // [x_hi (Kc) | x_lo (Kc)] (lda >= 2 Kc), Kc = the real channel count, and the packed weights hold,
+  // per tap, 32-channel blocks [W_hi (32) | W_lo (32)] (row length KT * 2 Kc). A k step covers one
+  // 32-channel block: its staged 128-B row piece is [x_hi 32 | x_lo 32] and the wave issues the split
+  // product's three MFMAs x_hi W_hi + x_lo W_hi + x_hi W_lo from the four fragments (x_hi read once
+  // for two products), so the bytes staged and the fragments read per MFMA are 2/3 of the
+  // K-concatenated form's
+  int x3n;
 };
 
 enum : int { WG_OUT_CONV = 0, WG_OUT_GCN = 1 };

@@ -49,6 +49,29 @@ F3_DEV void prep_x3cat(const PrepJob& j, int e) {
   d[2 * inner] = (__bf16)(val - (float)hi);
 }
 
+// bf16x3 native form (prep code 4, ConvGemmArgs::x3n): per tap, 32-channel blocks [W_hi (32) | W_lo (32)]
+// (dst [rows][KT][2 inner], channel c of a tap at (c / 32) * 64 + c % 32, its lo 32 further on); the
+// activation rows are [x_hi | x_lo] and the GEMM issues x_hi W_hi + x_lo W_hi + x_hi W_lo per block.
+// inner % 32 == 0. j.n counts the dst elements (2 per source value).
+F3_DEV void prep_x3n(const PrepJob& j, int e) {
+  const bool gcn = j.type == PREP_PACK_GCN || j.type == PREP_PACK_GCN_T;
+  const bool tr = j.type == PREP_PACK_CONV_T || j.type == PREP_PACK_GCN_T;
+  const int J = j.d0, I = j.d1, KT = gcn ? 1 : j.d2;
+  const int inner = gcn ? (tr ? J : j.d2 * I) : (tr ? J : I);
+  const int row = e / (KT * inner), r = e - row * KT * inner, dt = r / inner, c = r - dt * inner;
+  float val;
+  if (gcn) {
+    const int kc = tr ? row : c, cc = tr ? c : row, k = kc / I, ci = kc - k * I;
+    val = j.s0[((size_t)k * J + cc) * I + ci];
+  } else {
+    val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
+  }
+  const __bf16 hi = (__bf16)val;
+  __bf16* d = reinterpret_cast<__bf16*>(j.dst) + ((size_t)row * KT + dt) * 2 * inner + (c >> 5) * 64 + (c & 31);
+  d[0] = hi;
+  d[32] = (__bf16)(val - (float)hi);
+}
+
 // The job table plus each job's first block: a 1-D grid whose blocks are shared out in proportion
 // to the jobs' sizes (a fixed 64 blocks per job left the 256-channel packs to a few blocks looping
 // ~100 times while the small jobs' blocks idled: 83 us per launch in the bf16x3 step)
@@ -66,6 +89,10 @@ __global__ void prep_kernel(PrepLaunch L) {
   const int stride = nb * blockDim.x;
   if (j.bf16 == 3) {
     for (int e = lb * blockDim.x + threadIdx.x; e < j.n / 3; e += stride) prep_x3cat(j, e);
+    return;
+  }
+  if (j.bf16 == 4) {
+    for (int e = lb * blockDim.x + threadIdx.x; e < j.n / 2; e += stride) prep_x3n(j, e);
     return;
   }
   for (int e = lb * blockDim.x + threadIdx.x; e < j.n; e += stride) {
@@ -1872,7 +1899,7 @@ int f3_prep(const PrepTable& t, hipStream_t s) {
   L.t = t;
   L.boff[0] = 0;
   for (int j = 0; j < t.n; ++j) {  // ~4 items per thread, 1..2048 blocks per job
-    const long long items = t.jobs[j].bf16 == 3 ? t.jobs[j].n / 3 : t.jobs[j].n;
+    const long long items = t.jobs[j].bf16 == 3 ? t.jobs[j].n / 3 : t.jobs[j].bf16 == 4 ? t.jobs[j].n / 2 : t.jobs[j].n;
     L.boff[j + 1] = L.boff[j] + (int)std::min<long long>(2048, std::max<long long>(1, (items + 1023) / 1024));
   }
   hipLaunchKernelGGL(prep_kernel, dim3(L.boff[t.n]), dim3(256), 0, s, L);

@@ -539,6 +539,27 @@ inline int side_pct(bool split, int l) { return split && l >= 2 ? 75 : 0; }
 // runs on layer0.hip's fused kernels in their fp32 form (mix + GEMM + bias + BN1 sums in one pass;
 // backward dZ, dx, dA and dW partials in one pass): 10.14 -> 9.92 ms/step against the generic mix +
 // split GEMMs (profiles/r04_gcn0_x3_ab.txt)
+// bf16x3 GEMMs on the bf16 kernels in the native form (ConvGemmArgs::x3n, prep code 4: [x_hi | x_lo]
+// rows staged once, three MFMAs per 32-channel block) instead of the K-concatenated one (kwrap, prep
+// code 3: the third K segment re-stages x_hi). F3_X3N=0: the K-concatenated form (A/B, temporary)
+inline bool x3n_on() {
+  static const bool on = !getenv("F3_X3N") || atoi(getenv("F3_X3N")) != 0;
+  return on;
+}
+inline int x3code() { return x3n_on() ? 4 : 3; }
+// packed size (bf16 elements) of n weights in a bf16x3 code
+inline int x3mul(int code) { return code == 4 ? 2 : code == 3 ? 3 : 1; }
+// set a bf16x3 GEMM on [hi | lo] rows of C channels (lda 2C): native form, or K-concatenated (Kc 3C)
+inline void x3_gemm(ConvGemmArgs& a, int C) {
+  if (x3n_on()) {
+    a.x3n = 1;
+  } else {
+    a.g.Kc = 3 * C;
+    a.kwrap = C;
+  }
+  a.g.lda = 2 * C;
+}
+
 // prep code of the packed GEMM weights: 0 fp32, 1 bf16, 2 split hi / lo planes
 inline int wcode(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16 ? 1 : is_x3(n) ? 2 : 0; }
 // bf16 view of an activation slot (bf16 mode stores GEMM operand tensors as bf16)
@@ -576,20 +597,18 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
     // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
     const bool l0f = wc == 2 && f3_gcn0_ok(K, V, Ci, C);  // fp32 weights (layer0.hip)
-    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? 3 : (l0f ? 0 : wc);
-    add_job(pt, PREP_PACK_GCN, C * K * Ci * (gc == 3 ? 3 : 1), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
-    add_job(pt, PREP_PACK_CONV, C * 9 * C * (wc == 2 ? 3 : 1), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
-            wc == 2 ? 3 : wc);  // bf16x3: K-concatenated for the bf16 implicit-GEMM kernels
+    // bf16x3: the bf16 implicit-GEMM kernels' packing (native [hi 32 | lo 32] blocks, code 4)
+    const int xc = wc == 2 ? x3code() : wc;
+    const int gc = wc == 2 && f3_mix_x3_ok(K, V, Ci) ? xc : (l0f ? 0 : wc);
+    add_job(pt, PREP_PACK_GCN, C * K * Ci * x3mul(gc), X.gw, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
+    add_job(pt, PREP_PACK_CONV, C * 9 * C * x3mul(xc), X.tw, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, xc);
     if (train) {
-      add_job(pt, PREP_PACK_GCN_T, C * K * Ci * (gc == 3 ? 3 : 1), X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
-      add_job(pt, PREP_PACK_CONV_T, C * 9 * C * (wc == 2 ? 3 : 1), X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9,
-              wc == 2 ? 3 : wc);
+      add_job(pt, PREP_PACK_GCN_T, C * K * Ci * x3mul(gc), X.gwT, q.p(L.gcn_w), nullptr, nullptr, C, Ci, K, gc);
+      add_job(pt, PREP_PACK_CONV_T, C * 9 * C * x3mul(xc), X.twT, q.p(L.tcn_w), nullptr, nullptr, C, C, 9, xc);
     }
     if (L.res == RES_CONV) {
-      const int rc = wc == 2 ? 3 : wc;  // bf16x3: K-concatenated
-      add_job(pt, PREP_PACK_CONV, C * Ci * (rc == 3 ? 3 : 1), X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, rc);
-      if (train)
-        add_job(pt, PREP_PACK_CONV_T, C * Ci * (rc == 3 ? 3 : 1), X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, rc);
+      add_job(pt, PREP_PACK_CONV, C * Ci * x3mul(xc), X.rw, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, xc);
+      if (train) add_job(pt, PREP_PACK_CONV_T, C * Ci * x3mul(xc), X.rwT, q.p(L.res_w), nullptr, nullptr, C, Ci, 1, xc);
     }
   }
   F3_TRY(f3_prep(pt, s));
@@ -645,10 +664,9 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       ga.in = hb ? nullptr : X.z; ga.inb = bfa(X.z, hb); ga.zero = w.zero;
       ga.w = X.gw; ga.wb = bf(X.gw, wq); ga.out = X.g; ga.outb = bfa(X.g, hb); ga.x3 = x3;
       ga.bias = X.beff; ga.st_sum = X.bn1.fsum; ga.st_sq = X.bn1.fsq;
-      if (gcat) {  // [Z_hi | Z_lo | Z_hi] x [W_hi | W_hi | W_lo] over 3 K Ci on the bf16 kernels
+      if (gcat) {  // the [Z_hi | Z_lo] rows of K Ci channels on the bf16 kernels
         ga.x3 = 0; ga.in = nullptr; ga.inb = bfa(X.z, 1);
-        ga.g = geom(Mi, C, 3 * K * Ci, 1, 1, 0, 0, Ti, Ti, V, 2 * K * Ci, C);
-        ga.kwrap = K * Ci;
+        x3_gemm(ga, K * Ci);
       }
       F3_TRY(f3_conv_gemm(&ga, 0, EPI_BIASV | EPI_STATS, s));
     }
@@ -660,11 +678,10 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       if (hb && !X.xb) return F3_ESTATE;
       ra.w = X.rw; ra.wb = bf(X.rw, wq); ra.out = X.r; ra.outb = bfa(X.r, hb); ra.x3 = x3;
       ra.bias = q.p(L.res_b); ra.st_sum = X.bnr.fsum; ra.st_sq = X.bnr.fsq;
-      if (x3) {  // the previous block's [x_hi | x_lo | x_hi] copy against [W_hi | W_hi | W_lo]
+      if (x3) {  // the previous block's [x_hi | x_lo] copy
         if (!X.xb) return F3_ESTATE;
         ra.x3 = 0; ra.in = nullptr; ra.inb = X.xb;
-        ra.g = geom(Mo, C, 3 * Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
-        ra.kwrap = Ci;
+        x3_gemm(ra, Ci);
       }
       F3_TRY(f3_conv_gemm(&ra, 0, EPI_BIAS | EPI_STATS, s));
     }
@@ -681,10 +698,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
       std::memset(&br, 0, sizeof(br));
       br.M = Mi; br.C = C; br.bn = bn1; br.g = X.g; br.u = X.u; br.g16 = hb; br.x3 = x3;
       F3_TRY(f3_bnrelu_bf16(&br, s));
-      if (x3) {
-        ta.g = geom(Mo, C, 3 * C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
-        ta.kwrap = C;
-      }
+      if (x3) x3_gemm(ta, C);
       ta.inb = X.u; ta.zero = w.zero;
       F3_TRY(f3_conv_gemm(&ta, 0, EPI_BIAS | EPI_STATS | EPI_GAP, s));
     } else {
@@ -812,10 +826,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     td.g = geom(Mi, C, C, 9, L.stride, 4, 1, Ti, To, V, C, C);
     td.in = (hb || x3) ? nullptr : dh; td.inb = bfa(dh, hb || x3); td.zero = w.zero;
     td.w = X.twT; td.wb = bf(X.twT, wq); td.out = W.dv; td.aux = X.g; td.ldaux = C; td.epi_bn = bn1;
-    if (x3) {  // K-concatenated dh rows
-      td.g = geom(Mi, C, 3 * C, 9, L.stride, 4, 1, Ti, To, V, 2 * C, C);
-      td.kwrap = C;
-    }
+    if (x3) x3_gemm(td, C);  // dh rows [hi | lo]
     td.outb = bfa(W.dv, hb); td.auxb = hb ? reinterpret_cast<const unsigned short*>(X.g) : nullptr;
     td.st_sum = X.bn1.bsum; td.st_sq = X.bn1.bsq;
     if (part & 1) F3_TRY(f3_conv_gemm(&td, 0, EPI_RELUMASK, s));
@@ -848,10 +859,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     gd.g = geom(Mi, K * Ci, C, 1, 1, 0, 0, Ti, Ti, V, C, K * Ci);
     gd.in = hb ? nullptr : dg; gd.inb = bfa(dg, hb); gd.zero = w.zero;
     gd.w = X.gwT; gd.wb = bf(X.gwT, wq); gd.x3 = x3; gd.out = W.dZ;
-    if (gcat) {  // [dg_hi | dg_lo | dg_hi] x [W^T_hi | W^T_hi | W^T_lo] over 3C
+    if (gcat) {  // dg rows [hi | lo]
       gd.x3 = 0; gd.in = nullptr; gd.inb = bfa(dg, 1);
-      gd.g = geom(Mi, K * Ci, 3 * C, 1, 1, 0, 0, Ti, Ti, V, 2 * C, K * Ci);
-      gd.kwrap = C;
+      x3_gemm(gd, C);
     }
     const bool dzb = hb && f3_mix_lds_ok(K, V, Ci);  // bf16 dZ feeds the LDS graph-mix backward
     if (dzb) {
@@ -872,10 +882,9 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       rd.g = geom(Mi, Ci, C, 1, L.stride, 0, 1, Ti, To, V, C, Ci);
       rd.in = hb ? nullptr : dres; rd.inb = bfa(dres, hb); rd.zero = w.zero;
       rd.w = X.rwT; rd.wb = bf(X.rwT, wq); rd.x3 = x3; rd.out = dx;
-      if (x3) {  // K-concatenated over 3C
+      if (x3) {  // dres rows [hi | lo]
         rd.x3 = 0; rd.in = nullptr; rd.inb = bfa(dres, 1);
-        rd.g = geom(Mi, Ci, 3 * C, 1, L.stride, 0, 1, Ti, To, V, 2 * C, Ci);
-        rd.kwrap = C;
+        x3_gemm(rd, C);
       }
       if (part & 1) F3_TRY(f3_conv_gemm(&rd, 0, EPI_ADD, s));
     }
@@ -1681,17 +1690,18 @@ int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, flo
                           int V, int Cin, int Cout, int KT, int stride, int pad, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!x3 || !bias || !out || !wpack || !x3cat_shape_ok(N, T_in, V, Cin, Cout, KT, stride, pad)) return F3_EINVAL;
-  if (w) {  // [Cout][KT][W_hi | W_hi | W_lo] (w == NULL: wpack already packed)
+  if (w) {  // the step's packing (native [W_hi 32 | W_lo 32] blocks; w == NULL: wpack already packed)
     PrepTable t;
     t.n = 0;
-    add_job(t, PREP_PACK_CONV, Cout * KT * Cin * 3, static_cast<float*>(wpack), w, nullptr, nullptr, Cout, Cin, KT, 3);
+    add_job(t, PREP_PACK_CONV, Cout * KT * Cin * x3mul(x3code()), static_cast<float*>(wpack), w, nullptr, nullptr,
+            Cout, Cin, KT, x3code());
     F3_TRY(f3_prep(t, s));
   }
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.g = geom(N * T_out * V, Cout, 3 * Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
-  a.kwrap = Cin;
+  a.g = geom(N * T_out * V, Cout, Cin, KT, stride, pad, 0, T_out, T_in, V, 2 * Cin, Cout);
+  x3_gemm(a, Cin);
   a.inb = static_cast<const unsigned short*>(x3); a.zero = test_zero_page();
   a.wb = static_cast<const unsigned short*>(wpack); a.out = out; a.bias = bias;
   if (!f3_igemm_ok(a)) return F3_EINVAL;
@@ -1702,17 +1712,18 @@ int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void
                                 int Cin, int Cout, int KT, int stride, int pad, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!dy3 || !dx || !wpack || !x3cat_shape_ok(N, T_in, V, Cin, Cout, KT, stride, pad)) return F3_EINVAL;
-  if (w) {  // [Cin][KT][W^T_hi | W^T_hi | W^T_lo]
+  if (w) {  // the transposed packing, as the step's
     PrepTable t;
     t.n = 0;
-    add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin * 3, static_cast<float*>(wpack), w, nullptr, nullptr, Cout, Cin, KT, 3);
+    add_job(t, PREP_PACK_CONV_T, Cout * KT * Cin * x3mul(x3code()), static_cast<float*>(wpack), w, nullptr, nullptr,
+            Cout, Cin, KT, x3code());
     F3_TRY(f3_prep(t, s));
   }
   const int T_out = (T_in + 2 * pad - KT) / stride + 1;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.g = geom(N * T_in * V, Cin, 3 * Cout, KT, stride, pad, 1, T_in, T_out, V, 2 * Cout, Cin);
-  a.kwrap = Cout;
+  a.g = geom(N * T_in * V, Cin, Cout, KT, stride, pad, 1, T_in, T_out, V, 2 * Cout, Cin);
+  x3_gemm(a, Cout);
   a.inb = static_cast<const unsigned short*>(dy3); a.zero = test_zero_page();
   a.wb = static_cast<const unsigned short*>(wpack); a.out = dx;
   if (!f3_igemm_ok(a)) return F3_EINVAL;

