@@ -204,8 +204,10 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A0W; ++i) {
       const int pa = (wave + BG_WAVES * i) % (BM / 8);
-      __builtin_amdgcn_global_load_lds(in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx(0, swz(pa * 8 + sub, pch)),
-                                       (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
+      // (the source computed outside the builtin's argument list: a lambda call inside it drops
+      // the kernel's host stub without a diagnostic)
+      const void* src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx(0, swz(pa * 8 + sub, pch));
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
     stage_w(0, 0);
     stage_w(1, 1);
@@ -532,14 +534,16 @@ static bool big_win_ok(const ConvGemmArgs& a) {
          g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % cb == 0 && g.Kc / cb >= 2 && !igemm_parity(g);
 }
 
-template <bool X3N>
+// (a plain function: hipcc left the device stubs of the WIN instances undefined when they were
+// launched from a function template)
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
   const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
-#define F3_WCASE(E)                                                                                 \
-  if (epi == (E)) {                                                                                \
-    hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a);  \
-    F3_LAUNCH_CHECK();                                                                              \
-    return F3_OK;                                                                                   \
+#define F3_WCASE(E)                                                                                   \
+  if (epi == (E)) {                                                                                  \
+    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
+    F3_LAUNCH_CHECK();                                                                                \
+    return F3_OK;                                                                                     \
   }
   F3_WCASE(EPI_BIAS | EPI_STATS | EPI_GAP)   // tcn forward
   F3_WCASE(EPI_RELUMASK)                     // tcn dgrad
@@ -554,7 +558,7 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   if (big_win_ok(a)) {
-    const int r = a.x3n ? launch_win<true>(a, epi, s) : launch_win<false>(a, epi, s);
+    const int r = launch_win(a, epi, s);
     if (r != F3_EINVAL) return r;
   }
   if (a.g.Nc == 256) return a.x3n ? launch_big<1, 8, true>(a, epi, s) : launch_big<1, 8, false>(a, epi, s);
