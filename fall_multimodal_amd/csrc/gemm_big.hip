@@ -27,15 +27,21 @@ constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 
 // (Loading the weight fragments straight from global memory into registers, so the LDS stages carry
 // the A rows only, measured slower: 67 -> 87 us on the layer-6 forward)
-// WIN (clip window): for stride-1 temporal convs whose clips are exactly 144 rows (T*V = 144,
-// the 256-channel layers at T = 8) a workgroup owns two whole clips x BN = 128 output channels.
-// Each channel chunk's 288 input rows are staged ONCE (two 36-KiB A buffers) and all KT taps
-// read them shifted by (dt - P) frames, rows falling outside the clip read as zero; only the
-// weights are staged per (chunk, tap) step (16 KiB). Per workgroup that is 4 x 36 + 36 x 16 =
-// 720 KiB of L2 -> LDS fill instead of 36 x 50 KiB = 1.8 MiB for the 144 x 256 tile.
+// WIN (clip window, WIN = the clip rows of the layout): for 9-tap temporal convs a workgroup owns
+// whole clips x BN = 128 output channels — two 144-row clips (WIN = 144, one per wave row: the
+// 256-channel layers at T = 8) or one clip of up to 270 rows (WIN = 270: the 128-channel layers at
+// T = 15). Per channel chunk the clips' input rows (the "window", 288 rows x 128 B) are staged ONCE
+// and every tap reads them shifted by its frame offset, rows outside the clip reading a zero row;
+// only the weights are staged per (chunk, tap) step (16 KiB). Three row maps share the engine:
+//   stride 1 (fwd or input gradient): one window per chunk, tap dt shifts by +-(dt - P) frames;
+//   stride-2 input gradient: a tile is one output-frame parity p of its clips; the window is the
+//     clips' dY frames and only the taps dt = p + P (mod 2) contribute, shifted by (p + P - dt) / 2;
+//   stride-2 forward: two windows per chunk, the even and the odd input frames; window q serves
+//     the taps dt = P + q (mod 2), shifted by (dt - P - q) / 2.
+// Per workgroup and chunk that is 36 KiB of A fill plus 16 KiB per tap instead of 52 KiB per tap.
 typedef __attribute__((address_space(3))) const char lds_cchar_t;
-constexpr int WIN_APS = 6;  // A pieces of the next chunk carried by one step (steps 2..7 of 9)
-template <int WM, int WN, bool WIN = false>
+constexpr int WIN_APS = 16;  // DMA slots per step for the next window's A pieces (<= 12 used)
+template <int WM, int WN, int WIN = 0>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
   static constexpr int AP = WIN ? WIN_APS : BM / 8, BP = BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
@@ -47,15 +53,16 @@ struct BigCfg {
   static constexpr int OT_NEED = 16 * 1024 + BM * (BN + 8) * 2;
   static constexpr int EPI_OFF = SOFF + BG_NST * STAGE > OT_NEED ? SOFF + BG_NST * STAGE : OT_NEED;
   static constexpr int ZOFF = EPI_OFF + 4 * BN * 4;  // WIN: one zero row, read for out-of-clip taps
-  static constexpr int SMEM = ZOFF + (WIN ? 128 : 0);
+  static constexpr int DOFF = ZOFF + 128;            // WIN: 1-KiB sink of the idle DMA slots
+  static constexpr int SMEM = WIN ? DOFF + 1024 : ZOFF;
 };
 
 // X3N: the bf16x3 native form (ConvGemmArgs::x3n): a k step is one 32-channel block, its staged row
 // piece [x_hi 32 | x_lo 32] / [W_hi 32 | W_lo 32], and the wave issues x_hi W_hi + x_lo W_hi + x_hi W_lo
-template <int EPI, int WM, int WN, bool WIN = false, bool X3N = false>
+template <int EPI, int WM, int WN, int WIN = 0, bool X3N = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
-  static_assert(!(WIN && (WM != 2 || BG_MT * 16 != 144)), "WIN: two 144-row clips");
+  static_assert(WIN == 0 || ((WIN == 144 || WIN == 270) && WM == 2 && WN == 4 && BG_MT * 16 == 144), "WIN layout");
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
   static_assert(WM * WN == BG_WAVES, "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
@@ -70,11 +77,18 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int tile = xcd_remap(blockIdx.x, gridDim.x);
-  int n0 = 0;  // first output channel of the tile (WIN: Nc / BN column tiles, neighbours share rows)
+  // WIN: first output channel (Nc / BN column tiles, neighbours share rows), output-frame parity of a
+  // stride-2 input gradient, first clip; the row map (0 stride 1, 1 stride-2 dgrad, 2 stride-2 fwd)
+  constexpr int CPW = WIN == 144 ? 2 : 1;  // clips per workgroup
+  int n0 = 0, wpar = 0, clip0 = 0;
+  const int wmode = g.S == 1 ? 0 : (g.transposed ? 1 : 2);
+  const int nclip = WIN ? g.M / (g.T_out * g.V) : 0;
   if (WIN) {
     const int ncol = g.Nc / BN;
     n0 = (tile % ncol) * BN;
     tile /= ncol;
+    if (wmode == 1) { wpar = tile & 1; tile >>= 1; }
+    clip0 = tile * CPW;
   }
   const bool par = !WIN && igemm_parity(g);
   int p = 0, Tp = g.T_out, Mp = g.M;
@@ -168,53 +182,90 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (WIN) {
-    // step u = (chunk c, tap dt), chunk-major: c = u / KT, dt = u % KT. Per step every wave
-    // issues PPW DMAs: its B pieces of step u's weight stage, the 6 A pieces of chunk c + 1 that
-    // step u carries (steps 2..7 of a chunk: the buffer they fill was last read in step c*KT - 1,
-    // and a step is issued two steps ahead), and otherwise a re-issue of its first B piece.
-    constexpr int KTW = 9;
-    const int nstep = KTW * kpt;
-    const int sgn = g.transposed ? -1 : 1;
+  if constexpr (WIN != 0) {
+    constexpr int CL = WIN, NPA = (CPW * CL + 7) / 8;  // window rows per clip, A pieces per window
+    const int V = g.V, P = g.P;
+    // taps of window q (q = input-frame parity for the stride-2 forward, else 0): dt = d0 + ds j,
+    // j < nt, frame shift s0 + ss j
+    int d0[2] = {0, 0}, nt[2] = {1, 1}, s0[2] = {0, 0}, ds = 1, ss = 1;
+    if (wmode == 0) {
+      d0[0] = 0; nt[0] = g.KT; ss = g.transposed ? -1 : 1; s0[0] = -ss * P;
+    } else {
+      ds = 2;
+      for (int q = 0; q < 2; ++q) {
+        d0[q] = ((wmode == 1 ? wpar : q) + P) & 1;
+        nt[q] = (g.KT - d0[q] + 1) >> 1;
+      }
+      ss = wmode == 1 ? -1 : 1;
+      s0[0] = wmode == 1 ? (wpar + P - d0[0]) >> 1 : (d0[0] - P) >> 1;
+      s0[1] = (d0[1] - P - 1) >> 1;
+    }
+    const int NQ = wmode == 2 ? 2 : 1;            // windows per chunk
+    const int KTC = wmode == 2 ? g.KT : nt[0];    // steps per chunk
+    const int nstep = KTC * kpt, nwin = NQ * kpt;
+    auto decode = [&](int u, int& c, int& q, int& j) {
+      c = u / KTC;
+      j = u - c * KTC;
+      q = (NQ == 2 && j >= nt[0]) ? 1 : 0;
+      if (q) j -= nt[0];
+    };
+    auto ntw = [&](int w) { return nt[NQ == 2 ? (w & 1) : 0]; };
+    // source of A piece pa (8 window rows) of window w: clip row l of clip clip0 + k -> input frame
+    auto asrc = [&](int w, int pa) -> const void* {
+      const int R = pa * 8 + sub, k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL;
+      const int f = l / V, v = l - f * V, fi = NQ == 2 ? 2 * f + (w & 1) : f, clip = clip0 + k;
+      if (l >= CL || fi >= g.T_in || clip >= nclip) return a.zero;
+      return in + (size_t)((clip * g.T_in + fi) * V + v) * g.lda + acolx((w / NQ) * CB, swz(R, pch));
+    };
+    // Step u = (chunk c, window q, tap j). Per step every wave issues PPW DMAs: its B pieces of the
+    // step's weight stage, then A pieces of the next window — step j >= 2 of window w carries
+    // window w + 1's, step 0 of window w the last group of its own (the buffer a window fills was
+    // last read by window w - 1, and a step is issued two steps ahead: steps 2 .. nt(w) of window
+    // w's range are the ones that can) — and a sink DMA of the zero row in slots left idle.
     auto stage_w = [&](int u, int buf) {
-      const int c = u / KTW, dt = u - c * KTW;
-      const int k0 = wcol(dt, c * CB);
+      int c, q, j;
+      decode(u, c, q, j);
+      const int w = c * NQ + q, k0 = wcol(d0[q] + ds * j, c * CB);
       char* sbase = smem + Cfg::SOFF + buf * STAGE;
-      const void* src0 = wb + (size_t)(n0 + wave * 8 + sub) * Ktot + k0 + swz(wave * 8 + sub, pch) * 8;
+      int tw = -1, kk = 0, ncar = 1;
+      if (j >= 2) { tw = w + 1; kk = j - 2; ncar = ntw(w) - 1; }
+      else if (j == 0 && w > 0) { tw = w; ncar = ntw(w - 1) - 1; kk = ncar - 1; }
+      if (tw >= nwin) tw = -1;
+      const int aps = (NPA + ncar - 1) / ncar;
 #pragma unroll
       for (int i = 0; i < PPW; ++i) {
-        const int q = wave + BG_WAVES * i;
-        const void* src = src0;
-        char* dst = sbase + wave * 1024;
-        if (q < Cfg::BP) {
-          src = wb + (size_t)(n0 + q * 8 + sub) * Ktot + k0 + swz(q * 8 + sub, pch) * 8;
-          dst = sbase + q * 1024;
-        } else if (q < NP && dt >= 2 && c + 1 < kpt) {
-          const int pa = (dt - 2) * WIN_APS + (q - Cfg::BP);  // A piece of chunk c + 1
-          if (pa < BM / 8) {
-            src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx((c + 1) * CB, swz(pa * 8 + sub, pch));
-            dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
+        const int qs = wave + BG_WAVES * i;
+        const void* src = a.zero;
+        char* dst = smem + Cfg::DOFF;
+        if (qs < Cfg::BP) {
+          src = wb + (size_t)(n0 + qs * 8 + sub) * Ktot + k0 + swz(qs * 8 + sub, pch) * 8;
+          dst = sbase + qs * 1024;
+        } else if (tw >= 0) {
+          const int sl = qs - Cfg::BP, pa = kk * aps + sl;
+          if (sl < aps && pa < NPA) {
+            src = asrc(tw, pa);
+            dst = smem + (tw & 1) * Cfg::AWIN + pa * 1024;
           }
         }
         __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
       }
     };
-    // chunk 0's A rows, then steps 0 and 1
-    constexpr int A0W = (BM / 8 + BG_WAVES - 1) / BG_WAVES;
+    // window 0's A rows, then steps 0 and 1
+    constexpr int A0W = (NPA + BG_WAVES - 1) / BG_WAVES;
 #pragma unroll
     for (int i = 0; i < A0W; ++i) {
-      const int pa = (wave + BG_WAVES * i) % (BM / 8);
-      // (the source computed outside the builtin's argument list: a lambda call inside it drops
-      // the kernel's host stub without a diagnostic)
-      const void* src = in + (size_t)(m0 + pa * 8 + sub) * g.lda + acolx(0, swz(pa * 8 + sub, pch));
+      const int pa = (wave + BG_WAVES * i) % NPA;
+      const void* src = asrc(0, pa);
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
     stage_w(0, 0);
-    stage_w(1, 1);
+    if (nstep > 1) stage_w(1, 1);
     if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
+    if (nstep > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const int wrow = wm * 144;  // this wave's clip in the tile
+    // the wave's rows: clip base row in the window and first output row of the clip
+    const int cbase = CPW == 2 ? wm * 144 : 0, lo0 = CPW == 2 ? 0 : wm * 144;
     // fragment reads as inline asm: hipcc otherwise issues each ds_read_b128 just before the MFMA
     // that consumes it with its own lgkmcnt(0), exposing the LDS latency ~14 times per step. Both
     // k halves' 22 reads are issued at once; each half is released by a counted wait whose asm
@@ -224,10 +275,11 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
     const unsigned zaddr = lds0 + Cfg::ZOFF + fg * 16;
     for (int u = 0; u < nstep; ++u) {
-      const int c = u / KTW, dt = u - c * KTW;
-      const int sh = sgn * (dt - g.P) * g.V;  // row shift of this tap inside the clip
+      int c, q, j;
+      decode(u, c, q, j);
+      const int sh = (s0[q] + ss * j) * V;  // row shift of this tap inside the clip
       if (u + 2 < nstep) stage_w(u + 2, (u + 2) % 3);
-      const unsigned sa = lds0 + (c & 1) * Cfg::AWIN;
+      const unsigned sa = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN;
       const unsigned sb = lds0 + Cfg::SOFF + (u % 3) * STAGE;
       u32x4_t f[2][BG_NT + BG_MT];
 #pragma unroll
@@ -240,8 +292,8 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         }
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x) {
-          const int rs = x * 16 + fr + sh, r = wrow + rs;
-          const unsigned ad = (rs >= 0 && rs < 144) ? sa + r * 128 + swz(r, cc) * 16 : zaddr;
+          const int rs = lo0 + x * 16 + fr + sh, r = cbase + rs;
+          const unsigned ad = (rs >= 0 && rs < CL) ? sa + r * 128 + swz(r, cc) * 16 : zaddr;
           asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][BG_NT + x]) : "v"(ad));
         }
       }
@@ -250,7 +302,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int q = 0; q < BG_NT + BG_MT; ++q) asm volatile("" : "+v"(f[ks][q]));
+        for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
 #pragma unroll
         for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
@@ -358,7 +410,18 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const bool stage_out = !(EPI & EPI_ADD) && a.outb && g.ldo % 8 == 0 && g.Nc % 8 == 0;
   __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
   const int TV = g.T_out * g.V;
-  const int nlo = m0 / TV;  // GAP is forward-only (no parity split): m0 is the first output row
+  const int nlo = WIN ? clip0 : m0 / TV;  // first clip (GAP is forward-only: no parity split)
+  // output row of tile row rl (-1: none)
+  auto orow = [&](int rl) -> int {
+    if constexpr (WIN != 0) {
+      const int k = (CPW == 2 && rl >= WIN) ? 1 : 0, lo = rl - k * WIN, clip = clip0 + k;
+      const int f = lo / g.V, v = lo - f * g.V, t = wmode == 1 ? 2 * f + wpar : f;
+      if (lo >= WIN || t >= g.T_out || clip >= nclip) return -1;
+      return (clip * g.T_out + t) * g.V + v;
+    } else {
+      return phys(m0 + rl);
+    }
+  };
   // Per 16-row group x: the group's 4 output rows are resolved and every operand the epilogue
   // reads (RELUMASK source g, graph-mixed bias) is loaded for all 4 rows x BG_NT columns before
   // any use, from clamped in-bounds addresses. A per-element conditional load (row outside the
@@ -376,7 +439,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int mc = max(phys(m0 + wm * 144 + x * 16 + fg * 4 + r), 0);
+        const int mc = max(orow(wm * 144 + x * 16 + fg * 4 + r), 0);
 #pragma unroll
         for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1));
       }
@@ -393,7 +456,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   for (int x = 0; x < BG_MT; ++x) {
     int mrow[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) mrow[r] = phys(m0 + wm * 144 + x * 16 + fg * 4 + r);
+    for (int r = 0; r < 4; ++r) mrow[r] = orow(wm * 144 + x * 16 + fg * 4 + r);
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) {
       const int jl = wn * 32 + y * 16 + fr, j = n0 + jl;  // tile-local / global column
@@ -479,7 +542,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     constexpr int CPR = BN / 8;  // 16-B chunks per tile row
     for (int q = tid; q < BM * CPR; q += blockDim.x) {
       const int rl = q / CPR, c = q - rl * CPR;
-      const int m = phys(m0 + rl), j = n0 + c * 8;
+      const int m = orow(rl), j = n0 + c * 8;
       if (m < 0 || j >= g.Nc) continue;
       *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
           *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
@@ -510,7 +573,7 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   }
 #define F3_BCASE(E)                                                                              \
   if (epi == (E)) {                                                                             \
-    hipLaunchKernelGGL((igemm_big<(E), WM, WN, false, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    hipLaunchKernelGGL((igemm_big<(E), WM, WN, 0, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
     F3_LAUNCH_CHECK();                                                                           \
     return F3_OK;                                                                                \
   }
@@ -525,23 +588,39 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   return F3_EINVAL;
 }
 
-// Clip-window form (WIN): stride-1 9-tap temporal convs (forward or input gradient) of the
-// 256-channel layers at T = 8, where a clip is exactly one wave's 144 rows.
-static bool big_win_ok(const ConvGemmArgs& a) {
+// Clip-window form (WIN): the clip rows of the window layout for a 9-tap temporal conv (stride 1
+// forward or input gradient, stride-2 forward or input gradient) whose window and output frames
+// fit 144 rows (two clips per tile) or 270 rows (one clip), else 0
+static int big_win_rows(const ConvGemmArgs& a) {
   const ConvGeom& g = a.g;
   const int cb = a.x3n ? 32 : G_BK;
-  return g.Nc % 128 == 0 && g.S == 1 && g.KT == 9 && 2 * g.P == g.KT - 1 && g.T_in == g.T_out &&
-         g.T_out * g.V == 144 && g.M % 288 == 0 && g.Kc % cb == 0 && g.Kc / cb >= 2 && !igemm_parity(g);
+  if (g.Nc % 128 || g.KT != 9 || 2 * g.P != g.KT - 1 || g.Kc % cb || g.T_out <= 0 || g.M % (g.T_out * g.V))
+    return 0;
+  int wf, of;  // window frames, output frames of one tile clip
+  if (g.S == 1) {
+    if (g.T_in != g.T_out) return 0;
+    wf = of = g.T_in;
+  } else if (g.S == 2) {
+    wf = g.transposed ? g.T_in : (g.T_in + 1) / 2;
+    of = g.transposed ? (g.T_out + 1) / 2 : g.T_out;
+  } else {
+    return 0;
+  }
+  const int rows = (wf > of ? wf : of) * g.V;
+  static const bool gen = !getenv("F3_WIN_GEN") || atoi(getenv("F3_WIN_GEN")) != 0;  // A/B (temporary)
+  if (!gen && (g.S != 1 || rows > 144 || g.M % 288)) return 0;
+  return rows <= 144 ? 144 : rows <= 270 ? 270 : 0;
 }
 
-// (a plain function: hipcc left the device stubs of the WIN instances undefined when they were
-// launched from a function template)
+template <int CL>
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
-  const int tiles = (a.g.M / 288) * (a.g.Nc / 128);
+  constexpr int CPW = CL == 144 ? 2 : 1;
+  const int nclip = a.g.M / (a.g.T_out * a.g.V);
+  const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / 128);
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
-    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_big<(E), 2, 4, true, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
+    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), 2, 4, CL, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), 2, 4, CL, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
     F3_LAUNCH_CHECK();                                                                                \
     return F3_OK;                                                                                     \
   }
@@ -557,8 +636,9 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0) return F3_OK;
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
-  if (big_win_ok(a)) {
-    const int r = launch_win(a, epi, s);
+  const int wrows = big_win_rows(a);
+  if (wrows) {
+    const int r = wrows == 144 ? launch_win<144>(a, epi, s) : launch_win<270>(a, epi, s);
     if (r != F3_EINVAL) return r;
   }
   if (a.g.Nc == 256) return a.x3n ? launch_big<1, 8, true>(a, epi, s) : launch_big<1, 8, false>(a, epi, s);
