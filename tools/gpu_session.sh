@@ -10,6 +10,8 @@
 #   step_prof_ag  the same for the reference loop body through the custom ops -> gpurun_out/step_ag_*.txt
 #   step_prof_serial  the bench step with every queue joined (F3_SERIAL=1): per-kernel alone times
 #                     -> gpurun_out/step_serial_kernels.txt
+#   kbench      tools/kbench.py over ${KB_KEYS} (tcn GEMMs alone)       -> gpurun_out/kbench.txt
+#   kpmc        SQ / LDS / MFMA counter passes of the same               -> gpurun_out/kpmc.txt
 #   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
 #   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches, one process per key in
 #               ${ROOF_KEYS:-wgrad_l5 wgrad wgrad_kernel tcn_fwd}          -> gpurun_out/roof_kernels_KEY.txt
@@ -79,6 +81,23 @@ for step in "$@"; do
       python tools/prof_summary.py gpurun_out/step_serial/run_results.db --per-step 11 --top 80 \
         > gpurun_out/step_serial_kernels.txt 2>&1
       head -25 gpurun_out/step_serial_kernels.txt ;;
+    kbench)
+      run kbench 120 python tools/kbench.py ${KB_KEYS:-l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kbench.txt 2>&1
+      cat gpurun_out/kbench.txt ;;
+    kpmc)
+      # SQ stall / LDS / MFMA counters of tools/kbench.py's kernels, one pass per set
+      i=0
+      for SET in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_WAVES SQ_INST_CYCLES_VMEM" \
+                 "FETCH_SIZE"; do
+        i=$((i + 1))
+        rm -rf gpurun_out/kpmc_$i
+        run kpmc_$i 90 rocprofv3 --pmc $SET -d gpurun_out/kpmc_$i -o run -- python tools/kbench.py \
+          ${KB_KEYS:-l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kpmc_$i.log 2>&1
+        db=$(find gpurun_out/kpmc_$i -name "*.db" | head -1)
+        python tools/pmc_kernels.py "$db" >> gpurun_out/kpmc.txt 2>&1
+      done
+      tail -40 gpurun_out/kpmc.txt ;;
     step_pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
         rm -rf gpurun_out/pmc_$C
