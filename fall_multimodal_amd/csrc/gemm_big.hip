@@ -184,67 +184,86 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (WIN != 0) {
     constexpr int CL = WIN, NPA = (CPW * CL + 7) / 8;  // window rows per clip, A pieces per window
-    const int V = g.V, P = g.P;
+    static_assert(Cfg::BP % BG_WAVES == 0 && PPW * BG_WAVES == Cfg::NP, "slots: B pieces, then A pieces");
+    const int V = g.V, P = g.P, TVin = g.T_in * V;
     // taps of window q (q = input-frame parity for the stride-2 forward, else 0): dt = d0 + ds j,
-    // j < nt, frame shift s0 + ss j
-    int d0[2] = {0, 0}, nt[2] = {1, 1}, s0[2] = {0, 0}, ds = 1, ss = 1;
+    // j < nt, frame shift s0 + ss j. (Pairs of scalars, not arrays: a runtime-indexed private array
+    // is promoted to LDS and costs a ds_read + wait per use.)
+    int d00 = 0, d01 = 0, nt0 = g.KT, nt1 = 1, s00 = 0, s01 = 0, ds = 1, ss = 1;
     if (wmode == 0) {
-      d0[0] = 0; nt[0] = g.KT; ss = g.transposed ? -1 : 1; s0[0] = -ss * P;
+      ss = g.transposed ? -1 : 1; s00 = -ss * P;
     } else {
       ds = 2;
-      for (int q = 0; q < 2; ++q) {
-        d0[q] = ((wmode == 1 ? wpar : q) + P) & 1;
-        nt[q] = (g.KT - d0[q] + 1) >> 1;
-      }
+      d00 = ((wmode == 1 ? wpar : 0) + P) & 1;
+      d01 = (1 + P) & 1;
+      nt0 = (g.KT - d00 + 1) >> 1;
+      nt1 = (g.KT - d01 + 1) >> 1;
       ss = wmode == 1 ? -1 : 1;
-      s0[0] = wmode == 1 ? (wpar + P - d0[0]) >> 1 : (d0[0] - P) >> 1;
-      s0[1] = (d0[1] - P - 1) >> 1;
+      s00 = wmode == 1 ? (wpar + P - d00) >> 1 : (d00 - P) >> 1;
+      s01 = (d01 - P - 1) >> 1;
     }
-    const int NQ = wmode == 2 ? 2 : 1;            // windows per chunk
-    const int KTC = wmode == 2 ? g.KT : nt[0];    // steps per chunk
-    const int nstep = KTC * kpt, nwin = NQ * kpt;
-    auto decode = [&](int u, int& c, int& q, int& j) {
-      c = u / KTC;
-      j = u - c * KTC;
-      q = (NQ == 2 && j >= nt[0]) ? 1 : 0;
-      if (q) j -= nt[0];
+    const int NQ = wmode == 2 ? 2 : 1;  // windows per chunk
+    const int nstep = (wmode == 2 ? g.KT : nt0) * kpt;
+    // per window parity: A pieces per carrying step (nt - 1 steps carry a window), valid window rows
+    const int aps0 = (NPA + nt0 - 2) / (nt0 - 1), aps1 = (NPA + nt1 - 2) / max(nt1 - 1, 1);
+    const int wlim0 = (NQ == 2 ? (g.T_in + 1) >> 1 : g.T_in) * V, wlim1 = (g.T_in >> 1) * V;
+    const unsigned minv = (65536u + V - 1) / V;  // l / V as (l * minv) >> 16 (l < 2^9, V < 2^7)
+    auto ntq = [&](int q) { return q ? nt1 : nt0; };
+    // (chunk c, window q, tap j) of a step, advanced without divisions
+    auto advance = [&](int& c, int& q, int& j) {
+      if (++j == ntq(q)) {
+        j = 0;
+        if (NQ == 2 && q == 0) { q = 1; } else { q = 0; ++c; }
+      }
     };
-    auto ntw = [&](int w) { return nt[NQ == 2 ? (w & 1) : 0]; };
-    // source of A piece pa (8 window rows) of window w: clip row l of clip clip0 + k -> input frame
-    auto asrc = [&](int w, int pa) -> const void* {
-      const int R = pa * 8 + sub, k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL;
-      const int f = l / V, v = l - f * V, fi = NQ == 2 ? 2 * f + (w & 1) : f, clip = clip0 + k;
-      if (l >= CL || fi >= g.T_in || clip >= nclip) return a.zero;
-      return in + (size_t)((clip * g.T_in + fi) * V + v) * g.lda + acolx((w / NQ) * CB, swz(R, pch));
+    // source of A piece pa (8 window rows) of window (c, q): clip row l of clip clip0 + k
+    auto asrc = [&](int c, int q, int pa) -> const void* {
+      const int R = pa * 8 + sub, k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL, clip = clip0 + k;
+      if (l >= (q ? wlim1 : wlim0) || clip >= nclip) return a.zero;
+      int row = clip * TVin + l;
+      if (NQ == 2) row += (int)(((unsigned)l * minv) >> 16) * V + q * V;  // input frame 2 f + q
+      return in + (size_t)row * g.lda + acolx(c * CB, swz(R, pch));
     };
-    // Step u = (chunk c, window q, tap j). Per step every wave issues PPW DMAs: its B pieces of the
-    // step's weight stage, then A pieces of the next window — step j >= 2 of window w carries
-    // window w + 1's, step 0 of window w the last group of its own (the buffer a window fills was
-    // last read by window w - 1, and a step is issued two steps ahead: steps 2 .. nt(w) of window
-    // w's range are the ones that can) — and a sink DMA of the zero row in slots left idle.
-    auto stage_w = [&](int u, int buf) {
-      int c, q, j;
-      decode(u, c, q, j);
-      const int w = c * NQ + q, k0 = wcol(d0[q] + ds * j, c * CB);
+    // the lane's B piece offsets (slots i < BP / 8; the A slots follow)
+    size_t boffw[Cfg::BP / BG_WAVES];
+#pragma unroll
+    for (int i = 0; i < Cfg::BP / BG_WAVES; ++i) {
+      const int r = (wave + BG_WAVES * i) * 8 + sub;
+      boffw[i] = (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
+    }
+    // Per step every wave issues PPW DMAs: its B pieces of the step's weight stage, then A pieces of
+    // the next window — step j >= 2 of window w carries window w + 1's, step 0 of window w the last
+    // group of its own (the buffer a window fills was last read by window w - 1, and a step is issued
+    // two steps ahead: steps 2 .. nt(w) of window w's range are the ones that can) — and a sink DMA
+    // of the zero row in slots left idle.
+    auto stage_w = [&](int c, int q, int j, int buf) {
+      const int k0 = wcol((q ? d01 : d00) + ds * j, c * CB);
       char* sbase = smem + Cfg::SOFF + buf * STAGE;
-      int tw = -1, kk = 0, ncar = 1;
-      if (j >= 2) { tw = w + 1; kk = j - 2; ncar = ntw(w) - 1; }
-      else if (j == 0 && w > 0) { tw = w; ncar = ntw(w - 1) - 1; kk = ncar - 1; }
-      if (tw >= nwin) tw = -1;
-      const int aps = (NPA + ncar - 1) / ncar;
+      bool car = false;
+      int tc = c, tq = q, kk = 0, na = 0;
+      if (j >= 2) {
+        car = true; kk = j - 2; na = q ? aps1 : aps0;
+        if (NQ == 2 && q == 0) tq = 1; else { tq = 0; tc = c + 1; }
+      } else if (j == 0 && (c > 0 || q > 0)) {
+        const int qp = NQ == 2 ? 1 - q : 0;
+        car = true; kk = ntq(qp) - 2; na = qp ? aps1 : aps0;
+      }
+      car = car && tc < kpt;
+      char* wdst = smem + ((tc * NQ + tq) & 1) * Cfg::AWIN;
 #pragma unroll
       for (int i = 0; i < PPW; ++i) {
-        const int qs = wave + BG_WAVES * i;
-        const void* src = a.zero;
-        char* dst = smem + Cfg::DOFF;
-        if (qs < Cfg::BP) {
-          src = wb + (size_t)(n0 + qs * 8 + sub) * Ktot + k0 + swz(qs * 8 + sub, pch) * 8;
-          dst = sbase + qs * 1024;
-        } else if (tw >= 0) {
-          const int sl = qs - Cfg::BP, pa = kk * aps + sl;
-          if (sl < aps && pa < NPA) {
-            src = asrc(tw, pa);
-            dst = smem + (tw & 1) * Cfg::AWIN + pa * 1024;
+        const void* src;
+        char* dst;
+        if (i < Cfg::BP / BG_WAVES) {
+          src = wb + boffw[i] + k0;
+          dst = sbase + (wave + BG_WAVES * i) * 1024;
+        } else {
+          const int sl = wave + BG_WAVES * i - Cfg::BP, pa = kk * na + sl;
+          src = a.zero;
+          dst = smem + Cfg::DOFF;
+          if (car && sl < na && pa < NPA) {
+            src = asrc(tc, tq, pa);
+            dst = wdst + pa * 1024;
           }
         }
         __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
@@ -255,11 +274,16 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A0W; ++i) {
       const int pa = (wave + BG_WAVES * i) % NPA;
-      const void* src = asrc(0, pa);
+      const void* src = asrc(0, 0, pa);
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
-    stage_w(0, 0);
-    if (nstep > 1) stage_w(1, 1);
+    int sc = 0, sq = 0, sj = 0;  // the step staged next
+    stage_w(sc, sq, sj, 0);
+    advance(sc, sq, sj);
+    if (nstep > 1) {
+      stage_w(sc, sq, sj, 1);
+      advance(sc, sq, sj);
+    }
     if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
     if (nstep > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -269,33 +293,45 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     // fragment reads as inline asm: hipcc otherwise issues each ds_read_b128 just before the MFMA
     // that consumes it with its own lgkmcnt(0), exposing the LDS latency ~14 times per step. Both
     // k halves' 22 reads are issued at once; each half is released by a counted wait whose asm
-    // also passes the fragments through (nothing can use them earlier). Out-of-clip tap rows read
-    // a zero row instead of being masked.
+    // also passes the fragments through (nothing can use them earlier). A fragment rows: the
+    // lane's row of tile x is t + 16 x (t = first row + tap shift); swz(r, c) = c ^ (r & 7) is the
+    // same for every x, so one base per k half plus an immediate 2 KiB x stride addresses them all,
+    // and a row outside the clip reads the zero row (its address minus that stride).
     typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
-    const unsigned zaddr = lds0 + Cfg::ZOFF + fg * 16;
+    const unsigned zrow = lds0 + Cfg::ZOFF;
+    unsigned boffr[2][BG_NT];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        const int r = wn * 32 + y * 16 + fr;
+        boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
+      }
+    int c = 0, q = 0, j = 0;  // the step computed
     for (int u = 0; u < nstep; ++u) {
-      int c, q, j;
-      decode(u, c, q, j);
-      const int sh = (s0[q] + ss * j) * V;  // row shift of this tap inside the clip
-      if (u + 2 < nstep) stage_w(u + 2, (u + 2) % 3);
-      const unsigned sa = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN;
-      const unsigned sb = lds0 + Cfg::SOFF + (u % 3) * STAGE;
+      const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
+      if (u + 2 < nstep) {
+        stage_w(sc, sq, sj, (u + 2) % 3);
+        advance(sc, sq, sj);
+      }
+      const unsigned rb = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN + (unsigned)(cbase + t) * 128;
+      const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
+      const unsigned soff = (u % 3) * STAGE;
       u32x4_t f[2][BG_NT + BG_MT];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int cc = ks * 4 + fg;
 #pragma unroll
-        for (int y = 0; y < BG_NT; ++y) {
-          const int r = wn * 32 + y * 16 + fr;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(sb + r * 128 + swz(r, cc) * 16));
-        }
-#pragma unroll
-        for (int x = 0; x < BG_MT; ++x) {
-          const int rs = lo0 + x * 16 + fr + sh, r = cbase + rs;
-          const unsigned ad = (rs >= 0 && rs < CL) ? sa + r * 128 + swz(r, cc) * 16 : zaddr;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][BG_NT + x]) : "v"(ad));
-        }
+        for (int y = 0; y < BG_NT; ++y)
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(boffr[ks][y] + soff));
+        static_assert(BG_MT == 9, "F3_AREAD list");
+#define F3_AREAD(X)                                                                                        \
+  {                                                                                                        \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X);  \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ad), "n"(2048 * (X))); \
+  }
+        F3_AREAD(0) F3_AREAD(1) F3_AREAD(2) F3_AREAD(3) F3_AREAD(4) F3_AREAD(5) F3_AREAD(6) F3_AREAD(7) F3_AREAD(8)
+#undef F3_AREAD
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -324,6 +360,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       if (u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      advance(c, q, j);
     }
   } else {
     if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)

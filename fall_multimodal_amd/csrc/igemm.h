@@ -27,7 +27,11 @@ F3_DEV int g_src_row(int n, int t, int v, int dt, const ConvGeom& g) {
   return (n * g.T_in + ti) * g.V + v;
 }
 
-F3_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+// 16-B chunk c of a 128-B LDS row r sits at position c ^ (r & 7): conflict-free ds_read_b128 fragment
+// reads (16 consecutive rows x one chunk per half-wave group) at ANY first row, so tap-shifted window
+// reads cost no bank conflicts (the former c ^ ((r >> 1) & 7) was conflict-free only at even 16-row
+// offsets: 26 % of the window kernels' LDS cycles were conflicts)
+F3_DEV int swz(int r, int c) { return c ^ (r & 7); }
 
 // A operand column of K index k (ConvGemmArgs::kwrap: the third segment of a bf16x3 row re-reads the
 // hi segment; 64-column chunks never straddle the boundary since kwrap % 64 == 0)
