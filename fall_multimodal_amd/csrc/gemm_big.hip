@@ -39,19 +39,26 @@ constexpr int BG_WAVES = 8, BG_THREADS = 64 * BG_WAVES;
 //   stride-2 forward: two windows per chunk, the even and the odd input frames; window q serves
 //     the taps dt = P + q (mod 2), shifted by (dt - P - q) / 2.
 // Per workgroup and chunk that is 36 KiB of A fill plus 16 KiB per tap instead of 52 KiB per tap.
+// WIN = 540 (the 64-channel layers at T = 30): one clip of up to 540 rows x BN = 64 per workgroup
+// (4 x 2 waves); the two channel chunks' windows (69 KiB each) leave room for two weight stages
+// only, so steps are issued one ahead instead of two.
 typedef __attribute__((address_space(3))) const char lds_cchar_t;
-constexpr int WIN_APS = 16;  // DMA slots per step for the next window's A pieces (<= 12 used)
 template <int WM, int WN, int WIN = 0>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
-  static constexpr int AP = WIN ? WIN_APS : BM / 8, BP = BN / 8, NP = AP + BP;  // 1-KiB pieces per stage
+  static constexpr int CPW = WIN == 144 ? 2 : 1;                 // WIN: clips per workgroup
+  static constexpr int NPA = (CPW * WIN + 7) / 8;                // WIN: A pieces per window
+  static constexpr int NST = WIN == 540 ? 2 : BG_NST, LA = NST - 1;  // weight stages, steps issued ahead
+  // 1-KiB pieces per stage: A then B (WIN: slots for the next window's carried A pieces, <= 12 used
+  // at two steps ahead, <= 8 at one)
+  static constexpr int AP = WIN ? (WIN == 540 ? 8 : 16) : BM / 8, BP = BN / 8, NP = AP + BP;
   static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;              // pieces per wave
   static constexpr int STAGE = WIN ? BN * 128 : NP * 1024;
-  static constexpr int AWIN = WIN ? BM * 128 : 0;    // one A window buffer (WIN: two of them)
+  static constexpr int AWIN = NPA * 1024;            // one A window buffer (WIN: two of them)
   static constexpr int SOFF = 2 * AWIN;              // byte offset of the per-step stages
   // the epilogue's output image (16 KiB + BM x (BN + 8) bf16) reuses the stages' bytes
   static constexpr int OT_NEED = 16 * 1024 + BM * (BN + 8) * 2;
-  static constexpr int EPI_OFF = SOFF + BG_NST * STAGE > OT_NEED ? SOFF + BG_NST * STAGE : OT_NEED;
+  static constexpr int EPI_OFF = SOFF + NST * STAGE > OT_NEED ? SOFF + NST * STAGE : OT_NEED;
   static constexpr int ZOFF = EPI_OFF + 4 * BN * 4;  // WIN: one zero row, read for out-of-clip taps
   static constexpr int DOFF = ZOFF + 128;            // WIN: 1-KiB sink of the idle DMA slots
   static constexpr int SMEM = WIN ? DOFF + 1024 : ZOFF;
@@ -62,7 +69,9 @@ struct BigCfg {
 template <int EPI, int WM, int WN, int WIN = 0, bool X3N = false>
 __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
-  static_assert(WIN == 0 || ((WIN == 144 || WIN == 270) && WM == 2 && WN == 4 && BG_MT * 16 == 144), "WIN layout");
+  static_assert(WIN == 0 || ((WIN == 144 || WIN == 270) && WM == 2 && WN == 4) || (WIN == 540 && WM == 4 && WN == 2),
+                "WIN layout");
+  static_assert(BG_MT * 16 == 144, "a wave owns 144 rows");
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
   static_assert(WM * WN == BG_WAVES, "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
@@ -79,7 +88,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   int tile = xcd_remap(blockIdx.x, gridDim.x);
   // WIN: first output channel (Nc / BN column tiles, neighbours share rows), output-frame parity of a
   // stride-2 input gradient, first clip; the row map (0 stride 1, 1 stride-2 dgrad, 2 stride-2 fwd)
-  constexpr int CPW = WIN == 144 ? 2 : 1;  // clips per workgroup
+  constexpr int CPW = Cfg::CPW, LA = Cfg::LA;  // clips per workgroup, steps issued ahead
   int n0 = 0, wpar = 0, clip0 = 0;
   const int wmode = g.S == 1 ? 0 : (g.transposed ? 1 : 2);
   const int nclip = WIN ? g.M / (g.T_out * g.V) : 0;
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 #pragma unroll
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (WIN != 0) {
-    constexpr int CL = WIN, NPA = (CPW * CL + 7) / 8;  // window rows per clip, A pieces per window
+    constexpr int CL = WIN, NPA = Cfg::NPA;  // window rows per clip, A pieces per window
     static_assert(Cfg::BP % BG_WAVES == 0 && PPW * BG_WAVES == Cfg::NP, "slots: B pieces, then A pieces");
     const int V = g.V, P = g.P, TVin = g.T_in * V;
     // taps of window q (q = input-frame parity for the stride-2 forward, else 0): dt = d0 + ds j,
@@ -204,8 +213,9 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     }
     const int NQ = wmode == 2 ? 2 : 1;  // windows per chunk
     const int nstep = (wmode == 2 ? g.KT : nt0) * kpt;
-    // per window parity: A pieces per carrying step (nt - 1 steps carry a window), valid window rows
-    const int aps0 = (NPA + nt0 - 2) / (nt0 - 1), aps1 = (NPA + nt1 - 2) / max(nt1 - 1, 1);
+    // per window parity: A pieces per carrying step (nt - LA + 1 steps carry a window), valid rows
+    const int ncar0 = nt0 - LA + 1, ncar1 = max(nt1 - LA + 1, 1);
+    const int aps0 = (NPA + ncar0 - 1) / ncar0, aps1 = (NPA + ncar1 - 1) / ncar1;
     const int wlim0 = (NQ == 2 ? (g.T_in + 1) >> 1 : g.T_in) * V, wlim1 = (g.T_in >> 1) * V;
     const unsigned minv = (65536u + V - 1) / V;  // l / V as (l * minv) >> 16 (l < 2^9, V < 2^7)
     auto ntq = [&](int q) { return q ? nt1 : nt0; };
@@ -232,21 +242,21 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       boffw[i] = (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
     }
     // Per step every wave issues PPW DMAs: its B pieces of the step's weight stage, then A pieces of
-    // the next window — step j >= 2 of window w carries window w + 1's, step 0 of window w the last
+    // the next window — step j >= LA of window w carries window w + 1's, step 0 of window w the last
     // group of its own (the buffer a window fills was last read by window w - 1, and a step is issued
-    // two steps ahead: steps 2 .. nt(w) of window w's range are the ones that can) — and a sink DMA
+    // LA steps ahead: steps LA .. nt(w) of window w's range are the ones that can) — and a sink DMA
     // of the zero row in slots left idle.
     auto stage_w = [&](int c, int q, int j, int buf) {
       const int k0 = wcol((q ? d01 : d00) + ds * j, c * CB);
       char* sbase = smem + Cfg::SOFF + buf * STAGE;
       bool car = false;
       int tc = c, tq = q, kk = 0, na = 0;
-      if (j >= 2) {
-        car = true; kk = j - 2; na = q ? aps1 : aps0;
+      if (j >= LA) {
+        car = true; kk = j - LA; na = q ? aps1 : aps0;
         if (NQ == 2 && q == 0) tq = 1; else { tq = 0; tc = c + 1; }
       } else if (j == 0 && (c > 0 || q > 0)) {
         const int qp = NQ == 2 ? 1 - q : 0;
-        car = true; kk = ntq(qp) - 2; na = qp ? aps1 : aps0;
+        car = true; kk = ntq(qp) - LA; na = qp ? aps1 : aps0;
       }
       car = car && tc < kpt;
       char* wdst = smem + ((tc * NQ + tq) & 1) * Cfg::AWIN;
@@ -280,12 +290,12 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     int sc = 0, sq = 0, sj = 0;  // the step staged next
     stage_w(sc, sq, sj, 0);
     advance(sc, sq, sj);
-    if (nstep > 1) {
+    if (LA == 2 && nstep > 1) {
       stage_w(sc, sq, sj, 1);
       advance(sc, sq, sj);
     }
     if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (nstep > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
+    if (LA == 2 && nstep > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // the wave's rows: clip base row in the window and first output row of the clip
@@ -311,13 +321,13 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     int c = 0, q = 0, j = 0;  // the step computed
     for (int u = 0; u < nstep; ++u) {
       const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
-      if (u + 2 < nstep) {
-        stage_w(sc, sq, sj, (u + 2) % 3);
+      if (u + LA < nstep) {
+        stage_w(sc, sq, sj, (u + LA) % Cfg::NST);
         advance(sc, sq, sj);
       }
       const unsigned rb = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN + (unsigned)(cbase + t) * 128;
       const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
-      const unsigned soff = (u % 3) * STAGE;
+      const unsigned soff = (u % Cfg::NST) * STAGE;
       u32x4_t f[2][BG_NT + BG_MT];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
             for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
         }
       }
-      if (u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      if (LA == 2 && u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       advance(c, q, j);
@@ -591,9 +601,33 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
 
 using namespace f3;
 
+// Clip-window form (WIN): the clip rows of the window layout for a 9-tap temporal conv (stride 1
+// forward or input gradient, stride-2 forward or input gradient) whose window and output frames
+// fit 144 rows (two clips per tile) or 270 rows (one clip), else 0
+static int big_win_rows(const ConvGemmArgs& a) {
+  const ConvGeom& g = a.g;
+  const int cb = a.x3n ? 32 : G_BK;
+  if ((g.Nc % 128 && g.Nc != 64) || g.KT != 9 || 2 * g.P != g.KT - 1 || g.Kc % cb || g.T_out <= 0 || g.M % (g.T_out * g.V))
+    return 0;
+  int wf, of;  // window frames, output frames of one tile clip
+  if (g.S == 1) {
+    if (g.T_in != g.T_out) return 0;
+    wf = of = g.T_in;
+  } else if (g.S == 2) {
+    wf = g.transposed ? g.T_in : (g.T_in + 1) / 2;
+    of = g.transposed ? (g.T_out + 1) / 2 : g.T_out;
+  } else {
+    return 0;
+  }
+  const int rows = (wf > of ? wf : of) * g.V;
+  if (g.Nc == 64) return g.S == 1 && rows <= 540 ? 540 : 0;
+  return rows <= 144 ? 144 : rows <= 270 ? 270 : 0;
+}
+
 // Large tiles pay when the k loop is long enough to amortise the 3-stage prologue.
 bool f3_igemm_big_ok(const ConvGemmArgs& a) {
   if (!f3_igemm_ok(a)) return false;
+  if (a.g.Nc == 64) return big_win_rows(a) == 540;  // the window form only
   if (a.g.Nc != 128 && a.g.Nc != 256) return false;
   return a.g.KT * a.g.Kc / (a.x3n ? 32 : G_BK) >= 6;
 }
@@ -625,39 +659,17 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   return F3_EINVAL;
 }
 
-// Clip-window form (WIN): the clip rows of the window layout for a 9-tap temporal conv (stride 1
-// forward or input gradient, stride-2 forward or input gradient) whose window and output frames
-// fit 144 rows (two clips per tile) or 270 rows (one clip), else 0
-static int big_win_rows(const ConvGemmArgs& a) {
-  const ConvGeom& g = a.g;
-  const int cb = a.x3n ? 32 : G_BK;
-  if (g.Nc % 128 || g.KT != 9 || 2 * g.P != g.KT - 1 || g.Kc % cb || g.T_out <= 0 || g.M % (g.T_out * g.V))
-    return 0;
-  int wf, of;  // window frames, output frames of one tile clip
-  if (g.S == 1) {
-    if (g.T_in != g.T_out) return 0;
-    wf = of = g.T_in;
-  } else if (g.S == 2) {
-    wf = g.transposed ? g.T_in : (g.T_in + 1) / 2;
-    of = g.transposed ? (g.T_out + 1) / 2 : g.T_out;
-  } else {
-    return 0;
-  }
-  const int rows = (wf > of ? wf : of) * g.V;
-  static const bool gen = !getenv("F3_WIN_GEN") || atoi(getenv("F3_WIN_GEN")) != 0;  // A/B (temporary)
-  if (!gen && (g.S != 1 || rows > 144 || g.M % 288)) return 0;
-  return rows <= 144 ? 144 : rows <= 270 ? 270 : 0;
-}
+bool f3_igemm_big_win_ok(const ConvGemmArgs& a) { return f3_igemm_big_ok(a) && big_win_rows(a) != 0; }
 
 template <int CL>
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
-  constexpr int CPW = CL == 144 ? 2 : 1;
+  constexpr int CPW = CL == 144 ? 2 : 1, WM = CL == 540 ? 4 : 2, WN = CL == 540 ? 2 : 4;
   const int nclip = a.g.M / (a.g.T_out * a.g.V);
-  const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / 128);
+  const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / (32 * WN));
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
-    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), 2, 4, CL, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_big<(E), 2, 4, CL, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
+    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
     F3_LAUNCH_CHECK();                                                                                \
     return F3_OK;                                                                                     \
   }
@@ -675,9 +687,11 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   const int wrows = big_win_rows(a);
   if (wrows) {
-    const int r = wrows == 144 ? launch_win<144>(a, epi, s) : launch_win<270>(a, epi, s);
+    const int r = wrows == 144 ? launch_win<144>(a, epi, s)
+                  : wrows == 270 ? launch_win<270>(a, epi, s) : launch_win<540>(a, epi, s);
     if (r != F3_EINVAL) return r;
   }
+  if (a.g.Nc == 64) return F3_EINVAL;
   if (a.g.Nc == 256) return a.x3n ? launch_big<1, 8, true>(a, epi, s) : launch_big<1, 8, false>(a, epi, s);
   return a.x3n ? launch_big<2, 4, true>(a, epi, s) : launch_big<2, 4, false>(a, epi, s);
 }

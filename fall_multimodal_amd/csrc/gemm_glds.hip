@@ -454,6 +454,12 @@ int f3_igemm_bf16(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (!f3_igemm_ok(a)) return F3_EINVAL;
   if (f3_tcn64_ok(a, epi)) return f3_tcn64(args, epi, s);
   if (f3_pw_ok(a, epi)) return f3_pw_gemm(args, epi, s);
+  // the clip-window form of igemm_big where it applies (whole clips per workgroup: 9-tap convs of
+  // 64 channels at T*V <= 540, of 128 / 256 channels at T*V <= 270)
+  if (f3_igemm_big_win_ok(a)) {
+    const int r = f3_igemm_big(args, epi, s);
+    if (r != F3_EINVAL) return r;
+  }
   // two LDS stages (three measured slower for both the windows and the tiles)
   if (igemm_win_ok(a, epi)) {
     if (a.x3n) return a.g.Nc == 128 ? launch_igemm<4, 2, true, true>(a, epi, s) : launch_igemm<2, 2, true, true>(a, epi, s);

@@ -130,6 +130,7 @@ int f3_tcn64(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_pw_ok(const f3::ConvGemmArgs& a, int epi);
 int f3_pw_gemm(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_igemm_big_ok(const f3::ConvGemmArgs& a);
+bool f3_igemm_big_win_ok(const f3::ConvGemmArgs& a);  // the clip-window form applies
 int f3_igemm_big(const f3::ConvGemmArgs* a, int epi, hipStream_t s);
 bool f3_wgrad_glds_ok(const f3::WgradArgs& a);
 int f3_wgrad_glds_bf16(const f3::WgradArgs* a, hipStream_t s);

@@ -151,7 +151,12 @@ def test_conv_backward_kernels_match_torch(shape, precision):
 
 X3CAT_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4, 15, 14, 256, 256, 9, 2, 4),
                 (2, 15, 14, 128, 256, 1, 2, 0), (4, 8, 18, 256, 256, 9, 1, 4), (2, 30, 18, 64, 192, 1, 1, 0),
-                (3, 30, 18, 192, 64, 1, 1, 0), (3, 15, 18, 256, 256, 9, 2, 4), (2, 29, 18, 128, 128, 9, 1, 4)]
+                (3, 30, 18, 192, 64, 1, 1, 0), (3, 15, 18, 256, 256, 9, 2, 4), (2, 29, 18, 128, 128, 9, 1, 4),
+                # the clip-window classes of igemm_big at the step's V = 18: 64 channels at T = 30 / 29
+                # (540-row clips), 128 channels at T = 15 (270) and the stride-2 30 / 29 -> 15 layer
+                # (forward by input-frame parity, input gradient by output-frame parity)
+                (3, 30, 18, 64, 64, 9, 1, 4), (2, 29, 18, 64, 64, 9, 1, 4), (3, 15, 18, 128, 128, 9, 1, 4),
+                (3, 30, 18, 128, 128, 9, 2, 4), (3, 29, 18, 128, 128, 9, 2, 4)]
 
 
 @pytest.mark.parametrize("shape", X3CAT_SHAPES)

@@ -82,7 +82,7 @@ for step in "$@"; do
         > gpurun_out/step_serial_kernels.txt 2>&1
       head -25 gpurun_out/step_serial_kernels.txt ;;
     kbench)
-      run kbench 120 python tools/kbench.py ${KB_KEYS:-l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kbench.txt 2>&1
+      run kbench 120 python tools/kbench.py ${KB_KEYS:-l1f l1d l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kbench.txt 2>&1
       cat gpurun_out/kbench.txt ;;
     kpmc)
       # SQ stall / LDS / MFMA counters of tools/kbench.py's kernels, one pass per set
@@ -93,7 +93,7 @@ for step in "$@"; do
         i=$((i + 1))
         rm -rf gpurun_out/kpmc_$i
         run kpmc_$i 90 rocprofv3 --pmc $SET -d gpurun_out/kpmc_$i -o run -- python tools/kbench.py \
-          ${KB_KEYS:-l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kpmc_$i.log 2>&1
+          ${KB_KEYS:-l1f l1d l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kpmc_$i.log 2>&1
         db=$(find gpurun_out/kpmc_$i -name "*.db" | head -1)
         python tools/pmc_kernels.py "$db" >> gpurun_out/kpmc.txt 2>&1
       done

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Time the bf16x3 tcn implicit GEMMs of the step alone (B=256, V=18), one shape per key:
 
-    python tools/kbench.py KEY [KEY ...]      keys: l4 l5 l7 l8 (layer), suffix f (forward) / d (dgrad)
+    python tools/kbench.py KEY [KEY ...]      keys: l1 l4 l5 l7 l8 (layer), suffix f (forward) / d (dgrad)
 
+    l1: 64 ch, T 30, stride 1
     l4: 128 ch, T 30 -> 15, stride 2    l5: 128 ch, T 15, stride 1
     l7: 256 ch, T 15 -> 8, stride 2     l8: 256 ch, T 8, stride 1
 
@@ -18,7 +19,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SHAPES = {"l4": (30, 128, 2), "l5": (15, 128, 1), "l7": (15, 256, 2), "l8": (8, 256, 1)}
+SHAPES = {"l1": (30, 64, 1), "l4": (30, 128, 2), "l5": (15, 128, 1), "l7": (15, 256, 2), "l8": (8, 256, 1)}
 
 
 def main():
