@@ -20,6 +20,12 @@
 // Row maps, the stride-2 parity split and the epilogues are those of igemm_bf16.
 #include "igemm.h"
 
+// F3_PROBE (tools/probe_build.sh only; 0 in the library): bit 1 drops the window loop's MFMAs, bit 2
+// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone
+#ifndef F3_PROBE
+#define F3_PROBE 0
+#endif
+
 namespace f3 {
 
 constexpr int BG_MT = 9, BG_NT = 2, BG_NST = 3;  // per-wave MFMA tiles (rows x cols), LDS stages
@@ -318,60 +324,93 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         const int r = wn * 32 + y * 16 + fr;
         boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
       }
-    int c = 0, q = 0, j = 0;  // the step computed
-    for (int u = 0; u < nstep; ++u) {
+    // Software pipeline over the k steps. A step's fragments are its hi half (chunks fg: x3n the hi
+    // operands, bf16 the first 32 k) and lo half (chunks 4 + fg); step u runs
+    //   G1: the hi-only products (18 MFMAs)        while lo(u) lands
+    //   wait lo(u) and stage u + 1; barrier
+    //   issue hi(u + 1) reads
+    //   G2: the products that need lo (36 / 18)    while hi(u + 1) lands
+    //   issue lo(u + 1) reads
+    // so the LDS reads of a step overlap the MFMAs of the one before instead of stalling every wave
+    // after each barrier (measured: the read phase alone cost ~1.5k cycles per step). hi is
+    // double-buffered across steps (the loop is unrolled by two), lo is rewritten after G2 issues.
+    constexpr int NF = BG_NT + BG_MT;
+    auto read_half = [&](u32x4_t (&fh)[NF], int hs, int c, int q, int j, int u) {
       const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
+      const unsigned rb = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN + (unsigned)(cbase + t) * 128;
+      const unsigned ab = rb + (((hs * 4 + fg) ^ (t & 7)) << 4);
+      const unsigned soff = (u % Cfg::NST) * STAGE;
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        if (F3_PROBE & 4) { fh[y] = u32x4_t{0u, 0u, 0u, 0u}; continue; }
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fh[y]) : "v"(boffr[hs][y] + soff));
+      }
+      static_assert(BG_MT == 9, "F3_AREAD list");
+#define F3_AREAD(X)                                                                                        \
+  if (F3_PROBE & 4) fh[BG_NT + (X)] = u32x4_t{0u, 0u, 0u, 0u};                                            \
+  else {                                                                                                   \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? ab : zrow - 2048u * (X);                \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fh[BG_NT + (X)]) : "v"(ad), "n"(2048 * (X)));    \
+  }
+      F3_AREAD(0) F3_AREAD(1) F3_AREAD(2) F3_AREAD(3) F3_AREAD(4) F3_AREAD(5) F3_AREAD(6) F3_AREAD(7) F3_AREAD(8)
+#undef F3_AREAD
+    };
+    auto mfma = [&](const u32x4_t& fa, const u32x4_t& fb, f32x4& d) {
+      if (F3_PROBE & 1) {  // probe build: fragments consumed, no MFMA
+        asm volatile("" : "+v"(d) : "v"(fa), "v"(fb));
+        return;
+      }
+      d = mfma_bf16x(__builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb), d);
+    };
+    u32x4_t hA[NF], hB[NF], lo[NF];
+    int c = 0, q = 0, j = 0;  // the step computed
+    auto step = [&](u32x4_t (&hc)[NF], u32x4_t (&hn)[NF], int u) {
       if (u + LA < nstep) {
-        stage_w(sc, sq, sj, (u + LA) % Cfg::NST);
+        if (!(F3_PROBE & 2)) stage_w(sc, sq, sj, (u + LA) % Cfg::NST);
         advance(sc, sq, sj);
       }
-      const unsigned rb = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN + (unsigned)(cbase + t) * 128;
-      const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
-      const unsigned soff = (u % Cfg::NST) * STAGE;
-      u32x4_t f[2][BG_NT + BG_MT];
+      // G1 (hi(u) was waited for: lgkmcnt(NF) leaves only lo(u)'s reads outstanding)
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NF) : "memory");
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int k = 0; k < NF; ++k) asm volatile("" : "+v"(hc[k]));
 #pragma unroll
-        for (int y = 0; y < BG_NT; ++y)
-          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(boffr[ks][y] + soff));
-        static_assert(BG_MT == 9, "F3_AREAD list");
-#define F3_AREAD(X)                                                                                        \
-  {                                                                                                        \
-    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X);  \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ad), "n"(2048 * (X))); \
-  }
-        F3_AREAD(0) F3_AREAD(1) F3_AREAD(2) F3_AREAD(3) F3_AREAD(4) F3_AREAD(5) F3_AREAD(6) F3_AREAD(7) F3_AREAD(8)
-#undef F3_AREAD
-      }
+      for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int y = 0; y < BG_NT; ++y) mfma(hc[BG_NT + x], hc[y], acc[x][y]);
 #pragma unroll
-        for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
+      for (int x = 0; x < BG_MT; ++x)  // pin G1 above the waits (hipcc sinks MFMAs below them)
 #pragma unroll
-        for (int x = 0; x < BG_MT; ++x)
+        for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y) {
-            // X3N: half 0 = the hi fragments (x_hi W_hi), half 1 = the lo ones (x_lo W_hi + x_hi W_lo)
-            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]),
-                                   __builtin_bit_cast(bf16x8, f[X3N ? 0 : ks][y]), acc[x][y]);
-            if (X3N && ks == 1)
-              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
-                                     acc[x][y]);
-          }
-        if (ks == 0) {  // pin the first half's MFMAs above the second wait (hipcc sinks them below it)
-#pragma unroll
-          for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-            for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
-        }
-      }
+      for (int k = 0; k < NF; ++k) asm volatile("" : "+v"(lo[k]));
       if (LA == 2 && u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       advance(c, q, j);
+      const bool more = u + 1 < nstep;
+      if (more) read_half(hn, 0, c, q, j, u + 1);
+      // G2: x3n x_lo W_hi + x_hi W_lo; bf16 the second 32 k
+#pragma unroll
+      for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) {
+          if (X3N) {
+            mfma(lo[BG_NT + x], hc[y], acc[x][y]);
+            mfma(hc[BG_NT + x], lo[y], acc[x][y]);
+          } else {
+            mfma(lo[BG_NT + x], lo[y], acc[x][y]);
+          }
+        }
+      if (more) read_half(lo, 1, c, q, j, u + 1);
+    };
+    read_half(hA, 0, 0, 0, 0, 0);
+    read_half(lo, 1, 0, 0, 0, 0);
+    for (int u = 0; u < nstep; u += 2) {
+      step(hA, hB, u);
+      if (u + 1 < nstep) step(hB, hA, u + 1);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else {
     if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
       if (EPI & EPI_ADD) return;
