@@ -21,7 +21,11 @@
 #include "igemm.h"
 
 // F3_PROBE (tools/probe_build.sh only; 0 in the library): bit 1 drops the window loop's MFMAs, bit 2
-// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone
+// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone. (Measured
+// on l8d with this loop: 126 us full, 77 without MFMA, 55 without MFMA and DMA: the legs add up almost
+// linearly. A software-pipelined loop (next step's hi fragments read under the current step's lo
+// products) and a ping-pong of the SIMD partner waves (one loads while the other multiplies) were
+// both 2-5 % SLOWER: the loading leg is instruction-issue bound, not latency bound.)
 #ifndef F3_PROBE
 #define F3_PROBE 0
 #endif
@@ -324,90 +328,66 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
         const int r = wn * 32 + y * 16 + fr;
         boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
       }
-    // Ping-pong over the k steps: the two waves that share a SIMD (wave w and w + 4) alternate roles
-    // every segment (one segment = one s_barrier interval). In segment 2u waves 0-3 LOAD step u (its
-    // LDS fragments, plus their DMAs of stage u + LA) while waves 4-7 COMPUTE step u - 1 (its 54 / 36
-    // MFMAs from registers); in segment 2u + 1 the roles swap. So each SIMD's matrix pipe runs one
-    // wave's MFMAs while its partner's LDS reads, address math and DMA issue go on beside them
-    // (MI355X_MICROARCH.md "two waves per SIMD"), instead of both waves reading, then both
-    // multiplying (measured: reads, DMA and MFMA cost nearly additively in that form).
-    // Ordering: stage v's DMAs are issued by waves 0-3 in segment 2(v - LA) and by waves 4-7 in
-    // 2(v - LA) + 1; a loading wave ends its segment with a counted vmcnt that leaves only the stage
-    // it just issued in flight, so stage v is complete everywhere (after the barrier) before segment
-    // 2v reads it, and stage v - NST's reads ended in segment 2(v - NST) + 1 < 2(v - LA). The
-    // A-window carry keeps its step ranges (see stage_w).
-    constexpr int NF = BG_NT + BG_MT;
-    const bool grp1 = wave >= BG_WAVES / 2;  // waves 4-7: one segment behind
-    u32x4_t f0[NF], f1[NF];                   // the step's hi / lo fragments
-    int c = 0, q = 0, j = 0;                  // the step loaded next
-    auto load = [&](int u) {
+    int c = 0, q = 0, j = 0;  // the step computed
+    for (int u = 0; u < nstep; ++u) {
+      const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
       if (u + LA < nstep) {
         if (!(F3_PROBE & 2)) stage_w(sc, sq, sj, (u + LA) % Cfg::NST);
         advance(sc, sq, sj);
       }
-      const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
       const unsigned rb = lds0 + ((c * NQ + q) & 1) * Cfg::AWIN + (unsigned)(cbase + t) * 128;
       const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
       const unsigned soff = (u % Cfg::NST) * STAGE;
+      u32x4_t f[2][BG_NT + BG_MT];
 #pragma unroll
-      for (int y = 0; y < BG_NT; ++y) {
-        if (F3_PROBE & 4) { f0[y] = f1[y] = u32x4_t{0u, 0u, 0u, 0u}; continue; }
-        asm volatile("ds_read_b128 %0, %1" : "=v"(f0[y]) : "v"(boffr[0][y] + soff));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(f1[y]) : "v"(boffr[1][y] + soff));
-      }
-      static_assert(BG_MT == 9, "F3_AREAD list");
-#define F3_AREAD(X)                                                                                        \
-  if (F3_PROBE & 4) f0[BG_NT + (X)] = f1[BG_NT + (X)] = u32x4_t{0u, 0u, 0u, 0u};                          \
-  else {                                                                                                   \
-    const bool ok = (unsigned)(t + 16 * (X)) < (unsigned)CL;                                              \
-    const unsigned a0 = ok ? ab0 : zrow - 2048u * (X), a1 = ok ? ab1 : zrow - 2048u * (X);                \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f0[BG_NT + (X)]) : "v"(a0), "n"(2048 * (X)));    \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f1[BG_NT + (X)]) : "v"(a1), "n"(2048 * (X)));    \
-  }
-      F3_AREAD(0) F3_AREAD(1) F3_AREAD(2) F3_AREAD(3) F3_AREAD(4) F3_AREAD(5) F3_AREAD(6) F3_AREAD(7) F3_AREAD(8)
-#undef F3_AREAD
-      advance(c, q, j);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int k = 0; k < NF; ++k) asm volatile("" : "+v"(f0[k]), "+v"(f1[k]));
-      if (LA == 2 && u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    auto mfma = [&](const u32x4_t& fa, const u32x4_t& fb, f32x4& d) {
-      if (F3_PROBE & 1) {  // probe build: fragments consumed, no MFMA
-        asm volatile("" : "+v"(d) : "v"(fa), "v"(fb));
-        return;
-      }
-      d = mfma_bf16x(__builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb), d);
-    };
-    auto compute = [&]() {
-#pragma unroll
-      for (int x = 0; x < BG_MT; ++x)
+      for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
         for (int y = 0; y < BG_NT; ++y) {
-          mfma(f0[BG_NT + x], f0[y], acc[x][y]);  // x3n: x_hi W_hi; bf16: the first 32 k
-          if (X3N) {
-            mfma(f1[BG_NT + x], f0[y], acc[x][y]);  // x_lo W_hi
-            mfma(f0[BG_NT + x], f1[y], acc[x][y]);  // x_hi W_lo
-          } else {
-            mfma(f1[BG_NT + x], f1[y], acc[x][y]);  // the second 32 k
-          }
+          if (F3_PROBE & 4) { f[ks][y] = u32x4_t{0u, 0u, 0u, 0u}; continue; }
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(boffr[ks][y] + soff));
         }
-      // the fragments stay live until every MFMA has issued (the next load overwrites them)
-#pragma unroll
-      for (int k = 0; k < NF; ++k) asm volatile("" : "+v"(f0[k]), "+v"(f1[k]));
-    };
-    for (int u = 0; u <= nstep; ++u) {
-      // segment 2u: waves 0-3 load step u, waves 4-7 compute step u - 1
-      if (!grp1) { if (u < nstep) load(u); }
-      else if (u > 0) compute();
-      __builtin_amdgcn_s_barrier();
-      // segment 2u + 1: waves 0-3 compute step u, waves 4-7 load step u
-      if (u < nstep) {
-        if (!grp1) compute();
-        else load(u);
-        __builtin_amdgcn_s_barrier();
+        static_assert(BG_MT == 9, "F3_AREAD list");
+#define F3_AREAD(X)                                                                                        \
+  if (F3_PROBE & 4) f[ks][BG_NT + (X)] = u32x4_t{0u, 0u, 0u, 0u};                                         \
+  else {                                                                                                   \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X);  \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ad), "n"(2048 * (X))); \
+  }
+        F3_AREAD(0) F3_AREAD(1) F3_AREAD(2) F3_AREAD(3) F3_AREAD(4) F3_AREAD(5) F3_AREAD(6) F3_AREAD(7) F3_AREAD(8)
+#undef F3_AREAD
       }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
+#pragma unroll
+        for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) {
+            if (F3_PROBE & 1) {  // probe build: fragments consumed, no MFMA
+              asm volatile("" : "+v"(acc[x][y]) : "v"(f[ks][BG_NT + x]), "v"(f[ks][y]));
+              continue;
+            }
+            // X3N: half 0 = the hi fragments (x_hi W_hi), half 1 = the lo ones (x_lo W_hi + x_hi W_lo)
+            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]),
+                                   __builtin_bit_cast(bf16x8, f[X3N ? 0 : ks][y]), acc[x][y]);
+            if (X3N && ks == 1)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
+                                     acc[x][y]);
+          }
+        if (ks == 0) {  // pin the first half's MFMAs above the second wait (hipcc sinks them below it)
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+        }
+      }
+      if (LA == 2 && u + 2 < nstep) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      advance(c, q, j);
     }
   } else {
     if (nchunk == 0) {  // parity class without taps (1x1 stride-2 input gradient, odd rows)
