@@ -1005,8 +1005,12 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
 // stores), summed by wgrad_slab_reduce_kernel. One workgroup per CU (118 KiB of LDS), two stages.
 // Needs: bf16 operands, forward geometry with S = 1, KT = 9, P = 4, T_in = T_out, V even,
 // T*V % 8 == 0, roundup(T*V, 32) == 32*NKS, Nc % 64 == 0, Kc % 64 == 0.
+// CH (frame chunks, the 64-channel layers at T = 30 / 29, whose 540-row clips do not fit two
+// stages): the unit of work is a chunk of F = a.taps_f frames of a clip (F*V <= 32*NKS rows of dY)
+// with its input rows from 4 frames before to 4 frames after — halo rows are real rows there,
+// staged every unit (the zero page outside the clip), and dY rows past the chunk stage as zeros.
 // ----------------------------------------------------------------------------
-template <int NKS>
+template <int NKS, bool CH = false>
 __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   constexpr int R = 128;                    // row bytes of both tiles (64 bf16)
   constexpr int TVP = 32 * NKS;             // padded clip rows
@@ -1022,18 +1026,23 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const int j0 = (tile % jt) * 64, i0 = (tile / jt) * 64;
   // bf16x3 row segments (x3seg, as wgrad_big): (dY_hi, X_hi), (dY_lo, X_hi), (dY_hi, X_lo)
   const int seg = a.x3seg ? bz % 3 : 0;
-  const int n_begin = (a.x3seg ? bz / 3 : bz) * a.rows_per_split;  // clips per split
-  const int n_end = min(g.M / TV, n_begin + a.rows_per_split);
+  // units: whole clips, or (CH) chunks of F frames, upc per clip
+  const int F = CH ? a.taps_f : g.T_out, upc = CH ? (g.T_out + F - 1) / F : 1;
+  const int n_begin = (a.x3seg ? bz / 3 : bz) * a.rows_per_split;  // units per split
+  const int n_end = min(g.M / TV * upc, n_begin + a.rows_per_split);
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
   const __bf16* xb = reinterpret_cast<const __bf16*>(a.inb) + (seg == 2 ? g.Kc : 0);
   const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
 
   // ---- staging: 1-KiB pieces (8 rows), dY pieces then input pieces; a lane's slots are fixed ----
-  const int npy = TV / 8, np = 2 * npy, ppw = (np + 7) / 8;
+  // whole clips: TV / 8 dY pieces and as many input pieces (the halo rows stay zero); CH: all TVP / 8
+  // dY pieces (rows past the chunk from the zero page) and the (F + 8) V rows of the input window
+  const int npy = CH ? TVP / 8 : TV / 8, npx = CH ? ((F + 8) * V + 7) / 8 : TV / 8;
+  const int np = npy + npx, ppw = (np + 7) / 8;
   const int sub = lane >> 3, ph = lane & 7;
-  constexpr int PPW_MAX = (2 * TVP / 8 + 7) / 8;
+  constexpr int PPW_MAX = CH ? (X_BYTES / R / 8 + TVP / 8 + 7) / 8 : (2 * TVP / 8 + 7) / 8;
   unsigned ldso[PPW_MAX];
-  long long srco[PPW_MAX];
+  int srow[PPW_MAX], scol[PPW_MAX];  // the lane's row (clip-local dY row / window-local input row), column
   bool isy[PPW_MAX];
 #pragma unroll
   for (int k = 0; k < PPW_MAX; ++k) {
@@ -1041,20 +1050,31 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
     if (piece >= np) piece %= np;  // the last round re-issues earlier pieces: same bytes, same place
     const bool y = piece < npy;
     const int pr = y ? piece : piece - npy;           // piece index within its tile
-    const int crow = pr * 8 + sub;                    // clip-local row
-    const int brow = y ? crow : 4 * V + crow;         // buffer row in its region
+    const int crow = pr * 8 + sub;                    // dY row / (CH) input window row
+    const int brow = y ? crow : (CH ? crow : 4 * V + crow);  // buffer row in its region
     const int u = (ph >> 1) ^ wswz<4>(brow);
     const int col = (u * 2 + (ph & 1)) * 8;
     isy[k] = y;
     ldso[k] = (unsigned)((y ? 0 : Y_BYTES) + brow * R + ph * 16);
-    srco[k] = y ? (long long)crow * a.ldy + j0 + col : (long long)crow * g.lda + i0 + col;
+    srow[k] = crow;
+    scol[k] = y ? j0 + col : i0 + col;
   }
   auto stage = [&](int n, int buf) {
-    const long long by = (long long)n * TV * a.ldy, bx = (long long)n * TV * g.lda;
+    // unit n: clip n / upc, frames f0 .. f0 + nf - 1 (CH); input window from frame f0 - 4
+    const int clip = n / upc, f0 = (n - clip * upc) * F, nf = min(F, g.T_out - f0);
+    const long long ybase = (long long)(clip * g.T_out + f0) * V;
+    const long long xbase = (long long)(clip * g.T_in + f0 - (CH ? 4 : 0)) * V;
 #pragma unroll
     for (int k = 0; k < PPW_MAX; ++k) {
       if (k < ppw) {
-        const __bf16* src = isy[k] ? dyb + by + srco[k] : xb + bx + srco[k];
+        const int r = srow[k];
+        bool ok = true;
+        if (CH) {
+          const int xr = (f0 - 4) * V + r;  // clip-local input row of a window row
+          ok = isy[k] ? r < nf * V : (r < (nf + 8) * V && xr >= 0 && xr < g.T_in * V);
+        }
+        const __bf16* src = !ok ? reinterpret_cast<const __bf16*>(a.zero)
+                            : isy[k] ? dyb + (ybase + r) * a.ldy + scol[k] : xb + (xbase + r) * g.lda + scol[k];
         // the DMA writes lane L's 16 B at (M0 + instruction offset) + 16 L: pass the piece base
         __builtin_amdgcn_global_load_lds((const void*)src,
                                          (lds_void_t*)(size_t)(lds0 + buf * STAGE + ldso[k] - lane * 16), 16, 0, 0);
@@ -1098,8 +1118,15 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   const int nst = n_end - n_begin;
   if (nst > 0) stage(n_begin, 0);
   // zero the rows no stage ever writes (dY padding past T*V, the input halo and tail), in both
-  // buffers, while the first clip's DMA is in flight (disjoint bytes)
-  {
+  // buffers, while the first clip's DMA is in flight (disjoint bytes); CH: only the input rows past
+  // the staged window
+  if (CH) {
+    const int xw = npx * 8;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      for (int o = Y_BYTES + xw * R + tid * 16; o < STAGE; o += 512 * 16)
+        *reinterpret_cast<f32x4*>(smem + b * STAGE + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
     const int zr[3][2] = {{TV * R, Y_BYTES}, {Y_BYTES, Y_BYTES + 4 * V * R}, {Y_BYTES + (4 * V + TV) * R, STAGE}};
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -1213,8 +1240,9 @@ __global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __r
 // products of one row range on adjacent workgroups; 10.39 -> 10.25-10.32 ms/step against
 // segment-major, profiles/r04_zimg_segminor_ab.txt)
 
-// wgrad_taps applies (see its comment); nks = padded clip rows / 32
-static int wgrad_taps_nks(const WgradArgs& a) {
+// wgrad_taps applies (see its comment); nks = padded clip (or chunk) rows / 32, +16 for the chunked
+// form, whose chunk frame count goes to a.taps_f
+static int wgrad_taps_nks(WgradArgs& a) {
   const ConvGeom& g = a.g;
   if (!a.dyb || !a.inb || !a.slab || a.outmap != WG_OUT_CONV || a.groups > 1 || g.transposed) return 0;
   if (g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out || g.V % 2 || g.V > 18) return 0;
@@ -1222,11 +1250,22 @@ static int wgrad_taps_nks(const WgradArgs& a) {
   const int TV = g.T_out * g.V;
   if (TV % 8 || g.M % TV) return 0;
   const int nks = (TV + 31) / 32;
-  return nks == 4 || nks == 5 ? nks : 0;
+  if (nks == 4 || nks == 5) return nks;
+  // frame chunks: the fewest chunks whose dY rows fit 6 k steps and whose window (F + 8 frames) fits
+  // the input region (TVP + 8 * 18 rows)
+  for (int upc = 2; upc <= 8; ++upc) {
+    const int F = (g.T_out + upc - 1) / upc, ks = (F * g.V + 31) / 32;
+    if ((ks == 5 || ks == 6) && (F + 8) * g.V <= 32 * ks + 8 * 18) {
+      a.taps_f = F;
+      return 16 + ks;
+    }
+  }
+  return 0;
 }
 
 static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
-  const int TV = a.g.T_out * a.g.V, clips = a.g.M / TV;
+  const int TV = a.g.T_out * a.g.V;
+  const int clips = a.g.M / TV * (nks > 16 ? (a.g.T_out + a.taps_f - 1) / a.taps_f : 1);  // units
   const int tiles = (a.g.Nc / 64) * (a.g.Kc / 64);
   const long long per_split = (long long)a.g.Nc * 9 * a.g.Kc;
   // one workgroup per CU, or the share wg_pct of them (side-queue launches beside the main chains)
@@ -1241,7 +1280,9 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   splits *= nseg;
   const dim3 grid(tiles * splits);
   if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
+  else if (nks == 4) hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
+  else if (nks == 21) hipLaunchKernelGGL((wgrad_taps<5, true>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_taps<6, true>), grid, dim3(512), 0, s, a);
   F3_LAUNCH_CHECK();
   if (a.dw_ref) {
     hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
@@ -1325,8 +1366,9 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   if (bigv) {
     // all 9 taps of a clip-sized stride-1 layer from one staged copy of each clip (wgrad_taps); clip
     // segments with halo rows for the other (9,1) layers measured slower (61 vs 35 us)
-    const int nks = wgrad_taps_nks(a);
-    if (nks) return launch_wgrad_taps(a, nks, s);
+    WgradArgs at = a;
+    const int nks = wgrad_taps_nks(at);
+    if (nks) return launch_wgrad_taps(at, nks, s);
   }
   if (a.x3seg && !bigv) return F3_EINVAL;  // (row segments: wgrad_taps / wgrad_big only)
   // Tile choice (layer-6 tcn weight gradient alone, B = 256, lean loop): 256 x 128 63 us,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the bf16x3 tcn implicit GEMMs of the step alone (B=256, V=18), one shape per key:
 
-    python tools/kbench.py KEY [KEY ...]      keys: l1 l4 l5 l7 l8 (layer), suffix f (forward) / d (dgrad)
+    python tools/kbench.py KEY [KEY ...]      keys: l1 l4 l5 l7 l8 (layer), suffix f (forward) / d (dgrad) / w (weight gradient)
 
     l1: 64 ch, T 30, stride 1
     l4: 128 ch, T 30 -> 15, stride 2    l5: 128 ch, T 15, stride 1
@@ -47,6 +47,13 @@ def main():
                                               st), "fwd")
             run = lambda: lib.f3_conv_forward_x3cat(L.ptr(x3), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, S,
                                                     P, st)
+        elif key[2] == "w":  # the weight gradient (three row segments + the slab reduce)
+            x3 = split(torch.randn(N, T, V, C, device=dev))
+            dy3 = split(torch.randn(N, To, V, C, device=dev))
+            dw = torch.empty(C, C, KT, device=dev)
+            db = torch.empty(C, device=dev)
+            run = lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, C, C,
+                                                            KT, S, P, st)
         else:
             dy3 = split(torch.randn(N, To, V, C, device=dev))
             dx = torch.empty(N, T, V, C, device=dev)
@@ -64,7 +71,7 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1000 / 20
-        flop = 2.0 * N * (To if key[2] == "f" else T) * V * C * C * KT / (S if key[2] == "d" else 1)
+        flop = 2.0 * N * (T if key[2] == "d" else To) * V * C * C * KT / (S if key[2] == "d" else 1)
         print(f"{key}: {us:8.1f} us/launch  {flop / us / 1e6:7.1f} TF/s algorithmic", flush=True)
 
 
