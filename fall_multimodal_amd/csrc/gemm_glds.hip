@@ -1248,11 +1248,14 @@ static int wgrad_taps_nks(WgradArgs& a) {
   if (g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out || g.V % 2 || g.V > 18) return 0;
   if (g.Nc % 64 || g.Kc % 64 || a.ldy % 8 || g.lda % 8) return 0;
   const int TV = g.T_out * g.V;
-  if (TV % 8 || g.M % TV) return 0;
+  if (g.M % TV) return 0;
   const int nks = (TV + 31) / 32;
-  if (nks == 4 || nks == 5) return nks;
+  if (TV % 8 == 0 && (nks == 4 || nks == 5)) return nks;
   // frame chunks: the fewest chunks whose dY rows fit 6 k steps and whose window (F + 8 frames) fits
-  // the input region (TVP + 8 * 18 rows)
+  // the input region (TVP + 8 * 18 rows). Only from 128 channels: on the 64-channel T = 30 layers (one
+  // 64 x 64 tile, 231 splits) the chunked kernel took 66 us + a 19-56 us reduce over 16 workgroups
+  // against wgrad_big's 63 + 10 (bf16x3, B = 256); the 128-channel T = 15 layer gains (85 vs 104 us)
+  if (g.Nc < 128) return 0;
   for (int upc = 2; upc <= 8; ++upc) {
     const int F = (g.T_out + upc - 1) / upc, ks = (F * g.V + 31) / 32;
     if ((ks == 5 || ks == 6) && (F + 8) * g.V <= 32 * ks + 8 * 18) {
