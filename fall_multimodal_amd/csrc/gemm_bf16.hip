@@ -548,7 +548,7 @@ int f3_conv_gemm_bf16(const ConvGemmArgs* args, int pro, int epi, hipStream_t s)
   const ConvGemmArgs& a = *args;
   if (a.g.M <= 0 || a.g.Nc <= 0) return F3_OK;
   if (a.inb && !pro && f3_igemm_ok(a)) return f3_igemm_bf16(args, epi, s);
-  if (a.x3n || a.kwrap) return F3_EINVAL;  // (the bf16x3 operand forms exist on the LDS-DMA kernels only)
+  if (a.x3n) return F3_EINVAL;  // (the bf16x3 operand forms exist on the LDS-DMA kernels only)
   if (pro && a.g.Kc > 256) return F3_EINVAL;
   if (!a.wb) return F3_EINVAL;
   // wide output channels: 128x128 tiles; narrow (64 / small gcn dgrad): 128x64

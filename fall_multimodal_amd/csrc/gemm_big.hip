@@ -139,7 +139,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   };
   // weight column of (tap dt, channel offset i0), A column of the lane's 16-B chunk cg
   auto wcol = [&](int dt, int i0) { return X3N ? dt * 2 * g.Kc + 2 * i0 : dt * g.Kc + i0; };
-  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : acol(a, i0) + cg * 8; };
+  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : i0 + cg * 8; };
   const unsigned short* in = a.inb;
   const unsigned short* wb = a.wb;
 

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void igemm_bf16(ConvGemmArgs a) {
   const int dt0 = par ? ((p + g.P) & 1) : 0;      // first tap of this parity
   const int nchunk = (par ? (g.KT - dt0 + 1) / 2 : g.KT) * kpt;
   auto wcol = [&](int dt, int i0) { return X3N ? dt * 2 * g.Kc + 2 * i0 : dt * g.Kc + i0; };
-  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : acol(a, i0) + cg * 8; };
+  auto acolx = [&](int i0, int cg) { return X3N ? x3n_col(g.Kc, i0, cg) : i0 + cg * 8; };
   // window mode: stage t = (chunk t / KT, tap t % KT); window row of tile row r for tap dt:
   // r + wofs(dt) with wofs = dt*V (forward) or (2P - dt)*V (input gradient)
   const int PV = g.P * g.V, WR = BM + 2 * PV;
@@ -404,9 +404,8 @@ using namespace f3;
 
 bool f3_igemm_ok(const ConvGemmArgs& a) {
   if (!a.inb || !a.wb || !a.zero || a.g.lda % 8 != 0) return false;
-  if (a.x3n) return a.kwrap == 0 && a.g.Kc % 32 == 0 && a.g.lda >= 2 * a.g.Kc;
-  return a.g.Kc % G_BK == 0 &&
-         (a.kwrap == 0 || (a.kwrap % G_BK == 0 && a.g.Kc == 3 * a.kwrap && a.g.lda >= 2 * a.kwrap));
+  if (a.x3n) return a.g.Kc % 32 == 0 && a.g.lda >= 2 * a.g.Kc;
+  return a.g.Kc % G_BK == 0;
 }
 
 // Window mode (see igemm_bf16): stride-1 temporal convs with "same" padding whose output

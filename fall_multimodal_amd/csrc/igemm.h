@@ -33,10 +33,6 @@ F3_DEV int g_src_row(int n, int t, int v, int dt, const ConvGeom& g) {
 // offsets: 26 % of the window kernels' LDS cycles were conflicts)
 F3_DEV int swz(int r, int c) { return c ^ (r & 7); }
 
-// A operand column of K index k (ConvGemmArgs::kwrap: the third segment of a bf16x3 row re-reads the
-// hi segment; 64-column chunks never straddle the boundary since kwrap % 64 == 0)
-F3_DEV int acol(const ConvGemmArgs& a, int k) { return (a.kwrap > 0 && k >= 2 * a.kwrap) ? k - 2 * a.kwrap : k; }
-
 // bf16x3 native form (ConvGemmArgs::x3n): the 16-B chunk cg (0..7) of the staged 128-B row piece of
 // channel block i0 (32 channels) comes from the hi half (cg < 4: column i0 + 8 cg) or the lo half
 // (cg >= 4: column C + i0 + 8 (cg - 4)) of a row [x_hi (C) | x_lo (C)]

@@ -44,10 +44,6 @@ struct ConvGemmArgs {
   const unsigned short* auxb;  // RELUMASK source rows stored bf16 (instead of aux)
   BnRef epi_bn;
   int x3;             // 1: split-bf16 kernel (fp32 in / out; wb = hi plane, wb + Nc*KT*Kc = lo plane)
-  // bf16x3 on the bf16 kernels (K-concatenated, Kc = 3 kwrap): the activation rows hold [x_hi | x_lo]
-  // (2 kwrap columns, lda >= 2 kwrap) and the third K segment re-reads x_hi: A column k >= 2 kwrap
-  // is read at k - 2 kwrap (igemm_bf16 / igemm_big; 0 = off)
-  int kwrap;
   // bf16x3 native form (x3n = 1, igemm_bf16 / igemm_big / pw_gemm): the activation rows hold
   // [x_hi (Kc) | x_lo (Kc)] (lda >= 2 Kc), Kc = the real channel count, and the packed weights hold,
   // per tap, 32-channel blocks [W_hi (32) | W_lo (32)] (row length KT * 2 Kc). A k step covers one

@@ -14,7 +14,7 @@ struct PrepJob {
   const float* s1;
   const float* s2;
   int d0, d1, d2;
-  int bf16;  // dst type: 0 fp32, 1 bf16, 2 bf16 hi / lo planes, 3 K-concatenated [hi | hi | lo] (bf16x3),
+  int bf16;  // dst type: 0 fp32, 1 bf16, 2 bf16 hi / lo planes,
              // 4 per-tap 32-channel blocks [hi 32 | lo 32] (bf16x3 native, ConvGemmArgs::x3n)
 };
 

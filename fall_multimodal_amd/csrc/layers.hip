@@ -21,34 +21,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // ----------------------------------------------------------------------------
 // prep: A_eff = A * E, gcn bias through the graph, weight packing  (one launch)
 // ----------------------------------------------------------------------------
-// bf16x3 on the bf16 kernels (prep code 3): every tap's k range is tripled to [W_hi | W_hi | W_lo]
-// (dst [rows][KT][3 inner]; the activation operand is [x_hi | x_lo | x_hi]), so one bf16 GEMM over
-// 3 inner computes x_hi W_hi + x_lo W_hi + x_hi W_lo. j.n counts the dst elements.
-//   PACK_CONV    src [J][I][KT]   -> dst [J][KT][3I]        (d0 J, d1 I, d2 KT)
-//   PACK_CONV_T  src [J][I][KT]   -> dst [I][KT][3J]
-//   PACK_GCN     src [K*C][Cin]   -> dst [C][3 K Cin]       (d0 C, d1 Cin, d2 K; one "tap")
-//   PACK_GCN_T   src [K*C][Cin]   -> dst [K Cin][3C]
-// One item e = one source value (j.n / 3 items), written to its three places.
-F3_DEV void prep_x3cat(const PrepJob& j, int e) {
-  const bool gcn = j.type == PREP_PACK_GCN || j.type == PREP_PACK_GCN_T;
-  const bool tr = j.type == PREP_PACK_CONV_T || j.type == PREP_PACK_GCN_T;
-  const int J = j.d0, I = j.d1, KT = gcn ? 1 : j.d2;
-  const int inner = gcn ? (tr ? J : j.d2 * I) : (tr ? J : I);  // channels per tap of the packed operand
-  const int row = e / (KT * inner), r = e - row * KT * inner, dt = r / inner, c = r - dt * inner;
-  float val;
-  if (gcn) {  // W[k*C + c][ci]: (k, ci) from the packed row (transposed) or column
-    const int kc = tr ? row : c, cc = tr ? c : row, k = kc / I, ci = kc - k * I;
-    val = j.s0[((size_t)k * J + cc) * I + ci];
-  } else {  // source weight [J][I][KT]: PACK_CONV row = output channel jj, c = input channel i
-    val = tr ? j.s0[((size_t)c * I + row) * KT + dt] : j.s0[((size_t)row * I + c) * KT + dt];
-  }
-  const __bf16 hi = (__bf16)val;
-  __bf16* d = reinterpret_cast<__bf16*>(j.dst) + ((size_t)row * KT + dt) * 3 * inner + c;
-  d[0] = hi;
-  d[inner] = hi;
-  d[2 * inner] = (__bf16)(val - (float)hi);
-}
-
 // bf16x3 native form (prep code 4, ConvGemmArgs::x3n): per tap, 32-channel blocks [W_hi (32) | W_lo (32)]
 // (dst [rows][KT][2 inner], channel c of a tap at (c / 32) * 64 + c % 32, its lo 32 further on); the
 // activation rows are [x_hi | x_lo] and the GEMM issues x_hi W_hi + x_lo W_hi + x_hi W_lo per block.
@@ -87,10 +59,6 @@ __global__ void prep_kernel(PrepLaunch L) {
   const PrepJob j = L.t.jobs[jb];
   const int nb = L.boff[jb + 1] - L.boff[jb], lb = blockIdx.x - L.boff[jb];
   const int stride = nb * blockDim.x;
-  if (j.bf16 == 3) {
-    for (int e = lb * blockDim.x + threadIdx.x; e < j.n / 3; e += stride) prep_x3cat(j, e);
-    return;
-  }
   if (j.bf16 == 4) {
     for (int e = lb * blockDim.x + threadIdx.x; e < j.n / 2; e += stride) prep_x3n(j, e);
     return;
@@ -1526,7 +1494,7 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(BnReluArgs a) {
         l[4 + e] = (__bf16)(u1 - (float)o[4 + e]);
       }
     }
-    if constexpr (X3) {  // row [hi | lo] of 2C (the K-concatenated tcn operand; kwrap re-reads hi)
+    if constexpr (X3) {  // row [hi | lo] of 2C (the bf16x3 tcn operand)
       const long long e0 = qq * 8, m = e0 / a.C, c = e0 - m * a.C;
       __bf16* row = reinterpret_cast<__bf16*>(a.u) + m * 2 * a.C + c;
       *reinterpret_cast<bf16x8*>(row) = o;
@@ -1899,7 +1867,7 @@ int f3_prep(const PrepTable& t, hipStream_t s) {
   L.t = t;
   L.boff[0] = 0;
   for (int j = 0; j < t.n; ++j) {  // ~4 items per thread, 1..2048 blocks per job
-    const long long items = t.jobs[j].bf16 == 3 ? t.jobs[j].n / 3 : t.jobs[j].bf16 == 4 ? t.jobs[j].n / 2 : t.jobs[j].n;
+    const long long items = t.jobs[j].bf16 == 4 ? t.jobs[j].n / 2 : t.jobs[j].n;
     L.boff[j + 1] = L.boff[j] + (int)std::min<long long>(2048, std::max<long long>(1, (items + 1023) / 1024));
   }
   hipLaunchKernelGGL(prep_kernel, dim3(L.boff[t.n]), dim3(256), 0, s, L);

@@ -540,23 +540,15 @@ inline int side_pct(bool split, int l) { return split && l >= 2 ? 75 : 0; }
 // backward dZ, dx, dA and dW partials in one pass): 10.14 -> 9.92 ms/step against the generic mix +
 // split GEMMs (profiles/r04_gcn0_x3_ab.txt)
 // bf16x3 GEMMs on the bf16 kernels in the native form (ConvGemmArgs::x3n, prep code 4: [x_hi | x_lo]
-// rows staged once, three MFMAs per 32-channel block) instead of the K-concatenated one (kwrap, prep
-// code 3: the third K segment re-stages x_hi). F3_X3N=0: the K-concatenated form (A/B, temporary)
-inline bool x3n_on() {
-  static const bool on = !getenv("F3_X3N") || atoi(getenv("F3_X3N")) != 0;
-  return on;
-}
-inline int x3code() { return x3n_on() ? 4 : 3; }
-// packed size (bf16 elements) of n weights in a bf16x3 code
-inline int x3mul(int code) { return code == 4 ? 2 : code == 3 ? 3 : 1; }
-// set a bf16x3 GEMM on [hi | lo] rows of C channels (lda 2C): native form, or K-concatenated (Kc 3C)
+// rows staged once, three MFMAs per 32-channel block). The round-4 K-concatenated form (Kc = 3C,
+// [W_hi | W_hi | W_lo], the third K segment re-staging x_hi) measured 8 % slower per step (9.97-10.02
+// vs 9.11-9.12 ms, profiles/r05_x3n_ab.txt) and is gone.
+constexpr int x3code() { return 4; }
+// packed size (bf16 elements) of n weights in a prep code
+inline int x3mul(int code) { return code == 4 ? 2 : 1; }
+// set a bf16x3 GEMM on [hi | lo] rows of C channels (lda 2C)
 inline void x3_gemm(ConvGemmArgs& a, int C) {
-  if (x3n_on()) {
-    a.x3n = 1;
-  } else {
-    a.g.Kc = 3 * C;
-    a.kwrap = C;
-  }
+  a.x3n = 1;
   a.g.lda = 2 * C;
 }
 
@@ -595,7 +587,7 @@ int stream_forward(const f3_net& net, int si, int N, int train, const Ptrs& q, W
     const int C = L.cout, Ci = L.cin;
     add_job(pt, PREP_MUL, K * V * V, X.aeff, q.b(S.A), q.p(L.edge), nullptr, 0, 0, 0);
     add_job(pt, PREP_GCN_BIAS, V * C, X.beff, q.b(S.A), q.p(L.edge), q.p(L.gcn_b), C, V, K);
-    // bf16x3 with the split-bf16 mix: K-concatenated gcn weights (code 3) for the bf16 kernels
+    // bf16x3 with the split-bf16 mix: native-form gcn weights (code 4) for the bf16 kernels
     const bool l0f = wc == 2 && f3_gcn0_ok(K, V, Ci, C);  // fp32 weights (layer0.hip)
     // bf16x3: the bf16 implicit-GEMM kernels' packing (native [hi 32 | lo 32] blocks, code 4)
     const int xc = wc == 2 ? x3code() : wc;

@@ -76,8 +76,7 @@ F3_DEV void pw_wait_vm(int k) {
   }
 }
 
-// F32O: fp32 output rows (a.out) instead of bf16 (the bf16x3 mode's fp32 activations), with the
-// A operand's K-concatenated [hi | lo | hi] columns through ConvGemmArgs::kwrap. X3N: the bf16x3
+// F32O: fp32 output rows (a.out) instead of bf16 (the bf16x3 mode's fp32 activations). X3N: the bf16x3
 // native form (ConvGemmArgs::x3n; the weight slices alternate hi / lo per 32-channel block, the A
 // block's 128-B chunks are [x_hi 32 | x_lo 32], three MFMAs per block), fp32 output as F32O
 template <int EPI, int KS, int WN, int BM, bool F32O = false, bool X3N = false>
@@ -158,7 +157,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gemm_kernel(ConvGemmArgs a, int
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int q = wave + 8 * i, kc = q / RGN;
-      const unsigned short* p = src ? src + (X3N ? x3n_col(g.Kc, kc * 32, cgl) : acol(a, kc * 64) + cgl * 8) : a.zero;
+      const unsigned short* p = src ? src + (X3N ? x3n_col(g.Kc, kc * 32, cgl) : kc * 64 + cgl * 8) : a.zero;
       __builtin_amdgcn_global_load_lds((const void*)p, (lds_void_t*)(dst + q * 1024), 16, 0, 0);
     }
   };
@@ -330,11 +329,6 @@ using namespace f3;
   X(EPI_BIAS, 2, 3)                                                                                   \
   X(0, 2, 3) X(0, 4, 3) X(0, 4, 6) X(0, 6, 1) X(0, 8, 3) X(0, 8, 4)                                   \
   X(EPI_ADD, 4, 1) X(EPI_ADD, 8, 2)
-// the bf16x3 mode's K-concatenated 1x1 GEMMs (K = 3 C) with fp32 output rows (F32O): the gcn input
-// gradients (K 192 / 384 / 768) and the residual forwards (the residual input gradients' 64-row A
-// blocks at K = 384 / 768 do not fit the EPI_ADD ring)
-#define F3_PW_TABLE_X3(X)                                                                             \
-  X(0, 6, 1) X(0, 12, 2) X(0, 24, 1) X(EPI_BIAS | EPI_STATS, 6, 2) X(EPI_BIAS | EPI_STATS, 12, 2)
 // the bf16x3 native form (KS = 2 Kc / 32): the gcn forwards at K Cin = 192 (KS 12, graph-mixed bias +
 // BN sums; at K Cin = 384 a 32-row A block is 48 KB and the ring would hold two), the gcn input
 // gradients (C = 64 / 128 / 256), the residual forwards and the 64-channel residual input gradient
@@ -344,14 +338,12 @@ using namespace f3;
   X(0, 4, 3) X(0, 8, 3) X(0, 16, 2) X(EPI_BIAS | EPI_STATS, 4, 2) X(EPI_BIAS | EPI_STATS, 8, 2)      \
   X(EPI_ADD, 8, 1)
 
-// mode 0: bf16, 1: bf16x3 K-concatenated (kwrap), 2: bf16x3 native (x3n)
+// mode 0: bf16, 2: bf16x3 native (x3n)
 static bool pw_has(int epi, int ks, int wn, int mode) {
 #define F3_PW_HAS(E, KSV, WNV) \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) return true;
   if (mode == 2) {
     F3_PW_TABLE_X3N(F3_PW_HAS)
-  } else if (mode == 1) {
-    F3_PW_TABLE_X3(F3_PW_HAS)
   } else {
     F3_PW_TABLE(F3_PW_HAS)
   }
@@ -359,7 +351,7 @@ static bool pw_has(int epi, int ks, int wn, int mode) {
   return false;
 }
 
-static int pw_mode(const ConvGemmArgs& a) { return a.x3n ? 2 : a.kwrap > 0 ? 1 : 0; }
+static int pw_mode(const ConvGemmArgs& a) { return a.x3n ? 2 : 0; }
 // 32-deep k slices of the weight panel (x3n: hi and lo of every 32-channel block)
 static int pw_ks(const ConvGemmArgs& a) { return (a.x3n ? 2 : 1) * a.g.Kc / 32; }
 
@@ -372,18 +364,17 @@ static int pw_wn(const ConvGemmArgs& a, int epi) {
   return 0;
 }
 
-// (the bf16x3 mode's K-concatenated 1x1 GEMMs run on this kernel too: 9.89 -> 9.84 ms/step in three
-// of three interleaved rounds against the tiled kernels, profiles/r04_pw_x3_ab.txt)
+// (the bf16x3 mode's 1x1 GEMMs run on this kernel too: 9.89 -> 9.84 ms/step in three of three
+// interleaved rounds against the tiled kernels, profiles/r04_pw_x3_ab.txt)
 
 // Shapes this kernel takes: 1x1 (KT = 1, P = 0) convs over bf16 rows with Kc in {64, 128, 192, 256}
 // and an instantiated column group; the forward at stride 1 or 2, the input gradient (transposed)
 // at stride 1 or, accumulating (EPI_ADD), stride 2.
 bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
   const ConvGeom& g = a.g;
-  // bf16x3: [hi | lo | hi] x [W_hi | W_hi | W_lo] over K = 3 kwrap, or the native form (x3n); fp32 out
-  const bool x3 = a.kwrap > 0 || a.x3n;
+  // bf16x3: the native form (x3n); fp32 out
+  const bool x3 = a.x3n;
   if (!a.inb || !a.wb || !a.zero) return false;
-  if (a.kwrap > 0 && (a.x3n || a.kwrap % 64 || g.Kc != 3 * a.kwrap || g.lda < 2 * a.kwrap)) return false;
   if (a.x3n && (g.Kc % 32 || g.lda < 2 * g.Kc)) return false;
   if (g.KT != 1 || g.P != 0 || (!a.x3n && g.Kc % 64 != 0) || g.Nc % 64 != 0 || g.lda % 8 != 0) return false;
   if (!a.x3n && g.Kc > 256 && g.Kc != 384 && g.Kc != 768) return false;
@@ -443,12 +434,6 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
     F3_LAUNCH_CHECK();                                            \
     return F3_OK;                                                 \
   }
-#define F3_PW_LAUNCH_X3(E, KSV, WNV)                                       \
-  if (epi == (E) && ks == (KSV) && wn == (WNV)) {                          \
-    pw_launch<(E), KSV, WNV, (E) != EPI_ADD>(a, grid, ncg, per_wg, s);     \
-    F3_LAUNCH_CHECK();                                                     \
-    return F3_OK;                                                          \
-  }
 #define F3_PW_LAUNCH_X3N(E, KSV, WNV)                                          \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) {                              \
     pw_launch<(E), KSV, WNV, (E) != EPI_ADD, true>(a, grid, ncg, per_wg, s);   \
@@ -457,13 +442,10 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
   }
   if (mode == 2) {
     F3_PW_TABLE_X3N(F3_PW_LAUNCH_X3N)
-  } else if (mode == 1) {
-    F3_PW_TABLE_X3(F3_PW_LAUNCH_X3)
   } else {
     F3_PW_TABLE(F3_PW_LAUNCH)
   }
 #undef F3_PW_LAUNCH_X3N
-#undef F3_PW_LAUNCH_X3
 #undef F3_PW_LAUNCH
   return F3_EINVAL;
 }

@@ -234,7 +234,7 @@ using namespace f3;
 // epilogues of the bf16 step (tcn forward, tcn input gradient).
 bool f3_tcn64_ok(const ConvGemmArgs& a, int epi) {
   const ConvGeom& g = a.g;
-  if (!a.inb || !a.wb || !a.zero || !a.outb || a.kwrap || a.x3n) return false;
+  if (!a.inb || !a.wb || !a.zero || !a.outb || a.x3n) return false;
   if (g.Kc != 64 || g.Nc != 64 || g.KT != 9 || g.S != 1 || g.P != 4 || g.T_in != g.T_out) return false;
   if (g.V > 18 || g.lda % 8 != 0 || g.ldo % 8 != 0 || g.T_out * g.V < T64_BM || g.M % (g.T_out * g.V) != 0) return false;
   if (epi == (EPI_BIAS | EPI_STATS | EPI_GAP)) return a.gap && a.st_sum && a.st_sq && a.bias;
