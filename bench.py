@@ -113,7 +113,7 @@ def launch_check(world, rank):
     dist.destroy_process_group()
 
 
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r04_roofline_pmc.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r05_roofline_pmc.json")
 RGB_PMC = os.path.join(ROOT, "profiles", "r04_rgb_pmc.json")
 
 
@@ -201,30 +201,30 @@ def roofline_kernels(dev, batch, V, precision, only=None):
 
 
 def roofline_kernels_x3(dev, batch, V, only=None):
-    """bf16x3 (the headline mode): the step's tcn GEMMs on the layer-6 / layer-5 shapes (C=256, 9 taps,
-    T=8 output frames, B clips), launched alone through the C ABI exactly as the step launches them:
-    K-concatenated operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
-    step's producers write them) on the bf16 LDS-DMA kernels:
-    * "wgrad_l5": the layer-5 weight gradient (stride 2, T 15 -> 8): wgrad_big<4,2,4,4,32,2> (taps in groups
-      of two from one staged dY copy) over three
-      row segments of the [hi | lo] rows (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo: the split product's
-      three terms; split-K partials in the slab) + the slab reduce into dW[Cout][Cin][KT]
-      (f3_conv_backward_weight_x3cat) - the headline: the step's largest kernel share in this mode;
-    * "wgrad": the same on layer 6 (stride 1, T 8), where the step runs wgrad_taps<5> (all 9 taps from
-      one staged copy of each clip) over the three segments + its reduce; "wgrad_kernel": that GEMM
-      alone (dw = NULL);
-    * "tcn_fwd": the layer-6 forward over K = 9 x 3C (f3_conv_forward_x3cat, fp32 out + bias).
-    Algorithmic FLOP per launch = 2*M*N*K with M = B*8*V, N = 256, K = 9*256 (43.5 GFLOP at B=256,
-    V=18), priced against the dense bf16 MFMA peak; the split product issues 3 bf16 products per FLOP
-    (mfma_issue_frac). Algorithmic bytes (the stored formats: [hi | lo] rows = 4 B per element, fp32
-    outputs and weights): wgrad = dY + X + dW, tcn_fwd = X + W + Y. `only`: one key (the per-key PMC
-    passes of tools/roofline_pmc.py)."""
+    """bf16x3 (the headline mode): the step's largest GEMM families (the round-5 serial step profile,
+    profiles/r05_x3_step_serial_kernels.txt), each launched alone through the C ABI exactly as the step
+    launches it, on operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the step's
+    producers write them) in the native split form (three bf16 MFMA products per algorithmic FLOP):
+    * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,2,2,2,64> over the
+      three row segments (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo) + the slab reduce — the HEADLINE: the
+      step's largest serial family;
+    * "dgrad_l8": the 256-channel T=8 stride-1 tcn input gradient, igemm_big's clip-window form
+      (two clips x 128 channels per workgroup, the 9 taps reading one staged window) — the second;
+    * "wgrad_l5": the 256-channel stride-2 (T 15 -> 8) weight gradient, wgrad_big<4,2,4,4,32,2>;
+    * "wgrad" / "wgrad_kernel": the T=8 stride-1 weight gradient (wgrad_taps<5>, all 9 taps from one
+      staged copy of each clip) with / without its reduce;
+    * "tcn_fwd": the T=8 stride-1 forward (clip window, fp32 out + bias).
+    Algorithmic FLOP per launch = 2*M*N*K of the reference's conv (M output rows, K = 9 Cin), priced
+    against the dense bf16 MFMA peak; mfma_issue_frac counts the 3 products. Algorithmic bytes (the
+    stored formats: [hi | lo] rows = 4 B per element, fp32 outputs and weights): wgrad = dY + X + dW,
+    dgrad = dY + W + dX, fwd = X + W + Y. `only`: one key (the per-key PMC passes of
+    tools/roofline_pmc.py)."""
     import fall_multimodal_amd._lib as L
     lib = L.lib()
     N, T, C, KT = batch, 8, 256, 9
-    flop = 2.0 * (N * T * V) * C * (KT * C)   # algorithmic (the split's 3 products: products_per_flop)
     peak = PEAK_MFMA_TFLOPS["bf16x3"]
     st = L.stream_handle()
+    want = (lambda k: only is None or k == only)
 
     def split(t):
         rows, c = t.numel() // t.shape[-1], t.shape[-1]
@@ -232,38 +232,67 @@ def roofline_kernels_x3(dev, batch, V, only=None):
         L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), rows, c, st), "split")
         return out
 
+    def conv_flop(rows, cout, cin):
+        return 2.0 * rows * cout * KT * cin
+
+    out = {}
     x3 = split(torch.randn(N, T, V, C, device=dev))
     dy3 = split(torch.randn(N, T, V, C, device=dev))
-    x5 = split(torch.randn(N, 15, V, C, device=dev))
     w = torch.randn(C, C, KT, device=dev) / 48.0
     b = torch.zeros(C, device=dev)
-    y = torch.empty(N, T, V, C, device=dev)
-    wp = torch.empty(3 * C * KT * C // 2, device=dev)
-    L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1, 4, st),
-            "conv")  # packs w; the timed launches reuse it (the GEMM alone)
-    out = {}
-    want = (lambda k: only is None or k == only)
-    row8, row15, wbytes = N * T * V * C * 4, N * 15 * V * C * 4, C * C * KT * 4   # [hi | lo] rows: 4 B / element
-    ms = _time_launch(lambda: lib.f3_conv_forward_x3cat(L.ptr(x3), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C,
-                                                        KT, 1, 4, st)) if want("tcn_fwd") else 0.0
-    out["tcn_fwd"] = {"kernel": f"igemm_big (clip window) over K = 9 x 3C, bf16x3 K-concatenated (tcn 9x1 fwd, C=256, "
-                                f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes * 3 // 2}
+    wp = torch.empty(C * KT * C, device=dev)
+    row8, row15, wbytes = N * T * V * C * 4, N * 15 * V * C * 4, C * C * KT * 4  # [hi | lo] rows: 4 B / element
+    if want("tcn_fwd"):
+        y = torch.empty(N, T, V, C, device=dev)
+        L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C, C, KT, 1, 4,
+                                          st), "conv")  # packs w; the timed launches reuse it (the GEMM alone)
+        ms = _time_launch(lambda: lib.f3_conv_forward_x3cat(L.ptr(x3), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C,
+                                                            C, KT, 1, 4, st))
+        out["tcn_fwd"] = {"kernel": f"igemm_big<1,2,4,144,x3n> clip window (tcn 9x1 fwd, bf16x3, C=256, T=8, N={N}, "
+                                    f"V={V})", "ms": ms, "bytes": row8 + row8 + wbytes, "flop": conv_flop(N * T * V, C, C)}
+    if want("dgrad_l8"):
+        dx = torch.empty(N, T, V, C, device=dev)
+        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wp), N, T, V, C, C, KT, 1, 4, st),
+                "dgrad")
+        ms = _time_launch(lambda: lib.f3_conv_backward_data_x3cat(L.ptr(dy3), None, L.ptr(dx), L.ptr(wp), N, T, V, C, C,
+                                                                  KT, 1, 4, st))
+        out["dgrad_l8"] = {"kernel": f"igemm_big<0,2,4,144,x3n> clip window (tcn 9x1 input gradient, bf16x3, C=256, "
+                                     f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes,
+                           "flop": conv_flop(N * T * V, C, C)}
     dw = torch.empty(C, C, KT, device=dev)
     db = torch.empty(C, device=dev)
-    ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V, C,
-                                                                C, KT, 1, 4, st)) if want("wgrad") else 0.0
-    out["wgrad"] = {"kernel": f"wgrad_taps<5> x 3 row segments + reduce (tcn 9x1 weight gradient, bf16x3, C=256, "
-                              f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes}
-    ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), None, None, N, T, V, C, C, KT, 1,
-                                                                4, st)) if want("wgrad_kernel") else 0.0
-    out["wgrad_kernel"] = {"kernel": f"wgrad_taps<5> x 3 row segments alone (bf16x3, partials left in the slab, "
-                                     f"C=256, T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes}
-    ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15, V, C,
-                                                                C, KT, 2, 4, st)) if want("wgrad_l5") else 0.0
-    out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,2> (2-tap groups) x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
-                                 f"bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms,
-                       "bytes": row8 + row15 + wbytes}
-    return _roofline_records({k: v for k, v in out.items() if want(k)}, flop, peak, products=3)
+    if want("wgrad"):
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), L.ptr(dw), L.ptr(db), N, T, V,
+                                                                    C, C, KT, 1, 4, st))
+        out["wgrad"] = {"kernel": f"wgrad_taps<5> x 3 row segments + reduce (tcn 9x1 weight gradient, bf16x3, C=256, "
+                                  f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes,
+                        "flop": conv_flop(N * T * V, C, C)}
+    if want("wgrad_kernel"):
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x3), None, None, N, T, V, C, C, KT,
+                                                                    1, 4, st))
+        out["wgrad_kernel"] = {"kernel": f"wgrad_taps<5> x 3 row segments alone (bf16x3, partials left in the slab, "
+                                         f"C=256, T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes,
+                               "flop": conv_flop(N * T * V, C, C)}
+    if want("wgrad_l5"):
+        x5 = split(torch.randn(N, 15, V, C, device=dev))
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15,
+                                                                    V, C, C, KT, 2, 4, st))
+        out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,2> (2-tap groups) x 3 row segments + slab reduce (tcn 9x1 "
+                                     f"weight gradient, bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms,
+                           "bytes": row8 + row15 + wbytes, "flop": conv_flop(N * T * V, C, C)}
+    if want("wgrad_l1"):
+        C1, T1 = 64, 30
+        x1 = split(torch.randn(N, T1, V, C1, device=dev))
+        dy1 = split(torch.randn(N, T1, V, C1, device=dev))
+        dw1 = torch.empty(C1, C1, KT, device=dev)
+        db1 = torch.empty(C1, device=dev)
+        ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy1), L.ptr(x1), L.ptr(dw1), L.ptr(db1), N, T1,
+                                                                    V, C1, C1, KT, 1, 4, st))
+        row30 = N * T1 * V * C1 * 4
+        out["wgrad_l1"] = {"kernel": f"wgrad_big<2,2,2,2,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
+                                     f"bf16x3, C=64, T=30, N={N}, V={V})", "ms": ms,
+                           "bytes": row30 + row30 + C1 * C1 * KT * 4, "flop": conv_flop(N * T1 * V, C1, C1)}
+    return _roofline_records(out, None, peak, products=3)
 
 
 def _roofline_records(out, flop, peak, products=1):
@@ -278,12 +307,13 @@ def _roofline_records(out, flop, peak, products=1):
             pmc = json.load(f)
     res = {}
     for key, r in out.items():
-        achieved = flop / (r["ms"] * 1e-3) / 1e12
+        fl = r.get("flop", flop)  # per-key FLOPs where the keys' shapes differ
+        achieved = fl / (r["ms"] * 1e-3) / 1e12
         t = pmc.get(key, {})
         traffic = t.get("bytes_per_launch") if t.get("kernel") == r["kernel"] else None
         res[key] = {"kernel": r["kernel"], "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "flop_per_launch": flop, "ms_per_launch": round(r["ms"], 4),
+                    "flop_per_launch": fl, "ms_per_launch": round(r["ms"], 4),
                     "products_per_flop": products, "mfma_issue_frac": round(products * achieved / peak, 4),
                     "algorithmic_bytes": r.get("bytes"),
                     "traffic_over_algorithmic": None if (traffic is None or not r.get("bytes")) else
@@ -1032,7 +1062,9 @@ def main():
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "build-defined, timed on its own (rgb_branch key)",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
                        "ranks": world, "collective": "rccl all_reduce (2 buckets, high-priority streams)" if world > 1 else None},
-            "roofline": roofs.get("wgrad_l5", roofs["tcn_fwd"]),
+            "roofline": roofs.get("wgrad_l1", roofs.get("wgrad_l5", roofs["tcn_fwd"])),
+            "roofline_dgrad_l8": roofs.get("dgrad_l8"),
+            "roofline_wgrad_l5": roofs.get("wgrad_l5"),
             "roofline_wgrad_l6": roofs.get("wgrad"),
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
             "roofline_tcn_fwd": roofs["tcn_fwd"],

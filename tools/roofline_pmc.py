@@ -9,7 +9,7 @@ different keys (layer 6 / layer 5 / the GEMM alone) never mix.
     on the box: per KEY and counter C: timeout -s KILL 60 rocprofv3 --pmc C --kernel-trace
                     -d gpurun_out/rpmc_KEY_C -o run -- python tools/roofline_pmc.py run KEY
                 (tools/gpu_session.sh roof_pmc)
-    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r04_roofline_pmc.json
+    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r05_roofline_pmc.json
 
 FETCH_SIZE on gfx950 counts 1/2 of the bytes of wide streaming reads (MI355X_MICROARCH.md,
 HBM section; calibrated here on rmsprop_kernel: 51.6 MB read = 2 x FETCH_SIZE), so fetch is
@@ -26,10 +26,12 @@ sys.path.insert(0, ROOT)
 
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
 _RED = "wgrad_slab_reduce_kernel"
-KERNELS = {"wgrad_l5": ["wgrad_big<4, 2, 4, 4, ", _RED],
-           "wgrad": ["wgrad_taps<5>", "wgrad_taps_reduce_kernel"],
-           "wgrad_kernel": ["wgrad_taps<5>"],
-           "tcn_fwd": ["igemm_big<"]}
+KERNELS = {"wgrad_l1": ["wgrad_big<2, 2, 2, 2, 64", _RED],
+           "dgrad_l8": ["igemm_big<0, 2, 4, 144"],
+           "wgrad_l5": ["wgrad_big<4, 2, 4, 4, ", _RED],
+           "wgrad": ["wgrad_taps<5", "wgrad_taps_reduce_kernel"],
+           "wgrad_kernel": ["wgrad_taps<5"],
+           "tcn_fwd": ["igemm_big<1, 2, 4, 144"]}
 
 
 def run(key):
