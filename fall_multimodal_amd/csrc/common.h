@@ -103,6 +103,13 @@ inline bool f3_debug_sync() {
   static const bool on = getenv("F3_DEBUG_SYNC") != nullptr;
   return on;
 }
+#ifndef F3_TRY
+#define F3_TRY(x)               \
+  do {                          \
+    int _s = (x);               \
+    if (_s != F3_OK) return _s; \
+  } while (0)
+#endif
 #define F3_LAUNCH_CHECK()                                                              \
   do {                                                                                 \
     if (f3_debug_sync()) (void)hipDeviceSynchronize();                                 \

@@ -17,6 +17,7 @@
 // Epilogues as conv_gemm_f32 (bias, graph-mixed bias, BN statistics, channel-attention
 // pooling, ReLU mask + BN-backward sums, accumulate).
 #include "igemm.h"
+#include "layers.h"
 
 #include <algorithm>
 
@@ -658,8 +659,11 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
       for (int x = 0; x < WJ; ++x) dbs[wm * 16 * WJ + x * 16 + fr] = dbp[x];
     }
     __syncthreads();
-    for (int t = tid; t < TJ; t += 256)
-      if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
+    for (int t = tid; t < TJ; t += 256) {
+      if (j0 + t >= g.Nc) continue;
+      if (a.dbpart) a.dbpart[(size_t)bz * g.Nc + j0 + t] = nst > 0 ? dbs[t] : 0.f;  // every (split, j) once
+      else if (nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
+    }
   }
   const bool to_slab = a.slab != nullptr && a.outmap == WG_OUT_CONV;
   if (nst == 0 && !to_slab) return;  // (a slab tile is written even when empty: it is summed)
@@ -952,9 +956,13 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
       for (int x = 0; x < MJ; ++x) dbs[wj * 16 * MJ + x * 16 + fr] = dbp[x];
     }
     __syncthreads();
-    for (int t = tid; t < TJ; t += NW * 64)
-      if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
+    if (!a.dbpart)
+      for (int t = tid; t < TJ; t += NW * 64)
+        if (j0 + t < g.Nc && nst > 0) atomic_add_f(a.db + j0 + t, dbs[t]);
   }
+  if (a.dbpart && a.db && by == 0)  // every (split, column) row element written once (0: no bias terms)
+    for (int t = tid; t < TJ; t += NW * 64)
+      if (j0 + t < g.Nc) a.dbpart[(size_t)bz * g.Nc + j0 + t] = (do_db && nst > 0) ? dbs[t] : 0.f;
   const bool to_slab = a.slab != nullptr && a.outmap == WG_OUT_CONV;
   if (nst == 0 && !to_slab) return;
   float* slab = to_slab ? a.slab + (size_t)bz * g.Nc * g.KT * g.Kc : nullptr;
@@ -1183,11 +1191,16 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
   }
   // bias gradient: the ones column of wave (kh 1, wi 0) in the i0 == 0 tiles; lane (fg, fr = 0)
   // holds co = x*16 + fg*4 + r (all 16 columns carry the same sum); x3seg: dY_hi + dY_lo only
-  if (a.db && seg < 2 && i0 == 0 && kh == 1 && wi == 0 && fr == 0 && nst > 0) {
+  if (a.db && i0 == 0 && kh == 1 && wi == 0 && fr == 0) {
+    const bool any = seg < 2 && nst > 0;
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomic_add_f(a.db + j0 + x * 16 + fg * 4 + r, acc[4][x][r]);
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + x * 16 + fg * 4 + r;
+        if (a.dbpart) a.dbpart[(size_t)bz * g.Nc + j] = any ? acc[4][x][r] : 0.f;  // every (split, j) once
+        else if (any) atomic_add_f(a.db + j, acc[4][x][r]);
+      }
   }
   // partials in fragment order, slab[split][tile][wi][dt][x][lane] as 16-B pieces: each store is
   // one contiguous KiB per wave (the reference-layout scatter took 80 4-B stores per lane at
@@ -1280,6 +1293,9 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   splits = (clips + cps - 1) / cps;
   a.rows_per_split = cps;  // clips per split
   splits *= nseg;
+  // bias-gradient partial rows after the slab partials (deterministic order), where the slab has room
+  a.dbpart = (a.db && (long long)splits * (per_split + a.g.Nc) <= a.slab_cap) ? a.slab + (size_t)splits * per_split
+                                                                              : nullptr;
   const dim3 grid(tiles * splits);
   if (nks == 5) hipLaunchKernelGGL(wgrad_taps<5>, grid, dim3(512), 0, s, a);
   else if (nks == 4) hipLaunchKernelGGL(wgrad_taps<4>, grid, dim3(512), 0, s, a);
@@ -1291,6 +1307,7 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
                        a.dw_ref);
     F3_LAUNCH_CHECK();
   }
+  if (a.dbpart) return f3_colsum(a.dbpart, splits, a.g.Nc, a.db, s);
   return F3_OK;
 }
 
@@ -1338,6 +1355,9 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   splits = (a.g.M + rps - 1) / rps;
   a.rows_per_split = rps;
   splits *= nseg;  // slab partials (all segments)
+  // bias-gradient partial rows after the slab partials (deterministic order), where the slab has room
+  a.dbpart = (a.db && to_slab && (long long)splits * (per_split + a.g.Nc) <= a.slab_cap)
+                 ? a.slab + (size_t)splits * per_split : nullptr;
   // XCD-aware 1-D grid: measured in the B=256 step, HBM fetch per launch 273 -> 40 MB (tcn layers
   // 0-2) and 171 -> 68 MB (layers 3-6) at unchanged kernel time against a round-robin 3-D grid
   a.xcd = 1;
@@ -1349,6 +1369,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
                        a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref, a.gcn_cin);
     F3_LAUNCH_CHECK();
   }
+  if (a.dbpart) return f3_colsum(a.dbpart, splits, a.g.Nc, a.db, s);
   return F3_OK;
 }
 

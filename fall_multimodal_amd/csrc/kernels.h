@@ -86,6 +86,8 @@ struct WgradArgs {
   long long gs_dy, gs_in, gs_dw, gs_db;
   int wg_pct;                 // split sizing, percent of the resident workgroup slots (0: all)
   int taps_f;                 // (set by the launcher) wgrad_taps frame-chunk length
+  float* dbpart;              // (set by the launcher) bias-gradient partial rows [splits][Nc] after the slab
+                              // partials, summed in split order (deterministic); null: float atomics
   int x3;                     // 1: split-bf16 kernel on fp32 dy / in (gemm_x3.hip)
   // bf16x3 on the bf16 kernels by row segments (wgrad_big / wgrad_taps): dy / in are [hi | lo] rows
   // (ldy = 2 Nc, lda = 2 Kc) and the GEMM runs over 3 segments of the rows, (dY_hi, X_hi),

@@ -261,8 +261,13 @@ __global__ __launch_bounds__(256) void databn_bwd2_kernel(DataBnArgs a) {
   if (tid < VC) {
     double S = 0.0, Q = 0.0;
     for (int g2 = 0; g2 < ngrp; ++g2) { S += red[0][g2 * VC + tid]; Q += red[1][g2 * VC + tid]; }
-    atomic_add_f(a.dgamma + tid, (float)Q);
-    atomic_add_f(a.dbeta + tid, (float)S);
+    if (a.part) {  // this block's partial row [gamma (VC) | beta (VC)], summed in block order
+      a.part[(size_t)blockIdx.x * 2 * VC + tid] = (float)Q;
+      a.part[(size_t)blockIdx.x * 2 * VC + VC + tid] = (float)S;
+    } else {
+      atomic_add_f(a.dgamma + tid, (float)Q);
+      atomic_add_f(a.dbeta + tid, (float)S);
+    }
   }
 }
 
@@ -313,7 +318,10 @@ int f3_gcn0_bwd(const Gcn0Args* a, hipStream_t s) {
 int f3_databn_bwd2(const DataBnArgs* a, hipStream_t s) {
   if (a->V * a->C > 256 || a->C > 4) return F3_EINVAL;
   const int rows = a->N * a->T;
-  hipLaunchKernelGGL(databn_bwd2_kernel, dim3((rows + DB2_ROWS - 1) / DB2_ROWS), dim3(256), 0, s, *a);
+  const int blocks = (rows + DB2_ROWS - 1) / DB2_ROWS, VC = a->V * a->C;
+  hipLaunchKernelGGL(databn_bwd2_kernel, dim3(blocks), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  return F3_OK;
+  if (!a->part) return F3_OK;
+  F3_TRY(f3_colsum_ld(a->part, blocks, 2 * VC, VC, a->dgamma, s));
+  return f3_colsum_ld(a->part + VC, blocks, 2 * VC, VC, a->dbeta, s);
 }

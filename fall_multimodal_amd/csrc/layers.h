@@ -29,6 +29,7 @@ struct DataBnArgs {
   const float* dout;     // backward
   float* dgamma;
   float* dbeta;
+  float* part;           // databn_bwd2: partial rows [blocks][2 VC] (gamma, beta), summed in order
 };
 
 struct MixArgs {
@@ -117,6 +118,9 @@ struct BlockArgs {
                          // [hi | lo] of 2C bf16 (the K-concatenated GEMM operands)
   float* dgamma2;
   float* dbeta2;
+  // deterministic reductions: per-chunk partial rows of pool (forward, [chunks][N*C]) and of P1, P2,
+  // Q2 (backward, three [chunks][N*C] blocks), summed in chunk order by f3_colsum; null: float atomics
+  float* part;
   float* dgammar;
   float* dbetar;
 };
@@ -180,6 +184,9 @@ struct CaArgs {
   float* g_W1;
   float* g_W2;
   float* g_b2;
+  // deterministic weight gradients: per clip-group partial rows [groups][2 H C + C] (g_W1, g_W2, g_b2),
+  // summed in group order by f3_colsum; null: float atomics
+  float* wpart;
 };
 
 struct BnRunJob {
@@ -229,6 +236,8 @@ int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
 int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);  // out[c] += sum_r part[r][c]
+// the same over rows `ld` floats apart (fixed summation order, as f3_colsum)
+int f3_colsum_ld(const float* part, int rows, long long ld, int cols, float* out, hipStream_t s);
 int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);
 int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);          // input-gradient chain (ca_bwd1/2/3)
 int f3_ca_bwd_weights(const f3::CaArgs* a, hipStream_t s);  // W1/W2/b2 gradients (ca_bwd_w)

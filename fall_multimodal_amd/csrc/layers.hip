@@ -1151,8 +1151,12 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
   if (a.pool) {
     f32x4 r = quad_reduce(pool, lds, C4);
     if (tid < C4) {
+      if (a.part) {  // this chunk's row of the pooled mean (f3_block_out sums the chunks in order)
+        *reinterpret_cast<f32x4*>(a.part + ((size_t)blockIdx.x * a.N + n) * C + tid * 4) = r * a.inv_tv;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomic_add_f(a.pool + (size_t)n * C + tid * 4 + e, r[e] * a.inv_tv);
+        for (int e = 0; e < 4; ++e) atomic_add_f(a.pool + (size_t)n * C + tid * 4 + e, r[e] * a.inv_tv);
+      }
     }
   }
 }
@@ -1204,21 +1208,35 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   // residual BN's channel sums over all clips (sum dz = sum_n P1, sum dz*xhat_r = sum_n Q2) are
   // folded in by ca_bwd3, which walks the clips anyway: double atomics from every chunk of every
   // clip onto the same C addresses made the conv-residual form of this kernel 100 us.
+  // (a.part: the chunk's partial rows, summed in chunk order by f3_block_bwd_reduce)
+  const size_t prow = ((size_t)blockIdx.x * a.N + n) * C + tid * 4, pblk = (size_t)a.chunks * a.N * C;
   f32x4 s1 = quad_reduce(p1, lds, C4);
   if (tid < C4) {
+    if (a.part) {
+      *reinterpret_cast<f32x4*>(a.part + prow) = s1;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) atomic_add_f(a.P1 + (size_t)n * C + tid * 4 + e, s1[e]);
+      for (int e = 0; e < 4; ++e) atomic_add_f(a.P1 + (size_t)n * C + tid * 4 + e, s1[e]);
+    }
   }
   f32x4 s2 = quad_reduce(p2, lds, C4);
   if (tid < C4) {
+    if (a.part) {
+      *reinterpret_cast<f32x4*>(a.part + pblk + prow) = s2;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) atomic_add_f(a.P2 + (size_t)n * C + tid * 4 + e, s2[e]);
+      for (int e = 0; e < 4; ++e) atomic_add_f(a.P2 + (size_t)n * C + tid * 4 + e, s2[e]);
+    }
   }
   if (RES == RES_CONV) {
     f32x4 t2 = quad_reduce(q2, lds, C4);
     if (tid < C4) {
+      if (a.part) {
+        *reinterpret_cast<f32x4*>(a.part + 2 * pblk + prow) = t2;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomic_add_f(a.Q2 + (size_t)n * C + tid * 4 + e, t2[e]);
+        for (int e = 0; e < 4; ++e) atomic_add_f(a.Q2 + (size_t)n * C + tid * 4 + e, t2[e]);
+      }
     }
   }
 }
@@ -1550,24 +1568,31 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_any_kernel(BnReluArgs a) {
   }
 }
 
-// out[c] += sum_r part[r][c]: 64 columns x 64 rows per workgroup, one atomic per column
-__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int rows, int cols, float* out) {
-  __shared__ float red[4][64];
+// out[c] += sum_r part[r][c], in a fixed order (the same bits every run): a workgroup owns 64 columns
+// and all rows; its 16 row groups sum rows rg, rg + 16, ... and the 16 partials are added in group
+// order. (The first version split the rows over workgroups with one float atomic per column and
+// workgroup: order-dependent sums.)
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* part, int rows, int cols, float* out, long long ld) {
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int r0 = blockIdx.y * 64 + rg * 16, r1 = min(rows, r0 + 16);
   float s0 = 0.f, s1 = 0.f;
   if (c < cols) {
-    int r = r0;
-    for (; r + 1 < r1; r += 2) {
-      s0 += part[(size_t)r * cols + c];
-      s1 += part[(size_t)(r + 1) * cols + c];
+    int r = rg;
+    for (; r + 16 < rows; r += 32) {
+      s0 += part[(size_t)r * ld + c];
+      s1 += part[(size_t)(r + 16) * ld + c];
     }
-    if (r < r1) s0 += part[(size_t)r * cols + c];
+    if (r < rows) s0 += part[(size_t)r * ld + c];
   }
   red[rg][lane] = s0 + s1;
   __syncthreads();
-  if (rg == 0 && c < cols) atomic_add_f(out + c, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
+  if (rg == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][lane];
+    out[c] += t;
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1764,12 +1789,20 @@ __global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
       }
     }
   }
+  // a.wpart: this clip group's partial row [g_W1 (H C) | g_W2 (C H) | g_b2 (C)], summed in group order
+  float* wrow = a.wpart ? a.wpart + (size_t)blockIdx.y * (2 * H * C + C) : nullptr;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int j = jg + 4 * q;
-    if (j < H && cok) atomic_add_f(a.g_W1 + (size_t)j * C + c, w1[q]);  // lanes: consecutive c
+    if (j < H && cok) {
+      if (wrow) wrow[(size_t)j * C + c] = w1[q];
+      else atomic_add_f(a.g_W1 + (size_t)j * C + c, w1[q]);  // lanes: consecutive c
+    }
   }
-  if (jg == 0 && cok) atomic_add_f(a.g_b2 + c, b2);
+  if (jg == 0 && cok) {
+    if (wrow) wrow[2 * H * C + c] = b2;
+    else atomic_add_f(a.g_b2 + c, b2);
+  }
   // gW2 rows c0..c0+63 are one contiguous [64][H] block: transpose through LDS so the
   // atomics go out lane-contiguous
   float* t2 = &dq1s[0][0];  // 32*64 floats >= 64*H/2; use both arrays (64*H <= 4096)
@@ -1781,7 +1814,10 @@ __global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
   }
   __syncthreads();
   const int c0 = blockIdx.x * 64, nc = min(64, C - c0);
-  for (int e = threadIdx.x; e < nc * H; e += 256) atomic_add_f(a.g_W2 + (size_t)c0 * H + e, t2[e]);
+  for (int e = threadIdx.x; e < nc * H; e += 256) {
+    if (wrow) wrow[H * C + (size_t)c0 * H + e] = t2[e];
+    else atomic_add_f(a.g_W2 + (size_t)c0 * H + e, t2[e]);
+  }
 }
 
 // per clip: dgap = W1^T dq1 ; e = dgap/TV ; BN2 backward sums D1, D2. kCaB3Clips clips per
@@ -2230,6 +2266,7 @@ static void launch_block_bwd(const BlockArgs& a, hipStream_t s) {
 int f3_block_out(BlockArgs a, hipStream_t s) {
   if (a.C % 4 || a.C > 256 || 256 % (a.C / 4)) return F3_EINVAL;
   a.chunks = chunks_for(a.TV);
+  if (!a.pool) a.part = nullptr;
   const dim3 grid(a.chunks, a.N);
 #define F3_BO(A, R) hipLaunchKernelGGL((block_out_kernel<A, R>), grid, dim3(256), 0, s, a)
   if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
@@ -2244,6 +2281,7 @@ int f3_block_out(BlockArgs a, hipStream_t s) {
   }
 #undef F3_BO
   F3_LAUNCH_CHECK();
+  if (a.part) return f3_colsum(a.part, a.chunks, a.N * a.C, a.pool, s);
   return F3_OK;
 }
 
@@ -2253,6 +2291,11 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
   launch_block_bwd<true>(a, s);
   F3_LAUNCH_CHECK();
+  if (!a.part) return F3_OK;
+  const size_t blk = (size_t)a.chunks * a.N * a.C;
+  F3_TRY(f3_colsum(a.part, a.chunks, a.N * a.C, a.P1, s));
+  F3_TRY(f3_colsum(a.part + blk, a.chunks, a.N * a.C, a.P2, s));
+  if (a.res_kind == RES_CONV) F3_TRY(f3_colsum(a.part + 2 * blk, a.chunks, a.N * a.C, a.Q2, s));
   return F3_OK;
 }
 
@@ -2292,7 +2335,14 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
 
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return F3_OK;
-  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, s, part, rows, cols, out);
+  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, rows, cols, out, (long long)cols);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_colsum_ld(const float* part, int rows, long long ld, int cols, float* out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return F3_OK;
+  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, rows, cols, out, ld);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
@@ -2345,9 +2395,15 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
 
 int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
-  hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, (a->N + kCaWClips - 1) / kCaWClips), dim3(256), 0, s, *a);
+  const int groups = (a->N + kCaWClips - 1) / kCaWClips, H = a->C / 4, C = a->C;
+  hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, groups), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
-  return F3_OK;
+  if (!a->wpart) return F3_OK;
+  // the partial rows are [groups][2 H C + C]: sum each segment's columns over the groups
+  const int ld = 2 * H * C + C;
+  F3_TRY(f3_colsum_ld(a->wpart, groups, ld, H * C, a->g_W1, s));
+  F3_TRY(f3_colsum_ld(a->wpart + H * C, groups, ld, C * H, a->g_W2, s));
+  return f3_colsum_ld(a->wpart + 2 * H * C, groups, ld, C, a->g_b2, s);
 }
 
 int f3_bn_running(const BnRunTable& t, hipStream_t s) {

@@ -289,6 +289,10 @@ struct StreamWs {
   LayerWs L[7];
   float *dv, *dZ, *dx[2], *dpool;
   float* slab;  // bf16 weight-gradient split partials (see WgradArgs::slab); one per skeleton stream
+  // deterministic reductions: partial rows summed in a fixed order (f3_colsum) instead of float atomics,
+  // one region for the stream's main queue (pool, P1/P2/Q2, data_bn) and one for its side queue (CA weights)
+  float* detm;
+  float* dets;
 };
 
 struct Ws {
@@ -297,6 +301,7 @@ struct Ws {
   float *y1, *p1, *y2, *p2, *dy1, *dp1, *dy2, *dp2;
   BnWs cbn1, cbn2, sbn;
   float *seq, *gates, *cell, *hmean, *ybn, *a1, *satt, *sout, *sdy, *sdpre2, *sdpre1, *dhmean;
+  float* lwpart;  // LSTM weight-gradient partial rows (LstmArgs::wpart)
   // head
   float *out, *dlogits, *ds;
   float *skel, *sensor;  // copies of the step's inputs (backward re-reads them)
@@ -441,6 +446,19 @@ Ws plan(const f3_net& net, int N, char* base) {
     W.dx[0] = A.take<float>(maxMC);
     W.dx[1] = A.take<float>(maxMC);
     W.dpool = A.take<float>((size_t)N * 256);
+    {  // partial-row regions (see StreamWs::detm / dets)
+      size_t m = (size_t)((S.T * V + 95) / 96) * N * 256;  // pool partials of the last block
+      size_t d = 0;
+      for (int l = 0; l < 7; ++l) {
+        const LayerIdx& L = S.L[l];
+        const size_t ch = (size_t)(L.T_out * V + 95) / 96;  // f3_block_* chunks per clip
+        m = std::max(m, 3 * ch * N * L.cout);
+        d = std::max(d, (size_t)((N + 7) / 8) * (2 * (L.cout / 4) * L.cout + L.cout));
+      }
+      m = std::max(m, (size_t)((N * S.T + 31) / 32) * 2 * V * S.cin);  // data_bn gamma / beta partials
+      W.detm = A.take<float>(m);
+      W.dets = A.take<float>(d);
+    }
   }
   if (net.has_sensor) {
     if (cnn) {
@@ -455,6 +473,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     w.seq = A.take<float>((size_t)N * Tl * 128);
     w.gates = A.take<float>((size_t)2 * N * Tl * 256);
     w.cell = A.take<float>((size_t)2 * N * Tl * 64);
+    w.lwpart = A.take<float>((size_t)2 * ((N + LSTM_NB - 1) / LSTM_NB) * 256 * (1 + (net.has_cnn ? 32 : net.lstm.S) + 64));
     w.hmean = A.take<float>((size_t)N * 128);
     w.ybn = A.take<float>((size_t)N * 128);
     w.a1 = A.take<float>((size_t)N * 16);
@@ -503,11 +522,6 @@ struct Ptrs {
   }
 };
 
-#define F3_TRY(x)              \
-  do {                         \
-    int _s = (x);              \
-    if (_s != F3_OK) return _s; \
-  } while (0)
 
 ConvGeom geom(int M, int Nc, int Kc, int KT, int S, int P, int tr, int T_out, int T_in, int V, int lda, int ldo) {
   ConvGeom g;
@@ -711,6 +725,7 @@ int stream_forward_layer(const f3_net& net, int si, int N, int train, const Ptrs
     ba.N = N; ba.TV = To * V; ba.C = C; ba.res_kind = L.res; ba.inv_tv = 1.f / (float)(To * V);
     ba.bn2 = bn2; ba.bnr = bnr; ba.h = X.h; ba.r = X.r; ba.x = X.x; ba.att = X.att; ba.out = X.out;
     ba.pool = l == 6 ? W.pool : nullptr;
+    ba.part = W.detm;
     ba.act16 = hb;
     if (x3 && X.outb) { ba.outb = X.outb; ba.x3 = 1; }
     F3_TRY(f3_block_out(ba, s));
@@ -795,6 +810,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.dresb = L.res == RES_CONV ? bfa(dres, hb || x3) : nullptr;  // bf16x3: [hi | lo] rows
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
+    ba.part = W.detm;
     if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
     CaArgs ca;
     std::memset(&ca, 0, sizeof(ca));
@@ -908,6 +924,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 1, ss));
     }
+    ca.wpart = W.dets;
     if (part & 2) F3_TRY(f3_ca_bwd_weights(&ca, ss));
     if (L.res == RES_CONV) {
       WgradArgs rw;
@@ -977,6 +994,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
   d.N = N; d.T = S.T; d.V = V; d.C = S.cin; d.motion = S.motion; d.skel = skel;
   d.bn = q.ref(S.dbn, W.dbn, (float)(N * S.T), 0);
   d.dout = dout; d.dgamma = q.g(S.dbn.w); d.dbeta = q.g(S.dbn.b);
+  d.part = W.detm;
   if (part & 1) {  // the coalesced single-pass data_bn gradient where its shape fits, else the per-channel one
     const int st = f3_databn_bwd2(&d, s);
     if (st == F3_EINVAL) F3_TRY(f3_databn_bwd(&d, s));
@@ -1018,6 +1036,7 @@ void sensor_args(const f3_net& net, int N, int train, const Ptrs& q, Ws& w, cons
     if (q.G) {
       la.g_w_ih[d] = q.g(net.lstm.wih[d]); la.g_w_hh[d] = q.g(net.lstm.whh[d]);
       la.g_b_ih[d] = q.g(net.lstm.bih[d]); la.g_b_hh[d] = q.g(net.lstm.bhh[d]);
+      la.wpart = w.lwpart;
     }
   }
   la.seq = w.seq; la.gates = w.gates; la.cell = w.cell; la.hmean = w.hmean;

@@ -24,6 +24,9 @@ struct LstmArgs {
   float* g_w_hh[2];
   float* g_b_ih[2];
   float* g_b_hh[2];
+  // deterministic weight gradients: per (direction, clip tile) partial rows [2][tiles][4H (1 + S + H)]
+  // (bias | w_ih | w_hh), summed in tile order by f3_colsum; null: float atomics
+  float* wpart;
 };
 
 struct SHeadArgs {

@@ -10,6 +10,7 @@
 // backward kernel runs BPTT in the same layout with W_hh staged in LDS for dh.
 #include "common.h"
 #include "sensor.h"
+#include "layers.h"
 
 #include <algorithm>
 
@@ -198,6 +199,14 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (a.wpart) {  // this (direction, clip tile)'s partial row [bias | w_ih | w_hh], summed by f3_lstm_bwd
+    float* row = a.wpart + ((size_t)dir * gridDim.x + blockIdx.x) * G4 * (1 + S + H);
+    row[tid] = gb;
+    for (int s = 0; s < S && s < 32; ++s) row[G4 + tid * S + s] = gwi[s];
+#pragma unroll
+    for (int u = 0; u < H; ++u) row[G4 * (1 + S) + tid * H + u] = gwh[u];
+    return;
   }
   atomic_add_f(a.g_b_ih[dir] + tid, gb);
   atomic_add_f(a.g_b_hh[dir] + tid, gb);
@@ -565,6 +574,15 @@ int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
   (void)once;
   hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), lds, s, *a);
   F3_LAUNCH_CHECK();
+  if (!a->wpart) return F3_OK;
+  const int tiles = grid.x, S = a->S, row = G4 * (1 + S + H);
+  for (int d = 0; d < 2; ++d) {
+    const float* p = a->wpart + (size_t)d * tiles * row;
+    F3_TRY(f3_colsum_ld(p, tiles, row, G4, a->g_b_ih[d], s));
+    F3_TRY(f3_colsum_ld(p, tiles, row, G4, a->g_b_hh[d], s));
+    F3_TRY(f3_colsum_ld(p + G4, tiles, row, G4 * S, a->g_w_ih[d], s));
+    F3_TRY(f3_colsum_ld(p + G4 * (1 + S), tiles, row, G4 * H, a->g_w_hh[d], s));
+  }
   return F3_OK;
 }
 
