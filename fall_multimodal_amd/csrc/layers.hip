@@ -1209,7 +1209,8 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   // folded in by ca_bwd3, which walks the clips anyway: double atomics from every chunk of every
   // clip onto the same C addresses made the conv-residual form of this kernel 100 us.
   // (a.part: the chunk's partial rows, summed in chunk order by f3_block_bwd_reduce)
-  const size_t prow = ((size_t)blockIdx.x * a.N + n) * C + tid * 4, pblk = (size_t)a.chunks * a.N * C;
+  // partial rows [chunk][P1 | P2 | Q2][N*C]
+  const size_t pblk = (size_t)a.N * C, prow = (size_t)blockIdx.x * 3 * pblk + (size_t)n * C + tid * 4;
   f32x4 s1 = quad_reduce(p1, lds, C4);
   if (tid < C4) {
     if (a.part) {
@@ -2292,10 +2293,12 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   launch_block_bwd<true>(a, s);
   F3_LAUNCH_CHECK();
   if (!a.part) return F3_OK;
-  const size_t blk = (size_t)a.chunks * a.N * a.C;
-  F3_TRY(f3_colsum(a.part, a.chunks, a.N * a.C, a.P1, s));
-  F3_TRY(f3_colsum(a.part + blk, a.chunks, a.N * a.C, a.P2, s));
-  if (a.res_kind == RES_CONV) F3_TRY(f3_colsum(a.part + 2 * blk, a.chunks, a.N * a.C, a.Q2, s));
+  const int nc = a.N * a.C, nseg = a.res_kind == RES_CONV ? 3 : 2;
+  if (a.P2 == a.P1 + nc && (nseg == 2 || a.Q2 == a.P1 + 2 * nc))  // contiguous [P1 | P2 | Q2]: one launch
+    return f3_colsum_ld(a.part, a.chunks, 3LL * nc, nseg * nc, a.P1, s);
+  F3_TRY(f3_colsum_ld(a.part, a.chunks, 3LL * nc, nc, a.P1, s));
+  F3_TRY(f3_colsum_ld(a.part + nc, a.chunks, 3LL * nc, nc, a.P2, s));
+  if (nseg == 3) F3_TRY(f3_colsum_ld(a.part + 2 * nc, a.chunks, 3LL * nc, nc, a.Q2, s));
   return F3_OK;
 }
 

@@ -366,9 +366,10 @@ Ws plan(const f3_net& net, int N, char* base) {
       bn_take_b(A, X.bn1, L.cout);
       bn_take_b(A, X.bn2, L.cout);
       if (L.res == RES_CONV) bn_take_b(A, X.bnr, L.cout);
-      X.P1 = A.take<float>((size_t)N * L.cout);
-      X.P2 = A.take<float>((size_t)N * L.cout);
-      X.Q2 = L.res == RES_CONV ? A.take<float>((size_t)N * L.cout) : nullptr;
+      // [P1 | P2 | Q2] contiguous: f3_block_bwd_reduce sums their partial rows in one launch
+      X.P1 = A.take<float>((size_t)3 * N * L.cout);
+      X.P2 = X.P1 + (size_t)N * L.cout;
+      X.Q2 = L.res == RES_CONV ? X.P1 + (size_t)2 * N * L.cout : nullptr;
       X.G = A.take<float>((size_t)V * L.cout);
       X.dAeff = A.take<float>((size_t)K * V * V);
     }

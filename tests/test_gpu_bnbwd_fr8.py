@@ -2,11 +2,12 @@
 (needs an MI355X). The knob is read once per process, so each setting runs in a child process
 (tests/fr8_grads.py): the B=32 step's gradients and logits with FR=8 against FR=4 on the same
 weights and batch. T = 30 (position stream) and 29 (motion stream) are not multiples of 8, so the
-ragged last frame group of every clip is exercised. The step's reductions are deterministic (fixed
-summation order, tests/test_gpu_determinism.py), so two FR=4 runs are bit-identical; FR only changes
+ragged last frame group of every clip is exercised. The bf16x3 step's reductions are deterministic
+(fixed summation order, tests/test_gpu_determinism.py), so two FR=4 runs are bit-identical; FR only changes
 how the per-node column sums are partitioned into partial rows (a different but fixed summation
 order), so FR=8 must match FR=4 within a fixed tolerance: identical logits (FR is backward-only) and
-gradients within FR8_REL of the max."""
+gradients within FR8_REL of the max. (The fp32 mode's kernels keep float atomics: there FR=8 is
+measured against the run-to-run floor of two FR=4 runs.)"""
 import os
 import subprocess
 import sys
@@ -25,9 +26,8 @@ def _cmp(a, b):
     return cos, rel, dl
 
 
-# a different summation order in the BN1-backward column sums, amplified by the small-batch BN
-# backward of the layers after it (B=32)
-FR8_REL = {"fp32": 1e-3, "bf16x3": 5e-3}
+# bf16x3: a different (fixed) summation order in the BN1-backward column sums; measured 3.2e-8 of max
+FR8_REL = 1e-6
 
 
 @pytest.mark.gpu
@@ -48,7 +48,12 @@ def test_bn_bwd_apply_fr8_matches_fr4(precision, tmp_path):
     cos8, rel8, dl8 = _cmp(res["4a"], res["8"])
     print(f"{precision}: FR=4 vs FR=4 cosine {cos0:.9f} rel {rel0:.2e} dlogit {dl0:.1e}; "
           f"FR=8 vs FR=4 cosine {cos8:.9f} rel {rel8:.2e} dlogit {dl8:.1e}")
+    if precision == "fp32":  # the fp32 mode's kernels keep float atomics: run-to-run floor
+        assert dl8 <= 4 * dl0 + 1e-5, (dl8, dl0)
+        assert rel8 <= 4 * rel0 + 2e-4, (rel8, rel0)
+        assert 1 - cos8 <= 4 * (1 - cos0) + 1e-7, (cos8, cos0)
+        return
     assert np.array_equal(res["4a"]["grads"], res["4b"]["grads"]) and dl0 == 0.0
     assert dl8 == 0.0, dl8
-    assert rel8 <= FR8_REL[precision], (rel8, FR8_REL[precision])
-    assert cos8 >= 1 - 1e-7, cos8
+    assert rel8 <= FR8_REL, rel8
+    assert cos8 >= 1 - 1e-9, cos8

@@ -80,6 +80,9 @@ def test_captured_step_matches_eager(phased, precision):
     assert all(np.isfinite(losses)), losses
     # step 1 is the same forward; after it the two runs differ by float-atomic ordering noise, which
     # RMSprop's first steps amplify (lr*g/sqrt(v) ~ 10*lr*sign(g), also for gradients at rounding
-    # level): measured 2e-4 after one update (1.2e-3 once in bf16x3, phased), 0.4-0.8 % after two
-    np.testing.assert_allclose(losses[:2], ref[:2], rtol=4e-3)
+    # level): measured 2e-4 after one update, 0.4-0.8 % after two. The bf16x3 step's reductions are
+    # deterministic (tests/test_gpu_determinism.py): there the captured replay is bit-identical
+    if precision == "bf16x3":
+        assert losses == ref, (losses, ref)
+    np.testing.assert_allclose(losses[:2], ref[:2], rtol=1e-3)
     np.testing.assert_allclose(losses[2], ref[2], rtol=2e-2)
