@@ -745,12 +745,17 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
 // drop by NTW (each wave holds NTW x MJ x MI accumulators). Taps past KT (the last group when
 // NTW does not divide KT) are staged from the zero page and their MFMAs skipped.
 // ----------------------------------------------------------------------------
-template <int WJW, int WIW, int MJ, int MI, int BK = 64, int NTW = 1, int NSTG = 3>
+// X3F (bf16x3, the three row segments fused): the staged rows carry both halves of the operands,
+// [dY_hi (TJ) | dY_lo (TJ)] and [X_hi (TI) | X_lo (TI)], and the wave issues the split product's three
+// MFMAs dY_hi X_hi + dY_lo X_hi + dY_hi X_lo per fragment set: one staging for all three terms instead
+// of one per row segment (x3seg), 2/3 of the staged bytes per MFMA with the tap groups on top.
+template <int WJW, int WIW, int MJ, int MI, int BK = 64, int NTW = 1, int NSTG = 3, bool X3F = false>
 __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   constexpr int NW = WJW * WIW;  // waves: 8 (one workgroup per CU) or 4 (the 64-wide tiles)
-  constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;
-  constexpr int UJ = TJ / 16, UI = TI / 16;
-  constexpr int RJ = TJ * 2, RI = TI * 2;  // row bytes of the dY / input tiles
+  constexpr int TJ = WJW * 16 * MJ, TI = WIW * 16 * MI;      // output tile
+  constexpr int HS = X3F ? 2 : 1;                             // staged halves (hi | lo)
+  constexpr int UJ = HS * TJ / 16, UI = HS * TI / 16;         // 32-B units per staged row
+  constexpr int RJ = HS * TJ * 2, RI = HS * TI * 2;  // row bytes of the dY / input tiles
   constexpr int NKS = BK / 32;             // 32-deep MFMA k steps per stage
   constexpr int Y_BYTES = BK * RJ, X_BYTES = BK * RI, STAGE = Y_BYTES + NTW * X_BYTES;
   constexpr int YPW = Y_BYTES / 1024 / NW, XPW = X_BYTES / 1024 / NW, PPW = YPW + NTW * XPW;  // pieces per wave
@@ -785,8 +790,8 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int i0 = (by - grp * itiles) * TI;
   // bf16x3 row segments (x3seg): split bz = row range bz / 3, segment seg = bz % 3, whose
   // operands sit at column offsets (0, 0) hi x hi, (Nc, 0) lo x hi, (0, Kc) hi x lo of the rows
-  const int seg = a.x3seg ? bz % 3 : 0;
-  const int r_begin = (a.x3seg ? bz / 3 : bz) * a.rows_per_split;
+  const int seg = (a.x3seg && !X3F) ? bz % 3 : 0;
+  const int r_begin = ((a.x3seg && !X3F) ? bz / 3 : bz) * a.rows_per_split;
   const int r_end = min(g.M, r_begin + a.rows_per_split);
   const bool do_db = a.db && by == 0 && seg < 2;
   const __bf16* dyb = reinterpret_cast<const __bf16*>(a.dyb) + (seg == 1 ? g.Nc : 0);
@@ -795,18 +800,24 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
 
   // ---- staging lanes: fixed column, rows walked 64 at a time ----
-  const int ysub = lane / (TJ / 8), yph = lane % (TJ / 8);
-  const int xsub = lane / (TI / 8), xph = lane % (TI / 8);
+  const int ysub = lane / (HS * TJ / 8), yph = lane % (HS * TJ / 8);
+  const int xsub = lane / (HS * TI / 8), xph = lane % (HS * TI / 8);
+  // X3F: staged unit u < U/2 is the hi half's column j0 + 16 u, else the lo half's (offset Nc / Kc)
   int ycol[YPW], yrow[YPW];
+  bool yok[YPW];
 #pragma unroll
   for (int i = 0; i < YPW; ++i) {
     const int rr = (i * NW + wave) * YRPI + ysub;
     yrow[i] = r_begin + rr;
-    ycol[i] = j0 + ((yph >> 1) ^ wswz<UJ>(rr)) * 16 + (yph & 1) * 8;
+    const int u = (yph >> 1) ^ wswz<UJ>(rr), lo = X3F && u >= UJ / 2;
+    const int cl = j0 + (lo ? u - UJ / 2 : u) * 16 + (yph & 1) * 8;  // logical column
+    yok[i] = cl < g.Nc;
+    ycol[i] = cl + (lo ? g.Nc : 0);
   }
   // input rows: m = (n*T_out + t)*V + v -> source (n*T_in + t*S + dt - P)*V + v
   const int dv = BK % g.V, dnt = BK / g.V;
   int xm[XPW], xv[XPW], xt[XPW], xn[XPW], xcol[XPW];
+  bool xok[XPW];
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
     const int rr = (i * NW + wave) * XRPI + xsub;
@@ -816,7 +827,10 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     xv[i] = m - nt * g.V;
     xn[i] = nt / g.T_out;
     xt[i] = nt - xn[i] * g.T_out;
-    xcol[i] = i0 + ((xph >> 1) ^ wswz<UI>(rr)) * 16 + (xph & 1) * 8;
+    const int u = (xph >> 1) ^ wswz<UI>(rr), lo = X3F && u >= UI / 2;
+    const int cl = i0 + (lo ? u - UI / 2 : u) * 16 + (xph & 1) * 8;
+    xok[i] = cl < g.Kc;
+    xcol[i] = cl + (lo ? g.Kc : 0);
   }
   const int tshift = dt0 - g.P;
   const int ntap = min(NTW, g.KT - dt0);  // valid taps of this group
@@ -824,7 +838,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     const unsigned sy = lds0 + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < YPW; ++i) {
-      const __bf16* src = (yrow[i] < r_end && ycol[i] < g.Nc) ? dyb + (size_t)yrow[i] * a.ldy + ycol[i] : zero;
+      const __bf16* src = (yrow[i] < r_end && yok[i]) ? dyb + (size_t)yrow[i] * a.ldy + ycol[i] : zero;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (lds_void_t*)(size_t)(sy + (i * NW + wave) * 1024), 16, 0, 0);
       yrow[i] += BK;
@@ -833,7 +847,7 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
 #pragma unroll
     for (int i = 0; i < XPW; ++i) {
       const int tb = xt[i] * g.S + tshift;
-      const bool okr = xm[i] < r_end && xcol[i] < g.Kc;
+      const bool okr = xm[i] < r_end && xok[i];
       const long long rb = (long long)(xn[i] * g.T_in + tb) * g.V + xv[i];
 #pragma unroll
       for (int tt = 0; tt < NTW; ++tt) {  // tap dt0 + tt: input frame tb + tt (rows V apart)
@@ -856,14 +870,19 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
   const int fr = lane & 15, fg = lane >> 4, tq = fr >> 2, tp = fr & 3;
   const int r0 = 8 * fg + tq;                 // rows r0, r0+4 (lo/hi), +32 for the second k half
   const int fj = wswz<UJ>(r0), fi = wswz<UI>(r0);  // unchanged at r0 + 4, r0 + 32, r0 + 36
-  unsigned offa[MJ], offb[NB];
+  // fragment h of tile x: X3F h = 0 the hi half, 1 the lo half (units U/2 further)
+  constexpr int NH = HS;
+  unsigned offa[NH][MJ], offb[NH][NB];
 #pragma unroll
-  for (int x = 0; x < MJ; ++x) offa[x] = r0 * RJ + (((wj * MJ + x) ^ fj) * 32) + tp * 8;
+  for (int h = 0; h < NH; ++h) {
 #pragma unroll
-  for (int tt = 0; tt < NTW; ++tt)
+    for (int x = 0; x < MJ; ++x) offa[h][x] = r0 * RJ + (((h * UJ / 2 + wj * MJ + x) ^ fj) * 32) + tp * 8;
 #pragma unroll
-    for (int y = 0; y < MI; ++y)
-      offb[tt * MI + y] = Y_BYTES + tt * X_BYTES + r0 * RI + (((wi * MI + y) ^ fi) * 32) + tp * 8;
+    for (int tt = 0; tt < NTW; ++tt)
+#pragma unroll
+      for (int y = 0; y < MI; ++y)
+        offb[h][tt * MI + y] = Y_BYTES + tt * X_BYTES + r0 * RI + (((h * UI / 2 + wi * MI + y) ^ fi) * 32) + tp * 8;
+  }
 
   f32x4 acc[MJ][NB];
 #pragma unroll
@@ -895,41 +914,57 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
     const unsigned base = lds0 + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      s16x4_t lo[MJ + NB], hi[MJ + NB];
+      // rows r0 / r0 + 4 of the fragment's 8 (lo / hi of the transposed read), + 32 for k step 1
+      s16x4_t lo[NH * (MJ + NB)], hi[NH * (MJ + NB)];
 #pragma unroll
-      for (int x = 0; x < MJ; ++x) {
-        const unsigned p = base + offa[x];
-        if (ks == 0) {
-          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[x]) : "v"(p));
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[x]) : "v"(p), "n"(4 * RJ));
-        } else {
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[x]) : "v"(p), "n"(32 * RJ));
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[x]) : "v"(p), "n"(36 * RJ));
+      for (int h = 0; h < NH; ++h) {
+#pragma unroll
+        for (int x = 0; x < MJ; ++x) {
+          const unsigned p = base + offa[h][x];
+          const int q = h * (MJ + NB) + x;
+          if (ks == 0) {
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[q]) : "v"(p));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[q]) : "v"(p), "n"(4 * RJ));
+          } else {
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[q]) : "v"(p), "n"(32 * RJ));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[q]) : "v"(p), "n"(36 * RJ));
+          }
         }
-      }
 #pragma unroll
-      for (int y = 0; y < NB; ++y) {
-        const unsigned p = base + offb[y];
-        if (ks == 0) {
-          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[MJ + y]) : "v"(p));
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[MJ + y]) : "v"(p), "n"(4 * RI));
-        } else {
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[MJ + y]) : "v"(p), "n"(32 * RI));
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[MJ + y]) : "v"(p), "n"(36 * RI));
+        for (int y = 0; y < NB; ++y) {
+          const unsigned p = base + offb[h][y];
+          const int q = h * (MJ + NB) + MJ + y;
+          if (ks == 0) {
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[q]) : "v"(p));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[q]) : "v"(p), "n"(4 * RI));
+          } else {
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[q]) : "v"(p), "n"(32 * RI));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[q]) : "v"(p), "n"(36 * RI));
+          }
         }
       }
       tr_wait(lo, hi);
-      bf16x8 fa[MJ], fb[NB];
+      bf16x8 fa[NH][MJ], fb[NH][NB];
 #pragma unroll
-      for (int x = 0; x < MJ; ++x) fa[x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[x], hi[x], 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int h = 0; h < NH; ++h) {
 #pragma unroll
-      for (int y = 0; y < NB; ++y)
-        fb[y] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[MJ + y], hi[MJ + y], 0, 1, 2, 3, 4, 5, 6, 7));
-      if (do_db && wi == 0) {
+        for (int x = 0; x < MJ; ++x) {
+          const int q = h * (MJ + NB) + x;
+          fa[h][x] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[q], hi[q], 0, 1, 2, 3, 4, 5, 6, 7));
+        }
 #pragma unroll
-        for (int x = 0; x < MJ; ++x)
+        for (int y = 0; y < NB; ++y) {
+          const int q = h * (MJ + NB) + MJ + y;
+          fb[h][y] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo[q], hi[q], 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      }
+      if (do_db && wi == 0) {  // (X3F: dY_hi + dY_lo)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dbp[x] += (float)fa[x][e];
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int x = 0; x < MJ; ++x)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dbp[x] += (float)fa[h][x][e];
       }
 #pragma unroll
       for (int tt = 0; tt < NTW; ++tt) {
@@ -937,7 +972,14 @@ __global__ __launch_bounds__(WJW * WIW * 64) void wgrad_big(WgradArgs a_) {
 #pragma unroll
         for (int x = 0; x < MJ; ++x)
 #pragma unroll
-          for (int y = 0; y < MI; ++y) acc[x][tt * MI + y] = mfma_bf16x(fa[x], fb[tt * MI + y], acc[x][tt * MI + y]);
+          for (int y = 0; y < MI; ++y) {
+            f32x4& d = acc[x][tt * MI + y];
+            d = mfma_bf16x(fa[0][x], fb[0][tt * MI + y], d);
+            if (X3F) {  // dY_lo X_hi + dY_hi X_lo
+              d = mfma_bf16x(fa[NH - 1][x], fb[0][tt * MI + y], d);
+              d = mfma_bf16x(fa[0][x], fb[NH - 1][tt * MI + y], d);
+            }
+          }
       }
     }
     // stage t + 1 must have landed: at most NST - 2 later stages still in flight
@@ -1413,6 +1455,18 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   if (bigv && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
     if (taps9) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
+  }
+  static const int x3f = getenv("F3_X3F") ? atoi(getenv("F3_X3F")) : 1;  // A/B (temporary)
+  if (x3f && bigv && a.x3seg && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && (a.g.Nc < 128 || a.g.Kc < 128)) {
+    // bf16x3 on the 64-wide tiles: the three row segments fused into one staging (X3F); the
+    // 64-channel 9-tap layers in groups of taps
+    WgradArgs af = a;
+    af.x3seg = 0;
+    if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2, 32, 1, 3, true>>(af, s);
+    if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4, 32, 1, 3, true>>(af, s);
+    if (taps9 && x3f == 3) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 3, 3, true>, 3>(af, s);
+    if (taps9 && x3f == 2) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 2, 3, true>, 2>(af, s);
+    return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 1, 3, true>>(af, s);
   }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);
