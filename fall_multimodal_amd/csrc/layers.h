@@ -46,7 +46,7 @@ struct MixArgs {
   const unsigned short* dzb;  // bwd: dZ in bf16 (instead of z) — LDS mix path only
   int no_colsum;         // bwd: leave the dA partial rows in `part` (caller reduces: f3_mix_bwd_parts)
   int x3;                // bf16x3 mode: fp32 x / z / dz on the split-bf16 MFMA kernels (mix_*_x3)
-  unsigned short* z3;    // bf16x3 fwd: Z as rows [hi | lo] of 2 K Cin bf16 (the K-concatenated gcn
+  unsigned short* z3;    // bf16x3 fwd: Z as rows [hi | lo] of 2 K Cin bf16 (the bf16x3 gcn
                          // GEMM / weight-gradient operand) instead of fp32 z
 };
 constexpr int kMixParts = 1024;
@@ -115,7 +115,7 @@ struct BlockArgs {
   unsigned short* dhb;   // bf16 mode: dh written as bf16 (GEMM operand) instead of fp32
   unsigned short* dresb; // bf16 mode, conv residual: dr as bf16 instead of fp32
   int x3;                // bf16x3 mode: dhb, dresb (backward) and outb (forward) receive rows
-                         // [hi | lo] of 2C bf16 (the K-concatenated GEMM operands)
+                         // [hi | lo] of 2C bf16 (the bf16x3 GEMM operands)
   float* dgamma2;
   float* dbeta2;
   // deterministic reductions: per-chunk partial rows of pool (forward, [chunks][N*C]) and of P1, P2,

@@ -1137,7 +1137,7 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
           ob[e] = (__bf16)o[e];
           lb[e] = (__bf16)(o[e] - (float)ob[e]);
         }
-        if (a.x3) {  // row [hi | lo] of 2C: the next block's K-concatenated residual-conv operand
+        if (a.x3) {  // row [hi | lo] of 2C: the next block's bf16x3 residual-conv operand
           __bf16* row = reinterpret_cast<__bf16*>(a.outb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = ob;
           *reinterpret_cast<bf16x4*>(row + C) = lb;
@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
           hb[e] = (__bf16)dh[e];
           lb[e] = (__bf16)(dh[e] - (float)hb[e]);
         }
-        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated tcn operand), lo = RNE bf16(dh - hi)
+        if (a.x3) {  // row [hi | lo] of 2C (the bf16x3 tcn operand), lo = RNE bf16(dh - hi)
           __bf16* row = reinterpret_cast<__bf16*>(a.dhb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = hb;
           *reinterpret_cast<bf16x4*>(row + C) = lb;
@@ -1330,7 +1330,7 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
           rb[e] = (__bf16)dr[e];
           rl[e] = (__bf16)(dr[e] - (float)rb[e]);
         }
-        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated residual dgrad / wgrad operand)
+        if (a.x3) {  // row [hi | lo] of 2C (the bf16x3 residual dgrad / wgrad operand)
           __bf16* row = reinterpret_cast<__bf16*>(a.dresb) + 2 * (off[u] - c0) + c0;
           *reinterpret_cast<bf16x4*>(row) = rb;
           *reinterpret_cast<bf16x4*>(row + C) = rl;
@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(BnBwdArgs a) {
           ob[e] = (__bf16)o[e];
           lb[e] = (__bf16)(o[e] - (float)ob[e]);
         }
-        if (a.x3) {  // row [hi | lo] of 2C (the K-concatenated gcn dgrad / wgrad operand)
+        if (a.x3) {  // row [hi | lo] of 2C (the bf16x3 gcn dgrad / wgrad operand)
           __bf16* row = reinterpret_cast<__bf16*>(a.dgb) + 2 * (off - c0) + c0;
           *reinterpret_cast<bf16x8*>(row) = ob;
           *reinterpret_cast<bf16x8*>(row + C) = lb;
@@ -2056,7 +2056,7 @@ static bool mix_x3_ok(const MixArgs& a) {
          a.V <= 32;
 }
 
-// bf16x3 K-concatenated operand rows: out[r] = [hi | lo] of x[r] (2C bf16), hi = RNE bf16(x),
+// bf16x3 operand rows: out[r] = [hi | lo] of x[r] (2C bf16), hi = RNE bf16(x),
 // lo = RNE bf16(x - hi). One thread per 4 channels: a 16-B read, two 8-B writes.
 __global__ __launch_bounds__(256) void split_x3cat_kernel(const float* __restrict__ x, __bf16* __restrict__ out,
                                                           long long n4, int C4) {

@@ -395,7 +395,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       const size_t Mi = (size_t)N * L.T_in * V, Mo = (size_t)N * L.T_out * V;
       const int C = L.cout, Ci = L.cin;
       // bf16x3 with the split-bf16 graph mix (Ci = 64 / 128 / 256): the gcn GEMM operands Z and dg
-      // as rows [hi | lo] of 2 K Ci / 2C bf16 (the fp32 slot), the packed weights K-concatenated
+      // as rows [hi | lo] of 2 K Ci / 2C bf16 (the fp32 slot), the packed weights in the native form
       const bool gcat = x3 && f3_mix_x3_ok(K, V, Ci);
       X.x = xin;
       X.xb = xinb;
@@ -409,14 +409,15 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.q1 = A.take<float>((size_t)N * C / 4);
       X.hid = A.take<float>((size_t)N * C / 4);
       X.att = A.take<float>((size_t)N * C);
-      X.gw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * (gcat ? 3 : 2)));
-      X.gwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * (gcat ? 3 : 2)));
-      // bf16x3: the tcn weights K-concatenated [hi | hi | lo] per tap (3 C 9 C bf16 = 1.5x the fp32 slot)
-      X.tw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
-      X.twT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * (x3 ? 3 : 2)));
-      if (L.res == RES_CONV) {  // (bf16x3: K-concatenated, 3 C Ci bf16)
-        X.rw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * (x3 ? 3 : 2)));
-        X.rwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * (x3 ? 3 : 2)));
+      // packed GEMM weights: the fp32 slot (2 bf16 per weight) holds every form: fp32, bf16, the split
+      // hi / lo planes, and the bf16x3 native [W_hi 32 | W_lo 32] blocks (prep code 4)
+      X.gw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * 2));
+      X.gwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * K * Ci * 2));
+      X.tw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * 2));
+      X.twT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * 9 * C * 2));
+      if (L.res == RES_CONV) {
+        X.rw = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * 2));
+        X.rwT = reinterpret_cast<float*>(A.take<unsigned short>((size_t)C * Ci * 2));
       }
       X.aeff = A.take<float>((size_t)K * V * V);
       X.beff = A.take<float>((size_t)V * C);
@@ -550,7 +551,7 @@ inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X
 // chip. Measured (bf16x3 step): 10.17 -> 10.07 ms at 50 or 75 %, flat over 50-90 % and the first split
 // layer 0-2 (profiles/r04_ntw_ab.txt, r04_frac_ab.txt)
 inline int side_pct(bool split, int l) { return split && l >= 2 ? 75 : 0; }
-// bf16x3: the first block's gcn (Cin = 3: a 9-column GEMM, too narrow for the K-concatenated kernels)
+// bf16x3: the first block's gcn (Cin = 3: a 9-column GEMM, too narrow for the bf16 implicit-GEMM kernels)
 // runs on layer0.hip's fused kernels in their fp32 form (mix + GEMM + bias + BN1 sums in one pass;
 // backward dZ, dx, dA and dW partials in one pass): 10.14 -> 9.92 ms/step against the generic mix +
 // split GEMMs (profiles/r04_gcn0_x3_ab.txt)
@@ -1687,7 +1688,7 @@ int f3_pointwise_conv(const void* x, const void* wpack, const float* bias, void*
   return f3_igemm_bf16(&a, epi, (hipStream_t)stream);
 }
 
-// ---- bf16x3 on the bf16 kernels, as the step launches them (K-concatenated operands) ----
+// ---- bf16x3 on the bf16 kernels, as the step launches them ([hi | lo] operand rows, native form) ----
 int f3_split_x3cat(const float* x, void* out, int64_t rows, int C, void* stream) {
   if (!x || !out || rows < 0 || C <= 0 || C % 4) return F3_EINVAL;
   return f3_split_x3(x, static_cast<unsigned short*>(out), rows, C, (hipStream_t)stream);
