@@ -57,13 +57,15 @@ typedef __attribute__((address_space(3))) const char lds_cchar_t;
 template <int WM, int WN, int WIN = 0>
 struct BigCfg {
   static constexpr int BM = 16 * BG_MT * WM, BN = 16 * BG_NT * WN;
-  static constexpr int CPW = WIN == 144 ? 2 : 1;                 // WIN: clips per workgroup
+  static constexpr int NW = WM * WN;                                // waves
+  // WIN: clips per workgroup (WIN = 144 with 4 waves: one clip x 128 channels, two workgroups per CU)
+  static constexpr int CPW = WIN == 144 && WM == 2 ? 2 : 1;
   static constexpr int NPA = (CPW * WIN + 7) / 8;                // WIN: A pieces per window
-  static constexpr int NST = WIN == 540 ? 2 : BG_NST, LA = NST - 1;  // weight stages, steps issued ahead
+  static constexpr int NST = (WIN == 540 || (WIN == 144 && WM == 1)) ? 2 : BG_NST, LA = NST - 1;  // weight stages, issued ahead
   // 1-KiB pieces per stage: A then B (WIN: slots for the next window's carried A pieces, <= 12 used
   // at two steps ahead, <= 8 at one)
-  static constexpr int AP = WIN ? (WIN == 540 ? 8 : 16) : BM / 8, BP = BN / 8, NP = AP + BP;
-  static constexpr int PPW = (NP + BG_WAVES - 1) / BG_WAVES;              // pieces per wave
+  static constexpr int AP = WIN ? (WIN == 540 || WM == 1 ? 8 : 16) : BM / 8, BP = BN / 8, NP = AP + BP;
+  static constexpr int PPW = (NP + NW - 1) / NW;                          // pieces per wave
   static constexpr int STAGE = WIN ? BN * 128 : NP * 1024;
   static constexpr int AWIN = NPA * 1024;            // one A window buffer (WIN: two of them)
   static constexpr int SOFF = 2 * AWIN;              // byte offset of the per-step stages
@@ -78,13 +80,15 @@ struct BigCfg {
 // X3N: the bf16x3 native form (ConvGemmArgs::x3n): a k step is one 32-channel block, its staged row
 // piece [x_hi 32 | x_lo 32] / [W_hi 32 | W_lo 32], and the wave issues x_hi W_hi + x_lo W_hi + x_hi W_lo
 template <int EPI, int WM, int WN, int WIN = 0, bool X3N = false>
-__global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
+__global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
-  static_assert(WIN == 0 || ((WIN == 144 || WIN == 270) && WM == 2 && WN == 4) || (WIN == 540 && WM == 4 && WN == 2),
+  constexpr int NW = WM * WN, NT = 64 * NW;  // waves, threads
+  static_assert(WIN == 0 || ((WIN == 144 || WIN == 270) && WM == 2 && WN == 4) || (WIN == 540 && WM == 4 && WN == 2) ||
+                    (WIN == 144 && WM == 1 && WN == 4),
                 "WIN layout");
   static_assert(BG_MT * 16 == 144, "a wave owns 144 rows");
   constexpr int BM = Cfg::BM, BN = Cfg::BN, AP = Cfg::AP, NP = Cfg::NP, PPW = Cfg::PPW, STAGE = Cfg::STAGE;
-  static_assert(WM * WN == BG_WAVES, "wave grid");
+  static_assert(NW == BG_WAVES || (WIN == 144 && NW == 4), "wave grid");
   static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
   // ONE shared array (a second __shared__ object can de-pipeline LDS-DMA code)
   __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
   const unsigned short* wb = a.wb;
 
   if (EPI & EPI_RELUMASK) {
-    for (int t = tid; t < BN; t += BG_THREADS) {
+    for (int t = tid; t < BN; t += NT) {
       float sc, sh, mu, rs;
       bn_coeff(a.epi_bn, n0 + t, sc, sh, mu, rs);
       epi_sc[t] = sc; epi_sh[t] = sh; epi_mu[t] = mu; epi_rs[t] = rs;
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (WIN != 0) {
     constexpr int CL = WIN, NPA = Cfg::NPA;  // window rows per clip, A pieces per window
-    static_assert(Cfg::BP % BG_WAVES == 0 && PPW * BG_WAVES == Cfg::NP, "slots: B pieces, then A pieces");
+    static_assert(Cfg::BP % NW == 0 && PPW * NW == Cfg::NP, "slots: B pieces, then A pieces");
     const int V = g.V, P = g.P, TVin = g.T_in * V;
     // taps of window q (q = input-frame parity for the stride-2 forward, else 0): dt = d0 + ds j,
     // j < nt, frame shift s0 + ss j. (Pairs of scalars, not arrays: a runtime-indexed private array
@@ -246,10 +250,10 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       return in + (size_t)row * g.lda + acolx(c * CB, swz(R, pch));
     };
     // the lane's B piece offsets (slots i < BP / 8; the A slots follow)
-    size_t boffw[Cfg::BP / BG_WAVES];
+    size_t boffw[Cfg::BP / NW];
 #pragma unroll
-    for (int i = 0; i < Cfg::BP / BG_WAVES; ++i) {
-      const int r = (wave + BG_WAVES * i) * 8 + sub;
+    for (int i = 0; i < Cfg::BP / NW; ++i) {
+      const int r = (wave + NW * i) * 8 + sub;
       boffw[i] = (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
     }
     // Per step every wave issues PPW DMAs: its B pieces of the step's weight stage, then A pieces of
@@ -275,11 +279,11 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       for (int i = 0; i < PPW; ++i) {
         const void* src;
         char* dst;
-        if (i < Cfg::BP / BG_WAVES) {
+        if (i < Cfg::BP / NW) {
           src = wb + boffw[i] + k0;
-          dst = sbase + (wave + BG_WAVES * i) * 1024;
+          dst = sbase + (wave + NW * i) * 1024;
         } else {
-          const int sl = wave + BG_WAVES * i - Cfg::BP, pa = kk * na + sl;
+          const int sl = wave + NW * i - Cfg::BP, pa = kk * na + sl;
           src = a.zero;
           dst = smem + Cfg::DOFF;
           if (car && sl < na && pa < NPA) {
@@ -291,10 +295,10 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       }
     };
     // window 0's A rows, then steps 0 and 1
-    constexpr int A0W = (NPA + BG_WAVES - 1) / BG_WAVES;
+    constexpr int A0W = (NPA + NW - 1) / NW;
 #pragma unroll
     for (int i = 0; i < A0W; ++i) {
-      const int pa = (wave + BG_WAVES * i) % NPA;
+      const int pa = (wave + NW * i) % NPA;
       const void* src = asrc(0, 0, pa);
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
     // the second-dispatched half of the workgroup (waves 4-7, the SIMD partners of 0-3) at a higher
     // issue priority for the whole loop: it loses every arbitration otherwise (MI355X_MICROARCH.md,
     // "two waves per SIMD" item 4); F3_PROBE bit 8 (probe builds) leaves it off
-    if (!(F3_PROBE & 8) && wave >= BG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
+    if (!(F3_PROBE & 8) && NW == BG_WAVES && wave >= BG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
     int c = 0, q = 0, j = 0;  // the step computed
     for (int u = 0; u < nstep; ++u) {
       const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(BG_THREADS) void igemm_big(ConvGemmArgs a) {
       }
     }
     __syncthreads();
-    for (int t = tid; t < BN; t += BG_THREADS) {
+    for (int t = tid; t < BN; t += NT) {
       if (n0 + t >= g.Nc) continue;
       float s0 = 0.f, s1 = 0.f, g0 = 0.f, g1 = 0.f;
 #pragma unroll
@@ -683,15 +687,17 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
 
 bool f3_igemm_big_win_ok(const ConvGemmArgs& a) { return f3_igemm_big_ok(a) && big_win_rows(a) != 0; }
 
-template <int CL>
+// W4 (WIN = 144 only): the 4-wave form, one clip x 128 channels per workgroup and two workgroups per
+// CU, whose independent barriers interleave one workgroup's fragment reads with the other's MFMAs
+template <int CL, bool W4 = false>
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
-  constexpr int CPW = CL == 144 ? 2 : 1, WM = CL == 540 ? 4 : 2, WN = CL == 540 ? 2 : 4;
+  constexpr int WM = CL == 540 ? 4 : W4 ? 1 : 2, WN = CL == 540 ? 2 : 4, CPW = BigCfg<WM, WN, CL>::CPW;
   const int nclip = a.g.M / (a.g.T_out * a.g.V);
   const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / (32 * WN));
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
-    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, false>), dim3(tiles), dim3(BG_THREADS), 0, s, a);     \
+    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, false>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);     \
     F3_LAUNCH_CHECK();                                                                                \
     return F3_OK;                                                                                     \
   }
@@ -709,7 +715,8 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   const int wrows = big_win_rows(a);
   if (wrows) {
-    const int r = wrows == 144 ? launch_win<144>(a, epi, s)
+    static const bool w4 = getenv("F3_WIN4") && atoi(getenv("F3_WIN4")) != 0;  // A/B (temporary)
+    const int r = wrows == 144 ? (w4 ? launch_win<144, true>(a, epi, s) : launch_win<144>(a, epi, s))
                   : wrows == 270 ? launch_win<270>(a, epi, s) : launch_win<540>(a, epi, s);
     if (r != F3_EINVAL) return r;
   }
