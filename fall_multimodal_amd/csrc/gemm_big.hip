@@ -21,8 +21,9 @@
 #include "igemm.h"
 
 // F3_PROBE (tools/probe_build.sh only; 0 in the library): bit 1 drops the window loop's MFMAs, bit 2
-// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone; bit 8 the
-// static priority of waves 4-7. (Measured
+// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone. (A static
+// issue priority for waves 4-7, MI355X_MICROARCH.md "two waves per SIMD" item 4, measured within
+// noise on l1d / l5d / l8d / l8f: profiles/r05_window_prio_ab.txt.) (Measured
 // on l8d with this loop: 126 us full, 77 without MFMA, 55 without MFMA and DMA: the legs add up almost
 // linearly. A software-pipelined loop (next step's hi fragments read under the current step's lo
 // products) and a ping-pong of the SIMD partner waves (one loads while the other multiplies) were
@@ -333,10 +334,6 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
         const int r = wn * 32 + y * 16 + fr;
         boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
       }
-    // the second-dispatched half of the workgroup (waves 4-7, the SIMD partners of 0-3) at a higher
-    // issue priority for the whole loop: it loses every arbitration otherwise (MI355X_MICROARCH.md,
-    // "two waves per SIMD" item 4); F3_PROBE bit 8 (probe builds) leaves it off
-    if (!(F3_PROBE & 8) && NW == BG_WAVES && wave >= BG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
     int c = 0, q = 0, j = 0;  // the step computed
     for (int u = 0; u < nstep; ++u) {
       const int t = lo0 + fr + ((q ? s01 : s00) + ss * j) * V;  // lane's tile-0 row in the clip, tap-shifted

@@ -1456,16 +1456,15 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
     if (taps9) return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 3>, 3>(a, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2>>(a, s);
   }
-  static const int x3f = getenv("F3_X3F") ? atoi(getenv("F3_X3F")) : 1;  // A/B (temporary)
-  if (x3f && bigv && a.x3seg && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && (a.g.Nc < 128 || a.g.Kc < 128)) {
-    // bf16x3 on the 64-wide tiles: the three row segments fused into one staging (X3F); the
-    // 64-channel 9-tap layers in groups of taps
+  if (bigv && a.x3seg && a.g.Nc % 64 == 0 && a.g.Kc % 64 == 0 && (a.g.Nc < 128 || a.g.Kc < 128)) {
+    // bf16x3 on the 64-wide tiles: the three row segments fused into one staging (X3F, 32-row
+    // stages: 48 KiB, three workgroups per CU). The 64-channel T=30 tcn weight gradient alone: 97.4 ->
+    // 77.0 us, step 8.83-8.86 -> 8.73 ms; tap groups of 2 / 3 on top measured 87 / 110 us (fewer
+    // workgroups per CU), profiles/r05_x3f_ab.txt
     WgradArgs af = a;
     af.x3seg = 0;
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2, 32, 1, 3, true>>(af, s);
     if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4, 32, 1, 3, true>>(af, s);
-    if (taps9 && x3f == 3) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 3, 3, true>, 3>(af, s);
-    if (taps9 && x3f == 2) return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 2, 3, true>, 2>(af, s);
     return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 1, 3, true>>(af, s);
   }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
