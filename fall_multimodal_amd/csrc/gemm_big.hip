@@ -684,8 +684,9 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
 
 bool f3_igemm_big_win_ok(const ConvGemmArgs& a) { return f3_igemm_big_ok(a) && big_win_rows(a) != 0; }
 
-// W4 (WIN = 144 only): the 4-wave form, one clip x 128 channels per workgroup and two workgroups per
-// CU, whose independent barriers interleave one workgroup's fragment reads with the other's MFMAs
+// W4 (WIN = 144 only): a 4-wave form, one clip x 128 channels per workgroup, meant to run two
+// independent workgroups per CU. Measured 1.5-1.75x SLOWER alone (l8d 134 -> 235 us) and the step
+// 8.73 -> 9.36 ms (profiles/r05_win4_ab.txt); not dispatched, kept as the template's 4-wave case.
 template <int CL, bool W4 = false>
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int WM = CL == 540 ? 4 : W4 ? 1 : 2, WN = CL == 540 ? 2 : 4, CPW = BigCfg<WM, WN, CL>::CPW;
@@ -712,8 +713,7 @@ int f3_igemm_big(const ConvGemmArgs* args, int epi, hipStream_t s) {
   if (!f3_igemm_big_ok(a)) return F3_EINVAL;
   const int wrows = big_win_rows(a);
   if (wrows) {
-    static const bool w4 = getenv("F3_WIN4") && atoi(getenv("F3_WIN4")) != 0;  // A/B (temporary)
-    const int r = wrows == 144 ? (w4 ? launch_win<144, true>(a, epi, s) : launch_win<144>(a, epi, s))
+    const int r = wrows == 144 ? launch_win<144>(a, epi, s)
                   : wrows == 270 ? launch_win<270>(a, epi, s) : launch_win<540>(a, epi, s);
     if (r != F3_EINVAL) return r;
   }
