@@ -1446,6 +1446,15 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
   // rounds; 3-tap groups for the 64 x 64 tiles and 4-stage rings gave nothing (profiles/r04_ntw_ab.txt,
   // r04_last_ab.txt, r04_nst4_ab.txt)
   const bool taps9 = a.g.KT == 9;
+  if (bigv && a.x3seg && !taps9 && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
+    // the 128 / 256-channel 1x1 (gcn, residual) bf16x3 weight gradients with the row segments fused (X3F):
+    // 128 B of LDS fill per MFMA instead of 192 (profiles/r05_x3f8_ab.txt: step 8.75 -> 8.66 ms)
+    WgradArgs af = a;
+    af.x3seg = 0;
+    if (a.g.Nc % 256 == 0) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 1, 3, true>>(af, s);
+    if (a.g.Kc % 256 == 0) return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4, 32, 1, 3, true>>(af, s);
+    return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 1, 3, true>>(af, s);
+  }
   if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
     if (taps9) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
