@@ -417,47 +417,45 @@ def sensor_bench(dev, precision="fp32"):
 
 
 def cnn1d_stage_times(model, step, x, lab, B, S, T=30, reps=20):
-    """GB/s of the sensor CNN1D launches (GSTCAN_UR_conv.ipynb:493-514: Conv1d(S->16,k5) BN ReLU
-    MaxPool, Conv1d(16->32,k5) BN ReLU MaxPool), from HIP events around each launch on the sensor
-    queue (f3_net_sensor_times), mean over `reps` steps. Since round 4 the two layers run as six
-    fused launches (sensor.hip cnn_f*/cnn_b*: BN1 + ReLU + pool1 in conv2's load, pool1's backward
-    behind conv2's, BatchNorm sums as per-workgroup partial rows added by the next launch). Algorithmic
-    bytes (fp32, each tensor once): conv1 fwd x + w1 + y1; pool1+conv2 fwd y1 + p1 + w2 + y2; pool2 fwd
-    y2 + p2; pool2 bwd y2 + dp2 + dy2; conv2+pool1 bwd y2 + dy2 + p1 + w2 + dW2 + y1 + dy1; conv1 bwd
-    y1 + dy1 + x + dW1. The tensors are 0.02-1 MB, so these launches are latency-bound (a few us each)."""
+    """Time of the sensor CNN1D (GSTCAN_UR_conv.ipynb:493-514: Conv1d(S->16,k5) BN ReLU MaxPool,
+    Conv1d(16->32,k5) BN ReLU MaxPool) in the training step, from HIP events around its launches on
+    the sensor queue (f3_net_sensor_times), mean over `reps` steps. Since round 5 each direction is
+    ONE cooperative launch (sensor.hip cnn1d_coop_*: the BatchNorm statistics and weight gradients
+    reduced across workgroups after group barriers). Algorithmic bytes (fp32, each tensor once):
+    forward x + w1 + y1 + p1 + w2 + y2 + p2; backward dp2 + y2 + dy2 + p1 + w2 + dW2 + y1 + dy1 + x +
+    dW1. The tensors are 0.02-1 MB, so the launches are latency-bound (barriers, not bytes)."""
     import ctypes
     import fall_multimodal_amd._lib as FL
     L, check = FL.lib(), FL.check
     h = model._native.h
     f32 = 4
-    acc = [0.0] * 6
+    acc = [0.0] * 2
     check(L.f3_net_sensor_times(h, 1, None), "sensor times on")
     for _ in range(3):
         step(None, x, lab)
     torch.cuda.synchronize()
-    ms = (ctypes.c_float * 6)()
+    ms = (ctypes.c_float * 2)()
     for _ in range(reps):
         step(None, x, lab)
         check(L.f3_net_sensor_times(h, 1, ms), "sensor times")
-        for i in range(6):
+        for i in range(2):
             acc[i] += ms[i] / reps
     check(L.f3_net_sensor_times(h, 0, None), "sensor times off")
     T2, T3 = T // 2, (T // 2) // 2
     xb, y1, p1, y2, p2 = (B * T * S * f32, B * T * 16 * f32, B * T2 * 16 * f32, B * T2 * 32 * f32,
                           B * T3 * 32 * f32)
     w1, w2 = 16 * S * 5 * f32, 32 * 16 * 5 * f32
-    nbytes = {"conv1_fwd": xb + w1 + y1, "pool1_conv2_fwd": y1 + p1 + w2 + y2, "pool2_fwd": y2 + p2,
-              "pool2_bwd": y2 + p2 + y2, "conv2_pool1_bwd": 2 * y2 + p1 + 2 * w2 + 2 * y1,
-              "conv1_bwd": 2 * y1 + xb + w1}
+    nbytes = {"forward": xb + w1 + y1 + p1 + w2 + y2 + p2,
+              "backward": p2 + 2 * y2 + p1 + 2 * w2 + 2 * y1 + xb + 2 * w1}
     out = {}
     for i, nm in enumerate(nbytes):
         us = acc[i] * 1e3
         out[nm] = {"us": round(us, 2), "bytes": nbytes[nm], "GBps": round(nbytes[nm] / (us * 1e-6) / 1e9, 1)}
     out["total_us"] = round(sum(acc) * 1e3, 2)
     out["batch"] = B
-    out["form"] = "six launches (conv1 | BN1+ReLU+pool1 | conv2 | BN2+ReLU+pool2, and their backward)"
-    out["note"] = ("HIP events around each stage on the sensor queue (a stage may hold several launches); "
-                   "latency-bound (tensors of 0.02-1 MB): GB/s against 8 TB/s is not a meaningful fraction here")
+    out["form"] = "one cooperative launch per direction (group barriers for the BatchNorm statistics)"
+    out["note"] = ("HIP events around the launch on the sensor queue; latency-bound (tensors of 0.02-1 MB): "
+                   "GB/s against 8 TB/s is not a meaningful fraction here")
     return out
 
 

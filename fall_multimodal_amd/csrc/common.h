@@ -88,6 +88,34 @@ F3_DEV float ld_act(const void* p, size_t off, bool b16) {
   return b16 ? bf2f(reinterpret_cast<const unsigned short*>(p)[off]) : reinterpret_cast<const float*>(p)[off];
 }
 
+// Group barrier of co-resident workgroups (cooperative launches: the TARGCN node-partitioned GRU,
+// the sensor CNN1D). Every workgroup of the group adds 1 to *cnt and waits until it reaches
+// `target` (k x group size at the k-th barrier; *cnt zeroed before the launch). `arrive` false:
+// this workgroup does not count itself (the F3_GN_SKIP_ARRIVE test knob, which makes the group's
+// barriers time out). A barrier that does not complete within ~2^22 polls sets *err and stops
+// waiting; once *err is set, every later barrier returns after the first poll that sees it, so a
+// faulted launch drains quickly (the caller reports or poisons its outputs).
+F3_DEV void gn_barrier(int* cnt, int target, int* err, bool arrive = true) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's exchange stores have reached L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // agent-scope release: the group's other XCDs see the stores
+    if (arrive) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int polls = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      ++polls;
+      if ((polls & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (polls > (1 << 22)) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __threadfence();  // acquire: no stale lines of the exchanged rows survive in this CU / XCD
+  }
+  __syncthreads();
+}
+
 }  // namespace f3
 
 // Error plumbing for the C ABI: never abort, return a status.

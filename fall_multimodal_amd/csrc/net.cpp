@@ -91,10 +91,10 @@ struct f3_net {
   hipEvent_t ev_p1[4] = {nullptr, nullptr, nullptr, nullptr};
   int p1_mask = 0;  // bit i: ev_p1[i] recorded by the last phase-1 backward
   bool par_init = false, par_ok = false;
-  // f3_net_sensor_times: events around the sensor CNN1D launches (0 = off). Forward
-  // 0 | conv1 | 1 | pool1 + conv2 | 2 | pool2 | 3, backward 4 | pool2' | 5 | conv2' + pool1' | 6 | conv1' | 7
+  // f3_net_sensor_times: events around the sensor CNN1D launches (0 = off): 0 | forward | 1,
+  // 2 | backward | 3
   int stiming = 0;
-  hipEvent_t sev[8] = {};
+  hipEvent_t sev[4] = {};
   void smark(int i, hipStream_t s) {
     if (stiming && sev[i]) (void)hipEventRecord(sev[i], s);
   }
@@ -300,6 +300,8 @@ struct Ws {
   // sensor
   float *y1, *p1, *y2, *p2, *dy1, *dp1, *dy2, *dp2;
   BnWs cbn1, cbn2, sbn;
+  float* cpart = nullptr;                          // cooperative CNN1D partial rows
+  int *csyncf = nullptr, *csyncb = nullptr;        // its barrier counter + error flag (zeroed regions)
   float *seq, *gates, *cell, *hmean, *ybn, *a1, *satt, *sout, *sdy, *sdpre2, *sdpre1, *dhmean;
   float* lwpart;  // LSTM weight-gradient partial rows (LstmArgs::wpart)
   // head
@@ -351,6 +353,7 @@ Ws plan(const f3_net& net, int N, char* base) {
     if (cnn) {
       bn_take(A, w.cbn1, 16);
       bn_take(A, w.cbn2, 32);
+      w.csyncf = A.take<int>(f3_cnn1d_coop_sync_ints());
     }
     bn_take(A, w.sbn, 128);
   }
@@ -377,6 +380,7 @@ Ws plan(const f3_net& net, int N, char* base) {
   if (net.has_sensor && cnn) {
     bn_take_b(A, w.cbn1, 16);
     bn_take_b(A, w.cbn2, 32);
+    w.csyncb = A.take<int>(f3_cnn1d_coop_sync_ints());
     w.dp2 = A.take<float>((size_t)N * Tl * 32);
   }
   w.zb1 = A.take<char>(0);
@@ -471,6 +475,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       w.dy1 = A.take<float>((size_t)N * Ts * 16);
       w.dp1 = A.take<float>((size_t)N * (Ts / 2) * 16);
       w.dy2 = A.take<float>((size_t)N * (Ts / 2) * 32);
+      w.cpart = A.take<float>(f3_cnn1d_coop_part_floats(N, net.cfg.sensor_dim, 16, 32));
     }
     w.seq = A.take<float>((size_t)N * Tl * 128);
     w.gates = A.take<float>((size_t)2 * N * Tl * 256);
@@ -1309,14 +1314,10 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
     Conv1dArgs c1, c2;
     sensor_args(*net, N, training, q, w, w.sensor, la, sa, c1, c2);
     if (net->has_cnn) {
+      const CnnCoop coop{w.cpart, w.csyncf};
       net->smark(0, ss);
-      F3_TRY(f3_conv1d_fwd(&c1, ss));
-      F3_TRY(f3_bnrelupool_fwd(&c1, ss));
+      F3_TRY(f3_cnn1d_fwd(&c1, &c2, &coop, ss));
       net->smark(1, ss);
-      F3_TRY(f3_conv1d_fwd(&c2, ss));
-      net->smark(2, ss);
-      F3_TRY(f3_bnrelupool_fwd(&c2, ss));
-      net->smark(3, ss);
       if (training) {
         add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
         add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
@@ -1541,12 +1542,10 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     F3_TRY(f3_shead_bwd(&sa, ss));
     F3_TRY(f3_lstm_bwd(&la, ss));
     if (net->has_cnn) {
-      net->smark(4, ss);
-      net->smark(5, ss);
-      F3_TRY(f3_conv1d_bwd(&c2, ss));
-      net->smark(6, ss);
-      F3_TRY(f3_conv1d_bwd(&c1, ss));
-      net->smark(7, ss);
+      const CnnCoop coop{w.cpart, w.csyncb};
+      net->smark(2, ss);
+      F3_TRY(f3_cnn1d_bwd(&c1, &c2, &coop, ss));
+      net->smark(3, ss);
     }
     return F3_OK;
   };
@@ -1570,10 +1569,10 @@ int f3_net_sensor_times(f3_net* net, int enable, float* ms) {
     for (auto& e : net->sev)
       if (!e && hipEventCreate(&e) != hipSuccess) return F3_EHIP;
   }
-  if (ms) {  // fwd: conv1 | pool1 + conv2 | pool2; bwd: pool2' | conv2' + pool1' | conv1' (ms)
+  if (ms) {  // forward, backward (ms)
     if (!net->stiming) return F3_ESTATE;
-    const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}};
-    for (int i = 0; i < 6; ++i) {
+    const int pairs[2][2] = {{0, 1}, {2, 3}};
+    for (int i = 0; i < 2; ++i) {
       if (hipEventSynchronize(net->sev[pairs[i][1]]) != hipSuccess ||
           hipEventElapsedTime(&ms[i], net->sev[pairs[i][0]], net->sev[pairs[i][1]]) != hipSuccess)
         return F3_EHIP;

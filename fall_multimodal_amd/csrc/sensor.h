@@ -76,6 +76,18 @@ struct Conv1dArgs {
   float* dx;                  // [N][T][Ci] (=) or null
 };
 
+// The two CNN1D layers as ONE cooperative launch per direction (f3_cnn1d_fwd / f3_cnn1d_bwd): a
+// workgroup per clip (up to kCnnCoopG, clips walked n = b, b + G, ...), the BatchNorm statistics and
+// the weight gradients reduced across workgroups in fixed order after group barriers (gn_barrier)
+// instead of separate launches and float atomics.
+constexpr int kCnnCoopG = 256;
+struct CnnCoop {
+  float* part;  // partial rows, f3_cnn1d_coop_part_floats(N, Ci1, Co1, Co2) floats
+  int* sync;    // f3_cnn1d_coop_sync_ints() ints: barrier counters, error flag; zero at launch
+};
+int f3_cnn1d_coop_sync_ints();
+size_t f3_cnn1d_coop_part_floats(int N, int Ci1, int Co1, int Co2);
+
 struct HeadArgs {
   int N, C, nblk;
   const float* feat[3];       // feature blocks [N][ld_k]
@@ -105,6 +117,10 @@ int f3_shead_bwd(const f3::SHeadArgs* a, hipStream_t s);
 int f3_conv1d_fwd(const f3::Conv1dArgs* a, hipStream_t s);
 int f3_bnrelupool_fwd(const f3::Conv1dArgs* a, hipStream_t s);
 int f3_conv1d_bwd(const f3::Conv1dArgs* a, hipStream_t s);
+// both CNN1D layers: the cooperative launch (training, `coop` given, not under stream capture,
+// F3_CNN1D_COOP unset or 1), else the per-layer launches above (eval, capture)
+int f3_cnn1d_fwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, const f3::CnnCoop* coop, hipStream_t s);
+int f3_cnn1d_bwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, const f3::CnnCoop* coop, hipStream_t s);
 int f3_head_fwd(const f3::HeadArgs* a, hipStream_t s);
 int f3_ce(const f3::HeadArgs* a, hipStream_t s);
 int f3_head_bwd(const f3::HeadArgs* a, hipStream_t s);

@@ -544,6 +544,443 @@ __global__ __launch_bounds__(C1D_THREADS) void conv1d_bwd_kernel(Conv1dArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// Cooperative CNN1D: both layers in one launch per direction. Workgroup b
+// (1024 threads) walks clips n = b, b + G, ... (G = min(N, kCnnCoopG, CUs): one workgroup per CU, so
+// all are resident while the chip is not held by other work; a barrier that cannot complete times out
+// instead of hanging, below). A BatchNorm's batch statistics need every clip, so each stage writes
+// per-workgroup partial rows, crosses a group barrier (coop_barrier), and every workgroup then sums
+// the G rows in the same fixed order (fp64): the coefficients are identical everywhere and run to
+// run. The weight / bias gradients are per-thread register partials over the workgroup's clips,
+// written as rows and summed per column across the G rows after the last barrier (no float
+// atomics). Per-clip tensors stay in the workspace (y1, p1, y2 for the backward; dy1 / dy2 are
+// re-read by the workgroup that wrote them). Forward: conv1 + stats | barrier | BN1 ReLU pool1 conv2
+// + stats | barrier | BN2 ReLU pool2. Backward: pool2' + stats | barrier | BN2' conv2' (dW2, dp1)
+// pool1' + stats | barrier | BN1' conv1' (dW1) | barrier | column sums. A barrier that times out sets
+// the error flag; the launch then writes NaN into its outputs (p2 / the weight gradients), so the
+// loss shows it. The per-clip loops are LDS-latency bound: a convolution output is split over Q
+// adjacent lanes (partial sums over input channels, combined by shuffles in lane order), and 16
+// waves per CU hide the LDS latency (4 waves per CU measured 2x slower).
+// ----------------------------------------------------------------------------
+// F3_PROBE (tools/probe_build.sh with SRC=sensor; timing only, results wrong): bit 1 the group
+// barriers reduced to a workgroup barrier, bit 2 the cross-workgroup partial-row loads skipped,
+// bit 4 the per-clip convolutions skipped
+#ifndef F3_PROBE
+#define F3_PROBE 0
+#endif
+constexpr int kCoopNT = 1024;                                  // threads per workgroup
+constexpr int kCoopWMAX = (C1D_WMAX * C1D_THREADS + kCoopNT - 1) / kCoopNT;  // weight-gradient elements per thread
+
+// Cross-workgroup exchange without cache maintenance: the partial rows are written and read with
+// agent-scope atomic stores / loads (they bypass the non-coherent per-XCD L2 line by line), so the
+// barrier needs no release / acquire fence (gn_barrier's agent-scope fences write back and
+// invalidate the XCD's L2 at every arrival). Everything else a workgroup reads after a barrier it
+// wrote itself (same CU).
+F3_DEV void xst(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+F3_DEV float xld(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of column c over rows r0, r0 + dr, ... < G of partial rows (width ld), in row order; the
+// agent-scope loads issued 16 at a time (each is a memory-side round trip)
+template <typename Acc>
+F3_DEV Acc coop_colsum(const float* part, int ld, int c, int r0, int dr, int G) {
+  Acc v = 0;
+  for (int r = r0; r < G; r += 16 * dr) {
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      x[j] = !(F3_PROBE & 2) && r + j * dr < G ? xld(part + (size_t)(r + j * dr) * ld + c) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v += (Acc)x[j];
+  }
+  return v;
+}
+
+// The k-th barrier (k = 1, 2, ...): arrivals are counted in groups of kCoopGS workgroups, each on its
+// own counter; the last arriver of a group adds 1 to the top counter, and the last group's last
+// arriver publishes k in the release word, which the others poll (same-address agent-scope atomics
+// serialize at the memory side). Words 256 B apart (sync layout: err | top | release | groups).
+constexpr int kCoopGS = 16;
+constexpr int kCoopSyncInts = 64 * (3 + kCnnCoopG / kCoopGS);
+F3_DEV void coop_barrier(int* sync, int k, int G) {
+  if (F3_PROBE & 1) {
+    __syncthreads();
+    return;
+  }
+  int* err = sync;
+  int* top = sync + 64;
+  int* rel = sync + 128;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's exchange stores are complete
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int g = blockIdx.x / kCoopGS, ng = (G + kCoopGS - 1) / kCoopGS;
+    const int gsz = min(kCoopGS, G - g * kCoopGS);
+    if (__hip_atomic_fetch_add(sync + 192 + 64 * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gsz - 1 &&
+        __hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * ng - 1)
+      __hip_atomic_store(rel, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int polls = 0;
+    while (__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++polls & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (polls > (1 << 22)) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+F3_DEV bool coop_failed(const int* sync) {
+  return __hip_atomic_load(const_cast<int*>(sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+struct CnnCoopArgs {
+  Conv1dArgs c1, c2;
+  float* part;
+  int* sync;
+  int G;
+};
+
+// lanes per output of a convolution over `red` reduced channels: 4, 2 or 1 (all outputs of a clip
+// in one pass where the workgroup has the threads)
+F3_DEV int coop_q(int outs, int red) {
+  if (outs * 4 <= kCoopNT && red % 4 == 0) return 4;
+  if (outs * 2 <= kCoopNT && red % 2 == 0) return 2;
+  return 1;
+}
+// the sum of v over the Q adjacent lanes of an output, added in lane order (lane q = 0 holds it)
+F3_DEV float coop_qsum(float v, int Q) {
+  if (Q == 1) return v;
+  const float v1 = __shfl_down(v, 1);
+  if (Q == 2) return v + v1;
+  const float v2 = __shfl_down(v, 2), v3 = __shfl_down(v, 3);
+  return ((v + v1) + v2) + v3;
+}
+
+// per-channel batch statistics from G partial rows [sum (C) | sumsq (C)] (fp64, row order), as
+// bn_coeff computes them; block 0 stores the sums for the running-statistics update
+F3_DEV void coop_bn_stats(const float* part, int G, int C, const BnRef& bn, double* st_sum, double* st_sq,
+                          float* co, double* red) {
+  const int tid = threadIdx.x, cols = 2 * C, ng = kCoopNT / cols, c = tid % cols, rg = tid / cols;
+  red[tid] = rg < ng ? coop_colsum<double>(part, cols, c, rg, ng, G) : 0.0;
+  __syncthreads();
+  if (tid < C) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int g = 0; g < ng; ++g) {
+      s1 += red[g * cols + tid];
+      s2 += red[g * cols + C + tid];
+    }
+    if (blockIdx.x == 0) {
+      st_sum[tid] = s1;
+      st_sq[tid] = s2;
+    }
+    const double m = s1 / (double)bn.count;
+    double var = s2 / (double)bn.count - m * m;
+    if (var < 0) var = 0;
+    const float mean = (float)m, rstd = (float)(1.0 / sqrt(var + (double)kBnEps));
+    const float sc = bn.gamma[tid] * rstd;
+    co[tid] = sc;                          // scale
+    co[C + tid] = bn.beta[tid] - mean * sc;  // shift
+    co[2 * C + tid] = mean;
+    co[3 * C + tid] = rstd;
+  }
+  __syncthreads();
+}
+
+// the block's per-thread channel partials -> row[0 .. C): thread tid's value belongs to channel
+// (tid / Q) % C (lanes q > 0 hold 0); summed in thread order
+F3_DEV void coop_rowsum(float v, float* row, float* red, int C, int Q = 1) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  red[tid] = v;
+  __syncthreads();
+  if (tid < C) {
+    float s = 0.f;
+    for (int i = tid * Q; i < kCoopNT; i += C * Q) s += red[i];
+    xst(row + tid, s);
+  }
+}
+
+// y = conv(x) + b for one clip: x [T][Ci], w [Co][Ci][5] in LDS; Q lanes per output split the input
+// channels; lane 0 of an output keeps its channel's sums (fixed per thread: kCoopNT / Q % Co == 0)
+F3_DEV void coop_conv(const float* xs, const float* ws, const float* b, int T, int Ci, int Co, int Q, float* y,
+                      float& s1, float& s2) {
+  const int tid = threadIdx.x, q = tid % Q, cn = Ci / Q, c0 = q * cn;
+  for (int i = tid / Q; i < T * Co; i += kCoopNT / Q) {  // (uniform trip count: T * Co * Q <= kCoopNT or a multiple)
+    const int t = i / Co, o = i - t * Co;
+    float acc = 0.f;
+    if (!(F3_PROBE & 4))
+      for (int k = 0; k < 5; ++k) {
+        const int ti = t + k - 2;
+        if (ti < 0 || ti >= T) continue;
+        const float* xr = xs + ti * Ci + c0;
+        const float* wr = ws + (o * Ci + c0) * 5 + k;
+        for (int c = 0; c < cn; ++c) acc += wr[c * 5] * xr[c];
+      }
+    acc = coop_qsum(acc, Q) + b[o];
+    if (q == 0) {
+      y[i] = acc;
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+}
+
+// BN + ReLU + MaxPool(2) of one clip's conv output y [T][C] (global) -> out [T/2][C] (and LDS copy)
+F3_DEV void coop_pool(const float* y, int T, int C, const float* co, float* out, float* lds) {
+  for (int i = threadIdx.x; i < (T / 2) * C; i += kCoopNT) {
+    const int o = i % C, tp = i / C;
+    const float sc = co[o], sh = co[C + o];
+    const float v = fmaxf(fmaxf(y[2 * tp * C + o] * sc + sh, 0.f), fmaxf(y[(2 * tp + 1) * C + o] * sc + sh, 0.f));
+    if (lds) lds[i] = v;
+    out[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(kCoopNT) void cnn1d_coop_fwd_kernel(CnnCoopArgs a) {
+  extern __shared__ double cc_smd[];
+  const Conv1dArgs &c1 = a.c1, &c2 = a.c2;
+  const int tid = threadIdx.x, G = a.G, b = blockIdx.x;
+  const int T1 = c1.T, T2 = c2.T, T3 = T2 / 2, Ci1 = c1.Ci, C1 = c1.Co, C2 = c2.Co;
+  double* redd = cc_smd;                                      // [NT]
+  float* red = reinterpret_cast<float*>(redd + kCoopNT);       // [NT]
+  float* w1s = red + kCoopNT;                                 // [C1][Ci1][5]
+  float* w2s = w1s + C1 * Ci1 * 5;                            // [C2][C1][5]
+  float* xs = w2s + C2 * C1 * 5;                              // [T1][Ci1]
+  float* ps = xs + T1 * Ci1;                                  // [T2][C1] pool1 output of the clip
+  float* co = ps + T2 * C1;                                   // [4][C] BN scale / shift / mean / rstd
+  float* part1 = a.part;                                      // [G][2 C1]
+  float* part2 = part1 + (size_t)G * 2 * C1;                  // [G][2 C2]
+  for (int i = tid; i < C1 * Ci1 * 5; i += kCoopNT) w1s[i] = c1.w[i];
+  for (int i = tid; i < C2 * C1 * 5; i += kCoopNT) w2s[i] = c2.w[i];
+  // conv1 + BN1 partial sums
+  const int Q1 = coop_q(T1 * C1, Ci1), Q2 = coop_q(T2 * C2, C1);
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = b; n < c1.N; n += G) {
+    __syncthreads();  // (the previous clip's conv reads of xs)
+    for (int i = tid; i < T1 * Ci1; i += kCoopNT) xs[i] = c1.x[(size_t)n * T1 * Ci1 + i];
+    __syncthreads();
+    coop_conv(xs, w1s, c1.b, T1, Ci1, C1, Q1, c1.y + (size_t)n * T1 * C1, s1, s2);
+  }
+  coop_rowsum(s1, part1 + (size_t)b * 2 * C1, red, C1, Q1);
+  coop_rowsum(s2, part1 + (size_t)b * 2 * C1 + C1, red, C1, Q1);
+  coop_barrier(a.sync, 1, G);
+  // BN1 + ReLU + pool1 -> p1, conv2 + BN2 partial sums
+  coop_bn_stats(part1, G, C1, c1.bn, c1.st_sum, c1.st_sq, co, redd);
+  s1 = s2 = 0.f;
+  for (int n = b; n < c1.N; n += G) {
+    __syncthreads();
+    coop_pool(c1.y + (size_t)n * T1 * C1, T1, C1, co, c1.p + (size_t)n * T2 * C1, ps);
+    __syncthreads();
+    coop_conv(ps, w2s, c2.b, T2, C1, C2, Q2, c2.y + (size_t)n * T2 * C2, s1, s2);
+  }
+  coop_rowsum(s1, part2 + (size_t)b * 2 * C2, red, C2, Q2);
+  coop_rowsum(s2, part2 + (size_t)b * 2 * C2 + C2, red, C2, Q2);
+  coop_barrier(a.sync, 2, G);
+  // BN2 + ReLU + pool2 -> p2 (the LSTM input)
+  coop_bn_stats(part2, G, C2, c2.bn, c2.st_sum, c2.st_sq, co, redd);
+  const bool bad = coop_failed(a.sync);
+  for (int n = b; n < c1.N; n += G) coop_pool(c2.y + (size_t)n * T2 * C2, T2, C2, co, c2.p + (size_t)n * T3 * C2, nullptr);
+  if (bad) {
+    __syncthreads();
+    for (int n = b; n < c1.N; n += G)
+      for (int i = tid; i < T3 * C2; i += kCoopNT) c2.p[(size_t)n * T3 * C2 + i] = __builtin_nanf("");
+  }
+}
+
+// dy = gradient through MaxPool(2) + ReLU to the BN output for one clip (first max wins ties, as
+// max_pool1d), with the BN-backward partial sums (thread-fixed channel); co = scale | shift | mean | rstd
+F3_DEV void coop_pool_bwd(const float* y, const float* dp, int T, int C, const float* co, float* dy, float& s1,
+                          float& s2) {
+  const int tid = threadIdx.x, o = tid % C, Tp = T / 2;
+  const float sc = co[o], sh = co[C + o], mu = co[2 * C + o], rs = co[3 * C + o];
+  for (int i = tid; i < T * C; i += kCoopNT) {
+    const int t = i / C, tp = t >> 1;
+    const float yv = y[i];
+    float d = 0.f;
+    if (tp < Tp) {
+      const float v0 = fmaxf(y[(2 * tp) * C + o] * sc + sh, 0.f);
+      const float v1 = fmaxf(y[(2 * tp + 1) * C + o] * sc + sh, 0.f);
+      const int win = (v1 > v0) ? 1 : 0;
+      if ((t & 1) == win && fmaxf(yv * sc + sh, 0.f) > 0.f) d = dp[tp * C + o];
+    }
+    dy[i] = d;
+    s1 += d;
+    s2 += d * ((yv - mu) * rs);
+  }
+}
+
+// BN backward sums from G partial rows [sum dy | sum dy*xhat] (fp64, row order) -> co[4C..6C):
+// k1 = sum dy / M, k2 = sum dy*xhat / M; block 0 adds them to the gamma / beta gradients
+F3_DEV void coop_bn_bwd_sums(const float* part, int G, int C, float M, float* g_gamma, float* g_beta, float* co,
+                             double* red) {
+  const int tid = threadIdx.x, cols = 2 * C, ng = kCoopNT / cols, c = tid % cols, rg = tid / cols;
+  red[tid] = rg < ng ? coop_colsum<double>(part, cols, c, rg, ng, G) : 0.0;
+  __syncthreads();
+  if (tid < C) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int g = 0; g < ng; ++g) {
+      s1 += red[g * cols + tid];
+      s2 += red[g * cols + C + tid];
+    }
+    if (blockIdx.x == 0 && g_gamma) {
+      g_gamma[tid] += (float)s2;
+      g_beta[tid] += (float)s1;
+    }
+    co[4 * C + tid] = (float)s1 / M;
+    co[5 * C + tid] = (float)s2 / M;
+  }
+  __syncthreads();
+}
+
+// dc = BN backward of dy for one clip into LDS
+F3_DEV void coop_bn_bwd_apply(const float* y, const float* dy, int T, int C, const float* gam, const float* co,
+                              float* dcs) {
+  for (int i = threadIdx.x; i < T * C; i += kCoopNT) {
+    const int o = i % C;
+    const float rs = co[3 * C + o];
+    dcs[i] = gam[o] * rs * (dy[i] - co[4 * C + o] - (y[i] - co[2 * C + o]) * rs * co[5 * C + o]);
+  }
+}
+
+// weight / bias gradient partials of one clip: dW[o][c][k] += sum_t dc[t][o] x[t + k - 2][c]
+F3_DEV void coop_wgrad(const float* dcs, const float* xs, int T, int Ci, int Co, float* gw, float& gb) {
+  const int tid = threadIdx.x, NW = Co * Ci * 5;
+  if (tid < Co)
+    for (int t = 0; t < T; ++t) gb += dcs[t * Co + tid];
+#pragma unroll
+  for (int e = 0; e < kCoopWMAX; ++e) {
+    const int i = tid + e * kCoopNT;
+    if (i >= NW) break;
+    const int o = i / (Ci * 5), r = i - o * Ci * 5, c = r / 5, k = r - c * 5;
+    float acc = 0.f;
+    for (int t = max(0, 2 - k); t < min(T, T + 2 - k); ++t) acc += dcs[t * Co + o] * xs[(t + k - 2) * Ci + c];
+    gw[e] += acc;
+  }
+}
+
+F3_DEV void coop_wgrad_row(const float* gw, float gb, int NW, int Co, float* row) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < kCoopWMAX; ++e) {
+    const int i = tid + e * kCoopNT;
+    if (i < NW) xst(row + i, gw[e]);
+  }
+  if (tid < Co) xst(row + NW + tid, gb);
+}
+
+__global__ __launch_bounds__(kCoopNT) void cnn1d_coop_bwd_kernel(CnnCoopArgs a) {
+  extern __shared__ double cc_smd[];
+  const Conv1dArgs &c1 = a.c1, &c2 = a.c2;
+  const int tid = threadIdx.x, G = a.G, b = blockIdx.x, N = c1.N;
+  const int T1 = c1.T, T2 = c2.T, Ci1 = c1.Ci, C1 = c1.Co, C2 = c2.Co;
+  const int NW1 = C1 * Ci1 * 5, NW2 = C2 * C1 * 5;
+  double* redd = cc_smd;
+  float* red = reinterpret_cast<float*>(redd + kCoopNT);
+  float* w2s = red + kCoopNT;                     // [C2][C1][5]
+  float* dcs = w2s + NW2;                         // [max(T2 C2, T1 C1)]
+  float* xs = dcs + max(T2 * C2, T1 * C1);        // [max(T2 C1, T1 Ci1)]
+  float* dps = xs + max(T2 * C1, T1 * Ci1);       // [T2][C1] dp1 of the clip
+  float* co1 = dps + T2 * C1;                     // [6][C1]: scale shift mean rstd k1 k2
+  float* co2 = co1 + 6 * C1;                      // [6][C2]
+  float* part3 = a.part;                          // [G][2 C2]  BN2 backward sums
+  float* part4 = part3 + (size_t)G * 2 * C2;      // [G][NW2 + C2] dW2 | db2
+  float* part5 = part4 + (size_t)G * (NW2 + C2);  // [G][2 C1]  BN1 backward sums
+  float* part6 = part5 + (size_t)G * 2 * C1;      // [G][NW1 + C1] dW1 | db1
+  for (int i = tid; i < NW2; i += kCoopNT) w2s[i] = c2.w[i];
+  if (tid < C1) {
+    float sc, sh, mu, rs;
+    bn_coeff(c1.bn, tid, sc, sh, mu, rs);
+    co1[tid] = sc; co1[C1 + tid] = sh; co1[2 * C1 + tid] = mu; co1[3 * C1 + tid] = rs;
+  }
+  if (tid < C2) {
+    float sc, sh, mu, rs;
+    bn_coeff(c2.bn, tid, sc, sh, mu, rs);
+    co2[tid] = sc; co2[C2 + tid] = sh; co2[2 * C2 + tid] = mu; co2[3 * C2 + tid] = rs;
+  }
+  __syncthreads();
+  // pool2 / ReLU2 backward + BN2 backward partial sums
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = b; n < N; n += G)
+    coop_pool_bwd(c2.y + (size_t)n * T2 * C2, c2.dp + (size_t)n * (T2 / 2) * C2, T2, C2, co2,
+                  c2.dy + (size_t)n * T2 * C2, s1, s2);
+  coop_rowsum(s1, part3 + (size_t)b * 2 * C2, red, C2);
+  coop_rowsum(s2, part3 + (size_t)b * 2 * C2 + C2, red, C2);
+  coop_barrier(a.sync, 1, G);
+  // BN2 backward, conv2 backward (dW2, db2, dp1), pool1 / ReLU1 backward + BN1 backward partial sums
+  coop_bn_bwd_sums(part3, G, C2, c2.bn.count, c2.g_gamma, c2.g_beta, co2, redd);
+  float gw[kCoopWMAX], gb = 0.f;
+#pragma unroll
+  for (int e = 0; e < kCoopWMAX; ++e) gw[e] = 0.f;
+  s1 = s2 = 0.f;
+  const int Qd = coop_q(T2 * C1, C2);  // lanes per dp1 output (split over the conv2 output channels)
+  for (int n = b; n < N; n += G) {
+    __syncthreads();  // the previous clip's readers of dcs / xs / dps are done
+    coop_bn_bwd_apply(c2.y + (size_t)n * T2 * C2, c2.dy + (size_t)n * T2 * C2, T2, C2, c2.bn.gamma, co2, dcs);
+    for (int i = tid; i < T2 * C1; i += kCoopNT) xs[i] = c1.p[(size_t)n * T2 * C1 + i];
+    __syncthreads();
+    if (!(F3_PROBE & 4)) coop_wgrad(dcs, xs, T2, C1, C2, gw, gb);
+    {  // dp1 = conv2^T dc2
+      const int q = tid % Qd, on = C2 / Qd, o0 = q * on;
+      for (int i = tid / Qd; i < T2 * C1; i += kCoopNT / Qd) {
+        const int ti = i / C1, c = i - ti * C1;
+        float acc = 0.f;
+        if (!(F3_PROBE & 4))
+          for (int k = 0; k < 5; ++k) {
+            const int t = ti - k + 2;
+            if (t < 0 || t >= T2) continue;
+            for (int o = o0; o < o0 + on; ++o) acc += dcs[t * C2 + o] * w2s[(o * C1 + c) * 5 + k];
+          }
+        acc = coop_qsum(acc, Qd);
+        if (q == 0) dps[i] = acc;
+      }
+    }
+    __syncthreads();
+    coop_pool_bwd(c1.y + (size_t)n * T1 * C1, dps, T1, C1, co1, c1.dy + (size_t)n * T1 * C1, s1, s2);
+  }
+  coop_wgrad_row(gw, gb, NW2, C2, part4 + (size_t)b * (NW2 + C2));
+  coop_rowsum(s1, part5 + (size_t)b * 2 * C1, red, C1);
+  coop_rowsum(s2, part5 + (size_t)b * 2 * C1 + C1, red, C1);
+  coop_barrier(a.sync, 2, G);
+  // BN1 backward, conv1 weight gradient
+  coop_bn_bwd_sums(part5, G, C1, c1.bn.count, c1.g_gamma, c1.g_beta, co1, redd);
+#pragma unroll
+  for (int e = 0; e < kCoopWMAX; ++e) gw[e] = 0.f;
+  gb = 0.f;
+  for (int n = b; n < N; n += G) {
+    __syncthreads();
+    coop_bn_bwd_apply(c1.y + (size_t)n * T1 * C1, c1.dy + (size_t)n * T1 * C1, T1, C1, c1.bn.gamma, co1, dcs);
+    for (int i = tid; i < T1 * Ci1; i += kCoopNT) xs[i] = c1.x[(size_t)n * T1 * Ci1 + i];
+    __syncthreads();
+    if (!(F3_PROBE & 4)) coop_wgrad(dcs, xs, T1, Ci1, C1, gw, gb);
+  }
+  coop_wgrad_row(gw, gb, NW1, C1, part6 + (size_t)b * (NW1 + C1));
+  coop_barrier(a.sync, 3, G);
+  // column sums of the weight / bias gradient rows: 64 columns per workgroup pass, 16 row groups
+  // (rows r = g, g + 16, ...) added in group order
+  const bool bad = coop_failed(a.sync);
+  const int L4 = NW2 + C2, L6 = NW1 + C1, lane = tid & 63, rg = tid >> 6;
+  for (int c0 = b * 64; c0 < L4 + L6; c0 += G * 64) {
+    const int col = c0 + lane;
+    const bool l2 = col < L4;
+    const int c = l2 ? col : col - L4, L = l2 ? L4 : L6;
+    float v = 0.f;
+    if (col < L4 + L6) v = coop_colsum<float>((l2 ? part4 : part6) + c, L, 0, rg, kCoopNT / 64, G);
+    __syncthreads();
+    red[tid] = v;
+    __syncthreads();
+    if (rg == 0 && col < L4 + L6) {
+      v = 0.f;
+      for (int g = 0; g < kCoopNT / 64; ++g) v += red[64 * g + lane];
+      if (bad) v = __builtin_nanf("");
+      const Conv1dArgs& cc = l2 ? c2 : c1;
+      const int NW = l2 ? NW2 : NW1;
+      if (c < NW) cc.g_w[c] += v;
+      else cc.g_b[c - NW] += v;
+    }
+  }
+}
 
 }  // namespace f3
 
@@ -630,6 +1067,78 @@ int f3_bnrelupool_fwd(const Conv1dArgs* a, hipStream_t s) {
                      dim3(C1D_THREADS), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
+}
+
+namespace f3 {
+int f3_cnn1d_coop_sync_ints() { return kCoopSyncInts; }
+size_t f3_cnn1d_coop_part_floats(int N, int Ci1, int Co1, int Co2) {
+  const size_t G = (size_t)std::max(1, std::min(N, kCnnCoopG));
+  const size_t fwd = 2 * (size_t)(Co1 + Co2), NW1 = (size_t)Co1 * Ci1 * 5, NW2 = (size_t)Co2 * Co1 * 5;
+  const size_t bwd = 2 * (size_t)Co2 + NW2 + Co2 + 2 * (size_t)Co1 + NW1 + Co1;
+  return G * std::max(fwd, bwd);
+}
+}  // namespace f3
+
+// the cooperative form applies (training statistics, both layers' shapes in range, one row of
+// channel sums per workgroup pass); otherwise the caller runs the per-layer launches
+static bool cnn_coop_ok(const Conv1dArgs& c1, const Conv1dArgs& c2, const CnnCoop* coop) {
+  const char* env = getenv("F3_CNN1D_COOP");  // (read per call: the tests compare both forms)
+  const bool on = !env || atoi(env) != 0;
+  if (!on || !coop || !coop->part || !coop->sync || c1.bn.eval || c2.bn.eval || c1.N < 1) return false;
+  if (!c1d_ok(c1) || !c1d_ok(c2) || c2.Ci != c1.Co || c2.T != c1.T / 2 || c2.N != c1.N || c2.T < 2 || c1.Co > c2.Co)
+    return false;
+  // whole stats row groups; channel-fixed threads for every lane split (kCoopNT / Q % Co == 0)
+  return kCoopNT % (2 * c1.Co) == 0 && kCoopNT % (2 * c2.Co) == 0 && (kCoopNT / 4) % c2.Co == 0 &&
+         (kCoopNT / 4) % c1.Co == 0;
+}
+
+static size_t cnn_coop_fwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
+  return kCoopNT * 12 + 4 * ((size_t)c1.Co * c1.Ci * 5 + (size_t)c2.Co * c1.Co * 5 + (size_t)c1.T * c1.Ci +
+                             (size_t)c2.T * c1.Co + 4 * c2.Co);
+}
+static size_t cnn_coop_bwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
+  return kCoopNT * 12 + 4 * ((size_t)c2.Co * c1.Co * 5 + std::max(c2.T * c2.Co, c1.T * c1.Co) +
+                             std::max(c2.T * c1.Co, c1.T * c1.Ci) + (size_t)c2.T * c1.Co + 6 * c1.Co + 6 * c2.Co);
+}
+
+// a plain launch of G <= CUs workgroups of 1024 threads (one per CU): a cooperative launch measured
+// 20-30 us of extra queue latency per call here; co-residency is the CU count, and a barrier that
+// still cannot complete times out (error flag, NaN outputs) rather than hang
+static int cnn_coop_launch(void (*fn)(CnnCoopArgs), const Conv1dArgs& c1, const Conv1dArgs& c2, const CnnCoop& coop,
+                           size_t lds, hipStream_t s) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 1;
+    return std::max(1, n);
+  }();
+  CnnCoopArgs arg;
+  arg.c1 = c1;
+  arg.c2 = c2;
+  arg.part = coop.part;
+  arg.sync = coop.sync;
+  arg.G = std::min(std::min(c1.N, kCnnCoopG), cus);
+  if (lds > 64 * 1024) return F3_EINVAL;
+  hipLaunchKernelGGL(fn, dim3(arg.G), dim3(kCoopNT), lds, s, arg);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_cnn1d_fwd(const Conv1dArgs* c1, const Conv1dArgs* c2, const CnnCoop* coop, hipStream_t s) {
+  if (cnn_coop_ok(*c1, *c2, coop))
+    return cnn_coop_launch(cnn1d_coop_fwd_kernel, *c1, *c2, *coop, cnn_coop_fwd_lds(*c1, *c2), s);
+  F3_TRY(f3_conv1d_fwd(c1, s));
+  F3_TRY(f3_bnrelupool_fwd(c1, s));
+  F3_TRY(f3_conv1d_fwd(c2, s));
+  return f3_bnrelupool_fwd(c2, s);
+}
+
+int f3_cnn1d_bwd(const Conv1dArgs* c1, const Conv1dArgs* c2, const CnnCoop* coop, hipStream_t s) {
+  if (cnn_coop_ok(*c1, *c2, coop))
+    return cnn_coop_launch(cnn1d_coop_bwd_kernel, *c1, *c2, *coop, cnn_coop_bwd_lds(*c1, *c2), s);
+  F3_TRY(f3_conv1d_bwd(c2, s));
+  return f3_conv1d_bwd(c1, s);
 }
 
 int f3_conv1d_bwd(const Conv1dArgs* a, hipStream_t s) {

@@ -456,29 +456,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
 constexpr int GN_THREADS = 256;
 constexpr int GN_XS = IP + 8;  // LDS row stride (bf16): 272-B rows
 
-// `arrive` false: this workgroup does not count itself (the F3_GN_SKIP_ARRIVE test knob, which
-// makes the group's barriers time out). Once any barrier has timed out (err set), every later
-// barrier returns after the first poll that sees the flag, so a faulted launch drains quickly.
-F3_DEV void gn_barrier(int* cnt, int target, int* err, bool arrive = true) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's exchange stores have reached L2
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();  // agent-scope release: the group's other XCDs see the stores
-    if (arrive) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int polls = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      ++polls;
-      if ((polls & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      if (polls > (1 << 22)) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __threadfence();  // acquire: no stale lines of the exchanged rows survive in this CU / XCD
-  }
-  __syncthreads();
-}
+// (gn_barrier: common.h)
 
 __global__ __launch_bounds__(GN_THREADS) void gru_fwd_node_kernel(GruFwdArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Ys[GN_BT * GN_XS];  // S.[x, h] (gate) / S.[x, r*h] (update)

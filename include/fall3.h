@@ -96,10 +96,9 @@ int f3_net_backward(f3_net* net, int batch, const float* params, const float* do
 /* Timing of the sensor CNN1D stages (GSTCAN_UR_conv.ipynb:493-514; models with the CNN1D
  * sensor branch only). enable=1 records HIP events around the Conv1D launches of every later
  * forward / backward on the sensor queue; ms (may be NULL) receives the last forward + backward's
- * 6 stage times in ms: conv1 fwd (conv + BN1 partial rows), pool1 + conv2 fwd (BN1 + ReLU +
- * MaxPool fused into conv2's load, BN2 rows), pool2 fwd, pool2 bwd (MaxPool / ReLU backward + BN2
- * backward rows), conv2 bwd + pool1 bwd, conv1 bwd. No reference counterpart: measurement only
- * (SURVEY §8d). */
+ * 2 times in ms: both CNN1D layers forward, both backward (one cooperative launch each in
+ * training; the per-layer launches in eval or under stream capture). No reference counterpart:
+ * measurement only. */
 int f3_net_sensor_times(f3_net* net, int enable, float* ms);
 
 /* The same backward in two phases, for overlapping the data-parallel gradient all-reduce

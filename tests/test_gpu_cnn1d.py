@@ -1,0 +1,78 @@
+"""The sensor CNN1D's cooperative form (one launch per direction, sensor.hip cnn1d_coop_*) against
+the per-layer launches it replaces in training (needs an MI355X). Parity against the oracle and the
+reference's golden vectors is in test_gpu_parity.py (golden cases ur_sensor / ur_nb run the
+cooperative form by default); here: the same step through both forms, ragged and multi-clip
+workgroup batches, and run-to-run bit identity of the cooperative form (fixed-order reductions)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(model, x, dout, coop):
+    os.environ["F3_CNN1D_COOP"] = "1" if coop else "0"
+    try:
+        N = x.shape[0]
+        ws = torch.zeros(model._native.workspace_bytes(N), dtype=torch.uint8, device=x.device)
+        out = torch.empty(N, dout.shape[1], device=x.device)
+        model.native_forward(None, x, out, ws, True)
+        grads = torch.zeros(model._native.nparam, device=x.device)
+        model.native_backward(N, dout, grads, ws)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("F3_CNN1D_COOP", None)
+    return out.cpu().double(), grads.cpu().double()
+
+
+@pytest.mark.parametrize("N", [256, 5, 300, 600])
+def test_cooperative_cnn1d_matches_per_layer_launches(N):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import fall_multimodal_amd as f3
+    d = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = f3.CNN_BiLSTM(device=d)
+    g = torch.Generator().manual_seed(N)
+    x = torch.randn(N, 30, 4, generator=g).to(d)
+    dout = torch.randn(N, model.spec.num_class, generator=g).to(d)
+    o1, g1 = _step(model, x, dout, True)
+    o0, g0 = _step(model, x, dout, False)
+    assert torch.isfinite(o1).all() and torch.isfinite(g1).all()
+    # the same arithmetic in another summation order (BN sums fp64 in both; weight-gradient sums
+    # fp32 over clips): logits within 1e-5, each gradient tensor within 1e-4 of its own max
+    torch.testing.assert_close(o1, o0, rtol=1e-5, atol=1e-5)
+    worst, gmax = 0.0, float(g0.abs().max())
+    for name, shape, off in model.param_views():
+        n = 1
+        for s in shape:
+            n *= s
+        a, b = g1[off:off + n], g0[off:off + n]
+        if name.startswith("cnn.") and name.endswith(".0.bias"):
+            # a conv bias feeding a batch-statistics BatchNorm has an exactly-zero gradient: both
+            # forms leave rounding residue only
+            assert float(a.abs().max()) <= 1e-5 * gmax and float(b.abs().max()) <= 1e-5 * gmax, name
+            continue
+        scale = max(float(b.abs().max()), 1e-12)
+        r = float((a - b).abs().max()) / scale
+        worst = max(worst, r)
+        assert r <= 1e-4, (name, r)
+    print(f"N={N}: max |dlogit| {float((o1 - o0).abs().max()):.2e}, worst gradient rel diff {worst:.2e}")
+
+
+def test_cooperative_cnn1d_is_deterministic():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import fall_multimodal_amd as f3
+    d = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = f3.CNN_BiLSTM(device=d)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(512, 30, 4, generator=g).to(d)
+    dout = torch.randn(512, model.spec.num_class, generator=g).to(d)
+    a = _step(model, x, dout, True)
+    b = _step(model, x, dout, True)
+    assert torch.equal(a[0], b[0])
+    # the LSTM's own weight gradients use fixed-order partial rows too (f3_lstm_bwd)
+    assert torch.equal(a[1], b[1]), int((a[1] != b[1]).sum())
