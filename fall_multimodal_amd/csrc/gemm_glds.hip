@@ -692,15 +692,36 @@ __global__ __launch_bounds__(256) void wgrad_glds_bf16(WgradArgs a) {
   }
 }
 
+// The bias-gradient partial rows of a weight-gradient launch (WgradArgs::dbpart, one row of Nc per
+// split) summed by the first ceil(Nc / 64) workgroups of its slab reduce (no separate launch):
+// db[c] += sum_s dbpart[s][c], waves 0-3 over interleaved splits, combined in wave order.
+F3_DEV void wgrad_bias_block(const float* __restrict__ dbpart, int splits, int Nc, float* __restrict__ db, int blk,
+                             float (*part)[64]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = blk * 64 + lane;
+  float acc = 0.f;
+  if (wave < 4 && c < Nc)
+    for (int sp = wave; sp < splits; sp += 4) acc += dbpart[(size_t)sp * Nc + c];
+  if (wave < 4) part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < Nc) db[c] += ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
 // dw_ref[j][i][dt] += sum_s slab[s][j][dt*Kc + i]. A workgroup owns 64 consecutive slab
 // elements (one (j, dt) row piece, Kc % 64 == 0); its 4 waves sum interleaved split subsets
-// (coalesced 256-B reads, independent loads) and combine through LDS.
+// (coalesced 256-B reads, independent loads) and combine through LDS. With dbpart, the first
+// nbias = ceil(Nc / 64) workgroups sum the bias rows instead (wgrad_bias_block).
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
                                                                 int Kc, int KT, float* __restrict__ dw_ref,
-                                                                int gcn_cin = 0) {
+                                                                int gcn_cin, const float* __restrict__ dbpart,
+                                                                float* __restrict__ db) {
   __shared__ float part[4][64];
+  const int nbias = dbpart ? (Nc + 63) / 64 : 0;
+  if ((int)blockIdx.x < nbias) {
+    wgrad_bias_block(dbpart, splits, Nc, db, blockIdx.x, part);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t e = (size_t)blockIdx.x * 64 + lane;  // slab element (j, dt, i)
+  const size_t e = (size_t)(blockIdx.x - nbias) * 64 + lane;  // slab element (j, dt, i)
   const size_t stride = (size_t)Nc * KT * Kc;
   float acc0 = 0.f, acc1 = 0.f;
   int sp = wave;
@@ -1263,10 +1284,17 @@ __global__ __launch_bounds__(512) void wgrad_taps(WgradArgs a) {
 // [16 co][16 ci][9] that is exactly the reference layout of those 16 output rows (144
 // contiguous floats each), and the workgroup adds it into dw_ref as 16-B pieces.
 __global__ __launch_bounds__(576) void wgrad_taps_reduce_kernel(const float* __restrict__ slab, int splits, int Nc,
-                                                                 int Kc, float* __restrict__ dw_ref) {
+                                                                 int Kc, float* __restrict__ dw_ref,
+                                                                 const float* __restrict__ dbpart,
+                                                                 float* __restrict__ db) {
   __shared__ __attribute__((aligned(16))) float img[16 * 16 * 9];
+  const int nbias = dbpart ? (Nc + 63) / 64 : 0;  // (the bias rows first, as wgrad_slab_reduce_kernel)
+  if ((int)blockIdx.x < nbias) {
+    wgrad_bias_block(dbpart, splits, Nc, db, blockIdx.x, reinterpret_cast<float (*)[64]>(img));
+    return;
+  }
   const int tiles = (Nc / 64) * (Kc / 64), jt = Nc / 64;
-  const int b = blockIdx.x, tile = b >> 4, wi = (b >> 2) & 3, x = b & 3;
+  const int b = blockIdx.x - nbias, tile = b >> 4, wi = (b >> 2) & 3, x = b & 3;
   const int j0 = (tile % jt) * 64 + x * 16, i0 = (tile / jt) * 64 + wi * 16;
   const int tid = threadIdx.x, dt = tid >> 6, lane = tid & 63, fr = lane & 15, fg = lane >> 4;
   const f32x4* p = reinterpret_cast<const f32x4*>(slab) + (((size_t)tile * 4 + wi) * 9 + dt) * 4 * 64 + x * 64 + lane;
@@ -1344,10 +1372,12 @@ static int launch_wgrad_taps(WgradArgs a, int nks, hipStream_t s) {
   else if (nks == 21) hipLaunchKernelGGL((wgrad_taps<5, true>), grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL((wgrad_taps<6, true>), grid, dim3(512), 0, s, a);
   F3_LAUNCH_CHECK();
-  if (a.dw_ref) {
-    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc, a.g.Kc,
-                       a.dw_ref);
+  if (a.dw_ref) {  // (with the bias rows: no separate colsum launch)
+    const int nbias = a.dbpart ? (a.g.Nc + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_taps_reduce_kernel, dim3(nbias + tiles * 16), dim3(576), 0, s, a.slab, splits, a.g.Nc,
+                       a.g.Kc, a.dw_ref, a.dbpart, a.db);
     F3_LAUNCH_CHECK();
+    return F3_OK;
   }
   if (a.dbpart) return f3_colsum(a.dbpart, splits, a.g.Nc, a.db, s);
   return F3_OK;
@@ -1406,10 +1436,12 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   const dim3 grid(gx * gy * splits * groups);
   hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), 0, s, a);
   F3_LAUNCH_CHECK();
-  if (to_slab && a.dw_ref) {
-    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(per_split / 64)), dim3(256), 0, s, a.slab, splits,
-                       a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref, a.gcn_cin);
+  if (to_slab && a.dw_ref) {  // (with the bias rows: no separate colsum launch)
+    const int nbias = a.dbpart ? (a.g.Nc + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)(nbias + per_split / 64)), dim3(256), 0, s, a.slab,
+                       splits, a.g.Nc, a.g.Kc, a.g.KT, a.dw_ref, a.gcn_cin, a.dbpart, a.db);
     F3_LAUNCH_CHECK();
+    return F3_OK;
   }
   if (a.dbpart) return f3_colsum(a.dbpart, splits, a.g.Nc, a.db, s);
   return F3_OK;

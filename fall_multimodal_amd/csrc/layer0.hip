@@ -322,6 +322,6 @@ int f3_databn_bwd2(const DataBnArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(databn_bwd2_kernel, dim3(blocks), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   if (!a->part) return F3_OK;
-  F3_TRY(f3_colsum_ld(a->part, blocks, 2 * VC, VC, a->dgamma, s));
-  return f3_colsum_ld(a->part + VC, blocks, 2 * VC, VC, a->dbeta, s);
+  const ColsumJob j[2] = {{a->part, a->dgamma, 2LL * VC, blocks, VC}, {a->part + VC, a->dbeta, 2LL * VC, blocks, VC}};
+  return f3_colsum_multi(j, 2, s);
 }

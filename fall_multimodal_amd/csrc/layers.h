@@ -235,6 +235,15 @@ int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);
 int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
 int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
+// several independent column sums in one launch (each as f3_colsum_ld)
+constexpr int kColsumJobs = 8;
+struct ColsumJob {
+  const float* part;
+  float* out;
+  long long ld;
+  int rows, cols;
+};
+int f3_colsum_multi(const ColsumJob* jobs, int n, hipStream_t s);
 int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);  // out[c] += sum_r part[r][c]
 // the same over rows `ld` floats apart (fixed summation order, as f3_colsum)
 int f3_colsum_ld(const float* part, int rows, long long ld, int cols, float* out, hipStream_t s);

@@ -1572,11 +1572,24 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_any_kernel(BnReluArgs a) {
 // out[c] += sum_r part[r][c], in a fixed order (the same bits every run): a workgroup owns 64 columns
 // and all rows; its 16 row groups sum rows rg, rg + 16, ... and the 16 partials are added in group
 // order. (The first version split the rows over workgroups with one float atomic per column and
-// workgroup: order-dependent sums.)
-__global__ __launch_bounds__(1024) void colsum_kernel(const float* part, int rows, int cols, float* out, long long ld) {
+// workgroup: order-dependent sums.) One launch serves up to kColsumJobs independent sums (the
+// workgroups of job j are blk[j] .. blk[j + 1] - 1): the reductions of one producer share a launch.
+struct ColsumJobs {
+  int n;
+  const float* part[kColsumJobs];
+  float* out[kColsumJobs];
+  long long ld[kColsumJobs];
+  int rows[kColsumJobs], cols[kColsumJobs], blk[kColsumJobs + 1];
+};
+__global__ __launch_bounds__(1024) void colsum_kernel(ColsumJobs J) {
   __shared__ float red[16][64];
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.blk[j + 1]) ++j;
+  const float* part = J.part[j];
+  const int rows = J.rows[j], cols = J.cols[j];
+  const long long ld = J.ld[j];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = (blockIdx.x - J.blk[j]) * 64 + lane;
   float s0 = 0.f, s1 = 0.f;
   if (c < cols) {
     int r = rg;
@@ -1592,7 +1605,7 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* part, int row
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) t += red[g][lane];
-    out[c] += t;
+    J.out[j][c] += t;
   }
 }
 
@@ -2296,9 +2309,10 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   const int nc = a.N * a.C, nseg = a.res_kind == RES_CONV ? 3 : 2;
   if (a.P2 == a.P1 + nc && (nseg == 2 || a.Q2 == a.P1 + 2 * nc))  // contiguous [P1 | P2 | Q2]: one launch
     return f3_colsum_ld(a.part, a.chunks, 3LL * nc, nseg * nc, a.P1, s);
-  F3_TRY(f3_colsum_ld(a.part, a.chunks, 3LL * nc, nc, a.P1, s));
-  F3_TRY(f3_colsum_ld(a.part + nc, a.chunks, 3LL * nc, nc, a.P2, s));
-  if (nseg == 3) F3_TRY(f3_colsum_ld(a.part + 2 * nc, a.chunks, 3LL * nc, nc, a.Q2, s));
+  const ColsumJob j[3] = {{a.part, a.P1, 3LL * nc, a.chunks, nc},
+                          {a.part + nc, a.P2, 3LL * nc, a.chunks, nc},
+                          {a.part + 2 * nc, a.Q2, 3LL * nc, a.chunks, nc}};
+  F3_TRY(f3_colsum_multi(j, nseg, s));
   return F3_OK;
 }
 
@@ -2336,18 +2350,35 @@ int f3_bn_bwd_apply(BnBwdArgs a, hipStream_t s) {
   return f3_colsum(a.Gpart, fch * a.N, a.V * a.C, a.G, s);
 }
 
-int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) {
-  if (rows <= 0 || cols <= 0) return F3_OK;
-  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, rows, cols, out, (long long)cols);
+int f3_colsum_multi(const ColsumJob* jobs, int n, hipStream_t s) {
+  if (n < 0 || n > kColsumJobs) return F3_EINVAL;
+  ColsumJobs J;
+  J.n = 0;
+  J.blk[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (jobs[i].rows <= 0 || jobs[i].cols <= 0) continue;
+    const int k = J.n++;
+    J.part[k] = jobs[i].part;
+    J.out[k] = jobs[i].out;
+    J.ld[k] = jobs[i].ld;
+    J.rows[k] = jobs[i].rows;
+    J.cols[k] = jobs[i].cols;
+    J.blk[k + 1] = J.blk[k] + (jobs[i].cols + 63) / 64;
+  }
+  if (J.n == 0) return F3_OK;
+  hipLaunchKernelGGL(colsum_kernel, dim3(J.blk[J.n]), dim3(1024), 0, s, J);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
 
+int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s) {
+  const ColsumJob j{part, out, (long long)cols, rows, cols};
+  return f3_colsum_multi(&j, 1, s);
+}
+
 int f3_colsum_ld(const float* part, int rows, long long ld, int cols, float* out, hipStream_t s) {
-  if (rows <= 0 || cols <= 0) return F3_OK;
-  hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, rows, cols, out, ld);
-  F3_LAUNCH_CHECK();
-  return F3_OK;
+  const ColsumJob j{part, out, ld, rows, cols};
+  return f3_colsum_multi(&j, 1, s);
 }
 
 int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
@@ -2404,9 +2435,10 @@ int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s) {
   if (!a->wpart) return F3_OK;
   // the partial rows are [groups][2 H C + C]: sum each segment's columns over the groups
   const int ld = 2 * H * C + C;
-  F3_TRY(f3_colsum_ld(a->wpart, groups, ld, H * C, a->g_W1, s));
-  F3_TRY(f3_colsum_ld(a->wpart + H * C, groups, ld, C * H, a->g_W2, s));
-  return f3_colsum_ld(a->wpart + 2 * H * C, groups, ld, C, a->g_b2, s);
+  const ColsumJob j[3] = {{a->wpart, a->g_W1, ld, groups, H * C},
+                          {a->wpart + H * C, a->g_W2, ld, groups, C * H},
+                          {a->wpart + 2 * H * C, a->g_b2, ld, groups, C}};
+  return f3_colsum_multi(j, 3, s);
 }
 
 int f3_bn_running(const BnRunTable& t, hipStream_t s) {

@@ -1013,14 +1013,15 @@ int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
   F3_LAUNCH_CHECK();
   if (!a->wpart) return F3_OK;
   const int tiles = grid.x, S = a->S, row = G4 * (1 + S + H);
+  ColsumJob j[8];
   for (int d = 0; d < 2; ++d) {
     const float* p = a->wpart + (size_t)d * tiles * row;
-    F3_TRY(f3_colsum_ld(p, tiles, row, G4, a->g_b_ih[d], s));
-    F3_TRY(f3_colsum_ld(p, tiles, row, G4, a->g_b_hh[d], s));
-    F3_TRY(f3_colsum_ld(p + G4, tiles, row, G4 * S, a->g_w_ih[d], s));
-    F3_TRY(f3_colsum_ld(p + G4 * (1 + S), tiles, row, G4 * H, a->g_w_hh[d], s));
+    j[4 * d + 0] = {p, a->g_b_ih[d], row, tiles, G4};
+    j[4 * d + 1] = {p, a->g_b_hh[d], row, tiles, G4};
+    j[4 * d + 2] = {p + G4, a->g_w_ih[d], row, tiles, G4 * S};
+    j[4 * d + 3] = {p + G4 * (1 + S), a->g_w_hh[d], row, tiles, G4 * H};
   }
-  return F3_OK;
+  return f3_colsum_multi(j, 8, s);
 }
 
 int f3_shead_fwd(const SHeadArgs* a, hipStream_t s) {
