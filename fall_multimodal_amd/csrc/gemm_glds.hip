@@ -1487,6 +1487,15 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
     if (a.g.Kc % 256 == 0) return launch_wgrad<128, 256, 512, wgrad_big<2, 4, 4, 4, 32, 1, 3, true>>(af, s);
     return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 1, 3, true>>(af, s);
   }
+  if (bigv && a.x3seg && taps9 && a.g.Nc % 128 == 0 && a.g.Kc % 128 == 0) {
+    // the 9-tap bf16x3 weight gradients wgrad_taps does not take (the stride-2 layers), X3F: 256 x 128
+    // tiles tap by tap (a 2-tap group of fused rows needs 192 KiB), 128 x 128 tiles in 2-tap groups.
+    // Step 8.66-8.68 -> 8.52-8.59 ms (profiles/r05_x3f9_ab.txt; the 128-channel layer's share neutral)
+    WgradArgs af = a;
+    af.x3seg = 0;
+    if (a.g.Nc % 256 == 0) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 1, 3, true>>(af, s);
+    return launch_wgrad<128, 128, 512, wgrad_big<2, 4, 4, 2, 32, 2, 3, true>, 2>(af, s);
+  }
   if (bigv && a.g.Nc % 256 == 0 && a.g.Kc % 128 == 0) {
     if (taps9) return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4, 32, 2>, 2>(a, s);
     return launch_wgrad<256, 128, 512, wgrad_big<4, 2, 4, 4>>(a, s);
