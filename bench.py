@@ -113,7 +113,7 @@ def launch_check(world, rank):
     dist.destroy_process_group()
 
 
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r05_roofline_pmc.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r05_roofline_pmc_final.json")
 RGB_PMC = os.path.join(ROOT, "profiles", "r04_rgb_pmc.json")
 
 
@@ -201,16 +201,17 @@ def roofline_kernels(dev, batch, V, precision, only=None):
 
 
 def roofline_kernels_x3(dev, batch, V, only=None):
-    """bf16x3 (the headline mode): the step's largest GEMM families (the round-5 serial step profile,
-    profiles/r05_x3_step_serial_kernels.txt), each launched alone through the C ABI exactly as the step
-    launches it, on operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the step's
-    producers write them) in the native split form (three bf16 MFMA products per algorithmic FLOP):
-    * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,2,2,2,64> over the
-      three row segments (dy_hi x_hi, dy_lo x_hi, dy_hi x_lo) + the slab reduce — the HEADLINE: the
-      step's largest serial family;
+    """bf16x3 (the headline mode): the step's largest GEMM families (the round-5 serial step profile at
+    HEAD, profiles/r05_x3_step_serial_kernels_final.txt), each launched alone through the C ABI exactly as
+    the step launches it, on operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
+    step's producers write them) in the native split form (three bf16 MFMA products per algorithmic FLOP):
     * "dgrad_l8": the 256-channel T=8 stride-1 tcn input gradient, igemm_big's clip-window form
-      (two clips x 128 channels per workgroup, the 9 taps reading one staged window) — the second;
-    * "wgrad_l5": the 256-channel stride-2 (T 15 -> 8) weight gradient, wgrad_big<4,2,4,4,32,2>;
+      (two clips x 128 channels per workgroup, the 9 taps reading one staged window) — the HEADLINE:
+      the WIN=144 input-gradient family is the step's largest serial family (600 us/step);
+    * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,2,2,2,32> X3F (the
+      three products dy_hi x_hi, dy_lo x_hi, dy_hi x_lo from one staging of [hi | lo] rows) + the slab
+      reduce — the third (500 us/step; the second is the WIN=144 forward, "tcn_fwd");
+    * "wgrad_l5": the 256-channel stride-2 (T 15 -> 8) weight gradient, wgrad_big<4,2,4,4,32> X3F;
     * "wgrad" / "wgrad_kernel": the T=8 stride-1 weight gradient (wgrad_taps<5>, all 9 taps from one
       staged copy of each clip) with / without its reduce;
     * "tcn_fwd": the T=8 stride-1 forward (clip window, fp32 out + bias).
@@ -277,8 +278,8 @@ def roofline_kernels_x3(dev, batch, V, only=None):
         x5 = split(torch.randn(N, 15, V, C, device=dev))
         ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy3), L.ptr(x5), L.ptr(dw), L.ptr(db), N, 15,
                                                                     V, C, C, KT, 2, 4, st))
-        out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,2> (2-tap groups) x 3 row segments + slab reduce (tcn 9x1 "
-                                     f"weight gradient, bf16x3, stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms,
+        out["wgrad_l5"] = {"kernel": f"wgrad_big<4,2,4,4,32,X3F> + slab reduce (tcn 9x1 weight gradient, bf16x3, "
+                                     f"stride 2, C=256, T=15->8, N={N}, V={V})", "ms": ms,
                            "bytes": row8 + row15 + wbytes, "flop": conv_flop(N * T * V, C, C)}
     if want("wgrad_l1"):
         C1, T1 = 64, 30
@@ -289,8 +290,8 @@ def roofline_kernels_x3(dev, batch, V, only=None):
         ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy1), L.ptr(x1), L.ptr(dw1), L.ptr(db1), N, T1,
                                                                     V, C1, C1, KT, 1, 4, st))
         row30 = N * T1 * V * C1 * 4
-        out["wgrad_l1"] = {"kernel": f"wgrad_big<2,2,2,2,64> x 3 row segments + slab reduce (tcn 9x1 weight gradient, "
-                                     f"bf16x3, C=64, T=30, N={N}, V={V})", "ms": ms,
+        out["wgrad_l1"] = {"kernel": f"wgrad_big<2,2,2,2,32,X3F> + slab reduce (tcn 9x1 weight gradient, bf16x3, "
+                                     f"C=64, T=30, N={N}, V={V})", "ms": ms,
                            "bytes": row30 + row30 + C1 * C1 * KT * 4, "flop": conv_flop(N * T1 * V, C1, C1)}
     return _roofline_records(out, None, peak, products=3)
 
@@ -1060,8 +1061,8 @@ def main():
                        "joints": V, "imu_axes": S, "classes": C, "rgb_branch": "build-defined, timed on its own (rgb_branch key)",
                        "hip_graph": bool(a.graph and not a.no_graph), "final_loss": round(loss, 5),
                        "ranks": world, "collective": "rccl all_reduce (2 buckets, high-priority streams)" if world > 1 else None},
-            "roofline": roofs.get("wgrad_l1", roofs.get("wgrad_l5", roofs["tcn_fwd"])),
-            "roofline_dgrad_l8": roofs.get("dgrad_l8"),
+            "roofline": roofs.get("dgrad_l8", roofs.get("wgrad_l1", roofs["tcn_fwd"])),
+            "roofline_wgrad_l1": roofs.get("wgrad_l1"),
             "roofline_wgrad_l5": roofs.get("wgrad_l5"),
             "roofline_wgrad_l6": roofs.get("wgrad"),
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),

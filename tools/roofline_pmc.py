@@ -26,9 +26,9 @@ sys.path.insert(0, ROOT)
 
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
 _RED = "wgrad_slab_reduce_kernel"
-KERNELS = {"wgrad_l1": ["wgrad_big<2, 2, 2, 2, 64", _RED],
+KERNELS = {"wgrad_l1": ["wgrad_big<2, 2, 2, 2, 32, 1, 3, true", _RED],
            "dgrad_l8": ["igemm_big<0, 2, 4, 144"],
-           "wgrad_l5": ["wgrad_big<4, 2, 4, 4, ", _RED],
+           "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 32, 1, 3, true", _RED],
            "wgrad": ["wgrad_taps<5", "wgrad_taps_reduce_kernel"],
            "wgrad_kernel": ["wgrad_taps<5"],
            "tcn_fwd": ["igemm_big<1, 2, 4, 144"]}
