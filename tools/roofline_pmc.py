@@ -9,7 +9,7 @@ different keys (layer 6 / layer 5 / the GEMM alone) never mix.
     on the box: per KEY and counter C: timeout -s KILL 60 rocprofv3 --pmc C --kernel-trace
                     -d gpurun_out/rpmc_KEY_C -o run -- python tools/roofline_pmc.py run KEY
                 (tools/gpu_session.sh roof_pmc)
-    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r05_roofline_pmc.json
+    summarize:  python tools/roofline_pmc.py summarize gpurun_out > profiles/r05_roofline_pmc_final.json
 
 FETCH_SIZE on gfx950 counts 1/2 of the bytes of wide streaming reads (MI355X_MICROARCH.md,
 HBM section; calibrated here on rmsprop_kernel: 51.6 MB read = 2 x FETCH_SIZE), so fetch is
