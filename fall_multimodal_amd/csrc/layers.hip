@@ -1569,42 +1569,43 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_any_kernel(BnReluArgs a) {
   }
 }
 
-// out[c] += sum_r part[r][c], in a fixed order (the same bits every run): a workgroup owns 64 columns
-// and all rows; its 16 row groups sum rows rg, rg + 16, ... and the 16 partials are added in group
-// order. (The first version split the rows over workgroups with one float atomic per column and
-// workgroup: order-dependent sums.) One launch serves up to kColsumJobs independent sums (the
-// workgroups of job j are blk[j] .. blk[j + 1] - 1): the reductions of one producer share a launch.
+// out[c] += sum_r part[r][c], in a fixed order (the same bits every run): a workgroup owns 1024 / RG
+// columns and all rows; its RG row groups (RG = 16, or the power of two <= rows: few-row sums keep all
+// threads on columns) sum rows rg, rg + RG, ... and the RG partials are added in group order. (The
+// first version split the rows over workgroups with one float atomic per column and workgroup:
+// order-dependent sums.) One launch serves up to kColsumJobs independent sums (the workgroups of job
+// j are blk[j] .. blk[j + 1] - 1): the reductions of one producer share a launch.
 struct ColsumJobs {
   int n;
   const float* part[kColsumJobs];
   float* out[kColsumJobs];
   long long ld[kColsumJobs];
-  int rows[kColsumJobs], cols[kColsumJobs], blk[kColsumJobs + 1];
+  int rows[kColsumJobs], cols[kColsumJobs], rg[kColsumJobs], blk[kColsumJobs + 1];
 };
+static int colsum_rg(int rows) { return rows >= 16 ? 16 : rows >= 8 ? 8 : rows >= 4 ? 4 : rows >= 2 ? 2 : 1; }
 __global__ __launch_bounds__(1024) void colsum_kernel(ColsumJobs J) {
-  __shared__ float red[16][64];
+  __shared__ float red[1024];
   int j = 0;
   while (j + 1 < J.n && (int)blockIdx.x >= J.blk[j + 1]) ++j;
   const float* part = J.part[j];
-  const int rows = J.rows[j], cols = J.cols[j];
+  const int rows = J.rows[j], cols = J.cols[j], RG = J.rg[j], CPB = 1024 / RG;
   const long long ld = J.ld[j];
-  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = (blockIdx.x - J.blk[j]) * 64 + lane;
+  const int lane = threadIdx.x % CPB, rg = threadIdx.x / CPB;
+  const int c = (blockIdx.x - J.blk[j]) * CPB + lane;
   float s0 = 0.f, s1 = 0.f;
   if (c < cols) {
     int r = rg;
-    for (; r + 16 < rows; r += 32) {
+    for (; r + RG < rows; r += 2 * RG) {
       s0 += part[(size_t)r * ld + c];
-      s1 += part[(size_t)(r + 16) * ld + c];
+      s1 += part[(size_t)(r + RG) * ld + c];
     }
     if (r < rows) s0 += part[(size_t)r * ld + c];
   }
-  red[rg][lane] = s0 + s1;
+  red[threadIdx.x] = s0 + s1;
   __syncthreads();
   if (rg == 0 && c < cols) {
     float t = 0.f;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) t += red[g][lane];
+    for (int g = 0; g < RG; ++g) t += red[g * CPB + lane];
     J.out[j][c] += t;
   }
 }
@@ -2363,7 +2364,9 @@ int f3_colsum_multi(const ColsumJob* jobs, int n, hipStream_t s) {
     J.ld[k] = jobs[i].ld;
     J.rows[k] = jobs[i].rows;
     J.cols[k] = jobs[i].cols;
-    J.blk[k + 1] = J.blk[k] + (jobs[i].cols + 63) / 64;
+    J.rg[k] = colsum_rg(jobs[i].rows);
+    const int cpb = 1024 / J.rg[k];
+    J.blk[k + 1] = J.blk[k] + (jobs[i].cols + cpb - 1) / cpb;
   }
   if (J.n == 0) return F3_OK;
   hipLaunchKernelGGL(colsum_kernel, dim3(J.blk[J.n]), dim3(1024), 0, s, J);
