@@ -1570,8 +1570,9 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_any_kernel(BnReluArgs a) {
 }
 
 // out[c] += sum_r part[r][c], in a fixed order (the same bits every run): a workgroup owns 1024 / RG
-// columns and all rows; its RG row groups (RG = 16, or the power of two <= rows: few-row sums keep all
-// threads on columns) sum rows rg, rg + RG, ... and the RG partials are added in group order. (The
+// columns and all rows; its RG row groups (colsum_rg: fewer for few-row sums, up to 64 for tall narrow
+// ones) sum rows rg, rg + RG, ... (four interleaved accumulators) and the RG partials are added in
+// group order. (The
 // first version split the rows over workgroups with one float atomic per column and workgroup:
 // order-dependent sums.) One launch serves up to kColsumJobs independent sums (the workgroups of job
 // j are blk[j] .. blk[j + 1] - 1): the reductions of one producer share a launch.
@@ -1582,7 +1583,13 @@ struct ColsumJobs {
   long long ld[kColsumJobs];
   int rows[kColsumJobs], cols[kColsumJobs], rg[kColsumJobs], blk[kColsumJobs + 1];
 };
-static int colsum_rg(int rows) { return rows >= 16 ? 16 : rows >= 8 ? 8 : rows >= 4 ? 4 : rows >= 2 ? 2 : 1; }
+// row groups: the power of two <= rows up to 16, then up to 64 while the job has fewer than 256
+// workgroups (tall, narrow sums: the BN-backward G rows are 2048 x 1152, 18 workgroups at 16 groups)
+static int colsum_rg(int rows, int cols) {
+  int rg = rows >= 16 ? 16 : rows >= 8 ? 8 : rows >= 4 ? 4 : rows >= 2 ? 2 : 1;
+  while (rg < 64 && 2 * rg <= rows && (cols + 1024 / rg - 1) / (1024 / rg) < 256) rg *= 2;
+  return rg;
+}
 __global__ __launch_bounds__(1024) void colsum_kernel(ColsumJobs J) {
   __shared__ float red[1024];
   int j = 0;
@@ -1592,16 +1599,18 @@ __global__ __launch_bounds__(1024) void colsum_kernel(ColsumJobs J) {
   const long long ld = J.ld[j];
   const int lane = threadIdx.x % CPB, rg = threadIdx.x / CPB;
   const int c = (blockIdx.x - J.blk[j]) * CPB + lane;
-  float s0 = 0.f, s1 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four loads in flight per thread
   if (c < cols) {
     int r = rg;
-    for (; r + RG < rows; r += 2 * RG) {
+    for (; r + 3 * RG < rows; r += 4 * RG) {
       s0 += part[(size_t)r * ld + c];
       s1 += part[(size_t)(r + RG) * ld + c];
+      s2 += part[(size_t)(r + 2 * RG) * ld + c];
+      s3 += part[(size_t)(r + 3 * RG) * ld + c];
     }
-    if (r < rows) s0 += part[(size_t)r * ld + c];
+    for (; r < rows; r += RG) s0 += part[(size_t)r * ld + c];
   }
-  red[threadIdx.x] = s0 + s1;
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (rg == 0 && c < cols) {
     float t = 0.f;
@@ -2364,7 +2373,7 @@ int f3_colsum_multi(const ColsumJob* jobs, int n, hipStream_t s) {
     J.ld[k] = jobs[i].ld;
     J.rows[k] = jobs[i].rows;
     J.cols[k] = jobs[i].cols;
-    J.rg[k] = colsum_rg(jobs[i].rows);
+    J.rg[k] = colsum_rg(jobs[i].rows, jobs[i].cols);
     const int cpb = 1024 / J.rg[k];
     J.blk[k + 1] = J.blk[k] + (jobs[i].cols + cpb - 1) / cpb;
   }
