@@ -1026,28 +1026,37 @@ __global__ __launch_bounds__(256) void mix_bwd_x3_kernel(MixArgs a) {
 }
 
 // gcn bias through the graph + edge importance: db[k*C+c] += sum_w colsumAeff_k[w] G[w][c];
-// dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff
-__global__ __launch_bounds__(256) void gcn_bias_db_kernel(GcnBiasBwdArgs a) {
-  __shared__ float cs[1024];  // colsum_k[w] of A_eff
-  for (int e = threadIdx.x; e < a.K * a.V; e += blockDim.x) {
-    const int k = e / a.V, w = e - k * a.V;
+// dAeff[k,v,w] += sum_c b[k*C+c] G[w][c];  dE = A * dAeff. One launch: the first ceil(K C / 256)
+// workgroups the bias gradient (A_eff staged in LDS with all threads, then the column sums), the
+// next K V workgroups one (k, w) of dE each (the two parts are independent). Both run in the step's
+// tail; the first version read A_eff column by column from L2 (18 dependent loads per thread).
+__global__ __launch_bounds__(256) void gcn_bias_bwd_kernel(GcnBiasBwdArgs a) {
+  __shared__ float sm[3072 + 1024];
+  const int ndb = (a.K * a.C + 255) / 256, KV = a.K * a.V;
+  if ((int)blockIdx.x < ndb) {
+    float* Ae = sm;          // A_eff [K][V][V]
+    float* cs = sm + 3072;   // colsum_k[w]
+    for (int e = threadIdx.x; e < KV * a.V; e += blockDim.x) Ae[e] = a.Aeff[e];
+    __syncthreads();
+    for (int e = threadIdx.x; e < KV; e += blockDim.x) {
+      const int k = e / a.V, w = e - k * a.V;
+      float acc = 0.f;
+      for (int v = 0; v < a.V; ++v) acc += Ae[(k * a.V + v) * a.V + w];
+      cs[e] = acc;
+    }
+    __syncthreads();
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.K * a.C) return;
+    const int k = e / a.C, c = e - k * a.C;
     float acc = 0.f;
-    for (int v = 0; v < a.V; ++v) acc += a.Aeff[(k * a.V + v) * a.V + w];
-    cs[e] = acc;
+#pragma unroll 6
+    for (int w = 0; w < a.V; ++w) acc += cs[k * a.V + w] * a.G[w * a.C + c];
+    a.db[e] += acc;
+    return;
   }
-  __syncthreads();
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.K * a.C) return;
-  const int k = e / a.C, c = e - k * a.C;
-  float acc = 0.f;
-  for (int w = 0; w < a.V; ++w) acc += cs[k * a.V + w] * a.G[w * a.C + c];
-  a.db[e] += acc;
-}
-
-// one workgroup per (k, w): s = sum_c b[k*C+c] G[w][c]; dE[k][v][w] += A*(dAeff + s)
-__global__ __launch_bounds__(256) void gcn_bias_dE_kernel(GcnBiasBwdArgs a) {
-  __shared__ float red[4];
-  const int k = blockIdx.x / a.V, w = blockIdx.x - k * a.V;
+  // (k, w): s = sum_c b[k*C+c] G[w][c]; dE[k][v][w] += A*(dAeff + s)
+  float* red = sm;
+  const int kw = blockIdx.x - ndb, k = kw / a.V, w = kw - k * a.V;
   float acc = 0.f;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) acc += a.bias[k * a.C + c] * a.G[w * a.C + c];
   acc = warp_sum(acc);
@@ -2250,10 +2259,8 @@ int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
 }
 
 int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
-  if (a->K * a->V > 1024) return F3_EINVAL;
-  hipLaunchKernelGGL(gcn_bias_db_kernel, dim3((a->K * a->C + 255) / 256), dim3(256), 0, s, *a);
-  F3_LAUNCH_CHECK();
-  hipLaunchKernelGGL(gcn_bias_dE_kernel, dim3(a->K * a->V), dim3(256), 0, s, *a);
+  if (a->K * a->V * a->V > 3072 || a->K * a->V > 1024) return F3_EINVAL;
+  hipLaunchKernelGGL(gcn_bias_bwd_kernel, dim3((a->K * a->C + 255) / 256 + a->K * a->V), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
 }
