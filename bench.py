@@ -208,7 +208,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
     * "dgrad_l8": the 256-channel T=8 stride-1 tcn input gradient, igemm_big's clip-window form
       (two clips x 128 channels per workgroup, the 9 taps reading one staged window) — the HEADLINE:
       the WIN=144 input-gradient family is the step's largest serial family (600 us/step);
-    * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,2,2,2,32> X3F (the
+    * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,4,2,1,32> X3F (the
       three products dy_hi x_hi, dy_lo x_hi, dy_hi x_lo from one staging of [hi | lo] rows) + the slab
       reduce — the third (500 us/step; the second is the WIN=144 forward, "tcn_fwd");
     * "wgrad_l5": the 256-channel stride-2 (T 15 -> 8) weight gradient, wgrad_big<4,2,4,4,32> X3F;
@@ -290,7 +290,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
         ms = _time_launch(lambda: lib.f3_conv_backward_weight_x3cat(L.ptr(dy1), L.ptr(x1), L.ptr(dw1), L.ptr(db1), N, T1,
                                                                     V, C1, C1, KT, 1, 4, st))
         row30 = N * T1 * V * C1 * 4
-        out["wgrad_l1"] = {"kernel": f"wgrad_big<2,2,2,2,32,X3F> + slab reduce (tcn 9x1 weight gradient, bf16x3, "
+        out["wgrad_l1"] = {"kernel": f"wgrad_big<2,4,2,1,32,X3F> + slab reduce (tcn 9x1 weight gradient, bf16x3, "
                                      f"C=64, T=30, N={N}, V={V})", "ms": ms,
                            "bytes": row30 + row30 + C1 * C1 * KT * 4, "flop": conv_flop(N * T1 * V, C1, C1)}
     return _roofline_records(out, None, peak, products=3)

@@ -1515,7 +1515,10 @@ int f3_wgrad_glds_bf16(const WgradArgs* args, hipStream_t s) {
     af.x3seg = 0;
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2, 32, 1, 3, true>>(af, s);
     if (a.g.Kc % 128 == 0) return launch_wgrad<64, 128, 256, wgrad_big<2, 2, 2, 4, 32, 1, 3, true>>(af, s);
-    return launch_wgrad<64, 64, 256, wgrad_big<2, 2, 2, 2, 32, 1, 3, true>>(af, s);
+    // (64 x 64: 8 waves of 32 x 16 instead of 4 of 32 x 32 — same 73.8 us alone, step 8.52 -> 8.45 ms in
+    // three of three rounds, more waves per CU beside the main chains; a 4-stage ring 86 us,
+    // profiles/r05_w64_ab.txt)
+    return launch_wgrad<64, 64, 512, wgrad_big<2, 4, 2, 1, 32, 1, 3, true>>(af, s);
   }
   if (bigv) {  // 64-wide tiles: 4 waves, same lean loop (64-channel tcn: 38 -> 28 us)
     if (a.g.Nc % 128 == 0) return launch_wgrad<128, 64, 256, wgrad_big<2, 2, 4, 2>>(a, s);

@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
 _RED = "wgrad_slab_reduce_kernel"
-KERNELS = {"wgrad_l1": ["wgrad_big<2, 2, 2, 2, 32, 1, 3, true", _RED],
+KERNELS = {"wgrad_l1": ["wgrad_big<2, 4, 2, 1, 32, 1, 3, true", _RED],
            "dgrad_l8": ["igemm_big<0, 2, 4, 144"],
            "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 32, 1, 3, true", _RED],
            "wgrad": ["wgrad_taps<5", "wgrad_taps_reduce_kernel"],
