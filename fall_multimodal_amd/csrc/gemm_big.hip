@@ -28,6 +28,9 @@
 // linearly. A software-pipelined loop (next step's hi fragments read under the current step's lo
 // products) and a ping-pong of the SIMD partner waves (one loads while the other multiplies) were
 // both 2-5 % SLOWER: the loading leg is instruction-issue bound, not latency bound.)
+#ifndef F3_TILE_BATCH
+#define F3_TILE_BATCH 1  // batched fragment reads in the tiled X3N loop (0: the hipcc-scheduled reads, A/B)
+#endif
 #ifndef F3_PROBE
 #define F3_PROBE 0
 #endif
@@ -414,8 +417,52 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
       if (t + 2 < nchunk) stage(t + 2, (t + 2) % 3);
       const char* sa = smem + buf * STAGE;
       const char* sb = sa + AP * 1024;
-      // (batched inline-asm fragment reads as in the WIN loop measured neutral here: DESIGN.md §4.6)
-      if constexpr (X3N) {
+      // X3N: the 22 fragment reads of a step issued at once (inline asm, immediate row offsets: a
+      // fragment's rows keep r & 7 over the 16-row tiles, so one swizzled base serves all), the hi
+      // half's products under a counted wait, as the WIN loop. (In the round-2 bf16 form the batched
+      // reads measured neutral here)
+      if constexpr (X3N && F3_TILE_BATCH) {
+        static_assert(BG_NT == 2 && BG_MT == 9, "batched tile reads");
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        const unsigned l0 = (unsigned)(size_t)(lds_cchar_t*)smem + buf * STAGE;
+        const int ra = wm * 144 + fr, rw = wn * 32 + fr;
+        const unsigned ah[2] = {l0 + ra * 128 + swz(ra, fg) * 16, l0 + ra * 128 + swz(ra, 4 + fg) * 16};
+        const unsigned bh[2] = {l0 + AP * 1024 + rw * 128 + swz(rw, fg) * 16,
+                                l0 + AP * 1024 + rw * 128 + swz(rw, 4 + fg) * 16};
+        u32x4_t f[2][BG_NT + BG_MT];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][0]) : "v"(bh[ks]));
+          asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(f[ks][1]) : "v"(bh[ks]));
+#define F3_TREAD(X) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ah[ks]), "n"(2048 * (X)));
+          F3_TREAD(0) F3_TREAD(1) F3_TREAD(2) F3_TREAD(3) F3_TREAD(4) F3_TREAD(5) F3_TREAD(6) F3_TREAD(7) F3_TREAD(8)
+#undef F3_TREAD
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y) {
+              // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (the products' order of the loop below)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
+                                     acc[x][y]);
+              if (ks == 1)
+                acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
+                                       acc[x][y]);
+            }
+          if (ks == 0) {
+#pragma unroll
+            for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+              for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+          }
+        }
+      } else if constexpr (X3N) {
         // the hi and lo fragments of the block (chunks fg and 4 + fg), three products
         bf16x8 fah[BG_MT], fal[BG_MT], fbh[BG_NT], fbl[BG_NT];
 #pragma unroll
