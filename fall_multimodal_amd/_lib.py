@@ -22,7 +22,7 @@ EXPORTS = (
     "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_split_x3cat",
     "f3_conv_forward_x3cat", "f3_conv_backward_data_x3cat", "f3_conv_backward_weight_x3cat", "f3_graph_mix_forward",
     "f3_graph_mix_backward", "f3_graph_mix_forward_ex", "f3_graph_mix_backward_ex", "f3_net_backward_phase",
-    "f3_net_grad_split", "f3_net_wait_phase1", "f3_net_backward_rmsprop", "f3_net_fused_rmsprop", "f3_net_precision",
+    "f3_net_grad_split", "f3_net_wait_phase1", "f3_net_backward_rmsprop", "f3_net_fused_rmsprop", "f3_net_precision", "f3_net_status",
     "f3_targcn_create", "f3_targcn_destroy", "f3_targcn_num_entries", "f3_targcn_entry", "f3_targcn_param_count",
     "f3_targcn_buffer_count", "f3_targcn_workspace_bytes", "f3_targcn_forward", "f3_targcn_backward", "f3_targcn_stage_times", "f3_targcn_status", "f3_net_sensor_times", "f3_soft_ce",
     "f3_sktr_create", "f3_sktr_destroy", "f3_sktr_num_entries", "f3_sktr_entry", "f3_sktr_param_count",
@@ -85,6 +85,7 @@ def lib():
         "f3_net_backward_rmsprop": (I, [P, I, P, P, P, P, P, F, F, F, P]),
         "f3_net_fused_rmsprop": (I, [P]),
         "f3_net_precision": (I, [P]),
+        "f3_net_status": (I, [P, I]),
         "f3_rmsprop_step": (I, [P, P, P, I64, F, F, F, F, P]),
         "f3_conv_forward": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
         "f3_status_string": (ctypes.c_char_p, [I]),

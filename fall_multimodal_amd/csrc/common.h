@@ -148,3 +148,18 @@ inline bool f3_debug_sync() {
       return F3_EHIP;                                                                  \
     }                                                                                  \
   } while (0)
+// Raise a kernel's dynamic-LDS limit once per process (the result is cached per call site) and
+// fail as F3_EHIP when the runtime refuses it, naming the attribute instead of the launch after it.
+inline int f3_set_lds_limit(const void* fn, int bytes, const char* where, int line) {
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) return F3_OK;
+  (void)hipGetLastError();  // the refusal must not surface as the next launch's error
+  fprintf(stderr, "fall3: %s:%d hipFuncSetAttribute(MaxDynamicSharedMemorySize=%d) failed: %s\n", where, line, bytes,
+          hipGetErrorString(e));
+  return F3_EHIP;
+}
+#define F3_LDS_LIMIT(fn, bytes)                                                                  \
+  do {                                                                                           \
+    static const int _r = f3_set_lds_limit((const void*)(fn), (int)(bytes), __FILE__, __LINE__); \
+    if (_r != F3_OK) return _r;                                                                  \
+  } while (0)

@@ -1967,11 +1967,9 @@ static size_t mix_lds(const MixArgs& a, bool bwd) {
   return f * sizeof(float);
 }
 
-// kernels with no static LDS may take up to the full 160 KiB as dynamic LDS
-static void allow_big_lds(const void* fn) {
-  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipGetLastError();  // a refused attribute must not surface as the next launch's error
-}
+// kernels with no static LDS may take up to the full 160 KiB as dynamic LDS (F3_LDS_LIMIT: once per
+// kernel, a refusal returns F3_EHIP)
+#define F3_BIG_LDS(fn) F3_LDS_LIMIT(fn, 160 * 1024)
 
 static size_t mix_lds_bwd2(const MixArgs& a) {
   return sizeof(float) * std::max((size_t)(2 * a.V + a.K * a.V) * (a.Cin + 20), (size_t)a.K * a.V * a.V);
@@ -1979,8 +1977,7 @@ static size_t mix_lds_bwd2(const MixArgs& a) {
 
 template <int KS, int CIN, bool XB>
 static int launch_mix_fwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_fwd_wave_kernel<KS, CIN, XB>), true);
-  (void)once;
+  F3_BIG_LDS((mix_fwd_wave_kernel<KS, CIN, XB>));
   // a wave per frame (the workgroup-per-frame mix_fwd_lds_kernel measured slower; a bf16-MFMA form
   // with 64-channel groups assembled in LDS measured slower too: 31 / 34 / 29 us vs 25 / 25 / 25 at
   // the three layer shapes: the fp32 MFMA work is not what bounds these kernels)
@@ -2011,10 +2008,9 @@ static bool mix_lds_ok(const MixArgs& a) { return f3_mix_lds_ok(a.K, a.V, a.Cin)
 template <int CIN>
 static int launch_mix_fwd_bf16(const MixArgs* a, hipStream_t s) {
   constexpr size_t lds = (size_t)96 * (2 * CIN + 16);
+  F3_LDS_LIMIT(mix_fwd_bf16_kernel<CIN>, lds);
   static const int slots = [] {
     int per_cu = 0, dev = 0, cus = 256;
-    (void)hipFuncSetAttribute((const void*)mix_fwd_bf16_kernel<CIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mix_fwd_bf16_kernel<CIN>, 256, lds) !=
             hipSuccess || per_cu < 1)
       per_cu = 1;
@@ -2051,8 +2047,8 @@ static int launch_mix_fwd_x3(const MixArgs* a, hipStream_t s) {
     const size_t lds = mix_x3_lds_fwd<CIN>() + (size_t)a->V * 4 * a->K * CIN;
     if (lds > 160 * 1024) return F3_EINVAL;
     static size_t lds0 = lds;
-    static const int slots = (allow_big_lds((const void*)mix_fwd_x3_kernel<CIN, true>),
-                              resident_slots(mix_fwd_x3_kernel<CIN, true>, lds0));
+    F3_BIG_LDS((mix_fwd_x3_kernel<CIN, true>));
+    static const int slots = resident_slots(mix_fwd_x3_kernel<CIN, true>, lds0);
     const int grid = std::max(1, std::min(a->frames, lds == lds0 ? slots : 256));
     hipLaunchKernelGGL((mix_fwd_x3_kernel<CIN, true>), dim3(grid), dim3(256), lds, s, *a);
     F3_LAUNCH_CHECK();
@@ -2141,8 +2137,7 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
     const int r = a->Cin == 64 ? mix_fwd_ks<64>(a, s) : a->Cin == 128 ? mix_fwd_ks<128>(a, s) : mix_fwd_ks<256>(a, s);
     if (r >= 0) return r;
   }
-  static bool once = (allow_big_lds((const void*)mix_fwd_kernel), true);
-  (void)once;
+  F3_BIG_LDS(mix_fwd_kernel);
   if (mix_lds(*a, false) > 160 * 1024) return F3_EINVAL;
   const int grid = min(a->frames, 2048);
   hipLaunchKernelGGL(mix_fwd_kernel, dim3(grid), dim3(256), mix_lds(*a, false), s, *a);
@@ -2152,9 +2147,8 @@ int f3_mix_fwd(const MixArgs* a, hipStream_t s) {
 
 template <int KS, int CIN, bool ZB16>
 static int launch_mix_bwd(const MixArgs* a, hipStream_t s) {
-  static bool once = (allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16, false>),
-                      allow_big_lds((const void*)mix_bwd_lds_kernel<KS, CIN, ZB16, true>), true);
-  (void)once;
+  F3_BIG_LDS((mix_bwd_lds_kernel<KS, CIN, ZB16, false>));
+  F3_BIG_LDS((mix_bwd_lds_kernel<KS, CIN, ZB16, true>));
   const int grid = std::min(a->frames, 768);  // resident workgroups loop over frames
   if (a->accumulate)
     hipLaunchKernelGGL((mix_bwd_lds_kernel<KS, CIN, ZB16, true>), dim3(grid), dim3(256), mix_lds_bwd2(*a), s, *a);
@@ -2176,12 +2170,10 @@ template <int CIN>
 static size_t mix_bf16_lds() { return (size_t)96 * (2 * CIN + 16); }
 template <int CIN>
 static int mix_bwd_bf16_grid(const MixArgs* a) {
+  F3_LDS_LIMIT((mix_bwd_bf16_kernel<CIN, false>), mix_bf16_lds<CIN>());
+  F3_LDS_LIMIT((mix_bwd_bf16_kernel<CIN, true>), mix_bf16_lds<CIN>());
   static const int slots = [] {
     int per_cu = 0, dev = 0, cus = 256;
-    (void)hipFuncSetAttribute((const void*)mix_bwd_bf16_kernel<CIN, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)mix_bf16_lds<CIN>());
-    (void)hipFuncSetAttribute((const void*)mix_bwd_bf16_kernel<CIN, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)mix_bf16_lds<CIN>());
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mix_bwd_bf16_kernel<CIN, true>, 256,
                                                      mix_bf16_lds<CIN>()) != hipSuccess || per_cu < 1)
       per_cu = 1;
@@ -2249,8 +2241,7 @@ int f3_mix_bwd(const MixArgs* a, hipStream_t s) {
     if (r >= 0) return r;
   }
   if (a->dzb) return F3_EINVAL;  // the generic kernel reads fp32 dZ
-  static bool once = (allow_big_lds((const void*)mix_bwd_kernel), true);
-  (void)once;
+  F3_BIG_LDS(mix_bwd_kernel);
   if (a->K * a->V * a->V > 1024 || mix_lds(*a, true) > 160 * 1024) return F3_EINVAL;
   const int grid = min(a->frames, 1024);
   hipLaunchKernelGGL(mix_bwd_kernel, dim3(grid), dim3(256), mix_lds(*a, true), s, *a);

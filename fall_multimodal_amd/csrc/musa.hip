@@ -953,13 +953,7 @@ int f3_mu_dropmask_scratch_floats(int N, int T, int V) { return 2 * N * V + N * 
 int f3_mu_dropmask(const DropMaskArgs* a, hipStream_t s) {
   const size_t lds = sizeof(float) * 2 * (size_t)a->N * a->T;
   if (a->V > 32 || a->T > 64 || a->T * a->V > 64 * 32 || lds > 150 * 1024 || !a->scr) return F3_EINVAL;
-  static bool once = [] {
-    (void)hipFuncSetAttribute((const void*)mu_drop_final_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              150 * 1024);
-    (void)hipGetLastError();
-    return true;
-  }();
-  (void)once;
+  F3_LDS_LIMIT(mu_drop_final_kernel, 150 * 1024);
   hipLaunchKernelGGL(mu_drop_s_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(mu_drop_t_kernel, dim3(a->N), dim3(256), 0, s, *a);

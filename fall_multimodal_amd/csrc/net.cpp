@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "common.h"
+#include "status_ring.h"
 #include "kernels.h"
 #include "layers.h"
 #include "sensor.h"
@@ -95,6 +96,10 @@ struct f3_net {
   // 2 | backward | 3
   int stiming = 0;
   hipEvent_t sev[4] = {};
+  // the cooperative CNN1D's group-barrier error word (sync[0] of its forward / backward launch),
+  // copied to the host after each launch; reported once as F3_EDEVICE by the next f3_net_forward /
+  // backward call or f3_net_status (status_ring.h)
+  StatusRing cstatus;
   void smark(int i, hipStream_t s) {
     if (stiming && sev[i]) (void)hipEventRecord(sev[i], s);
   }
@@ -1280,6 +1285,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
                    const float* skel, const float* sensor, float* out, void* workspace, void* stream) {
   if (!net || !params || !buffers || !out || !workspace || N < 1) return F3_EINVAL;
   if (training && N < 2) return F3_EBATCH;
+  F3_TRY(net->cstatus.take(false));
   hipStream_t s = (hipStream_t)stream;
   Ws w = plan(*net, N, (char*)workspace);
   Ptrs q{*net, params, buffers, counters, nullptr};
@@ -1318,6 +1324,7 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
       net->smark(0, ss);
       F3_TRY(f3_cnn1d_fwd(&c1, &c2, &coop, ss));
       net->smark(1, ss);
+      if (training) F3_TRY(net->cstatus.post(w.csyncf, ss));
       if (training) {
         add_bnrun(run, q, net->cnn.bn1, w.cbn1.fsum, w.cbn1.fsq, (double)N * net->cfg.sensor_frames);
         add_bnrun(run, q, net->cnn.bn2, w.cbn2.fsum, w.cbn2.fsq, (double)N * (net->cfg.sensor_frames / 2));
@@ -1455,6 +1462,11 @@ int f3_net_fused_rmsprop(f3_net* net) {
 
 int f3_net_precision(const f3_net* net) { return net ? net->cfg.precision : -1; }
 
+int f3_net_status(f3_net* net, int wait) {
+  if (!net) return F3_EINVAL;
+  return net->cstatus.take(wait != 0);
+}
+
 int f3_net_backward_phase(f3_net* net, int N, const float* params, const float* dout, float* grads, void* workspace,
                           int phase, void* stream) {
   return net_backward(net, N, params, dout, grads, workspace, phase, stream, nullptr);
@@ -1467,6 +1479,7 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
                  void* stream, const FusedOpt* opt) {
   if (!net || !params || !grads || !workspace || N < 2 || phase < 0 || phase > 2) return F3_EINVAL;
   if (phase != 2 && !dout) return F3_EINVAL;
+  F3_TRY(net->cstatus.take(false));
   if (opt && phase != 0) return F3_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   Ws w = plan(*net, N, (char*)workspace);
@@ -1546,6 +1559,7 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
       net->smark(2, ss);
       F3_TRY(f3_cnn1d_bwd(&c1, &c2, &coop, ss));
       net->smark(3, ss);
+      F3_TRY(net->cstatus.post(w.csyncb, ss));
     }
     return F3_OK;
   };
@@ -1926,7 +1940,7 @@ const char* f3_status_string(int st) {
     case F3_EBATCH: return "Expected more than 1 value per channel when training";
     case F3_EHIP: return "HIP launch error";
     case F3_ESTATE: return "backward without a training forward";
-    case F3_EDEVICE: return "device-side check failed (a GRU group barrier timed out; outputs are invalid)";
+    case F3_EDEVICE: return "device-side check failed (a group barrier timed out: TARGCN GRU or sensor CNN1D; outputs are invalid)";
     default: return "unknown status";
   }
 }

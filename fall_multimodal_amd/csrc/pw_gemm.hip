@@ -395,15 +395,13 @@ bool f3_pw_ok(const ConvGemmArgs& a, int epi) {
 constexpr int pw_bm(int ks) { return ks > 8 ? 32 : 64; }
 
 template <int EPI, int KS, int WN, bool F32O = false, bool X3N = false>
-static void pw_launch(const ConvGemmArgs& a, int grid, int ncg, int per_wg, hipStream_t s) {
+static int pw_launch(const ConvGemmArgs& a, int grid, int ncg, int per_wg, hipStream_t s) {
   constexpr int BM = pw_bm(KS);
   constexpr int lds = PwLds<EPI, KS, WN, BM, F32O>::BYTES;
-  static bool once = (hipFuncSetAttribute((const void*)pw_gemm_kernel<EPI, KS, WN, BM, F32O, X3N>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds),
-                      true);
-  (void)once;
+  F3_LDS_LIMIT((pw_gemm_kernel<EPI, KS, WN, BM, F32O, X3N>), lds);
   hipLaunchKernelGGL((pw_gemm_kernel<EPI, KS, WN, BM, F32O, X3N>), dim3(grid), dim3(PW_THREADS), lds, s, a, ncg,
                      per_wg);
+  return F3_OK;
 }
 
 int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
@@ -430,13 +428,13 @@ int f3_pw_gemm(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const int grid = ncg * nranges;
 #define F3_PW_LAUNCH(E, KSV, WNV)                                 \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) {                 \
-    pw_launch<(E), KSV, WNV>(a, grid, ncg, per_wg, s);            \
+    F3_TRY((pw_launch<(E), KSV, WNV>(a, grid, ncg, per_wg, s)));   \
     F3_LAUNCH_CHECK();                                            \
     return F3_OK;                                                 \
   }
 #define F3_PW_LAUNCH_X3N(E, KSV, WNV)                                          \
   if (epi == (E) && ks == (KSV) && wn == (WNV)) {                              \
-    pw_launch<(E), KSV, WNV, (E) != EPI_ADD, true>(a, grid, ncg, per_wg, s);   \
+    F3_TRY((pw_launch<(E), KSV, WNV, (E) != EPI_ADD, true>(a, grid, ncg, per_wg, s))); \
     F3_LAUNCH_CHECK();                                                         \
     return F3_OK;                                                              \
   }

@@ -603,7 +603,9 @@ F3_DEV Acc coop_colsum(const float* part, int ld, int c, int r0, int dr, int G) 
 // serialize at the memory side). Words 256 B apart (sync layout: err | top | release | groups).
 constexpr int kCoopGS = 16;
 constexpr int kCoopSyncInts = 64 * (3 + kCnnCoopG / kCoopGS);
-F3_DEV void coop_barrier(int* sync, int k, int G) {
+// skip (tests only, F3_CNN_SKIP_ARRIVE): workgroup 0 never arrives, so every barrier of the launch
+// times out, after 2^14 polls instead of 2^22
+F3_DEV void coop_barrier(int* sync, int k, int G, int skip) {
   if (F3_PROBE & 1) {
     __syncthreads();
     return;
@@ -616,14 +618,16 @@ F3_DEV void coop_barrier(int* sync, int k, int G) {
   if (threadIdx.x == 0) {
     const int g = blockIdx.x / kCoopGS, ng = (G + kCoopGS - 1) / kCoopGS;
     const int gsz = min(kCoopGS, G - g * kCoopGS);
-    if (__hip_atomic_fetch_add(sync + 192 + 64 * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gsz - 1 &&
+    if (!(skip && blockIdx.x == 0) &&
+        __hip_atomic_fetch_add(sync + 192 + 64 * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gsz - 1 &&
         __hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * ng - 1)
       __hip_atomic_store(rel, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lim = skip ? (1 << 14) : (1 << 22);
     int polls = 0;
     while (__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
       __builtin_amdgcn_s_sleep(2);
       if ((++polls & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      if (polls > (1 << 22)) {
+      if (polls > lim) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -640,6 +644,7 @@ struct CnnCoopArgs {
   float* part;
   int* sync;
   int G;
+  int skip;  // tests: F3_CNN_SKIP_ARRIVE (coop_barrier)
 };
 
 // lanes per output of a convolution over `red` reduced channels: 4, 2 or 1 (all outputs of a clip
@@ -765,7 +770,7 @@ __global__ __launch_bounds__(kCoopNT) void cnn1d_coop_fwd_kernel(CnnCoopArgs a) 
   }
   coop_rowsum(s1, part1 + (size_t)b * 2 * C1, red, C1, Q1);
   coop_rowsum(s2, part1 + (size_t)b * 2 * C1 + C1, red, C1, Q1);
-  coop_barrier(a.sync, 1, G);
+  coop_barrier(a.sync, 1, G, a.skip);
   // BN1 + ReLU + pool1 -> p1, conv2 + BN2 partial sums
   coop_bn_stats(part1, G, C1, c1.bn, c1.st_sum, c1.st_sq, co, redd);
   s1 = s2 = 0.f;
@@ -777,7 +782,7 @@ __global__ __launch_bounds__(kCoopNT) void cnn1d_coop_fwd_kernel(CnnCoopArgs a) 
   }
   coop_rowsum(s1, part2 + (size_t)b * 2 * C2, red, C2, Q2);
   coop_rowsum(s2, part2 + (size_t)b * 2 * C2 + C2, red, C2, Q2);
-  coop_barrier(a.sync, 2, G);
+  coop_barrier(a.sync, 2, G, a.skip);
   // BN2 + ReLU + pool2 -> p2 (the LSTM input)
   coop_bn_stats(part2, G, C2, c2.bn, c2.st_sum, c2.st_sq, co, redd);
   const bool bad = coop_failed(a.sync);
@@ -907,7 +912,7 @@ __global__ __launch_bounds__(kCoopNT) void cnn1d_coop_bwd_kernel(CnnCoopArgs a) 
                   c2.dy + (size_t)n * T2 * C2, s1, s2);
   coop_rowsum(s1, part3 + (size_t)b * 2 * C2, red, C2);
   coop_rowsum(s2, part3 + (size_t)b * 2 * C2 + C2, red, C2);
-  coop_barrier(a.sync, 1, G);
+  coop_barrier(a.sync, 1, G, a.skip);
   // BN2 backward, conv2 backward (dW2, db2, dp1), pool1 / ReLU1 backward + BN1 backward partial sums
   coop_bn_bwd_sums(part3, G, C2, c2.bn.count, c2.g_gamma, c2.g_beta, co2, redd);
   float gw[kCoopWMAX], gb = 0.f;
@@ -942,7 +947,7 @@ __global__ __launch_bounds__(kCoopNT) void cnn1d_coop_bwd_kernel(CnnCoopArgs a) 
   coop_wgrad_row(gw, gb, NW2, C2, part4 + (size_t)b * (NW2 + C2));
   coop_rowsum(s1, part5 + (size_t)b * 2 * C1, red, C1);
   coop_rowsum(s2, part5 + (size_t)b * 2 * C1 + C1, red, C1);
-  coop_barrier(a.sync, 2, G);
+  coop_barrier(a.sync, 2, G, a.skip);
   // BN1 backward, conv1 weight gradient
   coop_bn_bwd_sums(part5, G, C1, c1.bn.count, c1.g_gamma, c1.g_beta, co1, redd);
 #pragma unroll
@@ -956,7 +961,7 @@ __global__ __launch_bounds__(kCoopNT) void cnn1d_coop_bwd_kernel(CnnCoopArgs a) 
     if (!(F3_PROBE & 4)) coop_wgrad(dcs, xs, T1, Ci1, C1, gw, gb);
   }
   coop_wgrad_row(gw, gb, NW1, C1, part6 + (size_t)b * (NW1 + C1));
-  coop_barrier(a.sync, 3, G);
+  coop_barrier(a.sync, 3, G, a.skip);
   // column sums of the weight / bias gradient rows: 64 columns per workgroup pass, 16 row groups
   // (rows r = g, g + 16, ...) added in group order
   const bool bad = coop_failed(a.sync);
@@ -1006,9 +1011,7 @@ int f3_lstm_bwd(const LstmArgs* a, hipStream_t s) {
   dim3 grid((a->N + LSTM_NB - 1) / LSTM_NB, 2);
   const size_t lds = lstm_bwd_lds(*a);
   if (lds > 160 * 1024) return F3_EINVAL;
-  static bool once = (hipFuncSetAttribute((const void*)lstm_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024), (void)hipGetLastError(), true);
-  (void)once;
+  F3_LDS_LIMIT(lstm_bwd_kernel, 160 * 1024);
   hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), lds, s, *a);
   F3_LAUNCH_CHECK();
   if (!a->wpart) return F3_OK;
@@ -1080,6 +1083,15 @@ size_t f3_cnn1d_coop_part_floats(int N, int Ci1, int Co1, int Co2) {
 }
 }  // namespace f3
 
+static size_t cnn_coop_fwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
+  return kCoopNT * 12 + 4 * ((size_t)c1.Co * c1.Ci * 5 + (size_t)c2.Co * c1.Co * 5 + (size_t)c1.T * c1.Ci +
+                             (size_t)c2.T * c1.Co + 4 * c2.Co);
+}
+static size_t cnn_coop_bwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
+  return kCoopNT * 12 + 4 * ((size_t)c2.Co * c1.Co * 5 + std::max(c2.T * c2.Co, c1.T * c1.Co) +
+                             std::max(c2.T * c1.Co, c1.T * c1.Ci) + (size_t)c2.T * c1.Co + 6 * c1.Co + 6 * c2.Co);
+}
+
 // the cooperative form applies (training statistics, both layers' shapes in range, one row of
 // channel sums per workgroup pass); otherwise the caller runs the per-layer launches
 static bool cnn_coop_ok(const Conv1dArgs& c1, const Conv1dArgs& c2, const CnnCoop* coop) {
@@ -1089,17 +1101,12 @@ static bool cnn_coop_ok(const Conv1dArgs& c1, const Conv1dArgs& c2, const CnnCoo
   if (!c1d_ok(c1) || !c1d_ok(c2) || c2.Ci != c1.Co || c2.T != c1.T / 2 || c2.N != c1.N || c2.T < 2 || c1.Co > c2.Co)
     return false;
   // whole stats row groups; channel-fixed threads for every lane split (kCoopNT / Q % Co == 0)
-  return kCoopNT % (2 * c1.Co) == 0 && kCoopNT % (2 * c2.Co) == 0 && (kCoopNT / 4) % c2.Co == 0 &&
-         (kCoopNT / 4) % c1.Co == 0;
-}
-
-static size_t cnn_coop_fwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
-  return kCoopNT * 12 + 4 * ((size_t)c1.Co * c1.Ci * 5 + (size_t)c2.Co * c1.Co * 5 + (size_t)c1.T * c1.Ci +
-                             (size_t)c2.T * c1.Co + 4 * c2.Co);
-}
-static size_t cnn_coop_bwd_lds(const Conv1dArgs& c1, const Conv1dArgs& c2) {
-  return kCoopNT * 12 + 4 * ((size_t)c2.Co * c1.Co * 5 + std::max(c2.T * c2.Co, c1.T * c1.Co) +
-                             std::max(c2.T * c1.Co, c1.T * c1.Ci) + (size_t)c2.T * c1.Co + 6 * c1.Co + 6 * c2.Co);
+  if (!(kCoopNT % (2 * c1.Co) == 0 && kCoopNT % (2 * c2.Co) == 0 && (kCoopNT / 4) % c2.Co == 0 &&
+        (kCoopNT / 4) % c1.Co == 0))
+    return false;
+  // both directions' per-clip tensors must fit the 64 KiB the launch takes (it grows with the sensor
+  // frames: e.g. T >= 300 at Ci = 4); longer clips take the per-layer launches
+  return cnn_coop_fwd_lds(c1, c2) <= 64 * 1024 && cnn_coop_bwd_lds(c1, c2) <= 64 * 1024;
 }
 
 // a plain launch of G <= CUs workgroups of 1024 threads (one per CU): a cooperative launch measured
@@ -1120,6 +1127,8 @@ static int cnn_coop_launch(void (*fn)(CnnCoopArgs), const Conv1dArgs& c1, const 
   arg.part = coop.part;
   arg.sync = coop.sync;
   arg.G = std::min(std::min(c1.N, kCnnCoopG), cus);
+  const char* skip = getenv("F3_CNN_SKIP_ARRIVE");  // tests: force a barrier timeout (read per call)
+  arg.skip = skip && atoi(skip) != 0;
   if (lds > 64 * 1024) return F3_EINVAL;
   hipLaunchKernelGGL(fn, dim3(arg.G), dim3(kCoopNT), lds, s, arg);
   F3_LAUNCH_CHECK();

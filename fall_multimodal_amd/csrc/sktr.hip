@@ -574,15 +574,8 @@ static int grid_for(long long items, int cap = 2048) {
 
 template <int L>
 static int launch_attn(const AttnArgs& a, bool bwd, hipStream_t s) {
-  static bool once = [] {
-    (void)hipFuncSetAttribute((const void*)sk_attn_fwd_kernel<L>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)attn_fwd_lds<L>());
-    (void)hipFuncSetAttribute((const void*)sk_attn_bwd_kernel<L>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)attn_bwd_lds<L>());
-    (void)hipGetLastError();
-    return true;
-  }();
-  (void)once;
+  F3_LDS_LIMIT(sk_attn_fwd_kernel<L>, attn_fwd_lds<L>());
+  F3_LDS_LIMIT(sk_attn_bwd_kernel<L>, attn_bwd_lds<L>());
   const int threads = attn_threads(L);
   if (bwd)
     hipLaunchKernelGGL(sk_attn_bwd_kernel<L>, dim3(a.nseq), dim3(threads), attn_bwd_lds<L>(), s, a);

@@ -2791,10 +2791,6 @@ using namespace f3;
 using namespace f3::tg;
 
 namespace {
-template <typename K>
-void allow_lds(K kernel, int bytes) {
-  if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-}
 template <bool B16>
 int gru_lds(int V, bool bwd) {
   using TT = typename Op<B16>::T;
@@ -2826,8 +2822,7 @@ int f3_tg_prep(const PrepArgs* a, int b16, hipStream_t s) {
 template <bool B16>
 static int gru_fwd_launch(const GruFwdArgs& a, hipStream_t s) {
   const int lds = gru_lds<B16>(a.V, false);
-  static bool once = (allow_lds(gru_fwd_kernel<B16>, 160 * 1024), true);
-  (void)once;
+  F3_LDS_LIMIT(gru_fwd_kernel<B16>, 160 * 1024);
   const int grid = (a.B + Op<B16>::BTF - 1) / Op<B16>::BTF;
   hipLaunchKernelGGL(gru_fwd_kernel<B16>, dim3(grid), dim3(GRU_THREADS), lds, s, a);
   F3_LAUNCH_CHECK();
@@ -2837,8 +2832,7 @@ static int gru_fwd_launch(const GruFwdArgs& a, hipStream_t s) {
 template <bool B16>
 static int gru_bwd_launch(const GruBwdArgs& a, hipStream_t s) {
   const int lds = gru_lds<B16>(a.V, true);
-  static bool once = (allow_lds(gru_bwd_kernel<B16>, 160 * 1024), true);
-  (void)once;
+  F3_LDS_LIMIT(gru_bwd_kernel<B16>, 160 * 1024);
   const int grid = (a.B + Op<B16>::BTB - 1) / Op<B16>::BTB;
   hipLaunchKernelGGL(gru_bwd_kernel<B16>, dim3(grid), dim3(GRU_THREADS), lds, s, a);
   F3_LAUNCH_CHECK();
@@ -2987,15 +2981,13 @@ static int ta_grid(const TaArgs& a) {
 
 int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
   if (a->b16) {  // bf16 mode: one wave per sequence on bf16 MFMA
-    static bool once_m = (allow_lds(ta_fwd_mfma_kernel, TAM_LDS), true);
-    (void)once_m;
+    F3_LDS_LIMIT(ta_fwd_mfma_kernel, TAM_LDS);
     const int grid = std::max(1, std::min(ta_grid(*a), (a->B * a->V + TAM_WAVES - 1) / TAM_WAVES));
     hipLaunchKernelGGL(ta_fwd_mfma_kernel, dim3(grid), dim3(64 * TAM_WAVES), TAM_LDS, s, *a);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }
-  static bool once = (allow_lds(ta_fwd_kernel, TA_FWD_LDS), true);
-  (void)once;
+  F3_LDS_LIMIT(ta_fwd_kernel, TA_FWD_LDS);
   hipLaunchKernelGGL(ta_fwd_kernel, dim3(ta_grid(*a)), dim3(TA_THREADS), TA_FWD_LDS, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;
@@ -3004,9 +2996,8 @@ int f3_tg_ta_fwd(const TaArgs* a, hipStream_t s) {
 int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
   const TaArgs* a = a_;
   if (a->b16) {  // bf16 mode: one wave per sequence on bf16 MFMA
-    static bool once_m = (allow_lds(ta_bwd_mfma_kernel<1>, std::max(TAB_LDS1, TAB_RED_LDS)),
-                          allow_lds(ta_bwd_mfma_kernel<2>, std::max(TAB_LDS2, TAB_RED_LDS)), true);
-    (void)once_m;
+    F3_LDS_LIMIT(ta_bwd_mfma_kernel<1>, std::max(TAB_LDS1, TAB_RED_LDS));
+    F3_LDS_LIMIT(ta_bwd_mfma_kernel<2>, std::max(TAB_LDS2, TAB_RED_LDS));
     const int grid = std::max(1, std::min({ta_grid(*a), (a->B * a->V + TAB_WAVES - 1) / TAB_WAVES, TA_MAX_WG}));
     // the workgroup reduction reuses the LDS as [4 waves][4096] + column sums
     const int lds1 = a->part ? std::max(TAB_LDS1, TAB_RED_LDS) : TAB_LDS1;
@@ -3041,8 +3032,7 @@ int f3_tg_ta_bwd(const TaArgs* a_, hipStream_t s) {
     }
     return F3_OK;
   }
-  static bool once = (allow_lds(ta_bwd_kernel, TA_BWD_LDS), true);
-  (void)once;
+  F3_LDS_LIMIT(ta_bwd_kernel, TA_BWD_LDS);
   hipLaunchKernelGGL(ta_bwd_kernel, dim3(ta_grid(*a)), dim3(TA_THREADS), TA_BWD_LDS, s, *a);
   F3_LAUNCH_CHECK();
   return F3_OK;

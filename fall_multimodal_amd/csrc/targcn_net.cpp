@@ -20,6 +20,7 @@
 #include "fall3.h"
 #include "kernels.h"
 #include "sensor.h"
+#include "status_ring.h"
 #include "targcn.h"
 
 using namespace f3;
@@ -58,18 +59,15 @@ struct f3_targcn {
   // f3_targcn_stage_times: timing events around the recurrences and the TA layers (0 = off)
   int timing = 0;
   hipEvent_t tev[11] = {};
-  // GRU group-barrier error flag, copied after the recurrences of every call into the next slot of a
-  // ring of pinned host words (one event each), so a flag is never overwritten by a later call's copy
-  // before the host has read it; `sticky` keeps a read flag until a status query reports it
-  static constexpr int kStatusRing = 16;
-  int* status_host = nullptr;              // [kStatusRing]
-  hipEvent_t status_ev[kStatusRing] = {};
-  int status_head = 0, status_count = 0;   // oldest pending slot, number of pending copies
-  bool sticky = false;
+  // GRU group-barrier error flag: copied after the recurrences of every call into a pinned ring
+  // (status_ring.h), reported once as F3_EDEVICE
+  StatusRing status;
+  // F3_TG_PROF (debugging aid): the GRU forward / backward per-phase stamp buffers, owned here so they are
+  // released by f3_targcn_destroy, never by an exit-time destructor after the HIP runtime's teardown
+  long long* prof[2] = {nullptr, nullptr};
   ~f3_targcn() {
     for (auto& e : tev) if (e) (void)hipEventDestroy(e);
-    for (auto& e : status_ev) if (e) (void)hipEventDestroy(e);
-    if (status_host) (void)hipHostFree(status_host);
+    for (auto& p : prof) if (p) (void)hipFree(p);
   }
 
   int64_t add(const std::string& name, std::vector<int64_t> shape, int kind = F3_ENTRY_PARAM) {
@@ -232,62 +230,10 @@ int gn_skip_arrive(bool backward) {
   return v == 1 || (v == 2 && backward);
 }
 
-bool capturing(hipStream_t s) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
-    (void)hipGetLastError();
-    return true;
-  }
-  return cs != hipStreamCaptureStatusNone;
-}
+int take_status(f3_targcn* net, bool wait) { return net->status.take(wait); }
 
-// fold the completed copies (oldest first; wait: all of them) into `sticky`; a flag raised by any
-// earlier call -> F3_EDEVICE once (then cleared)
-int take_status(f3_targcn* net, bool wait) {
-  while (net->status_count > 0) {
-    const int i = net->status_head;
-    if (wait) {
-      if (hipEventSynchronize(net->status_ev[i]) != hipSuccess) return F3_EHIP;
-    } else if (hipEventQuery(net->status_ev[i]) != hipSuccess) {
-      (void)hipGetLastError();
-      break;  // later copies are behind this one on the same stream order
-    }
-    net->sticky = net->sticky || net->status_host[i] != 0;
-    net->status_host[i] = 0;
-    net->status_head = (i + 1) % f3_targcn::kStatusRing;
-    --net->status_count;
-  }
-  if (!net->sticky) return F3_OK;
-  net->sticky = false;
-  return F3_EDEVICE;
-}
-
-// enqueue the copy of the flag (gsync[GN_MAXG]) into the next free slot of the ring (a full ring
-// first waits for its oldest copy and folds it into `sticky`)
-int post_status(f3_targcn* net, const int* gsync, hipStream_t s) {
-  constexpr int R = f3_targcn::kStatusRing;
-  if (capturing(s)) return F3_OK;  // the node-partitioned path is off under capture
-  if (!net->status_host) {
-    if (hipHostMalloc(&net->status_host, sizeof(int) * R, hipHostMallocDefault) != hipSuccess) return F3_EHIP;
-    for (int i = 0; i < R; ++i) net->status_host[i] = 0;
-  }
-  if (net->status_count == R) {
-    const int i = net->status_head;
-    if (hipEventSynchronize(net->status_ev[i]) != hipSuccess) return F3_EHIP;
-    net->sticky = net->sticky || net->status_host[i] != 0;
-    net->status_host[i] = 0;
-    net->status_head = (i + 1) % R;
-    --net->status_count;
-  }
-  const int slot = (net->status_head + net->status_count) % R;
-  if (!net->status_ev[slot] && hipEventCreateWithFlags(&net->status_ev[slot], hipEventDisableTiming) != hipSuccess)
-    return F3_EHIP;
-  if (hipMemcpyAsync(net->status_host + slot, gsync + GN_MAXG, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
-    return F3_EHIP;
-  if (hipEventRecord(net->status_ev[slot], s) != hipSuccess) return F3_EHIP;
-  ++net->status_count;
-  return F3_OK;
-}
+// enqueue the copy of the flag (gsync[GN_MAXG]); the node-partitioned path is off under capture
+int post_status(f3_targcn* net, const int* gsync, hipStream_t s) { return net->status.post(gsync + GN_MAXG, s); }
 
 }  // namespace
 
@@ -408,7 +354,7 @@ int f3_targcn_forward(f3_targcn* net, int B, const float* params, const float* b
     g.XG = at<void>(ws, p.XG[l]); g.XI = at<void>(ws, p.XI[l]); g.UG = at<void>(ws, p.UG[l]); g.UI = at<void>(ws, p.UI[l]);
     g.hx = at<unsigned short>(ws, p.hx); g.rhx = at<unsigned short>(ws, p.rhx); g.gsync = at<int>(ws, p.gsync);
     g.dbg_skip_arrive = gn_skip_arrive(false);
-    static long long* prof = nullptr;
+    long long*& prof = net->prof[0];
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
     TG_TRY(f3_tg_gru_fwd(&g, b16, s));
@@ -502,7 +448,7 @@ int f3_targcn_backward(f3_targcn* net, int B, const float* params, const float* 
     g.DXG = at<void>(ws, p.DXG); g.DUG = at<void>(ws, p.DUG);
     g.gx1 = at<unsigned short>(ws, p.gx1); g.gx2 = at<unsigned short>(ws, p.gx2); g.gsync = at<int>(ws, p.gsync);
     g.dbg_skip_arrive = gn_skip_arrive(true);
-    static long long* prof = nullptr;
+    long long*& prof = net->prof[1];
     if (getenv("F3_TG_PROF") && !prof && hipMalloc(&prof, T * 8 * sizeof(long long)) != hipSuccess) prof = nullptr;
     g.prof = getenv("F3_TG_PROF") ? prof : nullptr;
     mark(net, l == 1 ? 7 : 9, s);

@@ -255,15 +255,11 @@ int f3_tcn64(const ConvGemmArgs* args, int epi, hipStream_t s) {
   const int per_wg = (ntiles + cus - 1) / cus;
   const int grid = (ntiles + per_wg - 1) / per_wg;
   if (epi == (EPI_BIAS | EPI_STATS | EPI_GAP)) {
-    static bool once = (hipFuncSetAttribute((const void*)tcn64_kernel<EPI_BIAS | EPI_STATS | EPI_GAP>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, T64_LDS), true);
-    (void)once;
+    F3_LDS_LIMIT((tcn64_kernel<EPI_BIAS | EPI_STATS | EPI_GAP>), T64_LDS);
     hipLaunchKernelGGL((tcn64_kernel<EPI_BIAS | EPI_STATS | EPI_GAP>), dim3(grid), dim3(T64_THREADS), T64_LDS, s, a,
                        ntiles, per_wg);
   } else if (epi == EPI_RELUMASK) {
-    static bool once = (hipFuncSetAttribute((const void*)tcn64_kernel<EPI_RELUMASK>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, T64_LDS), true);
-    (void)once;
+    F3_LDS_LIMIT(tcn64_kernel<EPI_RELUMASK>, T64_LDS);
     hipLaunchKernelGGL((tcn64_kernel<EPI_RELUMASK>), dim3(grid), dim3(T64_THREADS), T64_LDS, s, a, ntiles, per_wg);
   } else {
     return F3_EINVAL;

@@ -23,6 +23,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import sys
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -47,6 +48,19 @@ def default_precision():
     if p not in PRECISION_IDS:
         raise ValueError(f"F3_PRECISION must be one of {sorted(PRECISION_IDS)}, got {p!r}")
     return p
+
+
+_PRECISION_LOGGED = set()
+
+
+def _log_precision_once(prec, defaulted):
+    """One stderr line per process and precision when a net is built: the default moved from fp32
+    to bf16x3 in round 5, so a caller that relied on the old default is told."""
+    if prec in _PRECISION_LOGGED or os.environ.get("F3_QUIET"):
+        return
+    _PRECISION_LOGGED.add(prec)
+    how = "default; F3_PRECISION or precision= selects fp32 / bf16" if defaulted else "requested"
+    print(f"fall_multimodal_amd: skeleton GEMMs in {prec} ({how})", file=sys.stderr)
 
 
 @dataclass
@@ -83,11 +97,12 @@ class NativeNet:
         c.softmax_output = int(spec.softmax_output)
         c.naming = 1 if spec.naming == "notebook" else 0
         c.frames, c.sensor_frames = spec.frames, spec.sensor_frames
-        if spec.precision is None:
-            spec.precision = default_precision()
-        if spec.precision not in PRECISION_IDS:
-            raise ValueError(f"precision must be one of {sorted(PRECISION_IDS)}, got {spec.precision!r}")
-        c.precision = PRECISION_IDS[spec.precision]
+        # resolved here, not written back into the caller's spec
+        prec = spec.precision if spec.precision is not None else default_precision()
+        if prec not in PRECISION_IDS:
+            raise ValueError(f"precision must be one of {sorted(PRECISION_IDS)}, got {prec!r}")
+        _log_precision_once(prec, spec.precision is None)
+        c.precision = PRECISION_IDS[prec]
         h = ctypes.c_void_p()
         check(L.f3_net_create(ctypes.byref(c), ctypes.byref(h)), "f3_net_create")
         self.h = h
@@ -99,7 +114,7 @@ class NativeNet:
                                  ctypes.byref(off)), "f3_net_entry")
             self.entries.append((name.value.decode(), kind.value, tuple(shape[d] for d in range(nd.value)),
                                  off.value))
-        self.precision = spec.precision
+        self.precision = prec
         self.nparam = L.f3_net_param_count(h)
         self.nbuf = L.f3_net_buffer_count(h)
         self.ncnt = L.f3_net_counter_count(h)
@@ -239,6 +254,17 @@ class Fall3Net(nn.Module):
 
     def flat_parameters(self):
         return self._flat_params
+
+    @property
+    def precision(self):
+        """The precision the native net was built with (spec.precision, or the default it resolved to)."""
+        return self._native.precision
+
+    def device_status(self, wait=True):
+        """Raise if a device-side check of the last training forward / backward failed (F3_EDEVICE:
+        the sensor branch's cooperative CNN1D group barrier timed out and wrote NaN into its outputs);
+        wait=False checks only copies that have completed. The next forward / backward also raises."""
+        check(lib().f3_net_status(self._native.h, 1 if wait else 0), "fall3 device status")
 
     def param_views(self):
         return [(name, shape, off) for name, kind, shape, off in self._native.entries if kind == ENTRY_PARAM]

@@ -32,14 +32,17 @@ class GradSync:
     the phase-1 gradients: the head bucket is then issued from a side stream ordered after them
     rather than after everything on the caller's stream."""
 
-    def __init__(self, grads: torch.Tensor, split: int, group=None, wait_phase1=None):
+    def __init__(self, grads: torch.Tensor, split: int, group=None, wait_phase1=None, force=False):
         self.grads, self.split, self.group = grads, int(split), group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.wait_phase1 = wait_phase1
+        # force: issue both buckets even at world 1 (a world-1 sum is the identity), so the collective
+        # path runs on a one-GPU box (tests/test_gpu_rccl.py); needs an initialised process group
+        self.active = self.world > 1 or bool(force)
         # high priority: ROCm draws high-priority streams from their own hardware-queue pool, so the head
         # bucket's wait + all-reduce never queue behind main-chain kernels on a shared normal-priority
         # queue (the step's four native queues already fill GPU_MAX_HW_QUEUES = 4; DESIGN.md §5)
-        self._side = (torch.cuda.Stream(device=grads.device, priority=-1) if (self.world > 1 and grads.is_cuda)
+        self._side = (torch.cuda.Stream(device=grads.device, priority=-1) if (self.active and grads.is_cuda)
                       else None)
         self._work = []
 
@@ -50,7 +53,7 @@ class GradSync:
     def start_head(self, after_current=False):
         """after_current: order the bucket after everything on the caller's stream (a replayed
         graph, whose phase 1 joined its queues) instead of after phase 1's per-queue events."""
-        if self.world <= 1:
+        if not self.active:
             return
         if after_current and self._side is not None:
             self._side.wait_stream(torch.cuda.current_stream())
@@ -65,7 +68,7 @@ class GradSync:
             self._reduce(self.grads[:self.split])
 
     def start_tail(self):
-        if self.world > 1:
+        if self.active:
             self._reduce(self.grads[self.split:])
 
     def finish(self):
@@ -93,7 +96,7 @@ class TrainStep:
     effect as with the reference's optimizer.step() (model/main.py:127, 321-322)."""
 
     def __init__(self, model, batch, lr=1e-3, alpha=0.99, eps=1e-8, process_group=None, optimizer=None,
-                 phased=None):
+                 phased=None, force_sync=False):
         self.model = model
         self.N = batch
         self.lr, self.alpha, self.eps = lr, alpha, eps
@@ -109,17 +112,19 @@ class TrainStep:
         self.pg = process_group
         h = nat.h
         self.sync = GradSync(self.grads, lib().f3_net_grad_split(h), process_group,
-                             wait_phase1=lambda st: check(lib().f3_net_wait_phase1(h, st), "wait phase 1"))
+                             wait_phase1=lambda st: check(lib().f3_net_wait_phase1(h, st), "wait phase 1"),
+                             force=force_sync)
         self.world = self.sync.world
-        # phased=True runs the two-phase backward even on one rank (times its cost against phase 0)
-        self.phased = self.world > 1 if phased is None else bool(phased)
+        # phased=True runs the two-phase backward even on one rank (times its cost against phase 0);
+        # force_sync=True (tests) also issues the two all-reduce buckets at world 1
+        self.phased = (self.world > 1 or force_sync) if phased is None else bool(phased)
         # expose the flat gradient through the usual .grad attributes
         for (name, shape, off), p in zip(model.param_views(), model.parameters()):
             p.grad = self.grads[off:off + int(np.prod(shape))].view(shape)
         self.graph = None
         self._static = None
         # world 1: the RMSprop update per layer inside the backward (F3_FUSED_OPT=0: one launch after it)
-        self.fused_optimizer = self.world == 1 and os.environ.get("F3_FUSED_OPT", "1") != "0"
+        self.fused_optimizer = not self.sync.active and os.environ.get("F3_FUSED_OPT", "1") != "0"
 
     # -- the pieces ------------------------------------------------------------
     def prepare(self, skel, sensor, label):

@@ -131,6 +131,15 @@ int f3_net_fused_rmsprop(f3_net* net);
 /* The F3_PRECISION_* the net was created with (reads back f3_config.precision; -1 for NULL). */
 int f3_net_precision(const f3_net* net);
 
+/* Device status of the last training forward / backward (the sensor branch's cooperative CNN1D:
+ * its group barriers time out instead of hanging when the workgroups cannot all be resident; the
+ * launch then writes NaN into its outputs). Returns F3_EDEVICE if a copy of that error word flagged
+ * a timeout (wait = 1: after every enqueued copy has completed; 0: those that have). Every
+ * f3_net_forward / _backward* also returns F3_EDEVICE once when it finds a completed, flagged copy
+ * from an earlier call. No reference counterpart: the reference's nn.Conv1d cannot fail this way
+ * (GSTCAN_UR_conv.ipynb:493-514). */
+int f3_net_status(f3_net* net, int wait);
+
 /* torch.optim.RMSprop(lr, alpha, eps), no momentum / weight decay / centering, on
  * g = grad_scale * grads (1.0 = torch semantics; 1/world after a summed all-reduce):
  * sq = alpha*sq + (1-alpha)*g^2 ; p -= lr*g/(sqrt(sq)+eps). */

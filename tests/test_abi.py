@@ -92,7 +92,7 @@ def test_build_model_one_argument_call_is_bf16x3(name, monkeypatch):
     cfg.merge_from_dict({"MODEL": {"NAME": name}, "GRAPH": {"LAYOUT": "coco_mmpose", "STRATEGY": "spatial"},
                          "DATA": {"NUM_CLASSES": 11, "SENSOR_DIM": 6}})
     model = f3.build_model(cfg, device="cpu")
-    assert model.spec.precision == "bf16x3"
+    assert model.precision == "bf16x3" and model.spec.precision is None
     assert L.lib().f3_net_precision(model._native.h) == 4          # F3_PRECISION_BF16X3
     assert L.lib().f3_net_fused_rmsprop(model._native.h) == 1      # per-layer RMSprop plan holds
     monkeypatch.setenv("F3_PRECISION", "fp32")

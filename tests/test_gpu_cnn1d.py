@@ -76,3 +76,53 @@ def test_cooperative_cnn1d_is_deterministic():
     assert torch.equal(a[0], b[0])
     # the LSTM's own weight gradients use fixed-order partial rows too (f3_lstm_bwd)
     assert torch.equal(a[1], b[1]), int((a[1] != b[1]).sum())
+
+
+def test_cooperative_cnn1d_barrier_timeout_is_reported(monkeypatch):
+    """a group barrier of the cooperative CNN1D that times out writes NaN into its outputs,
+    and the host must be told, as for TARGCN's GRU barriers. F3_CNN_SKIP_ARRIVE=1 makes workgroup 0
+    skip its arrivals (every barrier of the launch then times out after 2^14 polls); the error word
+    is copied to a pinned host ring after each launch (status_ring.h) and reported once as
+    F3_EDEVICE by device_status() or the next forward / backward. A clean step before and after
+    reports OK."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import fall_multimodal_amd as f3
+    d = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = f3.CNN_BiLSTM(device=d)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(64, 30, 4, generator=g).to(d)
+    dout = torch.randn(64, model.spec.num_class, generator=g).to(d)
+    o, gr = _step(model, x, dout, True)
+    model.device_status(wait=True)
+    assert torch.isfinite(o).all() and torch.isfinite(gr).all()
+    monkeypatch.setenv("F3_CNN_SKIP_ARRIVE", "1")
+    with pytest.raises(RuntimeError, match="barrier"):
+        _step(model, x, dout, True)
+        model.device_status(wait=True)
+    monkeypatch.delenv("F3_CNN_SKIP_ARRIVE")
+    torch.cuda.synchronize()
+    model.device_status(wait=True)  # reported once, then clear
+    o, gr = _step(model, x, dout, True)
+    model.device_status(wait=True)
+    assert torch.isfinite(o).all() and torch.isfinite(gr).all()
+
+
+def test_long_sensor_clips_take_the_per_layer_launches():
+    """the cooperative form's per-clip tensors grow with the sensor frames; past its 64 KiB
+    of LDS (T = 400 at Ci = 4 here) the step must take the per-layer launches instead of failing with
+    F3_EINVAL. Checked against the per-layer form forced by F3_CNN1D_COOP=0: identical results."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import fall_multimodal_amd as f3
+    d = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = f3.CNN_BiLSTM(device=d, sensor_frames=400)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(16, 400, 4, generator=g).to(d)
+    dout = torch.randn(16, model.spec.num_class, generator=g).to(d)
+    o1, g1 = _step(model, x, dout, True)
+    o0, g0 = _step(model, x, dout, False)
+    assert torch.isfinite(o1).all() and torch.isfinite(g1).all()
+    assert torch.equal(o1, o0) and torch.equal(g1, g0)

@@ -1012,7 +1012,7 @@ def test_main_py_autograd_path_bf16x3_vs_oracle():
     if "F3_PRECISION" in os.environ:
         pytest.skip("F3_PRECISION overrides the default mode")
     model = f3.build_model(cfg, device=d)
-    assert model.spec.precision == "bf16x3"
+    assert model.precision == "bf16x3" and model.spec.precision is None
     model.load_state_dict(o["st"])
     model.train()
     opt = f3.RMSprop(model.parameters(), lr=1e-3)

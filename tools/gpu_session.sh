@@ -22,6 +22,7 @@
 #   ab          tools/ab.sh env $AB_CFGS (eager bench A/B, optional serial profiles) -> gpurun_out/ab.log
 #   bench_tg    bench.py --model targcn per TG_CFGS config                -> gpurun_out/bench_tg_*.json
 #   smoke       __graft_entry__.smoke()
+#   exit_prof   tools/exit_check.py under rocprofv3 --kernel-trace (exit status after finalisation) -> gpurun_out/exit_prof.log
 #   py:<file>   python <file> (a tool script)                           -> gpurun_out/<name>.log
 set -o pipefail
 mkdir -p gpurun_out
@@ -149,6 +150,10 @@ for step in "$@"; do
       grep -E "ms/step|==" gpurun_out/ab.log | head -40 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    exit_prof)  # tools/exit_check.py under a rocprofv3 kernel trace: the exit status after finalisation
+      run exit_prof 240 rocprofv3 --kernel-trace --stats -d gpurun_out/exitprof -o run -- \
+        python tools/exit_check.py > gpurun_out/exit_prof.log 2>&1
+      grep -E "exit_check|Abort|SIGSEGV" gpurun_out/exit_prof.log ;;
     bench_tg)  # the TARGCN (cfg 2) line alone, A/B over TG_CFGS (env assignments, "-" = defaults)
       for cfg in ${TG_CFGS:--}; do
         envs=(); [ "$cfg" != "-" ] && IFS=',' read -ra envs <<< "$cfg"
