@@ -26,6 +26,7 @@ cores on a bounded sample). The bf16 and fp32 modes' step times are reported bes
 """
 import argparse
 import json
+import math
 import subprocess
 import os
 import sys
@@ -252,14 +253,42 @@ def roofline_kernels_x3(dev, batch, V, only=None):
         out["tcn_fwd"] = {"kernel": f"igemm_big<1,2,4,144,x3n> clip window (tcn 9x1 fwd, bf16x3, C=256, T=8, N={N}, "
                                     f"V={V})", "ms": ms, "bytes": row8 + row8 + wbytes, "flop": conv_flop(N * T * V, C, C)}
     if want("dgrad_l8"):
+        # the instance the step runs (stream_backward's td): the RELUMASK epilogue reads g (fp32) and
+        # BN1's coefficients, masks dv where bn1(g) <= 0 and adds the BN1-backward sums
         dx = torch.empty(N, T, V, C, device=dev)
-        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wp), N, T, V, C, C, KT, 1, 4, st),
-                "dgrad")
-        ms = _time_launch(lambda: lib.f3_conv_backward_data_x3cat(L.ptr(dy3), None, L.ptr(dx), L.ptr(wp), N, T, V, C, C,
-                                                                  KT, 1, 4, st))
-        out["dgrad_l8"] = {"kernel": f"igemm_big<0,2,4,144,x3n> clip window (tcn 9x1 input gradient, bf16x3, C=256, "
-                                     f"T=8, N={N}, V={V})", "ms": ms, "bytes": row8 + row8 + wbytes,
+        g = torch.randn(N, T, V, C, device=dev)
+        gam, bet = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+        gd = g.reshape(-1, C).double()
+        bsum, bsq = gd.sum(0), (gd * gd).sum(0)
+        ssum, ssq = torch.zeros(C, dtype=torch.float64, device=dev), torch.zeros(C, dtype=torch.float64, device=dev)
+        args = (L.ptr(dx), None, L.ptr(g), L.ptr(gam), L.ptr(bet), L.ptr(bsum), L.ptr(bsq), float(N * T * V),
+                L.ptr(ssum), L.ptr(ssq), N, T, V, C, C, st)
+        L.check(lib.f3_conv_step_x3cat(1, L.ptr(dy3), L.ptr(w), L.ptr(wp), *args), "dgrad relumask")
+        ms = _time_launch(lambda: lib.f3_conv_step_x3cat(1, L.ptr(dy3), None, L.ptr(wp), *args))
+        out["dgrad_l8"] = {"kernel": f"igemm_big<16,2,4,144,x3n> clip window, RELUMASK epilogue (tcn 9x1 input "
+                                     f"gradient as the step runs it, bf16x3, C=256, T=8, N={N}, V={V})", "ms": ms,
+                           "bytes": row8 + row8 + wbytes + N * T * V * C * 4,  # + the mask operand g (fp32)
                            "flop": conv_flop(N * T * V, C, C)}
+    for key, Tg, Cg in (("gcn_l5", 15, 128), ("gcn_l6", 8, 256)):
+        if not want(key):
+            continue
+        # the 1x1 GCN contraction (stgcan.py:50-56) of skeleton layers 5 / 6 as the step runs it: the
+        # graph-mixed rows [Z_hi | Z_lo] of K * C_in = 3 * Cg channels -> 256, graph-mixed bias + BN1 sums
+        Kc = 3 * Cg
+        z3 = split(torch.randn(N, Tg, V, Kc, device=dev))
+        wg = torch.randn(C, Kc, device=dev) / math.sqrt(Kc)
+        wpg = torch.empty(C * Kc, device=dev)
+        og = torch.empty(N, Tg, V, C, device=dev)
+        bv = torch.randn(V, C, device=dev) * 0.1
+        ssum, ssq = torch.zeros(C, dtype=torch.float64, device=dev), torch.zeros(C, dtype=torch.float64, device=dev)
+        args = (L.ptr(og), L.ptr(bv), None, None, None, None, None, 0.0, L.ptr(ssum), L.ptr(ssq), N, Tg, V, Kc, C, st)
+        L.check(lib.f3_conv_step_x3cat(0, L.ptr(z3), L.ptr(wg), L.ptr(wpg), *args), "gcn")
+        ms = _time_launch(lambda: lib.f3_conv_step_x3cat(0, L.ptr(z3), None, L.ptr(wpg), *args))
+        M = N * Tg * V
+        nb = M * Kc * 4 + C * Kc * 4 + M * C * 4 + V * C * 4  # Z [hi | lo], W packed, g fp32, bias
+        out[key] = {"kernel": f"1x1 gcn GEMM, graph-mixed bias + BN1 sums (bf16x3, K*Cin={Kc} -> {C}, T={Tg}, "
+                              f"N={N}, V={V}; igemm_big<6,1,8,0,x3n>)",
+                    "ms": ms, "bytes": nb, "flop": 2.0 * M * C * Kc}
     dw = torch.empty(C, C, KT, device=dev)
     db = torch.empty(C, device=dev)
     if want("wgrad"):
@@ -294,6 +323,24 @@ def roofline_kernels_x3(dev, batch, V, only=None):
                                      f"C=64, T=30, N={N}, V={V})", "ms": ms,
                            "bytes": row30 + row30 + C1 * C1 * KT * 4, "flop": conv_flop(N * T1 * V, C1, C1)}
     return _roofline_records(out, None, peak, products=3)
+
+
+def _gcn_roofline(roofs):
+    """The north star's "MFMA utilisation for the graph GEMM against gfx950 peak": the 1x1 GCN contraction
+    of skeleton layers 5 and 6 (stgcan.py:50-56) as the step launches it, MFMA fractions as the other keys
+    plus its fraction of the HBM peak (the bf16x3 operand rows make it HBM-leaning: 77-128 FLOP per
+    algorithmic byte against a ridge of 312 bf16 / 104 bf16x3-product FLOP per byte)."""
+    if not roofs or "gcn_l5" not in roofs:
+        return None
+    res = {}
+    for k in ("gcn_l5", "gcn_l6"):
+        r = dict(roofs[k])
+        if r.get("algorithmic_bytes"):
+            gbs = r["algorithmic_bytes"] / (r["ms_per_launch"] * 1e-3) / 1e9
+            r["hbm_achieved_gbs"] = round(gbs, 1)
+            r["hbm_frac"] = round(gbs / PEAK_HBM_GBS, 4)
+        res[k[4:]] = r
+    return res
 
 
 def _roofline_records(out, flop, peak, products=1):
@@ -1068,6 +1115,7 @@ def main():
             "roofline_wgrad_kernel": roofs.get("wgrad_kernel"),
             "roofline_tcn_fwd": roofs["tcn_fwd"],
             "roofline_graph_mix": mix,
+            "roofline_gcn": _gcn_roofline(roofs),
             "step_mfma": {"flop_per_clip": FLOP_PER_CLIP.get((V, S)), "achieved_tflops": None if FLOP_PER_CLIP.get(
                 (V, S)) is None else round(B * FLOP_PER_CLIP[(V, S)] / (dt / a.steps) / 1e12, 2),
                 "products_per_flop": PRODUCTS[a.precision],

@@ -20,7 +20,7 @@ EXPORTS = (
     "f3_net_buffer_count", "f3_net_counter_count", "f3_net_workspace_bytes", "f3_net_forward",
     "f3_net_loss", "f3_net_backward", "f3_rmsprop_step", "f3_conv_forward", "f3_status_string",
     "f3_net_debug_tensor", "f3_conv_backward_data", "f3_conv_backward_weight", "f3_conv_wgrad_packed", "f3_split_x3cat",
-    "f3_conv_forward_x3cat", "f3_conv_backward_data_x3cat", "f3_conv_backward_weight_x3cat", "f3_graph_mix_forward",
+    "f3_conv_forward_x3cat", "f3_conv_backward_data_x3cat", "f3_conv_backward_weight_x3cat", "f3_conv_step_x3cat", "f3_graph_mix_forward",
     "f3_graph_mix_backward", "f3_graph_mix_forward_ex", "f3_graph_mix_backward_ex", "f3_net_backward_phase",
     "f3_net_grad_split", "f3_net_wait_phase1", "f3_net_backward_rmsprop", "f3_net_fused_rmsprop", "f3_net_precision", "f3_net_status",
     "f3_targcn_create", "f3_targcn_destroy", "f3_targcn_num_entries", "f3_targcn_entry", "f3_targcn_param_count",
@@ -97,6 +97,7 @@ def lib():
         "f3_conv_forward_x3cat": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
         "f3_conv_backward_data_x3cat": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
         "f3_conv_backward_weight_x3cat": (I, [P, P, P, P, I, I, I, I, I, I, I, I, P]),
+        "f3_conv_step_x3cat": (I, [I, P, P, P, P, P, P, P, P, P, P, F, P, P, I, I, I, I, I, P]),
         "f3_graph_mix_forward": (I, [P, P, P, I, I, I, I, P]),
         "f3_graph_mix_backward": (I, [P, P, P, P, P, I, I, I, I, P]),
         "f3_graph_mix_forward_ex": (I, [P, P, P, I, I, I, I, I, P]),

@@ -1756,6 +1756,46 @@ int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void
   return f3_conv_gemm(&a, 0, 0, s);
 }
 
+int f3_conv_step_x3cat(int kind, const void* in3, const float* w, void* wpack, float* out, const float* bias_v,
+                       const float* g, const float* gamma, const float* beta, const double* bn_sum,
+                       const double* bn_sq, float bn_count, double* st_sum, double* st_sq, int N, int T, int V,
+                       int Cin, int Cout, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const bool gcn = kind == F3_STEP_GCN_FWD, dgrad = kind == F3_STEP_TCN_DGRAD;
+  if ((!gcn && !dgrad) || !in3 || !wpack || !out || !st_sum || !st_sq) return F3_EINVAL;
+  if (gcn && !bias_v) return F3_EINVAL;
+  if (dgrad && (!g || !gamma || !beta || !bn_sum || !bn_sq || bn_count <= 0.f)) return F3_EINVAL;
+  const int KT = gcn ? 1 : 9, pad = gcn ? 0 : 4;
+  if (!x3cat_shape_ok(N, T, V, Cin, Cout, KT, 1, pad)) return F3_EINVAL;
+  if (w) {  // the step's packing (w == NULL: wpack already packed)
+    PrepTable t;
+    t.n = 0;
+    add_job(t, gcn ? PREP_PACK_CONV : PREP_PACK_CONV_T, Cout * KT * Cin * x3mul(x3code()), static_cast<float*>(wpack),
+            w, nullptr, nullptr, Cout, Cin, KT, x3code());
+    F3_TRY(f3_prep(t, s));
+  }
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.inb = static_cast<const unsigned short*>(in3); a.zero = test_zero_page();
+  a.wb = static_cast<const unsigned short*>(wpack); a.out = out; a.st_sum = st_sum; a.st_sq = st_sq;
+  if (gcn) {  // stream_forward_layer's gcn GEMM: [Z_hi | Z_lo] rows of K Ci channels, graph-mixed bias, BN1 sums
+    a.g = geom(N * T * V, Cout, Cin, 1, 1, 0, 0, T, T, V, Cin, Cout);
+    x3_gemm(a, Cin);
+    a.bias = bias_v;
+    if (!f3_igemm_ok(a)) return F3_EINVAL;
+    return f3_conv_gemm(&a, 0, EPI_BIASV | EPI_STATS, s);
+  }
+  // stream_backward's tcn input gradient: dh rows [hi | lo] of Cout channels (the tcn's output) into
+  // dv[M][Cin]; ReLU mask of bn1(g) and the BN1-backward sums in the epilogue (RELUMASK)
+  a.g = geom(N * T * V, Cin, Cout, KT, 1, pad, 1, T, T, V, Cout, Cin);
+  x3_gemm(a, Cout);
+  a.aux = g; a.ldaux = Cin;
+  a.epi_bn.sum = bn_sum; a.epi_bn.sumsq = bn_sq; a.epi_bn.gamma = gamma; a.epi_bn.beta = beta;
+  a.epi_bn.count = bn_count; a.epi_bn.eval = 0;
+  if (!f3_igemm_ok(a)) return F3_EINVAL;
+  return f3_conv_gemm(&a, 0, EPI_RELUMASK, s);
+}
+
 int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, float* db, int N, int T_in, int V,
                                   int Cin, int Cout, int KT, int stride, int pad, void* stream) {
   hipStream_t s = (hipStream_t)stream;

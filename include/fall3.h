@@ -170,18 +170,30 @@ int f3_conv_backward_weight(const void* dy, const void* x, float* dw, float* db,
 int f3_conv_wgrad_packed(const void* dy, const void* x, float* slab, long long slab_floats, int N, int T_in, int V,
                          int Cin, int Cout, int KT, int stride, int pad, void* stream);
 
-/* F3_PRECISION_BF16X3 as the training step runs it (K-concatenation on the bf16 LDS-DMA kernels):
- * f3_split_x3cat writes each fp32 row x[r][0..C) as the bf16 row [hi | lo] of 2C (hi = RNE bf16(x),
- * lo = RNE bf16(x - hi)); the packed weight of a tap is [W_hi | W_hi | W_lo] and the GEMM's third K
- * segment re-reads x_hi, so ONE bf16 GEMM over K = 3C computes x_hi W_hi + x_lo W_hi + x_hi W_lo (the
- * split product, ~2^-16 relative).
+/* F3_PRECISION_BF16X3 as the training step runs it (the native split form on the bf16 LDS-DMA kernels):
+ * f3_split_x3cat writes each fp32 row x[r][0..C) as the bf16 row of 2C made of 32-channel blocks
+ * [x_hi 32 | x_lo 32] (hi = RNE bf16(x), lo = RNE bf16(x - hi)); the packed weight holds, per tap, the
+ * blocks [W_hi 32 | W_lo 32] (prep code 4), and a k step issues x_hi W_hi + x_lo W_hi + x_hi W_lo (the
+ * split product, ~2^-16 relative) from one staged row piece.
  * f3_conv_forward_x3cat / f3_conv_backward_data_x3cat: x3 / dy3 are such rows ([N,T,V,2Cin] /
- * [N,T_out,V,2Cout]); wpack is scratch of 1.5 * Cout*KT*Cin floats (w == NULL reuses it); out / dx
+ * [N,T_out,V,2Cout]); wpack is scratch of 2 * Cout*KT*Cin bf16 (w == NULL reuses it); out / dx
  * fp32 as f3_conv_forward / f3_conv_backward_data (bias required, epilogue + bias).
- * f3_conv_backward_weight_x3cat: the bf16 weight-gradient GEMM over three row segments of the rows,
- * dy_hi x_hi + dy_lo x_hi + dy_hi x_lo (split-K partials summed into dw [Cout][Cin][KT]; db from
- * dy_hi + dy_lo; both overwritten, db may be NULL). dw == NULL: the GEMM alone at the step's split
- * count, partials left in an internal slab (timing). Requires Cin, Cout multiples of 64. */
+ * f3_conv_backward_weight_x3cat: the bf16 weight-gradient GEMM on the same rows, dy_hi x_hi + dy_lo
+ * x_hi + dy_hi x_lo (split-K partials summed into dw [Cout][Cin][KT]; db from dy_hi + dy_lo; both
+ * overwritten, db may be NULL). dw == NULL: the GEMM alone at the step's split count, partials left in
+ * an internal slab (timing). Requires Cin, Cout multiples of 64.
+ * f3_conv_step_x3cat: two GEMMs with the epilogues the step gives them, launched alone (measurement,
+ * SURVEY §8d; bench.py roofline keys), through the step's own dispatch:
+ *   kind F3_STEP_GCN_FWD (stgcan.py:50-56): the gcn 1x1 conv over the graph-mixed rows in3 = [Z_hi | Z_lo]
+ *     of Cin = K*C_in channels, out = conv + bias_v[(row % V)][Cout] (the graph-mixed bias), the BN1
+ *     batch sums of out added into st_sum / st_sq (fp64); w [Cout][Cin] (T = the frames);
+ *   kind F3_STEP_TCN_DGRAD (stgcan.py:112-121, backward): the (9,1) tcn input gradient, stride 1, from
+ *     in3 = dh rows of Cout channels into out = dv [N,T,V,Cin], masked where bn1(g) <= 0 (g fp32
+ *     [N,T,V,Cin]; BN from gamma / beta and the batch sums bn_sum / bn_sq over bn_count values) with
+ *     the BN1-backward sums sum(dv), sum(dv * g_hat) added into st_sum / st_sq; w [Cout][Cin][9].
+ *   gcn-only / dgrad-only pointers may be NULL for the other kind. */
+#define F3_STEP_GCN_FWD 0
+#define F3_STEP_TCN_DGRAD 1
 int f3_split_x3cat(const float* x, void* out, int64_t rows, int C, void* stream);
 int f3_conv_forward_x3cat(const void* x3, const float* w, const float* bias, float* out, void* wpack, int N, int T_in,
                           int V, int Cin, int Cout, int KT, int stride, int pad, void* stream);
@@ -189,6 +201,10 @@ int f3_conv_backward_data_x3cat(const void* dy3, const float* w, float* dx, void
                                 int Cin, int Cout, int KT, int stride, int pad, void* stream);
 int f3_conv_backward_weight_x3cat(const void* dy3, const void* x3, float* dw, float* db, int N, int T_in, int V,
                                   int Cin, int Cout, int KT, int stride, int pad, void* stream);
+int f3_conv_step_x3cat(int kind, const void* in3, const float* w, void* wpack, float* out, const float* bias_v,
+                       const float* g, const float* gamma, const float* beta, const double* bn_sum,
+                       const double* bn_sq, float bn_count, double* st_sum, double* st_sq, int N, int T, int V,
+                       int Cin, int Cout, void* stream);
 
 /* The 1x1 conv GEMM of the bf16 step with the step's epilogues (stgcan.py:50-56 gcn conv, its
  * input gradient; stgcan.py:123-144 stride-2 residual conv and its input gradient), through the

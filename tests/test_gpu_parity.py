@@ -216,6 +216,77 @@ def test_conv_x3cat_kernels_match_torch(shape):
     assert max(errs.values()) <= X3_TOL, errs
 
 
+@pytest.mark.parametrize("kind,T,Cin,Cout", [(0, 15, 384, 256), (0, 8, 768, 256), (1, 8, 256, 256)])
+def test_conv_step_x3cat_epilogues_match_torch(kind, T, Cin, Cout):
+    """f3_conv_step_x3cat, the entry bench.py's roofline_gcn / roofline (dgrad_l8) keys time: the step's
+    gcn 1x1 GEMM with the graph-mixed bias and BN1 sums (kind 0, skeleton layers 5 / 6 shapes), and the
+    T=8 tcn input gradient with the RELUMASK epilogue (kind 1: dv masked where bn1(g) <= 0, the
+    BN1-backward sums sum(dv), sum(dv g_hat)). Against fp64 on the fp32 operands within X3_TOL of the
+    max; the sums within 1e-4 of their max."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    lib, st = L.lib(), L.stream_handle()
+    N, V = 3, 18
+    torch.manual_seed(11 + kind)
+    M = N * T * V
+    ind = Cin if kind == 0 else Cout  # channels of the GEMM's input rows
+
+    def split(t):
+        t = t.float().contiguous().to(d)
+        out = torch.empty(t.numel() // t.shape[-1], 2 * t.shape[-1], device=d, dtype=torch.bfloat16)
+        L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), t.numel() // t.shape[-1], t.shape[-1], st), "split")
+        return out
+
+    xin = torch.randn(N, T, V, ind, dtype=torch.float64)
+    in3 = split(xin)
+    ssum = torch.zeros(Cout if kind == 0 else Cin, dtype=torch.float64, device=d)
+    ssq = torch.zeros_like(ssum)
+    if kind == 0:
+        w = torch.randn(Cout, Cin, dtype=torch.float64) / np.sqrt(Cin)
+        bv = torch.randn(V, Cout, dtype=torch.float64) * 0.1
+        out = torch.empty(N, T, V, Cout, device=d)
+        wp = torch.empty(Cout * Cin + 64, device=d)
+        L.check(lib.f3_conv_step_x3cat(0, L.ptr(in3), L.ptr(w.float().to(d)), L.ptr(wp), L.ptr(out),
+                                       L.ptr(bv.float().to(d)), None, None, None, None, None, 0.0, L.ptr(ssum), L.ptr(ssq),
+                                       N, T, V, Cin, Cout, st), "gcn step")
+        ref = xin @ w.T + bv.view(1, 1, V, Cout)
+        rs, rq = ref.reshape(-1, Cout).sum(0), (ref.reshape(-1, Cout) ** 2).sum(0)
+    else:
+        w = torch.randn(Cout, Cin, 9, 1, dtype=torch.float64) / np.sqrt(9 * Cin)
+        g = torch.randn(N, T, V, Cin, dtype=torch.float64)
+        gam, bet = torch.rand(Cin, dtype=torch.float64) + 0.5, torch.randn(Cin, dtype=torch.float64) * 0.3
+        for _ in range(8):  # no element within 1e-3 of the ReLU kink (fp32 vs fp64 would flip its mask)
+            gs = g.reshape(-1, Cin)
+            bsum, bsq = gs.sum(0), (gs * gs).sum(0)
+            mean = bsum / M
+            rstd = 1.0 / torch.sqrt(bsq / M - mean * mean + 1e-5)
+            z = (g - mean) * rstd * gam + bet
+            near = z.abs() < 1e-3
+            if not bool(near.any()):
+                break
+            g = torch.where(near, g + 0.01, g)
+        out = torch.empty(N, T, V, Cin, device=d)
+        wp = torch.empty(Cout * Cin * 9 + 64, device=d)
+        L.check(lib.f3_conv_step_x3cat(1, L.ptr(in3), L.ptr(w.float().reshape(Cout, Cin, 9).contiguous().to(d)),
+                                       L.ptr(wp), L.ptr(out), None, L.ptr(g.float().to(d)), L.ptr(gam.float().to(d)),
+                                       L.ptr(bet.float().to(d)), L.ptr(bsum.to(d)), L.ptr(bsq.to(d)), float(M),
+                                       L.ptr(ssum), L.ptr(ssq), N, T, V, Cin, Cout, st), "dgrad step")
+        # dv = relu'(bn1(g)) * conv_T(dh): the input gradient of conv2d(x, w, padding (4, 0))
+        xx = torch.zeros(N, Cin, T, V, dtype=torch.float64, requires_grad=True)
+        y = torch.nn.functional.conv2d(xx, w, padding=(4, 0))
+        y.backward(xin.permute(0, 3, 1, 2))
+        dv = xx.grad.permute(0, 2, 3, 1)
+        ghat = (g - mean) * rstd
+        ref = torch.where(ghat * gam + bet > 0, dv, torch.zeros_like(dv))
+        rs, rq = ref.reshape(-1, Cin).sum(0), (ref * ghat).reshape(-1, Cin).sum(0)
+    torch.cuda.synchronize()
+    e = float((out.cpu().double() - ref).abs().max() / ref.abs().max())
+    es = float((ssum.cpu() - rs).abs().max() / rs.abs().max())
+    eq = float((ssq.cpu() - rq).abs().max() / rq.abs().max())
+    print(f"step kind {kind} T={T} {Cin}->{Cout}: out {e:.2e}, sums {es:.2e} / {eq:.2e}")
+    assert e <= X3_TOL and es <= 1e-4 and eq <= 1e-4, (e, es, eq)
+
+
 @pytest.mark.parametrize("V,K,Cin,F", [(14, 3, 64, 40), (18, 3, 64, 37), (18, 3, 256, 20), (14, 3, 3, 30),
                                         (18, 3, 2, 29), (18, 1, 128, 9), (14, 2, 128, 11)])
 def test_graph_mix_kernels_match_torch(V, K, Cin, F):

@@ -14,7 +14,7 @@
 #   kpmc        SQ / LDS / MFMA counter passes of the same               -> gpurun_out/kpmc.txt
 #   step_pmc    FETCH_SIZE / WRITE_SIZE passes of the step alone        -> gpurun_out/step_hbm_traffic.txt
 #   roof_prof   rocprofv3 kernel trace of bench.py's roofline launches, one process per key in
-#               ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd}          -> gpurun_out/roof_kernels_KEY.txt
+#               ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd gcn_l5 gcn_l6}          -> gpurun_out/roof_kernels_KEY.txt
 #   roof_pmc    FETCH_SIZE / WRITE_SIZE passes of the same, per key     -> gpurun_out/roofline_pmc.json
 #   rgb_pmc     FETCH_SIZE / WRITE_SIZE passes of the RGB branch kernels -> gpurun_out/rgb_pmc.json
 #   bench       bench.py (default run, 20 steps)                        -> gpurun_out/bench.json
@@ -110,14 +110,14 @@ for step in "$@"; do
       python tools/pmc_summary.py gpurun_out --top 60 > gpurun_out/step_hbm_traffic.txt 2>&1
       head -30 gpurun_out/step_hbm_traffic.txt ;;
     roof_prof)
-      for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd}; do
+      for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd gcn_l5 gcn_l6}; do
         run roof_prof_$K 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof_$K -o run -- \
           python tools/roofline_pmc.py run $K > gpurun_out/roof_prof_$K.log 2>&1
         python tools/prof_summary.py gpurun_out/roof_$K/run_results.db --top 30 > gpurun_out/roof_kernels_$K.txt 2>&1
         head -8 gpurun_out/roof_kernels_$K.txt
       done ;;
     roof_pmc)
-      for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd}; do
+      for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd gcn_l5 gcn_l6}; do
         for C in FETCH_SIZE WRITE_SIZE; do
           rm -rf gpurun_out/rpmc_${K}_$C
           run rpmc_${K}_$C 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/rpmc_${K}_$C -o run -- \
