@@ -20,6 +20,8 @@
 // Row maps, the stride-2 parity split and the epilogues are those of igemm_bf16.
 #include "igemm.h"
 
+#include <type_traits>
+
 // F3_PROBE (tools/probe_build.sh only; 0 in the library): bit 1 drops the window loop's MFMAs, bit 2
 // its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone. (A static
 // issue priority for waves 4-7, MI355X_MICROARCH.md "two waves per SIMD" item 4, measured within
@@ -80,6 +82,176 @@ struct BigCfg {
   static constexpr int DOFF = ZOFF + 128;            // WIN: 1-KiB sink of the idle DMA slots
   static constexpr int SMEM = WIN ? DOFF + 1024 : ZOFF;
 };
+
+// The epilogue of igemm_big and igemm_win1 (as igemm_bf16): bias / graph-mixed bias, BN statistics,
+// channel-attention GAP, ReLU mask + BN-backward sums, accumulate; bf16 outputs through an LDS image.
+// WIN: rows are clip-window rows (clip0, wmode / wpar as the kernels'); else phys(m0 + tile row).
+template <int EPI, int WM, int WN, int WIN, class Phys>
+F3_DEV __attribute__((always_inline)) void big_epilogue(const ConvGemmArgs& a, f32x4 (&acc)[BG_MT][BG_NT], char* smem,
+                                                        int n0, int clip0, int nclip, int wmode, int wpar, int m0,
+                                                        Phys phys) {
+  using Cfg = BigCfg<WM, WN, WIN>;
+  constexpr int NT = 64 * WM * WN, BM = Cfg::BM, BN = Cfg::BN, CPW = Cfg::CPW;
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fg = lane >> 4;
+  float* epi_sc = reinterpret_cast<float*>(smem + Cfg::EPI_OFF);
+  float* epi_sh = epi_sc + BN;
+  float* epi_mu = epi_sh + BN;
+  float* epi_rs = epi_mu + BN;
+  // ---------------- epilogue (as igemm_bf16) ----------------
+  float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]  (stage 0 is free now)
+  float* gred = red + 2 * WM * BN;               // [WM][2][BN]
+  float ssum[BG_NT], ssq[BG_NT], gap0[BG_NT], gap1[BG_NT];
+#pragma unroll
+  for (int y = 0; y < BG_NT; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
+  // bf16 outputs leave through an LDS image of the tile: the MFMA C layout gives a lane 4 rows of
+  // ONE column (2-B scattered stores); the image is copied out as 16-B row chunks instead
+  constexpr int OTS = BN + 8, OT_OFF = 16 * 1024;  // row stride (elements), byte offset past red/gred
+  static_assert(OT_OFF + BM * OTS * 2 <= Cfg::SMEM, "output staging tile");
+  const bool stage_out = !(EPI & EPI_ADD) && a.outb && g.ldo % 8 == 0 && g.Nc % 8 == 0;
+  __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
+  const int TV = g.T_out * g.V;
+  const int nlo = WIN ? clip0 : m0 / TV;  // first clip (GAP is forward-only: no parity split)
+  // output row of tile row rl (-1: none)
+  auto orow = [&](int rl) -> int {
+    if constexpr (WIN != 0) {
+      const int k = (CPW == 2 && rl >= WIN) ? 1 : 0, lo = rl - k * WIN, clip = clip0 + k;
+      const int f = lo / g.V, v = lo - f * g.V, t = wmode == 1 ? 2 * f + wpar : f;
+      if (lo >= WIN || t >= g.T_out || clip >= nclip) return -1;
+      return (clip * g.T_out + t) * g.V + v;
+    } else {
+      return phys(m0 + rl);
+    }
+  };
+  // Per 16-row group x: the group's 4 output rows are resolved and every operand the epilogue
+  // reads (RELUMASK source g, graph-mixed bias) is loaded for all 4 rows x BG_NT columns before
+  // any use, from clamped in-bounds addresses. A per-element conditional load (row outside the
+  // parity class, column past Nc, or the fp32/bf16 select) made hipcc wait vmcnt(0) on every
+  // element: 72 dependent round trips per lane in the RELUMASK epilogue.
+  const bool aux16 = a.auxb != nullptr;
+  float biasj[BG_NT];  // EPI_BIAS: one value per column, loaded once
+#pragma unroll
+  for (int y = 0; y < BG_NT; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1)] : 0.f;
+  // all groups' operands first: a load issued after the group's stores would make its first
+  // use wait (vmcnt counts stores too) for every store before it
+  float pre[BG_MT][4][BG_NT];
+  auto preload = [&](auto load) {
+#pragma unroll
+    for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mc = max(orow(wm * 144 + x * 16 + fg * 4 + r), 0);
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1));
+      }
+  };
+  if (EPI & EPI_RELUMASK) {
+    if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
+    else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
+  } else if (EPI & EPI_BIASV) {
+    preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
+  } else if (EPI & EPI_ADD) {
+    preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
+  }
+#pragma unroll
+  for (int x = 0; x < BG_MT; ++x) {
+    int mrow[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mrow[r] = orow(wm * 144 + x * 16 + fg * 4 + r);
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) {
+      const int jl = wn * 32 + y * 16 + fr, j = n0 + jl;  // tile-local / global column
+      const bool jok = j < g.Nc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mrow[r];
+        if (!jok || m < 0) continue;
+        float v = acc[x][y][r];
+        if (EPI & EPI_BIAS) v += biasj[y];
+        if (EPI & EPI_BIASV) v += pre[x][r][y];
+        if (EPI & EPI_RELUMASK) {
+          const float gv = pre[x][r][y];
+          if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
+          const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
+          ssum[y] += v;
+          ssq[y] += v * xh;
+        } else if (EPI & EPI_STATS) {
+          ssum[y] += v;
+          ssq[y] += v * v;
+        }
+        if (EPI & EPI_GAP) {
+          const int n = m / TV;
+          if (n == nlo) gap0[y] += v;
+          else if (n == nlo + 1) gap1[y] += v;
+          else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
+        }
+        if (!(EPI & EPI_ADD) && a.outb) {
+          if (stage_out) ot[(wm * 144 + x * 16 + fg * 4 + r) * OTS + jl] = (__bf16)v;
+          else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
+        } else {
+          float* o = a.out + (size_t)m * g.ldo + j;
+          if (EPI & EPI_ADD) *o = pre[x][r][y] + v;
+          else *o = v;
+        }
+      }
+    }
+  }
+  if (EPI & (EPI_STATS | EPI_RELUMASK | EPI_GAP)) {
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) {
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        ssum[y] += __shfl_xor(ssum[y], o, 64);
+        ssq[y] += __shfl_xor(ssq[y], o, 64);
+        gap0[y] += __shfl_xor(gap0[y], o, 64);
+        gap1[y] += __shfl_xor(gap1[y], o, 64);
+      }
+    }
+    if (fg == 0) {
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        const int jl = wn * 32 + y * 16 + fr;
+        red[(wm * 2 + 0) * BN + jl] = ssum[y];
+        red[(wm * 2 + 1) * BN + jl] = ssq[y];
+        gred[(wm * 2 + 0) * BN + jl] = gap0[y];
+        gred[(wm * 2 + 1) * BN + jl] = gap1[y];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < BN; t += NT) {
+      if (n0 + t >= g.Nc) continue;
+      float s0 = 0.f, s1 = 0.f, g0 = 0.f, g1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s0 += red[(w * 2 + 0) * BN + t];
+        s1 += red[(w * 2 + 1) * BN + t];
+        g0 += gred[(w * 2 + 0) * BN + t];
+        g1 += gred[(w * 2 + 1) * BN + t];
+      }
+      if (EPI & (EPI_STATS | EPI_RELUMASK)) {
+        atomic_add_d(a.st_sum + n0 + t, (double)s0);
+        atomic_add_d(a.st_sq + n0 + t, (double)s1);
+      }
+      if (EPI & EPI_GAP) {
+        atomic_add_f(a.gap + (size_t)nlo * g.Nc + n0 + t, g0);
+        if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + n0 + t, g1);
+      }
+    }
+  }
+  if (stage_out) {
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+    for (int q = tid; q < BM * CPR; q += blockDim.x) {
+      const int rl = q / CPR, c = q - rl * CPR;
+      const int m = orow(rl), j = n0 + c * 8;
+      if (m < 0 || j >= g.Nc) continue;
+      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
+          *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
+    }
+  }
+}
 
 // X3N: the bf16x3 native form (ConvGemmArgs::x3n): a k step is one 32-channel block, its staged row
 // piece [x_hi 32 | x_lo 32] / [W_hi 32 | W_lo 32], and the wave issues x_hi W_hi + x_lo W_hi + x_hi W_lo
@@ -514,157 +686,201 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
   }
   __syncthreads();
 
-  // ---------------- epilogue (as igemm_bf16) ----------------
-  float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]  (stage 0 is free now)
-  float* gred = red + 2 * WM * BN;               // [WM][2][BN]
-  float ssum[BG_NT], ssq[BG_NT], gap0[BG_NT], gap1[BG_NT];
-#pragma unroll
-  for (int y = 0; y < BG_NT; ++y) ssum[y] = ssq[y] = gap0[y] = gap1[y] = 0.f;
-  // bf16 outputs leave through an LDS image of the tile: the MFMA C layout gives a lane 4 rows of
-  // ONE column (2-B scattered stores); the image is copied out as 16-B row chunks instead
-  constexpr int OTS = BN + 8, OT_OFF = 16 * 1024;  // row stride (elements), byte offset past red/gred
-  static_assert(OT_OFF + BM * OTS * 2 <= (int)sizeof(smem), "output staging tile");
-  const bool stage_out = !(EPI & EPI_ADD) && a.outb && g.ldo % 8 == 0 && g.Nc % 8 == 0;
-  __bf16* ot = reinterpret_cast<__bf16*>(smem + OT_OFF);
-  const int TV = g.T_out * g.V;
-  const int nlo = WIN ? clip0 : m0 / TV;  // first clip (GAP is forward-only: no parity split)
-  // output row of tile row rl (-1: none)
-  auto orow = [&](int rl) -> int {
-    if constexpr (WIN != 0) {
-      const int k = (CPW == 2 && rl >= WIN) ? 1 : 0, lo = rl - k * WIN, clip = clip0 + k;
-      const int f = lo / g.V, v = lo - f * g.V, t = wmode == 1 ? 2 * f + wpar : f;
-      if (lo >= WIN || t >= g.T_out || clip >= nclip) return -1;
-      return (clip * g.T_out + t) * g.V + v;
-    } else {
-      return phys(m0 + rl);
-    }
-  };
-  // Per 16-row group x: the group's 4 output rows are resolved and every operand the epilogue
-  // reads (RELUMASK source g, graph-mixed bias) is loaded for all 4 rows x BG_NT columns before
-  // any use, from clamped in-bounds addresses. A per-element conditional load (row outside the
-  // parity class, column past Nc, or the fp32/bf16 select) made hipcc wait vmcnt(0) on every
-  // element: 72 dependent round trips per lane in the RELUMASK epilogue.
-  const bool aux16 = a.auxb != nullptr;
-  float biasj[BG_NT];  // EPI_BIAS: one value per column, loaded once
-#pragma unroll
-  for (int y = 0; y < BG_NT; ++y) biasj[y] = (EPI & EPI_BIAS) ? a.bias[min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1)] : 0.f;
-  // all groups' operands first: a load issued after the group's stores would make its first
-  // use wait (vmcnt counts stores too) for every store before it
-  float pre[BG_MT][4][BG_NT];
-  auto preload = [&](auto load) {
-#pragma unroll
-    for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mc = max(orow(wm * 144 + x * 16 + fg * 4 + r), 0);
-#pragma unroll
-        for (int y = 0; y < BG_NT; ++y) pre[x][r][y] = load(mc, min(n0 + wn * 32 + y * 16 + fr, g.Nc - 1));
-      }
-  };
+  big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, wmode, wpar, m0, phys);
+}
+
+template <int I, int N, class F>
+F3_DEV __attribute__((always_inline)) void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// igemm_win1: the stride-1 clip-window GEMM (9 taps, pad 4; forward or input gradient) in the bf16x3
+// native form with the tap schedule unrolled at compile time. igemm_big's window loop derives each
+// step's (chunk, tap), its weight offset and the A-carry piece of the next window at run time (the
+// carry decision alone is ~60 SALU / VALU instructions with exec-masked branches per step, ~300
+// non-MFMA instructions per 54 MFMAs in all: the load leg the probe builds found issue-bound,
+// DESIGN.md §4.12). Here a chunk's 9 steps are straight-line code: the tap, the LDS stage, which
+// steps carry and which piece a wave carries are constants; a wave issues its weight pieces plus ONE
+// A-carry piece per step (a wave with nothing to carry sinks the zero row, so the vmcnt count stays
+// one constant). LDS layout, fragment reads, MFMA order and the epilogue are igemm_big's, so the two
+// forms give bit-identical results.
+template <int EPI, int WM, int WN, int WIN>
+__global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
+  using Cfg = BigCfg<WM, WN, WIN>;
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int KT = 9, P = 4, CL = WIN;
+  constexpr int BN = Cfg::BN, STAGE = Cfg::STAGE, NST = Cfg::NST, LA = Cfg::LA, CPW = Cfg::CPW, NPA = Cfg::NPA;
+  constexpr int NCAR = KT - LA + 1;             // carrying steps per window
+  constexpr int APS = (NPA + NCAR - 1) / NCAR;  // A pieces per carrying step: one per wave < APS
+  constexpr int BSL = Cfg::BP / NW;             // weight pieces per wave and step
+  constexpr int DPS = BSL + 1;                  // DMAs per wave and step
+  constexpr int A0W = (NPA + NW - 1) / NW;      // window 0's pieces per wave
+  static_assert(APS <= NW && Cfg::BP % NW == 0 && (LA == 1 || LA == 2), "one carry piece per wave");
+  static_assert(NCAR * APS >= NPA, "carry groups cover the window");
+  static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int ncol = g.Nc / BN;
+  const int n0 = (tile % ncol) * BN, clip0 = (tile / ncol) * CPW;
+  const int nclip = g.M / (g.T_out * g.V);
+  const int V = g.V, TVin = g.T_in * V, kpt = g.Kc / 32, nstep = KT * kpt;
+  const int ss = g.transposed ? -1 : 1;  // tap dt reads frame t + ss (dt - P)
   if (EPI & EPI_RELUMASK) {
-    if (aux16) preload([&](int mc, int jc) { return bf2f(a.auxb[(size_t)mc * a.ldaux + jc]); });
-    else preload([&](int mc, int jc) { return a.aux[(size_t)mc * a.ldaux + jc]; });
-  } else if (EPI & EPI_BIASV) {
-    preload([&](int mc, int jc) { return a.bias[(mc % g.V) * g.Nc + jc]; });
-  } else if (EPI & EPI_ADD) {
-    preload([&](int mc, int jc) { return a.out[(size_t)mc * g.ldo + jc]; });
-  }
-#pragma unroll
-  for (int x = 0; x < BG_MT; ++x) {
-    int mrow[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) mrow[r] = orow(wm * 144 + x * 16 + fg * 4 + r);
-#pragma unroll
-    for (int y = 0; y < BG_NT; ++y) {
-      const int jl = wn * 32 + y * 16 + fr, j = n0 + jl;  // tile-local / global column
-      const bool jok = j < g.Nc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mrow[r];
-        if (!jok || m < 0) continue;
-        float v = acc[x][y][r];
-        if (EPI & EPI_BIAS) v += biasj[y];
-        if (EPI & EPI_BIASV) v += pre[x][r][y];
-        if (EPI & EPI_RELUMASK) {
-          const float gv = pre[x][r][y];
-          if (gv * epi_sc[jl] + epi_sh[jl] <= 0.f) v = 0.f;
-          const float xh = (gv - epi_mu[jl]) * epi_rs[jl];
-          ssum[y] += v;
-          ssq[y] += v * xh;
-        } else if (EPI & EPI_STATS) {
-          ssum[y] += v;
-          ssq[y] += v * v;
-        }
-        if (EPI & EPI_GAP) {
-          const int n = m / TV;
-          if (n == nlo) gap0[y] += v;
-          else if (n == nlo + 1) gap1[y] += v;
-          else atomic_add_f(a.gap + (size_t)n * g.Nc + j, v);
-        }
-        if (!(EPI & EPI_ADD) && a.outb) {
-          if (stage_out) ot[(wm * 144 + x * 16 + fg * 4 + r) * OTS + jl] = (__bf16)v;
-          else reinterpret_cast<__bf16*>(a.outb)[(size_t)m * g.ldo + j] = (__bf16)v;
-        } else {
-          float* o = a.out + (size_t)m * g.ldo + j;
-          if (EPI & EPI_ADD) *o = pre[x][r][y] + v;
-          else *o = v;
-        }
-      }
-    }
-  }
-  if (EPI & (EPI_STATS | EPI_RELUMASK | EPI_GAP)) {
-#pragma unroll
-    for (int y = 0; y < BG_NT; ++y) {
-#pragma unroll
-      for (int o = 16; o < 64; o <<= 1) {
-        ssum[y] += __shfl_xor(ssum[y], o, 64);
-        ssq[y] += __shfl_xor(ssq[y], o, 64);
-        gap0[y] += __shfl_xor(gap0[y], o, 64);
-        gap1[y] += __shfl_xor(gap1[y], o, 64);
-      }
-    }
-    if (fg == 0) {
-#pragma unroll
-      for (int y = 0; y < BG_NT; ++y) {
-        const int jl = wn * 32 + y * 16 + fr;
-        red[(wm * 2 + 0) * BN + jl] = ssum[y];
-        red[(wm * 2 + 1) * BN + jl] = ssq[y];
-        gred[(wm * 2 + 0) * BN + jl] = gap0[y];
-        gred[(wm * 2 + 1) * BN + jl] = gap1[y];
-      }
-    }
-    __syncthreads();
+    float* epi_sc = reinterpret_cast<float*>(smem + Cfg::EPI_OFF);
     for (int t = tid; t < BN; t += NT) {
-      if (n0 + t >= g.Nc) continue;
-      float s0 = 0.f, s1 = 0.f, g0 = 0.f, g1 = 0.f;
+      float sc, sh, mu, rs;
+      bn_coeff(a.epi_bn, n0 + t, sc, sh, mu, rs);
+      epi_sc[t] = sc; epi_sc[BN + t] = sh; epi_sc[2 * BN + t] = mu; epi_sc[3 * BN + t] = rs;
+    }
+  }
+  const unsigned short* in = a.inb;
+  const unsigned short* wb = a.wb;
+  const int sub = lane >> 3, pch = lane & 7;
+  // the lane's 16-B chunk of a staged A row piece: swz(R, pch) with R & 7 == sub, in the x3n row
+  const int sA = pch ^ sub, colA = 8 * sA + (sA >= 4 ? g.Kc - 32 : 0);
+  const int Ktot = KT * g.Kc * 2;
+  const unsigned short* bsrc[BSL];
 #pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s0 += red[(w * 2 + 0) * BN + t];
-        s1 += red[(w * 2 + 1) * BN + t];
-        g0 += gred[(w * 2 + 0) * BN + t];
-        g1 += gred[(w * 2 + 1) * BN + t];
+  for (int i = 0; i < BSL; ++i) {
+    const int r = (wave + NW * i) * 8 + sub;
+    bsrc[i] = wb + (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
+  }
+  // A piece pa (8 window rows) of chunk c's window: clip row l of clip clip0 + k
+  // (the empty asm keeps the per-step values in the step: hoisted out of the chunk loop for all 9
+  // unrolled taps they spill)
+  auto asrc = [&](int c, int pa) -> const void* {
+    int R = pa * 8 + sub;
+    asm volatile("" : "+v"(R));
+    const int k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL, clip = clip0 + k;
+    if (l >= TVin || clip >= nclip) return a.zero;
+    return in + (size_t)(clip * TVin + l) * g.lda + c * 32 + colA;
+  };
+  // stage of step (c, J): the weight pieces of tap J, chunk c, and the A carry: steps J >= LA carry
+  // group J - LA of window c + 1, step 0 the last group (KT - LA) of its own window
+  auto stage = [&](auto JC, int c) {
+    constexpr int J = decltype(JC)::value;
+    char* sbase = smem + Cfg::SOFF + ((c * (KT % NST) + J) % NST) * STAGE;
+    const int k0 = J * 2 * g.Kc + 64 * c;
+#pragma unroll
+    for (int i = 0; i < BSL; ++i)
+      __builtin_amdgcn_global_load_lds(bsrc[i] + k0, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
+    const void* src = a.zero;
+    char* dst = smem + Cfg::DOFF;
+    if constexpr (J >= LA) {
+      const int pa = (J - LA) * APS + wave;
+      if (wave < APS && pa < NPA && c + 1 < kpt) {
+        src = asrc(c + 1, pa);
+        dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
       }
-      if (EPI & (EPI_STATS | EPI_RELUMASK)) {
-        atomic_add_d(a.st_sum + n0 + t, (double)s0);
-        atomic_add_d(a.st_sq + n0 + t, (double)s1);
-      }
-      if (EPI & EPI_GAP) {
-        atomic_add_f(a.gap + (size_t)nlo * g.Nc + n0 + t, g0);
-        if ((nlo + 1) * TV < g.M && g1 != 0.f) atomic_add_f(a.gap + (size_t)(nlo + 1) * g.Nc + n0 + t, g1);
+    } else if constexpr (J == 0) {
+      const int pa = (KT - LA) * APS + wave;
+      if (c > 0 && wave < APS && pa < NPA) {
+        src = asrc(c, pa);
+        dst = smem + (c & 1) * Cfg::AWIN + pa * 1024;
       }
     }
+    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
+  };
+  // window 0's rows, then the stages of steps 0 .. LA - 1 (they carry nothing: sink DMAs)
+#pragma unroll
+  for (int i = 0; i < A0W; ++i) {
+    const int pa = (wave + NW * i) % NPA;
+    __builtin_amdgcn_global_load_lds(asrc(0, pa), (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
   }
-  if (stage_out) {
-    __syncthreads();
-    constexpr int CPR = BN / 8;  // 16-B chunks per tile row
-    for (int q = tid; q < BM * CPR; q += blockDim.x) {
-      const int rl = q / CPR, c = q - rl * CPR;
-      const int m = orow(rl), j = n0 + c * 8;
-      if (m < 0 || j >= g.Nc) continue;
-      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.outb) + (size_t)m * g.ldo + j) =
-          *reinterpret_cast<const uint4*>(ot + rl * OTS + c * 8);
+  stage(std::integral_constant<int, 0>{}, 0);
+  if constexpr (LA == 2) stage(std::integral_constant<int, 1>{}, 0);
+  if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (LA == 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(DPS) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 acc[BG_MT][BG_NT];
+#pragma unroll
+  for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+  const unsigned zrow = lds0 + Cfg::ZOFF;
+  unsigned boffr[2][BG_NT];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int y = 0; y < BG_NT; ++y) {
+      const int r = wn * 32 + y * 16 + fr;
+      boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
     }
+  // the wave's rows: clip base row in the window and first output row of the clip
+  const int cbase = CPW == 2 ? wm * 144 : 0, lo0 = CPW == 2 ? 0 : wm * 144;
+  for (int c = 0; c < kpt; ++c) {
+    const unsigned wrow = lds0 + (c & 1) * Cfg::AWIN + (unsigned)cbase * 128;
+    const bool more = c + 1 < kpt;
+    static_for<0, KT>([&](auto JC) {
+      constexpr int J = decltype(JC)::value;
+      constexpr int JS = (J + LA) % KT, CS = (J + LA) / KT;  // the step staged now: (c + CS, JS)
+      const bool issue = CS == 0 || more;
+      if (issue) stage(std::integral_constant<int, JS>{}, c + CS);
+      int t = lo0 + fr + ss * (J - P) * V;  // lane's tile-0 row in the clip, tap-shifted
+      asm volatile("" : "+v"(t));
+      const unsigned rb = wrow + (unsigned)t * 128;
+      const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
+      const unsigned soff = ((c * (KT % NST) + J) % NST) * STAGE;
+      u32x4_t f[2][BG_NT + BG_MT];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int y = 0; y < BG_NT; ++y) asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(boffr[ks][y] + soff));
+#define F3_AREAD1(X)                                                                                      \
+  {                                                                                                       \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X);  \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ad), "n"(2048 * (X))); \
   }
+        F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6) F3_AREAD1(7)
+        F3_AREAD1(8)
+#undef F3_AREAD1
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
+#pragma unroll
+        for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) {
+            // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order)
+            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
+                                   acc[x][y]);
+            if (ks == 1)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
+                                     acc[x][y]);
+          }
+        if (ks == 0) {
+#pragma unroll
+          for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+            for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+        }
+      }
+      // the step staged LA ahead must land before its compute: with LA = 2 this step's own DMAs
+      // (the step after next) stay in flight
+      if (LA == 2 && issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    });
+  }
+  (void)nstep;
+  __syncthreads();
+  auto none = [](int) { return -1; };
+  big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, 0, 0, 0, none);
 }
 
 }  // namespace f3
@@ -734,14 +950,24 @@ bool f3_igemm_big_win_ok(const ConvGemmArgs& a) { return f3_igemm_big_ok(a) && b
 // W4 (WIN = 144 only): a 4-wave form, one clip x 128 channels per workgroup, meant to run two
 // independent workgroups per CU. Measured 1.5-1.75x SLOWER alone (l8d 134 -> 235 us) and the step
 // 8.73 -> 9.36 ms (profiles/r05_win4_ab.txt); not dispatched, kept as the template's 4-wave case.
+// F3_WIN1=0 (A/B only): the stride-1 window GEMMs on igemm_big's run-time tap schedule instead of
+// igemm_win1 (read per call: tests compare the two forms)
+static bool win1_enabled() {
+  const char* e = getenv("F3_WIN1");
+  return !e || atoi(e) != 0;
+}
+
 template <int CL, bool W4 = false>
 static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int WM = CL == 540 ? 4 : W4 ? 1 : 2, WN = CL == 540 ? 2 : 4, CPW = BigCfg<WM, WN, CL>::CPW;
   const int nclip = a.g.M / (a.g.T_out * a.g.V);
   const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / (32 * WN));
+  // stride 1, 9 taps, pad 4, native split form: the compile-time tap schedule (igemm_win1)
+  const bool w1 = !W4 && a.x3n && a.g.S == 1 && a.g.KT == 9 && a.g.P == 4 && win1_enabled();
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
-    if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
+    if (w1) hipLaunchKernelGGL((igemm_win1<(E), WM, WN, CL>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
+    else if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
     else hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, false>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);     \
     F3_LAUNCH_CHECK();                                                                                \
     return F3_OK;                                                                                     \

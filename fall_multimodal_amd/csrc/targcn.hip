@@ -2839,9 +2839,27 @@ static int gru_bwd_launch(const GruBwdArgs& a, hipStream_t s) {
   return F3_OK;
 }
 
-// node-partitioned forward (see gru_fwd_node_kernel): bf16 mode, exchange buffers present, a
-// cooperative launch of V x ceil(B / GN_BT) workgroups. Returns false (caller falls back to the
-// clip-tile kernel) when the cooperative launch is refused.
+// Workgroups of a node-partitioned kernel that are resident together: the occupancy query's answer
+// per CU, capped at 6 (MI355X_MICROARCH.md "Residency and cooperative launch": the hardware admits
+// floor(800 / (ceil(sgpr / 16) * 16 + 16)) 256-thread blocks per CU, 6 at these kernels' 94-106 SGPRs),
+// times the CUs.
+static int gn_resident(const void* kernel) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, GN_THREADS, 0) != hipSuccess || per_cu < 1 ||
+      hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return std::min(per_cu, 6) * cus;
+}
+
+// node-partitioned forward (see gru_fwd_node_kernel): bf16 mode, exchange buffers present, a launch
+// of V x ceil(B / GN_BT) workgroups when they are all resident together (the group barriers need it);
+// else false and the caller runs the clip-tile kernel. A plain launch, not hipLaunchCooperativeKernel:
+// residency is the same (the occupancy check above is what the cooperative launch adds), the
+// cooperative launch costs 15-20 us of queue latency per call, and a process that used it died with
+// SIGSEGV in rocprofiler-sdk's exit handlers under rocprofv3.
 static bool gru_fwd_node(const GruFwdArgs& a, hipStream_t s) {
   const int NG = (a.B + GN_BT - 1) / GN_BT;
   if (!a.hx || !a.rhx || !a.gsync || NG > GN_MAXG || a.V > VMAX || a.prof) return false;
@@ -2851,14 +2869,10 @@ static bool gru_fwd_node(const GruFwdArgs& a, hipStream_t s) {
     return false;
   }
   if (hipMemsetAsync(a.gsync, 0, sizeof(int) * NG, s) != hipSuccess) return false;
-  GruFwdArgs arg = a;
-  void* params[] = {&arg};
-  const hipError_t e = hipLaunchCooperativeKernel((const void*)gru_fwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS),
-                                                  params, 0, s);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
+  static const int resident = gn_resident((const void*)gru_fwd_node_kernel);
+  if (NG * a.V > resident) return false;
+  hipLaunchKernelGGL(gru_fwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS), 0, s, a);
+  if (hipGetLastError() != hipSuccess) return false;
   return true;
 }
 
@@ -2877,14 +2891,10 @@ static bool gru_bwd_node(const GruBwdArgs& a, hipStream_t s) {
     return false;
   }
   if (hipMemsetAsync(a.gsync, 0, sizeof(int) * NG, s) != hipSuccess) return false;
-  GruBwdArgs arg = a;
-  void* params[] = {&arg};
-  const hipError_t e = hipLaunchCooperativeKernel((const void*)gru_bwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS),
-                                                  params, 0, s);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
+  static const int resident = gn_resident((const void*)gru_bwd_node_kernel);
+  if (NG * a.V > resident) return false;
+  hipLaunchKernelGGL(gru_bwd_node_kernel, dim3(NG * a.V), dim3(GN_THREADS), 0, s, a);
+  if (hipGetLastError() != hipSuccess) return false;
   return true;
 }
 

@@ -112,7 +112,8 @@ def test_cooperative_cnn1d_barrier_timeout_is_reported(monkeypatch):
 def test_long_sensor_clips_take_the_per_layer_launches():
     """the cooperative form's per-clip tensors grow with the sensor frames; past its 64 KiB
     of LDS (T = 400 at Ci = 4 here) the step must take the per-layer launches instead of failing with
-    F3_EINVAL. Checked against the per-layer form forced by F3_CNN1D_COOP=0: identical results."""
+    F3_EINVAL. Checked against the per-layer form forced by F3_CNN1D_COOP=0: the same forward bit for bit,
+    gradients within 1e-5 of their max (the per-layer backward's weight gradients use float atomics)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import fall_multimodal_amd as f3
@@ -125,4 +126,5 @@ def test_long_sensor_clips_take_the_per_layer_launches():
     o1, g1 = _step(model, x, dout, True)
     o0, g0 = _step(model, x, dout, False)
     assert torch.isfinite(o1).all() and torch.isfinite(g1).all()
-    assert torch.equal(o1, o0) and torch.equal(g1, g0)
+    assert torch.equal(o1, o0)
+    assert float((g1 - g0).abs().max()) <= 1e-5 * float(g0.abs().max())

@@ -216,6 +216,60 @@ def test_conv_x3cat_kernels_match_torch(shape):
     assert max(errs.values()) <= X3_TOL, errs
 
 
+@pytest.mark.parametrize("shape", [(4, 8, 18, 256, 256), (3, 15, 18, 128, 128), (3, 30, 18, 64, 64),
+                                   (2, 29, 18, 64, 64), (3, 8, 18, 256, 256)])
+def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
+    """igemm_win1 (the stride-1 clip-window GEMM with its tap schedule unrolled at compile time) against
+    igemm_big's run-time schedule (F3_WIN1=0): the same staged bytes, fragment reads and MFMA order, so
+    forward (bias epilogue), input gradient and the step's RELUMASK input gradient (with its BN1-backward
+    sums) must agree bit for bit, on ragged clip counts (odd N at two clips per workgroup) and T = 29."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    lib, st = L.lib(), L.stream_handle()
+    N, T, V, Ci, Co = shape
+    torch.manual_seed(21)
+
+    def split(t):
+        t = t.float().contiguous().to(d)
+        out = torch.empty(t.numel() // t.shape[-1], 2 * t.shape[-1], device=d, dtype=torch.bfloat16)
+        L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), t.numel() // t.shape[-1], t.shape[-1], st), "split")
+        return out
+
+    x3 = split(torch.randn(N, T, V, Ci))
+    dy3 = split(torch.randn(N, T, V, Co))
+    w = (torch.randn(Co, Ci, 9) / np.sqrt(9 * Ci)).to(d)
+    b = torch.randn(Co).to(d)
+    g = torch.randn(N, T, V, Ci, device=d)
+    gam, bet = torch.rand(Ci, device=d) + 0.5, torch.randn(Ci, device=d) * 0.3
+    gd = g.reshape(-1, Ci).double()
+    bsum, bsq = gd.sum(0), (gd * gd).sum(0)
+
+    def run():
+        y = torch.empty(N, T, V, Co, device=d)
+        wp = torch.empty(Co * Ci * 9 + 64, device=d)
+        L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, Ci, Co, 9, 1, 4,
+                                          st), "fwd")
+        dx = torch.empty(N, T, V, Ci, device=d)
+        wpt = torch.empty(Co * Ci * 9 + 64, device=d)
+        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wpt), N, T, V, Ci, Co, 9, 1, 4,
+                                                st), "dgrad")
+        dv = torch.empty(N, T, V, Ci, device=d)
+        s1 = torch.zeros(Ci, dtype=torch.float64, device=d)
+        s2 = torch.zeros_like(s1)
+        L.check(lib.f3_conv_step_x3cat(1, L.ptr(dy3), L.ptr(w), L.ptr(wpt), L.ptr(dv), None, L.ptr(g), L.ptr(gam),
+                                       L.ptr(bet), L.ptr(bsum), L.ptr(bsq), float(N * T * V), L.ptr(s1), L.ptr(s2), N, T,
+                                       V, Ci, Co, st), "dgrad relumask")
+        torch.cuda.synchronize()
+        return y, dx, dv
+
+    new = run()
+    monkeypatch.setenv("F3_WIN1", "0")
+    old = run()
+    for name, p, q in zip(("y", "dx", "dv"), new, old):
+        assert torch.isfinite(p).all(), name
+        assert torch.equal(p, q), (name, float((p - q).abs().max()))
+
+
 @pytest.mark.parametrize("kind,T,Cin,Cout", [(0, 15, 384, 256), (0, 8, 768, 256), (1, 8, 256, 256)])
 def test_conv_step_x3cat_epilogues_match_torch(kind, T, Cin, Cout):
     """f3_conv_step_x3cat, the entry bench.py's roofline_gcn / roofline (dgrad_l8) keys time: the step's
