@@ -689,12 +689,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
   big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, wmode, wpar, m0, phys);
 }
 
-template <int I, int N, class F>
-F3_DEV __attribute__((always_inline)) void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
+// x through an empty asm: the compiler cannot move work that depends on it out of the step
+F3_DEV int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
 }
 
 // igemm_win1: the stride-1 clip-window GEMM (9 taps, pad 4; forward or input gradient) in the bf16x3
@@ -753,34 +751,33 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
   // A piece pa (8 window rows) of chunk c's window: clip row l of clip clip0 + k
   // (the empty asm keeps the per-step values in the step: hoisted out of the chunk loop for all 9
   // unrolled taps they spill)
-  auto asrc = [&](int c, int pa) -> const void* {
-    int R = pa * 8 + sub;
-    asm volatile("" : "+v"(R));
+  auto asrc = [&](int c, int R) -> const void* {  // R = pa * 8 + sub
     const int k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL, clip = clip0 + k;
     if (l >= TVin || clip >= nclip) return a.zero;
     return in + (size_t)(clip * TVin + l) * g.lda + c * 32 + colA;
   };
   // stage of step (c, J): the weight pieces of tap J, chunk c, and the A carry: steps J >= LA carry
   // group J - LA of window c + 1, step 0 the last group (KT - LA) of its own window
-  auto stage = [&](auto JC, int c) {
-    constexpr int J = decltype(JC)::value;
+  auto stage = [&](const int J, int c) {
     char* sbase = smem + Cfg::SOFF + ((c * (KT % NST) + J) % NST) * STAGE;
     const int k0 = J * 2 * g.Kc + 64 * c;
 #pragma unroll
-    for (int i = 0; i < BSL; ++i)
-      __builtin_amdgcn_global_load_lds(bsrc[i] + k0, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
+    for (int i = 0; i < BSL; ++i) {
+      const void* wsrc = bsrc[i] + k0;
+      __builtin_amdgcn_global_load_lds(wsrc, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
+    }
     const void* src = a.zero;
     char* dst = smem + Cfg::DOFF;
-    if constexpr (J >= LA) {
+    if (J >= LA) {
       const int pa = (J - LA) * APS + wave;
       if (wave < APS && pa < NPA && c + 1 < kpt) {
-        src = asrc(c + 1, pa);
+        src = asrc(c + 1, opaque_v(wave * 8 + sub) + (J - LA) * APS * 8);
         dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
       }
-    } else if constexpr (J == 0) {
+    } else if (J == 0) {
       const int pa = (KT - LA) * APS + wave;
       if (c > 0 && wave < APS && pa < NPA) {
-        src = asrc(c, pa);
+        src = asrc(c, opaque_v(wave * 8 + sub) + (KT - LA) * APS * 8);
         dst = smem + (c & 1) * Cfg::AWIN + pa * 1024;
       }
     }
@@ -790,10 +787,11 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
 #pragma unroll
   for (int i = 0; i < A0W; ++i) {
     const int pa = (wave + NW * i) % NPA;
-    __builtin_amdgcn_global_load_lds(asrc(0, pa), (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
+    const void* src = asrc(0, pa * 8 + sub);
+    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
   }
-  stage(std::integral_constant<int, 0>{}, 0);
-  if constexpr (LA == 2) stage(std::integral_constant<int, 1>{}, 0);
+  stage(0, 0);
+  if (LA == 2) stage(1, 0);
   if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (LA == 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(DPS) : "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -822,13 +820,12 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
   for (int c = 0; c < kpt; ++c) {
     const unsigned wrow = lds0 + (c & 1) * Cfg::AWIN + (unsigned)cbase * 128;
     const bool more = c + 1 < kpt;
-    static_for<0, KT>([&](auto JC) {
-      constexpr int J = decltype(JC)::value;
-      constexpr int JS = (J + LA) % KT, CS = (J + LA) / KT;  // the step staged now: (c + CS, JS)
+#pragma unroll
+    for (int J = 0; J < KT; ++J) {  // unrolled: J, JS, CS are constants in every copy
+      const int JS = (J + LA) % KT, CS = (J + LA) / KT;  // the step staged now: (c + CS, JS)
       const bool issue = CS == 0 || more;
-      if (issue) stage(std::integral_constant<int, JS>{}, c + CS);
-      int t = lo0 + fr + ss * (J - P) * V;  // lane's tile-0 row in the clip, tap-shifted
-      asm volatile("" : "+v"(t));
+      if (issue) stage(JS, c + CS);
+      const int t = opaque_v(lo0 + fr) + ss * (J - P) * V;  // lane's tile-0 row in the clip, tap-shifted
       const unsigned rb = wrow + (unsigned)t * 128;
       const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
       const unsigned soff = ((c * (KT % NST) + J) % NST) * STAGE;
@@ -875,7 +872,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
       if (LA == 2 && issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-    });
+    }
   }
   (void)nstep;
   __syncthreads();
