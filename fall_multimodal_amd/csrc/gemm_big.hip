@@ -959,8 +959,11 @@ static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int WM = CL == 540 ? 4 : W4 ? 1 : 2, WN = CL == 540 ? 2 : 4, CPW = BigCfg<WM, WN, CL>::CPW;
   const int nclip = a.g.M / (a.g.T_out * a.g.V);
   const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / (32 * WN));
-  // stride 1, 9 taps, pad 4, native split form: the compile-time tap schedule (igemm_win1)
-  const bool w1 = !W4 && a.x3n && a.g.S == 1 && a.g.KT == 9 && a.g.P == 4 && win1_enabled();
+  // stride 1, 9 taps, pad 4, native split form: the compile-time tap schedule (igemm_win1). Alone
+  // (tools/kbench.py, profiles/r06_win1_kbench.txt): T=8 fwd / dgrad 138 / 132 -> 114 / 110 us, T=15 75 /
+  // 77 -> 67 / 66, T=30 dgrad 46 -> 43; the T=30 forward measured 43.6 -> 45.2 and stays on igemm_big
+  const bool w1 = !W4 && a.x3n && a.g.S == 1 && a.g.KT == 9 && a.g.P == 4 && (CL != 540 || a.g.transposed) &&
+                  win1_enabled();
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
     if (w1) hipLaunchKernelGGL((igemm_win1<(E), WM, WN, CL>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \

@@ -300,9 +300,10 @@ def test_conv_step_x3cat_epilogues_match_torch(kind, T, Cin, Cout):
         bv = torch.randn(V, Cout, dtype=torch.float64) * 0.1
         out = torch.empty(N, T, V, Cout, device=d)
         wp = torch.empty(Cout * Cin + 64, device=d)
-        L.check(lib.f3_conv_step_x3cat(0, L.ptr(in3), L.ptr(w.float().to(d)), L.ptr(wp), L.ptr(out),
-                                       L.ptr(bv.float().to(d)), None, None, None, None, None, 0.0, L.ptr(ssum), L.ptr(ssq),
-                                       N, T, V, Cin, Cout, st), "gcn step")
+        # (device copies held in names: a temporary freed after ptr() would be reused by the next one)
+        wd, bvd = w.float().to(d), bv.float().to(d)
+        L.check(lib.f3_conv_step_x3cat(0, L.ptr(in3), L.ptr(wd), L.ptr(wp), L.ptr(out), L.ptr(bvd), None, None, None,
+                                       None, None, 0.0, L.ptr(ssum), L.ptr(ssq), N, T, V, Cin, Cout, st), "gcn step")
         ref = xin @ w.T + bv.view(1, 1, V, Cout)
         rs, rq = ref.reshape(-1, Cout).sum(0), (ref.reshape(-1, Cout) ** 2).sum(0)
     else:
@@ -321,10 +322,11 @@ def test_conv_step_x3cat_epilogues_match_torch(kind, T, Cin, Cout):
             g = torch.where(near, g + 0.01, g)
         out = torch.empty(N, T, V, Cin, device=d)
         wp = torch.empty(Cout * Cin * 9 + 64, device=d)
-        L.check(lib.f3_conv_step_x3cat(1, L.ptr(in3), L.ptr(w.float().reshape(Cout, Cin, 9).contiguous().to(d)),
-                                       L.ptr(wp), L.ptr(out), None, L.ptr(g.float().to(d)), L.ptr(gam.float().to(d)),
-                                       L.ptr(bet.float().to(d)), L.ptr(bsum.to(d)), L.ptr(bsq.to(d)), float(M),
-                                       L.ptr(ssum), L.ptr(ssq), N, T, V, Cin, Cout, st), "dgrad step")
+        wd = w.float().reshape(Cout, Cin, 9).contiguous().to(d)
+        gd, gamd, betd, bsd, bqd = g.float().to(d), gam.float().to(d), bet.float().to(d), bsum.to(d), bsq.to(d)
+        L.check(lib.f3_conv_step_x3cat(1, L.ptr(in3), L.ptr(wd), L.ptr(wp), L.ptr(out), None, L.ptr(gd), L.ptr(gamd),
+                                       L.ptr(betd), L.ptr(bsd), L.ptr(bqd), float(M), L.ptr(ssum), L.ptr(ssq), N, T, V,
+                                       Cin, Cout, st), "dgrad step")
         # dv = relu'(bn1(g)) * conv_T(dh): the input gradient of conv2d(x, w, padding (4, 0))
         xx = torch.zeros(N, Cin, T, V, dtype=torch.float64, requires_grad=True)
         y = torch.nn.functional.conv2d(xx, w, padding=(4, 0))
