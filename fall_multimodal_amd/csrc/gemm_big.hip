@@ -255,7 +255,11 @@ F3_DEV __attribute__((always_inline)) void big_epilogue(const ConvGemmArgs& a, f
 
 // X3N: the bf16x3 native form (ConvGemmArgs::x3n): a k step is one 32-channel block, its staged row
 // piece [x_hi 32 | x_lo 32] / [W_hi 32 | W_lo 32], and the wave issues x_hi W_hi + x_lo W_hi + x_hi W_lo
-template <int EPI, int WM, int WN, int WIN = 0, bool X3N = false>
+// K1 (tiled form, 1x1 convolutions: the gcn / residual GEMMs): every staging slot's source row is fixed
+// for the launch and its column advances by one channel block per k step, so the slots' source pointers
+// are computed once and a step adds a constant (the generic staging re-derives the tap, the row map and
+// the column per slot and step: ~470 non-MFMA instructions per 54 MFMAs)
+template <int EPI, int WM, int WN, int WIN = 0, bool X3N = false, bool K1 = false>
 __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
   constexpr int NW = WM * WN, NT = 64 * NW;  // waves, threads
@@ -352,7 +356,34 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_big(ConvGemmArgs a) {
       boff[i] = j * Ktot + swz(j, pch) * 8;
     }
   }
+  // K1: per slot the source of k step 0 and the element step per k step (0 for a zero row)
+  const unsigned short* k1src[K1 ? PPW : 1];
+  int k1step[K1 ? PPW : 1];
+  if constexpr (K1) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = (wave + BG_WAVES * i) % NP;
+      if (q < AP) {
+        const int r = rowmap_src(amap[i], dt0, g);
+        k1src[i] = r >= 0 ? in + (size_t)r * g.lda + acolx(0, swz(q * 8 + sub, pch)) : a.zero;
+        k1step[i] = r >= 0 ? CB : 0;
+      } else {
+        k1src[i] = wb + boff[i] + wcol(dt0, 0);
+        k1step[i] = X3N ? 2 * CB : CB;
+      }
+    }
+  }
   auto stage = [&](int t, int buf) {
+    if constexpr (K1) {
+      char* sb = smem + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int q = (wave + BG_WAVES * i) % NP;
+        const void* src = k1src[i] + t * k1step[i];
+        __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(sb + q * 1024), 16, 0, 0);
+      }
+      return;
+    }
     int tap, i0;
     tapchunk(t, tap, i0);
     const int dt = par ? dt0 + 2 * tap : tap;
@@ -915,6 +946,12 @@ bool f3_igemm_big_ok(const ConvGemmArgs& a) {
   return a.g.KT * a.g.Kc / (a.x3n ? 32 : G_BK) >= 6;
 }
 
+// F3_K1=0 (A/B only): the 1x1 tiled GEMMs on the generic per-step staging (read per call)
+static bool k1_enabled() {
+  const char* e = getenv("F3_K1");
+  return !e || atoi(e) != 0;
+}
+
 template <int WM, int WN, bool X3N>
 static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int BM = BigCfg<WM, WN>::BM;
@@ -925,9 +962,11 @@ static int launch_big(const ConvGemmArgs& a, int epi, hipStream_t s) {
     const int M0 = nclip * ((a.g.T_out + 1) >> 1) * a.g.V, M1 = nclip * (a.g.T_out >> 1) * a.g.V;
     tiles = (M0 + BM - 1) / BM + (M1 + BM - 1) / BM;
   }
+  const bool k1 = a.g.KT == 1 && k1_enabled();
 #define F3_BCASE(E)                                                                              \
   if (epi == (E)) {                                                                             \
-    hipLaunchKernelGGL((igemm_big<(E), WM, WN, 0, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    if (k1) hipLaunchKernelGGL((igemm_big<(E), WM, WN, 0, X3N, true>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_big<(E), WM, WN, 0, X3N>), dim3(tiles), dim3(BG_THREADS), 0, s, a); \
     F3_LAUNCH_CHECK();                                                                           \
     return F3_OK;                                                                                \
   }

@@ -270,6 +270,60 @@ def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
         assert torch.equal(p, q), (name, float((p - q).abs().max()))
 
 
+@pytest.mark.parametrize("shape", [(3, 15, 18, 384, 256, 1), (3, 8, 18, 768, 256, 1), (2, 15, 14, 128, 256, 2),
+                                   (3, 30, 18, 128, 128, 1), (3, 29, 18, 128, 256, 2)])
+def test_k1_staging_matches_generic_staging_bitwise(shape, monkeypatch):
+    """igemm_big's 1x1 (K1) staging, fixed source pointers advanced per k step, against the generic
+    per-step staging (F3_K1=0): the same bytes staged, so forward (bias), input gradient (stride-2: the
+    parity tiles) and the step's gcn epilogue (graph-mixed bias + BN1 sums, f3_conv_step_x3cat kind 0)
+    agree bit for bit. Shapes: the layer-5 / 6 gcn GEMMs, the stride-2 residual convs, a ragged T = 29."""
+    d = dev()
+    import fall_multimodal_amd._lib as L
+    lib, st = L.lib(), L.stream_handle()
+    N, T, V, Ci, Co, S = shape
+    To = (T - 1) // S + 1
+    torch.manual_seed(23)
+
+    def split(t):
+        t = t.float().contiguous().to(d)
+        out = torch.empty(t.numel() // t.shape[-1], 2 * t.shape[-1], device=d, dtype=torch.bfloat16)
+        L.check(lib.f3_split_x3cat(L.ptr(t), L.ptr(out), t.numel() // t.shape[-1], t.shape[-1], st), "split")
+        return out
+
+    x3 = split(torch.randn(N, T, V, Ci))
+    dy3 = split(torch.randn(N, To, V, Co))
+    w = (torch.randn(Co, Ci, 1) / np.sqrt(Ci)).to(d)
+    b = torch.randn(Co).to(d)
+    bv = (torch.randn(V, Co) * 0.1).to(d)
+
+    def run():
+        y = torch.empty(N, To, V, Co, device=d)
+        wp = torch.empty(Co * Ci + 64, device=d)
+        L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, Ci, Co, 1, S, 0,
+                                          st), "fwd")
+        dx = torch.empty(N, T, V, Ci, device=d)
+        wpt = torch.empty(Co * Ci + 64, device=d)
+        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wpt), N, T, V, Ci, Co, 1, S, 0,
+                                                st), "dgrad")
+        outs = [y, dx]
+        if S == 1:
+            gq = torch.empty(N, T, V, Co, device=d)
+            s1 = torch.zeros(Co, dtype=torch.float64, device=d)
+            s2 = torch.zeros_like(s1)
+            L.check(lib.f3_conv_step_x3cat(0, L.ptr(x3), None, L.ptr(wp), L.ptr(gq), L.ptr(bv), None, None, None, None,
+                                           None, 0.0, L.ptr(s1), L.ptr(s2), N, T, V, Ci, Co, st), "gcn step")
+            outs.append(gq)
+        torch.cuda.synchronize()
+        return outs
+
+    new = run()
+    monkeypatch.setenv("F3_K1", "0")
+    old = run()
+    for name, p, q in zip(("y", "dx", "gcn"), new, old):
+        assert torch.isfinite(p).all(), name
+        assert torch.equal(p, q), (name, float((p - q).abs().max()))
+
+
 @pytest.mark.parametrize("kind,T,Cin,Cout", [(0, 15, 384, 256), (0, 8, 768, 256), (1, 8, 256, 256)])
 def test_conv_step_x3cat_epilogues_match_torch(kind, T, Cin, Cout):
     """f3_conv_step_x3cat, the entry bench.py's roofline_gcn / roofline (dgrad_l8) keys time: the step's
