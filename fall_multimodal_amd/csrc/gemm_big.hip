@@ -725,40 +725,96 @@ F3_DEV int opaque_v(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// The window kernel's inline asm lives in these helpers: hipcc's host pass silently drops a kernel's
+// launch stub when a lambda inside it holds a VGPR-constrained asm statement (found bisecting the
+// undefined __device_stub__ symbols of the first igemm_win1 build).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+F3_DEV u32x4_t lds_rd128(unsigned addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+template <int OFF>
+F3_DEV u32x4_t lds_rd128o(unsigned addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+template <int N>
+F3_DEV void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
+template <int N>
+F3_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+F3_DEV void pin_v(u32x4_t& v) { asm volatile("" : "+v"(v)); }
+F3_DEV void pin_v(f32x4& v) { asm volatile("" : "+v"(v)); }
 
-// igemm_win1: the stride-1 clip-window GEMM (9 taps, pad 4; forward or input gradient) in the bf16x3
-// native form with the tap schedule unrolled at compile time. igemm_big's window loop derives each
-// step's (chunk, tap), its weight offset and the A-carry piece of the next window at run time (the
-// carry decision alone is ~60 SALU / VALU instructions with exec-masked branches per step, ~300
-// non-MFMA instructions per 54 MFMAs in all: the load leg the probe builds found issue-bound,
-// DESIGN.md §4.12). Here a chunk's 9 steps are straight-line code: the tap, the LDS stage, which
-// steps carry and which piece a wave carries are constants; a wave issues its weight pieces plus ONE
-// A-carry piece per step (a wave with nothing to carry sinks the zero row, so the vmcnt count stays
-// one constant). LDS layout, fragment reads, MFMA order and the epilogue are igemm_big's, so the two
-// forms give bit-identical results.
-template <int EPI, int WM, int WN, int WIN>
+template <int I, int N, class F>
+F3_DEV __attribute__((always_inline)) void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// The compile-time step schedule of one channel chunk of the clip-window GEMM (9 taps, pad 4):
+//   MODE 0, stride 1 (forward or input gradient): one window, steps j = tap dt = j, frame shift
+//     ss (j - 4) (ss = -1 for the input gradient, at run time);
+//   MODE 1, stride-2 input gradient: the window is the clips' dY frames; a tile is one output-frame
+//     parity p (NT = 5 - p steps): tap dt = p + 2 j, shift 2 - j;
+//   MODE 2, stride-2 forward: two windows per chunk (q = 0 the even input frames, q = 1 the odd ones);
+//     steps 0-4 window 0 with taps 0, 2, .. 8 (shift j - 2), steps 5-8 window 1 with taps 1, 3, 5, 7
+//     (shift j - 7).
+template <int MODE, int NT>
+struct WinSched {
+  static constexpr int NS = MODE == 1 ? NT : 9;                         // steps per chunk
+  static constexpr int q(int j) { return MODE == 2 && j >= 5 ? 1 : 0; }
+  static constexpr int jj(int j) { return MODE == 2 && j >= 5 ? j - 5 : j; }  // step within its window
+  static constexpr int ntq(int qq) { return MODE == 2 ? (qq ? 4 : 5) : NS; }  // steps of window qq
+  static constexpr int dt(int j) {
+    return MODE == 0 ? j : MODE == 1 ? (5 - NT) + 2 * j : (q(j) ? 1 + 2 * jj(j) : 2 * jj(j));
+  }
+  static constexpr int shift(int j) { return MODE == 1 ? 2 - j : MODE == 2 ? jj(j) - 2 : j - 4; }  // x ss (MODE 0)
+};
+
+// igemm_win1: the clip-window GEMM in the bf16x3 native form with the tap schedule unrolled at compile
+// time. igemm_big's window loop derives each step's (chunk, window, tap), its weight offset and the
+// A-carry piece of the next window at run time (the carry decision alone is ~60 SALU / VALU
+// instructions with exec-masked branches per step, ~300 non-MFMA instructions per 54 MFMAs in all:
+// the load leg the probe builds found issue-bound). Here a chunk's steps are
+// straight-line code: the tap, the LDS stage, which steps carry and which pieces a wave carries are
+// constants; a wave issues its weight pieces plus ASL A-carry pieces per step (a slot with nothing to
+// carry sinks the zero row, so the vmcnt count stays one constant). LDS layout, fragment reads, MFMA
+// order and the epilogue are igemm_big's, so the two forms give bit-identical results.
+template <int EPI, int WM, int WN, int WIN, int MODE, int NTP = 5>
 __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
   constexpr int NW = WM * WN, NT = 64 * NW;
-  constexpr int KT = 9, P = 4, CL = WIN;
+  constexpr int KT = 9, CL = WIN;
   constexpr int BN = Cfg::BN, STAGE = Cfg::STAGE, NST = Cfg::NST, LA = Cfg::LA, CPW = Cfg::CPW, NPA = Cfg::NPA;
-  constexpr int NCAR = KT - LA + 1;             // carrying steps per window
-  constexpr int APS = (NPA + NCAR - 1) / NCAR;  // A pieces per carrying step: one per wave < APS
-  constexpr int BSL = Cfg::BP / NW;             // weight pieces per wave and step
-  constexpr int DPS = BSL + 1;                  // DMAs per wave and step
-  constexpr int A0W = (NPA + NW - 1) / NW;      // window 0's pieces per wave
-  static_assert(APS <= NW && Cfg::BP % NW == 0 && (LA == 1 || LA == 2), "one carry piece per wave");
-  static_assert(NCAR * APS >= NPA, "carry groups cover the window");
-  static_assert(Cfg::SMEM <= 160 * 1024, "LDS");
+  constexpr int BSL = Cfg::BP / NW;                               // weight pieces per wave and step
+  constexpr int NQ = MODE == 2 ? 2 : 1;                           // windows per chunk
+  // carry pieces per step: a window is carried by the LA.. steps of the window before it and that
+  // window's step 0 (the last group): ntq - LA + 1 groups of aps pieces
+  constexpr int APS_MAX = MODE == 0 ? (NPA + (KT - LA)) / (KT - LA + 1) : (NPA + (4 - LA)) / (4 - LA + 1);
+  constexpr int ASL = (APS_MAX + NW - 1) / NW;                    // A slots per wave and step
+  constexpr int DPS = BSL + ASL;                                  // DMAs per wave and step
+  constexpr int A0W = (NPA + NW - 1) / NW;                        // window 0's pieces per wave
+  static_assert(Cfg::BP % NW == 0 && (LA == 1 || LA == 2) && (MODE == 0 || LA == 2), "win1 staging");
+  static_assert(Cfg::SMEM <= 160 * 1024 && (NST - 1) * DPS < 64, "LDS / vmcnt");
   __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int ncol = g.Nc / BN;
-  const int n0 = (tile % ncol) * BN, clip0 = (tile / ncol) * CPW;
+  const int n0 = (tile % ncol) * BN;
+  tile /= ncol;
+  const int wpar = MODE == 1 ? 5 - NTP : 0;  // MODE 1: this launch's output-frame parity (NTP taps)
+  const int clip0 = tile * CPW;
   const int nclip = g.M / (g.T_out * g.V);
-  const int V = g.V, TVin = g.T_in * V, kpt = g.Kc / 32, nstep = KT * kpt;
-  const int ss = g.transposed ? -1 : 1;  // tap dt reads frame t + ss (dt - P)
+  const int V = g.V, TVin = g.T_in * V, kpt = g.Kc / 32;
+  const int ss = MODE == 0 ? (g.transposed ? -1 : 1) : 1;  // MODE 0: tap dt reads frame t + ss (dt - 4)
+  // valid rows of window q (MODE 2: the even / odd input frames)
+  const int wlim0 = (MODE == 2 ? (g.T_in + 1) >> 1 : g.T_in) * V, wlim1 = (g.T_in >> 1) * V;
+  const unsigned minv = (65536u + V - 1) / V;  // l / V as (l * minv) >> 16 (l < 2^9, V < 2^7)
   if (EPI & EPI_RELUMASK) {
     float* epi_sc = reinterpret_cast<float*>(smem + Cfg::EPI_OFF);
     for (int t = tid; t < BN; t += NT) {
@@ -779,136 +835,143 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
     const int r = (wave + NW * i) * 8 + sub;
     bsrc[i] = wb + (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
   }
-  // A piece pa (8 window rows) of chunk c's window: clip row l of clip clip0 + k
-  // (the empty asm keeps the per-step values in the step: hoisted out of the chunk loop for all 9
-  // unrolled taps they spill)
-  auto asrc = [&](int c, int R) -> const void* {  // R = pa * 8 + sub
+  // window row R (= piece * 8 + sub) of chunk c, window q: clip row l of clip clip0 + k
+  auto asrc = [&](int c, int qq, int R) -> const void* {
     const int k = (CPW == 2 && R >= CL) ? 1 : 0, l = R - k * CL, clip = clip0 + k;
-    if (l >= TVin || clip >= nclip) return a.zero;
-    return in + (size_t)(clip * TVin + l) * g.lda + c * 32 + colA;
+    if (l >= (qq ? wlim1 : wlim0) || clip >= nclip) return a.zero;
+    int row = clip * TVin + l;
+    if (MODE == 2) row += (int)(((unsigned)l * minv) >> 16) * V + qq * V;  // input frame 2 f + q
+    return in + (size_t)row * g.lda + c * 32 + colA;
   };
-  // stage of step (c, J): the weight pieces of tap J, chunk c, and the A carry: steps J >= LA carry
-  // group J - LA of window c + 1, step 0 the last group (KT - LA) of its own window
-  auto stage = [&](const int J, int c) {
-    char* sbase = smem + Cfg::SOFF + ((c * (KT % NST) + J) % NST) * STAGE;
-    const int k0 = J * 2 * g.Kc + 64 * c;
-#pragma unroll
-    for (int i = 0; i < BSL; ++i) {
-      const void* wsrc = bsrc[i] + k0;
-      __builtin_amdgcn_global_load_lds(wsrc, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
-    }
-    const void* src = a.zero;
-    char* dst = smem + Cfg::DOFF;
-    if (J >= LA) {
-      const int pa = (J - LA) * APS + wave;
-      if (wave < APS && pa < NPA && c + 1 < kpt) {
-        src = asrc(c + 1, opaque_v(wave * 8 + sub) + (J - LA) * APS * 8);
-        dst = smem + ((c + 1) & 1) * Cfg::AWIN + pa * 1024;
-      }
-    } else if (J == 0) {
-      const int pa = (KT - LA) * APS + wave;
-      if (c > 0 && wave < APS && pa < NPA) {
-        src = asrc(c, opaque_v(wave * 8 + sub) + (KT - LA) * APS * 8);
-        dst = smem + (c & 1) * Cfg::AWIN + pa * 1024;
-      }
-    }
-    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
-  };
-  // window 0's rows, then the stages of steps 0 .. LA - 1 (they carry nothing: sink DMAs)
-#pragma unroll
-  for (int i = 0; i < A0W; ++i) {
-    const int pa = (wave + NW * i) % NPA;
-    const void* src = asrc(0, pa * 8 + sub);
-    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
-  }
-  stage(0, 0);
-  if (LA == 2) stage(1, 0);
-  if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (LA == 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(DPS) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
 
-  const int wm = wave / WN, wn = wave % WN;
-  const int fr = lane & 15, fg = lane >> 4;
-  f32x4 acc[BG_MT][BG_NT];
+  using S = WinSched<MODE, NTP>;
+  constexpr int NS = S::NS;
+    // stage of step (c, J): the weight pieces of its tap, then the A carry: steps jj >= LA carry group
+    // jj - LA of the next window, step jj = 0 (except the first window) its own window's last group
+    auto stage = [&](const int J, int c) {
+      const int Q = S::q(J), JJ = S::jj(J);
+      char* sbase = smem + Cfg::SOFF + ((c * (NS % NST) + J) % NST) * STAGE;
+      const int k0 = S::dt(J) * 2 * g.Kc + 64 * c;
 #pragma unroll
-  for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-    for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
-  const unsigned zrow = lds0 + Cfg::ZOFF;
-  unsigned boffr[2][BG_NT];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int y = 0; y < BG_NT; ++y) {
-      const int r = wn * 32 + y * 16 + fr;
-      boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
-    }
-  // the wave's rows: clip base row in the window and first output row of the clip
-  const int cbase = CPW == 2 ? wm * 144 : 0, lo0 = CPW == 2 ? 0 : wm * 144;
-  for (int c = 0; c < kpt; ++c) {
-    const unsigned wrow = lds0 + (c & 1) * Cfg::AWIN + (unsigned)cbase * 128;
-    const bool more = c + 1 < kpt;
-#pragma unroll
-    for (int J = 0; J < KT; ++J) {  // unrolled: J, JS, CS are constants in every copy
-      const int JS = (J + LA) % KT, CS = (J + LA) / KT;  // the step staged now: (c + CS, JS)
-      const bool issue = CS == 0 || more;
-      if (issue) stage(JS, c + CS);
-      const int t = opaque_v(lo0 + fr) + ss * (J - P) * V;  // lane's tile-0 row in the clip, tap-shifted
-      const unsigned rb = wrow + (unsigned)t * 128;
-      const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
-      const unsigned soff = ((c * (KT % NST) + J) % NST) * STAGE;
-      u32x4_t f[2][BG_NT + BG_MT];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int y = 0; y < BG_NT; ++y) asm volatile("ds_read_b128 %0, %1" : "=v"(f[ks][y]) : "v"(boffr[ks][y] + soff));
-#define F3_AREAD1(X)                                                                                      \
-  {                                                                                                       \
-    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X);  \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][BG_NT + (X)]) : "v"(ad), "n"(2048 * (X))); \
-  }
-        F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6) F3_AREAD1(7)
-        F3_AREAD1(8)
-#undef F3_AREAD1
+      for (int i = 0; i < BSL; ++i) {
+        const void* wsrc = bsrc[i] + k0;
+        __builtin_amdgcn_global_load_lds(wsrc, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
       }
+      // target window (tc, tq), group kk, pieces per group na; carry == false: sink
+      const bool NEXT = JJ >= LA, OWN = JJ == 0;
+      const int TQ = NEXT ? (NQ == 2 && Q == 0 ? 1 : 0) : Q;
+      const int QP = NQ == 2 ? 1 - Q : 0;  // the window before (OWN)
+      const int KK = NEXT ? JJ - LA : S::ntq(QP) - LA;
+      const int NCAR = (NEXT ? S::ntq(Q) : S::ntq(QP)) - LA + 1;
+      const int NA = (NPA + NCAR - 1) / NCAR;  // (<= ASL * NW: APS_MAX)
+      const int tc = NEXT && !(NQ == 2 && Q == 0) ? c + 1 : c;
+      const bool car = (NEXT || OWN) && tc < kpt && !(OWN && c == 0 && Q == 0);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(BG_NT + BG_MT) : "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int s2 = 0; s2 < ASL; ++s2) {
+        const void* src = a.zero;
+        char* dst = smem + Cfg::DOFF;
+        const int sl = wave + NW * s2, pa = KK * NA + sl;
+        if (car && sl < NA && pa < NPA) {
+          src = asrc(tc, TQ, opaque_v(wave * 8 + sub) + (KK * NA + NW * s2) * 8);
+          dst = smem + (NQ == 2 ? TQ : (tc & 1)) * Cfg::AWIN + pa * 1024;
+        }
+        __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
+      }
+    };
+    // window 0's rows (chunk 0, q 0), then the stages of steps 0 .. LA - 1 (they carry nothing)
 #pragma unroll
-        for (int qq = 0; qq < BG_NT + BG_MT; ++qq) asm volatile("" : "+v"(f[ks][qq]));
+    for (int i = 0; i < A0W; ++i) {
+      const int pa = (wave + NW * i) % NPA;
+      const void* src = asrc(0, 0, pa * 8 + sub);
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
+    }
+    stage(0, 0);
+    if constexpr (LA == 2) stage(1, 0);
+    if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (LA == 2) wait_vm<DPS>();
+    else wait_vm<0>();
+    wait_lgkm<0>();
+    __builtin_amdgcn_s_barrier();
+
+    const int wm = wave / WN, wn = wave % WN;
+    const int fr = lane & 15, fg = lane >> 4;
+    f32x4 acc[BG_MT][BG_NT];
 #pragma unroll
-        for (int x = 0; x < BG_MT; ++x)
+    for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y) {
-            // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order)
-            acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
-                                   acc[x][y]);
-            if (ks == 1)
-              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]), __builtin_bit_cast(bf16x8, f[1][y]),
-                                     acc[x][y]);
-          }
-        if (ks == 0) {
+      for (int y = 0; y < BG_NT; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned lds0 = (unsigned)(size_t)(lds_cchar_t*)smem;
+    const unsigned zrow = lds0 + Cfg::ZOFF;
+    unsigned boffr[2][BG_NT];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int y = 0; y < BG_NT; ++y) {
+        const int r = wn * 32 + y * 16 + fr;
+        boffr[ks][y] = lds0 + Cfg::SOFF + r * 128 + swz(r, ks * 4 + fg) * 16;
+      }
+    // the wave's rows: clip base row in the window and first output row of the clip
+    const int cbase = CPW == 2 ? wm * 144 : 0, lo0 = CPW == 2 ? 0 : wm * 144;
+    for (int c = 0; c < kpt; ++c) {
+      const bool more = c + 1 < kpt;
+#pragma unroll
+      for (int J = 0; J < NS; ++J) {  // unrolled: the schedule below folds to constants per step
+        const int JS = (J + LA) % NS, CS = (J + LA) / NS;  // the step staged now: (c + CS, JS)
+        const bool issue = CS == 0 || more;
+        if (issue) stage(JS, c + CS);
+        const unsigned wrow = lds0 + (NQ == 2 ? S::q(J) : (c & 1)) * Cfg::AWIN + (unsigned)cbase * 128;
+        const int t = opaque_v(lo0 + fr) + (MODE == 0 ? ss * S::shift(J) : S::shift(J)) * V;  // tap-shifted row
+        const unsigned rb = wrow + (unsigned)t * 128;
+        const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
+        const unsigned soff = ((c * (NS % NST) + J) % NST) * STAGE;
+        u32x4_t f[2][BG_NT + BG_MT];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int y = 0; y < BG_NT; ++y) f[ks][y] = lds_rd128(boffr[ks][y] + soff);
+#define F3_AREAD1(X)                                                                                 \
+  {                                                                                                  \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X); \
+    f[ks][BG_NT + (X)] = lds_rd128o<2048 * (X)>(ad);                                                 \
+  }
+          F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6) F3_AREAD1(7)
+          F3_AREAD1(8)
+#undef F3_AREAD1
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks == 0) wait_lgkm<BG_NT + BG_MT>();
+          else wait_lgkm<0>();
+#pragma unroll
+          for (int qq = 0; qq < BG_NT + BG_MT; ++qq) pin_v(f[ks][qq]);
 #pragma unroll
           for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
-            for (int y = 0; y < BG_NT; ++y) asm volatile("" : "+v"(acc[x][y]));
+            for (int y = 0; y < BG_NT; ++y) {
+              // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order)
+              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
+                                     acc[x][y]);
+              if (ks == 1)
+                acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]),
+                                       __builtin_bit_cast(bf16x8, f[1][y]), acc[x][y]);
+            }
+          if (ks == 0) {
+#pragma unroll
+            for (int x = 0; x < BG_MT; ++x)
+#pragma unroll
+              for (int y = 0; y < BG_NT; ++y) pin_v(acc[x][y]);
+          }
         }
+        // the step staged LA ahead must land before its compute: with LA = 2 this step's own DMAs
+        // (the step after next) stay in flight
+        if (LA == 2 && issue) wait_vm<DPS>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
       }
-      // the step staged LA ahead must land before its compute: with LA = 2 this step's own DMAs
-      // (the step after next) stay in flight
-      if (LA == 2 && issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
     }
-  }
-  (void)nstep;
-  __syncthreads();
-  auto none = [](int) { return -1; };
-  big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, 0, 0, 0, none);
+    __syncthreads();
+    auto none = [](int) { return -1; };
+    big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, MODE, wpar, 0, none);
 }
 
 }  // namespace f3
@@ -986,11 +1049,26 @@ bool f3_igemm_big_win_ok(const ConvGemmArgs& a) { return f3_igemm_big_ok(a) && b
 // W4 (WIN = 144 only): a 4-wave form, one clip x 128 channels per workgroup, meant to run two
 // independent workgroups per CU. Measured 1.5-1.75x SLOWER alone (l8d 134 -> 235 us) and the step
 // 8.73 -> 9.36 ms (profiles/r05_win4_ab.txt); not dispatched, kept as the template's 4-wave case.
-// F3_WIN1=0 (A/B only): the stride-1 window GEMMs on igemm_big's run-time tap schedule instead of
-// igemm_win1 (read per call: tests compare the two forms)
-static bool win1_enabled() {
+// F3_WIN1 (A/B only; read per call, the tests compare the forms): 0 = the window GEMMs on igemm_big's
+// run-time tap schedule, 1 = igemm_win1 for stride 1 only, unset / 2 = igemm_win1 for every mode
+static bool win1_enabled(int mode) {
   const char* e = getenv("F3_WIN1");
-  return !e || atoi(e) != 0;
+  const int v = e ? atoi(e) : 2;
+  return mode == 0 ? v >= 1 : v >= 2;
+}
+
+template <int E, int WM, int WN, int CL>
+static void launch_win1(const ConvGemmArgs& a, int mode, int tiles, hipStream_t s) {
+  if constexpr (CL == 540) {  // (64-channel layers: stride 1 only)
+    hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+    else if (mode == 1) {  // one launch per output-frame parity (5 / 4 taps: a compile-time schedule each)
+      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 5>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
+      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 4>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
+    }
+    else hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 2>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+  }
 }
 
 template <int CL, bool W4 = false>
@@ -998,14 +1076,16 @@ static int launch_win(const ConvGemmArgs& a, int epi, hipStream_t s) {
   constexpr int WM = CL == 540 ? 4 : W4 ? 1 : 2, WN = CL == 540 ? 2 : 4, CPW = BigCfg<WM, WN, CL>::CPW;
   const int nclip = a.g.M / (a.g.T_out * a.g.V);
   const int tiles = (nclip + CPW - 1) / CPW * (a.g.S == 2 && a.g.transposed ? 2 : 1) * (a.g.Nc / (32 * WN));
-  // stride 1, 9 taps, pad 4, native split form: the compile-time tap schedule (igemm_win1). Alone
+  // 9 taps, pad 4, native split form: the compile-time tap schedule (igemm_win1). Alone
   // (tools/kbench.py, profiles/r06_win1_kbench.txt): T=8 fwd / dgrad 138 / 132 -> 114 / 110 us, T=15 75 /
-  // 77 -> 67 / 66, T=30 dgrad 46 -> 43; the T=30 forward measured 43.6 -> 45.2 and stays on igemm_big
-  const bool w1 = !W4 && a.x3n && a.g.S == 1 && a.g.KT == 9 && a.g.P == 4 && (CL != 540 || a.g.transposed) &&
-                  win1_enabled();
+  // 77 -> 67 / 66, T=30 dgrad 46 -> 43; the T=30 forward measured 43.6 -> 45.2 and stays on igemm_big.
+  // Stride 2: MODE 1 (input gradient by output-frame parity), MODE 2 (forward, even / odd windows).
+  const int mode = a.g.S == 1 ? 0 : a.g.transposed ? 1 : 2;
+  const bool w1 = !W4 && a.x3n && a.g.KT == 9 && a.g.P == 4 && (CL != 540 || (a.g.transposed && mode == 0)) &&
+                  win1_enabled(mode);
 #define F3_WCASE(E)                                                                                   \
   if (epi == (E)) {                                                                                  \
-    if (w1) hipLaunchKernelGGL((igemm_win1<(E), WM, WN, CL>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
+    if (w1) launch_win1<(E), WM, WN, CL>(a, mode, tiles, s);                                          \
     else if (a.x3n) hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, true>), dim3(tiles), dim3(64 * WM * WN), 0, s, a); \
     else hipLaunchKernelGGL((igemm_big<(E), WM, WN, CL, false>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);     \
     F3_LAUNCH_CHECK();                                                                                \

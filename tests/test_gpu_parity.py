@@ -216,17 +216,21 @@ def test_conv_x3cat_kernels_match_torch(shape):
     assert max(errs.values()) <= X3_TOL, errs
 
 
-@pytest.mark.parametrize("shape", [(4, 8, 18, 256, 256), (3, 15, 18, 128, 128), (3, 30, 18, 64, 64),
-                                   (2, 29, 18, 64, 64), (3, 8, 18, 256, 256)])
+@pytest.mark.parametrize("shape", [(4, 8, 18, 256, 256, 1), (3, 15, 18, 128, 128, 1), (3, 30, 18, 64, 64, 1),
+                                   (2, 29, 18, 64, 64, 1), (3, 8, 18, 256, 256, 1), (3, 15, 18, 256, 256, 2),
+                                   (4, 15, 18, 256, 256, 2), (3, 30, 18, 128, 128, 2), (3, 29, 18, 128, 128, 2)])
 def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
-    """igemm_win1 (the stride-1 clip-window GEMM with its tap schedule unrolled at compile time) against
-    igemm_big's run-time schedule (F3_WIN1=0): the same staged bytes, fragment reads and MFMA order, so
-    forward (bias epilogue), input gradient and the step's RELUMASK input gradient (with its BN1-backward
-    sums) must agree bit for bit, on ragged clip counts (odd N at two clips per workgroup) and T = 29."""
+    """igemm_win1 (the clip-window GEMM with its tap schedule unrolled at compile time: stride 1, and
+    stride 2 by output-frame parity (input gradient, one launch per parity) or by even / odd input
+    frames (forward)) against igemm_big's run-time schedule (F3_WIN1=0): the same staged bytes,
+    fragment reads and MFMA order, so forward (bias epilogue), input gradient and, at stride 1, the
+    step's RELUMASK input gradient (with its BN1-backward sums) must agree bit for bit, on ragged clip
+    counts (odd N at two clips per workgroup) and T = 29."""
     d = dev()
     import fall_multimodal_amd._lib as L
     lib, st = L.lib(), L.stream_handle()
-    N, T, V, Ci, Co = shape
+    N, T, V, Ci, Co, S = shape
+    To = (T + 8 - 9) // S + 1
     torch.manual_seed(21)
 
     def split(t):
@@ -236,7 +240,7 @@ def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
         return out
 
     x3 = split(torch.randn(N, T, V, Ci))
-    dy3 = split(torch.randn(N, T, V, Co))
+    dy3 = split(torch.randn(N, To, V, Co))
     w = (torch.randn(Co, Ci, 9) / np.sqrt(9 * Ci)).to(d)
     b = torch.randn(Co).to(d)
     g = torch.randn(N, T, V, Ci, device=d)
@@ -245,14 +249,17 @@ def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
     bsum, bsq = gd.sum(0), (gd * gd).sum(0)
 
     def run():
-        y = torch.empty(N, T, V, Co, device=d)
+        y = torch.empty(N, To, V, Co, device=d)
         wp = torch.empty(Co * Ci * 9 + 64, device=d)
-        L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, Ci, Co, 9, 1, 4,
+        L.check(lib.f3_conv_forward_x3cat(L.ptr(x3), L.ptr(w), L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, Ci, Co, 9, S, 4,
                                           st), "fwd")
         dx = torch.empty(N, T, V, Ci, device=d)
         wpt = torch.empty(Co * Ci * 9 + 64, device=d)
-        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wpt), N, T, V, Ci, Co, 9, 1, 4,
+        L.check(lib.f3_conv_backward_data_x3cat(L.ptr(dy3), L.ptr(w), L.ptr(dx), L.ptr(wpt), N, T, V, Ci, Co, 9, S, 4,
                                                 st), "dgrad")
+        if S == 2:
+            torch.cuda.synchronize()
+            return y, dx
         dv = torch.empty(N, T, V, Ci, device=d)
         s1 = torch.zeros(Ci, dtype=torch.float64, device=d)
         s2 = torch.zeros_like(s1)
