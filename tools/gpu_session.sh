@@ -27,15 +27,20 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# raw rocprofv3 databases stay on the box (gpurun copies back at most 64 MiB of gpurun_out/); only the
+# summaries made from them go to gpurun_out/
+export PROF_DIR=${PROF_DIR:-/tmp/f3prof}
+P=$PROF_DIR
+mkdir -p "$P"
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 rc_all=0
 run() {  # name limit cmd...
   local name=$1 lim=$2
   shift 2
-  echo "== $name ($(date +%T))"
+  echo "== $name ($(date +%T))" >&2
   timeout -k 10 "$lim" "$@"
   local rc=$?
-  echo "== $name rc=$rc ($(date +%T))"
+  echo "== $name rc=$rc ($(date +%T))" >&2
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
     echo "== stopping: $name ended with $rc"
     exit $rc
@@ -55,11 +60,11 @@ for step in "$@"; do
       fi
       tail -5 gpurun_out/gpu_tests.log ;;
     step_prof)
-      run step_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step -o run -- \
+      run step_prof 300 rocprofv3 --kernel-trace --stats -d $P/step -o run -- \
         python tools/step_only.py 8 > gpurun_out/step_prof.log 2>&1
-      python tools/prof_summary.py gpurun_out/step/run_results.db --per-step 11 --top 60 \
+      python tools/prof_summary.py $P/step/run_results.db --per-step 11 --top 60 \
         > gpurun_out/step_kernels.txt 2>&1
-      python tools/timeline.py gpurun_out/step/run_results.db --list > gpurun_out/step_timeline.txt 2>&1
+      python tools/timeline.py $P/step/run_results.db --list > gpurun_out/step_timeline.txt 2>&1
       head -25 gpurun_out/step_kernels.txt ;;
     step_time)
       for pr in ${PRECS:-bf16}; do
@@ -68,18 +73,18 @@ for step in "$@"; do
       done
       cat gpurun_out/step_time.log ;;
     step_prof_ag)
-      run step_prof_ag 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step_ag -o run -- \
+      run step_prof_ag 300 rocprofv3 --kernel-trace --stats -d $P/step_ag -o run -- \
         python tools/step_only.py 8 autograd > gpurun_out/step_prof_ag.log 2>&1
-      python tools/prof_summary.py gpurun_out/step_ag/run_results.db --per-step 11 --top 60 \
+      python tools/prof_summary.py $P/step_ag/run_results.db --per-step 11 --top 60 \
         > gpurun_out/step_ag_kernels.txt 2>&1
-      python tools/timeline.py gpurun_out/step_ag/run_results.db --list > gpurun_out/step_ag_timeline.txt 2>&1
+      python tools/timeline.py $P/step_ag/run_results.db --list > gpurun_out/step_ag_timeline.txt 2>&1
       head -25 gpurun_out/step_ag_kernels.txt ;;
     step_prof_serial)
       export F3_SERIAL=1
-      run step_prof_serial 300 rocprofv3 --kernel-trace --stats -d gpurun_out/step_serial -o run -- \
+      run step_prof_serial 300 rocprofv3 --kernel-trace --stats -d $P/step_serial -o run -- \
         python tools/step_only.py 8 > gpurun_out/step_prof_serial.log 2>&1
       unset F3_SERIAL
-      python tools/prof_summary.py gpurun_out/step_serial/run_results.db --per-step 11 --top 80 \
+      python tools/prof_summary.py $P/step_serial/run_results.db --per-step 11 --top 80 \
         > gpurun_out/step_serial_kernels.txt 2>&1
       head -25 gpurun_out/step_serial_kernels.txt ;;
     kbench)
@@ -92,49 +97,49 @@ for step in "$@"; do
                  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_WAVES SQ_INST_CYCLES_VMEM" \
                  "FETCH_SIZE"; do
         i=$((i + 1))
-        rm -rf gpurun_out/kpmc_$i
-        run kpmc_$i 90 rocprofv3 --pmc $SET -d gpurun_out/kpmc_$i -o run -- python tools/kbench.py \
+        rm -rf $P/kpmc_$i
+        run kpmc_$i 90 rocprofv3 --pmc $SET -d $P/kpmc_$i -o run -- python tools/kbench.py \
           ${KB_KEYS:-l1f l1d l4f l4d l5f l5d l7f l7d l8f l8d} > gpurun_out/kpmc_$i.log 2>&1
-        db=$(find gpurun_out/kpmc_$i -name "*.db" | head -1)
+        db=$(find $P/kpmc_$i -name "*.db" | head -1)
         python tools/pmc_kernels.py "$db" >> gpurun_out/kpmc.txt 2>&1
       done
       tail -40 gpurun_out/kpmc.txt ;;
     step_pmc)
       for C in FETCH_SIZE WRITE_SIZE; do
-        rm -rf gpurun_out/pmc_$C
-        run pmc_$C 120 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run -- python tools/step_only.py 2 \
+        rm -rf $P/pmc_$C
+        run pmc_$C 120 rocprofv3 --pmc $C -d $P/pmc_$C -o run -- python tools/step_only.py 2 \
           > gpurun_out/step_pmc_$C.log 2>&1
-        db=$(find gpurun_out/pmc_$C -name "*.db" | head -1)
-        [ -n "$db" ] && [ "$db" != "gpurun_out/pmc_$C/run_results.db" ] && mv "$db" gpurun_out/pmc_$C/run_results.db
+        db=$(find $P/pmc_$C -name "*.db" | head -1)
+        [ -n "$db" ] && [ "$db" != "$P/pmc_$C/run_results.db" ] && mv "$db" $P/pmc_$C/run_results.db
       done
-      python tools/pmc_summary.py gpurun_out --top 60 > gpurun_out/step_hbm_traffic.txt 2>&1
+      python tools/pmc_summary.py $P --top 60 > gpurun_out/step_hbm_traffic.txt 2>&1
       head -30 gpurun_out/step_hbm_traffic.txt ;;
     roof_prof)
       for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd gcn_l5 gcn_l6}; do
-        run roof_prof_$K 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof_$K -o run -- \
+        run roof_prof_$K 300 rocprofv3 --kernel-trace --stats -d $P/roof_$K -o run -- \
           python tools/roofline_pmc.py run $K > gpurun_out/roof_prof_$K.log 2>&1
-        python tools/prof_summary.py gpurun_out/roof_$K/run_results.db --top 30 > gpurun_out/roof_kernels_$K.txt 2>&1
+        python tools/prof_summary.py $P/roof_$K/run_results.db --top 30 > gpurun_out/roof_kernels_$K.txt 2>&1
         head -8 gpurun_out/roof_kernels_$K.txt
       done ;;
     roof_pmc)
       for K in ${ROOF_KEYS:-wgrad_l1 dgrad_l8 wgrad_l5 wgrad wgrad_kernel tcn_fwd gcn_l5 gcn_l6}; do
         for C in FETCH_SIZE WRITE_SIZE; do
-          rm -rf gpurun_out/rpmc_${K}_$C
-          run rpmc_${K}_$C 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/rpmc_${K}_$C -o run -- \
+          rm -rf $P/rpmc_${K}_$C
+          run rpmc_${K}_$C 120 rocprofv3 --pmc $C --kernel-trace -d $P/rpmc_${K}_$C -o run -- \
             python tools/roofline_pmc.py run $K > gpurun_out/roof_pmc_${K}_$C.log 2>&1
-          db=$(find gpurun_out/rpmc_${K}_$C -name "*.db" | head -1)
-          [ -n "$db" ] && [ "$db" != "gpurun_out/rpmc_${K}_$C/run_results.db" ] && mv "$db" gpurun_out/rpmc_${K}_$C/run_results.db
+          db=$(find $P/rpmc_${K}_$C -name "*.db" | head -1)
+          [ -n "$db" ] && [ "$db" != "$P/rpmc_${K}_$C/run_results.db" ] && mv "$db" $P/rpmc_${K}_$C/run_results.db
         done
       done
-      python tools/roofline_pmc.py summarize gpurun_out > gpurun_out/roofline_pmc.json 2>&1
+      python tools/roofline_pmc.py summarize $P > gpurun_out/roofline_pmc.json 2>&1
       cat gpurun_out/roofline_pmc.json | head -40 ;;
     rgb_pmc)   # HBM traffic of the RGB branch kernels (bench.py rgb_branch) -> gpurun_out/rgb_pmc.json
       for C in FETCH_SIZE WRITE_SIZE; do
-        rm -rf gpurun_out/pmc_$C
-        run rgbpmc_$C 180 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run -- python tools/rgb_bench.py \
+        rm -rf $P/pmc_$C
+        run rgbpmc_$C 180 rocprofv3 --pmc $C -d $P/pmc_$C -o run -- python tools/rgb_bench.py \
           > gpurun_out/rgb_pmc_$C.log 2>&1
-        db=$(find gpurun_out/pmc_$C -name "*.db" | head -1)
-        [ -n "$db" ] && [ "$db" != "gpurun_out/pmc_$C/run_results.db" ] && mv "$db" gpurun_out/pmc_$C/run_results.db
+        db=$(find $P/pmc_$C -name "*.db" | head -1)
+        [ -n "$db" ] && [ "$db" != "$P/pmc_$C/run_results.db" ] && mv "$db" $P/pmc_$C/run_results.db
       done
       python tools/rgb_pmc.py gpurun_out > gpurun_out/rgb_pmc.json 2>&1
       cat gpurun_out/rgb_pmc.json ;;
@@ -151,7 +156,7 @@ for step in "$@"; do
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     exit_prof)  # tools/exit_check.py under a rocprofv3 kernel trace: the exit status after finalisation
-      run exit_prof 240 rocprofv3 --kernel-trace --stats -d gpurun_out/exitprof -o run -- \
+      run exit_prof 240 rocprofv3 --kernel-trace --stats -d $P/exitprof -o run -- \
         python tools/exit_check.py > gpurun_out/exit_prof.log 2>&1
       grep -E "exit_check|Abort|SIGSEGV" gpurun_out/exit_prof.log ;;
     bench_tg)  # the TARGCN (cfg 2) line alone, A/B over TG_CFGS (env assignments, "-" = defaults)

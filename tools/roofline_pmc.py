@@ -40,8 +40,9 @@ def run(key):
     import torch
     import bench
     r = bench.roofline_kernels(torch.device("cuda"), 256, 18, "bf16x3", only=key)
-    os.makedirs(os.path.join(ROOT, "gpurun_out", "roof_names"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "roof_names", key + ".json"), "w") as f:
+    out = os.environ.get("PROF_DIR", os.path.join(ROOT, "gpurun_out"))  # (tools/gpu_session.sh sets it)
+    os.makedirs(os.path.join(out, "roof_names"), exist_ok=True)
+    with open(os.path.join(out, "roof_names", key + ".json"), "w") as f:
         json.dump(r[key], f)
     print(json.dumps({k: [v["kernel"], v["ms_per_launch"], v["frac"]] for k, v in r.items()}))
 
