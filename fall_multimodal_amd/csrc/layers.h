@@ -123,6 +123,10 @@ struct BlockArgs {
   float* part;
   float* dgammar;
   float* dbetar;
+  // block_bwd_apply (bf16x3): per (chunk, clip) column sums of the fp32 dh rows (the tcn bias gradient)
+  // and, conv residual, of dres (its bias), rows [chunks][N][C | C] summed by the caller's colsum; the
+  // weight-gradient kernels then run without their in-loop bias sums. null: not written
+  float* dbpart;
 };
 
 struct BnBwdArgs {
@@ -234,6 +238,7 @@ int f3_block_bwd_reduce(f3::BlockArgs a, hipStream_t s);
 int f3_block_bwd_apply(f3::BlockArgs a, hipStream_t s);
 int f3_bn_bwd_apply(f3::BnBwdArgs a, hipStream_t s);
 int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
+int f3_block_chunks(int TV);                 // row chunks per clip of the block kernels (dbpart rows: chunks * N)
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
 // several independent column sums in one launch (each as f3_colsum_ld)
 constexpr int kColsumJobs = 8;

@@ -1289,6 +1289,7 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   const f32x4 ev = *reinterpret_cast<const f32x4*>(a.e + (size_t)n * C + c0);
   f32x4 dbc = {0, 0, 0, 0};
   if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
+  f32x4 sdh = {0, 0, 0, 0}, sdr = {0, 0, 0, 0};  // (dbpart) the chunk's column sums of dh / dres
   for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
     f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
     size_t off[kRowU];
@@ -1314,6 +1315,10 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
         } else {
           dr[e] = dz;
         }
+      }
+      if (mb + u * RP < r1) {  // (rows past the chunk re-store its last row: summed once)
+        sdh += dh;
+        if (RES == RES_CONV) sdr += dr;
       }
       if (a.dhb) {
         bf16x4 hb, lb;
@@ -1349,6 +1354,16 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
       } else if (RES != RES_NONE) {
         *reinterpret_cast<f32x4*>(a.dres + off[u]) = dr;
       }
+    }
+  }
+  if (a.dbpart) {  // partial rows [chunk][n][C | C] (fixed-order sums in the caller's colsum)
+    __shared__ __attribute__((aligned(16))) float lds[1024];
+    float* row = a.dbpart + ((size_t)blockIdx.x * a.N + n) * 2 * C;
+    const f32x4 s1 = quad_reduce(sdh, lds, C4);
+    if (tid < C4) *reinterpret_cast<f32x4*>(row + tid * 4) = s1;
+    if (RES == RES_CONV) {
+      const f32x4 s2 = quad_reduce(sdr, lds, C4);
+      if (tid < C4) *reinterpret_cast<f32x4*>(row + C + tid * 4) = s2;
     }
   }
 }
@@ -2259,6 +2274,7 @@ int f3_gcn_bias_bwd(const GcnBiasBwdArgs* a, hipStream_t s) {
 // rows per workgroup of the clip-chunk elementwise kernels (block_out, block_bwd_*): 96 (192 or 270
 // measured no faster, profiles/r03_chunk_ab.txt)
 static int chunks_for(int TV) { return max(1, (TV + 95) / 96); }
+int f3_block_chunks(int TV) { return chunks_for(TV); }
 
 // backward block kernels: instantiate on (activation type, residual kind, pooled gradient)
 template <bool A16, int RES, bool DNC>

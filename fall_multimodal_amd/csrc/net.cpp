@@ -286,6 +286,7 @@ struct LayerWs {
   // per-layer partial rows of the BN1-backward node sums (G) and the graph-mix dA, reduced on
   // the side stream
   float *gpart = nullptr, *mixpart = nullptr;
+  float* dbpart = nullptr;  // bf16x3: block_bwd_apply's dh / dres column-sum rows (tcn / residual bias grads)
 };
 
 struct StreamWs {
@@ -437,6 +438,7 @@ Ws plan(const f3_net& net, int N, char* base) {
       X.dh = reinterpret_cast<float*>(A.take<unsigned short>(Mo * C * 2));  // x3: [hi | lo] rows
       X.dg = gcat ? reinterpret_cast<float*>(A.take<unsigned short>(2 * Mi * C)) : A.take<float>(Mi * C);
       X.gpart = A.take<float>((size_t)f3_bn_bwd_parts(N, L.T_in * V, V) * V * C);
+      if (x3) X.dbpart = A.take<float>((size_t)f3_block_chunks(L.T_out * V) * N * 2 * C);
       X.mixpart = A.take<float>((size_t)kMixParts * K * V * V);
       // (bf16x3: dres as rows [hi | lo] of 2C bf16)
       if (L.res == RES_CONV) X.dres = x3 ? reinterpret_cast<float*>(A.take<unsigned short>(2 * Mo * C)) : A.take<float>(Mo * C);
@@ -824,6 +826,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     ba.part = W.detm;
     if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
+    ba.dbpart = x3 ? X.dbpart : nullptr;  // (block_bwd_apply only: the bias-gradient rows)
     CaArgs ca;
     std::memset(&ca, 0, sizeof(ca));
     ca.N = N; ca.C = C; ca.inv_tv = 1.f / (float)(To * V); ca.bn2 = bn2;
@@ -930,8 +933,15 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       tw.slab = W.slab; tw.slab_cap = kWgradSlabFloats * 4; tw.dw_ref = q.g(L.tcn_w);
       tw.g = geom(Mo, C, C, 9, L.stride, 4, 0, To, Ti, V, 2 * C, C);
       tw.x3seg = 1;
+      tw.db = nullptr;  // the bias gradient from block_bwd_apply's dh rows (colsum below)
       if (!f3_wgrad_glds_ok(tw)) return F3_EINVAL;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
+      if (part & 2) {
+        const int rows = f3_block_chunks(To * V) * N;
+        const ColsumJob jb[2] = {{X.dbpart, q.g(L.tcn_b), 2LL * C, rows, C},
+                                 {X.dbpart + C, L.res == RES_CONV ? q.g(L.res_b) : nullptr, 2LL * C, rows, C}};
+        F3_TRY(f3_colsum_multi(jb, L.res == RES_CONV ? 2 : 1, ss));
+      }
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 1, ss));
@@ -953,6 +963,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
         rw.slab = W.slab; rw.slab_cap = kWgradSlabFloats * 4; rw.dw_ref = q.g(L.res_w);
         rw.g = geom(Mo, C, Ci, 1, L.stride, 0, 0, To, Ti, V, 2 * Ci, C);
         rw.x3seg = 1;
+        rw.db = nullptr;  // summed from block_bwd_apply's dres rows with the tcn bias
         if (!f3_wgrad_glds_ok(rw)) return F3_EINVAL;
       } else {
         rw.dy = dres; rw.in = X.x;
