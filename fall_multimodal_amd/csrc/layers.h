@@ -241,7 +241,7 @@ int f3_bn_bwd_parts(int N, int TV, int V);  // Gpart rows f3_bn_bwd_apply writes
 int f3_block_chunks(int TV);                 // row chunks per clip of the block kernels (dbpart rows: chunks * N)
 int f3_bnrelu_bf16(const f3::BnReluArgs* a, hipStream_t s);
 // several independent column sums in one launch (each as f3_colsum_ld)
-constexpr int kColsumJobs = 8;
+constexpr int kColsumJobs = 10;
 struct ColsumJob {
   const float* part;
   float* out;
@@ -254,5 +254,7 @@ int f3_colsum(const float* part, int rows, int cols, float* out, hipStream_t s);
 int f3_colsum_ld(const float* part, int rows, long long ld, int cols, float* out, hipStream_t s);
 int f3_ca_fwd(const f3::CaArgs* a, hipStream_t s);
 int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);          // input-gradient chain (ca_bwd1/2/3)
-int f3_ca_bwd_weights(const f3::CaArgs* a, hipStream_t s);  // W1/W2/b2 gradients (ca_bwd_w)
+// W1/W2/b2 gradients (ca_bwd_w); with `defer`, the three column sums of its partial rows are appended
+// to defer[*ndefer...] (ndefer advanced) for one batched f3_colsum_multi by the caller instead of launched
+int f3_ca_bwd_weights(const f3::CaArgs* a, hipStream_t s, ColsumJob* defer = nullptr, int* ndefer = nullptr);
 int f3_bn_running(const f3::BnRunTable& t, hipStream_t s);

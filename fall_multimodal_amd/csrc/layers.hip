@@ -2453,7 +2453,7 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s) {
+int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s, ColsumJob* defer, int* ndefer) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
   const int groups = (a->N + kCaWClips - 1) / kCaWClips, H = a->C / 4, C = a->C;
   hipLaunchKernelGGL(ca_bwd_w_kernel, dim3((a->C + 63) / 64, groups), dim3(256), 0, s, *a);
@@ -2464,6 +2464,11 @@ int f3_ca_bwd_weights(const CaArgs* a, hipStream_t s) {
   const ColsumJob j[3] = {{a->wpart, a->g_W1, ld, groups, H * C},
                           {a->wpart + H * C, a->g_W2, ld, groups, C * H},
                           {a->wpart + 2 * H * C, a->g_b2, ld, groups, C}};
+  if (defer) {
+    if (!ndefer || *ndefer + 3 > kColsumJobs) return F3_EINVAL;
+    for (int i = 0; i < 3; ++i) defer[(*ndefer)++] = j[i];
+    return F3_OK;
+  }
   return f3_colsum_multi(j, 3, s);
 }
 

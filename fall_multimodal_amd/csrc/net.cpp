@@ -806,6 +806,8 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     float* const dh = X.dh;
     float* const dg = X.dg;
     float* const dres = X.dres;
+    ColsumJob cj[kColsumJobs];  // side-queue column sums, launched together before the gcn bias step
+    int ncj = 0;
     const BnRef bn1 = q.ref(L.bn1, X.bn1, (float)Mi, 0);
     const BnRef bn2 = q.ref(L.bn2, X.bn2, (float)Mo, 0);
     BnRef bnr;
@@ -938,16 +940,15 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 0, ss));
       if (part & 2) {
         const int rows = f3_block_chunks(To * V) * N;
-        const ColsumJob jb[2] = {{X.dbpart, q.g(L.tcn_b), 2LL * C, rows, C},
-                                 {X.dbpart + C, L.res == RES_CONV ? q.g(L.res_b) : nullptr, 2LL * C, rows, C}};
-        F3_TRY(f3_colsum_multi(jb, L.res == RES_CONV ? 2 : 1, ss));
+        cj[ncj++] = {X.dbpart, q.g(L.tcn_b), 2LL * C, rows, C};
+        if (L.res == RES_CONV) cj[ncj++] = {X.dbpart + C, q.g(L.res_b), 2LL * C, rows, C};
       }
     } else {
       tw.dy = dh; tw.in = X.g; tw.pro_bn = bn1;
       if (part & 2) F3_TRY(f3_conv_wgrad(&tw, 1, ss));
     }
     ca.wpart = W.dets;
-    if (part & 2) F3_TRY(f3_ca_bwd_weights(&ca, ss));
+    if (part & 2) F3_TRY(f3_ca_bwd_weights(&ca, ss, cj, &ncj));
     if (L.res == RES_CONV) {
       WgradArgs rw;
       std::memset(&rw, 0, sizeof(rw));
@@ -972,14 +973,19 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     }
     if (split) {  // reductions whose results only feed weight gradients
       const int T = L.T_in, fch = f3_bn_bwd_parts(N, T * V, V);
-      if (part & 2) F3_TRY(f3_colsum(X.gpart, fch, V * C, X.G, ss));
+      if (part & 2) cj[ncj++] = {X.gpart, X.G, (long long)V * C, fch, V * C};
       const int mparts = g0 ? 0 : f3_mix_bwd_parts(&mx);
-      if (mparts && (part & 2)) F3_TRY(f3_colsum(X.mixpart, mparts, K * V * V, X.dAeff, ss));
+      if (mparts && (part & 2)) cj[ncj++] = {X.mixpart, X.dAeff, (long long)K * V * V, mparts, K * V * V};
     }
     if (g0 && (part & 2)) {  // the first block's dA_eff and gcn weight gradient partial rows
-      F3_TRY(f3_colsum(b0.part_dA, g0_parts, K * V * V, X.dAeff, ss));
-      F3_TRY(f3_colsum(b0.part_dW, g0_parts, K * C * Ci, q.g(L.gcn_w), ss));
+      cj[ncj++] = {b0.part_dA, X.dAeff, (long long)K * V * V, g0_parts, K * V * V};
+      cj[ncj++] = {b0.part_dW, q.g(L.gcn_w), (long long)K * C * Ci, g0_parts, K * C * Ci};
     }
+    // this layer's side-queue column sums (attention weights, tcn / residual biases, BN G, dA_eff,
+    // layer-0 gcn rows) as one launch; each job's summation order is that of its own f3_colsum
+    if (ncj > kColsumJobs) return F3_EINVAL;
+    F3_TRY(f3_colsum_multi(cj, ncj, ss));
+    ncj = 0;
     WgradArgs gw;
     std::memset(&gw, 0, sizeof(gw));
     gw.wg_pct = side_pct(split, l);

@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 # bench.py roofline key -> kernel name patterns whose per-launch means add up to one launch of it
 _RED = "wgrad_slab_reduce_kernel"
 KERNELS = {"wgrad_l1": ["wgrad_big<2, 4, 2, 1, 32, 1, 3, true", _RED],
-           "dgrad_l8": ["igemm_big<16, 2, 4, 144"],
+           "dgrad_l8": ["igemm_win1<16, 2, 4, 144"],
            "gcn_l5": ["igemm_big<6, 1, 8, 0"],
            "gcn_l6": ["igemm_big<6, 1, 8, 0"],
            "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 32, 1, 3, true", _RED],
