@@ -19,8 +19,8 @@ GPU, torch.distributed.run as a child process) and fails if the node has fewer t
 Prints ONE JSON line (rank 0) with value = global clips/s over the timed region (max over
 ranks) in the parity-meeting bf16x3 mode (split-bf16 products on bf16 MFMA, fp32 activations: logits
 within 1e-3 of the fp64 oracle, identical argmax), the roofline of the dominant kernel (the
-temporal-conv weight-gradient GEMM, measured live with HIP events on the stream it runs on; HBM
-traffic from profiles/r04_roofline_pmc.json) and the CPU baseline (the oracle timed on this host's
+temporal-conv input-gradient clip-window GEMM, measured live with HIP events on the stream it runs on;
+HBM traffic from profiles/r06_roofline_pmc.json) and the CPU baseline (the oracle timed on this host's
 cores on a bounded sample). The bf16 and fp32 modes' step times are reported beside it
 (bf16_mode, fp32_mode); `--precision bf16` makes the faster, lower-precision bf16 mode the line.
 """
@@ -114,7 +114,7 @@ def launch_check(world, rank):
     dist.destroy_process_group()
 
 
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r05_roofline_pmc_final.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc.json")
 RGB_PMC = os.path.join(ROOT, "profiles", "r04_rgb_pmc.json")
 
 
@@ -202,13 +202,16 @@ def roofline_kernels(dev, batch, V, precision, only=None):
 
 
 def roofline_kernels_x3(dev, batch, V, only=None):
-    """bf16x3 (the headline mode): the step's largest GEMM families (the round-5 serial step profile at
-    HEAD, profiles/r05_x3_step_serial_kernels_final.txt), each launched alone through the C ABI exactly as
+    """bf16x3 (the headline mode): the step's largest GEMM families (the serial step profiles,
+    profiles/r05_x3_step_serial_kernels_final.txt, r06_colsum_batch_serial_kernels.txt), each launched alone
+    through the C ABI exactly as
     the step launches it, on operand rows [hi | lo] (f3_split_x3cat, done once outside the timing, as the
     step's producers write them) in the native split form (three bf16 MFMA products per algorithmic FLOP):
-    * "dgrad_l8": the 256-channel T=8 stride-1 tcn input gradient, igemm_big's clip-window form
-      (two clips x 128 channels per workgroup, the 9 taps reading one staged window) — the HEADLINE:
-      the WIN=144 input-gradient family is the step's largest serial family (600 us/step);
+    * "dgrad_l8": the 256-channel T=8 stride-1 tcn input gradient, the clip-window form with the
+      compile-time tap schedule (igemm_win1: two clips x 128 channels per workgroup, the 9 taps reading
+      one staged window) and the RELUMASK epilogue the step runs — the HEADLINE: the WIN=144 input
+      gradient was the step's largest serial family in round 5 (600 us/step; 3 instances and 680 us
+      per step in round 6, the stride-2 ones split by output-frame parity);
     * "wgrad_l1": the 64-channel T=30 tcn weight gradient (layers 0-3), wgrad_big<2,4,2,1,32> X3F (the
       three products dy_hi x_hi, dy_lo x_hi, dy_hi x_lo from one staging of [hi | lo] rows) + the slab
       reduce — the third (500 us/step; the second is the WIN=144 forward, "tcn_fwd");
@@ -250,7 +253,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
                                           st), "conv")  # packs w; the timed launches reuse it (the GEMM alone)
         ms = _time_launch(lambda: lib.f3_conv_forward_x3cat(L.ptr(x3), None, L.ptr(b), L.ptr(y), L.ptr(wp), N, T, V, C,
                                                             C, KT, 1, 4, st))
-        out["tcn_fwd"] = {"kernel": f"igemm_big<1,2,4,144,x3n> clip window (tcn 9x1 fwd, bf16x3, C=256, T=8, N={N}, "
+        out["tcn_fwd"] = {"kernel": f"igemm_win1<1,2,4,144,0,5> clip window, compile-time tap schedule (tcn 9x1 fwd, bf16x3, C=256, T=8, N={N}, "
                                     f"V={V})", "ms": ms, "bytes": row8 + row8 + wbytes, "flop": conv_flop(N * T * V, C, C)}
     if want("dgrad_l8"):
         # the instance the step runs (stream_backward's td): the RELUMASK epilogue reads g (fp32) and
@@ -265,7 +268,7 @@ def roofline_kernels_x3(dev, batch, V, only=None):
                 L.ptr(ssum), L.ptr(ssq), N, T, V, C, C, st)
         L.check(lib.f3_conv_step_x3cat(1, L.ptr(dy3), L.ptr(w), L.ptr(wp), *args), "dgrad relumask")
         ms = _time_launch(lambda: lib.f3_conv_step_x3cat(1, L.ptr(dy3), None, L.ptr(wp), *args))
-        out["dgrad_l8"] = {"kernel": f"igemm_big<16,2,4,144,x3n> clip window, RELUMASK epilogue (tcn 9x1 input "
+        out["dgrad_l8"] = {"kernel": f"igemm_win1<16,2,4,144,0,5> clip window, compile-time tap schedule, RELUMASK epilogue (tcn 9x1 input "
                                      f"gradient as the step runs it, bf16x3, C=256, T=8, N={N}, V={V})", "ms": ms,
                            "bytes": row8 + row8 + wbytes + N * T * V * C * 4,  # + the mask operand g (fp32)
                            "flop": conv_flop(N * T * V, C, C)}

@@ -11,8 +11,8 @@
 // Tile 128 x BN (BN = 128 or 64) x 64, 4 waves in 2x2 (each 64 x BN/2 = 4 x BN/32 MFMA
 // 16x16x32 tiles), two LDS stages. Each stage is filled by 1-KiB LDS-DMA wave-instructions
 // (8 rows x 128 B); a row's 16-B chunks are stored XOR-swizzled (chunk c of row r at
-// c ^ ((r>>1)&7)) through the per-lane SOURCE address, which makes the 16-lane ds_read_b128
-// fragment reads conflict-free. The implicit-GEMM row gather is also in the source address:
+// c ^ (r & 7), igemm.h swz) through the per-lane SOURCE address, which makes the 16-lane
+// ds_read_b128 fragment reads conflict-free at any row shift. The implicit-GEMM row gather is also in the source address:
 // a row outside the clip (temporal zero padding) or past M reads a zero line.
 // Epilogues as conv_gemm_f32 (bias, graph-mixed bias, BN statistics, channel-attention
 // pooling, ReLU mask + BN-backward sums, accumulate).
@@ -1404,7 +1404,7 @@ static int launch_wgrad(WgradArgs a, hipStream_t s) {
   const int gy = ((a.g.KT + NTW - 1) / NTW) * ((a.g.Kc + TI - 1) / TI);  // (tap groups of NTW)
   // Split-K over rows sized to ONE round of resident workgroups: rounding the split count up
   // (a ceil of 512 / tiles) put 513-540 workgroups on 512 slots on MI355X — a second round
-  // for a handful of workgroups. F3_WGRAD_WGS overrides the target.
+  // for a handful of workgroups.
   static const int slots = resident_wgs((const void*)KERNEL, THREADS);
   // wg_pct (percent): size the splits to that share of the resident slots, leaving CUs to the main
   // chains the side-queue weight gradients run beside

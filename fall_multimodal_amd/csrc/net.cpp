@@ -553,8 +553,9 @@ void add_job(PrepTable& t, int type, int n, float* dst, const float* s0, const f
 
 // bf16 view of a packed operand (the fp32-sized slot holds the bf16 copy in bf16 mode)
 inline const unsigned short* bf(const float* p, int on) { return on ? reinterpret_cast<const unsigned short*>(p) : nullptr; }
-// bf16x3 mode (F3_PRECISION_BF16X3): fp32 activations as in the fp32 mode, GEMMs on the split-bf16
-// kernels (gemm_x3.hip) with the packed weights as bf16 hi / lo planes (prep code 2)
+// bf16x3 mode (F3_PRECISION_BF16X3, the default): fp32 activations as in the fp32 mode; GEMM operands
+// as bf16 rows [x_hi | x_lo] written by their producers and weights packed per tap in 32-channel
+// blocks [W_hi | W_lo] (prep code 4), three bf16 MFMA products per block (x3_gemm below)
 inline int is_x3(const f3_net& n) { return n.cfg.precision == F3_PRECISION_BF16X3; }
 // Side-queue weight gradients of layers >= 2 are split for 75 % of the chip's workgroup slots, so the
 // main chains running beside them keep CUs (a whole-chip wgrad_big grid holds every CU's LDS until it

@@ -438,7 +438,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_fwd_kernel(GruFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Node-partitioned forward recurrence (bf16 mode; F3_GRU_NODE, default on). gru_fwd_kernel keeps
+// Node-partitioned forward recurrence (bf16 mode; always taken where its shape fits). gru_fwd_kernel keeps
 // a clip tile and ALL nodes in one workgroup and re-streams the 17 node weight matrices from L2
 // every step (816 KB per step; measured 19 us of gate GEMM + 14 us of update GEMM per 42 us step,
 // profiles/r03_gru_phases.txt). Here a GROUP of V workgroups shares a tile of GN_BT clips and
@@ -961,7 +961,7 @@ __global__ __launch_bounds__(GRU_THREADS) void gru_bwd_kernel(GruBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Node-partitioned backward recurrence (bf16 mode; F3_GRU_NODE bit 2, default on): the layout of
+// Node-partitioned backward recurrence (bf16 mode, where its shape fits): the layout of
 // gru_fwd_node_kernel applied to gru_bwd_kernel's step. Workgroup (g, n) owns node n of a tile of
 // GN_BT clips: its Wb / Lb tiles (the input-gradient B operands of both EmbGCN products) stay in
 // registers, the element-wise epilogues touch only node n's rows, and the two S^T mixes of the

@@ -9,8 +9,8 @@ alone, so this test checks their results on the step's own tensors after a full 
 TrainStep (both skeleton streams, all four queues busy), at the shape they serve (layer 6:
 C=256, T=8, V=18):
   * forward  h  = conv9x1(u, W) + b           (igemm_big clip window)      vs torch fp32
-  * dgrad    dg = BN1-backward(relu-mask(conv9x1^T(dh, W)))  (igemm_big window, transposed rows,
-               RELUMASK epilogue; then bn_bwd_apply)   vs torch fp32 on the same dh, u, g
+  * dgrad    dg = BN1-backward(relu-mask(conv9x1^T(dh, W)))  (clip window -- igemm_win1 in bf16x3 --
+               transposed rows, RELUMASK epilogue; then bn_bwd_apply)   vs torch fp32 on the same dh, u, g
   * wgrad    dW = sum dh x shifted u           (wgrad_taps + its reduce)   vs torch fp32
 A garbage tap or fragment shows up as O(max) errors; the bounds are bf16 output rounding."""
 import ctypes
@@ -38,8 +38,10 @@ def _view(ws, ptr, n, dtype):
 def test_asm_wait_kernels_inside_the_step(layer, C, T, precision):
     """layer 6: igemm_big clip window + wgrad_taps; layer 1 (64 channels, T=30): the
     weight-stationary tcn64 forward / input gradient (tcn64.hip) and wgrad_big. bf16x3: the same
-    kernels over the K-concatenated [hi | lo] rows (u, dh, dg stored as bf16 rows [x_hi | x_lo] of 2C,
-    h / g fp32, weights fp32), checked against torch fp64 on hi + lo at the split's 1e-4 of max."""
+    path in the native split form (u, dh, dg stored as bf16 rows [x_hi | x_lo] of 2C, h / g fp32,
+    weights fp32; the window GEMMs issue x_hi W_hi + x_lo W_hi + x_hi W_lo, the 64-channel T=30 layers
+    through the WIN=540 clip windows, the tcn input gradients through igemm_win1), checked against
+    torch fp64 on hi + lo at the split's 1e-4 of max."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import fall_multimodal_amd as f3

@@ -161,10 +161,12 @@ X3CAT_SHAPES = [(3, 30, 14, 64, 64, 9, 1, 4), (2, 30, 18, 64, 128, 9, 2, 4), (4,
 
 @pytest.mark.parametrize("shape", X3CAT_SHAPES)
 def test_conv_x3cat_kernels_match_torch(shape):
-    """bf16x3 as the step runs it: fp32 operands split by f3_split_x3cat into [hi | lo] rows and
-    K-concatenated weights [W_hi | W_hi | W_lo] on the bf16 LDS-DMA kernels (forward, input gradient);
-    the weight gradient as one bf16 GEMM on [hi | lo] x [hi | lo] with the quadrant fold. Each against
-    fp64 on the fp32 operands within X3_TOL of the max (the split-bf16 product, ~2^-16 per term)."""
+    """bf16x3 as the step runs it: fp32 operands split by f3_split_x3cat into [hi | lo] rows, the
+    weights packed per tap in 32-channel blocks [W_hi 32 | W_lo 32] (prep code 4), and the bf16 LDS-DMA
+    kernels issuing x_hi W_hi + x_lo W_hi + x_hi W_lo per k step (the native split form: forward, input
+    gradient); the weight gradient from the same [hi | lo] rows (dY_hi X_hi + dY_lo X_hi + dY_hi X_lo).
+    Each against fp64 on the fp32 operands within X3_TOL of the max (the split-bf16 product, ~2^-16 per
+    term)."""
     d = dev()
     import fall_multimodal_amd._lib as L
     lib, st = L.lib(), L.stream_handle()
@@ -740,7 +742,7 @@ def test_backward_rmsprop_per_layer_updates(precision):
 @pytest.mark.parametrize("layout,S,B", [("coco_mmpose", 6, 32), ("coco_cut", 15, 24), ("coco_mmpose", 6, 13)])
 def test_fused_train_step_vs_oracle(layout, S, B, precision):
     """TrainStep (native fwd + CE + bwd + RMSprop) vs the CPU oracle at a larger batch: the HAR
-    layout (V=14, S=15; the motion stream's T=29 and the V=14 tilings of the K-concatenated kernels)
+    layout (V=14, S=15; the motion stream's T=29 and the V=14 tilings of the native split-form kernels)
     and a ragged batch (B=13). Logits within 1e-3 with identical argmax, gradients conditioning-aware
     (bf16x3: envelope at the split's 2^-16)."""
     d = dev()
@@ -821,10 +823,11 @@ def _train_gpu(st, layout, S, precision, batches, d, steps, evaluate=None, check
 
 
 def test_bf16_step_tracks_oracle():
-    """bf16 mode (GEMM operands rounded to bf16, fp32 accumulate, everything else fp32):
-    one step vs the fp32 oracle. Bounds, measured on MI355X with margin: logits within
-    3e-2 of the oracle's (the fp32 mode's bound is 1e-3), same argmax on >= 95 % of clips,
-    whole-model gradient cosine >= 0.99."""
+    """bf16 mode (activations stored bf16, GEMM operands bf16, fp32 accumulate): one step vs the
+    fp32 oracle. This is the fast, lower-precision mode, not a parity mode (the parity modes, bf16x3 --
+    the default and the headline -- and fp32, are held to logits within 1e-3 elsewhere in this file).
+    Bounds, measured on MI355X with margin: logits within 3e-2 of the oracle's, same argmax on >= 95 %
+    of clips, whole-model gradient cosine >= 0.99."""
     d = dev()
     import fall_multimodal_amd as f3
     torch.set_num_threads(min(16, os.cpu_count() or 1))
