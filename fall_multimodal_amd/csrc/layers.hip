@@ -1824,16 +1824,26 @@ __global__ __launch_bounds__(256) void ca_bwd_w_kernel(CaArgs a) {
   float w1[16], w2[16], b2 = 0.f;
 #pragma unroll
   for (int q = 0; q < 16; ++q) w1[q] = w2[q] = 0.f;
-  for (int n = n0; n < n1 && cok; ++n) {
-    const float gap = a.gapsum[(size_t)n * C + c] * a.inv_tv * sc + sh;
-    const float d2 = a.dq2[(size_t)n * C + c];
+  // the group's gapsum / dq2 loads all go out before the sums (one round trip, not one per clip)
+  float gv[kCaWClips], dv[kCaWClips];
+#pragma unroll
+  for (int m = 0; m < kCaWClips; ++m) {
+    const bool ok = cok && n0 + m < n1;
+    gv[m] = ok ? a.gapsum[(size_t)(n0 + m) * C + c] : 0.f;
+    dv[m] = ok ? a.dq2[(size_t)(n0 + m) * C + c] : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < kCaWClips; ++m) {
+    if (!cok || n0 + m >= n1) break;
+    const float gap = gv[m] * a.inv_tv * sc + sh;
+    const float d2 = dv[m];
     b2 += d2;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int j = jg + 4 * q;
       if (j < H) {
-        w1[q] += dq1s[n - n0][j] * gap;
-        w2[q] += d2 * hs[n - n0][j];
+        w1[q] += dq1s[m][j] * gap;
+        w2[q] += d2 * hs[m][j];
       }
     }
   }
@@ -1919,6 +1929,198 @@ __global__ __launch_bounds__(256) void ca_bwd3_kernel(CaArgs a) {
     if (a.bnr_bsum) {
       atomic_add_d(a.bnr_bsum + c, r1);
       atomic_add_d(a.bnr_bsq + c, r2);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Channel attention with the loads of each phase issued up front (N <= 256, C % 64 == 0). The kernels
+// above walk 16-256 long load chains per thread (a W1 / W2 row or column, a gapsum row, one element
+// per iteration): on the main chains the five of them cost ~43 us per layer and stream in the serial
+// step profile (ca_bwd3 alone 16.8 us), latency, not bytes. Here each thread's loads go out together
+// and the sums run from registers / LDS; 1024-thread workgroups, four lanes per row (64-B pieces).
+// ca_bwd3x keeps ca_bwd3's summation order (k sequential per clip, the clips of a workgroup added in
+// clip order before its double atomics).
+// ----------------------------------------------------------------------------
+F3_DEV float block_sum16(float v, float* red) {  // 1024 threads
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += red[i];
+  return s;
+}
+
+// one workgroup per hidden unit j; thread (n, p): clip n, channels 4p + 16i (float4 i)
+__global__ __launch_bounds__(1024) void ca_fwd1x_kernel(CaArgs a) {
+  __shared__ __attribute__((aligned(16))) float w1[256], sc2[256], sh2[256];
+  __shared__ float red[16];
+  const int j = blockIdx.x, C = a.C, H = C / 4, tid = threadIdx.x;
+  const int n = tid >> 2, p = tid & 3, nv = C / 16;
+  const bool live = n < a.N;
+  f32x4 gv[16];
+  const float* gp = a.gapsum + (size_t)(live ? n : 0) * C + 4 * p;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nv) gv[i] = *reinterpret_cast<const f32x4*>(gp + 16 * i);
+  for (int c = tid; c < C; c += 1024) {
+    float mu, rs;
+    bn_coeff(a.bn2, c, sc2[c], sh2[c], mu, rs);
+    w1[c] = a.W1[(size_t)j * C + c];
+  }
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i >= nv) continue;
+    const int c = 4 * p + 16 * i;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += w1[c + e] * (gv[i][e] * a.inv_tv * sc2[c + e] + sh2[c + e]);
+  }
+  q += __shfl_xor(q, 1, 64);
+  q += __shfl_xor(q, 2, 64);
+  q += a.b1[j];
+  const bool own = live && p == 0;
+  const float s = block_sum16(own ? q : 0.f, red);
+  const float mean_b = s / (float)a.N;
+  const float s2 = block_sum16(own ? (q - mean_b) * (q - mean_b) : 0.f, red);
+  const float var_b = s2 / (float)a.N;
+  if (tid == 0 && !a.bnca.eval) {
+    a.ca_sum[j] = (double)mean_b * a.N;
+    a.ca_sq[j] = ((double)var_b + (double)mean_b * mean_b) * a.N;
+  }
+  float mean, rstd;
+  if (a.bnca.eval) {
+    mean = a.bnca.rmean[j];
+    rstd = rsqrtf(a.bnca.rvar[j] + kBnEps);
+  } else {
+    mean = mean_b;
+    rstd = rsqrtf(var_b + kBnEps);
+  }
+  const float gm = a.bnca.gamma[j] * rstd, bt = a.bnca.beta[j] - mean * gm;
+  if (own) {
+    a.q1[(size_t)n * H + j] = q;
+    a.hid[(size_t)n * H + j] = fmaxf(q * gm + bt, 0.f);
+  }
+}
+
+// one workgroup per clip: att = sigmoid(W2 hid + b2); thread (c, p): W2 row c, hidden units 4p + 16i
+__global__ __launch_bounds__(1024) void ca_fwd2x_kernel(CaArgs a) {
+  __shared__ float hs[64];
+  const int n = blockIdx.x, C = a.C, H = C / 4, tid = threadIdx.x;
+  const int c = tid >> 2, p = tid & 3, nv = H / 16;
+  const bool live = c < C;
+  f32x4 wv[4];
+  const float* w = a.W2 + (size_t)(live ? c : 0) * H + 4 * p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < nv) wv[i] = *reinterpret_cast<const f32x4*>(w + 16 * i);
+  if (tid < H) hs[tid] = a.hid[(size_t)n * H + tid];
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= nv) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += wv[i][e] * hs[4 * p + 16 * i + e];
+  }
+  q += __shfl_xor(q, 1, 64);
+  q += __shfl_xor(q, 2, 64);
+  if (live && p == 0) a.att[(size_t)n * C + c] = sigmoidf_(a.b2[c] + q);
+}
+
+// per clip: dq2 = (g2 P2 + b2 P1) a (1 - a); dbn = (W2^T dq2) (hid > 0); thread (r, j) sums channels
+// r + 16i of hidden unit j, the 16 partials added in r order
+__global__ __launch_bounds__(1024) void ca_bwd1x_kernel(CaArgs a) {
+  __shared__ float dq[256];
+  __shared__ float part[16][64];
+  const int n = blockIdx.x, C = a.C, H = C / 4, tid = threadIdx.x;
+  const int j = tid & 63, r = tid >> 6, nci = C / 16;
+  const bool jl = j < H;
+  float wv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nci) wv[i] = jl ? a.W2[(size_t)(r + 16 * i) * H + j] : 0.f;
+  if (tid < C) {
+    const size_t o = (size_t)n * C + tid;
+    const float da = a.bn2.gamma[tid] * a.P2[o] + a.bn2.beta[tid] * a.P1[o];
+    const float at = a.att[o];
+    const float d = da * at * (1.f - at);
+    dq[tid] = d;
+    a.dq2[o] = d;
+  }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nci) acc += dq[r + 16 * i] * wv[i];
+  part[r][j] = acc;
+  __syncthreads();
+  if (tid < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += part[q][tid];
+    a.dbn[(size_t)n * H + tid] = a.hid[(size_t)n * H + tid] > 0.f ? t : 0.f;
+  }
+}
+
+// per 4 clips: dgap = W1^T dq1, e = dgap / TV, BN2 (and residual BN) backward sums; thread (clip nn, c)
+__global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
+  __shared__ float dq[4][64];
+  __shared__ double sred[4][4][256];  // [sum][clip][channel]
+  const int n0 = blockIdx.x * 4, C = a.C, H = C / 4, N = a.N, tid = threadIdx.x;
+  const int nn = tid >> 8, c = tid & 255, n = n0 + nn;
+  const bool cl = c < C, live = cl && n < N;
+  float wk[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k)
+    if (k < H) wk[k] = cl ? a.W1[(size_t)k * C + c] : 0.f;
+  const size_t o = (size_t)(live ? n : 0) * C + (cl ? c : 0);
+  const float at = a.att[o], p1 = a.P1[o], p2 = a.P2[o], gs = a.gapsum[o];
+  const float q2 = a.bnr_bsum ? a.Q2[o] : 0.f;
+  if (tid < 4 * H) {
+    const int m = tid / H, k = tid - m * H;
+    dq[m][k] = n0 + m < N ? a.dq1[(size_t)(n0 + m) * H + k] : 0.f;
+  }
+  __syncthreads();
+  double s1 = 0.0, s2 = 0.0, r1 = 0.0, r2 = 0.0;
+  if (live) {
+    float sc, sh, mu, rs;
+    bn_coeff(a.bn2, c, sc, sh, mu, rs);
+    float dg = 0.f;
+#pragma unroll
+    for (int k = 0; k < 64; ++k)
+      if (k < H) dg += dq[nn][k] * wk[k];
+    a.e[o] = dg * a.inv_tv;
+    const float xsum = (gs - mu / a.inv_tv) * rs;  // sum_tv xhat2
+    s1 = (double)(at * p1 + dg);
+    s2 = (double)(at * p2 + dg * a.inv_tv * xsum);
+    r1 = (double)p1;
+    r2 = (double)q2;
+  }
+  sred[0][nn][c] = s1;
+  sred[1][nn][c] = s2;
+  sred[2][nn][c] = r1;
+  sred[3][nn][c] = r2;
+  __syncthreads();
+  if (nn == 0 && cl) {
+    double t1 = 0.0, t2 = 0.0, u1 = 0.0, u2 = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      if (n0 + m >= N) break;
+      t1 += sred[0][m][c];
+      t2 += sred[1][m][c];
+      u1 += sred[2][m][c];
+      u2 += sred[3][m][c];
+    }
+    atomic_add_d(a.bn2_bsum + c, t1);
+    atomic_add_d(a.bn2_bsq + c, t2);
+    if (a.bnr_bsum) {
+      atomic_add_d(a.bnr_bsum + c, u1);
+      atomic_add_d(a.bnr_bsq + c, u2);
     }
   }
 }
@@ -2432,8 +2634,21 @@ int f3_bnrelu_bf16(const BnReluArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
+// F3_CA_X (default 1): the up-front-load channel-attention kernels where they fit (N <= 256, C % 64 == 0)
+static bool ca_x(const CaArgs* a) {
+  const char* e = getenv("F3_CA_X");  // (read per call: the A/B test flips it in one process)
+  return !(e && atoi(e) == 0) && a->N <= 256 && a->C % 64 == 0;
+}
+
 int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256 * kCaMaxRowsPerThread) return F3_EINVAL;
+  if (ca_x(a)) {
+    hipLaunchKernelGGL(ca_fwd1x_kernel, dim3(a->C / 4), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ca_fwd2x_kernel, dim3(a->N), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   hipLaunchKernelGGL(ca_fwd1_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_fwd2_kernel, dim3(a->N), dim3(256), 0, s, *a);
@@ -2443,6 +2658,15 @@ int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
 
 int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
+  if (ca_x(a)) {
+    hipLaunchKernelGGL(ca_bwd1x_kernel, dim3(a->N), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ca_bwd3x_kernel, dim3((a->N + 3) / 4), dim3(1024), 0, s, *a);
+    F3_LAUNCH_CHECK();
+    return F3_OK;
+  }
   hipLaunchKernelGGL(ca_bwd1_kernel, dim3(a->N), dim3(256), 0, s, *a);
   F3_LAUNCH_CHECK();
   hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);

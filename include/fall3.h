@@ -32,7 +32,7 @@ extern "C" {
 #define F3_EBATCH 1002 /* train-mode batch of 1: BatchNorm needs >1 value per channel */
 #define F3_EHIP 1003   /* HIP launch error */
 #define F3_ESTATE 1004 /* backward without a training forward on this workspace */
-#define F3_EDEVICE 1005 /* a device-side check failed (TARGCN: a GRU group barrier timed out) */
+#define F3_EDEVICE 1005 /* a device-side check failed (a group barrier of the TARGCN GRU or the sensor CNN1D timed out) */
 
 enum { F3_MODEL_TWO_STGCAN_BILSTM = 0, F3_MODEL_TWO_STGCAN = 1, F3_MODEL_STGCN = 2, F3_MODEL_BILSTM = 3 };
 enum { F3_SENSOR_NONE = 0, F3_SENSOR_BILSTM = 1, F3_SENSOR_CNN_BILSTM = 2 };
