@@ -127,6 +127,7 @@ struct BlockArgs {
   // and, conv residual, of dres (its bias), rows [chunks][N][C | C] summed by the caller's colsum; the
   // weight-gradient kernels then run without their in-loop bias sums. null: not written
   float* dbpart;
+  int no_colsum;  // block_bwd_reduce: leave P1 / P2 / Q2 in `part` (ca_bwd1x sums them, CaArgs::bpart)
 };
 
 struct BnBwdArgs {
@@ -191,7 +192,12 @@ struct CaArgs {
   // deterministic weight gradients: per clip-group partial rows [groups][2 H C + C] (g_W1, g_W2, g_b2),
   // summed in group order by f3_colsum; null: float atomics
   float* wpart;
+  // block_bwd_reduce's partial rows [chunks][3][N][C] (BlockArgs::no_colsum): ca_bwd1x sums each clip's
+  // P1 / P2 / Q2 from them in the order f3_colsum uses and writes P1 / P2 / Q2; null: already summed
+  const float* bpart;
+  int bchunks;
 };
+
 
 struct BnRunJob {
   const double* sum;
@@ -257,4 +263,7 @@ int f3_ca_bwd(const f3::CaArgs* a, hipStream_t s);          // input-gradient ch
 // W1/W2/b2 gradients (ca_bwd_w); with `defer`, the three column sums of its partial rows are appended
 // to defer[*ndefer...] (ndefer advanced) for one batched f3_colsum_multi by the caller instead of launched
 int f3_ca_bwd_weights(const f3::CaArgs* a, hipStream_t s, ColsumJob* defer = nullptr, int* ndefer = nullptr);
+// the up-front-load channel-attention kernels apply (N <= 256, C % 64 == 0, F3_CA_X != 0) and can take
+// block_bwd_reduce's partial rows of a T*V frame (chunks <= 16)
+bool f3_ca_x_ok(int N, int C, int TV);
 int f3_bn_running(const f3::BnRunTable& t, hipStream_t s);

@@ -2032,6 +2032,19 @@ __global__ __launch_bounds__(1024) void ca_fwd2x_kernel(CaArgs a) {
   if (live && p == 0) a.att[(size_t)n * C + c] = sigmoidf_(a.b2[c] + q);
 }
 
+// sum of `rows` (<= 16) partial rows `ld` floats apart in colsum_kernel's order for such a column (row
+// groups of the largest power of two <= rows, each group's rows in order, the groups in order, onto 0)
+F3_DEV float colsum_few(const float* p, long long ld, int rows) {
+  const int RG = rows >= 16 ? 16 : rows >= 8 ? 8 : rows >= 4 ? 4 : rows >= 2 ? 2 : 1;
+  float t = 0.f;
+  for (int g = 0; g < RG; ++g) {
+    float s0 = 0.f;
+    for (int r = g; r < rows; r += RG) s0 += p[(size_t)r * ld];
+    t += (s0 + 0.f) + (0.f + 0.f);
+  }
+  return 0.f + t;
+}
+
 // per clip: dq2 = (g2 P2 + b2 P1) a (1 - a); dbn = (W2^T dq2) (hid > 0); thread (r, j) sums channels
 // r + 16i of hidden unit j, the 16 partials added in r order
 __global__ __launch_bounds__(1024) void ca_bwd1x_kernel(CaArgs a) {
@@ -2046,7 +2059,19 @@ __global__ __launch_bounds__(1024) void ca_bwd1x_kernel(CaArgs a) {
     if (i < nci) wv[i] = jl ? a.W2[(size_t)(r + 16 * i) * H + j] : 0.f;
   if (tid < C) {
     const size_t o = (size_t)n * C + tid;
-    const float da = a.bn2.gamma[tid] * a.P2[o] + a.bn2.beta[tid] * a.P1[o];
+    float p1, p2;
+    if (a.bpart) {  // this clip's block sums from block_bwd_reduce's partial rows (no colsum launch)
+      const long long nc = (long long)a.N * C, ld = 3 * nc;
+      p1 = colsum_few(a.bpart + o, ld, a.bchunks);
+      p2 = colsum_few(a.bpart + nc + o, ld, a.bchunks);
+      const_cast<float*>(a.P1)[o] = p1;
+      const_cast<float*>(a.P2)[o] = p2;
+      if (a.bnr_bsum) const_cast<float*>(a.Q2)[o] = colsum_few(a.bpart + 2 * nc + o, ld, a.bchunks);
+    } else {
+      p1 = a.P1[o];
+      p2 = a.P2[o];
+    }
+    const float da = a.bn2.gamma[tid] * p2 + a.bn2.beta[tid] * p1;
     const float at = a.att[o];
     const float d = da * at * (1.f - at);
     dq[tid] = d;
@@ -2531,7 +2556,7 @@ int f3_block_bwd_reduce(BlockArgs a, hipStream_t s) {
   if (a.res_kind < RES_NONE || a.res_kind > RES_CONV) return F3_EINVAL;
   launch_block_bwd<true>(a, s);
   F3_LAUNCH_CHECK();
-  if (!a.part) return F3_OK;
+  if (!a.part || a.no_colsum) return F3_OK;
   const int nc = a.N * a.C, nseg = a.res_kind == RES_CONV ? 3 : 2;
   if (a.P2 == a.P1 + nc && (nseg == 2 || a.Q2 == a.P1 + 2 * nc))  // contiguous [P1 | P2 | Q2]: one launch
     return f3_colsum_ld(a.part, a.chunks, 3LL * nc, nseg * nc, a.P1, s);
@@ -2640,6 +2665,13 @@ static bool ca_x(const CaArgs* a) {
   return !(e && atoi(e) == 0) && a->N <= 256 && a->C % 64 == 0;
 }
 
+bool f3_ca_x_ok(int N, int C, int TV) {
+  CaArgs a;
+  a.N = N;
+  a.C = C;
+  return ca_x(&a) && f3_block_chunks(TV) <= 16;
+}
+
 int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256 * kCaMaxRowsPerThread) return F3_EINVAL;
   if (ca_x(a)) {
@@ -2658,6 +2690,7 @@ int f3_ca_fwd(const CaArgs* a, hipStream_t s) {
 
 int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   if (a->C > 256 || a->N > 256) return F3_EINVAL;
+  if (a->bpart && (!ca_x(a) || a->bchunks < 1 || a->bchunks > 16)) return F3_EINVAL;  // (f3_ca_x_ok decides)
   if (ca_x(a)) {
     hipLaunchKernelGGL(ca_bwd1x_kernel, dim3(a->N), dim3(1024), 0, s, *a);
     F3_LAUNCH_CHECK();

@@ -828,7 +828,11 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ba.dgamma2 = q.g(L.bn2.w); ba.dbeta2 = q.g(L.bn2.b);
     if (L.res == RES_CONV) { ba.dgammar = q.g(L.bnr.w); ba.dbetar = q.g(L.bnr.b); }
     ba.part = W.detm;
+    // the block sums P1 / P2 / Q2 summed by ca_bwd1x from the partial rows (one launch less per layer)
+    const bool ca_sums = f3_ca_x_ok(N, C, To * V);
+    ba.no_colsum = ca_sums;
     if (part & 1) F3_TRY(f3_block_bwd_reduce(ba, s));
+    ba.no_colsum = 0;
     ba.dbpart = x3 ? X.dbpart : nullptr;  // (block_bwd_apply only: the bias-gradient rows)
     CaArgs ca;
     std::memset(&ca, 0, sizeof(ca));
@@ -841,6 +845,7 @@ int stream_backward(const f3_net& net, int si, int N, const Ptrs& q, Ws& w, cons
     ca.bn2_bsum = X.bn2.bsum; ca.bn2_bsq = X.bn2.bsq;
     ca.g_bnca_gamma = q.g(L.bnca.w); ca.g_bnca_beta = q.g(L.bnca.b);
     ca.g_b1 = q.g(L.ca_b1); ca.g_W1 = q.g(L.ca_w1); ca.g_W2 = q.g(L.ca_w2); ca.g_b2 = q.g(L.ca_b2);
+    if (ca_sums) { ca.bpart = W.detm; ca.bchunks = f3_block_chunks(To * V); }
     if (part & 1) F3_TRY(f3_ca_bwd(&ca, s));  // the W1/W2 gradients (ca_bwd_w) go to the side stream
     if (part & 1) F3_TRY(f3_block_bwd_apply(ba, s));
     // (Starting the tcn / residual / CA weight gradients right after block_bwd_apply instead of after
