@@ -2092,13 +2092,93 @@ __global__ __launch_bounds__(1024) void ca_bwd1x_kernel(CaArgs a) {
   }
 }
 
-// per 4 clips: dgap = W1^T dq1, e = dgap / TV, BN2 (and residual BN) backward sums; thread (clip nn, c)
+// per 4 clips: dgap = W1^T dq1, e = dgap / TV, BN2 (and residual BN) backward sums; thread (clip nn, c).
+// FUSE2: ca_bwd2's attention-BN backward folded in. Every workgroup sums s1 = sum_n dbn and
+// s2 = sum_n dbn xhat over all clips for each hidden unit (thread (r, j): clips r + 16i; the 16 partials
+// added in r order), forms its own clips' dq1 rows (written for ca_bwd_w), and workgroup 0 adds the
+// attention BN's gamma / beta and b1 gradients: one main-chain launch less per layer.
+template <bool FUSE2>
 __global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
   __shared__ float dq[4][64];
   __shared__ double sred[4][4][256];  // [sum][clip][channel]
   const int n0 = blockIdx.x * 4, C = a.C, H = C / 4, N = a.N, tid = threadIdx.x;
   const int nn = tid >> 8, c = tid & 255, n = n0 + nn;
   const bool cl = c < C, live = cl && n < N;
+  if constexpr (FUSE2) {
+    __shared__ float ps[2][16][64];
+    __shared__ float s12[2][64], kk[64], mu[64], rsd[64];
+    const int j = tid & 63, r = tid >> 6;
+    const bool jl = j < H;
+    float mean = 0.f, rstd = 0.f;
+    if (jl) {
+      const double md = a.ca_sum[j] / N;
+      mean = (float)md;
+      const float var = (float)fmax(a.ca_sq[j] / N - md * md, 0.0);  // double: see ca_fwd1
+      rstd = rsqrtf(var + kBnEps);
+    }
+    float dv[16], xv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = r + 16 * i;
+      const bool ok = jl && m < N;
+      dv[i] = ok ? a.dbn[(size_t)m * H + j] : 0.f;
+      xv[i] = ok ? a.q1[(size_t)m * H + j] : 0.f;
+    }
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      xv[i] = (xv[i] - mean) * rstd;
+      t1 += dv[i];
+      t2 += dv[i] * xv[i];
+    }
+    ps[0][r][j] = t1;
+    ps[1][r][j] = t2;
+    if (r == 0) {
+      kk[j] = jl ? a.bnca.gamma[j] * rstd : 0.f;
+      mu[j] = mean;
+      rsd[j] = rstd;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float u1 = 0.f, u2 = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        u1 += ps[0][g][tid];
+        u2 += ps[1][g][tid];
+      }
+      s12[0][tid] = u1;
+      s12[1][tid] = u2;
+    }
+    __syncthreads();
+    if (tid < 4 * H) {  // this workgroup's clips' dq1 rows
+      const int m = tid / H, k = tid - m * H;
+      float v = 0.f;
+      if (n0 + m < N) {
+        const size_t q = (size_t)(n0 + m) * H + k;
+        const float xh = (a.q1[q] - mu[k]) * rsd[k];
+        v = kk[k] * (a.dbn[q] - s12[0][k] / N - xh * s12[1][k] / N);
+        a.dq1[q] = v;
+      }
+      dq[m][k] = v;
+    }
+    if (blockIdx.x == 0) {  // (uniform) the attention BN's gamma / beta and b1 gradients
+      const float S1 = s12[0][j], S2 = s12[1][j], kj = kk[j];
+      float t3 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (jl && r + 16 * i < N) t3 += kj * (dv[i] - S1 / N - xv[i] * S2 / N);
+      ps[0][r][j] = t3;  // (ps[0] was last read before the barrier above)
+      __syncthreads();
+      if (tid < H) {
+        float u = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) u += ps[0][g][tid];
+        a.g_bnca_gamma[tid] += s12[1][tid];
+        a.g_bnca_beta[tid] += s12[0][tid];
+        a.g_b1[tid] += u;
+      }
+    }
+  }
   float wk[64];
 #pragma unroll
   for (int k = 0; k < 64; ++k)
@@ -2106,7 +2186,7 @@ __global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
   const size_t o = (size_t)(live ? n : 0) * C + (cl ? c : 0);
   const float at = a.att[o], p1 = a.P1[o], p2 = a.P2[o], gs = a.gapsum[o];
   const float q2 = a.bnr_bsum ? a.Q2[o] : 0.f;
-  if (tid < 4 * H) {
+  if (!FUSE2 && tid < 4 * H) {
     const int m = tid / H, k = tid - m * H;
     dq[m][k] = n0 + m < N ? a.dq1[(size_t)(n0 + m) * H + k] : 0.f;
   }
@@ -2665,6 +2745,12 @@ static bool ca_x(const CaArgs* a) {
   return !(e && atoi(e) == 0) && a->N <= 256 && a->C % 64 == 0;
 }
 
+// F3_CA_X=1: the x kernels with ca_bwd2 as its own launch (A/B); unset or 2: ca_bwd2 folded into ca_bwd3x
+static bool ca_fuse2() {
+  const char* e = getenv("F3_CA_X");
+  return !(e && atoi(e) == 1);
+}
+
 bool f3_ca_x_ok(int N, int C, int TV) {
   CaArgs a;
   a.N = N;
@@ -2694,9 +2780,14 @@ int f3_ca_bwd(const CaArgs* a, hipStream_t s) {
   if (ca_x(a)) {
     hipLaunchKernelGGL(ca_bwd1x_kernel, dim3(a->N), dim3(1024), 0, s, *a);
     F3_LAUNCH_CHECK();
+    if (ca_fuse2()) {
+      hipLaunchKernelGGL(ca_bwd3x_kernel<true>, dim3((a->N + 3) / 4), dim3(1024), 0, s, *a);
+      F3_LAUNCH_CHECK();
+      return F3_OK;
+    }
     hipLaunchKernelGGL(ca_bwd2_kernel, dim3(a->C / 4), dim3(256), 0, s, *a);
     F3_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ca_bwd3x_kernel, dim3((a->N + 3) / 4), dim3(1024), 0, s, *a);
+    hipLaunchKernelGGL(ca_bwd3x_kernel<false>, dim3((a->N + 3) / 4), dim3(1024), 0, s, *a);
     F3_LAUNCH_CHECK();
     return F3_OK;
   }

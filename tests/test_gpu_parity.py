@@ -1395,7 +1395,8 @@ def test_custom_ops_opcheck():
 @pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 def test_ca_x_kernels_match_chain_kernels(precision, monkeypatch):
     """The channel-attention kernels with up-front loads (layers.hip ca_fwd1x / ca_fwd2x / ca_bwd1x /
-    ca_bwd3x, F3_CA_X=1, the default) against the load-chain kernels they replace (F3_CA_X=0), inside
+    ca_bwd3x with ca_bwd2 folded in, F3_CA_X unset or 2, the default) against the load-chain kernels
+    they replace (F3_CA_X=0), inside
     a B=256 training step of the 3-stream model (stgcan.py:59-74): logits within 1e-5 of max, the
     flattened gradients at cosine >= 0.999999, every gradient tensor within 5e-2 of its max, and the
     BN running statistics within 1e-5. The per-tensor bound is loose on purpose. The q1 / dhid / att
@@ -1410,7 +1411,7 @@ def test_ca_x_kernels_match_chain_kernels(precision, monkeypatch):
     st = oc.init_state(spec, 5)
     batch = [torch.from_numpy(x).to(d) for x in synthetic_batch(B, V, 11, S, 41)]
     res = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "2"):  # 2 (= unset): the default, ca_bwd2 folded into ca_bwd3x
         monkeypatch.setenv("F3_CA_X", mode)
         model = f3.TwoStreamSTGCAN_BiLSTM(3, {"layout": "coco_mmpose", "strategy": "spatial"}, 11, S, device=d,
                                           precision=precision)
@@ -1422,7 +1423,7 @@ def test_ca_x_kernels_match_chain_kernels(precision, monkeypatch):
                      {n: p.grad.detach().cpu().double() for n, p in model.named_parameters()},
                      {k: v.detach().cpu().double() for k, v in model.state_dict().items() if "running" in k})
     o0, g0, b0 = res["0"]
-    o1, g1, b1 = res["1"]
+    o1, g1, b1 = res["2"]
     assert float((o1 - o0).abs().max()) <= 1e-5 * float(o0.abs().max())
     worst, gmax = 0.0, max(float(g.abs().max()) for g in g0.values())
     a0 = torch.cat([g.reshape(-1) for g in g0.values()])
