@@ -33,7 +33,7 @@ KERNELS = {"wgrad_l1": ["wgrad_big<2, 4, 2, 1, 32, 1, 3, true", _RED],
            "wgrad_l5": ["wgrad_big<4, 2, 4, 4, 32, 1, 3, true", _RED],
            "wgrad": ["wgrad_taps<5", "wgrad_taps_reduce_kernel"],
            "wgrad_kernel": ["wgrad_taps<5"],
-           "tcn_fwd": ["igemm_big<1, 2, 4, 144"]}
+           "tcn_fwd": ["igemm_win1<1, 2, 4, 144"]}
 
 
 def run(key):
