@@ -23,7 +23,9 @@
 #include <type_traits>
 
 // F3_PROBE (tools/probe_build.sh only; 0 in the library): bit 1 drops the window loop's MFMAs, bit 2
-// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone. (A static
+// its weight / A-carry DMAs, bit 4 its LDS fragment reads — the bound each leg sets alone; bit 8 drops
+// igemm_win1's per-step s_barrier, bit 16 its epilogue (timing only, results wrong; bits 1, 2, 4 apply
+// to igemm_win1 too). (A static
 // issue priority for waves 4-7, MI355X_MICROARCH.md "two waves per SIMD" item 4, measured within
 // noise on l1d / l5d / l8d / l8f: profiles/r05_window_prio_ab.txt.) (Measured
 // on l8d with this loop: 126 us full, 77 without MFMA, 55 without MFMA and DMA: the legs add up almost
@@ -918,7 +920,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
       for (int J = 0; J < NS; ++J) {  // unrolled: the schedule below folds to constants per step
         const int JS = (J + LA) % NS, CS = (J + LA) / NS;  // the step staged now: (c + CS, JS)
         const bool issue = CS == 0 || more;
-        if (issue) stage(JS, c + CS);
+        if (issue && !(F3_PROBE & 2)) stage(JS, c + CS);
         const unsigned wrow = lds0 + (NQ == 2 ? S::q(J) : (c & 1)) * Cfg::AWIN + (unsigned)cbase * 128;
         const int t = opaque_v(lo0 + fr) + (MODE == 0 ? ss * S::shift(J) : S::shift(J)) * V;  // tap-shifted row
         const unsigned rb = wrow + (unsigned)t * 128;
@@ -928,11 +930,12 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-          for (int y = 0; y < BG_NT; ++y) f[ks][y] = lds_rd128(boffr[ks][y] + soff);
+          for (int y = 0; y < BG_NT; ++y)
+            f[ks][y] = (F3_PROBE & 4) ? u32x4_t{0u, 0u, 0u, 0u} : lds_rd128(boffr[ks][y] + soff);
 #define F3_AREAD1(X)                                                                                 \
   {                                                                                                  \
     const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X); \
-    f[ks][BG_NT + (X)] = lds_rd128o<2048 * (X)>(ad);                                                 \
+    f[ks][BG_NT + (X)] = (F3_PROBE & 4) ? u32x4_t{ad, 0u, 0u, 0u} : lds_rd128o<2048 * (X)>(ad);        \
   }
           F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6) F3_AREAD1(7)
           F3_AREAD1(8)
@@ -948,6 +951,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
           for (int x = 0; x < BG_MT; ++x)
 #pragma unroll
             for (int y = 0; y < BG_NT; ++y) {
+              if (F3_PROBE & 1) {  // probe build: fragments consumed, no MFMA
+                acc[x][y][0] += __builtin_bit_cast(float, f[ks][BG_NT + x][0] ^ f[ks][y][1]);
+                continue;
+              }
               // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order)
               acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
                                      acc[x][y]);
@@ -966,11 +973,15 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
         // (the step after next) stay in flight
         if (LA == 2 && issue) wait_vm<DPS>();
         else wait_vm<0>();
-        __builtin_amdgcn_s_barrier();
+        if (!(F3_PROBE & 8)) __builtin_amdgcn_s_barrier();
       }
     }
     __syncthreads();
     auto none = [](int) { return -1; };
+    if (F3_PROBE & 16) {  // probe build: no epilogue (one word per wave keeps the loop alive)
+      if (lane == 0) a.out[blockIdx.x * NW + wave] = acc[0][0][0] + acc[BG_MT - 1][BG_NT - 1][3];
+      return;
+    }
     big_epilogue<EPI, WM, WN, WIN>(a, acc, smem, n0, clip0, nclip, MODE, wpar, 0, none);
 }
 
