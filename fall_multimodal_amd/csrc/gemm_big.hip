@@ -786,21 +786,30 @@ struct WinSched {
 // constants; a wave issues its weight pieces plus ASL A-carry pieces per step (a slot with nothing to
 // carry sinks the zero row, so the vmcnt count stays one constant). LDS layout, fragment reads, MFMA
 // order and the epilogue are igemm_big's, so the two forms give bit-identical results.
-template <int EPI, int WM, int WN, int WIN, int MODE, int NTP = 5>
+//
+// PP (ping-pong, F3_WIN1_PP=1): the two waves of a SIMD (wave w and w + NW/2) run in opposite phases, so
+// one wave's fragment reads overlap the other's MFMAs (the probe builds found the two legs serialised,
+// DESIGN.md §4.13). Every wave runs the same sequence per step, read | barrier | multiply | barrier;
+// group B (waves NW/2 ..) starts one barrier late and skips the last one. Only group A issues the
+// weight / carry DMAs (twice the pieces per wave), and every wave completes its reads (lgkmcnt 0)
+// before the barrier that ends its read phase, so a stage is refilled only after both groups have
+// read it. Each wave issues the same MFMAs in the same order as the plain form: bit-identical results.
+template <int EPI, int WM, int WN, int WIN, int MODE, int NTP = 5, bool PP = false>
 __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
   using Cfg = BigCfg<WM, WN, WIN>;
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int KT = 9, CL = WIN;
   constexpr int BN = Cfg::BN, STAGE = Cfg::STAGE, NST = Cfg::NST, LA = Cfg::LA, CPW = Cfg::CPW, NPA = Cfg::NPA;
-  constexpr int BSL = Cfg::BP / NW;                               // weight pieces per wave and step
+  constexpr int NWS = PP ? NW / 2 : NW;                           // staging waves (PP: group A)
+  constexpr int BSL = Cfg::BP / NWS;                              // weight pieces per wave and step
   constexpr int NQ = MODE == 2 ? 2 : 1;                           // windows per chunk
   // carry pieces per step: a window is carried by the LA.. steps of the window before it and that
   // window's step 0 (the last group): ntq - LA + 1 groups of aps pieces
   constexpr int APS_MAX = MODE == 0 ? (NPA + (KT - LA)) / (KT - LA + 1) : (NPA + (4 - LA)) / (4 - LA + 1);
-  constexpr int ASL = (APS_MAX + NW - 1) / NW;                    // A slots per wave and step
+  constexpr int ASL = (APS_MAX + NWS - 1) / NWS;                  // A slots per wave and step
   constexpr int DPS = BSL + ASL;                                  // DMAs per wave and step
   constexpr int A0W = (NPA + NW - 1) / NW;                        // window 0's pieces per wave
-  static_assert(Cfg::BP % NW == 0 && (LA == 1 || LA == 2) && (MODE == 0 || LA == 2), "win1 staging");
+  static_assert(Cfg::BP % NWS == 0 && (LA == 1 || LA == 2) && (MODE == 0 || LA == 2), "win1 staging");
   static_assert(Cfg::SMEM <= 160 * 1024 && (NST - 1) * DPS < 64, "LDS / vmcnt");
   __shared__ __attribute__((aligned(16))) char smem[Cfg::SMEM];
   const ConvGeom& g = a.g;
@@ -834,7 +843,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
   const unsigned short* bsrc[BSL];
 #pragma unroll
   for (int i = 0; i < BSL; ++i) {
-    const int r = (wave + NW * i) * 8 + sub;
+    const int r = ((PP ? wave % NWS : wave) + NWS * i) * 8 + sub;  // (PP: group B never stages)
     bsrc[i] = wb + (size_t)(n0 + r) * Ktot + swz(r, pch) * 8;
   }
   // window row R (= piece * 8 + sub) of chunk c, window q: clip row l of clip clip0 + k
@@ -857,7 +866,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
 #pragma unroll
       for (int i = 0; i < BSL; ++i) {
         const void* wsrc = bsrc[i] + k0;
-        __builtin_amdgcn_global_load_lds(wsrc, (lds_void_t*)(sbase + (wave + NW * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(wsrc, (lds_void_t*)(sbase + (wave + NWS * i) * 1024), 16, 0, 0);
       }
       // target window (tc, tq), group kk, pieces per group na; carry == false: sink
       const bool NEXT = JJ >= LA, OWN = JJ == 0;
@@ -872,9 +881,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
       for (int s2 = 0; s2 < ASL; ++s2) {
         const void* src = a.zero;
         char* dst = smem + Cfg::DOFF;
-        const int sl = wave + NW * s2, pa = KK * NA + sl;
+        const int sl = wave + NWS * s2, pa = KK * NA + sl;
         if (car && sl < NA && pa < NPA) {
-          src = asrc(tc, TQ, opaque_v(wave * 8 + sub) + (KK * NA + NW * s2) * 8);
+          src = asrc(tc, TQ, opaque_v(wave * 8 + sub) + (KK * NA + NWS * s2) * 8);
           dst = smem + (NQ == 2 ? TQ : (tc & 1)) * Cfg::AWIN + pa * 1024;
         }
         __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
@@ -887,10 +896,13 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
       const void* src = asrc(0, 0, pa * 8 + sub);
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(smem + pa * 1024), 16, 0, 0);
     }
-    stage(0, 0);
-    if constexpr (LA == 2) stage(1, 0);
+    const bool grpB = PP && wave >= NWS;
+    if (!grpB) {
+      stage(0, 0);
+      if constexpr (LA == 2) stage(1, 0);
+    }
     if (tid < 8) *reinterpret_cast<f32x4*>(smem + Cfg::ZOFF + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (LA == 2) wait_vm<DPS>();
+    if (LA == 2 && !grpB) wait_vm<DPS>();
     else wait_vm<0>();
     wait_lgkm<0>();
     __builtin_amdgcn_s_barrier();
@@ -914,60 +926,71 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
       }
     // the wave's rows: clip base row in the window and first output row of the clip
     const int cbase = CPW == 2 ? wm * 144 : 0, lo0 = CPW == 2 ? 0 : wm * 144;
+    u32x4_t f[2][BG_NT + BG_MT];
+    if (grpB) __builtin_amdgcn_s_barrier();  // PP: group B runs one phase behind
+#define F3_W1_READS                                                                                  \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                 \
+    _Pragma("unroll") for (int y = 0; y < BG_NT; ++y)                                                \
+      f[ks][y] = (F3_PROBE & 4) ? u32x4_t{0u, 0u, 0u, 0u} : lds_rd128(boffr[ks][y] + soff);           \
+    F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6)       \
+    F3_AREAD1(7) F3_AREAD1(8)                                                                        \
+  }
+#define F3_AREAD1(X)                                                                                 \
+  {                                                                                                  \
+    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X); \
+    f[ks][BG_NT + (X)] = (F3_PROBE & 4) ? u32x4_t{ad, 0u, 0u, 0u} : lds_rd128o<2048 * (X)>(ad);        \
+  }
+#define F3_W1_MFMAS                                                                                  \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                 \
+    if (ks == 0) wait_lgkm<BG_NT + BG_MT>();                                                         \
+    else wait_lgkm<0>();                                                                             \
+    _Pragma("unroll") for (int qq = 0; qq < BG_NT + BG_MT; ++qq) pin_v(f[ks][qq]);                   \
+    _Pragma("unroll") for (int x = 0; x < BG_MT; ++x)                                                \
+      _Pragma("unroll") for (int y = 0; y < BG_NT; ++y) {                                            \
+        if (F3_PROBE & 1) { /* probe build: fragments consumed, no MFMA */                           \
+          acc[x][y][0] += __builtin_bit_cast(float, f[ks][BG_NT + x][0] ^ f[ks][y][1]);              \
+          continue;                                                                                  \
+        }                                                                                            \
+        /* half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order) */                   \
+        acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]), \
+                               acc[x][y]);                                                           \
+        if (ks == 1)                                                                                 \
+          acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]),                        \
+                                 __builtin_bit_cast(bf16x8, f[1][y]), acc[x][y]);                    \
+      }                                                                                              \
+    if (ks == 0) {                                                                                   \
+      _Pragma("unroll") for (int x = 0; x < BG_MT; ++x)                                              \
+        _Pragma("unroll") for (int y = 0; y < BG_NT; ++y) pin_v(acc[x][y]);                          \
+    }                                                                                                \
+  }
     for (int c = 0; c < kpt; ++c) {
       const bool more = c + 1 < kpt;
 #pragma unroll
       for (int J = 0; J < NS; ++J) {  // unrolled: the schedule below folds to constants per step
         const int JS = (J + LA) % NS, CS = (J + LA) / NS;  // the step staged now: (c + CS, JS)
         const bool issue = CS == 0 || more;
-        if (issue && !(F3_PROBE & 2)) stage(JS, c + CS);
         const unsigned wrow = lds0 + (NQ == 2 ? S::q(J) : (c & 1)) * Cfg::AWIN + (unsigned)cbase * 128;
         const int t = opaque_v(lo0 + fr) + (MODE == 0 ? ss * S::shift(J) : S::shift(J)) * V;  // tap-shifted row
         const unsigned rb = wrow + (unsigned)t * 128;
         const unsigned ab0 = rb + ((fg ^ (t & 7)) << 4), ab1 = rb + (((4 + fg) ^ (t & 7)) << 4);
         const unsigned soff = ((c * (NS % NST) + J) % NST) * STAGE;
-        u32x4_t f[2][BG_NT + BG_MT];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-          for (int y = 0; y < BG_NT; ++y)
-            f[ks][y] = (F3_PROBE & 4) ? u32x4_t{0u, 0u, 0u, 0u} : lds_rd128(boffr[ks][y] + soff);
-#define F3_AREAD1(X)                                                                                 \
-  {                                                                                                  \
-    const unsigned ad = (unsigned)(t + 16 * (X)) < (unsigned)CL ? (ks ? ab1 : ab0) : zrow - 2048u * (X); \
-    f[ks][BG_NT + (X)] = (F3_PROBE & 4) ? u32x4_t{ad, 0u, 0u, 0u} : lds_rd128o<2048 * (X)>(ad);        \
-  }
-          F3_AREAD1(0) F3_AREAD1(1) F3_AREAD1(2) F3_AREAD1(3) F3_AREAD1(4) F3_AREAD1(5) F3_AREAD1(6) F3_AREAD1(7)
-          F3_AREAD1(8)
-#undef F3_AREAD1
-        }
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          if (ks == 0) wait_lgkm<BG_NT + BG_MT>();
-          else wait_lgkm<0>();
-#pragma unroll
-          for (int qq = 0; qq < BG_NT + BG_MT; ++qq) pin_v(f[ks][qq]);
-#pragma unroll
-          for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-            for (int y = 0; y < BG_NT; ++y) {
-              if (F3_PROBE & 1) {  // probe build: fragments consumed, no MFMA
-                acc[x][y][0] += __builtin_bit_cast(float, f[ks][BG_NT + x][0] ^ f[ks][y][1]);
-                continue;
-              }
-              // half 0: x_hi W_hi; half 1: x_lo W_hi + x_hi W_lo (igemm_big's order)
-              acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[ks][BG_NT + x]), __builtin_bit_cast(bf16x8, f[0][y]),
-                                     acc[x][y]);
-              if (ks == 1)
-                acc[x][y] = mfma_bf16x(__builtin_bit_cast(bf16x8, f[0][BG_NT + x]),
-                                       __builtin_bit_cast(bf16x8, f[1][y]), acc[x][y]);
-            }
-          if (ks == 0) {
-#pragma unroll
-            for (int x = 0; x < BG_MT; ++x)
-#pragma unroll
-              for (int y = 0; y < BG_NT; ++y) pin_v(acc[x][y]);
+        if constexpr (PP) {
+          // read | barrier | multiply | barrier (group B one phase behind group A)
+          if (!grpB && issue && !(F3_PROBE & 2)) stage(JS, c + CS);
+          F3_W1_READS
+          wait_lgkm<0>();
+          __builtin_amdgcn_s_barrier();
+          F3_W1_MFMAS
+          if (!grpB) {
+            if (LA == 2 && issue) wait_vm<DPS>();
+            else wait_vm<0>();
           }
+          if (!(grpB && J == NS - 1 && !more) && !(F3_PROBE & 8)) __builtin_amdgcn_s_barrier();
+          continue;
+        } else {
+          if (issue && !(F3_PROBE & 2)) stage(JS, c + CS);
+          F3_W1_READS
+          F3_W1_MFMAS
         }
         // the step staged LA ahead must land before its compute: with LA = 2 this step's own DMAs
         // (the step after next) stay in flight
@@ -976,6 +999,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_win1(ConvGemmArgs a) {
         if (!(F3_PROBE & 8)) __builtin_amdgcn_s_barrier();
       }
     }
+#undef F3_W1_READS
+#undef F3_AREAD1
+#undef F3_W1_MFMAS
     __syncthreads();
     auto none = [](int) { return -1; };
     if (F3_PROBE & 16) {  // probe build: no epilogue (one word per wave keeps the loop alive)
@@ -1068,18 +1094,30 @@ static bool win1_enabled(int mode) {
   return mode == 0 ? v >= 1 : v >= 2;
 }
 
+// F3_WIN1_PP=1 (A/B; read per call): the ping-pong form of igemm_win1
+static bool win1_pp() {
+  const char* e = getenv("F3_WIN1_PP");
+  return e && atoi(e) == 1;
+}
+
+template <int E, int WM, int WN, int CL, bool PP>
+static void launch_win1_pp(const ConvGemmArgs& a, int mode, int tiles, hipStream_t s) {
+  if constexpr (CL == 540) {  // (64-channel layers: stride 1 only)
+    hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0, 5, PP>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0, 5, PP>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+    else if (mode == 1) {  // one launch per output-frame parity (5 / 4 taps: a compile-time schedule each)
+      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 5, PP>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
+      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 4, PP>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
+    }
+    else hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 2, 5, PP>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
+  }
+}
+
 template <int E, int WM, int WN, int CL>
 static void launch_win1(const ConvGemmArgs& a, int mode, int tiles, hipStream_t s) {
-  if constexpr (CL == 540) {  // (64-channel layers: stride 1 only)
-    hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
-  } else {
-    if (mode == 0) hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 0>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
-    else if (mode == 1) {  // one launch per output-frame parity (5 / 4 taps: a compile-time schedule each)
-      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 5>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
-      hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 1, 4>), dim3(tiles / 2), dim3(64 * WM * WN), 0, s, a);
-    }
-    else hipLaunchKernelGGL((igemm_win1<E, WM, WN, CL, 2>), dim3(tiles), dim3(64 * WM * WN), 0, s, a);
-  }
+  if (win1_pp()) launch_win1_pp<E, WM, WN, CL, true>(a, mode, tiles, s);
+  else launch_win1_pp<E, WM, WN, CL, false>(a, mode, tiles, s);
 }
 
 template <int CL, bool W4 = false>

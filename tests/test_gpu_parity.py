@@ -227,7 +227,7 @@ def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
     frames (forward)) against igemm_big's run-time schedule (F3_WIN1=0): the same staged bytes,
     fragment reads and MFMA order, so forward (bias epilogue), input gradient and, at stride 1, the
     step's RELUMASK input gradient (with its BN1-backward sums) must agree bit for bit, on ragged clip
-    counts (odd N at two clips per workgroup) and T = 29."""
+    counts (odd N at two clips per workgroup) and T = 29. The ping-pong form (F3_WIN1_PP=1) too."""
     d = dev()
     import fall_multimodal_amd._lib as L
     lib, st = L.lib(), L.stream_handle()
@@ -272,11 +272,15 @@ def test_win1_matches_runtime_tap_schedule_bitwise(shape, monkeypatch):
         return y, dx, dv
 
     new = run()
+    monkeypatch.setenv("F3_WIN1_PP", "1")  # the ping-pong form: the same MFMAs in the same order per wave
+    pp = run()
+    monkeypatch.delenv("F3_WIN1_PP")
     monkeypatch.setenv("F3_WIN1", "0")
     old = run()
-    for name, p, q in zip(("y", "dx", "dv"), new, old):
+    for name, p, q, r in zip(("y", "dx", "dv"), new, old, pp):
         assert torch.isfinite(p).all(), name
         assert torch.equal(p, q), (name, float((p - q).abs().max()))
+        assert torch.equal(r, p), ("ping-pong " + name, float((r - p).abs().max()))
 
 
 @pytest.mark.parametrize("shape", [(3, 15, 18, 384, 256, 1), (3, 8, 18, 768, 256, 1), (2, 15, 14, 128, 256, 2),
