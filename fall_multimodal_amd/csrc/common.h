@@ -41,6 +41,51 @@ F3_DEV void bn_coeff(const BnRef& b, int c, float& scale, float& shift, float& m
   shift = b.beta[c] - mean * scale;
 }
 
+// bn_coeff of channels c0 .. c0 + 3 with every load issued before any use (the per-channel calls
+// in a row were a chain of dependent round trips ahead of the streaming kernels' first loads);
+// the same arithmetic per channel, so bit-identical to four bn_coeff calls
+F3_DEV void bn_coeff4(const BnRef& b, int c0, float* scale, float* shift, float* mean, float* rstd) {
+  float g[4], be[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    g[e] = b.gamma[c0 + e];
+    be[e] = b.beta[c0 + e];
+  }
+  if (b.eval) {
+    float rm[4], rv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      rm[e] = b.rmean[c0 + e];
+      rv[e] = b.rvar[c0 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      mean[e] = rm[e];
+      rstd[e] = rsqrtf(rv[e] + kBnEps);
+    }
+  } else {
+    double sm[4], sq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sm[e] = b.sum[c0 + e];
+      sq[e] = b.sumsq[c0 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      double m = sm[e] / (double)b.count;
+      double v = sq[e] / (double)b.count - m * m;
+      if (v < 0) v = 0;
+      mean[e] = (float)m;
+      rstd[e] = (float)(1.0 / sqrt(v + (double)kBnEps));
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    scale[e] = g[e] * rstd[e];
+    shift[e] = be[e] - mean[e] * scale[e];
+  }
+}
+
 F3_DEV float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1109,13 +1109,9 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
-  float sc2[4], sh2[4], scr[4], shr[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float mu, rs;
-    bn_coeff(a.bn2, c0 + e, sc2[e], sh2[e], mu, rs);
-    if (RES == RES_CONV) bn_coeff(a.bnr, c0 + e, scr[e], shr[e], mu, rs);
-  }
+  float sc2[4], sh2[4], scr[4], shr[4], mu[4], rs[4];
+  bn_coeff4(a.bn2, c0, sc2, sh2, mu, rs);
+  if (RES == RES_CONV) bn_coeff4(a.bnr, c0, scr, shr, mu, rs);
   const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
   f32x4 pool = {0.f, 0.f, 0.f, 0.f};
   for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
@@ -1181,13 +1177,9 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
-  float mu2[4], rs2[4], mur[4], rsr[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float sc, sh;
-    bn_coeff(a.bn2, c0 + e, sc, sh, mu2[e], rs2[e]);
-    if (RES == RES_CONV) bn_coeff(a.bnr, c0 + e, sc, sh, mur[e], rsr[e]);
-  }
+  float mu2[4], rs2[4], mur[4], rsr[4], sc[4], sh[4];
+  bn_coeff4(a.bn2, c0, sc, sh, mu2, rs2);
+  if (RES == RES_CONV) bn_coeff4(a.bnr, c0, sc, sh, mur, rsr);
   f32x4 p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
   f32x4 dbc = {0, 0, 0, 0};
   if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
@@ -1269,20 +1261,29 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
-  float mu2[4], k2[4], m1[4], m2[4], rs2[4], mur[4], kr[4], n1[4], n2[4], rsr[4];
+  float mu2[4], k2[4], m1[4], m2[4], rs2[4], mur[4], kr[4], n1[4], n2[4], rsr[4], sc[4], sh[4];
+  double bs1[4], bs2[4], rs1[4], rsq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // (loads first: see bn_coeff4)
+    bs1[e] = a.bn2_bsum[c0 + e];
+    bs2[e] = a.bn2_bsq[c0 + e];
+    if (RES == RES_CONV) {
+      rs1[e] = a.bnr_bsum[c0 + e];
+      rsq[e] = a.bnr_bsq[c0 + e];
+    }
+  }
+  bn_coeff4(a.bn2, c0, sc, sh, mu2, rs2);
+  if (RES == RES_CONV) bn_coeff4(a.bnr, c0, sc, sh, mur, rsr);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int c = c0 + e;
-    float sc, sh;
-    bn_coeff(a.bn2, c, sc, sh, mu2[e], rs2[e]);
     k2[e] = a.bn2.gamma[c] * rs2[e];
-    m1[e] = (float)a.bn2_bsum[c] * invM;
-    m2[e] = (float)a.bn2_bsq[c] * invM;
+    m1[e] = (float)bs1[e] * invM;
+    m2[e] = (float)bs2[e] * invM;
     if (RES == RES_CONV) {
-      bn_coeff(a.bnr, c, sc, sh, mur[e], rsr[e]);
       kr[e] = a.bnr.gamma[c] * rsr[e];
-      n1[e] = (float)a.bnr_bsum[c] * invM;
-      n2[e] = (float)a.bnr_bsq[c] * invM;
+      n1[e] = (float)rs1[e] * invM;
+      n2[e] = (float)rsq[e] * invM;
     }
   }
   const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
