@@ -1109,22 +1109,26 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  // the first pass's rows are loaded before the coefficient prologue (they do not depend on it)
+  const int mb0 = r0 + tid / C4;
+  f32x4 h[kRowU], res[kRowU];
+  size_t off[kRowU];
+#define F3_BO_LOADS(MB)                                                  \
+  _Pragma("unroll") for (int u = 0; u < kRowU; ++u) {                    \
+    off[u] = (size_t)min((MB) + u * RP, r1 - 1) * C + c0;                \
+    h[u] = ld_act4<A16>(a.h, off[u]);                                    \
+    if (RES == RES_CONV) res[u] = ld_act4<A16>(a.r, off[u]);             \
+    else if (RES == RES_ID) res[u] = ld_act4<A16>(a.x, off[u]);          \
+    else res[u] = f32x4{0.f, 0.f, 0.f, 0.f};                             \
+  }
+  F3_BO_LOADS(mb0)
   float sc2[4], sh2[4], scr[4], shr[4], mu[4], rs[4];
   bn_coeff4(a.bn2, c0, sc2, sh2, mu, rs);
   if (RES == RES_CONV) bn_coeff4(a.bnr, c0, scr, shr, mu, rs);
   const f32x4 av = *reinterpret_cast<const f32x4*>(a.att + (size_t)n * C + c0);
   f32x4 pool = {0.f, 0.f, 0.f, 0.f};
-  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
-    f32x4 h[kRowU], res[kRowU];
-    size_t off[kRowU];
-#pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      off[u] = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
-      h[u] = ld_act4<A16>(a.h, off[u]);
-      if (RES == RES_CONV) res[u] = ld_act4<A16>(a.r, off[u]);
-      else if (RES == RES_ID) res[u] = ld_act4<A16>(a.x, off[u]);
-      else res[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int mb = mb0; mb < r1; mb += kRowU * RP) {
+    if (mb != mb0) F3_BO_LOADS(mb)
 #pragma unroll
     for (int u = 0; u < kRowU; ++u) {
       f32x4 o;
@@ -1153,6 +1157,7 @@ __global__ __launch_bounds__(256) void block_out_kernel(BlockArgs a) {
       if (mb + u * RP < r1) pool += o;
     }
   }
+#undef F3_BO_LOADS
   if (a.pool) {
     f32x4 r = quad_reduce(pool, lds, C4);
     if (tid < C4) {
@@ -1177,34 +1182,39 @@ __global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  // the first pass's rows are loaded before the coefficient prologue (they do not depend on it)
+  const int mb0 = r0 + tid / C4;
+  f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
+#define F3_BR_LOADS(MB)                                                          \
+  _Pragma("unroll") for (int u = 0; u < kRowU; ++u) {                            \
+    const size_t off = (size_t)min((MB) + u * RP, r1 - 1) * C + c0;              \
+    o[u] = ld_act4<A16>(a.out, off);                                             \
+    if (!DNC) d[u] = *reinterpret_cast<const f32x4*>(a.dout + off);              \
+    h[u] = ld_act4<A16>(a.h, off);                                               \
+    if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off);                         \
+  }
+  F3_BR_LOADS(mb0)
   float mu2[4], rs2[4], mur[4], rsr[4], sc[4], sh[4];
   bn_coeff4(a.bn2, c0, sc, sh, mu2, rs2);
   if (RES == RES_CONV) bn_coeff4(a.bnr, c0, sc, sh, mur, rsr);
   f32x4 p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
   f32x4 dbc = {0, 0, 0, 0};
   if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
-  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
-    f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
-#pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      const size_t off = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
-      o[u] = ld_act4<A16>(a.out, off);
-      d[u] = DNC ? dbc : *reinterpret_cast<const f32x4*>(a.dout + off);
-      h[u] = ld_act4<A16>(a.h, off);
-      if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off);
-    }
+  for (int mb = mb0; mb < r1; mb += kRowU * RP) {
+    if (mb != mb0) F3_BR_LOADS(mb)
 #pragma unroll
     for (int u = 0; u < kRowU; ++u) {
       const float w = mb + u * RP < r1 ? 1.f : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float dz = o[u][e] > 0.f ? d[u][e] * w : 0.f;
+        const float dz = o[u][e] > 0.f ? (DNC ? dbc[e] : d[u][e]) * w : 0.f;
         p1[e] += dz;
         p2[e] += dz * ((h[u][e] - mu2[e]) * rs2[e]);
         if (RES == RES_CONV) q2[e] += dz * ((rr[u][e] - mur[e]) * rsr[e]);
       }
     }
   }
+#undef F3_BR_LOADS
   // per-clip partial sums (a clip's chunks add into one row: <= chunks-way float atomics). The
   // residual BN's channel sums over all clips (sum dz = sum_n P1, sum dz*xhat_r = sum_n Q2) are
   // folded in by ca_bwd3, which walks the clips anyway: double atomics from every chunk of every
@@ -1261,6 +1271,19 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   int r0, r1;
   chunk_rows(a.TV, a.chunks, r0, r1);
   const int n = blockIdx.y, cq = tid % C4, c0 = cq * 4;
+  // the first pass's rows are loaded before the coefficient prologue (they do not depend on it)
+  const int mb0 = r0 + tid / C4;
+  f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
+  size_t off[kRowU];
+#define F3_BA_LOADS(MB)                                                          \
+  _Pragma("unroll") for (int u = 0; u < kRowU; ++u) {                            \
+    off[u] = (size_t)min((MB) + u * RP, r1 - 1) * C + c0;                        \
+    o[u] = ld_act4<A16>(a.out, off[u]);                                          \
+    if (!DNC) d[u] = *reinterpret_cast<const f32x4*>(a.dout + off[u]);           \
+    h[u] = ld_act4<A16>(a.h, off[u]);                                            \
+    if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off[u]);                      \
+  }
+  F3_BA_LOADS(mb0)
   float mu2[4], k2[4], m1[4], m2[4], rs2[4], mur[4], kr[4], n1[4], n2[4], rsr[4], sc[4], sh[4];
   double bs1[4], bs2[4], rs1[4], rsq[4];
 #pragma unroll
@@ -1291,23 +1314,14 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
   f32x4 dbc = {0, 0, 0, 0};
   if (DNC) dbc = *reinterpret_cast<const f32x4*>(a.dout_nc + (size_t)n * C + c0) * a.inv_tv;
   f32x4 sdh = {0, 0, 0, 0}, sdr = {0, 0, 0, 0};  // (dbpart) the chunk's column sums of dh / dres
-  for (int mb = r0 + tid / C4; mb < r1; mb += kRowU * RP) {
-    f32x4 o[kRowU], d[kRowU], h[kRowU], rr[kRowU];
-    size_t off[kRowU];
-#pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      off[u] = (size_t)min(mb + u * RP, r1 - 1) * C + c0;
-      o[u] = ld_act4<A16>(a.out, off[u]);
-      d[u] = DNC ? dbc : *reinterpret_cast<const f32x4*>(a.dout + off[u]);
-      h[u] = ld_act4<A16>(a.h, off[u]);
-      if (RES == RES_CONV) rr[u] = ld_act4<A16>(a.r, off[u]);
-    }
+  for (int mb = mb0; mb < r1; mb += kRowU * RP) {
+    if (mb != mb0) F3_BA_LOADS(mb)
 #pragma unroll
     for (int u = 0; u < kRowU; ++u) {
       f32x4 dh, dr;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float dz = o[u][e] > 0.f ? d[u][e] : 0.f;
+        const float dz = o[u][e] > 0.f ? (DNC ? dbc[e] : d[u][e]) : 0.f;
         const float xh = (h[u][e] - mu2[e]) * rs2[e];
         dh[e] = k2[e] * (dz * av[e] + ev[e] - m1[e] - xh * m2[e]);
         if (RES == RES_CONV) {
@@ -1357,6 +1371,7 @@ __global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockArgs a) {
       }
     }
   }
+#undef F3_BA_LOADS
   if (a.dbpart) {  // partial rows [chunk][n][C | C] (fixed-order sums in the caller's colsum)
     __shared__ __attribute__((aligned(16))) float lds[1024];
     float* row = a.dbpart + ((size_t)blockIdx.x * a.N + n) * 2 * C;
