@@ -28,6 +28,7 @@ namespace f3 {
 constexpr int G0_FB = 8;          // frames per block iteration
 constexpr int G0_MAXKC = 12;      // K * Cin
 constexpr int G0_MAXV = 25;
+constexpr int G0_DWB = 12;        // gcn0_bwd: dg rows loaded together in the weight-gradient pass
 
 F3_DEV float g0_bf(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
 F3_DEV unsigned short g0_rne(float f) {
@@ -204,11 +205,23 @@ __global__ __launch_bounds__(256) void gcn0_bwd_kernel(Gcn0Args a) {
         dacc[q] += acc;
       }
     }
-    // dW[k][c][ci] += sum_rows dg[row][c] Z[row][k*Ci + ci]
-    for (int r = rg; r < nr; r += 4) {
-      const float d = F32 ? dgf[((size_t)f0 * V + r) * C + c] : g0_bf(a.dg[((size_t)f0 * V + r) * C + c]);
+    // dW[k][c][ci] += sum_rows dg[row][c] Z[row][k*Ci + ci] (rows rg, rg + 4, ... in order; the rows'
+    // dg loads issued G0_DWB at a time instead of one round trip per row)
+    for (int rb = rg; rb < nr; rb += 4 * G0_DWB) {
+      float d[G0_DWB];
 #pragma unroll
-      for (int j = 0; j < KC; ++j) wacc[j] += d * zs[r * KC + j];
+      for (int i = 0; i < G0_DWB; ++i) {
+        const int r = min(rb + 4 * i, nr - 1);
+        d[i] = F32 ? dgf[((size_t)f0 * V + r) * C + c] : g0_bf(a.dg[((size_t)f0 * V + r) * C + c]);
+      }
+#pragma unroll
+      for (int i = 0; i < G0_DWB; ++i) {
+        const int r = rb + 4 * i;
+        if (r < nr) {
+#pragma unroll
+          for (int j = 0; j < KC; ++j) wacc[j] += d[i] * zs[r * KC + j];
+        }
+      }
     }
   }
   // this block's partial rows: dA_eff [KVV] at part_dA[blockIdx], dW at part_dW[blockIdx] in the
