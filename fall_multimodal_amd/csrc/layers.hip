@@ -53,6 +53,7 @@ struct PrepLaunch {
 };
 static_assert(sizeof(PrepLaunch) <= 4096, "kernel argument block");
 
+constexpr int kPrepVMax = 25;  // PREP_GCN_BIAS: joints whose column loads go out together
 __global__ void prep_kernel(PrepLaunch L) {
   int jb = 0;
   while (jb + 1 < L.t.n && (int)blockIdx.x >= L.boff[jb + 1]) ++jb;
@@ -108,7 +109,19 @@ __global__ void prep_kernel(PrepLaunch L) {
         float acc = 0.f;
         for (int k = 0; k < K; ++k) {
           float cs = 0.f;
-          for (int v = 0; v < V; ++v) cs += j.s0[(k * V + v) * V + w] * j.s1[(k * V + v) * V + w];
+          if (V <= kPrepVMax) {  // a column's loads issued together (the same sum, v ascending)
+            float av[kPrepVMax], ev[kPrepVMax];
+#pragma unroll
+            for (int v = 0; v < kPrepVMax; ++v) {
+              av[v] = v < V ? j.s0[(k * V + v) * V + w] : 0.f;
+              ev[v] = v < V ? j.s1[(k * V + v) * V + w] : 0.f;
+            }
+#pragma unroll
+            for (int v = 0; v < kPrepVMax; ++v)
+              if (v < V) cs += av[v] * ev[v];
+          } else {
+            for (int v = 0; v < V; ++v) cs += j.s0[(k * V + v) * V + w] * j.s1[(k * V + v) * V + w];
+          }
           acc += cs * j.s2[k * C + c];
         }
         val = acc;
