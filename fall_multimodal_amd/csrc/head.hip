@@ -34,10 +34,14 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
       for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, z[c]);
       float s = 0.f;
       for (int c = 0; c < a.C; ++c) s += __expf(z[c] - mx);
-      for (int c = 0; c < a.C; ++c) a.out[(size_t)n * a.C + c] = __expf(z[c] - mx) / s;
-    } else {
-      for (int c = 0; c < a.C; ++c) a.out[(size_t)n * a.C + c] = z[c];
+      for (int c = 0; c < a.C; ++c) z[c] = __expf(z[c] - mx) / s;
     }
+  }
+  __syncthreads();
+  // the module output, and the caller's copy of it (out2: no device-to-device copy afterwards)
+  if (threadIdx.x < a.C) {
+    a.out[(size_t)n * a.C + threadIdx.x] = z[threadIdx.x];
+    if (a.out2) a.out2[(size_t)n * a.C + threadIdx.x] = z[threadIdx.x];
   }
 }
 
@@ -46,6 +50,8 @@ constexpr int kCeOneBlock = 4096;  // batches up to this size: the single-workgr
 
 // ONE: a single 256-thread workgroup walks every row and stores the mean loss (no zeroed loss word
 // beforehand, no atomics: deterministic); otherwise one row per thread, atomics into a zeroed loss
+constexpr int kCeRegs = 16;  // class counts up to this: the row is loaded into registers up front
+
 template <bool ONE>
 __global__ void ce_kernel(HeadArgs a) {
   float lsum = 0.f;
@@ -53,15 +59,43 @@ __global__ void ce_kernel(HeadArgs a) {
   for (int n = n0; n < a.N; n += ONE ? blockDim.x : a.N) {
     const float* o = a.out + (size_t)n * a.C;
     const float* y = a.label + (size_t)n * a.C;
-    float mx = -INFINITY;
-    for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, o[c]);
-    float s = 0.f, ys = 0.f;
-    for (int c = 0; c < a.C; ++c) { s += expf(o[c] - mx); ys += y[c]; }
-    const float lse = mx + logf(s);
+    float* d = a.dout + (size_t)n * a.C;
     float l = 0.f;
-    for (int c = 0; c < a.C; ++c) {
-      l -= y[c] * (o[c] - lse);
-      a.dout[(size_t)n * a.C + c] = (expf(o[c] - lse) * ys - y[c]) / (float)a.N;
+    if (a.C <= kCeRegs) {
+      // every load issued before the first use (clamped indices: no branches between them); the
+      // same sequential sums as the loop form below, so the two agree bit for bit
+      float ov[kCeRegs], yv[kCeRegs];
+#pragma unroll
+      for (int c = 0; c < kCeRegs; ++c) {
+        const int cc = c < a.C ? c : a.C - 1;
+        ov[c] = o[cc];
+        yv[c] = y[cc];
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < kCeRegs; ++c)
+        if (c < a.C) mx = fmaxf(mx, ov[c]);
+      float s = 0.f, ys = 0.f;
+#pragma unroll
+      for (int c = 0; c < kCeRegs; ++c)
+        if (c < a.C) { s += expf(ov[c] - mx); ys += yv[c]; }
+      const float lse = mx + logf(s);
+#pragma unroll
+      for (int c = 0; c < kCeRegs; ++c)
+        if (c < a.C) {
+          l -= yv[c] * (ov[c] - lse);
+          d[c] = (expf(ov[c] - lse) * ys - yv[c]) / (float)a.N;
+        }
+    } else {
+      float mx = -INFINITY;
+      for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, o[c]);
+      float s = 0.f, ys = 0.f;
+      for (int c = 0; c < a.C; ++c) { s += expf(o[c] - mx); ys += y[c]; }
+      const float lse = mx + logf(s);
+      for (int c = 0; c < a.C; ++c) {
+        l -= y[c] * (o[c] - lse);
+        d[c] = (expf(o[c] - lse) * ys - y[c]) / (float)a.N;
+      }
     }
     lsum += l;
   }
@@ -125,21 +159,56 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(HeadArgs a) {
   }
 }
 
-// grid (N): dfeat[n][k] = sum_c dlog[n][c] W[c][k]
+// grid (N): the clip's dlogits row (head_dlogits' arithmetic, in the same order; stored for
+// head_wgrad), then dfeat[n][k] = sum_c dlog[n][c] W[c][k] from LDS
 __global__ __launch_bounds__(256) void head_dfeat_kernel(HeadArgs a) {
+  __shared__ float dl[64];
+  __shared__ float pg[2][64];
   const int n = blockIdx.x;
   const int K = a.width[0] + (a.nblk > 1 ? a.width[1] : 0) + (a.nblk > 2 ? a.width[2] : 0);
+  if (threadIdx.x < a.C) {
+    pg[0][threadIdx.x] = a.softmax_out ? a.out[(size_t)n * a.C + threadIdx.x] : 0.f;
+    pg[1][threadIdx.x] = a.g_out[(size_t)n * a.C + threadIdx.x];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.softmax_out) {
+      float dot = 0.f;
+      for (int c = 0; c < a.C; ++c) dot += pg[0][c] * pg[1][c];
+      for (int c = 0; c < a.C; ++c) dl[c] = pg[0][c] * (pg[1][c] - dot);
+    } else {
+      for (int c = 0; c < a.C; ++c) dl[c] = pg[1][c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < a.C) a.dlogits[(size_t)n * a.C + threadIdx.x] = dl[threadIdx.x];
   int off = 0;
   for (int b = 0; b < a.nblk; ++b) {
     if (a.dfeat[b]) {
       for (int k = threadIdx.x; k < a.width[b]; k += blockDim.x) {
         float acc = 0.f;
-        for (int c = 0; c < a.C; ++c) acc += a.dlogits[(size_t)n * a.C + c] * a.W[(size_t)c * K + off + k];
+        for (int c = 0; c < a.C; ++c) acc += dl[c] * a.W[(size_t)c * K + off + k];
         a.dfeat[b][(size_t)n * a.width[b] + k] = acc;
       }
     }
     off += a.width[b];
   }
+}
+
+// zero two float ranges in one launch (the backward's gradient buffer and its zeroed workspace
+// block); 16-byte aligned starts, float4 stores plus a scalar tail per range
+__global__ __launch_bounds__(256) void zero2_kernel(float* __restrict__ a, long long na, float* __restrict__ b,
+                                                   long long nb) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long a4 = na / 4, b4 = nb / 4;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  for (long long i = t; i < a4 + b4; i += stride) {
+    if (i < a4) reinterpret_cast<f32x4*>(a)[i] = z;
+    else reinterpret_cast<f32x4*>(b)[i - a4] = z;
+  }
+  if (t < na - a4 * 4) a[a4 * 4 + t] = 0.f;
+  if (t < nb - b4 * 4) b[b4 * 4 + t] = 0.f;
 }
 
 __global__ void rmsprop_kernel(float* __restrict__ p, float* __restrict__ sq, const float* __restrict__ g,
@@ -226,16 +295,38 @@ int f3_ce(const HeadArgs* a, hipStream_t s) {
   return F3_OK;
 }
 
-int f3_head_bwd(const HeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(head_dlogits_kernel, dim3((a->N + 255) / 256), dim3(256), 0, s, *a);
-  F3_LAUNCH_CHECK();
+int f3_head_bwd_data(const HeadArgs* a, hipStream_t s) {
+  if (a->C > 64) return F3_EINVAL;
   if (a->nblk > 0) {
-    const int K = a->width[0] + (a->nblk > 1 ? a->width[1] : 0) + (a->nblk > 2 ? a->width[2] : 0);
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3((K + 63) / 64, a->C), dim3(256), 0, s, *a);
-    F3_LAUNCH_CHECK();
     hipLaunchKernelGGL(head_dfeat_kernel, dim3(a->N), dim3(256), 0, s, *a);
-    F3_LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(head_dlogits_kernel, dim3((a->N + 255) / 256), dim3(256), 0, s, *a);
   }
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_head_bwd_weight(const HeadArgs* a, hipStream_t s) {
+  if (a->nblk == 0) return F3_OK;
+  const int K = a->width[0] + (a->nblk > 1 ? a->width[1] : 0) + (a->nblk > 2 ? a->width[2] : 0);
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3((K + 63) / 64, a->C), dim3(256), 0, s, *a);
+  F3_LAUNCH_CHECK();
+  return F3_OK;
+}
+
+int f3_head_bwd(const HeadArgs* a, hipStream_t s) {
+  F3_TRY(f3_head_bwd_data(a, s));
+  return f3_head_bwd_weight(a, s);
+}
+
+int f3_zero2(float* a, long long na, float* b, long long nb, hipStream_t s) {
+  if (na < 0 || nb < 0 || (na && !a) || (nb && !b) || ((uintptr_t)a | (uintptr_t)b) % 16) return F3_EINVAL;
+  const long long n4 = na / 4 + nb / 4;
+  if (n4 == 0 && na == 0 && nb == 0) return F3_OK;
+  const long long blocks = (n4 + 255) / 256;
+  const int grid = (int)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048);
+  hipLaunchKernelGGL(zero2_kernel, dim3(grid), dim3(256), 0, s, a, na, b, nb);
+  F3_LAUNCH_CHECK();
   return F3_OK;
 }
 

@@ -1366,11 +1366,12 @@ int f3_net_forward(f3_net* net, int N, int training, const float* params, float*
   if (net->cfg.model == F3_MODEL_BILSTM) {
     if (hipMemcpyAsync(w.out, w.sout, sizeof(float) * N * net->cfg.num_class, hipMemcpyDeviceToDevice, s) != hipSuccess)
       return F3_EHIP;
+    if (hipMemcpyAsync(out, w.out, sizeof(float) * N * net->cfg.num_class, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return F3_EHIP;
   } else {
+    h.out2 = out;  // the head writes the caller's copy itself
     F3_TRY(f3_head_fwd(&h, s));
   }
-  if (hipMemcpyAsync(out, w.out, sizeof(float) * N * net->cfg.num_class, hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return F3_EHIP;
   if (training) F3_TRY(f3_bn_running(run, s));
   return F3_OK;
 }
@@ -1554,8 +1555,15 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     net->p1_mask = 0;
     return F3_OK;
   }
-  if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
-  if (hipMemsetAsync(w.zb0, 0, w.zb1 - w.zb0, s) != hipSuccess) return F3_EHIP;
+  // the gradient buffer and the backward's zeroed workspace block: one launch when both are float
+  // ranges on 16-byte boundaries (the usual case), else two memsets
+  const size_t zb = w.zb1 - w.zb0;
+  if (zb % 4 == 0 && ((uintptr_t)grads | (uintptr_t)w.zb0) % 16 == 0) {
+    F3_TRY(f3_zero2(grads, net->nparam, reinterpret_cast<float*>(w.zb0), (long long)(zb / 4), s));
+  } else {
+    if (hipMemsetAsync(grads, 0, sizeof(float) * net->nparam, s) != hipSuccess) return F3_EHIP;
+    if (hipMemsetAsync(w.zb0, 0, zb, s) != hipSuccess) return F3_EHIP;
+  }
   HeadArgs h;
   head_args(*net, N, q, w, h);
   h.g_out = dout;
@@ -1567,11 +1575,14 @@ int net_backward(f3_net* net, int N, const float* params, const float* dout, flo
     sa.dout = dout;
     sa.dout_ld = net->cfg.num_class;
   } else {
-    F3_TRY(f3_head_bwd(&h, s));
+    F3_TRY(f3_head_bwd_data(&h, s));  // dlogits + feature gradients: what the streams' backward waits for
   }
   Branches br{*net, s, ensure_parallel(*net, s)};
   br.mask = (net->nstreams > 1 ? BR_MOTION : 0) | (net->has_sensor ? BR_SENSOR : 0) | (net->nstreams > 0 ? BR_SIDE : 0);
   F3_TRY(br.fork());
+  // the head Linear's weight gradients off the critical path, at the front of the side queue (which
+  // then waits for the first layer's data gradients anyway)
+  if (net->cfg.model != F3_MODEL_BILSTM) F3_TRY(f3_head_bwd_weight(&h, br.side()));
   auto sensor_bwd = [&]() -> int {
     if (!net->has_sensor) return F3_OK;
     const hipStream_t ss = br.at(2);

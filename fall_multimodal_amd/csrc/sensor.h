@@ -96,6 +96,7 @@ struct HeadArgs {
   const float* W;             // [C][sum(width)]
   const float* b;
   float* out;                 // [N][C]
+  float* out2;                // [N][C] second copy of out (the caller's buffer), or null
   int softmax_out;
   // loss
   const float* label;         // [N][C] soft targets or null
@@ -123,7 +124,12 @@ int f3_cnn1d_fwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, const f3::C
 int f3_cnn1d_bwd(const f3::Conv1dArgs* c1, const f3::Conv1dArgs* c2, const f3::CnnCoop* coop, hipStream_t s);
 int f3_head_fwd(const f3::HeadArgs* a, hipStream_t s);
 int f3_ce(const f3::HeadArgs* a, hipStream_t s);
-int f3_head_bwd(const f3::HeadArgs* a, hipStream_t s);
+int f3_head_bwd(const f3::HeadArgs* a, hipStream_t s);  // f3_head_bwd_data, then f3_head_bwd_weight
+// dlogits + feature gradients (the backward's critical path) / the Linear's weight gradients
+int f3_head_bwd_data(const f3::HeadArgs* a, hipStream_t s);
+int f3_head_bwd_weight(const f3::HeadArgs* a, hipStream_t s);
+// zero na floats at a and nb floats at b (16-byte aligned) in one launch
+int f3_zero2(float* a, long long na, float* b, long long nb, hipStream_t s);
 // RMSprop over up to kRmsRanges ranges of one flat buffer in one launch (offsets and lengths in
 // floats, multiples of 4: the entries of the flat parameter layout are 16-B aligned)
 constexpr int kRmsRanges = 8;
