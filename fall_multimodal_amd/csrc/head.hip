@@ -14,15 +14,29 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   __shared__ float z[64];
   const int n = blockIdx.x;
   int K = 0;
-  for (int b = 0; b < a.nblk; ++b) {
-    for (int k = threadIdx.x; k < a.width[b]; k += blockDim.x)
-      fs[K + k] = a.feat[b][(size_t)n * a.ld[b] + k];
-    K += a.width[b];
+  if (a.width[0] <= (int)blockDim.x && a.width[1] <= (int)blockDim.x && a.width[2] <= (int)blockDim.x) {
+    // blocks no wider than the workgroup: each thread's (up to three) loads go out together
+    float v[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+      v[b] = b < a.nblk && (int)threadIdx.x < a.width[b] ? a.feat[b][(size_t)n * a.ld[b] + threadIdx.x] : 0.f;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      if (b < a.nblk && (int)threadIdx.x < a.width[b]) fs[K + threadIdx.x] = v[b];
+      K += b < a.nblk ? a.width[b] : 0;
+    }
+  } else {
+    for (int b = 0; b < a.nblk; ++b) {
+      for (int k = threadIdx.x; k < a.width[b]; k += blockDim.x)
+        fs[K + k] = a.feat[b][(size_t)n * a.ld[b] + k];
+      K += a.width[b];
+    }
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int c = wave; c < a.C; c += blockDim.x >> 6) {
     float acc = 0.f;
+#pragma unroll 4  // (unrolled: the weight loads of four k steps go out together; same sum order)
     for (int k = lane; k < K; k += 64) acc += a.W[(size_t)c * K + k] * fs[k];
     acc = warp_sum(acc);
     if (lane == 0) z[c] = acc + a.b[c];

@@ -151,14 +151,26 @@ F3_DEV float stream_in(const float* skel, int motion, int n, int c, int t, int v
   return motion ? (p[V] - p[0]) : p[0];
 }
 
-__global__ void databn_stats_kernel(DataBnArgs a) {
+// one 1024-thread workgroup per channel (a channel's N*T inputs are strided by V floats: latency,
+// not bandwidth, bounds it), kDbnU inputs loaded per thread before they are summed
+constexpr int kDbnU = 4;
+__global__ __launch_bounds__(1024) void databn_stats_kernel(DataBnArgs a) {
   const int ch = blockIdx.x, v = ch / a.C, c = ch - v * a.C;
+  const int NT = a.N * a.T;
   double s = 0.0, q = 0.0;
-  for (int e = threadIdx.x; e < a.N * a.T; e += blockDim.x) {
-    const int n = e / a.T, t = e - n * a.T;
-    const float x = stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V);
-    s += x;
-    q += (double)x * x;
+  for (int e0 = threadIdx.x; e0 < NT; e0 += kDbnU * blockDim.x) {
+    float x[kDbnU];
+#pragma unroll
+    for (int u = 0; u < kDbnU; ++u) {
+      const int e = e0 + u * blockDim.x;
+      const int n = e / a.T, t = e - n * a.T;
+      x[u] = e < NT ? stream_in(a.skel, a.motion, n, c, t, v, a.T, a.V) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kDbnU; ++u) {
+      s += x[u];
+      q += (double)x[u] * x[u];
+    }
   }
   __shared__ double rs[2][16];
   s = warp_sum_d(s);
@@ -2286,9 +2298,19 @@ int f3_prep(const PrepTable& t, hipStream_t s) {
   PrepLaunch L;
   L.t = t;
   L.boff[0] = 0;
-  for (int j = 0; j < t.n; ++j) {  // ~4 items per thread, 1..2048 blocks per job
+  // items per thread (F3_PREP_IPT, default 4; 1..2048 blocks per job). The graph-mixed-bias job's
+  // items are 2*K*V loads each: one item per thread (at four, its 3,584 items on four workgroups
+  // were the launch's longest chain). 1 or 2 items per thread for the rest measured no faster (1:
+  // +0.8 % step, the extra workgroups), r06_prep_ipt_ab.txt.
+  static const int ipt = [] {
+    const char* e = std::getenv("F3_PREP_IPT");
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
+  }();
+  for (int j = 0; j < t.n; ++j) {
     const long long items = t.jobs[j].bf16 == 4 ? t.jobs[j].n / 2 : t.jobs[j].n;
-    L.boff[j + 1] = L.boff[j] + (int)std::min<long long>(2048, std::max<long long>(1, (items + 1023) / 1024));
+    const long long per = 256LL * (t.jobs[j].type == PREP_GCN_BIAS ? 1 : ipt);
+    L.boff[j + 1] = L.boff[j] + (int)std::min<long long>(2048, std::max<long long>(1, (items + per - 1) / per));
   }
   hipLaunchKernelGGL(prep_kernel, dim3(L.boff[t.n]), dim3(256), 0, s, L);
   F3_LAUNCH_CHECK();
@@ -2297,7 +2319,7 @@ int f3_prep(const PrepTable& t, hipStream_t s) {
 
 int f3_databn_fwd(const DataBnArgs* a, hipStream_t s) {
   if (!a->bn.eval) {
-    hipLaunchKernelGGL(databn_stats_kernel, dim3(a->V * a->C), dim3(256), 0, s, *a);
+    hipLaunchKernelGGL(databn_stats_kernel, dim3(a->V * a->C), dim3(1024), 0, s, *a);
     F3_LAUNCH_CHECK();
   }
   const int total = a->N * a->T * a->V * a->C;
