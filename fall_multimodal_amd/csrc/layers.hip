@@ -2145,6 +2145,13 @@ __global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
   const int n0 = blockIdx.x * 4, C = a.C, H = C / 4, N = a.N, tid = threadIdx.x;
   const int nn = tid >> 8, c = tid & 255, n = n0 + nn;
   const bool cl = c < C, live = cl && n < N;
+  // this thread's (clip, channel) operands and BN2 coefficients: loaded first, so their round trips
+  // overlap the FUSE2 part's loads and barriers (loads do not move across a barrier by themselves)
+  const size_t o = (size_t)(live ? n : 0) * C + (cl ? c : 0);
+  const float at = a.att[o], p1 = a.P1[o], p2 = a.P2[o], gs = a.gapsum[o];
+  const float q2 = a.bnr_bsum ? a.Q2[o] : 0.f;
+  float bsc = 0.f, bsh = 0.f, bmu = 0.f, brs = 0.f;
+  if (live) bn_coeff(a.bn2, c, bsc, bsh, bmu, brs);
   if constexpr (FUSE2) {
     __shared__ float ps[2][16][64];
     __shared__ float s12[2][64], kk[64], mu[64], rsd[64];
@@ -2224,9 +2231,6 @@ __global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
 #pragma unroll
   for (int k = 0; k < 64; ++k)
     if (k < H) wk[k] = cl ? a.W1[(size_t)k * C + c] : 0.f;
-  const size_t o = (size_t)(live ? n : 0) * C + (cl ? c : 0);
-  const float at = a.att[o], p1 = a.P1[o], p2 = a.P2[o], gs = a.gapsum[o];
-  const float q2 = a.bnr_bsum ? a.Q2[o] : 0.f;
   if (!FUSE2 && tid < 4 * H) {
     const int m = tid / H, k = tid - m * H;
     dq[m][k] = n0 + m < N ? a.dq1[(size_t)(n0 + m) * H + k] : 0.f;
@@ -2234,14 +2238,12 @@ __global__ __launch_bounds__(1024) void ca_bwd3x_kernel(CaArgs a) {
   __syncthreads();
   double s1 = 0.0, s2 = 0.0, r1 = 0.0, r2 = 0.0;
   if (live) {
-    float sc, sh, mu, rs;
-    bn_coeff(a.bn2, c, sc, sh, mu, rs);
     float dg = 0.f;
 #pragma unroll
     for (int k = 0; k < 64; ++k)
       if (k < H) dg += dq[nn][k] * wk[k];
     a.e[o] = dg * a.inv_tv;
-    const float xsum = (gs - mu / a.inv_tv) * rs;  // sum_tv xhat2
+    const float xsum = (gs - bmu / a.inv_tv) * brs;  // sum_tv xhat2
     s1 = (double)(at * p1 + dg);
     s2 = (double)(at * p2 + dg * a.inv_tv * xsum);
     r1 = (double)p1;
