@@ -4,7 +4,9 @@ Every cross-workgroup reduction on the bf16x3 (headline) step's path sums partia
 (f3_colsum: pooled means, per-clip block sums, channel-attention / data-BN / LSTM / bias weight
 gradients, graph-mix dA, BN-backward column sums, split-K weight-gradient slabs), so two identical
 steps give bit-identical outputs and gradients. The BN statistics accumulate float partials into fp64
-(exact sums at these magnitudes). This is what lets the parity gates elsewhere be fixed tolerances
+atomics: exact, hence order-independent, while each channel's partials span at most
+29 - ceil(log2 n) binades ("What the fp64 BN-statistic atomics guarantee"); a sum
+that nearly cancels can fall outside that, so for those sums this test is a measurement, not a proof. This is what lets the parity gates elsewhere be fixed tolerances
 instead of run-to-run floors. (The fp32 mode's own kernels — conv_wgrad_f32, the fp32 graph mix — keep
 float atomics and are not covered.)
 
